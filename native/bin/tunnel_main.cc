@@ -1,0 +1,244 @@
+// `tunnel serve|proxy` CLI.
+//
+// Flags, env fallbacks and defaults match reference tunnel/src/cli.rs:
+//   serve: --signal (TUNNEL_SIGNAL, wss://signal-server.fly.dev) --room (TUNNEL_ROOM, required)
+//          --upstream (TUNNEL_UPSTREAM, required) --advertise (default "/", no env)
+//          --turn/--turn-user/--turn-pass (TUNNEL_TURN, TUNNEL_TURN_USER, TUNNEL_TURN_PASS)
+//   proxy: --signal --room --listen (TUNNEL_LISTEN, 127.0.0.1:8000) --turn...
+// Logging filter from RUST_LOG (or TUNNEL_LOG), default info (main.rs:21-25).
+// Extra opt-in flags (defaults keep reference behaviour) are listed in --help.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "core/log.h"
+#include "tunnel/app.h"
+
+using namespace p2pt;
+
+static const char* kVersion = "0.2.0";
+
+namespace {
+
+struct Opt {
+  const char* name;
+  const char* env;
+  const char* dflt;
+  const char* help;
+  bool flag = false;  // boolean switch
+};
+
+const std::vector<Opt>& serve_opts() {
+  static const std::vector<Opt> o = {
+      {"signal", "TUNNEL_SIGNAL", "wss://signal-server.fly.dev", "WebSocket URL of the signaling server"},
+      {"room", "TUNNEL_ROOM", nullptr, "Room name to join"},
+      {"upstream", "TUNNEL_UPSTREAM", nullptr, "Upstream HTTP URL to forward requests to"},
+      {"advertise", nullptr, "/", "Path prefix to advertise (e.g. /v1)"},
+      {"turn", "TUNNEL_TURN", "", "TURN server URL (e.g. turn:turn.example.com:3478)"},
+      {"turn-user", "TUNNEL_TURN_USER", "", "TURN server username"},
+      {"turn-pass", "TUNNEL_TURN_PASS", "", "TURN server password"},
+  };
+  return o;
+}
+
+const std::vector<Opt>& proxy_opts() {
+  static const std::vector<Opt> o = {
+      {"signal", "TUNNEL_SIGNAL", "wss://signal-server.fly.dev", "WebSocket URL of the signaling server"},
+      {"room", "TUNNEL_ROOM", nullptr, "Room name to join"},
+      {"listen", "TUNNEL_LISTEN", "127.0.0.1:8000", "Local address to listen on"},
+      {"turn", "TUNNEL_TURN", "", "TURN server URL (e.g. turn:turn.example.com:3478)"},
+      {"turn-user", "TUNNEL_TURN_USER", "", "TURN server username"},
+      {"turn-pass", "TUNNEL_TURN_PASS", "", "TURN server password"},
+  };
+  return o;
+}
+
+// Opt-in extensions shared by both subcommands (not in the reference).
+const std::vector<Opt>& ext_opts() {
+  static const std::vector<Opt> o = {
+      {"transport", "TUNNEL_TRANSPORT", "webrtc", "webrtc | tcp-listen:HOST:PORT | tcp-connect:HOST:PORT"},
+      {"stun", "TUNNEL_STUN", "stun:stun.l.google.com:19302", "STUN server(s), comma-separated; 'none' disables"},
+      {"no-loopback-candidates", nullptr, nullptr, "Do not gather 127.0.0.1 host candidates", true},
+      {"ipv6", nullptr, nullptr, "Gather IPv6 host candidates", true},
+      {"gather-timeout-ms", "TUNNEL_GATHER_TIMEOUT_MS", "5000", "Max wait for ICE gathering before sending SDP"},
+      {"ice-timeout-ms", "TUNNEL_ICE_TIMEOUT_MS", "30000", "No traffic for this long => connection failed"},
+      {"sctp-mtu", "TUNNEL_SCTP_MTU", "1200", "SCTP packet size budget (bytes)"},
+      {"no-jumbo-loopback", nullptr, nullptr, "Disable large SCTP packets on loopback paths", true},
+      {"max-retries", "TUNNEL_MAX_RETRIES", "4294967295", "Give up after this many failed attempts"},
+      {"reset-backoff-after", "TUNNEL_RESET_BACKOFF_AFTER", "0", "Reset backoff after a session lasted N s (0=never)"},
+      {"ping-interval-ms", "TUNNEL_PING_INTERVAL_MS", "10000", "Keepalive PING interval"},
+      {"pong-timeout-ms", "TUNNEL_PONG_TIMEOUT_MS", "0", "Fail the session if no PONG for this long (0=off)"},
+      {"header-timeout-ms", "TUNNEL_HEADER_TIMEOUT_MS", "60000", "Proxy wait for response headers (504 after)"},
+      {"handshake-timeout-ms", "TUNNEL_HANDSHAKE_TIMEOUT_MS", "300000", "HELLO/AGREE timeout"},
+      {"listen-early", nullptr, nullptr, "proxy: bind before the tunnel is up and answer 503 until ready", true},
+      {"metrics-listen", "TUNNEL_METRICS_LISTEN", "", "Serve Prometheus metrics on HOST:PORT"},
+  };
+  return o;
+}
+
+void usage_main() {
+  printf("P2P HTTP tunnel over WebRTC\n\nUsage: tunnel <COMMAND>\n\nCommands:\n"
+         "  serve  Serve an upstream HTTP service through the tunnel\n"
+         "  proxy  Create a local HTTP proxy that tunnels to a remote provider\n"
+         "  help   Print this message or the help of the given subcommand(s)\n\n"
+         "Options:\n  -h, --help     Print help\n  -V, --version  Print version\n");
+}
+
+void usage_sub(const char* cmd, const std::vector<Opt>& opts) {
+  printf("Usage: tunnel %s [OPTIONS]\n\nOptions:\n", cmd);
+  for (auto* list : {&opts, &ext_opts()}) {
+    if (list == &ext_opts()) printf("\nExtensions (defaults keep reference behaviour):\n");
+    for (auto& o : *list) {
+      std::string left = std::string("      --") + o.name + (o.flag ? "" : " <VALUE>");
+      printf("%-36s %s", left.c_str(), o.help);
+      if (o.env) printf(" [env: %s=]", o.env);
+      if (o.dflt && *o.dflt) printf(" [default: %s]", o.dflt);
+      printf("\n");
+    }
+  }
+  printf("  -h, --help                           Print help\n");
+}
+
+bool parse_sub(int argc, char** argv, const char* cmd, const std::vector<Opt>& opts,
+               std::map<std::string, std::string>& out) {
+  std::vector<Opt> all = opts;
+  for (auto& o : ext_opts()) all.push_back(o);
+  for (int i = 2; i < argc; i++) {
+    std::string a = argv[i];
+    if (a == "-h" || a == "--help") {
+      usage_sub(cmd, opts);
+      exit(0);
+    }
+    if (a.rfind("--", 0) != 0) {
+      fprintf(stderr, "error: unexpected argument '%s' found\n", a.c_str());
+      return false;
+    }
+    std::string name = a.substr(2), val;
+    bool has_eq = false;
+    size_t eq = name.find('=');
+    if (eq != std::string::npos) {
+      val = name.substr(eq + 1);
+      name = name.substr(0, eq);
+      has_eq = true;
+    }
+    const Opt* found = nullptr;
+    for (auto& o : all)
+      if (name == o.name) found = &o;
+    if (!found) {
+      fprintf(stderr, "error: unexpected argument '--%s' found\n\nUsage: tunnel %s [OPTIONS]\n", name.c_str(), cmd);
+      return false;
+    }
+    if (found->flag) {
+      out[name] = "1";
+      continue;
+    }
+    if (!has_eq) {
+      if (i + 1 >= argc) {
+        fprintf(stderr, "error: a value is required for '--%s <VALUE>' but none was supplied\n", name.c_str());
+        return false;
+      }
+      val = argv[++i];
+    }
+    out[name] = val;
+  }
+  for (auto& o : all) {
+    if (out.count(o.name)) continue;
+    const char* e = o.env ? getenv(o.env) : nullptr;
+    if (e && !o.flag) out[o.name] = e;
+    else if (o.dflt) out[o.name] = o.dflt;
+  }
+  for (auto& o : opts) {
+    if (!o.dflt && !o.flag && !out.count(o.name)) {
+      fprintf(stderr, "error: the following required arguments were not provided:\n  --%s <%s>\n\nUsage: tunnel %s --%s <VALUE>\n",
+              o.name, o.name, cmd, o.name);
+      return false;
+    }
+  }
+  return true;
+}
+
+uint64_t num(const std::map<std::string, std::string>& m, const char* k) {
+  auto it = m.find(k);
+  return it == m.end() ? 0 : strtoull(it->second.c_str(), nullptr, 10);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  log::init_from_env();
+  if (argc < 2) {
+    usage_main();
+    return 2;
+  }
+  std::string cmd = argv[1];
+  if (cmd == "-V" || cmd == "--version") {
+    printf("tunnel %s\n", kVersion);
+    return 0;
+  }
+  if (cmd == "-h" || cmd == "--help" || cmd == "help") {
+    if (argc > 2 && std::string(argv[2]) == "serve") usage_sub("serve", serve_opts());
+    else if (argc > 2 && std::string(argv[2]) == "proxy") usage_sub("proxy", proxy_opts());
+    else usage_main();
+    return 0;
+  }
+  if (cmd != "serve" && cmd != "proxy") {
+    fprintf(stderr, "error: unrecognized subcommand '%s'\n\n", cmd.c_str());
+    usage_main();
+    return 2;
+  }
+  std::map<std::string, std::string> m;
+  if (!parse_sub(argc, argv, cmd.c_str(), cmd == "serve" ? serve_opts() : proxy_opts(), m)) return 2;
+
+  AppConfig cfg;
+  cfg.mode = cmd;
+  cfg.signal = m["signal"];
+  cfg.room = m["room"];
+  if (cmd == "serve") {
+    cfg.upstream = m["upstream"];
+    cfg.advertise = m["advertise"];
+  } else {
+    cfg.listen = m["listen"];
+  }
+  cfg.rtc.turn.url = m["turn"];
+  cfg.rtc.turn.username = m["turn-user"];
+  cfg.rtc.turn.password = m["turn-pass"];
+  cfg.transport = m["transport"];
+  cfg.rtc.stun_servers.clear();
+  if (m["stun"] != "none") {
+    std::string s = m["stun"];
+    size_t start = 0;
+    while (start < s.size()) {
+      size_t c = s.find(',', start);
+      if (c == std::string::npos) c = s.size();
+      if (c > start) cfg.rtc.stun_servers.push_back(s.substr(start, c - start));
+      start = c + 1;
+    }
+  }
+  cfg.rtc.include_loopback = !m.count("no-loopback-candidates");
+  cfg.rtc.include_ipv6 = m.count("ipv6") > 0;
+  cfg.rtc.gather_timeout_ms = num(m, "gather-timeout-ms");
+  cfg.rtc.ice_failed_timeout_ms = num(m, "ice-timeout-ms");
+  cfg.rtc.sctp_mtu = num(m, "sctp-mtu");
+  cfg.rtc.allow_jumbo_loopback = !m.count("no-jumbo-loopback");
+  cfg.max_retries = num(m, "max-retries");
+  cfg.reset_backoff_after_s = num(m, "reset-backoff-after");
+  cfg.ping_interval_ms = num(m, "ping-interval-ms");
+  cfg.pong_timeout_ms = num(m, "pong-timeout-ms");
+  cfg.header_timeout_ms = num(m, "header-timeout-ms");
+  cfg.handshake_timeout_ms = num(m, "handshake-timeout-ms");
+  cfg.listen_early = m.count("listen-early") > 0;
+  cfg.metrics_listen = m["metrics-listen"];
+
+  if (cmd == "serve") {
+    LOG_INFO("tunnel", "starting serve mode: signal=%s, room=%s, upstream=%s, advertise=%s", cfg.signal.c_str(),
+             cfg.room.c_str(), cfg.upstream.c_str(), cfg.advertise.c_str());
+  } else {
+    LOG_INFO("tunnel", "starting proxy mode: signal=%s, room=%s, listen=%s", cfg.signal.c_str(), cfg.room.c_str(),
+             cfg.listen.c_str());
+  }
+  if (cfg.rtc.turn.set()) LOG_INFO("tunnel", "TURN server configured: %s", cfg.rtc.turn.url.c_str());
+  return run_app(cfg);
+}

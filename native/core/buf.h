@@ -1,0 +1,147 @@
+// Refcounted immutable byte slices + a growable write buffer.
+//
+// Equivalent of the `bytes` crate usage in the reference (zero-copy decode of
+// tunnel frames, reference tunnel/src/protocol.rs:157-172). A Bytes is a view
+// into a shared, immutable allocation: slicing never copies.
+#pragma once
+
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <string_view>
+#include <vector>
+
+namespace p2pt {
+
+class Bytes {
+ public:
+  Bytes() = default;
+
+  static Bytes copy(const void* p, size_t n) {
+    auto v = std::make_shared<std::vector<uint8_t>>(static_cast<const uint8_t*>(p),
+                                                    static_cast<const uint8_t*>(p) + n);
+    return Bytes(std::move(v));
+  }
+  static Bytes copy(std::string_view s) { return copy(s.data(), s.size()); }
+  static Bytes take(std::vector<uint8_t>&& v) {
+    return Bytes(std::make_shared<std::vector<uint8_t>>(std::move(v)));
+  }
+  static Bytes take(std::string&& s) { return copy(s.data(), s.size()); }
+
+  const uint8_t* data() const { return ptr_; }
+  size_t size() const { return len_; }
+  bool empty() const { return len_ == 0; }
+  uint8_t operator[](size_t i) const { return ptr_[i]; }
+  const uint8_t* begin() const { return ptr_; }
+  const uint8_t* end() const { return ptr_ + len_; }
+
+  // Zero-copy sub-view sharing the same owner.
+  Bytes slice(size_t off, size_t n = SIZE_MAX) const {
+    Bytes b;
+    if (off > len_) off = len_;
+    if (n > len_ - off) n = len_ - off;
+    b.owner_ = owner_;
+    b.ptr_ = ptr_ + off;
+    b.len_ = n;
+    return b;
+  }
+  std::string_view view() const { return {reinterpret_cast<const char*>(ptr_), len_}; }
+  std::string str() const { return std::string(view()); }
+  bool operator==(const Bytes& o) const {
+    return len_ == o.len_ && (len_ == 0 || std::memcmp(ptr_, o.ptr_, len_) == 0);
+  }
+
+ private:
+  explicit Bytes(std::shared_ptr<std::vector<uint8_t>> v)
+      : owner_(std::move(v)), ptr_(owner_->data()), len_(owner_->size()) {}
+  std::shared_ptr<const std::vector<uint8_t>> owner_;
+  const uint8_t* ptr_ = nullptr;
+  size_t len_ = 0;
+};
+
+// Append-only big-endian writer over a std::vector.
+class ByteWriter {
+ public:
+  explicit ByteWriter(std::vector<uint8_t>& out) : out_(out) {}
+  void u8(uint8_t v) { out_.push_back(v); }
+  void u16(uint16_t v) {
+    out_.push_back(uint8_t(v >> 8));
+    out_.push_back(uint8_t(v));
+  }
+  void u32(uint32_t v) {
+    out_.push_back(uint8_t(v >> 24));
+    out_.push_back(uint8_t(v >> 16));
+    out_.push_back(uint8_t(v >> 8));
+    out_.push_back(uint8_t(v));
+  }
+  void u64(uint64_t v) {
+    u32(uint32_t(v >> 32));
+    u32(uint32_t(v));
+  }
+  void bytes(const void* p, size_t n) {
+    out_.insert(out_.end(), static_cast<const uint8_t*>(p), static_cast<const uint8_t*>(p) + n);
+  }
+  void bytes(std::string_view s) { bytes(s.data(), s.size()); }
+  void zeros(size_t n) { out_.insert(out_.end(), n, 0); }
+  size_t size() const { return out_.size(); }
+  std::vector<uint8_t>& vec() { return out_; }
+
+ private:
+  std::vector<uint8_t>& out_;
+};
+
+inline uint16_t rd16(const uint8_t* p) { return uint16_t(p[0] << 8 | p[1]); }
+inline uint32_t rd32(const uint8_t* p) {
+  return uint32_t(p[0]) << 24 | uint32_t(p[1]) << 16 | uint32_t(p[2]) << 8 | uint32_t(p[3]);
+}
+inline uint64_t rd64(const uint8_t* p) { return uint64_t(rd32(p)) << 32 | rd32(p + 4); }
+inline void wr16(uint8_t* p, uint16_t v) {
+  p[0] = uint8_t(v >> 8);
+  p[1] = uint8_t(v);
+}
+inline void wr32(uint8_t* p, uint32_t v) {
+  p[0] = uint8_t(v >> 24);
+  p[1] = uint8_t(v >> 16);
+  p[2] = uint8_t(v >> 8);
+  p[3] = uint8_t(v);
+}
+
+// Bounds-checked big-endian reader.
+class ByteReader {
+ public:
+  ByteReader(const uint8_t* p, size_t n) : p_(p), n_(n) {}
+  bool has(size_t k) const { return n_ - off_ >= k; }
+  size_t remaining() const { return n_ - off_; }
+  size_t offset() const { return off_; }
+  const uint8_t* cur() const { return p_ + off_; }
+  bool u8(uint8_t& v) {
+    if (!has(1)) return false;
+    v = p_[off_++];
+    return true;
+  }
+  bool u16(uint16_t& v) {
+    if (!has(2)) return false;
+    v = rd16(p_ + off_);
+    off_ += 2;
+    return true;
+  }
+  bool u32(uint32_t& v) {
+    if (!has(4)) return false;
+    v = rd32(p_ + off_);
+    off_ += 4;
+    return true;
+  }
+  bool skip(size_t k) {
+    if (!has(k)) return false;
+    off_ += k;
+    return true;
+  }
+
+ private:
+  const uint8_t* p_;
+  size_t n_;
+  size_t off_ = 0;
+};
+
+}  // namespace p2pt

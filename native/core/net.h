@@ -1,0 +1,151 @@
+// Sockets: addresses, non-blocking TCP connections (optionally TLS), TCP
+// listeners, async name resolution and local interface enumeration.
+//
+// TcpConn is the byte-stream used by the HTTP server (proxy side, reference
+// proxy.rs:175-220 via hyper), the HTTP client (serve side, reference
+// serve.rs:187-294 via reqwest) and the WebSocket client/server (reference
+// signaling.rs:80-151 via tokio-tungstenite; signal-server/src/index.ts:93).
+#pragma once
+
+#include <netinet/in.h>
+#include <sys/socket.h>
+
+#include <deque>
+#include <functional>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "core/buf.h"
+#include "core/reactor.h"
+
+typedef struct ssl_st SSL;
+typedef struct ssl_ctx_st SSL_CTX;
+
+namespace p2pt {
+
+struct SockAddr {
+  sockaddr_storage ss{};
+  socklen_t len = 0;
+
+  static bool parse(const std::string& host, uint16_t port, SockAddr& out);  // numeric only
+  // "1.2.3.4:80", "[::1]:80"
+  static bool parse_hostport(const std::string& hp, SockAddr& out);
+  int family() const { return ss.ss_family; }
+  uint16_t port() const;
+  void set_port(uint16_t p);
+  std::string ip() const;
+  std::string str() const;  // ip:port / [ip]:port
+  bool is_loopback() const;
+  bool is_link_local() const;
+  const sockaddr* sa() const { return reinterpret_cast<const sockaddr*>(&ss); }
+  sockaddr* sa() { return reinterpret_cast<sockaddr*>(&ss); }
+  bool operator==(const SockAddr& o) const;
+  bool operator!=(const SockAddr& o) const { return !(*this == o); }
+};
+
+struct IfaceAddr {
+  std::string name;
+  SockAddr addr;
+};
+// Up, non-tentative interface addresses (IPv4 + global/ULA IPv6).
+std::vector<IfaceAddr> local_addresses(bool include_loopback, bool include_ipv6);
+
+// Resolve host asynchronously (numeric hosts resolve inline). Callback runs on
+// the reactor thread with an empty vector on failure.
+void resolve_async(Reactor& r, const std::string& host, uint16_t port,
+                   std::function<void(std::vector<SockAddr>, std::string err)> cb);
+
+int set_nonblocking(int fd);
+std::string errno_str(int e);
+
+// Shared TLS client context (system trust store, hostname verification).
+SSL_CTX* tls_client_ctx();
+
+class TcpConn : public std::enable_shared_from_this<TcpConn> {
+ public:
+  using DataFn = std::function<void(const uint8_t*, size_t)>;
+  using CloseFn = std::function<void(const std::string& err)>;  // empty err == clean EOF
+
+  // Wrap an accepted / already-connected fd.
+  static std::shared_ptr<TcpConn> adopt(Reactor& r, int fd);
+  // Async connect (resolves, connects, optional TLS with SNI + verification).
+  static void connect(Reactor& r, const std::string& host, uint16_t port, bool tls,
+                      std::function<void(std::shared_ptr<TcpConn>, std::string err)> cb,
+                      uint64_t timeout_ms = 30000);
+
+  ~TcpConn();
+
+  void on_data(DataFn f) { on_data_ = std::move(f); }
+  void on_close(CloseFn f) { on_close_ = std::move(f); }
+  // Fires when the output buffer drains below `low_water` after having been above it.
+  void on_drain(Fn f, size_t low_water = 0) {
+    on_drain_ = std::move(f);
+    low_water_ = low_water;
+  }
+
+  void write(Bytes b);
+  void write(std::string s);
+  void write(const void* p, size_t n) { write(Bytes::copy(p, n)); }
+  size_t pending_out() const { return out_bytes_; }
+  void pause_reading();
+  void resume_reading();
+  bool reading_paused() const { return paused_; }
+  // Close after all pending output is written.
+  void close_after_flush();
+  // Immediate close (RST semantics not forced). Fires on_close("") if not yet closed.
+  void close(const std::string& why = "");
+  bool closed() const { return fd_ < 0; }
+  int fd() const { return fd_; }
+  SockAddr peer() const { return peer_; }
+  void set_nodelay(bool on);
+
+ private:
+  TcpConn(Reactor& r, int fd);
+  void on_events(uint32_t ev);
+  void do_read();
+  void do_write();
+  void update_interest();
+  void fail(const std::string& err);
+  void tls_handshake_step();
+
+  Reactor& r_;
+  int fd_;
+  SockAddr peer_;
+  SSL* ssl_ = nullptr;
+  bool handshaking_ = false;
+  std::function<void(std::string)> handshake_cb_;
+  bool want_write_for_read_ = false;
+  bool paused_ = false;
+  bool close_after_flush_ = false;
+  bool in_write_ = false;
+  std::deque<Bytes> out_;
+  size_t out_off_ = 0;
+  size_t out_bytes_ = 0;
+  bool above_low_ = false;
+  size_t low_water_ = 0;
+  DataFn on_data_;
+  CloseFn on_close_;
+  Fn on_drain_;
+  uint32_t interest_ = 0;
+  friend struct ConnectOp;
+};
+
+class TcpListener {
+ public:
+  using AcceptFn = std::function<void(int fd, SockAddr peer)>;
+  // host:port; port 0 picks an ephemeral port (see local_addr()).
+  static std::unique_ptr<TcpListener> bind(Reactor& r, const std::string& hostport, AcceptFn cb,
+                                           std::string* err);
+  ~TcpListener();
+  SockAddr local_addr() const;
+  int fd() const { return fd_; }
+
+ private:
+  TcpListener(Reactor& r, int fd, AcceptFn cb);
+  Reactor& r_;
+  int fd_;
+  AcceptFn cb_;
+};
+
+}  // namespace p2pt

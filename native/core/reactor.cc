@@ -1,0 +1,247 @@
+#include "core/reactor.h"
+
+#include <signal.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/signalfd.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstring>
+#include <stdexcept>
+
+namespace p2pt {
+
+namespace {
+thread_local Reactor* t_current = nullptr;
+constexpr uint64_t kWakeTag = ~uint64_t(0);
+constexpr uint64_t kSigTag = ~uint64_t(0) - 1;
+}  // namespace
+
+Reactor* Reactor::current() { return t_current; }
+
+Reactor::Reactor() {
+  epfd_ = epoll_create1(EPOLL_CLOEXEC);
+  if (epfd_ < 0) throw std::runtime_error("epoll_create1 failed");
+  evfd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+  epoll_event ev{};
+  ev.events = EPOLLIN;
+  ev.data.u64 = kWakeTag;
+  epoll_ctl(epfd_, EPOLL_CTL_ADD, evfd_, &ev);
+}
+
+Reactor::~Reactor() {
+  if (sigfd_ >= 0) close(sigfd_);
+  if (evfd_ >= 0) close(evfd_);
+  if (epfd_ >= 0) close(epfd_);
+  if (t_current == this) t_current = nullptr;
+}
+
+uint64_t Reactor::now_us() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return uint64_t(ts.tv_sec) * 1000000u + uint64_t(ts.tv_nsec) / 1000u;
+}
+
+// epoll data carries (generation << 32 | fd) so an event queued for an fd that
+// was removed (and possibly reused) within the same batch is ignored.
+void Reactor::add(int fd, uint32_t events, IoFn cb) {
+  uint64_t g = gen_++;
+  fds_[fd] = FdEntry{g, std::make_shared<IoFn>(std::move(cb))};
+  epoll_event ev{};
+  ev.events = events;
+  ev.data.u64 = (g << 32) | uint32_t(fd);
+  if (epoll_ctl(epfd_, EPOLL_CTL_ADD, fd, &ev) < 0) {
+    if (errno == EEXIST) epoll_ctl(epfd_, EPOLL_CTL_MOD, fd, &ev);
+    else throw std::runtime_error(std::string("epoll_ctl add: ") + strerror(errno));
+  }
+}
+
+void Reactor::modify(int fd, uint32_t events) {
+  auto it = fds_.find(fd);
+  if (it == fds_.end()) return;
+  epoll_event ev{};
+  ev.events = events;
+  ev.data.u64 = (it->second.gen << 32) | uint32_t(fd);
+  epoll_ctl(epfd_, EPOLL_CTL_MOD, fd, &ev);
+}
+
+void Reactor::remove(int fd) {
+  if (fds_.erase(fd)) epoll_ctl(epfd_, EPOLL_CTL_DEL, fd, nullptr);
+}
+
+Reactor::TimerId Reactor::call_at(uint64_t when_us, Fn fn) {
+  TimerId id = next_timer_++;
+  timers_.emplace(id, std::make_pair(when_us, std::move(fn)));
+  timer_order_.emplace(when_us, id);
+  return id;
+}
+
+void Reactor::cancel(TimerId id) {
+  auto it = timers_.find(id);
+  if (it == timers_.end()) return;
+  auto range = timer_order_.equal_range(it->second.first);
+  for (auto o = range.first; o != range.second; ++o) {
+    if (o->second == id) {
+      timer_order_.erase(o);
+      break;
+    }
+  }
+  timers_.erase(it);
+}
+
+void Reactor::post(Fn fn) { posted_.push_back(std::move(fn)); }
+
+void Reactor::post_threadsafe(Fn fn) {
+  {
+    std::lock_guard<std::mutex> lk(ts_mu_);
+    ts_posted_.push_back(std::move(fn));
+  }
+  uint64_t one = 1;
+  ssize_t r = write(evfd_, &one, sizeof one);
+  (void)r;
+}
+
+uint64_t Reactor::add_flush_hook(Fn fn) {
+  uint64_t id = next_hook_++;
+  flush_hooks_.emplace_back(id, std::move(fn));
+  return id;
+}
+
+void Reactor::remove_flush_hook(uint64_t id) {
+  for (auto& h : flush_hooks_)
+    if (h.first == id) h.second = nullptr;  // compacted in run_flush
+}
+
+void Reactor::on_signal(int signo, Fn fn) {
+  signals_[signo] = std::move(fn);
+  sigset_t mask;
+  sigemptyset(&mask);
+  for (auto& s : signals_) sigaddset(&mask, s.first);
+  sigprocmask(SIG_BLOCK, &mask, nullptr);
+  if (sigfd_ < 0) {
+    sigfd_ = signalfd(-1, &mask, SFD_NONBLOCK | SFD_CLOEXEC);
+    epoll_event ev{};
+    ev.events = EPOLLIN;
+    ev.data.u64 = kSigTag;
+    epoll_ctl(epfd_, EPOLL_CTL_ADD, sigfd_, &ev);
+  } else {
+    signalfd(sigfd_, &mask, SFD_NONBLOCK | SFD_CLOEXEC);
+  }
+}
+
+int Reactor::next_timeout_ms() const {
+  if (!posted_.empty()) return 0;
+  if (timer_order_.empty()) return 1000;
+  uint64_t now = now_us();
+  uint64_t when = timer_order_.begin()->first;
+  if (when <= now) return 0;
+  uint64_t ms = (when - now + 999) / 1000;
+  return ms > 1000 ? 1000 : int(ms);
+}
+
+void Reactor::run_timers() {
+  uint64_t now = now_us();
+  while (!timer_order_.empty() && timer_order_.begin()->first <= now) {
+    TimerId id = timer_order_.begin()->second;
+    timer_order_.erase(timer_order_.begin());
+    auto it = timers_.find(id);
+    if (it == timers_.end()) continue;
+    Fn fn = std::move(it->second.second);
+    timers_.erase(it);
+    fn();
+  }
+}
+
+void Reactor::run_posted() {
+  // Bounded: work posted by posted work runs in the next iteration.
+  size_t n = posted_.size();
+  for (size_t i = 0; i < n && !posted_.empty(); i++) {
+    Fn fn = std::move(posted_.front());
+    posted_.pop_front();
+    fn();
+  }
+}
+
+void Reactor::run_flush() {
+  // Hooks may register/remove hooks; iterate by index over a stable count.
+  size_t n = flush_hooks_.size();
+  for (size_t i = 0; i < n; i++) {
+    if (flush_hooks_[i].second) {
+      Fn f = flush_hooks_[i].second;  // copy: hook may remove itself
+      f();
+    }
+  }
+  size_t w = 0;
+  for (size_t i = 0; i < flush_hooks_.size(); i++)
+    if (flush_hooks_[i].second) flush_hooks_[w++] = std::move(flush_hooks_[i]);
+  flush_hooks_.resize(w);
+}
+
+void Reactor::run_once(int timeout_ms) {
+  epoll_event evs[256];
+  int n = epoll_wait(epfd_, evs, 256, timeout_ms);
+  if (n < 0 && errno != EINTR) throw std::runtime_error(std::string("epoll_wait: ") + strerror(errno));
+  for (int i = 0; i < n; i++) {
+    uint64_t tag = evs[i].data.u64;
+    if (tag == kWakeTag) {
+      uint64_t v;
+      while (read(evfd_, &v, sizeof v) > 0) {
+      }
+      std::vector<Fn> fns;
+      {
+        std::lock_guard<std::mutex> lk(ts_mu_);
+        fns.swap(ts_posted_);
+      }
+      for (auto& f : fns) f();
+      continue;
+    }
+    if (tag == kSigTag) {
+      signalfd_siginfo si;
+      while (read(sigfd_, &si, sizeof si) == sizeof si) {
+        auto it = signals_.find(int(si.ssi_signo));
+        if (it != signals_.end() && it->second) {
+          Fn f = it->second;
+          f();
+        }
+      }
+      continue;
+    }
+    int fd = int(uint32_t(tag));
+    uint64_t g = tag >> 32;
+    auto it = fds_.find(fd);
+    if (it == fds_.end() || it->second.gen != g) continue;
+    auto cb = it->second.cb;  // keep alive across the call
+    (*cb)(evs[i].events);
+  }
+  run_timers();
+  run_posted();
+  run_flush();
+}
+
+void Reactor::run() {
+  Reactor* prev = t_current;
+  t_current = this;
+  stop_ = false;
+  while (!stop_) run_once(next_timeout_ms());
+  t_current = prev;
+}
+
+bool Reactor::run_until(const std::function<bool()>& pred, uint64_t timeout_ms) {
+  Reactor* prev = t_current;
+  t_current = this;
+  uint64_t deadline = now_ms() + timeout_ms;
+  stop_ = false;
+  while (!stop_ && !pred()) {
+    uint64_t now = now_ms();
+    if (now >= deadline) break;
+    int t = next_timeout_ms();
+    int left = int(deadline - now);
+    run_once(t < left ? t : left);
+  }
+  t_current = prev;
+  return pred();
+}
+
+}  // namespace p2pt

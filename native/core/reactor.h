@@ -1,0 +1,100 @@
+// Single-threaded run-to-completion epoll reactor.
+//
+// Replaces tokio (reference tunnel/Cargo.toml:7) and the reference's web of
+// spawned tasks + unbounded mpsc channels (reference proxy.rs:106-172,
+// :391-419; serve.rs:68-80, :131-137): every connection, stream and timer is
+// a callback on one thread, so the tunnel hot path has no locks and no
+// cross-thread hand-offs.
+//
+// Flush hooks run once after every batch of ready events, before the next
+// epoll_wait. Transports use them to coalesce everything produced in one
+// batch (SCTP bundling, sendmmsg, SACK-per-batch) without adding latency.
+#pragma once
+
+#include <cstdint>
+#include <deque>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
+namespace p2pt {
+
+using Fn = std::function<void()>;
+
+class Reactor {
+ public:
+  using IoFn = std::function<void(uint32_t events)>;
+  using TimerId = uint64_t;
+
+  Reactor();
+  ~Reactor();
+  Reactor(const Reactor&) = delete;
+  Reactor& operator=(const Reactor&) = delete;
+
+  // The reactor that is running on this thread (or nullptr).
+  static Reactor* current();
+
+  // fd registration; events are EPOLLIN/EPOLLOUT/... masks.
+  void add(int fd, uint32_t events, IoFn cb);
+  void modify(int fd, uint32_t events);
+  void remove(int fd);
+  bool watching(int fd) const { return fds_.count(fd) != 0; }
+
+  // Timers (monotonic microseconds).
+  TimerId call_at(uint64_t when_us, Fn fn);
+  TimerId call_later_ms(uint64_t ms, Fn fn) { return call_at(now_us() + ms * 1000, std::move(fn)); }
+  TimerId call_later_us(uint64_t us, Fn fn) { return call_at(now_us() + us, std::move(fn)); }
+  void cancel(TimerId id);
+
+  // Deferred work on this thread (runs before the next epoll_wait).
+  void post(Fn fn);
+  // Thread-safe variant (wakes the loop through an eventfd).
+  void post_threadsafe(Fn fn);
+  // Hook that runs after each event batch; returns an id for removal.
+  uint64_t add_flush_hook(Fn fn);
+  void remove_flush_hook(uint64_t id);
+
+  // SIGINT/SIGTERM etc. delivered via signalfd on the loop thread.
+  void on_signal(int signo, Fn fn);
+
+  void run();
+  // Run until pred() is true or the timeout passes; returns pred().
+  bool run_until(const std::function<bool()>& pred, uint64_t timeout_ms);
+  void stop() { stop_ = true; }
+  bool stopped() const { return stop_; }
+
+  static uint64_t now_us();
+  static uint64_t now_ms() { return now_us() / 1000; }
+
+ private:
+  void run_once(int timeout_ms);
+  int next_timeout_ms() const;
+  void run_timers();
+  void run_posted();
+  void run_flush();
+
+  struct FdEntry {
+    uint64_t gen;
+    std::shared_ptr<IoFn> cb;
+  };
+  int epfd_ = -1;
+  int evfd_ = -1;
+  int sigfd_ = -1;
+  bool stop_ = false;
+  uint64_t gen_ = 1;
+  std::unordered_map<int, FdEntry> fds_;
+  std::multimap<uint64_t, TimerId> timer_order_;
+  std::unordered_map<TimerId, std::pair<uint64_t, Fn>> timers_;
+  TimerId next_timer_ = 1;
+  std::deque<Fn> posted_;
+  std::mutex ts_mu_;
+  std::vector<Fn> ts_posted_;
+  std::vector<std::pair<uint64_t, Fn>> flush_hooks_;
+  uint64_t next_hook_ = 1;
+  std::unordered_map<int, Fn> signals_;
+};
+
+}  // namespace p2pt

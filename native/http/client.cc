@@ -1,0 +1,302 @@
+#include "http/client.h"
+
+#include "core/log.h"
+
+namespace p2pt::http {
+
+class ClientConnPool {
+ public:
+  explicit ClientConnPool(Reactor& r) : r_(r) {}
+  std::shared_ptr<TcpConn> take(const std::string& key) {
+    auto it = idle_.find(key);
+    while (it != idle_.end() && !it->second.empty()) {
+      auto c = it->second.back();
+      it->second.pop_back();
+      if (!c->closed()) return c;
+    }
+    return nullptr;
+  }
+  void put(const std::string& key, std::shared_ptr<TcpConn> c) {
+    if (c->closed()) return;
+    auto& v = idle_[key];
+    if (v.size() >= 64) {
+      c->close();
+      return;
+    }
+    std::weak_ptr<TcpConn> w = c;
+    // An idle connection that becomes readable is either closing or broken.
+    c->on_data([w](const uint8_t*, size_t) {
+      if (auto s = w.lock()) s->close("unexpected data on idle connection");
+    });
+    std::weak_ptr<ClientConnPool> wp;  // pool outlives conns via HttpClient
+    c->on_close([this, key, w](const std::string&) { remove(key, w); });
+    v.push_back(std::move(c));
+  }
+  void remove(const std::string& key, const std::weak_ptr<TcpConn>& w) {
+    auto it = idle_.find(key);
+    if (it == idle_.end()) return;
+    auto s = w.lock();
+    auto& v = it->second;
+    for (size_t i = 0; i < v.size(); i++)
+      if (v[i] == s) {
+        v.erase(v.begin() + long(i));
+        break;
+      }
+  }
+  size_t idle() const {
+    size_t n = 0;
+    for (auto& kv : idle_) n += kv.second.size();
+    return n;
+  }
+  void clear() {
+    auto all = std::move(idle_);
+    idle_.clear();
+    for (auto& kv : all)
+      for (auto& c : kv.second) {
+        c->on_close(nullptr);
+        c->close();
+      }
+  }
+  Reactor& r_;
+
+ private:
+  std::map<std::string, std::vector<std::shared_ptr<TcpConn>>> idle_;
+};
+
+HttpClient::HttpClient(Reactor& r) : r_(r), pool_(std::make_shared<ClientConnPool>(r)) {}
+HttpClient::~HttpClient() { pool_->clear(); }
+size_t HttpClient::idle_connections() const { return pool_->idle(); }
+
+std::shared_ptr<ClientCall> HttpClient::request(ClientRequest req, ClientCallbacks cb) {
+  auto call = std::shared_ptr<ClientCall>(new ClientCall());
+  call->r_ = &r_;
+  call->pool_ = pool_;
+  call->req_ = std::move(req);
+  call->cb_ = std::move(cb);
+  call->start();
+  return call;
+}
+
+ClientCall::~ClientCall() {
+  if (conn_) {
+    conn_->on_close(nullptr);
+    conn_->close();
+  }
+}
+
+namespace {
+// Calls keep themselves alive until finished (fire-and-forget semantics like tokio::spawn).
+std::map<ClientCall*, std::shared_ptr<ClientCall>>& live_calls() {
+  static std::map<ClientCall*, std::shared_ptr<ClientCall>> m;
+  return m;
+}
+}  // namespace
+
+void ClientCall::start() {
+  std::string err;
+  if (!parse_url(req_.url, url_, &err) || (url_.scheme != "http" && url_.scheme != "https")) {
+    if (err.empty()) err = "unsupported scheme: " + url_.scheme;
+    auto self = shared_from_this();
+    live_calls()[this] = self;
+    r_->post([self, err] { self->finish("builder error for url (" + self->req_.url + "): " + err); });
+    return;
+  }
+  live_calls()[this] = shared_from_this();
+  pool_key_ = url_.scheme + "://" + url_.host + ":" + std::to_string(url_.port);
+  if (auto c = pool_->take(pool_key_)) {
+    attach(c, true);
+    return;
+  }
+  std::weak_ptr<ClientCall> w = shared_from_this();
+  TcpConn::connect(*r_, url_.host, url_.port, url_.tls(), [w](std::shared_ptr<TcpConn> c, std::string e) {
+    auto self = w.lock();
+    if (!self || self->finished_) {
+      if (c) c->close();
+      return;
+    }
+    if (!c) {
+      self->finish("error sending request for url (" + self->req_.url + "): " + e);
+      return;
+    }
+    self->attach(c, false);
+  });
+}
+
+void ClientCall::attach(std::shared_ptr<TcpConn> c, bool reused) {
+  conn_ = std::move(c);
+  reused_ = reused;
+  std::weak_ptr<ClientCall> w = shared_from_this();
+  conn_->on_data([w](const uint8_t* p, size_t n) {
+    if (auto s = w.lock()) s->on_data(p, n);
+  });
+  conn_->on_close([w](const std::string& err) {
+    if (auto s = w.lock()) s->on_close(err);
+  });
+  std::string head;
+  head.reserve(256);
+  head += req_.method;
+  head += ' ';
+  head += url_.path;
+  head += " HTTP/1.1\r\nhost: ";
+  head += url_.host_header();
+  head += "\r\n";
+  bool has_accept = false;
+  for (auto& h : req_.headers) {
+    if (iequals(h.name, "accept")) has_accept = true;
+    head += h.name;
+    head += ": ";
+    head += h.value;
+    head += "\r\n";
+  }
+  if (!has_accept) head += "accept: */*\r\n";
+  if (req_.body_len > 0 || req_.force_content_length) head += "content-length: " + std::to_string(req_.body_len) + "\r\n";
+  head += "\r\n";
+  conn_->write(std::move(head));
+  for (auto& b : req_.body) conn_->write(b);
+  if (paused_) conn_->pause_reading();
+}
+
+void ClientCall::on_data(const uint8_t* p, size_t n) {
+  got_any_ = true;
+  buf_.append(reinterpret_cast<const char*>(p), n);
+  process();
+}
+
+void ClientCall::process() {
+  auto self = shared_from_this();
+  while (!finished_ && !paused_) {
+    if (!head_done_) {
+      size_t used = 0;
+      std::string err;
+      Head h;
+      auto res = parse_response_head(buf_, h, used, &err);
+      if (res == ParseResult::Incomplete) return;
+      if (res == ParseResult::Error) {
+        finish("error sending request for url (" + req_.url + "): invalid HTTP response: " + err);
+        return;
+      }
+      buf_.erase(0, used);
+      if (h.status >= 100 && h.status < 200 && h.status != 101) continue;  // interim
+      head_ = std::move(h);
+      head_done_ = true;
+      uint64_t len = 0;
+      auto mode = response_body_mode(head_, req_.method, len);
+      body_.reset(mode, len);
+      bool close_tok = head_.has_token("connection", "close");
+      keep_alive_ = mode != BodyDecoder::Mode::UntilClose &&
+                    (head_.version_minor >= 1 ? !close_tok : head_.has_token("connection", "keep-alive"));
+      if (cb_.on_head) cb_.on_head(head_);
+      if (finished_ || paused_) return;
+    }
+    if (body_.done()) {
+      finish("");
+      return;
+    }
+    if (buf_.empty()) return;
+    size_t used = body_.feed(reinterpret_cast<const uint8_t*>(buf_.data()), buf_.size(),
+                             [this](const uint8_t* d, size_t k) {
+                               if (cb_.on_data && !finished_) cb_.on_data(d, k);
+                             });
+    if (used == SIZE_MAX) {
+      finish("error decoding response body: " + body_.error());
+      return;
+    }
+    buf_.erase(0, used);
+    if (body_.done()) {
+      if (!buf_.empty()) keep_alive_ = false;  // trailing garbage
+      finish("");
+      return;
+    }
+    if (used == 0) return;
+  }
+}
+
+void ClientCall::on_close(const std::string& err) {
+  auto self = shared_from_this();
+  conn_.reset();
+  if (finished_) return;
+  if (!got_any_ && reused_) {
+    // Stale pooled connection: retry once on a fresh one.
+    reused_ = false;
+    std::weak_ptr<ClientCall> w = self;
+    TcpConn::connect(*r_, url_.host, url_.port, url_.tls(), [w](std::shared_ptr<TcpConn> c, std::string e) {
+      auto s = w.lock();
+      if (!s || s->finished_) {
+        if (c) c->close();
+        return;
+      }
+      if (!c) {
+        s->finish("error sending request for url (" + s->req_.url + "): " + e);
+        return;
+      }
+      s->attach(c, false);
+    });
+    return;
+  }
+  keep_alive_ = false;
+  if (!head_done_) {
+    // The peer may have sent a complete head without body framing then closed.
+    process();
+    if (finished_) return;
+    finish("error sending request for url (" + req_.url + "): " +
+           (err.empty() ? std::string("connection closed before message completed") : err));
+    return;
+  }
+  // Deliver anything buffered (paused) before judging EOF.
+  paused_ = false;
+  process();
+  if (finished_) return;
+  if (body_.on_eof()) finish("");
+  else finish("error decoding response body: " + (err.empty() ? body_.error() : err));
+}
+
+void ClientCall::finish(const std::string& err) {
+  if (finished_) return;
+  finished_ = true;
+  auto self = shared_from_this();
+  if (conn_) {
+    auto c = std::move(conn_);
+    conn_.reset();
+    if (err.empty() && keep_alive_ && buf_.empty() && !c->closed()) {
+      c->resume_reading();
+      pool_->put(pool_key_, c);
+    } else {
+      c->on_close(nullptr);
+      c->close();
+    }
+  }
+  bool before_head = !head_done_;
+  auto cb = std::move(cb_.on_done);
+  cb_ = ClientCallbacks{};
+  if (cb) cb(err, before_head);
+  live_calls().erase(this);
+}
+
+void ClientCall::pause() {
+  if (paused_ || finished_) return;
+  paused_ = true;
+  if (conn_) conn_->pause_reading();
+}
+
+void ClientCall::resume() {
+  if (!paused_ || finished_) return;
+  paused_ = false;
+  if (conn_) conn_->resume_reading();
+  std::weak_ptr<ClientCall> w = shared_from_this();
+  r_->post([w] {
+    if (auto s = w.lock()) {
+      if (!s->buf_.empty()) s->process();
+    }
+  });
+}
+
+void ClientCall::cancel() {
+  if (finished_) return;
+  keep_alive_ = false;
+  auto cb = std::move(cb_.on_done);
+  cb_ = ClientCallbacks{};
+  finish("cancelled");
+  (void)cb;
+}
+
+}  // namespace p2pt::http

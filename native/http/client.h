@@ -1,0 +1,92 @@
+// Streaming HTTP/1.1 client for the serve side's upstream requests.
+//
+// Replaces reqwest (reference serve.rs:62, :203-263): method + all headers
+// except host/connection/transfer-encoding are forwarded (serve.rs:207-212),
+// the body is sent with a Content-Length, and the response body is delivered
+// piecewise as it arrives (reqwest's bytes_stream(), serve.rs:263) so SSE
+// tokens are relayed one read at a time. Supports Content-Length, chunked and
+// close-delimited (HTTP/1.0) responses, https:// via OpenSSL, and keep-alive
+// connection pooling per origin. Reading can be paused for back-pressure.
+#pragma once
+
+#include <functional>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "core/net.h"
+#include "http/http.h"
+
+namespace p2pt::http {
+
+struct ClientRequest {
+  std::string method;
+  std::string url;
+  std::vector<Header> headers;  // already filtered by the caller
+  std::vector<Bytes> body;      // gathered, not concatenated
+  uint64_t body_len = 0;
+  bool force_content_length = false;  // send content-length even when 0
+};
+
+struct ClientCallbacks {
+  std::function<void(const Head&)> on_head;
+  std::function<void(const uint8_t*, size_t)> on_data;
+  // err empty => complete body received. `before_head` tells whether any
+  // response head had been delivered (502 vs mid-stream ERROR semantics).
+  std::function<void(const std::string& err, bool before_head)> on_done;
+};
+
+class ClientConnPool;
+
+class ClientCall : public std::enable_shared_from_this<ClientCall> {
+ public:
+  void pause();
+  void resume();
+  void cancel();
+  bool finished() const { return finished_; }
+  ~ClientCall();
+
+ private:
+  friend class HttpClient;
+  void start();
+  void attach(std::shared_ptr<TcpConn> c, bool reused);
+  void on_data(const uint8_t* p, size_t n);
+  void on_close(const std::string& err);
+  void finish(const std::string& err);
+  void process();
+
+  Reactor* r_ = nullptr;
+  std::shared_ptr<ClientConnPool> pool_;
+  ClientRequest req_;
+  ClientCallbacks cb_;
+  Url url_;
+  std::string pool_key_;
+  std::shared_ptr<TcpConn> conn_;
+  bool reused_ = false;
+  bool got_any_ = false;
+  bool head_done_ = false;
+  bool finished_ = false;
+  bool paused_ = false;
+  bool keep_alive_ = false;
+  Head head_;
+  BodyDecoder body_;
+  std::string buf_;
+  uint64_t timeout_timer_ = 0;
+};
+
+class HttpClient {
+ public:
+  explicit HttpClient(Reactor& r);
+  ~HttpClient();
+  // Starts the request; callbacks run on the reactor thread. The returned
+  // handle may be dropped (the call keeps itself alive until done).
+  std::shared_ptr<ClientCall> request(ClientRequest req, ClientCallbacks cb);
+  size_t idle_connections() const;
+
+ private:
+  Reactor& r_;
+  std::shared_ptr<ClientConnPool> pool_;
+};
+
+}  // namespace p2pt::http

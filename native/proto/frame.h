@@ -1,0 +1,136 @@
+// Tunnel wire protocol: frame codec, HELLO/AGREE negotiation, header schemas.
+//
+// Wire-compatible with the reference (tunnel/src/protocol.rs):
+//   frame   = [type:u8][stream_id:u32 big-endian][payload...]  (protocol.rs:147-154)
+//   decode  = >=5 bytes, known type, zero-copy payload view      (protocol.rs:157-172)
+//   types   = HELLO 1, AGREE 2, PING 3, PONG 4, REQ_HEADERS 10, REQ_BODY 11,
+//             REQ_END 12, RES_HEADERS 20, RES_BODY 21, RES_END 22, ERROR 99
+//                                                                (protocol.rs:86-100)
+//   limits  = MAX_FRAME_SIZE 65536, MAX_BODY_CHUNK 65408         (protocol.rs:9-12)
+//   hello   = {"proto":"httptunnel","min_version":1,"max_version":1,"features":["sse"]}
+//   agree   = highest common version, feature intersection       (protocol.rs:41-81)
+//
+// Encoding is split into a 5-byte header plus a payload view so transports can
+// scatter/gather the two pieces instead of concatenating (the reference copies
+// every body chunk three times, serve.rs:269-276).
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <optional>
+#include <string>
+#include <vector>
+
+#include "core/buf.h"
+#include "core/json.h"
+
+namespace p2pt::proto {
+
+constexpr uint32_t kProtocolVersion = 1;
+constexpr const char* kProtocolName = "httptunnel";
+constexpr size_t kMaxFrameSize = 64 * 1024;
+constexpr size_t kMaxBodyChunk = kMaxFrameSize - 128;
+constexpr size_t kHeaderLen = 5;
+
+enum class MsgType : uint8_t {
+  Hello = 1,
+  Agree = 2,
+  Ping = 3,
+  Pong = 4,
+  ReqHeaders = 10,
+  ReqBody = 11,
+  ReqEnd = 12,
+  // Extension (only sent when both HELLOs list "cancel"): the proxy's client
+  // went away; serve aborts the upstream request. Not in the reference.
+  Cancel = 13,
+  ResHeaders = 20,
+  ResBody = 21,
+  ResEnd = 22,
+  Error = 99,
+};
+
+std::optional<MsgType> msg_type_from_u8(uint8_t v);
+const char* msg_type_name(MsgType t);  // "Hello", "ReqHeaders", ... (Rust Debug names)
+
+struct Frame {
+  MsgType type;
+  uint32_t stream_id;
+  Bytes payload;
+
+  // [type][stream_id] header.
+  void header(uint8_t out[kHeaderLen]) const;
+  // Header + payload in one buffer (tests / small control frames).
+  Bytes encode() const;
+  size_t wire_size() const { return kHeaderLen + payload.size(); }
+};
+
+// Decode a received message. Errors mirror the reference text:
+// "message too short: N bytes", "unknown message type: T".
+bool decode(const Bytes& raw, Frame& out, std::string* err);
+
+// ---- handshake
+struct Hello {
+  std::string proto = kProtocolName;
+  uint32_t min_version = 1;
+  uint32_t max_version = kProtocolVersion;
+  std::vector<std::string> features{"sse"};
+  Json to_json() const;
+  static bool from_json(const Json& j, Hello& out, std::string* err);
+};
+
+struct Agree {
+  uint32_t version = 1;
+  std::vector<std::string> features;
+  Json to_json() const;
+  static bool from_json(const Json& j, Agree& out, std::string* err);
+};
+
+// Features this build understands. "sse" is the reference's only feature;
+// "cancel" (client-disconnect propagation) is only *acted on* when
+// both peers list it, so reference peers are unaffected.
+const std::vector<std::string>& our_features();
+// Negotiate from a peer HELLO (reference Agree::from_hello, protocol.rs:44-80).
+bool agree_from_hello(const Hello& h, Agree& out, std::string* err,
+                      const std::vector<std::string>& ours = our_features());
+
+// ---- header metadata (protocol.rs:121-136). Header maps are single-valued:
+// a later header of the same (lower-cased) name replaces an earlier one,
+// matching the reference's HashMap<String,String>.
+using HeaderMap = std::vector<std::pair<std::string, std::string>>;
+void header_set(HeaderMap& h, std::string name_lower, std::string value);
+const std::string* header_get(const HeaderMap& h, std::string_view name_lower);
+
+struct RequestHeaders {
+  uint32_t stream_id = 0;
+  std::string method;
+  std::string path;
+  HeaderMap headers;
+  Json to_json() const;
+  static bool from_json(const Json& j, RequestHeaders& out, std::string* err);
+};
+
+struct ResponseHeaders {
+  uint32_t stream_id = 0;
+  uint16_t status = 200;
+  HeaderMap headers;
+  Json to_json() const;
+  static bool from_json(const Json& j, ResponseHeaders& out, std::string* err);
+};
+
+// Frame constructors (reference protocol.rs:176-262).
+Frame make_hello(const Hello& h);
+Frame make_agree(const Agree& a);
+Frame make_req_headers(const RequestHeaders& h);
+Frame make_res_headers(const ResponseHeaders& h);
+Frame make_body(MsgType t, uint32_t stream_id, Bytes data);
+Frame make_empty(MsgType t, uint32_t stream_id);
+Frame make_error(uint32_t stream_id, const std::string& msg);
+
+// Upstream URL rewrite (reference serve.rs:167-185, incl. quirk Q1: the prefix
+// is stripped without a path-segment boundary check).
+std::string build_upstream_url(const std::string& upstream_base, const std::string& advertise_prefix,
+                               const std::string& request_path);
+
+bool json_parse_bytes(const Bytes& b, Json& out, std::string* err);
+
+}  // namespace p2pt::proto

@@ -1,0 +1,74 @@
+// Application layer: supervisor (retry with exponential backoff), transport
+// establishment and role sessions.
+//
+// Mirrors reference tunnel/src/main.rs:
+//   - run_with_retry: re-run connect -> serve/proxy forever; backoff
+//     min(2 * 2^(min(attempt,10)-1), 60) s; attempt never reset (Q5, kept
+//     by default; --reset-backoff-after opts into a reset)         (main.rs:111-159)
+//   - Ctrl-C aborts a running attempt and a backoff sleep            (main.rs:119-125, :149-155)
+//   - startup log lines and "TURN server configured: ..."           (main.rs:43-48, :79-84)
+#pragma once
+
+#include <functional>
+#include <memory>
+#include <string>
+
+#include "core/reactor.h"
+#include "tunnel/channel.h"
+#include "tunnel/proxy.h"
+#include "tunnel/serve.h"
+
+namespace p2pt {
+
+struct TurnConfig {
+  std::string url;
+  std::string username;
+  std::string password;
+  bool set() const { return !url.empty(); }
+};
+
+struct RtcOptions {
+  std::vector<std::string> stun_servers{"stun:stun.l.google.com:19302"};
+  TurnConfig turn;
+  bool include_loopback = true;     // host candidates on lo (offline / same-host peers)
+  bool include_ipv6 = false;
+  uint64_t gather_timeout_ms = 5000;  // reference waits <= 5 s (rtc.rs:181-182)
+  uint64_t ice_failed_timeout_ms = 30000;
+  size_t sctp_mtu = 1200;             // interop-safe DTLS payload budget
+  bool allow_jumbo_loopback = true;   // larger SCTP packets when both ends say so and path is loopback
+};
+
+struct AppConfig {
+  std::string mode;  // "serve" | "proxy"
+  std::string signal = "wss://signal-server.fly.dev";
+  std::string room;
+  std::string upstream;
+  std::string advertise = "/";
+  std::string listen = "127.0.0.1:8000";
+  std::string transport = "webrtc";  // or tcp-listen:HOST:PORT / tcp-connect:HOST:PORT
+  RtcOptions rtc;
+  uint64_t max_retries = UINT32_MAX;
+  uint64_t reset_backoff_after_s = 0;  // 0 = never reset (reference)
+  uint64_t pong_timeout_ms = 0;
+  uint64_t ping_interval_ms = 10000;
+  uint64_t header_timeout_ms = 60000;
+  uint64_t handshake_timeout_ms = 300000;
+  bool listen_early = false;
+  std::string metrics_listen;
+};
+
+// Establishes one MessageChannel (signalling + WebRTC, or a TCP debug link).
+// The callback fires exactly once. The returned handle keeps the transport
+// machinery (peer connection, signalling socket) alive; dropping it tears
+// everything down (the signalling client sends "bye").
+using ConnectCb = std::function<void(std::shared_ptr<MessageChannel>, std::string err)>;
+std::shared_ptr<void> connect_transport(Reactor& r, const AppConfig& cfg, ConnectCb cb);
+
+// Runs the supervisor loop until Ctrl-C / SIGTERM or max_retries. Returns the
+// process exit code.
+int run_app(const AppConfig& cfg);
+
+// Backoff in seconds for the n-th failed attempt (n >= 1).
+uint64_t backoff_secs(uint64_t attempt);
+
+}  // namespace p2pt

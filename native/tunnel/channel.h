@@ -1,0 +1,62 @@
+// MessageChannel: a reliable, ordered, message-oriented pipe between the two
+// tunnel peers. This is the abstraction the roles (serve/proxy) run on; the
+// reference hard-wires them to an Arc<RTCDataChannel> plus an unbounded mpsc
+// of received messages (reference rtc.rs:23-28, :74-99).
+//
+// Implementations:
+//   - rtc::DataChannel   (WebRTC SCTP/DTLS/ICE, the production transport)
+//   - TcpMessageChannel  (length-prefixed frames over TCP; debug/bench
+//                         transport selected by --transport tcp-listen:/tcp-connect:)
+#pragma once
+
+#include <functional>
+#include <memory>
+#include <string>
+
+#include "core/buf.h"
+#include "core/net.h"
+#include "core/reactor.h"
+
+namespace p2pt {
+
+class MessageChannel {
+ public:
+  virtual ~MessageChannel() = default;
+  // Queue one message made of a small header and a payload view (gathered,
+  // never concatenated by the caller). Returns false when the channel is closed.
+  virtual bool send(const uint8_t* hdr, size_t hlen, const Bytes& payload) = 0;
+  // Bytes accepted by send() but not yet handed to the network.
+  virtual size_t buffered_amount() const = 0;
+  virtual bool is_open() const = 0;
+  virtual void close() = 0;
+  virtual std::string describe() const = 0;
+
+  // Message arrived (whole message, zero-copy view where possible).
+  std::function<void(Bytes)> on_message;
+  // Channel became open (may already be open when handed out).
+  std::function<void()> on_open;
+  // Channel or the underlying connection failed / closed.
+  std::function<void(const std::string&)> on_closed;
+  // buffered_amount() fell to or below buffered_low_threshold.
+  std::function<void()> on_buffered_low;
+  size_t buffered_low_threshold = 64 * 1024;
+};
+
+// [u32 length][message] framing over a TcpConn.
+class TcpMessageChannel : public MessageChannel, public std::enable_shared_from_this<TcpMessageChannel> {
+ public:
+  static std::shared_ptr<TcpMessageChannel> wrap(std::shared_ptr<TcpConn> c);
+  bool send(const uint8_t* hdr, size_t hlen, const Bytes& payload) override;
+  size_t buffered_amount() const override { return conn_ ? conn_->pending_out() : 0; }
+  bool is_open() const override { return conn_ && !conn_->closed(); }
+  void close() override;
+  std::string describe() const override;
+
+ private:
+  void on_data(const uint8_t* p, size_t n);
+  std::shared_ptr<TcpConn> conn_;
+  std::vector<uint8_t> inbuf_;
+  size_t inoff_ = 0;
+};
+
+}  // namespace p2pt

@@ -1,0 +1,161 @@
+#include "tunnel/metrics.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <string_view>
+
+#include "http/http.h"
+#include "proto/frame.h"
+
+namespace p2pt::metrics {
+namespace {
+struct Registry {
+  std::map<std::string, double> counters;
+  std::map<std::string, double> gauges;
+  std::map<std::string, std::function<double()>> gauge_fns;
+  uint64_t frames_sent[256] = {};
+  uint64_t bytes_sent[256] = {};
+  uint64_t frames_recv[256] = {};
+  uint64_t bytes_recv[256] = {};
+};
+Registry& reg() {
+  static Registry r;
+  return r;
+}
+
+std::string type_label(int t) {
+  auto mt = proto::msg_type_from_u8(uint8_t(t));
+  return mt ? proto::msg_type_name(*mt) : std::to_string(t);
+}
+}  // namespace
+
+void frame_sent(uint8_t type, size_t bytes) {
+  reg().frames_sent[type]++;
+  reg().bytes_sent[type] += bytes;
+}
+void frame_recv(uint8_t type, size_t bytes) {
+  reg().frames_recv[type]++;
+  reg().bytes_recv[type] += bytes;
+}
+void counter_add(const std::string& name, double v) { reg().counters[name] += v; }
+void gauge_set(const std::string& name, double v) { reg().gauges[name] = v; }
+void gauge_fn(const std::string& name, std::function<double()> fn) { reg().gauge_fns[name] = std::move(fn); }
+void gauge_fn_remove(const std::string& name) { reg().gauge_fns.erase(name); }
+double counter_get(const std::string& name) {
+  auto it = reg().counters.find(name);
+  return it == reg().counters.end() ? 0 : it->second;
+}
+
+std::string render_prometheus() {
+  auto& r = reg();
+  std::string out;
+  char buf[256];
+  auto line = [&](const std::string& name, const std::string& labels, double v) {
+    snprintf(buf, sizeof buf, " %.17g\n", v);
+    out += name;
+    if (!labels.empty()) out += "{" + labels + "}";
+    out += buf;
+  };
+  out += "# TYPE tunnel_frames_sent_total counter\n";
+  for (int t = 0; t < 256; t++)
+    if (r.frames_sent[t]) line("tunnel_frames_sent_total", "type=\"" + type_label(t) + "\"", double(r.frames_sent[t]));
+  out += "# TYPE tunnel_frame_bytes_sent_total counter\n";
+  for (int t = 0; t < 256; t++)
+    if (r.bytes_sent[t]) line("tunnel_frame_bytes_sent_total", "type=\"" + type_label(t) + "\"", double(r.bytes_sent[t]));
+  out += "# TYPE tunnel_frames_received_total counter\n";
+  for (int t = 0; t < 256; t++)
+    if (r.frames_recv[t]) line("tunnel_frames_received_total", "type=\"" + type_label(t) + "\"", double(r.frames_recv[t]));
+  out += "# TYPE tunnel_frame_bytes_received_total counter\n";
+  for (int t = 0; t < 256; t++)
+    if (r.bytes_recv[t]) line("tunnel_frame_bytes_received_total", "type=\"" + type_label(t) + "\"", double(r.bytes_recv[t]));
+  for (auto& kv : r.counters) {
+    out += "# TYPE " + kv.first + " counter\n";
+    line(kv.first, "", kv.second);
+  }
+  for (auto& kv : r.gauges) {
+    out += "# TYPE " + kv.first + " gauge\n";
+    line(kv.first, "", kv.second);
+  }
+  for (auto& kv : r.gauge_fns) {
+    out += "# TYPE " + kv.first + " gauge\n";
+    line(kv.first, "", kv.second());
+  }
+  return out;
+}
+
+namespace {
+struct MetricsServer {
+  std::unique_ptr<TcpListener> listener;
+  std::map<int, std::shared_ptr<TcpConn>> conns;
+  int next = 0;
+};
+}  // namespace
+
+std::shared_ptr<void> serve(Reactor& r, const std::string& addr, std::string* err) {
+  auto srv = std::make_shared<MetricsServer>();
+  std::weak_ptr<MetricsServer> w = srv;
+  Reactor* rp = &r;
+  srv->listener = TcpListener::bind(
+      r, addr,
+      [w, rp](int fd, SockAddr) {
+        auto s = w.lock();
+        if (!s) return;
+        auto c = TcpConn::adopt(*rp, fd);
+        int id = s->next++;
+        s->conns[id] = c;
+        auto buf = std::make_shared<std::string>();
+        std::weak_ptr<TcpConn> wc = c;
+        c->on_data([buf, wc](const uint8_t* p, size_t n) {
+          buf->append(reinterpret_cast<const char*>(p), n);
+          http::Head h;
+          size_t used = 0;
+          auto res = http::parse_request_head(*buf, h, used, nullptr);
+          auto conn = wc.lock();
+          if (!conn || res == http::ParseResult::Incomplete) return;
+          std::string body, status = "200 OK";
+          if (res == http::ParseResult::Error) {
+            status = "400 Bad Request";
+          } else if (h.target == "/metrics" || h.target == "/") {
+            body = render_prometheus();
+          } else {
+            status = "404 Not Found";
+            body = "not found\n";
+          }
+          conn->write("HTTP/1.1 " + status + "\r\ncontent-type: text/plain; version=0.0.4\r\ncontent-length: " +
+                      std::to_string(body.size()) + "\r\nconnection: close\r\n\r\n" + body);
+          conn->close_after_flush();
+        });
+        c->on_close([w, id](const std::string&) {
+          if (auto s2 = w.lock()) s2->conns.erase(id);
+        });
+      },
+      err);
+  if (!srv->listener) return nullptr;
+  return srv;
+}
+
+}  // namespace p2pt::metrics
+
+namespace p2pt::trace {
+namespace {
+FILE* sink() {
+  static FILE* f = [] () -> FILE* {
+    const char* p = getenv("TUNNEL_TRACE");
+    if (!p || !*p) return nullptr;
+    return fopen(p, "a");
+  }();
+  return f;
+}
+}  // namespace
+
+bool enabled() { return sink() != nullptr; }
+
+void event(const char* role, uint32_t sid, const char* ev) {
+  FILE* f = sink();
+  if (!f) return;
+  fprintf(f, "{\"t_us\":%llu,\"role\":\"%s\",\"sid\":%u,\"ev\":\"%s\"}\n",
+          static_cast<unsigned long long>(Reactor::now_us()), role, sid, ev);
+  fflush(f);
+}
+}  // namespace p2pt::trace

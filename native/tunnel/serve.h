@@ -1,0 +1,89 @@
+// Serve (provider) role: answers HELLO with AGREE, then turns REQ_* frames
+// into upstream HTTP requests and streams RES_* frames back.
+//
+// Behavioural parity with reference tunnel/src/serve.rs:
+//   - wait for HELLO (300 s), reply AGREE, log "sent AGREE, tunnel ready"  (:37-59)
+//   - PING every 10 s, first one immediately; PING -> PONG              (:68-80, :140-148)
+//   - REQ_HEADERS keyed by the JSON stream_id; REQ_BODY appended; REQ_END
+//     starts the upstream request                                        (:112-139)
+//   - upstream connect failure -> 502 text/plain "Bad Gateway: ..." + END (:219-242)
+//   - RES_BODY per upstream read, sub-chunked at 65408 B                 (:263-276)
+//   - mid-stream upstream failure -> ERROR "upstream error: ..." + END    (:278-290)
+// Local robustness fixes (wire-compatible): malformed
+// REQ_HEADERS (Q3) and unparseable methods (Q4) answer 400 instead of killing
+// the session / hanging the client; back-pressure pauses upstream reads
+// while the channel is congested (Q11); a negotiated CANCEL aborts the
+// upstream request (Q12).
+#pragma once
+
+#include <functional>
+#include <memory>
+#include <string>
+#include <unordered_map>
+
+#include "http/client.h"
+#include "proto/frame.h"
+#include "tunnel/channel.h"
+#include "tunnel/scheduler.h"
+
+namespace p2pt {
+
+struct ServeConfig {
+  std::string upstream;
+  std::string advertise = "/";
+  uint64_t handshake_timeout_ms = 300000;
+  uint64_t ping_interval_ms = 10000;
+  uint64_t pong_timeout_ms = 0;  // 0 = reference behaviour (PONG only logged)
+  size_t high_water = 4 << 20;
+  size_t low_water = 1 << 20;
+};
+
+class ServeSession : public std::enable_shared_from_this<ServeSession> {
+ public:
+  // `done` fires once with the reason the session ended (always an error:
+  // like the reference, a session only ends on failure).
+  static std::shared_ptr<ServeSession> start(Reactor& r, std::shared_ptr<MessageChannel> ch, ServeConfig cfg,
+                                             std::function<void(const std::string&)> done);
+  ~ServeSession();
+  void stop(const std::string& why);
+  size_t active_streams() const { return streams_.size() + inflight_.size(); }
+
+ private:
+  struct Pending {
+    proto::RequestHeaders headers;
+    std::vector<Bytes> body;
+    uint64_t body_len = 0;
+  };
+  struct Inflight {
+    std::shared_ptr<http::ClientCall> call;
+    bool cancelled = false;
+  };
+
+  ServeSession(Reactor& r, std::shared_ptr<MessageChannel> ch, ServeConfig cfg);
+  void on_open();
+  void on_message(Bytes raw);
+  void on_hello(const proto::Frame& f);
+  void handle_frame(const proto::Frame& f);
+  void start_request(uint32_t sid, Pending p);
+  void send_simple_response(uint32_t sid, uint16_t status, const std::string& body);
+  void send_ping();
+  void on_backpressure_relief();
+
+  Reactor& r_;
+  std::shared_ptr<MessageChannel> ch_;
+  std::unique_ptr<FrameScheduler> sched_;
+  ServeConfig cfg_;
+  std::function<void(const std::string&)> done_;
+  http::HttpClient client_;
+  bool handshaken_ = false;
+  bool stopped_ = false;
+  bool cancel_feature_ = false;
+  uint64_t hello_timer_ = 0;
+  uint64_t ping_timer_ = 0;
+  uint64_t last_pong_ms_ = 0;
+  std::unordered_map<uint32_t, Pending> streams_;
+  std::unordered_map<uint32_t, Inflight> inflight_;
+  bool upstream_paused_ = false;
+};
+
+}  // namespace p2pt

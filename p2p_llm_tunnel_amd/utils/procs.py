@@ -1,0 +1,170 @@
+"""Process fixtures: run the signal server, ``tunnel serve`` and ``tunnel
+proxy`` as real child processes and wait on their log lines.
+
+Replaces the reference's fixed ``sleep`` calls (scripts/test-local.sh:101)
+with readiness on the load-bearing log strings "tunnel ready" and
+"proxy listening" (reference scripts/test-tunnel.sh:79-86).
+"""
+from __future__ import annotations
+
+import os
+import re
+import signal
+import socket
+import subprocess
+import threading
+import time
+from dataclasses import dataclass, field
+
+from p2p_llm_tunnel_amd import binary
+
+
+def free_port(host: str = "127.0.0.1") -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind((host, 0))
+        return s.getsockname()[1]
+
+
+@dataclass
+class Proc:
+    name: str
+    popen: subprocess.Popen
+    lines: list = field(default_factory=list)
+    _cv: threading.Condition = field(default_factory=threading.Condition)
+
+    def _pump(self):
+        for raw in self.popen.stdout:
+            line = raw.decode("utf-8", "replace").rstrip("\n")
+            with self._cv:
+                self.lines.append(line)
+                self._cv.notify_all()
+        with self._cv:
+            self._cv.notify_all()
+
+    def wait_for(self, pattern: str, timeout: float = 30.0, start: int = 0) -> str:
+        rx = re.compile(pattern)
+        deadline = time.time() + timeout
+        with self._cv:
+            idx = start
+            while True:
+                while idx < len(self.lines):
+                    if rx.search(self.lines[idx]):
+                        return self.lines[idx]
+                    idx += 1
+                left = deadline - time.time()
+                if left <= 0 or (self.popen.poll() is not None and idx >= len(self.lines)):
+                    raise TimeoutError(f"{self.name}: no line matching {pattern!r} within {timeout}s; "
+                                       f"exit={self.popen.poll()} log tail:\n" + "\n".join(self.lines[-30:]))
+                self._cv.wait(min(left, 0.2))
+
+    def count(self, pattern: str) -> int:
+        rx = re.compile(pattern)
+        with self._cv:
+            return sum(1 for l in self.lines if rx.search(l))
+
+    def text(self) -> str:
+        with self._cv:
+            return "\n".join(self.lines)
+
+    def stop(self, timeout: float = 5.0):
+        if self.popen.poll() is None:
+            self.popen.send_signal(signal.SIGTERM)
+            try:
+                self.popen.wait(timeout)
+            except subprocess.TimeoutExpired:
+                self.popen.kill()
+                self.popen.wait()
+
+    def kill(self):
+        if self.popen.poll() is None:
+            self.popen.kill()
+            self.popen.wait()
+
+
+def spawn(name: str, argv: list[str], env: dict | None = None) -> Proc:
+    e = dict(os.environ)
+    e.setdefault("RUST_LOG", "info")
+    if env:
+        e.update(env)
+    p = subprocess.Popen(argv, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=e)
+    proc = Proc(name, p)
+    threading.Thread(target=proc._pump, daemon=True).start()
+    return proc
+
+
+def start_signal(port: int | None = None) -> tuple[Proc, int]:
+    port = port or free_port()
+    p = spawn("signal", [binary("tunnel-signal"), "--listen", f"127.0.0.1:{port}"])
+    p.wait_for(r"\[signal\] listening on", 10)
+    return p, port
+
+
+def start_serve(room: str, upstream: str, signal_port: int | None = None, extra: list[str] | None = None,
+                env: dict | None = None, transport: str | None = None) -> Proc:
+    argv = [binary("tunnel"), "serve", "--room", room, "--upstream", upstream, "--stun", "none"]
+    if signal_port:
+        argv += ["--signal", f"ws://127.0.0.1:{signal_port}"]
+    if transport:
+        argv += ["--transport", transport]
+    return spawn("serve", argv + (extra or []), env)
+
+
+def start_proxy(room: str, listen: str, signal_port: int | None = None, extra: list[str] | None = None,
+                env: dict | None = None, transport: str | None = None) -> Proc:
+    argv = [binary("tunnel"), "proxy", "--room", room, "--listen", listen, "--stun", "none"]
+    if signal_port:
+        argv += ["--signal", f"ws://127.0.0.1:{signal_port}"]
+    if transport:
+        argv += ["--transport", transport]
+    return spawn("proxy", argv + (extra or []), env)
+
+
+class Tunnel:
+    """signal server + serve + proxy for one upstream; use as a context manager."""
+
+    def __init__(self, upstream: str, transport: str = "webrtc", serve_extra=None, proxy_extra=None,
+                 env: dict | None = None, advertise: str | None = None, room: str | None = None):
+        self.upstream = upstream
+        self.transport = transport
+        self.serve_extra = list(serve_extra or [])
+        self.proxy_extra = list(proxy_extra or [])
+        if advertise:
+            self.serve_extra += ["--advertise", advertise]
+        self.env = env
+        self.room = room or f"room-{os.getpid()}-{time.time_ns()}"
+        self.procs: list[Proc] = []
+        self.signal = self.serve = self.proxy = None
+        self.proxy_port = free_port()
+
+    @property
+    def url(self) -> str:
+        return f"http://127.0.0.1:{self.proxy_port}"
+
+    def start(self, timeout: float = 30.0) -> "Tunnel":
+        if self.transport == "webrtc":
+            self.signal, sp = start_signal()
+            self.procs.append(self.signal)
+            st = pt = None
+        else:
+            sp = None
+            port = free_port()
+            st, pt = f"tcp-listen:127.0.0.1:{port}", f"tcp-connect:127.0.0.1:{port}"
+        self.serve = start_serve(self.room, self.upstream, sp, self.serve_extra, self.env, st)
+        self.procs.append(self.serve)
+        if st:
+            self.serve.wait_for("tcp transport: listening", timeout)
+        self.proxy = start_proxy(self.room, f"127.0.0.1:{self.proxy_port}", sp, self.proxy_extra, self.env, pt)
+        self.procs.append(self.proxy)
+        self.serve.wait_for("tunnel ready", timeout)
+        self.proxy.wait_for("proxy listening", timeout)
+        return self
+
+    def stop(self):
+        for p in reversed(self.procs):
+            p.stop()
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.stop()
