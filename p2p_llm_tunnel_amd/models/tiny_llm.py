@@ -1,0 +1,184 @@
+"""Llama-style decoder for the on-node inference upstream.
+
+The tunnel's serve side fronts an OpenAI/Ollama-compatible endpoint running
+on the MI355X node (BASELINE.json north star). This module is that
+endpoint's model: random-init weights (no checkpoints offline), bf16, with
+the decode step built from the gfx950 HIP kernels in ``p2p_llm_tunnel_amd.ops``
+(fused residual+RMSNorm, fused RoPE+KV-append, GQA flash-decoding,
+SwiGLU, argmax) and hipBLASLt GEMMs via ``torch.nn.functional.linear``.
+
+``reference_logits`` recomputes the same network in fp32 PyTorch (full
+causal attention over the whole sequence) for numerics tests.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+from p2p_llm_tunnel_amd import ops
+
+
+@dataclass(frozen=True)
+class LlamaConfig:
+    vocab: int = 32000
+    dim: int = 1024
+    n_layers: int = 4
+    n_heads: int = 16
+    n_kv_heads: int = 4
+    head_dim: int = 64
+    ffn: int = 2816
+    max_seq: int = 2048
+    eps: float = 1e-5
+    rope_theta: float = 10000.0
+
+
+CONFIGS = {
+    "tiny": LlamaConfig(),
+    "micro": LlamaConfig(vocab=4096, dim=256, n_layers=2, n_heads=4, n_kv_heads=2, head_dim=64, ffn=512, max_seq=512),
+    "small": LlamaConfig(vocab=32000, dim=2048, n_layers=8, n_heads=16, n_kv_heads=4, head_dim=128, ffn=5632,
+                         max_seq=4096),
+}
+
+
+class TinyLlama:
+    def __init__(self, cfg: LlamaConfig | str = "tiny", device="cuda", max_batch: int = 8, seed: int = 0):
+        self.cfg = CONFIGS[cfg] if isinstance(cfg, str) else cfg
+        c = self.cfg
+        self.device = torch.device(device)
+        self.max_batch = max_batch
+        g = torch.Generator(device="cpu").manual_seed(seed)
+
+        def w(*shape, scale):
+            return (torch.randn(*shape, generator=g) * scale).to(torch.bfloat16).to(self.device)
+
+        def norm_w(n):
+            return (1.0 + 0.1 * torch.randn(n, generator=g)).to(torch.bfloat16).to(self.device)
+
+        qkv_out = (c.n_heads + 2 * c.n_kv_heads) * c.head_dim
+        self.embed = w(c.vocab, c.dim, scale=1.0)
+        self.layers = []
+        for _ in range(c.n_layers):
+            self.layers.append({
+                "attn_norm": norm_w(c.dim),
+                "wqkv": w(qkv_out, c.dim, scale=1 / math.sqrt(c.dim)),
+                "wo": w(c.dim, c.n_heads * c.head_dim, scale=1 / math.sqrt(c.n_heads * c.head_dim)),
+                "ffn_norm": norm_w(c.dim),
+                "w_gate_up": w(2 * c.ffn, c.dim, scale=1 / math.sqrt(c.dim)),
+                "w_down": w(c.dim, c.ffn, scale=1 / math.sqrt(c.ffn)),
+            })
+        self.final_norm = norm_w(c.dim)
+        self.lm_head = w(c.vocab, c.dim, scale=1 / math.sqrt(c.dim))
+        cache_shape = (c.n_layers, max_batch, c.max_seq, c.n_kv_heads, c.head_dim)
+        self.k_cache = torch.zeros(cache_shape, dtype=torch.bfloat16, device=self.device)
+        self.v_cache = torch.zeros(cache_shape, dtype=torch.bfloat16, device=self.device)
+
+    # ------------------------------------------------------------------ HIP path
+    @torch.no_grad()
+    def decode_step(self, tokens: torch.Tensor, pos: torch.Tensor, pos_range: tuple[int, int],
+                    return_logits: bool = False):
+        """One token per slot. tokens: int64 [B]; pos: int32 [B] (cache position of this token).
+
+        Returns next-token ids (int64 [B]) and optionally the bf16 logits.
+        """
+        c = self.cfg
+        B = tokens.shape[0]
+        if B > self.max_batch:
+            raise ValueError("batch exceeds max_batch")
+        if pos_range[1] >= c.max_seq:
+            raise ValueError("sequence exceeds max_seq")
+        lens = pos + 1
+        max_len = pos_range[1] + 1
+        x = self.embed.index_select(0, tokens)
+        h = ops.rmsnorm(x, self.layers[0]["attn_norm"], c.eps)
+        residual = x
+        for i, L in enumerate(self.layers):
+            kc, vc = self.k_cache[i, :B], self.v_cache[i, :B]
+            qkv = F.linear(h, L["wqkv"])
+            q = ops.rope_qkv_cache(qkv, pos, kc, vc, c.n_heads, c.n_kv_heads, c.head_dim, c.rope_theta,
+                                   pos_range=pos_range)
+            a = ops.decode_attention(q, kc, vc, lens, max_len=max_len)
+            o = F.linear(a.view(B, -1), L["wo"])
+            h, residual = ops.rmsnorm(o, L["ffn_norm"], c.eps, residual=residual)
+            m = F.linear(ops.silu_mul(F.linear(h, L["w_gate_up"])), L["w_down"])
+            nxt = self.layers[i + 1]["attn_norm"] if i + 1 < len(self.layers) else self.final_norm
+            h, residual = ops.rmsnorm(m, nxt, c.eps, residual=residual)
+        logits = F.linear(h, self.lm_head)
+        ids = ops.argmax(logits)
+        return (ids, logits) if return_logits else ids
+
+    def cache_views_contiguous(self) -> bool:
+        return all(self.k_cache[i, : self.max_batch].is_contiguous() for i in range(self.cfg.n_layers))
+
+    # ------------------------------------------------------------------ fp32 reference
+    @torch.no_grad()
+    def reference_logits(self, seqs: torch.Tensor) -> torch.Tensor:
+        """fp32 forward of full sequences [B, T]; returns logits of the last position [B, V]."""
+        c = self.cfg
+        B, T = seqs.shape
+        f32 = lambda t: t.float()
+        x = f32(self.embed)[seqs]  # [B, T, dim]
+
+        def rms(v, wgt):
+            return v * torch.rsqrt(v.pow(2).mean(-1, keepdim=True) + c.eps) * f32(wgt)
+
+        def bf(v):  # mirror the bf16 storage points of the HIP path
+            return v.to(torch.bfloat16).float()
+
+        pos = torch.arange(T, device=seqs.device, dtype=torch.float32)
+        inv_freq = torch.exp2(-math.log2(c.rope_theta) * torch.arange(0, c.head_dim // 2, device=seqs.device,
+                                                                      dtype=torch.float32) * 2 / c.head_dim)
+        ang = pos[:, None] * inv_freq[None, :]
+        cos, sin = torch.cos(ang), torch.sin(ang)
+
+        def rope(t):  # [B, T, nh, D]
+            half = c.head_dim // 2
+            t1, t2 = t[..., :half], t[..., half:]
+            cc, ss = cos[None, :, None, :], sin[None, :, None, :]
+            return torch.cat([t1 * cc - t2 * ss, t2 * cc + t1 * ss], -1)
+
+        residual = x
+        h = bf(rms(x, self.layers[0]["attn_norm"]))
+        G = c.n_heads // c.n_kv_heads
+        mask = torch.full((T, T), float("-inf"), device=seqs.device).triu(1)
+        for i, L in enumerate(self.layers):
+            qkv = bf(h @ f32(L["wqkv"]).T)
+            q = qkv[..., : c.n_heads * c.head_dim].view(B, T, c.n_heads, c.head_dim)
+            k = qkv[..., c.n_heads * c.head_dim: (c.n_heads + c.n_kv_heads) * c.head_dim].view(
+                B, T, c.n_kv_heads, c.head_dim)
+            v = qkv[..., (c.n_heads + c.n_kv_heads) * c.head_dim:].view(B, T, c.n_kv_heads, c.head_dim)
+            q, k = bf(rope(q)), bf(rope(k))
+            k = k.repeat_interleave(G, dim=2)
+            v = v.repeat_interleave(G, dim=2)
+            s = torch.einsum("bqhd,bkhd->bhqk", q, k) / math.sqrt(c.head_dim) + mask
+            a = bf(torch.einsum("bhqk,bkhd->bqhd", s.softmax(-1), v).reshape(B, T, -1))
+            o = bf(a @ f32(L["wo"]).T)
+            residual = bf(residual + o)
+            h = bf(rms(residual, L["ffn_norm"]))
+            gu = bf(h @ f32(L["w_gate_up"]).T)
+            g_, u_ = gu[..., : c.ffn], gu[..., c.ffn:]
+            m = bf(bf(F.silu(g_) * u_) @ f32(L["w_down"]).T)
+            residual = bf(residual + m)
+            nxt = self.layers[i + 1]["attn_norm"] if i + 1 < len(self.layers) else self.final_norm
+            h = bf(rms(residual, nxt))
+        return (h[:, -1] @ f32(self.lm_head).T)
+
+    @torch.no_grad()
+    def generate(self, prompt: list[int], max_new: int) -> list[int]:
+        """Greedy single-sequence generation on slot 0 (prefill = sequential decode steps)."""
+        out = []
+        tok = None
+        for p, t in enumerate(prompt + [None] * max_new):
+            if p >= self.cfg.max_seq:
+                break
+            cur = t if t is not None else tok
+            ids = self.decode_step(torch.tensor([cur], device=self.device),
+                                   torch.tensor([p], dtype=torch.int32, device=self.device), (p, p))
+            tok = int(ids.item())
+            if p >= len(prompt) - 1:
+                out.append(tok)
+                if len(out) >= max_new:
+                    break
+        return out

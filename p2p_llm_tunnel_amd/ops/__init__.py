@@ -1,0 +1,178 @@
+"""Python front-end for the gfx950 HIP kernels (``kernels.hip``).
+
+The kernels are compiled in-tree into ``_hip_ops.so`` (see ``build.py``) and
+called through ctypes on the current torch stream. Every wrapper validates
+shapes, dtypes, devices and contiguity on the host *before* launching, so a
+mismatched tensor raises instead of faulting the GPU. There is no silent
+PyTorch fallback: if the library is missing on a GPU host, ``lib()`` raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def lib() -> ctypes.CDLL:
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(HERE, "_hip_ops.so")
+        if not os.path.exists(path):
+            from . import build as _b
+            _b.build()
+        _LIB = ctypes.CDLL(path)
+        vp, i, f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+        _LIB.p2pt_rmsnorm.argtypes = [vp, vp, vp, vp, vp, i, i, f, vp]
+        _LIB.p2pt_silu_mul.argtypes = [vp, vp, i, i, vp]
+        _LIB.p2pt_rope_qkv_cache.argtypes = [vp, vp, vp, vp, vp, i, i, i, i, i, f, vp]
+        _LIB.p2pt_decode_attention.argtypes = [vp, vp, vp, vp, vp, vp, i, i, i, i, i, i, i, f, vp]
+        _LIB.p2pt_argmax.argtypes = [vp, vp, i, i, vp]
+        for fn in ("p2pt_rmsnorm", "p2pt_silu_mul", "p2pt_rope_qkv_cache", "p2pt_decode_attention", "p2pt_argmax"):
+            getattr(_LIB, fn).restype = ctypes.c_int
+    return _LIB
+
+
+def loaded_path() -> str:
+    lib()
+    return os.path.join(HERE, "_hip_ops.so")
+
+
+def _stream(t: torch.Tensor):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _check(t: torch.Tensor, dtype, name: str, device=None):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be on a HIP device")
+    if device is not None and t.device != device:
+        raise ValueError(f"{name} on {t.device}, expected {device}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+def _ok(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"{what}: HIP launch failed (hipError {rc})")
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def rmsnorm(x: torch.Tensor, weight: torch.Tensor, eps: float = 1e-6, residual: torch.Tensor | None = None):
+    """out = rmsnorm(x [+ residual]) * weight. With a residual, returns (out, x + residual)."""
+    _check(x, torch.bfloat16, "x")
+    _check(weight, torch.bfloat16, "weight", x.device)
+    hidden = x.shape[-1]
+    if weight.shape != (hidden,):
+        raise ValueError(f"weight shape {tuple(weight.shape)} != ({hidden},)")
+    if hidden % 8 or hidden > 16384:
+        raise ValueError("hidden must be a multiple of 8 and <= 16384")
+    rows = x.numel() // hidden
+    out = torch.empty_like(x)
+    res_out = None
+    if residual is not None:
+        _check(residual, torch.bfloat16, "residual", x.device)
+        if residual.shape != x.shape:
+            raise ValueError("residual shape mismatch")
+        res_out = torch.empty_like(x)
+    _ok(lib().p2pt_rmsnorm(_p(x), _p(residual), _p(res_out), _p(weight), _p(out), rows, hidden, eps, _stream(x)),
+        "rmsnorm")
+    return out if residual is None else (out, res_out)
+
+
+def silu_mul(gate_up: torch.Tensor) -> torch.Tensor:
+    """[..., 2F] -> silu(gate) * up, [..., F]."""
+    _check(gate_up, torch.bfloat16, "gate_up")
+    two_f = gate_up.shape[-1]
+    if two_f % 16:
+        raise ValueError("last dim must be 2*F with F % 8 == 0")
+    F = two_f // 2
+    rows = gate_up.numel() // two_f
+    out = torch.empty(*gate_up.shape[:-1], F, dtype=gate_up.dtype, device=gate_up.device)
+    _ok(lib().p2pt_silu_mul(_p(gate_up), _p(out), rows, F, _stream(gate_up)), "silu_mul")
+    return out
+
+
+def rope_qkv_cache(qkv: torch.Tensor, pos: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                   n_heads: int, n_kv_heads: int, head_dim: int, theta: float = 10000.0,
+                   pos_range: tuple[int, int] | None = None) -> torch.Tensor:
+    """Apply RoPE to q and k of one new token per sequence and append k, v to the caches.
+
+    qkv: [B, (H + 2*Hkv) * D]; pos: int32 [B]; caches: [B, Smax, Hkv, D]. Returns q [B, H, D].
+    ``pos_range`` = host-known (min, max) of ``pos``; without it the bounds are
+    read back from the device (a sync) before launch.
+    """
+    _check(qkv, torch.bfloat16, "qkv")
+    _check(pos, torch.int32, "pos", qkv.device)
+    _check(k_cache, torch.bfloat16, "k_cache", qkv.device)
+    _check(v_cache, torch.bfloat16, "v_cache", qkv.device)
+    B = qkv.shape[0]
+    if qkv.shape != (B, (n_heads + 2 * n_kv_heads) * head_dim):
+        raise ValueError(f"qkv shape {tuple(qkv.shape)} inconsistent with heads")
+    if pos.shape != (B,):
+        raise ValueError("pos must be [B]")
+    Smax = k_cache.shape[1]
+    if k_cache.shape != (B, Smax, n_kv_heads, head_dim) or v_cache.shape != k_cache.shape:
+        raise ValueError(f"cache shape {tuple(k_cache.shape)} != ({B}, Smax, {n_kv_heads}, {head_dim})")
+    if n_heads % n_kv_heads or head_dim % 2:
+        raise ValueError("bad head config")
+    pmin, pmax = pos_range if pos_range is not None else (int(pos.min().item()), int(pos.max().item()))
+    if pmin < 0 or pmax >= Smax:
+        raise ValueError(f"positions out of cache range [0, {Smax})")
+    q = torch.empty(B, n_heads, head_dim, dtype=qkv.dtype, device=qkv.device)
+    _ok(lib().p2pt_rope_qkv_cache(_p(qkv), _p(pos), _p(q), _p(k_cache), _p(v_cache), B, n_heads, n_kv_heads,
+                                  head_dim, Smax, theta, _stream(qkv)), "rope_qkv_cache")
+    return q
+
+
+def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, lens: torch.Tensor,
+                     chunk: int = 256, max_len: int | None = None, scale: float | None = None) -> torch.Tensor:
+    """Single-token GQA attention over the KV cache. q: [B, H, D]; lens: int32 [B] (>= 1)."""
+    _check(q, torch.bfloat16, "q")
+    _check(k_cache, torch.bfloat16, "k_cache", q.device)
+    _check(v_cache, torch.bfloat16, "v_cache", q.device)
+    _check(lens, torch.int32, "lens", q.device)
+    B, H, D = q.shape
+    Smax, Hkv = k_cache.shape[1], k_cache.shape[2]
+    if k_cache.shape != (B, Smax, Hkv, D) or v_cache.shape != k_cache.shape:
+        raise ValueError("cache shape mismatch")
+    if D not in (64, 128):
+        raise ValueError("head_dim must be 64 or 128")
+    if H % Hkv or H // Hkv > 8:
+        raise ValueError("n_heads / n_kv_heads must be an integer <= 8")
+    if lens.shape != (B,):
+        raise ValueError("lens must be [B]")
+    if max_len is None:
+        max_len = int(lens.max().item())
+        if int(lens.min().item()) < 1:
+            raise ValueError("every sequence needs at least one cached token")
+    if max_len > Smax:
+        raise ValueError("lens exceed cache capacity")
+    nsplit = max(1, math.ceil(max_len / chunk))
+    ws = torch.empty(B * H * nsplit * (D + 2), dtype=torch.float32, device=q.device)
+    out = torch.empty_like(q)
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    _ok(lib().p2pt_decode_attention(_p(q), _p(k_cache), _p(v_cache), _p(lens), _p(out), _p(ws), B, H, Hkv, D, Smax,
+                                    nsplit, chunk, scale, _stream(q)), "decode_attention")
+    return out
+
+
+def argmax(logits: torch.Tensor) -> torch.Tensor:
+    """Row-wise argmax (first index on ties) of bf16 logits [B, V] -> int64 [B]."""
+    _check(logits, torch.bfloat16, "logits")
+    if logits.dim() != 2:
+        raise ValueError("logits must be [B, V]")
+    B, V = logits.shape
+    out = torch.empty(B, dtype=torch.int64, device=logits.device)
+    _ok(lib().p2pt_argmax(_p(logits), _p(out), B, V, _stream(logits)), "argmax")
+    return out

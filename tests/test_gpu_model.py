@@ -1,0 +1,59 @@
+"""The on-node inference upstream: HIP decode vs fp32 reference, and the
+GPU endpoint streamed through a real tunnel."""
+import http.client
+import json
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+cuda = pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a HIP device")
+
+
+@cuda
+@pytest.mark.parametrize("cfg", ["micro", "tiny"])
+def test_decode_matches_fp32_reference(cfg):
+    from p2p_llm_tunnel_amd.models.tiny_llm import TinyLlama
+    m = TinyLlama(cfg, device="cuda", max_batch=3, seed=1)
+    torch.manual_seed(0)
+    T = 37
+    seqs = torch.randint(0, m.cfg.vocab, (3, T), device="cuda")
+    logits = None
+    for p in range(T):
+        _, logits = m.decode_step(seqs[:, p], torch.full((3,), p, dtype=torch.int32, device="cuda"), (p, p),
+                                  return_logits=True)
+    ref = m.reference_logits(seqs)
+    err = (logits.float() - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    assert err < 0.05 * scale, (err, scale)
+    # top-1 agreement where the reference margin is comfortable
+    top2 = ref.topk(2, -1).values
+    confident = (top2[:, 0] - top2[:, 1]) > 0.05 * scale
+    assert torch.equal(logits.float().argmax(-1)[confident], ref.argmax(-1)[confident])
+
+
+@cuda
+def test_gpu_endpoint_through_tunnel():
+    from p2p_llm_tunnel_amd.models.server import start_server
+    from p2p_llm_tunnel_amd.utils.procs import Tunnel
+    srv, port, engine = start_server(device="cuda:0", config="micro", max_batch=4)
+    try:
+        with Tunnel(f"http://127.0.0.1:{port}", transport=os.environ.get("P2PT_TRANSPORT", "webrtc")) as t:
+            outs = []
+            for stream in (True, False):
+                c = http.client.HTTPConnection("127.0.0.1", t.proxy_port, timeout=60)
+                c.request("POST", "/v1/chat/completions",
+                          body=json.dumps({"stream": stream, "max_tokens": 6,
+                                           "messages": [{"role": "user", "content": "hi there"}]}),
+                          headers={"content-type": "application/json"})
+                r = c.getresponse()
+                assert r.status == 200
+                outs.append(r.read())
+            events = [l for l in outs[0].split(b"\n") if l.startswith(b"data: ")]
+            assert len(events) == 6 + 2 and events[-1] == b"data: [DONE]"
+            streamed = "".join(json.loads(e[6:])["choices"][0]["delta"].get("content", "") for e in events[:-1])
+            assert streamed == json.loads(outs[1])["choices"][0]["message"]["content"]  # deterministic greedy
+    finally:
+        engine.stop()
+        srv.shutdown()

@@ -1,0 +1,152 @@
+"""Numerics of the gfx950 HIP kernels vs plain fp32 PyTorch references.
+
+All tests need an MI355X (``-m gpu``). They also assert that the kernels ran
+from the in-tree ``_hip_ops.so`` (no silent fallback exists).
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+cuda = pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a HIP device")
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from p2p_llm_tunnel_amd import ops as o
+    o.lib()
+    return o
+
+
+def bf(x):
+    return x.to(torch.bfloat16)
+
+
+def close(a, b, tol):
+    err = (a.float() - b.float()).abs().max().item()
+    scale = b.float().abs().max().item() + 1e-6
+    assert err <= tol * scale, f"max err {err} vs scale {scale}"
+
+
+@cuda
+@pytest.mark.parametrize("rows,hidden", [(1, 1024), (7, 4096), (33, 8192), (4, 256), (2, 16384)])
+def test_rmsnorm(ops, rows, hidden):
+    torch.manual_seed(0)
+    x = bf(torch.randn(rows, hidden, device="cuda"))
+    w = bf(1 + 0.1 * torch.randn(hidden, device="cuda"))
+    ref = x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-6) * w.float()
+    close(ops.rmsnorm(x, w, 1e-6), ref, 1e-2)
+
+
+@cuda
+def test_rmsnorm_fused_residual(ops):
+    torch.manual_seed(1)
+    x = bf(torch.randn(9, 2048, device="cuda"))
+    r = bf(torch.randn(9, 2048, device="cuda"))
+    w = bf(torch.ones(2048, device="cuda"))
+    out, res = ops.rmsnorm(x, w, 1e-5, residual=r)
+    s = (x.float() + r.float()).to(torch.bfloat16).float()
+    assert torch.equal(res.float(), s)
+    close(out, s * torch.rsqrt(s.pow(2).mean(-1, keepdim=True) + 1e-5), 1e-2)
+
+
+@cuda
+@pytest.mark.parametrize("rows,F", [(1, 2816), (16, 5632), (3, 8)])
+def test_silu_mul(ops, rows, F):
+    torch.manual_seed(2)
+    gu = bf(torch.randn(rows, 2 * F, device="cuda") * 3)
+    ref = torch.nn.functional.silu(gu[:, :F].float()) * gu[:, F:].float()
+    close(ops.silu_mul(gu), ref, 1e-2)
+
+
+def rope_ref(x, pos, D, theta):
+    half = D // 2
+    inv = torch.exp2(-math.log2(theta) * torch.arange(half, device=x.device, dtype=torch.float32) * 2 / D)
+    ang = pos.float()[:, None, None] * inv[None, None, :]
+    c, s = torch.cos(ang), torch.sin(ang)
+    x1, x2 = x[..., :half].float(), x[..., half:].float()
+    return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], -1)
+
+
+@cuda
+@pytest.mark.parametrize("D", [64, 128])
+def test_rope_qkv_cache(ops, D):
+    torch.manual_seed(3)
+    B, H, Hkv, Smax = 5, 8, 2, 300
+    qkv = bf(torch.randn(B, (H + 2 * Hkv) * D, device="cuda"))
+    pos = torch.tensor([0, 1, 17, 150, 299], dtype=torch.int32, device="cuda")
+    kc = torch.zeros(B, Smax, Hkv, D, dtype=torch.bfloat16, device="cuda")
+    vc = torch.zeros_like(kc)
+    q = ops.rope_qkv_cache(qkv, pos, kc, vc, H, Hkv, D)
+    qr = rope_ref(qkv[:, : H * D].view(B, H, D), pos, D, 10000.0)
+    kr = rope_ref(qkv[:, H * D:(H + Hkv) * D].view(B, Hkv, D), pos, D, 10000.0)
+    close(q, qr, 1e-2)
+    bidx = torch.arange(B, device="cuda")
+    close(kc[bidx, pos.long()], kr, 1e-2)
+    assert torch.equal(vc[bidx, pos.long()], qkv[:, (H + Hkv) * D:].view(B, Hkv, D))
+    # untouched positions stay zero
+    assert kc[0, 1:].abs().sum().item() == 0
+
+
+def attn_ref(q, kc, vc, lens):
+    B, H, D = q.shape
+    Hkv = kc.shape[2]
+    G = H // Hkv
+    out = torch.empty(B, H, D, device=q.device)
+    for b in range(B):
+        L = int(lens[b])
+        k = kc[b, :L].float().repeat_interleave(G, dim=1)  # [L, H, D]
+        v = vc[b, :L].float().repeat_interleave(G, dim=1)
+        s = torch.einsum("hd,lhd->hl", q[b].float(), k) / math.sqrt(D)
+        out[b] = torch.einsum("hl,lhd->hd", s.softmax(-1), v)
+    return out
+
+
+@cuda
+@pytest.mark.parametrize("D,H,Hkv", [(64, 16, 4), (128, 32, 8), (128, 8, 1), (64, 8, 8)])
+@pytest.mark.parametrize("chunk", [64, 256])
+def test_decode_attention(ops, D, H, Hkv, chunk):
+    torch.manual_seed(4)
+    B, Smax = 4, 1100
+    q = bf(torch.randn(B, H, D, device="cuda"))
+    kc = bf(torch.randn(B, Smax, Hkv, D, device="cuda"))
+    vc = bf(torch.randn(B, Smax, Hkv, D, device="cuda"))
+    lens = torch.tensor([1, 63, 700, 1100], dtype=torch.int32, device="cuda")
+    out = ops.decode_attention(q, kc, vc, lens, chunk=chunk)
+    close(out, attn_ref(q, kc, vc, lens), 2e-2)
+
+
+@cuda
+@pytest.mark.parametrize("V", [32000, 4096, 1001])
+def test_argmax(ops, V):
+    torch.manual_seed(5)
+    x = bf(torch.randn(6, V, device="cuda"))
+    x[2, 5] = 100.0
+    x[3, :] = 1.0  # all ties -> first index
+    got = ops.argmax(x)
+    assert torch.equal(got, x.float().argmax(-1))
+    assert got[3].item() == 0
+
+
+@cuda
+def test_host_side_shape_checks(ops):
+    q = bf(torch.randn(2, 8, 64, device="cuda"))
+    kc = bf(torch.randn(2, 10, 2, 64, device="cuda"))
+    with pytest.raises(ValueError):
+        ops.decode_attention(q, kc, kc, torch.tensor([5, 11], dtype=torch.int32, device="cuda"))  # > Smax
+    with pytest.raises(TypeError):
+        ops.argmax(torch.randn(2, 10, device="cuda"))  # fp32
+    with pytest.raises(ValueError):
+        ops.rope_qkv_cache(bf(torch.randn(2, 5, device="cuda")), torch.zeros(2, dtype=torch.int32, device="cuda"),
+                           kc, kc, 8, 2, 64)
+
+
+@cuda
+def test_native_library_is_loaded(ops):
+    import os
+    path = ops.loaded_path()
+    assert os.path.exists(path)
+    with open("/proc/self/maps") as f:
+        assert "_hip_ops.so" in f.read()
