@@ -307,7 +307,7 @@ void TcpConn::do_read() {
         return;
       }
     }
-    if (on_data_) on_data_(buf, size_t(n));
+    if (auto cb = on_data_) (*cb)(buf, size_t(n));
     if (size_t(n) < sizeof buf && !ssl_) return;
   }
 }

@@ -76,7 +76,9 @@ class TcpConn : public std::enable_shared_from_this<TcpConn> {
 
   ~TcpConn();
 
-  void on_data(DataFn f) { on_data_ = std::move(f); }
+  // The callback may replace itself (e.g. an HTTP upgrade handing the socket
+  // to a WebSocket): it is held by shared_ptr and pinned during each call.
+  void on_data(DataFn f) { on_data_ = f ? std::make_shared<DataFn>(std::move(f)) : nullptr; }
   void on_close(CloseFn f) { on_close_ = std::move(f); }
   // Fires when the output buffer drains below `low_water` after having been above it.
   void on_drain(Fn f, size_t low_water = 0) {
@@ -124,7 +126,7 @@ class TcpConn : public std::enable_shared_from_this<TcpConn> {
   size_t out_bytes_ = 0;
   bool above_low_ = false;
   size_t low_water_ = 0;
-  DataFn on_data_;
+  std::shared_ptr<DataFn> on_data_;
   CloseFn on_close_;
   Fn on_drain_;
   uint32_t interest_ = 0;

@@ -1,0 +1,782 @@
+#include "rtc/ice.h"
+
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <sys/epoll.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+#include <sstream>
+
+#include "core/crypto.h"
+#include "core/log.h"
+#include "rtc/turn.h"
+
+namespace p2pt::rtc {
+
+static const char* kT = "tunnel::ice";
+
+// ---------------------------------------------------------------- Candidate
+
+uint32_t candidate_priority(const std::string& type, uint32_t local_pref, int component) {
+  uint32_t tp = type == "host" ? 126 : type == "prflx" ? 110 : type == "srflx" ? 100 : 0;
+  return (tp << 24) | ((local_pref & 0xFFFF) << 8) | uint32_t(256 - component);
+}
+
+std::string Candidate::to_sdp() const {
+  std::ostringstream o;
+  o << "candidate:" << foundation << " " << component << " " << transport << " " << priority << " " << addr.ip()
+    << " " << addr.port() << " typ " << type;
+  if (has_related) o << " raddr " << related.ip() << " rport " << related.port();
+  return o.str();
+}
+
+bool Candidate::parse(const std::string& s_in, Candidate& out, std::string* err) {
+  std::string s = s_in;
+  if (s.rfind("a=", 0) == 0) s = s.substr(2);
+  if (s.rfind("candidate:", 0) == 0) s = s.substr(10);
+  std::istringstream in(s);
+  std::vector<std::string> tok;
+  std::string t;
+  while (in >> t) tok.push_back(t);
+  if (tok.size() < 8 || tok[6] != "typ") {
+    if (err) *err = "malformed candidate: " + s_in;
+    return false;
+  }
+  out = Candidate{};
+  out.foundation = tok[0];
+  out.component = atoi(tok[1].c_str());
+  std::string tr = tok[2];
+  for (auto& c : tr) c = char(tolower(c));
+  out.transport = tr;
+  if (tr != "udp") {
+    if (err) *err = "unsupported candidate transport: " + tok[2];
+    return false;
+  }
+  out.priority = uint32_t(strtoul(tok[3].c_str(), nullptr, 10));
+  int port = atoi(tok[5].c_str());
+  if (!SockAddr::parse(tok[4], uint16_t(port), out.addr)) {
+    if (err) *err = "unresolvable candidate address (mDNS?): " + tok[4];
+    return false;
+  }
+  out.type = tok[7];
+  for (size_t i = 8; i + 1 < tok.size(); i += 2) {
+    if (tok[i] == "raddr") {
+      int rport = 0;
+      if (i + 3 < tok.size() && tok[i + 2] == "rport") rport = atoi(tok[i + 3].c_str());
+      out.has_related = SockAddr::parse(tok[i + 1], uint16_t(rport), out.related);
+    }
+  }
+  return true;
+}
+
+const char* ice_state_name(IceState s) {
+  switch (s) {
+    case IceState::New: return "new";
+    case IceState::Checking: return "checking";
+    case IceState::Connected: return "connected";
+    case IceState::Disconnected: return "disconnected";
+    case IceState::Failed: return "failed";
+    case IceState::Closed: return "closed";
+  }
+  return "?";
+}
+
+// ---------------------------------------------------------------- agent
+
+std::shared_ptr<IceAgent> IceAgent::create(Reactor& r, IceConfig cfg, bool controlling) {
+  return std::shared_ptr<IceAgent>(new IceAgent(r, std::move(cfg), controlling));
+}
+
+IceAgent::IceAgent(Reactor& r, IceConfig cfg, bool controlling)
+    : r_(r), cfg_(std::move(cfg)), controlling_(controlling), tiebreaker_(random_u64()) {
+  ufrag_ = random_ice_chars(16);
+  pwd_ = random_ice_chars(32);
+  rxbuf_.resize(size_t(32) * 65536);
+}
+
+IceAgent::~IceAgent() { close(); }
+
+void IceAgent::close() {
+  if (closed_) return;
+  closed_ = true;
+  if (tick_timer_) r_.cancel(tick_timer_);
+  tick_timer_ = 0;
+  if (flush_hook_) r_.remove_flush_hook(flush_hook_);
+  flush_hook_ = 0;
+  if (turn_) turn_->close();
+  turn_.reset();
+  for (auto& s : socks_) {
+    if (s.fd >= 0) {
+      r_.remove(s.fd);
+      ::close(s.fd);
+      s.fd = -1;
+    }
+  }
+  state_ = IceState::Closed;
+}
+
+void IceAgent::set_state(IceState s) {
+  if (s == state_) return;
+  state_ = s;
+  LOG_DEBUG(kT, "ICE state: %s", ice_state_name(s));
+  if (on_state) {
+    auto cb = on_state;
+    cb(s);
+  }
+}
+
+void IceAgent::open_sockets() {
+  auto addrs = local_addresses(cfg_.include_loopback, cfg_.include_ipv6);
+  // Non-loopback first so they get the higher local preference.
+  std::stable_sort(addrs.begin(), addrs.end(),
+                   [](const IfaceAddr& a, const IfaceAddr& b) { return !a.addr.is_loopback() && b.addr.is_loopback(); });
+  std::weak_ptr<IceAgent> w = shared_from_this();
+  for (auto& ia : addrs) {
+    int fd = ::socket(ia.addr.family(), SOCK_DGRAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+    if (fd < 0) continue;
+    if (ia.addr.family() == AF_INET6) {
+      int one = 1;
+      setsockopt(fd, IPPROTO_IPV6, IPV6_V6ONLY, &one, sizeof one);
+    }
+    int buf = 4 << 20;
+    setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &buf, sizeof buf);
+    setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &buf, sizeof buf);
+    SockAddr a = ia.addr;
+    a.set_port(0);
+    if (::bind(fd, a.sa(), a.len) < 0) {
+      ::close(fd);
+      continue;
+    }
+    SockAddr bound;
+    bound.len = sizeof bound.ss;
+    getsockname(fd, bound.sa(), &bound.len);
+    Sock s;
+    s.fd = fd;
+    s.addr = bound;
+    s.loopback = bound.is_loopback();
+    int si = int(socks_.size());
+    socks_.push_back(s);
+    r_.add(fd, EPOLLIN, [w, si](uint32_t) {
+      if (auto self = w.lock()) self->on_readable(si);
+    });
+  }
+}
+
+void IceAgent::add_local(Candidate c, int sock, bool relay) {
+  locals_.push_back(Local{c, sock, relay});
+  local_cands_.push_back(c);
+  int li = int(locals_.size()) - 1;
+  for (int ri = 0; ri < int(remotes_.size()); ri++) pair_up(li, ri);
+  LOG_DEBUG(kT, "local candidate: %s", c.to_sdp().c_str());
+  if (on_candidate) on_candidate(c);
+}
+
+void IceAgent::gather() {
+  if (gather_started_ || closed_) return;
+  gather_started_ = true;
+  open_sockets();
+  if (cfg_.auto_flush) flush_hook_ = r_.add_flush_hook([this] { flush(); });
+  uint32_t pref = 65535;
+  for (int si = 0; si < int(socks_.size()); si++) {
+    Candidate c;
+    c.type = "host";
+    c.addr = socks_[si].addr;
+    c.priority = candidate_priority("host", pref);
+    pref -= 256;
+    c.foundation = std::to_string(crc32_ieee(("host" + c.addr.ip()).data(), 4 + c.addr.ip().size()));
+    add_local(c, si, false);
+  }
+  if (socks_.empty()) LOG_WARN(kT, "no usable network interfaces for ICE");
+  start_srflx();
+  start_relay();
+  std::weak_ptr<IceAgent> w = shared_from_this();
+  tick_timer_ = r_.call_later_ms(20, [w] {
+    if (auto s = w.lock()) {
+      s->tick_timer_ = 0;
+      s->tick();
+    }
+  });
+  maybe_gathering_done();
+}
+
+static bool parse_server_url(const std::string& url, std::string& host, uint16_t& port, uint16_t dflt) {
+  std::string s = url;
+  size_t colon = s.find(':');
+  if (colon == std::string::npos) return false;
+  s = s.substr(colon + 1);  // strip scheme
+  if (s.rfind("//", 0) == 0) s = s.substr(2);
+  size_t q = s.find('?');
+  if (q != std::string::npos) s = s.substr(0, q);
+  port = dflt;
+  if (!s.empty() && s[0] == '[') {
+    size_t rb = s.find(']');
+    if (rb == std::string::npos) return false;
+    host = s.substr(1, rb - 1);
+    if (rb + 1 < s.size() && s[rb + 1] == ':') port = uint16_t(atoi(s.c_str() + rb + 2));
+    return true;
+  }
+  size_t pc = s.rfind(':');
+  if (pc != std::string::npos) {
+    host = s.substr(0, pc);
+    port = uint16_t(atoi(s.c_str() + pc + 1));
+  } else {
+    host = s;
+  }
+  return !host.empty();
+}
+
+void IceAgent::start_srflx() {
+  std::weak_ptr<IceAgent> w = shared_from_this();
+  for (auto& url : cfg_.stun_urls) {
+    std::string host;
+    uint16_t port;
+    if (!parse_server_url(url, host, port, 3478)) {
+      LOG_WARN(kT, "ignoring invalid STUN URL %s", url.c_str());
+      continue;
+    }
+    pending_gather_++;
+    // Bound the whole srflx attempt (DNS included) so gathering can finish
+    // offline without waiting for the resolver.
+    auto done = std::make_shared<bool>(false);
+    r_.call_later_ms(cfg_.stun_timeout_ms, [w, done] {
+      if (*done) return;
+      *done = true;
+      if (auto s = w.lock()) {
+        s->pending_gather_--;
+        s->maybe_gathering_done();
+      }
+    });
+    resolve_async(r_, host, port, [w, done, url](std::vector<SockAddr> addrs, std::string err) {
+      auto s = w.lock();
+      if (!s || *done) return;
+      if (addrs.empty()) {
+        LOG_DEBUG(kT, "STUN server %s unresolvable: %s", url.c_str(), err.c_str());
+        *done = true;
+        s->pending_gather_--;
+        s->maybe_gathering_done();
+        return;
+      }
+      for (int si = 0; si < int(s->socks_.size()); si++) {
+        if (s->socks_[si].loopback) continue;
+        for (auto& a : addrs) {
+          if (a.family() != s->socks_[si].addr.family()) continue;
+          auto m = stun::Message::make(stun::kBindingRequest);
+          SrflxReq rq{si, a, m.tid_key(), 1};
+          auto bytes = m.serialize(nullptr, true);
+          s->send_raw(-1 - si, a, bytes.data(), bytes.size());
+          s->srflx_.push_back(rq);
+          break;
+        }
+      }
+      // srflx responses are matched in handle_response; the timeout above
+      // closes the gathering window.
+      (void)done;
+    });
+  }
+}
+
+void IceAgent::start_relay() {
+  if (cfg_.turn_url.empty()) return;
+  int si = -1;
+  for (int i = 0; i < int(socks_.size()); i++)
+    if (!socks_[i].loopback && socks_[i].addr.family() == AF_INET) {
+      si = i;
+      break;
+    }
+  if (si < 0) {
+    LOG_WARN(kT, "TURN: no non-loopback IPv4 socket to allocate from");
+    return;
+  }
+  std::string host;
+  uint16_t port;
+  if (!parse_server_url(cfg_.turn_url, host, port, 3478)) {
+    LOG_WARN(kT, "invalid TURN URL %s", cfg_.turn_url.c_str());
+    return;
+  }
+  pending_gather_++;
+  std::weak_ptr<IceAgent> w = shared_from_this();
+  turn_ = TurnClient::create(r_, this, si, host, port, cfg_.turn_user, cfg_.turn_pass,
+                             [w, si](bool ok, const SockAddr& relayed, const SockAddr& mapped) {
+                               auto s = w.lock();
+                               if (!s) return;
+                               if (ok) {
+                                 Candidate c;
+                                 c.type = "relay";
+                                 c.addr = relayed;
+                                 c.related = mapped;
+                                 c.has_related = true;
+                                 c.priority = candidate_priority("relay", 65535);
+                                 c.foundation = std::to_string(
+                                     crc32_ieee(("relay" + relayed.ip()).data(), 5 + relayed.ip().size()));
+                                 s->add_local(c, si, true);
+                               }
+                               s->pending_gather_--;
+                               s->maybe_gathering_done();
+                             });
+}
+
+void IceAgent::maybe_gathering_done() {
+  if (gathering_done_ || pending_gather_ > 0) return;
+  gathering_done_ = true;
+  LOG_DEBUG(kT, "ICE gathering complete (%zu local candidates)", local_cands_.size());
+  if (on_gathering_done) {
+    auto cb = on_gathering_done;
+    std::weak_ptr<IceAgent> w = shared_from_this();
+    r_.post([w, cb] {
+      if (w.lock()) cb();
+    });
+  }
+}
+
+void IceAgent::set_remote_credentials(const std::string& ufrag, const std::string& pwd) {
+  remote_ufrag_ = ufrag;
+  remote_pwd_ = pwd;
+  if (state_ == IceState::New) {
+    checking_since_ = Reactor::now_ms();
+    set_state(IceState::Checking);
+  }
+}
+
+int IceAgent::find_remote(const SockAddr& a) const {
+  for (int i = 0; i < int(remotes_.size()); i++)
+    if (remotes_[i].addr == a) return i;
+  return -1;
+}
+
+void IceAgent::add_remote_candidate(const Candidate& c) {
+  if (closed_ || c.component != 1) return;
+  if (find_remote(c.addr) >= 0) return;
+  remotes_.push_back(c);
+  int ri = int(remotes_.size()) - 1;
+  LOG_DEBUG(kT, "remote candidate: %s", c.to_sdp().c_str());
+  for (int li = 0; li < int(locals_.size()); li++) pair_up(li, ri);
+  if (state_ == IceState::New && !remote_pwd_.empty()) {
+    checking_since_ = Reactor::now_ms();
+    set_state(IceState::Checking);
+  }
+}
+
+uint64_t IceAgent::pair_priority(const Local& l, const Candidate& r) const {
+  uint64_t g = controlling_ ? l.c.priority : r.priority;
+  uint64_t d = controlling_ ? r.priority : l.c.priority;
+  return (std::min(g, d) << 32) + 2 * std::max(g, d) + (g > d ? 1 : 0);
+}
+
+void IceAgent::pair_up(int li, int ri) {
+  const Local& l = locals_[li];
+  const Candidate& rc = remotes_[ri];
+  if (l.c.type == "srflx") return;  // checks run from the base (host) candidate
+  SockAddr laddr = l.relay ? l.c.addr : socks_[l.sock].addr;
+  if (laddr.family() != rc.addr.family()) return;
+  // Loopback sockets only talk to loopback remotes and vice versa.
+  if (!l.relay && socks_[l.sock].loopback != rc.addr.is_loopback()) return;
+  for (auto& p : pairs_)
+    if (p.local == li && p.remote == ri) return;
+  Pair p;
+  p.local = li;
+  p.remote = ri;
+  p.prio = pair_priority(l, rc);
+  pairs_.push_back(p);
+  if (l.relay && turn_) turn_->permit(rc.addr);
+}
+
+void IceAgent::send_raw(int local_idx, const SockAddr& to, const uint8_t* p, size_t n) {
+  Out o;
+  o.local = local_idx;
+  o.to = to;
+  o.data.assign(p, p + n);
+  outq_.push_back(std::move(o));
+}
+
+void IceAgent::send(const uint8_t* p, size_t n) {
+  if (sel_local_ < 0 || closed_) return;
+  send_raw(sel_local_, sel_remote_, p, n);
+}
+
+void IceAgent::flush() {
+  if (outq_.empty() || closed_) {
+    outq_.clear();
+    return;
+  }
+  // Group consecutive datagrams by socket for sendmmsg.
+  constexpr int kBatch = 64;
+  mmsghdr msgs[kBatch];
+  iovec iovs[kBatch];
+  size_t i = 0;
+  while (i < outq_.size()) {
+    // Resolve the socket (relay locals go through TURN).
+    int li = outq_[i].local;
+    if (li >= 0 && locals_[li].relay) {
+      if (turn_) turn_->send_to(outq_[i].to, outq_[i].data.data(), outq_[i].data.size());
+      i++;
+      continue;
+    }
+    int si = li >= 0 ? locals_[li].sock : (-1 - li);
+    int fd = socks_[si].fd;
+    int cnt = 0;
+    size_t j = i;
+    while (j < outq_.size() && cnt < kBatch) {
+      int lj = outq_[j].local;
+      if (lj >= 0 && locals_[lj].relay) break;
+      int sj = lj >= 0 ? locals_[lj].sock : (-1 - lj);
+      if (sj != si) break;
+      memset(&msgs[cnt], 0, sizeof msgs[cnt]);
+      iovs[cnt].iov_base = outq_[j].data.data();
+      iovs[cnt].iov_len = outq_[j].data.size();
+      msgs[cnt].msg_hdr.msg_iov = &iovs[cnt];
+      msgs[cnt].msg_hdr.msg_iovlen = 1;
+      msgs[cnt].msg_hdr.msg_name = const_cast<sockaddr*>(outq_[j].to.sa());
+      msgs[cnt].msg_hdr.msg_namelen = outq_[j].to.len;
+      cnt++;
+      j++;
+    }
+    int sent = 0;
+    while (sent < cnt) {
+      int rc = sendmmsg(fd, msgs + sent, unsigned(cnt - sent), 0);
+      if (rc < 0) {
+        if (errno == EINTR) continue;
+        // EAGAIN (socket buffer full) or unreachable: drop; SCTP retransmits.
+        if (errno != EAGAIN) LOG_TRACE(kT, "sendmmsg: %s", strerror(errno));
+        break;
+      }
+      sent += rc;
+    }
+    i = j;
+  }
+  outq_.clear();
+}
+
+int IceAgent::local_for_socket(int si, bool relay) const {
+  for (int i = 0; i < int(locals_.size()); i++)
+    if (locals_[i].sock == si && locals_[i].relay == relay && locals_[i].c.type != "srflx") return i;
+  return -1;
+}
+
+void IceAgent::on_readable(int si) {
+  if (closed_) return;
+  auto self = shared_from_this();
+  constexpr int kBatch = 32;
+  mmsghdr msgs[kBatch];
+  iovec iovs[kBatch];
+  sockaddr_storage from[kBatch];
+  for (int round = 0; round < 8 && !closed_; round++) {
+    for (int i = 0; i < kBatch; i++) {
+      memset(&msgs[i], 0, sizeof msgs[i]);
+      iovs[i].iov_base = rxbuf_.data() + size_t(i) * 65536;
+      iovs[i].iov_len = 65536;
+      msgs[i].msg_hdr.msg_iov = &iovs[i];
+      msgs[i].msg_hdr.msg_iovlen = 1;
+      msgs[i].msg_hdr.msg_name = &from[i];
+      msgs[i].msg_hdr.msg_namelen = sizeof from[i];
+    }
+    int n = recvmmsg(socks_[si].fd, msgs, kBatch, MSG_DONTWAIT, nullptr);
+    if (n <= 0) return;
+    for (int i = 0; i < n && !closed_; i++) {
+      SockAddr a;
+      memcpy(&a.ss, &from[i], msgs[i].msg_hdr.msg_namelen);
+      a.len = msgs[i].msg_hdr.msg_namelen;
+      const uint8_t* p = rxbuf_.data() + size_t(i) * 65536;
+      size_t len = msgs[i].msg_len;
+      if (turn_ && turn_->is_server(si, a)) {
+        turn_->on_packet(p, len);
+        continue;
+      }
+      handle_datagram(-1, si, a, p, len, false);
+    }
+    if (n < kBatch) return;
+  }
+}
+
+void IceAgent::handle_datagram(int, int si, const SockAddr& from, const uint8_t* p, size_t n, bool via_relay) {
+  if (n == 0) return;
+  last_rx_ = Reactor::now_ms();
+  if (stun::looks_like_stun(p, n)) {
+    handle_stun(si, from, p, n, via_relay);
+    return;
+  }
+  if (state_ == IceState::Disconnected && sel_local_ >= 0) set_state(IceState::Connected);
+  // Data before we selected a pair (the peer nominated first): use the path it used.
+  if (sel_local_ < 0) {
+    int li = local_for_socket(si, via_relay);
+    if (li >= 0 && find_remote(from) >= 0) {
+      sel_local_ = li;
+      sel_remote_ = from;
+    }
+  }
+  if (on_data) on_data(p, n);
+}
+
+void IceAgent::handle_stun(int si, const SockAddr& from, const uint8_t* p, size_t n, bool via_relay) {
+  stun::Message m;
+  if (!stun::Message::parse(p, n, m)) return;
+  if (m.fingerprint_off >= 0 && !stun::verify_fingerprint(p, n, m)) return;
+  if (m.cls() == 0 && m.method() == 1) {
+    handle_request(si, from, m, p, n, via_relay);
+  } else if (m.cls() == 2 || m.cls() == 3) {
+    handle_response(from, m, p, n);
+  }
+  // Binding indications (keepalives) need no action beyond last_rx_.
+}
+
+void IceAgent::handle_request(int si, const SockAddr& from, const stun::Message& m, const uint8_t* p, size_t n,
+                              bool via_relay) {
+  const stun::Attr* user = m.get(stun::kUsername);
+  if (!user || !stun::verify_integrity(p, n, m, pwd_)) {
+    auto resp = stun::Message{};
+    resp.type = stun::kBindingError;
+    memcpy(resp.tid, m.tid, 12);
+    resp.add_error(user ? 401 : 400, user ? "Unauthorized" : "Bad Request");
+    auto b = resp.serialize(nullptr, true);
+    int li = local_for_socket(si, via_relay);
+    send_raw(li >= 0 ? li : -1 - si, from, b.data(), b.size());
+    return;
+  }
+  size_t colon = user->value.find(':');
+  if (colon == std::string::npos || user->value.substr(0, colon) != ufrag_) return;
+  // Role conflict (RFC 8445 §7.3.1.1).
+  uint64_t their_tb;
+  bool conflict = false;
+  if (controlling_ && m.get_u64(stun::kIceControlling, their_tb)) {
+    if (tiebreaker_ >= their_tb) conflict = true;
+    else {
+      controlling_ = false;
+      LOG_DEBUG(kT, "ICE role conflict: switching to controlled");
+    }
+  } else if (!controlling_ && m.get_u64(stun::kIceControlled, their_tb)) {
+    if (tiebreaker_ >= their_tb) {
+      controlling_ = true;
+      LOG_DEBUG(kT, "ICE role conflict: switching to controlling");
+    } else {
+      conflict = true;
+    }
+  }
+  int li = local_for_socket(si, via_relay);
+  if (conflict) {
+    stun::Message resp;
+    resp.type = stun::kBindingError;
+    memcpy(resp.tid, m.tid, 12);
+    resp.add_error(487, "Role Conflict");
+    auto b = resp.serialize(&pwd_, true);
+    send_raw(li >= 0 ? li : -1 - si, from, b.data(), b.size());
+    return;
+  }
+  stun::Message resp;
+  resp.type = stun::kBindingSuccess;
+  memcpy(resp.tid, m.tid, 12);
+  resp.add_xor_addr(stun::kXorMappedAddress, from);
+  auto b = resp.serialize(&pwd_, true);
+  send_raw(li >= 0 ? li : -1 - si, from, b.data(), b.size());
+  if (li < 0) return;
+  // Peer-reflexive remote candidate.
+  int ri = find_remote(from);
+  if (ri < 0) {
+    Candidate c;
+    c.type = "prflx";
+    c.addr = from;
+    uint32_t prio = 0;
+    m.get_u32(stun::kPriority, prio);
+    c.priority = prio;
+    c.foundation = "prflx" + std::to_string(remotes_.size());
+    remotes_.push_back(c);
+    ri = int(remotes_.size()) - 1;
+    for (int l = 0; l < int(locals_.size()); l++) pair_up(l, ri);
+    if (state_ == IceState::New) {
+      checking_since_ = Reactor::now_ms();
+      set_state(IceState::Checking);
+    }
+  }
+  bool use_cand = m.get(stun::kUseCandidate) != nullptr;
+  for (int pi = 0; pi < int(pairs_.size()); pi++) {
+    Pair& pr = pairs_[pi];
+    if (pr.local != li || pr.remote != ri) continue;
+    if (use_cand && !controlling_) {
+      // Nominated by the controlling agent. Select right away (its check of
+      // this pair just succeeded end-to-end with our response).
+      if (sel_pair_ < 0) select_pair(pi);
+    }
+    if (pr.st == Pair::St::Waiting || pr.st == Pair::St::Failed) {
+      pr.st = Pair::St::Waiting;  // triggered check
+      pr.next_tx = 0;
+    }
+  }
+}
+
+void IceAgent::handle_response(const SockAddr& from, const stun::Message& m, const uint8_t* p, size_t n) {
+  std::string tid = m.tid_key();
+  for (size_t i = 0; i < srflx_.size(); i++) {
+    if (srflx_[i].tid != tid) continue;
+    SockAddr mapped;
+    if (m.cls() == 2 && (m.get_xor_addr(stun::kXorMappedAddress, mapped) || m.get_addr(stun::kMappedAddress, mapped))) {
+      int si = srflx_[i].sock;
+      bool dup = false;
+      for (auto& l : locals_)
+        if (l.c.addr == mapped) dup = true;
+      if (!dup) {
+        Candidate c;
+        c.type = "srflx";
+        c.addr = mapped;
+        c.related = socks_[si].addr;
+        c.has_related = true;
+        c.priority = candidate_priority("srflx", 65535 - uint32_t(si) * 256);
+        c.foundation = std::to_string(crc32_ieee(("srflx" + socks_[si].addr.ip()).data(), 5 + socks_[si].addr.ip().size()));
+        add_local(c, si, false);
+      }
+    }
+    srflx_.erase(srflx_.begin() + long(i));
+    return;
+  }
+  auto it = tx_pairs_.find(tid);
+  if (it == tx_pairs_.end()) return;
+  int pi = it->second;
+  tx_pairs_.erase(it);
+  if (pi >= int(pairs_.size())) return;
+  Pair& pr = pairs_[pi];
+  if (!remote_pwd_.empty() && !stun::verify_integrity(p, n, m, remote_pwd_)) return;
+  if (m.cls() == 3) {
+    if (m.error_code() == 487) {
+      controlling_ = !controlling_;
+      LOG_DEBUG(kT, "ICE 487 role conflict: now %s", controlling_ ? "controlling" : "controlled");
+      pr.st = Pair::St::Waiting;
+      pr.next_tx = 0;
+      pr.tries = 0;
+    } else {
+      pr.st = Pair::St::Failed;
+    }
+    return;
+  }
+  (void)from;
+  pr.st = Pair::St::Succeeded;
+  if (controlling_ && pr.use_cand) {
+    if (sel_pair_ < 0) select_pair(pi);
+  } else if (!controlling_ && pr.nominate_on_success && sel_pair_ < 0) {
+    select_pair(pi);
+  } else if (controlling_ && sel_pair_ < 0) {
+    // Regular nomination: follow up with USE-CANDIDATE on the first valid pair.
+    pr.use_cand = true;
+    pr.st = Pair::St::Waiting;
+    pr.next_tx = 0;
+    pr.tries = 0;
+  }
+}
+
+void IceAgent::select_pair(int pi) {
+  Pair& pr = pairs_[pi];
+  sel_pair_ = pi;
+  sel_local_ = pr.local;
+  sel_remote_ = remotes_[pr.remote].addr;
+  LOG_DEBUG(kT, "ICE selected pair %s", selected_desc().c_str());
+  last_rx_ = Reactor::now_ms();
+  set_state(IceState::Connected);
+}
+
+std::string IceAgent::selected_desc() const {
+  if (sel_local_ < 0) return "(none)";
+  const Local& l = locals_[sel_local_];
+  return l.c.type + ":" + (l.relay ? l.c.addr.str() : socks_[l.sock].addr.str()) + " <-> " + sel_remote_.str();
+}
+
+bool IceAgent::selected_same_host() const {
+  if (sel_local_ < 0 || locals_[sel_local_].relay) return false;
+  if (sel_remote_.is_loopback()) return true;
+  for (auto& s : socks_) {
+    SockAddr a = s.addr, b = sel_remote_;
+    a.set_port(0);
+    b.set_port(0);
+    if (a == b) return true;
+  }
+  return false;
+}
+
+void IceAgent::send_check(Pair& pr) {
+  const Candidate& rc = remotes_[pr.remote];
+  const Local& l = locals_[pr.local];
+  auto m = stun::Message::make(stun::kBindingRequest);
+  m.add(stun::kUsername, remote_ufrag_ + ":" + ufrag_);
+  m.add_u32(stun::kPriority, candidate_priority("prflx", (l.c.priority >> 8) & 0xFFFF));
+  if (controlling_) {
+    m.add_u64(stun::kIceControlling, tiebreaker_);
+    // Aggressive nomination: the first pair to succeed is used.
+    pr.use_cand = true;
+    m.add(stun::kUseCandidate, "");
+  } else {
+    m.add_u64(stun::kIceControlled, tiebreaker_);
+  }
+  auto b = m.serialize(&remote_pwd_, true);
+  if (!pr.tid.empty()) tx_pairs_.erase(pr.tid);
+  pr.tid = m.tid_key();
+  int pi = int(&pr - pairs_.data());
+  tx_pairs_[pr.tid] = pi;
+  send_raw(pr.local, rc.addr, b.data(), b.size());
+}
+
+void IceAgent::tick() {
+  if (closed_) return;
+  uint64_t now = Reactor::now_ms();
+  std::weak_ptr<IceAgent> w = shared_from_this();
+  if (!remote_pwd_.empty() && sel_pair_ < 0) {
+    // Retransmit in-progress checks; start the highest-priority waiting check (pacing Ta = 20 ms).
+    for (auto& pr : pairs_) {
+      if (pr.st != Pair::St::InProgress || now < pr.next_tx) continue;
+      if (pr.tries >= 7) {
+        pr.st = Pair::St::Failed;
+        continue;
+      }
+      send_check(pr);
+      pr.tries++;
+      pr.rto = std::min<uint64_t>(pr.rto * 2, 1600);
+      pr.next_tx = now + pr.rto;
+    }
+    Pair* best = nullptr;
+    for (auto& pr : pairs_)
+      if (pr.st == Pair::St::Waiting && (!best || pr.prio > best->prio)) best = &pr;
+    if (best) {
+      best->st = Pair::St::InProgress;
+      best->tries = 1;
+      best->rto = 100;
+      best->next_tx = now + best->rto;
+      send_check(*best);
+    }
+  }
+  if (state_ == IceState::Checking && sel_pair_ < 0 && sel_local_ < 0 && checking_since_ &&
+      now - checking_since_ > cfg_.failed_ms) {
+    LOG_WARN(kT, "ICE connectivity checks failed after %llu ms", static_cast<unsigned long long>(now - checking_since_));
+    set_state(IceState::Failed);
+    return;
+  }
+  if (sel_local_ >= 0) {
+    if (sel_pair_ < 0 && state_ != IceState::Connected && state_ != IceState::Disconnected) {
+      // Path learned from inbound data before our own nomination completed.
+      set_state(IceState::Connected);
+    }
+    // Consent freshness / keepalive on the selected pair (RFC 7675).
+    if (now - last_keepalive_ >= cfg_.keepalive_ms && !remote_pwd_.empty()) {
+      last_keepalive_ = now;
+      auto m = stun::Message::make(stun::kBindingRequest);
+      m.add(stun::kUsername, remote_ufrag_ + ":" + ufrag_);
+      m.add_u32(stun::kPriority, candidate_priority("prflx", 65535));
+      if (controlling_) m.add_u64(stun::kIceControlling, tiebreaker_);
+      else m.add_u64(stun::kIceControlled, tiebreaker_);
+      auto b = m.serialize(&remote_pwd_, true);
+      send_raw(sel_local_, sel_remote_, b.data(), b.size());
+    }
+    uint64_t idle = now - last_rx_;
+    if (idle > cfg_.failed_ms) {
+      LOG_WARN(kT, "ICE: no traffic from peer for %llu ms", static_cast<unsigned long long>(idle));
+      set_state(IceState::Failed);
+      return;
+    }
+    if (idle > cfg_.disconnected_ms && state_ == IceState::Connected) set_state(IceState::Disconnected);
+  }
+  if (closed_ || state_ == IceState::Failed) return;
+  uint64_t next = (sel_pair_ < 0 && !remote_pwd_.empty()) ? 20 : 250;
+  tick_timer_ = r_.call_later_ms(next, [w] {
+    if (auto s = w.lock()) {
+      s->tick_timer_ = 0;
+      s->tick();
+    }
+  });
+}
+
+}  // namespace p2pt::rtc

@@ -1,0 +1,189 @@
+// ICE agent (RFC 8445) over UDP: candidate gathering (host, server-reflexive
+// via STUN, relayed via TURN), connectivity checks with STUN short-term
+// credentials, nomination, consent/liveness, and the datagram path used by
+// DTLS once a pair is selected.
+//
+// Replaces webrtc-ice 0.11 as configured by the reference (tunnel/src/rtc.rs:31-72):
+// STUN server stun:stun.l.google.com:19302 plus an optional TURN server,
+// mDNS disabled (host IPs are advertised directly, rtc.rs:38-41).
+//
+// MI355X-host specifics: datagrams leave in one sendmmsg per reactor batch and
+// arrive through recvmmsg; 4 MiB socket buffers; loopback host candidates are
+// optional (offline / same-host peers).
+#pragma once
+
+#include <sys/socket.h>
+
+#include <deque>
+#include <functional>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "core/net.h"
+#include "core/reactor.h"
+#include "rtc/stun.h"
+
+namespace p2pt::rtc {
+
+struct Candidate {
+  std::string foundation;
+  int component = 1;
+  std::string transport = "udp";
+  uint32_t priority = 0;
+  SockAddr addr;
+  std::string type = "host";  // host | srflx | prflx | relay
+  SockAddr related;
+  bool has_related = false;
+
+  // "candidate:<foundation> 1 udp <prio> <ip> <port> typ <type> [raddr <ip> rport <port>]"
+  std::string to_sdp() const;
+  // Accepts with or without the "candidate:" / "a=candidate:" prefix. Only UDP.
+  static bool parse(const std::string& s, Candidate& out, std::string* err = nullptr);
+};
+
+uint32_t candidate_priority(const std::string& type, uint32_t local_pref, int component = 1);
+
+class TurnClient;
+
+struct IceConfig {
+  std::vector<std::string> stun_urls;  // "stun:host:port"
+  std::string turn_url;                // "turn:host:port[?transport=udp]"
+  std::string turn_user, turn_pass;
+  bool include_loopback = true;
+  bool include_ipv6 = false;
+  uint64_t stun_timeout_ms = 2000;
+  uint64_t disconnected_ms = 5000;
+  uint64_t failed_ms = 30000;
+  uint64_t keepalive_ms = 2500;
+  // Register a reactor flush hook that sends queued datagrams. Owners that
+  // must order their own flush before ICE's (PeerConnection) turn this off
+  // and call IceAgent::flush() themselves.
+  bool auto_flush = true;
+};
+
+enum class IceState { New, Checking, Connected, Disconnected, Failed, Closed };
+const char* ice_state_name(IceState s);
+
+class IceAgent : public std::enable_shared_from_this<IceAgent> {
+ public:
+  static std::shared_ptr<IceAgent> create(Reactor& r, IceConfig cfg, bool controlling);
+  ~IceAgent();
+
+  const std::string& local_ufrag() const { return ufrag_; }
+  const std::string& local_pwd() const { return pwd_; }
+  bool controlling() const { return controlling_; }
+
+  void gather();
+  bool gathering_done() const { return gathering_done_; }
+  const std::vector<Candidate>& local_candidates() const { return local_cands_; }
+  void set_remote_credentials(const std::string& ufrag, const std::string& pwd);
+  void add_remote_candidate(const Candidate& c);
+  void close();
+
+  // Datagram path (valid once a pair is usable). Queued and flushed with one
+  // sendmmsg per reactor iteration.
+  void send(const uint8_t* p, size_t n);
+  bool has_path() const { return sel_local_ >= 0; }
+  // True when both ends of the selected pair are on this host.
+  bool selected_same_host() const;
+  std::string selected_desc() const;
+  IceState state() const { return state_; }
+  // Send every queued datagram (sendmmsg, grouped by socket).
+  void flush();
+
+  std::function<void(const Candidate&)> on_candidate;
+  std::function<void()> on_gathering_done;
+  std::function<void(IceState)> on_state;
+  std::function<void(const uint8_t*, size_t)> on_data;  // non-STUN datagrams (DTLS)
+
+ private:
+  struct Sock {
+    int fd = -1;
+    SockAddr addr;  // bound address (with port)
+    bool loopback = false;
+  };
+  struct Local {
+    Candidate c;
+    int sock;       // index into socks_ (base socket)
+    bool relay = false;
+  };
+  struct Pair {
+    int local, remote;
+    uint64_t prio = 0;
+    enum class St { Waiting, InProgress, Succeeded, Failed } st = St::Waiting;
+    std::string tid;
+    int tries = 0;
+    uint64_t next_tx = 0;
+    uint64_t rto = 0;
+    bool use_cand = false;
+    bool nominate_on_success = false;
+  };
+
+  IceAgent(Reactor& r, IceConfig cfg, bool controlling);
+  void open_sockets();
+  void on_readable(int si);
+  void handle_datagram(int local_idx_hint, int si, const SockAddr& from, const uint8_t* p, size_t n, bool via_relay);
+  void handle_stun(int si, const SockAddr& from, const uint8_t* p, size_t n, bool via_relay);
+  void handle_request(int si, const SockAddr& from, const stun::Message& m, const uint8_t* p, size_t n, bool via_relay);
+  void handle_response(const SockAddr& from, const stun::Message& m, const uint8_t* p, size_t n);
+  void start_srflx();
+  void start_relay();
+  void maybe_gathering_done();
+  void add_local(Candidate c, int sock, bool relay);
+  void pair_up(int local, int remote);
+  uint64_t pair_priority(const Local& l, const Candidate& r) const;
+  void tick();
+  void send_check(Pair& p);
+  void send_raw(int local_idx, const SockAddr& to, const uint8_t* p, size_t n);
+  void select_pair(int pair_idx);
+  void set_state(IceState s);
+  int find_remote(const SockAddr& a) const;
+  int local_for_socket(int si, bool relay) const;
+
+  Reactor& r_;
+  IceConfig cfg_;
+  bool controlling_;
+  uint64_t tiebreaker_;
+  std::string ufrag_, pwd_;
+  std::string remote_ufrag_, remote_pwd_;
+  std::vector<Sock> socks_;
+  std::vector<Local> locals_;
+  std::vector<Candidate> local_cands_;
+  std::vector<Candidate> remotes_;
+  std::vector<Pair> pairs_;
+  std::map<std::string, int> tx_pairs_;  // STUN tid -> pair index
+  struct SrflxReq {
+    int sock;
+    SockAddr server;
+    std::string tid;
+    int tries = 0;
+  };
+  std::vector<SrflxReq> srflx_;
+  int pending_gather_ = 0;
+  bool gathering_done_ = false;
+  bool gather_started_ = false;
+  std::shared_ptr<TurnClient> turn_;
+  int sel_local_ = -1;
+  SockAddr sel_remote_;
+  int sel_pair_ = -1;
+  IceState state_ = IceState::New;
+  uint64_t tick_timer_ = 0;
+  uint64_t checking_since_ = 0;
+  uint64_t last_rx_ = 0;
+  uint64_t last_keepalive_ = 0;
+  uint64_t flush_hook_ = 0;
+  bool closed_ = false;
+  // Outgoing datagrams for the current batch.
+  struct Out {
+    int local;
+    SockAddr to;
+    std::vector<uint8_t> data;
+  };
+  std::vector<Out> outq_;
+  std::vector<uint8_t> rxbuf_;
+  friend class TurnClient;
+};
+
+}  // namespace p2pt::rtc

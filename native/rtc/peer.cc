@@ -1,0 +1,393 @@
+#include "rtc/peer.h"
+
+#include "core/json.h"
+#include "core/log.h"
+#include "tunnel/metrics.h"
+
+namespace p2pt::rtc {
+
+static const char* kT = "tunnel::rtc";
+
+// DCEP (RFC 8832) and WebRTC PPIDs (RFC 8831 §8).
+enum : uint32_t { kPpidDcep = 50, kPpidString = 51, kPpidBinary = 53, kPpidStringEmpty = 56, kPpidBinaryEmpty = 57 };
+enum : uint8_t { kDcepAck = 0x02, kDcepOpen = 0x03 };
+
+const char* pc_state_name(PcState s) {
+  switch (s) {
+    case PcState::New: return "New";
+    case PcState::Connecting: return "Connecting";
+    case PcState::Connected: return "Connected";
+    case PcState::Disconnected: return "Disconnected";
+    case PcState::Failed: return "Failed";
+    case PcState::Closed: return "Closed";
+  }
+  return "?";
+}
+
+// ---------------------------------------------------------------- DataChannel
+
+bool DataChannel::send(const uint8_t* hdr, size_t hlen, const Bytes& payload) {
+  auto pc = pc_.lock();
+  if (!pc || !is_open() || !pc->sctp_) return false;
+  std::vector<Bytes> pieces;
+  pieces.reserve(2);
+  pieces.push_back(Bytes::copy(hdr, hlen));
+  if (!payload.empty()) pieces.push_back(payload);
+  bool ok = pc->sctp_->send(uint16_t(stream_), kPpidBinary, pieces);
+  if (ok && buffered_amount() > buffered_low_threshold) above_low_ = true;
+  return ok;
+}
+
+size_t DataChannel::buffered_amount() const {
+  auto pc = pc_.lock();
+  return pc && pc->sctp_ ? pc->sctp_->buffered_amount() : 0;
+}
+
+void DataChannel::close() {
+  if (closed_) return;
+  auto pc = pc_.lock();
+  if (pc && pc->sctp_ && stream_ >= 0) pc->sctp_->request_stream_reset(uint16_t(stream_));
+  closed_ = true;
+  on_message = nullptr;
+  on_open = nullptr;
+  on_closed = nullptr;
+  on_buffered_low = nullptr;
+}
+
+std::string DataChannel::describe() const {
+  auto pc = pc_.lock();
+  return "webrtc:" + label_ + (pc ? " " + pc->describe_path() : "");
+}
+
+void DataChannel::set_open() {
+  if (open_ || closed_) return;
+  open_ = true;
+  LOG_INFO(kT, "data channel '%s' opened", label_.c_str());
+  if (on_open) {
+    auto cb = on_open;
+    cb();
+  }
+}
+
+void DataChannel::set_closed(const std::string& why) {
+  if (closed_) return;
+  closed_ = true;
+  open_ = false;
+  LOG_INFO(kT, "data channel '%s' closed", label_.c_str());
+  auto cb = std::move(on_closed);
+  on_closed = nullptr;
+  if (cb) cb(why);
+}
+
+// ---------------------------------------------------------------- PeerConnection
+
+std::shared_ptr<PeerConnection> PeerConnection::create(Reactor& r, PcConfig cfg, bool offerer) {
+  auto pc = std::shared_ptr<PeerConnection>(new PeerConnection(r, std::move(cfg), offerer));
+  std::weak_ptr<PeerConnection> w = pc;
+  pc->cfg_.ice.auto_flush = false;
+  pc->ice_ = IceAgent::create(r, pc->cfg_.ice, offerer);
+  pc->ice_->on_candidate = [w](const Candidate& c) {
+    auto s = w.lock();
+    if (s && s->on_ice_candidate) s->on_ice_candidate(candidate_json(c, s->ice_->local_ufrag()));
+  };
+  pc->ice_->on_gathering_done = [w] {
+    auto s = w.lock();
+    if (s && s->on_gathering_complete) s->on_gathering_complete();
+  };
+  pc->ice_->on_state = [w](IceState st) {
+    if (auto s = w.lock()) s->on_ice_state(st);
+  };
+  pc->ice_->on_data = [w](const uint8_t* p, size_t n) {
+    auto s = w.lock();
+    if (s && s->dtls_) s->dtls_->on_datagram(p, n);
+  };
+  // One flush per reactor batch, in dependency order: SCTP packets ->
+  // DTLS records -> ICE datagrams (sendmmsg).
+  pc->flush_hook_ = r.add_flush_hook([w] {
+    if (auto s = w.lock()) s->flush();
+  });
+  return pc;
+}
+
+PeerConnection::PeerConnection(Reactor& r, PcConfig cfg, bool offerer)
+    : r_(r), cfg_(std::move(cfg)), offerer_(offerer), mtu_(cfg_.sctp_mtu) {}
+
+PeerConnection::~PeerConnection() { close(); }
+
+void PeerConnection::flush() {
+  if (closed_) return;
+  if (sctp_) sctp_->flush();
+  if (ice_) ice_->flush();
+}
+
+void PeerConnection::close() {
+  if (closed_) return;
+  if (sctp_ && sctp_->established()) {
+    sctp_->abort("closed");
+    flush();
+  }
+  if (dtls_) {
+    dtls_->close();
+    if (ice_) ice_->flush();
+  }
+  closed_ = true;
+  if (flush_hook_) r_.remove_flush_hook(flush_hook_);
+  flush_hook_ = 0;
+  for (auto& kv : channels_) kv.second->set_closed("peer connection closed");
+  for (auto& dc : pending_) dc->set_closed("peer connection closed");
+  if (ice_) {
+    ice_->on_state = nullptr;
+    ice_->on_data = nullptr;
+    ice_->close();
+  }
+  state_ = PcState::Closed;
+}
+
+std::shared_ptr<DataChannel> PeerConnection::create_data_channel(const std::string& label) {
+  auto dc = std::make_shared<DataChannel>(weak_from_this(), label);
+  pending_.push_back(dc);
+  if (sctp_ && sctp_->established()) open_pending_channels();
+  return dc;
+}
+
+void PeerConnection::start_gathering() { ice_->gather(); }
+
+std::string PeerConnection::local_description() const {
+  SessionDesc d;
+  d.type = offerer_ ? "offer" : "answer";
+  d.ice_ufrag = ice_->local_ufrag();
+  d.ice_pwd = ice_->local_pwd();
+  d.fingerprint = DtlsTransport::local_fingerprint();
+  d.setup = offerer_ ? "actpass" : (dtls_client_ ? "active" : "passive");
+  d.mid = have_remote_ ? remote_.mid : "0";
+  d.candidates = ice_->local_candidates();
+  d.end_of_candidates = ice_->gathering_done();
+  if (cfg_.allow_jumbo) d.jumbo = cfg_.jumbo_mtu;
+  return d.to_string();
+}
+
+bool PeerConnection::set_remote_description(const std::string& sdp, std::string* err) {
+  SessionDesc d;
+  if (!SessionDesc::parse(sdp, d, err)) return false;
+  remote_ = d;
+  have_remote_ = true;
+  // DTLS role (RFC 8842 §5): the answerer picks "active" when offered actpass.
+  if (offerer_) dtls_client_ = d.setup == "passive";
+  else dtls_client_ = d.setup != "active";
+  ice_->set_remote_credentials(d.ice_ufrag, d.ice_pwd);
+  for (auto& c : d.candidates) ice_->add_remote_candidate(c);
+  if (state_ == PcState::New) set_state(PcState::Connecting);
+  return true;
+}
+
+std::string PeerConnection::candidate_json(const Candidate& c, const std::string& ufrag) {
+  Json j = Json::object();
+  j.set("candidate", Json(c.to_sdp()));
+  j.set("sdpMid", Json("0"));
+  j.set("sdpMLineIndex", Json(0));
+  j.set("usernameFragment", Json(ufrag));
+  return j.dump();
+}
+
+bool PeerConnection::add_ice_candidate(const std::string& cand, std::string* err) {
+  std::string line = cand;
+  Json j;
+  if (!cand.empty() && cand[0] == '{') {
+    if (!Json::parse(cand, j, err)) return false;
+    const Json* c = j.get("candidate");
+    if (!c || !c->is_string()) {
+      if (err) *err = "candidate JSON lacks a \"candidate\" string";
+      return false;
+    }
+    line = c->as_string();
+  }
+  if (line.empty()) return true;  // end-of-candidates marker
+  Candidate c;
+  if (!Candidate::parse(line, c, err)) return false;
+  ice_->add_remote_candidate(c);
+  return true;
+}
+
+void PeerConnection::set_state(PcState s) {
+  if (s == state_ || closed_) return;
+  state_ = s;
+  LOG_INFO(kT, "peer connection state: %s", pc_state_name(s));
+  if (on_state) {
+    auto cb = on_state;
+    cb(s);
+  }
+}
+
+void PeerConnection::fail(const std::string& why) {
+  if (state_ == PcState::Failed || closed_) return;
+  LOG_WARN(kT, "peer connection failed: %s", why.c_str());
+  set_state(PcState::Failed);
+  for (auto& kv : channels_) kv.second->set_closed(why);
+}
+
+void PeerConnection::on_ice_state(IceState s) {
+  switch (s) {
+    case IceState::Checking:
+      set_state(PcState::Connecting);
+      break;
+    case IceState::Connected:
+      if (!dtls_) start_dtls();
+      else if (state_ == PcState::Disconnected) set_state(PcState::Connected);
+      break;
+    case IceState::Disconnected:
+      if (state_ == PcState::Connected) set_state(PcState::Disconnected);
+      break;
+    case IceState::Failed:
+      fail("ICE connection failed");
+      break;
+    default:
+      break;
+  }
+}
+
+void PeerConnection::start_dtls() {
+  if (!have_remote_) return;
+  LOG_DEBUG(kT, "ICE connected via %s; starting DTLS as %s", ice_->selected_desc().c_str(),
+            dtls_client_ ? "client" : "server");
+  std::weak_ptr<PeerConnection> w = shared_from_this();
+  dtls_ = DtlsTransport::create(r_, dtls_client_, remote_.fingerprint, [w](const uint8_t* p, size_t n) {
+    auto s = w.lock();
+    if (s && s->ice_) s->ice_->send(p, n);
+  });
+  dtls_->on_connected = [w] {
+    if (auto s = w.lock()) s->start_sctp();
+  };
+  dtls_->on_data = [w](const uint8_t* p, size_t n) {
+    auto s = w.lock();
+    if (s && s->sctp_) s->sctp_->on_packet(p, n);
+  };
+  dtls_->on_closed = [w](const std::string& why) {
+    if (auto s = w.lock()) {
+      s->fail(why);
+    }
+  };
+  dtls_->start();
+}
+
+void PeerConnection::start_sctp() {
+  bool jumbo = cfg_.allow_jumbo && remote_.jumbo && ice_->selected_same_host();
+  mtu_ = jumbo ? std::min(cfg_.jumbo_mtu, remote_.jumbo) : cfg_.sctp_mtu;
+  if (jumbo) dtls_->set_record_limit(mtu_);
+  SctpConfig sc;
+  sc.mtu = mtu_;
+  sc.remote_port = remote_.sctp_port;
+  if (jumbo) sc.initial_cwnd = cfg_.jumbo_initial_cwnd;
+  std::weak_ptr<PeerConnection> w = shared_from_this();
+  sctp_ = SctpAssociation::create(r_, sc, [w](const uint8_t* p, size_t n) {
+    auto s = w.lock();
+    if (s && s->dtls_) s->dtls_->send(p, n);
+  });
+  sctp_->on_established = [w] {
+    auto s = w.lock();
+    if (!s) return;
+    LOG_DEBUG(kT, "SCTP established (packet size %zu)", s->mtu_);
+    s->open_pending_channels();
+  };
+  sctp_->on_message = [w](uint16_t st, uint32_t ppid, Bytes m) {
+    if (auto s = w.lock()) s->on_sctp_message(st, ppid, std::move(m));
+  };
+  sctp_->on_stream_reset = [w](uint16_t st) {
+    auto s = w.lock();
+    if (!s) return;
+    auto it = s->channels_.find(st);
+    if (it != s->channels_.end()) it->second->set_closed("data channel closed by peer");
+  };
+  sctp_->on_closed = [w](const std::string& why) {
+    auto s = w.lock();
+    if (!s) return;
+    for (auto& kv : s->channels_) kv.second->set_closed(why);
+    s->fail(why);
+  };
+  sctp_->on_sent = [w] {
+    auto s = w.lock();
+    if (!s) return;
+    for (auto& kv : s->channels_) {
+      auto& dc = kv.second;
+      if (dc->above_low_ && dc->buffered_amount() <= dc->buffered_low_threshold) {
+        dc->above_low_ = false;
+        if (dc->on_buffered_low) dc->on_buffered_low();
+      }
+    }
+  };
+  metrics::gauge_fn("tunnel_sctp_cwnd_bytes", [w] {
+    auto s = w.lock();
+    return s && s->sctp_ ? double(s->sctp_->cwnd()) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_sctp_srtt_us", [w] {
+    auto s = w.lock();
+    return s && s->sctp_ ? double(s->sctp_->srtt_us()) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_sctp_retransmits", [w] {
+    auto s = w.lock();
+    return s && s->sctp_ ? double(s->sctp_->stats().retransmits) : 0.0;
+  });
+  set_state(PcState::Connected);
+  sctp_->connect();
+}
+
+void PeerConnection::open_pending_channels() {
+  if (!sctp_ || !sctp_->established()) return;
+  // Stream ids: DTLS client uses even, server odd (RFC 8832 §6).
+  for (auto& dc : pending_) {
+    uint16_t sid = uint16_t(next_stream_ * 2 + (dtls_client_ ? 0 : 1));
+    next_stream_++;
+    dc->stream_ = sid;
+    channels_[sid] = dc;
+    std::vector<uint8_t> open;
+    open.push_back(kDcepOpen);
+    open.push_back(0x00);  // DATA_CHANNEL_RELIABLE (ordered)
+    open.push_back(0);
+    open.push_back(0);  // priority
+    open.insert(open.end(), 4, 0);  // reliability parameter
+    open.push_back(uint8_t(dc->label_.size() >> 8));
+    open.push_back(uint8_t(dc->label_.size()));
+    open.push_back(0);
+    open.push_back(0);  // protocol length
+    open.insert(open.end(), dc->label_.begin(), dc->label_.end());
+    sctp_->send(sid, kPpidDcep, {Bytes::take(std::move(open))});
+    LOG_DEBUG(kT, "sent DCEP OPEN for '%s' on stream %u", dc->label_.c_str(), sid);
+  }
+  pending_.clear();
+}
+
+void PeerConnection::on_sctp_message(uint16_t st, uint32_t ppid, Bytes msg) {
+  if (ppid == kPpidDcep) {
+    if (msg.empty()) return;
+    if (msg[0] == kDcepOpen && msg.size() >= 12) {
+      uint16_t llen = rd16(msg.data() + 8);
+      std::string label = msg.size() >= 12u + llen ? std::string(msg.view().substr(12, llen)) : "";
+      LOG_INFO(kT, "received data channel: %s", label.c_str());
+      auto dc = std::make_shared<DataChannel>(weak_from_this(), label);
+      dc->stream_ = st;
+      channels_[st] = dc;
+      sctp_->send(st, kPpidDcep, {Bytes::copy("\x02", 1)});
+      if (on_data_channel) on_data_channel(dc);
+      dc->set_open();
+    } else if (msg[0] == kDcepAck) {
+      auto it = channels_.find(st);
+      if (it != channels_.end()) it->second->set_open();
+    }
+    return;
+  }
+  auto it = channels_.find(st);
+  if (it == channels_.end()) return;
+  auto dc = it->second;
+  if (!dc->is_open()) {
+    // Data may follow an OPEN we have not ACKed to ourselves yet: an opener
+    // treats the first data from the peer as an implicit ACK (RFC 8832 §6).
+    dc->set_open();
+  }
+  if (ppid == kPpidBinaryEmpty || ppid == kPpidStringEmpty) msg = Bytes();
+  if (dc->on_message) dc->on_message(std::move(msg));
+}
+
+std::string PeerConnection::describe_path() const {
+  return ice_ ? ice_->selected_desc() + " mtu=" + std::to_string(mtu_) : "";
+}
+
+}  // namespace p2pt::rtc

@@ -1,0 +1,123 @@
+// PeerConnection: ICE + DTLS + SCTP + DCEP assembled into a data-only
+// WebRTC endpoint, and DataChannel (the MessageChannel the tunnel runs on).
+//
+// Replaces the webrtc-rs RTCPeerConnection/RTCDataChannel usage of the
+// reference (tunnel/src/rtc.rs:31-122): one reliable, ordered data channel
+// labelled "tunnel" created by the offerer (rtc.rs:133) and received by the
+// answerer via on_data_channel (rtc.rs:296-322); trickled ICE candidates as
+// JSON strings (rtc.rs:141-159); state changes Connected/Failed
+// (rtc.rs:166-174, :349-355).
+//
+// Bring-up order: ICE pair selected -> DTLS handshake (role from a=setup) ->
+// SCTP association (both sides INIT) -> DCEP OPEN/ACK (RFC 8832) -> open.
+// Datagrams produced in a reactor batch are flushed together: SCTP bundles,
+// DTLS encrypts one record per packet, ICE sends them with one sendmmsg.
+#pragma once
+
+#include <functional>
+#include <map>
+#include <memory>
+#include <string>
+
+#include "rtc/dtls.h"
+#include "rtc/ice.h"
+#include "rtc/sctp.h"
+#include "rtc/sdp.h"
+#include "tunnel/channel.h"
+
+namespace p2pt::rtc {
+
+enum class PcState { New, Connecting, Connected, Disconnected, Failed, Closed };
+const char* pc_state_name(PcState s);
+
+struct PcConfig {
+  IceConfig ice;
+  size_t sctp_mtu = 1200;
+  bool allow_jumbo = true;   // advertise/use large SCTP packets on same-host paths
+  size_t jumbo_mtu = 16000;
+  size_t jumbo_initial_cwnd = 1 << 20;
+};
+
+class PeerConnection;
+
+class DataChannel : public MessageChannel, public std::enable_shared_from_this<DataChannel> {
+ public:
+  DataChannel(std::weak_ptr<PeerConnection> pc, std::string label) : pc_(std::move(pc)), label_(std::move(label)) {}
+  bool send(const uint8_t* hdr, size_t hlen, const Bytes& payload) override;
+  size_t buffered_amount() const override;
+  bool is_open() const override { return open_ && !closed_; }
+  void close() override;
+  std::string describe() const override;
+  const std::string& label() const { return label_; }
+  int stream() const { return stream_; }
+
+ private:
+  friend class PeerConnection;
+  void set_open();
+  void set_closed(const std::string& why);
+  std::weak_ptr<PeerConnection> pc_;
+  std::string label_;
+  int stream_ = -1;
+  bool open_ = false;
+  bool closed_ = false;
+  bool above_low_ = false;
+};
+
+class PeerConnection : public std::enable_shared_from_this<PeerConnection> {
+ public:
+  static std::shared_ptr<PeerConnection> create(Reactor& r, PcConfig cfg, bool offerer);
+  ~PeerConnection();
+
+  std::shared_ptr<DataChannel> create_data_channel(const std::string& label);
+  void start_gathering();
+  bool gathering_complete() const { return ice_ && ice_->gathering_done(); }
+  // Current local SDP (type offer for the offerer, answer for the answerer)
+  // with every candidate gathered so far.
+  std::string local_description() const;
+  bool set_remote_description(const std::string& sdp, std::string* err);
+  // Candidate from signalling: a JSON RTCIceCandidateInit string (webrtc-rs
+  // form) or a bare "candidate:..." line.
+  bool add_ice_candidate(const std::string& cand, std::string* err);
+  static std::string candidate_json(const Candidate& c, const std::string& ufrag);
+  void close();
+  PcState state() const { return state_; }
+  std::string describe_path() const;
+  const SctpStats* sctp_stats() const { return sctp_ ? &sctp_->stats() : nullptr; }
+  size_t sctp_mtu() const { return mtu_; }
+
+  std::function<void(const std::string& candidate_json)> on_ice_candidate;
+  std::function<void()> on_gathering_complete;
+  std::function<void(PcState)> on_state;
+  std::function<void(std::shared_ptr<DataChannel>)> on_data_channel;
+
+ private:
+  friend class DataChannel;
+  PeerConnection(Reactor& r, PcConfig cfg, bool offerer);
+  void on_ice_state(IceState s);
+  void start_dtls();
+  void start_sctp();
+  void on_sctp_message(uint16_t stream, uint32_t ppid, Bytes msg);
+  void open_pending_channels();
+  void set_state(PcState s);
+  void fail(const std::string& why);
+  void flush();
+
+  Reactor& r_;
+  PcConfig cfg_;
+  bool offerer_;
+  std::shared_ptr<IceAgent> ice_;
+  std::shared_ptr<DtlsTransport> dtls_;
+  std::shared_ptr<SctpAssociation> sctp_;
+  SessionDesc remote_;
+  bool have_remote_ = false;
+  bool dtls_client_ = false;
+  PcState state_ = PcState::New;
+  std::vector<std::shared_ptr<DataChannel>> pending_;
+  std::map<uint16_t, std::shared_ptr<DataChannel>> channels_;
+  uint16_t next_stream_ = 0;
+  uint64_t flush_hook_ = 0;
+  size_t mtu_ = 1200;
+  bool closed_ = false;
+};
+
+}  // namespace p2pt::rtc

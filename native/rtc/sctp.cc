@@ -1,0 +1,858 @@
+#include "rtc/sctp.h"
+
+#include <openssl/hmac.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "core/crypto.h"
+#include "core/log.h"
+
+namespace p2pt::rtc {
+
+static const char* kT = "tunnel::sctp";
+
+namespace {
+enum : uint8_t {
+  kData = 0,
+  kInit = 1,
+  kInitAck = 2,
+  kSack = 3,
+  kHeartbeat = 4,
+  kHeartbeatAck = 5,
+  kAbort = 6,
+  kShutdown = 7,
+  kShutdownAck = 8,
+  kError = 9,
+  kCookieEcho = 10,
+  kCookieAck = 11,
+  kShutdownComplete = 14,
+  kReconfig = 130,
+  kForwardTsn = 192,
+};
+constexpr size_t kCommonHdr = 12;
+constexpr size_t kDataHdr = 16;
+
+inline bool tsn_lt(uint32_t a, uint32_t b) { return int32_t(a - b) < 0; }
+inline bool tsn_le(uint32_t a, uint32_t b) { return int32_t(a - b) <= 0; }
+
+void put16(std::vector<uint8_t>& v, uint16_t x) {
+  v.push_back(uint8_t(x >> 8));
+  v.push_back(uint8_t(x));
+}
+void put32(std::vector<uint8_t>& v, uint32_t x) {
+  v.push_back(uint8_t(x >> 24));
+  v.push_back(uint8_t(x >> 16));
+  v.push_back(uint8_t(x >> 8));
+  v.push_back(uint8_t(x));
+}
+void pad4(std::vector<uint8_t>& v) {
+  while (v.size() % 4) v.push_back(0);
+}
+}  // namespace
+
+struct SctpAssociation::Chunk {
+  uint32_t tsn;
+  uint16_t stream, ssn;
+  uint32_t ppid;
+  uint8_t flags;  // B=2, E=1, U=4
+  std::vector<Bytes> data;
+  size_t len;
+  uint64_t sent_us = 0;
+  int tx = 0;
+  int miss = 0;
+  bool acked = false;       // gap-acked
+  bool in_flight = false;   // counted in flight_size_
+  bool retransmit = false;  // marked for retransmission
+  bool fast = false;        // marked by fast retransmit (may bypass cwnd once)
+};
+
+struct SctpAssociation::InChunk {
+  uint32_t tsn;
+  uint8_t flags;
+  uint16_t stream;
+  uint32_t ppid;
+  std::vector<uint8_t> data;
+};
+
+std::shared_ptr<SctpAssociation> SctpAssociation::create(Reactor& r, SctpConfig cfg, PacketOut out) {
+  return std::shared_ptr<SctpAssociation>(new SctpAssociation(r, cfg, std::move(out)));
+}
+
+SctpAssociation::SctpAssociation(Reactor& r, SctpConfig cfg, PacketOut out) : r_(r), cfg_(cfg), out_(std::move(out)) {
+  do {
+    my_vtag_ = random_u32();
+  } while (my_vtag_ == 0);
+  my_init_tsn_ = random_u32();
+  next_tsn_ = my_init_tsn_;
+  cum_acked_ = my_init_tsn_ - 1;
+  random_bytes(cookie_key_, sizeof cookie_key_);
+  reconfig_seq_ = random_u32();
+  rto_us_ = cfg_.rto_initial_ms * 1000;
+  cwnd_ = cfg_.initial_cwnd ? cfg_.initial_cwnd : std::min<size_t>(4 * cfg_.mtu, std::max<size_t>(2 * cfg_.mtu, 4380));
+  ssthresh_ = SIZE_MAX / 2;
+  peer_rwnd_ = 0;
+  pkt_.reserve(65536);
+}
+
+SctpAssociation::~SctpAssociation() {
+  if (t3_timer_) r_.cancel(t3_timer_);
+  if (init_timer_) r_.cancel(init_timer_);
+  for (auto* c : inflight_) delete c;
+  for (auto& kv : ooo_) delete kv.second;
+}
+
+void SctpAssociation::set_mtu(size_t mtu) {
+  cfg_.mtu = mtu;
+  if (ssthresh_ < 4 * mtu) ssthresh_ = 4 * mtu;
+}
+
+// ------------------------------------------------------------------ output
+
+void SctpAssociation::emit_packet(std::vector<uint8_t>& pkt) {
+  // CRC32c over the packet with the checksum field zeroed, stored little-endian
+  // (RFC 9260 App. B; same byte order as usrsctp / webrtc-rs).
+  pkt[8] = pkt[9] = pkt[10] = pkt[11] = 0;
+  uint32_t crc = crc32c(pkt.data(), pkt.size());
+  pkt[8] = uint8_t(crc);
+  pkt[9] = uint8_t(crc >> 8);
+  pkt[10] = uint8_t(crc >> 16);
+  pkt[11] = uint8_t(crc >> 24);
+  stats_.packets_sent++;
+  if (out_) out_(pkt.data(), pkt.size());
+}
+
+static void begin_packet(std::vector<uint8_t>& pkt, uint16_t sport, uint16_t dport, uint32_t vtag) {
+  pkt.clear();
+  put16(pkt, sport);
+  put16(pkt, dport);
+  put32(pkt, vtag);
+  put32(pkt, 0);
+}
+
+void SctpAssociation::send_control(uint8_t type, uint8_t flags, const std::vector<uint8_t>& body, uint32_t vtag) {
+  std::vector<uint8_t> pkt;
+  begin_packet(pkt, cfg_.local_port, cfg_.remote_port, vtag);
+  pkt.push_back(type);
+  pkt.push_back(flags);
+  put16(pkt, uint16_t(4 + body.size()));
+  pkt.insert(pkt.end(), body.begin(), body.end());
+  pad4(pkt);
+  emit_packet(pkt);
+}
+
+void SctpAssociation::queue_control(uint8_t type, uint8_t flags, std::vector<uint8_t> body) {
+  std::vector<uint8_t> ch;
+  ch.push_back(type);
+  ch.push_back(flags);
+  put16(ch, uint16_t(4 + body.size()));
+  ch.insert(ch.end(), body.begin(), body.end());
+  pad4(ch);
+  ctrl_.push_back(std::move(ch));
+}
+
+void SctpAssociation::append_init_params(std::vector<uint8_t>& v) {
+  // Supported Extensions: FORWARD-TSN (0xC0), RE-CONFIG (0x82).
+  put16(v, 0x8008);
+  put16(v, 6);
+  v.push_back(0xC0);
+  v.push_back(0x82);
+  pad4(v);
+  // Forward-TSN-Supported.
+  put16(v, 0xC000);
+  put16(v, 4);
+}
+
+void SctpAssociation::send_init() {
+  std::vector<uint8_t> b;
+  put32(b, my_vtag_);
+  put32(b, cfg_.rwnd);
+  put16(b, 65535);  // outbound streams
+  put16(b, 65535);  // max inbound streams
+  put32(b, my_init_tsn_);
+  append_init_params(b);
+  send_control(kInit, 0, b, 0);
+}
+
+void SctpAssociation::connect() {
+  if (state_ != State::Closed) return;
+  state_ = State::CookieWait;
+  init_tries_ = 0;
+  std::weak_ptr<SctpAssociation> w = shared_from_this();
+  auto retry = std::make_shared<std::function<void()>>();
+  *retry = [w, retry] {
+    auto s = w.lock();
+    if (!s) return;
+    s->init_timer_ = 0;
+    if (s->state_ != State::CookieWait && s->state_ != State::CookieEchoed) return;
+    if (++s->init_tries_ > s->cfg_.max_init_retrans) {
+      s->closed("SCTP association setup timed out");
+      return;
+    }
+    if (s->state_ == State::CookieWait) s->send_init();
+    else s->send_control(kCookieEcho, 0, s->cookie_echo_, s->peer_vtag_);
+    uint64_t t = std::min<uint64_t>(s->cfg_.rto_initial_ms << std::min(s->init_tries_, 4), 5000);
+    s->init_timer_ = s->r_.call_later_ms(std::min<uint64_t>(t, 5000), *retry);
+  };
+  send_init();
+  init_timer_ = r_.call_later_ms(cfg_.rto_initial_ms, *retry);
+}
+
+std::string SctpAssociation::make_cookie(uint32_t peer_tag, uint32_t peer_tsn, uint32_t peer_rwnd, uint16_t peer_os,
+                                         uint16_t peer_mis) {
+  std::vector<uint8_t> c;
+  put32(c, peer_tag);
+  put32(c, peer_tsn);
+  put32(c, peer_rwnd);
+  put16(c, peer_os);
+  put16(c, peer_mis);
+  put32(c, my_vtag_);
+  uint64_t now = Reactor::now_ms();
+  put32(c, uint32_t(now >> 32));
+  put32(c, uint32_t(now));
+  unsigned int len = 0;
+  uint8_t mac[32];
+  HMAC(EVP_sha256(), cookie_key_, sizeof cookie_key_, c.data(), c.size(), mac, &len);
+  c.insert(c.end(), mac, mac + 32);
+  return std::string(c.begin(), c.end());
+}
+
+// ------------------------------------------------------------------ input
+
+void SctpAssociation::on_packet(const uint8_t* p, size_t n) {
+  if (n < kCommonHdr + 4) return;
+  uint32_t got = uint32_t(p[8]) | uint32_t(p[9]) << 8 | uint32_t(p[10]) << 16 | uint32_t(p[11]) << 24;
+  uint8_t hdr[kCommonHdr];
+  memcpy(hdr, p, kCommonHdr);
+  hdr[8] = hdr[9] = hdr[10] = hdr[11] = 0;
+  // crc32c() chains: the header (checksum zeroed) then the chunks.
+  uint32_t crc = crc32c(p + kCommonHdr, n - kCommonHdr, crc32c(hdr, kCommonHdr));
+  if (crc != got) {
+    LOG_TRACE(kT, "dropping SCTP packet with bad checksum");
+    return;
+  }
+  uint32_t vtag = rd32(p + 4);
+  stats_.packets_received++;
+  auto self = shared_from_this();
+  size_t off = kCommonHdr;
+  bool first = true;
+  while (off + 4 <= n && !closed_fired_) {
+    uint8_t type = p[off], flags = p[off + 1];
+    size_t clen = rd16(p + off + 2);
+    if (clen < 4 || off + clen > n) break;
+    const uint8_t* body = p + off + 4;
+    size_t blen = clen - 4;
+    // Verification tag rules (RFC 9260 §8.5).
+    bool ok_tag;
+    if (type == kInit) ok_tag = first && vtag == 0;
+    else if ((type == kAbort || type == kShutdownComplete) && (flags & 1)) ok_tag = vtag == peer_vtag_;
+    else ok_tag = vtag == my_vtag_;
+    if (!ok_tag) {
+      LOG_TRACE(kT, "dropping chunk %u with bad verification tag", type);
+      return;
+    }
+    switch (type) {
+      case kData: handle_data(flags, body, blen); break;
+      case kInit: handle_init(body, blen, vtag); break;
+      case kInitAck: handle_init_ack(body, blen); break;
+      case kSack: handle_sack(body, blen); break;
+      case kHeartbeat: handle_heartbeat(body, blen); break;
+      case kHeartbeatAck: break;
+      case kAbort: closed("SCTP association aborted by peer"); return;
+      case kShutdown: handle_shutdown(body, blen); break;
+      case kShutdownAck:
+        send_control(kShutdownComplete, 0, {}, peer_vtag_);
+        closed("SCTP association shut down");
+        return;
+      case kShutdownComplete: closed("SCTP association shut down"); return;
+      case kError: LOG_DEBUG(kT, "SCTP ERROR chunk from peer"); break;
+      case kCookieEcho: handle_cookie_echo(body, blen); break;
+      case kCookieAck:
+        if (state_ == State::CookieEchoed) enter_established();
+        break;
+      case kForwardTsn: handle_forward_tsn(body, blen); break;
+      case kReconfig: handle_reconfig(body, blen); break;
+      default:
+        // Unknown chunk: upper two bits say what to do (RFC 9260 §3.2).
+        if ((type & 0xC0) == 0x00 || (type & 0xC0) == 0x40) return;  // stop processing packet
+        break;
+    }
+    first = false;
+    off += (clen + 3) & ~size_t(3);
+  }
+}
+
+void SctpAssociation::handle_init(const uint8_t* c, size_t len, uint32_t) {
+  if (len < 16) return;
+  uint32_t tag = rd32(c), rwnd = rd32(c + 4);
+  uint16_t os = rd16(c + 8), mis = rd16(c + 10);
+  uint32_t tsn = rd32(c + 12);
+  if (tag == 0) return;
+  std::string cookie = make_cookie(tag, tsn, rwnd, os, mis);
+  std::vector<uint8_t> b;
+  put32(b, my_vtag_);
+  put32(b, cfg_.rwnd);
+  put16(b, 65535);
+  put16(b, 65535);
+  put32(b, my_init_tsn_);
+  append_init_params(b);
+  put16(b, 0x0007);  // State Cookie
+  put16(b, uint16_t(4 + cookie.size()));
+  b.insert(b.end(), cookie.begin(), cookie.end());
+  pad4(b);
+  send_control(kInitAck, 0, b, tag);
+}
+
+void SctpAssociation::handle_init_ack(const uint8_t* c, size_t len) {
+  if (state_ != State::CookieWait || len < 16) return;
+  peer_vtag_ = rd32(c);
+  uint32_t rwnd = rd32(c + 4);
+  uint32_t tsn = rd32(c + 12);
+  const uint8_t* cookie = nullptr;
+  size_t cookie_len = 0;
+  size_t off = 16;
+  while (off + 4 <= len) {
+    uint16_t pt = rd16(c + off), pl = rd16(c + off + 2);
+    if (pl < 4 || off + pl > len) break;
+    if (pt == 0x0007) {
+      cookie = c + off + 4;
+      cookie_len = pl - 4u;
+    }
+    off += (pl + 3u) & ~3u;
+  }
+  if (!cookie) return;
+  if (!have_peer_tsn_) {
+    peer_cum_tsn_ = tsn - 1;
+    have_peer_tsn_ = true;
+  }
+  peer_rwnd_ = rwnd;
+  cookie_echo_.assign(cookie, cookie + cookie_len);
+  state_ = State::CookieEchoed;
+  send_control(kCookieEcho, 0, cookie_echo_, peer_vtag_);
+}
+
+void SctpAssociation::handle_cookie_echo(const uint8_t* c, size_t len) {
+  if (len != 28 + 32) return;
+  unsigned int mlen = 0;
+  uint8_t mac[32];
+  HMAC(EVP_sha256(), cookie_key_, sizeof cookie_key_, c, 28, mac, &mlen);
+  if (memcmp(mac, c + 28, 32) != 0) {
+    LOG_DEBUG(kT, "invalid SCTP cookie");
+    return;
+  }
+  uint32_t peer_tag = rd32(c), peer_tsn = rd32(c + 4), peer_rwnd = rd32(c + 8);
+  uint32_t my_tag = rd32(c + 16);
+  if (my_tag != my_vtag_) return;
+  if (state_ == State::Established || state_ == State::ShutdownPending) {
+    if (peer_tag == peer_vtag_) queue_control(kCookieAck, 0, {});
+    return;
+  }
+  peer_vtag_ = peer_tag;
+  if (!have_peer_tsn_) {
+    peer_cum_tsn_ = peer_tsn - 1;
+    have_peer_tsn_ = true;
+  }
+  if (peer_rwnd_ == 0) peer_rwnd_ = peer_rwnd;
+  queue_control(kCookieAck, 0, {});
+  enter_established();
+}
+
+void SctpAssociation::enter_established() {
+  if (state_ == State::Established) return;
+  state_ = State::Established;
+  if (init_timer_) r_.cancel(init_timer_);
+  init_timer_ = 0;
+  LOG_DEBUG(kT, "SCTP association established (mtu %zu, cwnd %zu)", cfg_.mtu, cwnd_);
+  if (on_established) on_established();
+}
+
+void SctpAssociation::closed(const std::string& why) {
+  if (closed_fired_) return;
+  closed_fired_ = true;
+  state_ = State::Closed;
+  stop_t3();
+  if (init_timer_) r_.cancel(init_timer_);
+  init_timer_ = 0;
+  auto cb = std::move(on_closed);
+  on_closed = nullptr;
+  if (cb) cb(why);
+}
+
+void SctpAssociation::handle_heartbeat(const uint8_t* c, size_t len) {
+  queue_control(kHeartbeatAck, 0, std::vector<uint8_t>(c, c + len));
+}
+
+void SctpAssociation::handle_shutdown(const uint8_t*, size_t) {
+  state_ = State::ShutdownReceived;
+  maybe_finish_shutdown();
+}
+
+void SctpAssociation::maybe_finish_shutdown() {
+  if (!sendq_.empty() || !inflight_.empty()) return;
+  if (state_ == State::ShutdownReceived) {
+    state_ = State::ShutdownAckSent;
+    send_control(kShutdownAck, 0, {}, peer_vtag_);
+  } else if (state_ == State::ShutdownPending) {
+    state_ = State::ShutdownSent;
+    std::vector<uint8_t> b;
+    put32(b, peer_cum_tsn_);
+    send_control(kShutdown, 0, b, peer_vtag_);
+  }
+}
+
+void SctpAssociation::shutdown() {
+  if (state_ != State::Established) {
+    closed("SCTP association closed");
+    return;
+  }
+  state_ = State::ShutdownPending;
+  maybe_finish_shutdown();
+}
+
+void SctpAssociation::abort(const std::string& reason) {
+  if (peer_vtag_ && !closed_fired_) send_control(kAbort, 0, {}, peer_vtag_);
+  closed(reason);
+}
+
+void SctpAssociation::handle_data(uint8_t flags, const uint8_t* c, size_t len) {
+  if (len < 12 || !have_peer_tsn_) return;
+  uint32_t tsn = rd32(c);
+  uint16_t stream = rd16(c + 4);
+  uint32_t ppid = rd32(c + 8);
+  const uint8_t* data = c + 12;
+  size_t dlen = len - 12;
+  stats_.data_chunks_received++;
+  stats_.bytes_received += dlen;
+  sack_needed_ = true;
+  int32_t d = int32_t(tsn - peer_cum_tsn_);
+  if (d <= 0) {
+    if (dups_.size() < 32) dups_.push_back(tsn);
+    return;
+  }
+  auto deliver_chunk = [this](uint8_t fl, uint16_t st, uint32_t pp, const uint8_t* dp, size_t dn) {
+    bool B = fl & 2, E = fl & 1, U = fl & 4;
+    if (B && E) {
+      if (on_message) on_message(st, pp, Bytes::copy(dp, dn));
+      return;
+    }
+    Partial& pa = U ? partial_u_[st] : partial_[st];
+    if (B) {
+      pa.data.clear();
+      pa.ppid = pp;
+      pa.active = true;
+    }
+    if (!pa.active) return;  // middle fragment without a beginning (after FORWARD-TSN)
+    pa.data.insert(pa.data.end(), dp, dp + dn);
+    if (E) {
+      pa.active = false;
+      std::vector<uint8_t> msg;
+      msg.swap(pa.data);
+      if (on_message) on_message(st, pa.ppid, Bytes::take(std::move(msg)));
+    }
+  };
+  if (d == 1) {
+    peer_cum_tsn_ = tsn;
+    deliver_chunk(flags, stream, ppid, data, dlen);
+    // Drain now-contiguous out-of-order chunks.
+    while (!ooo_.empty()) {
+      auto it = ooo_.find(peer_cum_tsn_ + 1);
+      if (it == ooo_.end()) break;
+      InChunk* ic = it->second;
+      ooo_.erase(it);
+      ooo_bytes_ -= ic->data.size();
+      peer_cum_tsn_ = ic->tsn;
+      deliver_chunk(ic->flags, ic->stream, ic->ppid, ic->data.data(), ic->data.size());
+      delete ic;
+    }
+    return;
+  }
+  if (ooo_.count(tsn)) {
+    if (dups_.size() < 32) dups_.push_back(tsn);
+    return;
+  }
+  if (ooo_bytes_ + dlen > cfg_.rwnd) return;  // window exceeded: drop, peer retransmits
+  auto* ic = new InChunk{tsn, flags, stream, ppid, std::vector<uint8_t>(data, data + dlen)};
+  ooo_[tsn] = ic;
+  ooo_bytes_ += dlen;
+}
+
+void SctpAssociation::build_sack(std::vector<uint8_t>& b) {
+  size_t held = ooo_bytes_;
+  for (auto& kv : partial_) held += kv.second.data.size();
+  uint32_t a_rwnd = held >= cfg_.rwnd ? 0 : uint32_t(cfg_.rwnd - held);
+  // Gap blocks relative to the cumulative TSN (ooo_ keys sorted numerically;
+  // sort by serial distance to survive TSN wrap).
+  std::vector<uint32_t> offs;
+  offs.reserve(ooo_.size());
+  for (auto& kv : ooo_) offs.push_back(kv.first - peer_cum_tsn_);
+  std::sort(offs.begin(), offs.end());
+  std::vector<std::pair<uint16_t, uint16_t>> gaps;
+  for (uint32_t o : offs) {
+    if (o > 0xFFFF) break;
+    if (!gaps.empty() && gaps.back().second + 1 == o) gaps.back().second = uint16_t(o);
+    else gaps.emplace_back(uint16_t(o), uint16_t(o));
+    if (gaps.size() > 64) break;
+  }
+  put32(b, peer_cum_tsn_);
+  put32(b, a_rwnd);
+  put16(b, uint16_t(gaps.size()));
+  put16(b, uint16_t(dups_.size()));
+  for (auto& g : gaps) {
+    put16(b, g.first);
+    put16(b, g.second);
+  }
+  for (uint32_t d : dups_) put32(b, d);
+  dups_.clear();
+}
+
+void SctpAssociation::update_rto(uint64_t r) {
+  if (srtt_us_ == 0) {
+    srtt_us_ = r;
+    rttvar_us_ = r / 2;
+  } else {
+    uint64_t diff = srtt_us_ > r ? srtt_us_ - r : r - srtt_us_;
+    rttvar_us_ = (3 * rttvar_us_ + diff) / 4;
+    srtt_us_ = (7 * srtt_us_ + r) / 8;
+  }
+  uint64_t rto = srtt_us_ + std::max<uint64_t>(4 * rttvar_us_, 1000);
+  rto_us_ = std::clamp<uint64_t>(rto, cfg_.rto_min_ms * 1000, cfg_.rto_max_ms * 1000);
+}
+
+void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
+  if (len < 12) return;
+  uint32_t cum = rd32(c);
+  uint32_t a_rwnd = rd32(c + 4);
+  uint16_t ngap = rd16(c + 8), ndup = rd16(c + 10);
+  if (len < 12 + 4u * ngap + 4u * ndup) return;
+  stats_.sacks_received++;
+  if (tsn_lt(cum, cum_acked_)) return;  // stale SACK
+  uint64_t now = Reactor::now_us();
+  size_t newly_acked = 0;
+  size_t flight_before = flight_size_;
+  bool cum_advanced = tsn_lt(cum_acked_, cum);
+  uint64_t rtt_sample = 0;
+  while (!inflight_.empty() && tsn_le(inflight_.front()->tsn, cum)) {
+    Chunk* ch = inflight_.front();
+    inflight_.pop_front();
+    if (ch->in_flight) flight_size_ -= ch->len;
+    if (!ch->acked) {
+      newly_acked += ch->len;
+      if (ch->tx == 1) rtt_sample = now - ch->sent_us;
+    }
+    delete ch;
+  }
+  cum_acked_ = cum;
+  uint32_t highest_gap = cum;
+  for (uint16_t i = 0; i < ngap; i++) {
+    uint32_t s = cum + rd16(c + 12 + 4 * i), e = cum + rd16(c + 14 + 4 * i);
+    for (Chunk* ch : inflight_) {
+      if (tsn_lt(ch->tsn, s)) continue;
+      if (tsn_lt(e, ch->tsn)) break;
+      if (!ch->acked) {
+        ch->acked = true;
+        ch->retransmit = false;
+        if (ch->in_flight) {
+          flight_size_ -= ch->len;
+          ch->in_flight = false;
+        }
+        newly_acked += ch->len;
+        if (ch->tx == 1 && rtt_sample == 0) rtt_sample = now - ch->sent_us;
+      }
+      if (tsn_lt(highest_gap, ch->tsn)) highest_gap = ch->tsn;
+    }
+  }
+  if (rtt_sample) update_rto(rtt_sample);
+  // Miss indications -> fast retransmit (RFC 9260 §7.2.4).
+  bool new_fast = false;
+  if (highest_gap != cum) {
+    for (Chunk* ch : inflight_) {
+      if (!tsn_lt(ch->tsn, highest_gap)) break;
+      if (ch->acked || ch->retransmit) continue;
+      if (++ch->miss == 3) {
+        ch->miss = 0;
+        ch->retransmit = true;
+        ch->fast = true;
+        if (ch->in_flight) {
+          flight_size_ -= ch->len;
+          ch->in_flight = false;
+        }
+        new_fast = true;
+        stats_.fast_retransmits++;
+      }
+    }
+  }
+  if (cum_advanced) assoc_errors_ = 0;
+  // Congestion control (RFC 9260 §7.2.1-7.2.2).
+  if (newly_acked && cum_advanced && !fast_recovery_) {
+    if (cwnd_ <= ssthresh_) {
+      if (flight_before + cfg_.mtu >= cwnd_) cwnd_ += std::min(newly_acked, cfg_.mtu);
+    } else {
+      partial_acked_ += newly_acked;
+      if (partial_acked_ >= cwnd_ && flight_before + cfg_.mtu >= cwnd_) {
+        partial_acked_ -= cwnd_;
+        cwnd_ += cfg_.mtu;
+      }
+    }
+  }
+  if (new_fast && !fast_recovery_) {
+    ssthresh_ = std::max(cwnd_ / 2, 4 * cfg_.mtu);
+    cwnd_ = ssthresh_;
+    partial_acked_ = 0;
+    fast_recovery_ = true;
+    fast_recovery_exit_ = next_tsn_ - 1;
+  }
+  if (fast_recovery_ && !tsn_lt(cum, fast_recovery_exit_)) fast_recovery_ = false;
+  peer_rwnd_ = a_rwnd > flight_size_ ? a_rwnd - flight_size_ : 0;
+  if (inflight_.empty()) stop_t3();
+  else if (cum_advanced) start_t3();
+  maybe_finish_shutdown();
+}
+
+void SctpAssociation::handle_forward_tsn(const uint8_t* c, size_t len) {
+  if (len < 4) return;
+  uint32_t nc = rd32(c);
+  sack_needed_ = true;
+  if (!tsn_lt(peer_cum_tsn_, nc)) return;
+  for (auto it = ooo_.begin(); it != ooo_.end();) {
+    if (tsn_le(it->first, nc)) {
+      ooo_bytes_ -= it->second->data.size();
+      delete it->second;
+      it = ooo_.erase(it);
+    } else {
+      ++it;
+    }
+  }
+  peer_cum_tsn_ = nc;
+  for (auto& kv : partial_u_) kv.second.active = false;
+  // Continue delivery of anything now contiguous.
+  while (!ooo_.empty()) {
+    auto it = ooo_.find(peer_cum_tsn_ + 1);
+    if (it == ooo_.end()) break;
+    InChunk* ic = it->second;
+    ooo_.erase(it);
+    ooo_bytes_ -= ic->data.size();
+    std::vector<uint8_t> tmp = std::move(ic->data);
+    uint8_t fl = ic->flags;
+    uint16_t st = ic->stream;
+    uint32_t pp = ic->ppid;
+    delete ic;
+    // Re-enter the in-order path.
+    std::vector<uint8_t> hdr(12);
+    wr32(hdr.data(), peer_cum_tsn_ + 1);
+    wr16(hdr.data() + 4, st);
+    wr32(hdr.data() + 8, pp);
+    hdr.insert(hdr.end(), tmp.begin(), tmp.end());
+    handle_data(fl, hdr.data(), hdr.size());
+  }
+}
+
+void SctpAssociation::handle_reconfig(const uint8_t* c, size_t len) {
+  size_t off = 0;
+  while (off + 4 <= len) {
+    uint16_t pt = rd16(c + off), pl = rd16(c + off + 2);
+    if (pl < 4 || off + pl > len) break;
+    if (pt == 13 && pl >= 16) {  // Outgoing SSN Reset Request
+      uint32_t req_seq = rd32(c + off + 4);
+      std::vector<uint16_t> streams;
+      for (size_t k = 16; k + 2 <= pl; k += 2) streams.push_back(rd16(c + off + k));
+      std::vector<uint8_t> b;
+      put16(b, 16);  // Re-configuration Response
+      put16(b, 12);
+      put32(b, req_seq);
+      put32(b, 1);  // Success - Performed
+      queue_control(kReconfig, 0, b);
+      for (uint16_t s : streams) {
+        partial_.erase(s);
+        if (on_stream_reset) on_stream_reset(s);
+      }
+    }
+    off += (pl + 3u) & ~3u;
+  }
+}
+
+void SctpAssociation::request_stream_reset(uint16_t stream) {
+  if (state_ != State::Established) return;
+  std::vector<uint8_t> b;
+  put16(b, 13);
+  put16(b, 18);
+  put32(b, reconfig_seq_++);
+  put32(b, 0);
+  put32(b, next_tsn_ - 1);
+  put16(b, stream);
+  pad4(b);
+  queue_control(kReconfig, 0, b);
+}
+
+// ------------------------------------------------------------------ sender
+
+bool SctpAssociation::send(uint16_t stream, uint32_t ppid, const std::vector<Bytes>& pieces, bool unordered) {
+  if (closed_fired_ || state_ == State::ShutdownPending || state_ == State::ShutdownSent) return false;
+  Msg m;
+  m.stream = stream;
+  m.ppid = ppid;
+  m.unordered = unordered;
+  m.pieces = pieces;
+  m.len = 0;
+  for (auto& p : pieces) m.len += p.size();
+  if (m.len == 0) return false;
+  m.ssn = unordered ? 0 : next_ssn_[stream]++;
+  unsent_bytes_ += m.len;
+  sendq_.push_back(std::move(m));
+  return true;
+}
+
+void SctpAssociation::start_t3() {
+  stop_t3();
+  std::weak_ptr<SctpAssociation> w = shared_from_this();
+  t3_timer_ = r_.call_later_us(rto_us_, [w] {
+    if (auto s = w.lock()) {
+      s->t3_timer_ = 0;
+      s->on_t3();
+    }
+  });
+}
+
+void SctpAssociation::stop_t3() {
+  if (t3_timer_) r_.cancel(t3_timer_);
+  t3_timer_ = 0;
+}
+
+void SctpAssociation::on_t3() {
+  if (inflight_.empty()) return;
+  stats_.t3_expirations++;
+  if (++assoc_errors_ > cfg_.max_assoc_retrans) {
+    abort("SCTP: too many retransmissions");
+    return;
+  }
+  ssthresh_ = std::max(cwnd_ / 2, 4 * cfg_.mtu);
+  cwnd_ = cfg_.mtu;
+  partial_acked_ = 0;
+  fast_recovery_ = false;
+  rto_us_ = std::min<uint64_t>(rto_us_ * 2, cfg_.rto_max_ms * 1000);
+  for (Chunk* ch : inflight_) {
+    if (ch->acked) continue;
+    ch->retransmit = true;
+    ch->fast = false;
+    if (ch->in_flight) {
+      flight_size_ -= ch->len;
+      ch->in_flight = false;
+    }
+  }
+  LOG_DEBUG(kT, "T3-rtx expired: rto %llu ms, %zu chunks outstanding",
+            static_cast<unsigned long long>(rto_us_ / 1000), inflight_.size());
+  // flush() runs at the end of this reactor iteration and retransmits.
+}
+
+void SctpAssociation::flush() {
+  if (closed_fired_) return;
+  auto self = shared_from_this();
+  bool can_data = state_ == State::Established || state_ == State::ShutdownPending ||
+                  state_ == State::ShutdownReceived;
+  if (!can_data && ctrl_.empty()) return;
+  const size_t mtu = cfg_.mtu;
+  size_t max_payload = mtu - kCommonHdr - kDataHdr;
+  std::vector<uint8_t>& pkt = pkt_;
+  begin_packet(pkt, cfg_.local_port, cfg_.remote_port, peer_vtag_);
+  auto flush_pkt = [&] {
+    if (pkt.size() > kCommonHdr) emit_packet(pkt);
+    begin_packet(pkt, cfg_.local_port, cfg_.remote_port, peer_vtag_);
+  };
+  auto add_raw = [&](const std::vector<uint8_t>& ch) {
+    if (pkt.size() + ch.size() > mtu) flush_pkt();
+    pkt.insert(pkt.end(), ch.begin(), ch.end());
+  };
+  // SACK first (RFC 9260 §6.1: SACK goes before DATA when bundled).
+  if (sack_needed_ && have_peer_tsn_ && peer_vtag_) {
+    std::vector<uint8_t> b;
+    build_sack(b);
+    std::vector<uint8_t> ch;
+    ch.push_back(kSack);
+    ch.push_back(0);
+    put16(ch, uint16_t(4 + b.size()));
+    ch.insert(ch.end(), b.begin(), b.end());
+    add_raw(ch);
+    sack_needed_ = false;
+    stats_.sacks_sent++;
+  }
+  for (auto& ch : ctrl_) add_raw(ch);
+  ctrl_.clear();
+  if (!can_data) {
+    flush_pkt();
+    return;
+  }
+  uint64_t now = Reactor::now_us();
+  auto add_data = [&](Chunk* ch) {
+    size_t need = kDataHdr + ((ch->len + 3) & ~size_t(3));
+    if (pkt.size() + need > mtu) flush_pkt();
+    size_t start = pkt.size();
+    pkt.push_back(kData);
+    pkt.push_back(ch->flags);
+    put16(pkt, uint16_t(kDataHdr + ch->len));
+    put32(pkt, ch->tsn);
+    put16(pkt, ch->stream);
+    put16(pkt, ch->ssn);
+    put32(pkt, ch->ppid);
+    for (auto& b : ch->data) pkt.insert(pkt.end(), b.begin(), b.end());
+    pad4(pkt);
+    (void)start;
+    ch->sent_us = now;
+    ch->tx++;
+    if (!ch->in_flight) {
+      ch->in_flight = true;
+      flight_size_ += ch->len;
+    }
+    stats_.data_chunks_sent++;
+    stats_.bytes_sent += ch->len;
+  };
+  // Retransmissions first. A fast-retransmit burst may exceed cwnd once.
+  bool fast_budget = true;
+  bool sent_any = false;
+  for (Chunk* ch : inflight_) {
+    if (!ch->retransmit || ch->acked) continue;
+    bool allowed = flight_size_ + ch->len <= cwnd_ || flight_size_ == 0 || (ch->fast && fast_budget);
+    if (!allowed) break;
+    if (ch->fast) fast_budget = false;
+    ch->retransmit = false;
+    ch->fast = false;
+    ch->miss = 0;
+    add_data(ch);
+    stats_.retransmits++;
+    sent_any = true;
+  }
+  // New data.
+  while (!sendq_.empty()) {
+    Msg& m = sendq_.front();
+    size_t left = m.len - m.off;
+    size_t take = std::min(left, max_payload);
+    if (flight_size_ > 0 && (flight_size_ + take > cwnd_ || take > peer_rwnd_)) break;
+    if (flight_size_ == 0 && peer_rwnd_ == 0 && !inflight_.empty()) break;  // wait for window / T3 probe
+    auto* ch = new Chunk();
+    ch->tsn = next_tsn_++;
+    ch->stream = m.stream;
+    ch->ssn = m.ssn;
+    ch->ppid = m.ppid;
+    ch->flags = uint8_t((m.off == 0 ? 2 : 0) | (take == left ? 1 : 0) | (m.unordered ? 4 : 0));
+    ch->len = take;
+    // Slice [off, off+take) out of the gathered pieces without copying.
+    size_t pos = 0, want_lo = m.off, want_hi = m.off + take;
+    for (auto& piece : m.pieces) {
+      size_t lo = pos, hi = pos + piece.size();
+      pos = hi;
+      if (hi <= want_lo || lo >= want_hi) continue;
+      size_t a = std::max(lo, want_lo) - lo, b = std::min(hi, want_hi) - lo;
+      ch->data.push_back(piece.slice(a, b - a));
+    }
+    m.off += take;
+    unsent_bytes_ -= take;
+    inflight_.push_back(ch);
+    add_data(ch);
+    peer_rwnd_ = peer_rwnd_ > take ? peer_rwnd_ - take : 0;
+    sent_any = true;
+    if (m.off == m.len) sendq_.pop_front();
+  }
+  flush_pkt();
+  if (sent_any && !t3_timer_) start_t3();
+  if (sent_any && on_sent) on_sent();
+}
+
+}  // namespace p2pt::rtc

@@ -1,0 +1,76 @@
+// TURN client (RFC 8656, UDP allocations, long-term credentials).
+//
+// The reference wires --turn/--turn-user/--turn-pass into webrtc-rs's ICE
+// servers (tunnel/src/cli.rs:30-40, rtc.rs:54-63) while its README claims TURN
+// is "not yet implemented" (README.md:130). Here it is a real
+// client: Allocate (401 -> REALM/NONCE -> authenticated retry), Refresh before
+// expiry, CreatePermission per remote candidate, ChannelBind for compact
+// ChannelData framing, Send/Data indications until the channel is bound.
+#pragma once
+
+#include <functional>
+#include <map>
+#include <memory>
+#include <string>
+
+#include "core/net.h"
+#include "core/reactor.h"
+#include "rtc/stun.h"
+
+namespace p2pt::rtc {
+
+class IceAgent;
+
+class TurnClient : public std::enable_shared_from_this<TurnClient> {
+ public:
+  using AllocCb = std::function<void(bool ok, const SockAddr& relayed, const SockAddr& mapped)>;
+  static std::shared_ptr<TurnClient> create(Reactor& r, IceAgent* agent, int sock, const std::string& host,
+                                            uint16_t port, const std::string& user, const std::string& pass,
+                                            AllocCb cb);
+  ~TurnClient();
+  void close();
+  bool is_server(int sock, const SockAddr& from) const { return sock == sock_ && resolved_ && from == server_; }
+  void on_packet(const uint8_t* p, size_t n);
+  void permit(const SockAddr& peer);
+  void send_to(const SockAddr& peer, const uint8_t* p, size_t n);
+  bool allocated() const { return allocated_; }
+
+ private:
+  TurnClient(Reactor& r, IceAgent* agent, int sock) : r_(r), agent_(agent), sock_(sock) {}
+  void send_request(stun::Message m, std::function<void(const stun::Message&, const uint8_t*, size_t)> on_resp);
+  void allocate();
+  void refresh(uint32_t lifetime);
+  void create_permission(const SockAddr& peer);
+  void channel_bind(const SockAddr& peer);
+  void sign(stun::Message& m);
+  void raw_send(const uint8_t* p, size_t n);
+
+  Reactor& r_;
+  IceAgent* agent_;
+  int sock_;
+  SockAddr server_;
+  bool resolved_ = false;
+  std::string user_, pass_, realm_, nonce_, key_;
+  bool allocated_ = false;
+  bool closed_ = false;
+  SockAddr relayed_, mapped_;
+  AllocCb alloc_cb_;
+  uint64_t refresh_timer_ = 0, perm_timer_ = 0;
+  struct Pending {
+    std::function<void(const stun::Message&, const uint8_t*, size_t)> cb;
+    std::vector<uint8_t> bytes;
+    int tries = 0;
+    uint64_t timer = 0;
+  };
+  std::map<std::string, Pending> pending_;
+  struct PeerState {
+    bool permitted = false;
+    uint16_t channel = 0;
+    bool bound = false;
+  };
+  std::map<std::string, PeerState> peers_;  // key: addr string
+  std::map<uint16_t, SockAddr> channels_;
+  uint16_t next_channel_ = 0x4000;
+};
+
+}  // namespace p2pt::rtc

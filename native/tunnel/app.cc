@@ -247,8 +247,13 @@ int run_app(const AppConfig& cfg) {
   };
 
   auto interrupt = [&] {
-    if (st.backoff_timer) LOG_INFO(kT, "received Ctrl+C during retry backoff, exiting");
-    else LOG_INFO(kT, "received Ctrl+C, exiting");
+    if (st.backoff_timer) {
+      LOG_INFO(kT, "received Ctrl+C during retry backoff, exiting");
+      r.cancel(st.backoff_timer);
+      st.backoff_timer = 0;
+    } else {
+      LOG_INFO(kT, "received Ctrl+C, exiting");
+    }
     st.exit_code = 1;
     st.in_attempt = false;
     r.stop();

@@ -270,13 +270,14 @@ void WsConn::connect(Reactor& r, const std::string& url_s, ConnectCb cb, uint64_
     std::string req = "GET " + op->url.path + " HTTP/1.1\r\nHost: " + op->url.host_header() +
                       "\r\nConnection: Upgrade\r\nUpgrade: websocket\r\nSec-WebSocket-Version: 13\r\n"
                       "Sec-WebSocket-Key: " + op->key + "\r\n\r\n";
-    std::weak_ptr<WsConnectOp> wo = op;
-    c->on_close([wo](const std::string& err) {
-      if (auto o = wo.lock()) o->finish(nullptr, "connection closed during handshake" + (err.empty() ? "" : ": " + err));
+    // The handshake callbacks own the op until the socket is handed to the
+    // WsConn (wire() replaces them) or closed.
+    c->on_close([op](const std::string& err) {
+      op->finish(nullptr, "connection closed during handshake" + (err.empty() ? "" : ": " + err));
     });
-    c->on_data([wo](const uint8_t* p, size_t n) {
-      auto o = wo.lock();
-      if (!o || o->done) return;
+    c->on_data([op](const uint8_t* p, size_t n) {
+      auto o = op;
+      if (o->done) return;
       o->buf.append(reinterpret_cast<const char*>(p), n);
       http::Head h;
       size_t used = 0;
