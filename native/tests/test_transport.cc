@@ -1,0 +1,204 @@
+// Transport components in-process: SCTP association pair over a lossy,
+// reordering, duplicating link; DTLS pair; full PeerConnection pair over
+// loopback UDP (ICE + DTLS + SCTP + DCEP).
+#include <random>
+
+#include "core/reactor.h"
+#include "rtc/dtls.h"
+#include "rtc/peer.h"
+#include "rtc/sctp.h"
+#include "tests/testing.h"
+
+using namespace p2pt;
+using namespace p2pt::rtc;
+
+namespace {
+
+struct LossyLink {
+  Reactor& r;
+  double loss, dup;
+  uint64_t max_delay_us;
+  std::mt19937 rng{12345};
+  uint64_t dropped = 0;
+  LossyLink(Reactor& rr, double l, double d, uint64_t delay) : r(rr), loss(l), dup(d), max_delay_us(delay) {}
+  void carry(std::weak_ptr<SctpAssociation> to, const uint8_t* p, size_t n) {
+    std::uniform_real_distribution<double> u(0, 1);
+    if (u(rng) < loss) {
+      dropped++;
+      return;
+    }
+    int copies = u(rng) < dup ? 2 : 1;
+    for (int i = 0; i < copies; i++) {
+      auto pkt = std::make_shared<std::vector<uint8_t>>(p, p + n);
+      uint64_t d = max_delay_us ? std::uniform_int_distribution<uint64_t>(0, max_delay_us)(rng) : 0;
+      r.call_later_us(d, [to, pkt] {
+        if (auto s = to.lock()) s->on_packet(pkt->data(), pkt->size());
+      });
+    }
+  }
+};
+
+struct SctpPair {
+  Reactor r;
+  std::shared_ptr<SctpAssociation> a, b;
+  LossyLink link;
+  std::vector<std::pair<uint16_t, std::string>> got_a, got_b;
+  SctpPair(double loss, double dup, uint64_t delay, size_t mtu = 1200) : link(r, loss, dup, delay) {
+    SctpConfig cfg;
+    cfg.mtu = mtu;
+    cfg.rto_initial_ms = 100;
+    cfg.rto_min_ms = 20;
+    a = SctpAssociation::create(r, cfg, [this](const uint8_t* p, size_t n) { link.carry(b, p, n); });
+    b = SctpAssociation::create(r, cfg, [this](const uint8_t* p, size_t n) { link.carry(a, p, n); });
+    a->on_message = [this](uint16_t s, uint32_t, Bytes m) { got_a.emplace_back(s, m.str()); };
+    b->on_message = [this](uint16_t s, uint32_t, Bytes m) { got_b.emplace_back(s, m.str()); };
+    r.add_flush_hook([this] {
+      a->flush();
+      b->flush();
+    });
+  }
+};
+
+std::string payload(size_t n, uint32_t seed) {
+  std::string s(n, '\0');
+  std::mt19937 g(seed);
+  for (auto& c : s) c = char(g());
+  return s;
+}
+
+}  // namespace
+
+TEST(sctp_simultaneous_open_and_messages) {
+  SctpPair p(0, 0, 0);
+  p.a->connect();
+  p.b->connect();
+  CHECK(p.r.run_until([&] { return p.a->established() && p.b->established(); }, 2000));
+  std::vector<std::string> sent;
+  for (int i = 0; i < 50; i++) {
+    sent.push_back(payload(size_t(1 + (i * 7919) % 70000), uint32_t(i)));
+    p.a->send(1, 53, {Bytes::copy(sent.back())});
+  }
+  p.b->send(1, 53, {Bytes::copy("x", 1), Bytes::copy("yz", 2)});  // gathered pieces
+  CHECK(p.r.run_until([&] { return p.got_b.size() == 50 && p.got_a.size() == 1; }, 5000));
+  for (size_t i = 0; i < p.got_b.size() && i < sent.size(); i++) CHECK(p.got_b[i].second == sent[i]);
+  CHECK(!p.got_a.empty() && p.got_a[0].second == "xyz");
+  CHECK_EQ(p.a->stats().retransmits, uint64_t(0));
+}
+
+TEST(sctp_loss_reorder_dup_recovery) {
+  SctpPair p(0.05, 0.03, 3000);
+  p.a->connect();
+  p.b->connect();
+  CHECK(p.r.run_until([&] { return p.a->established() && p.b->established(); }, 5000));
+  std::vector<std::string> sent;
+  size_t total = 0;
+  for (int i = 0; i < 200; i++) {
+    sent.push_back(payload(size_t(1 + (i * 104729) % 20000), uint32_t(1000 + i)));
+    total += sent.back().size();
+    p.a->send(3, 53, {Bytes::copy(sent.back())});
+  }
+  CHECK(p.r.run_until([&] { return p.got_b.size() == sent.size() && p.a->bytes_in_flight() == 0; }, 30000));
+  CHECK_EQ(p.got_b.size(), sent.size());
+  bool in_order = true;
+  for (size_t i = 0; i < p.got_b.size() && i < sent.size(); i++) in_order &= p.got_b[i].second == sent[i];
+  CHECK(in_order);
+  CHECK(p.link.dropped > 0);
+  CHECK(p.a->stats().retransmits > 0);
+  (void)total;
+}
+
+TEST(sctp_jumbo_bulk_throughput) {
+  SctpPair p(0, 0, 0, 16000);
+  p.a->set_initial_cwnd(1 << 20);
+  p.a->connect();
+  p.b->connect();
+  CHECK(p.r.run_until([&] { return p.a->established() && p.b->established(); }, 2000));
+  std::string blk = payload(65413, 7);
+  const int n = 300;  // ~19.6 MB
+  for (int i = 0; i < n; i++) p.a->send(1, 53, {Bytes::copy(blk)});
+  uint64_t t0 = Reactor::now_us();
+  CHECK(p.r.run_until([&] { return p.got_b.size() == size_t(n); }, 20000));
+  double secs = double(Reactor::now_us() - t0) / 1e6;
+  printf("  sctp in-memory: %.1f MB/s (jumbo 16000)\n", n * 65413 / 1e6 / secs);
+  CHECK(p.got_b.size() == size_t(n) && p.got_b.back().second == blk);
+}
+
+TEST(dtls_pair_handshake_and_data) {
+  Reactor r;
+  std::shared_ptr<DtlsTransport> c, s;
+  std::string fp = DtlsTransport::local_fingerprint();
+  c = DtlsTransport::create(r, true, fp, [&](const uint8_t* p, size_t n) {
+    auto v = std::make_shared<std::vector<uint8_t>>(p, p + n);
+    r.post([&s, v] { s->on_datagram(v->data(), v->size()); });
+  });
+  s = DtlsTransport::create(r, false, fp, [&](const uint8_t* p, size_t n) {
+    auto v = std::make_shared<std::vector<uint8_t>>(p, p + n);
+    r.post([&c, v] { c->on_datagram(v->data(), v->size()); });
+  });
+  std::string got;
+  s->on_data = [&](const uint8_t* p, size_t n) { got.append(reinterpret_cast<const char*>(p), n); };
+  bool cc = false, sc = false;
+  c->on_connected = [&] { cc = true; };
+  s->on_connected = [&] { sc = true; };
+  c->start();
+  s->start();
+  CHECK(r.run_until([&] { return cc && sc; }, 3000));
+  CHECK(c->send(reinterpret_cast<const uint8_t*>("hello"), 5));
+  CHECK(r.run_until([&] { return got == "hello"; }, 1000));
+  CHECK(c->cipher().find("GCM") != std::string::npos || !c->cipher().empty());
+}
+
+TEST(dtls_fingerprint_mismatch_fails) {
+  Reactor r;
+  std::shared_ptr<DtlsTransport> c, s;
+  std::string fp = DtlsTransport::local_fingerprint();
+  std::string bad = "sha-256 00:11:22";
+  c = DtlsTransport::create(r, true, bad, [&](const uint8_t* p, size_t n) {
+    auto v = std::make_shared<std::vector<uint8_t>>(p, p + n);
+    r.post([&s, v] { if (s) s->on_datagram(v->data(), v->size()); });
+  });
+  s = DtlsTransport::create(r, false, fp, [&](const uint8_t* p, size_t n) {
+    auto v = std::make_shared<std::vector<uint8_t>>(p, p + n);
+    r.post([&c, v] { if (c) c->on_datagram(v->data(), v->size()); });
+  });
+  std::string why;
+  c->on_closed = [&](const std::string& w) { why = w; };
+  c->start();
+  CHECK(r.run_until([&] { return !why.empty(); }, 3000));
+  CHECK(why.find("fingerprint") != std::string::npos);
+  CHECK(!c->connected());
+}
+
+TEST(peerconnection_pair_loopback) {
+  Reactor r;
+  PcConfig cfg;
+  cfg.ice.include_loopback = true;
+  auto off = PeerConnection::create(r, cfg, true);
+  auto ans = PeerConnection::create(r, cfg, false);
+  off->on_ice_candidate = [&](const std::string& c) { ans->add_ice_candidate(c, nullptr); };
+  ans->on_ice_candidate = [&](const std::string& c) { off->add_ice_candidate(c, nullptr); };
+  auto dc = off->create_data_channel("tunnel");
+  std::shared_ptr<DataChannel> rdc;
+  std::vector<std::string> at_ans, at_off;
+  ans->on_data_channel = [&](std::shared_ptr<DataChannel> d) {
+    rdc = d;
+    d->on_message = [&](Bytes m) { at_ans.push_back(m.str()); };
+  };
+  dc->on_message = [&](Bytes m) { at_off.push_back(m.str()); };
+  off->start_gathering();
+  ans->start_gathering();
+  CHECK(r.run_until([&] { return off->gathering_complete(); }, 3000));
+  std::string err;
+  CHECK(ans->set_remote_description(off->local_description(), &err));
+  CHECK(off->set_remote_description(ans->local_description(), &err));
+  CHECK(r.run_until([&] { return dc->is_open() && rdc && rdc->is_open(); }, 5000));
+  uint8_t hdr[5] = {21, 0, 0, 0, 1};
+  for (int i = 0; i < 10; i++) dc->send(hdr, 5, Bytes::copy(std::to_string(i)));
+  rdc->send(hdr, 5, Bytes::copy("back"));
+  CHECK(r.run_until([&] { return at_ans.size() == 10 && at_off.size() == 1; }, 3000));
+  CHECK(at_ans.size() == 10 && at_ans[9] == std::string("\x15\x00\x00\x00\x01", 5) + "9");
+  CHECK(off->state() == PcState::Connected && ans->state() == PcState::Connected);
+  printf("  path: %s\n", off->describe_path().c_str());
+  off->close();
+  ans->close();
+}
