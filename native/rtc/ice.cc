@@ -330,6 +330,19 @@ void IceAgent::maybe_gathering_done() {
   }
 }
 
+void IceAgent::kick() {
+  // Run the check scheduler now instead of waiting for the next pacing tick.
+  if (closed_ || !gather_started_ || state_ == IceState::Failed) return;
+  if (tick_timer_) r_.cancel(tick_timer_);
+  std::weak_ptr<IceAgent> w = shared_from_this();
+  tick_timer_ = r_.call_later_us(0, [w] {
+    if (auto s = w.lock()) {
+      s->tick_timer_ = 0;
+      s->tick();
+    }
+  });
+}
+
 void IceAgent::set_remote_credentials(const std::string& ufrag, const std::string& pwd) {
   remote_ufrag_ = ufrag;
   remote_pwd_ = pwd;
@@ -337,6 +350,7 @@ void IceAgent::set_remote_credentials(const std::string& ufrag, const std::strin
     checking_since_ = Reactor::now_ms();
     set_state(IceState::Checking);
   }
+  kick();
 }
 
 int IceAgent::find_remote(const SockAddr& a) const {
@@ -356,6 +370,7 @@ void IceAgent::add_remote_candidate(const Candidate& c) {
     checking_since_ = Reactor::now_ms();
     set_state(IceState::Checking);
   }
+  if (!remote_pwd_.empty() && sel_pair_ < 0) kick();
 }
 
 uint64_t IceAgent::pair_priority(const Local& l, const Candidate& r) const {
@@ -395,10 +410,69 @@ void IceAgent::send(const uint8_t* p, size_t n) {
   send_raw(sel_local_, sel_remote_, p, n);
 }
 
+// Test-only fault injection on the datagram path (SURVEY §4.2 "fault
+// injection"): TUNNEL_FAULT_DROP / TUNNEL_FAULT_DUP are probabilities,
+// TUNNEL_FAULT_DELAY_MS a uniform random extra delay (which also reorders).
+// STUN (connectivity checks) is exempt so the path still comes up.
+namespace {
+struct FaultCfg {
+  double drop = 0, dup = 0;
+  uint64_t delay_us = 0;
+  bool on = false;
+  uint64_t rng = 0x9E3779B97F4A7C15ull;
+  FaultCfg() {
+    if (const char* e = getenv("TUNNEL_FAULT_DROP")) drop = atof(e);
+    if (const char* e = getenv("TUNNEL_FAULT_DUP")) dup = atof(e);
+    if (const char* e = getenv("TUNNEL_FAULT_DELAY_MS")) delay_us = uint64_t(atof(e) * 1000);
+    on = drop > 0 || dup > 0 || delay_us > 0;
+    rng ^= uint64_t(getpid()) << 20;
+  }
+  double uni() {
+    rng ^= rng << 13;
+    rng ^= rng >> 7;
+    rng ^= rng << 17;
+    return double(rng >> 11) / double(1ull << 53);
+  }
+};
+FaultCfg& fault() {
+  static FaultCfg f;
+  return f;
+}
+}  // namespace
+
 void IceAgent::flush() {
   if (outq_.empty() || closed_) {
     outq_.clear();
     return;
+  }
+  if (fault().on) {
+    std::vector<Out> keep;
+    for (auto& o : outq_) {
+      if (o.faulted || stun::looks_like_stun(o.data.data(), o.data.size()) || o.local < 0) {
+        keep.push_back(std::move(o));
+        continue;
+      }
+      FaultCfg& f = fault();
+      if (f.uni() < f.drop) continue;
+      int copies = f.uni() < f.dup ? 2 : 1;
+      for (int c = 0; c < copies; c++) {
+        if (f.delay_us) {
+          uint64_t d = uint64_t(f.uni() * double(f.delay_us));
+          auto held = std::make_shared<Out>(o);
+          held->faulted = true;
+          std::weak_ptr<IceAgent> w = shared_from_this();
+          r_.call_later_us(d, [w, held] {
+            auto s = w.lock();
+            if (!s || s->closed_) return;
+            s->outq_.push_back(std::move(*held));
+          });
+        } else {
+          keep.push_back(o);
+        }
+      }
+    }
+    outq_.swap(keep);
+    if (outq_.empty()) return;
   }
   // Group consecutive datagrams by socket for sendmmsg.
   constexpr int kBatch = 64;
@@ -599,6 +673,7 @@ void IceAgent::handle_request(int si, const SockAddr& from, const stun::Message&
     if (pr.st == Pair::St::Waiting || pr.st == Pair::St::Failed) {
       pr.st = Pair::St::Waiting;  // triggered check
       pr.next_tx = 0;
+      if (sel_pair_ < 0 && !remote_pwd_.empty()) kick();
     }
   }
 }

@@ -135,6 +135,7 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   void pair_up(int local, int remote);
   uint64_t pair_priority(const Local& l, const Candidate& r) const;
   void tick();
+  void kick();
   void send_check(Pair& p);
   void send_raw(int local_idx, const SockAddr& to, const uint8_t* p, size_t n);
   void select_pair(int pair_idx);
@@ -180,6 +181,7 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
     int local;
     SockAddr to;
     std::vector<uint8_t> data;
+    bool faulted = false;  // already passed the fault injector
   };
   std::vector<Out> outq_;
   std::vector<uint8_t> rxbuf_;
