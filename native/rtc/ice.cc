@@ -166,6 +166,7 @@ void IceAgent::open_sockets() {
 
 void IceAgent::add_local(Candidate c, int sock, bool relay) {
   locals_.push_back(Local{c, sock, relay});
+  if (cfg_.relay_only && !relay) return;  // kept as a socket base, never advertised or paired
   local_cands_.push_back(c);
   int li = int(locals_.size()) - 1;
   for (int ri = 0; ri < int(remotes_.size()); ri++) pair_up(li, ri);
@@ -279,20 +280,24 @@ void IceAgent::start_srflx() {
 
 void IceAgent::start_relay() {
   if (cfg_.turn_url.empty()) return;
-  int si = -1;
-  for (int i = 0; i < int(socks_.size()); i++)
-    if (!socks_[i].loopback && socks_[i].addr.family() == AF_INET) {
-      si = i;
-      break;
-    }
-  if (si < 0) {
-    LOG_WARN(kT, "TURN: no non-loopback IPv4 socket to allocate from");
-    return;
-  }
   std::string host;
   uint16_t port;
   if (!parse_server_url(cfg_.turn_url, host, port, 3478)) {
     LOG_WARN(kT, "invalid TURN URL %s", cfg_.turn_url.c_str());
+    return;
+  }
+  // A loopback TURN server (tests, same-host relays) is reached from the
+  // loopback socket; anything else from the first routable IPv4 socket.
+  SockAddr probe;
+  bool server_loopback = SockAddr::parse(host, port, probe) && probe.is_loopback();
+  int si = -1;
+  for (int i = 0; i < int(socks_.size()); i++)
+    if (socks_[i].loopback == server_loopback && socks_[i].addr.family() == AF_INET) {
+      si = i;
+      break;
+    }
+  if (si < 0) {
+    LOG_WARN(kT, "TURN: no suitable IPv4 socket to allocate from");
     return;
   }
   pending_gather_++;
@@ -383,6 +388,7 @@ void IceAgent::pair_up(int li, int ri) {
   const Local& l = locals_[li];
   const Candidate& rc = remotes_[ri];
   if (l.c.type == "srflx") return;  // checks run from the base (host) candidate
+  if (cfg_.relay_only && !l.relay) return;
   SockAddr laddr = l.relay ? l.c.addr : socks_[l.sock].addr;
   if (laddr.family() != rc.addr.family()) return;
   // Loopback sockets only talk to loopback remotes and vice versa.

@@ -53,6 +53,9 @@ struct IceConfig {
   std::string turn_user, turn_pass;
   bool include_loopback = true;
   bool include_ipv6 = false;
+  // iceTransportPolicy "relay": only TURN-relayed local candidates are
+  // advertised and checked (forces the TURN path, e.g. symmetric NATs).
+  bool relay_only = false;
   uint64_t stun_timeout_ms = 2000;
   uint64_t disconnected_ms = 5000;
   uint64_t failed_ms = 30000;

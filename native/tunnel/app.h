@@ -32,6 +32,7 @@ struct RtcOptions {
   TurnConfig turn;
   bool include_loopback = true;     // host candidates on lo (offline / same-host peers)
   bool include_ipv6 = false;
+  bool relay_only = false;            // iceTransportPolicy=relay
   uint64_t gather_timeout_ms = 5000;  // reference waits <= 5 s (rtc.rs:181-182)
   uint64_t ice_failed_timeout_ms = 30000;
   size_t sctp_mtu = 1200;             // interop-safe DTLS payload budget

@@ -1,0 +1,208 @@
+"""Minimal TURN server (RFC 8656, UDP relays, long-term credentials) for tests.
+
+Independent of the native code: the STUN codec here is written in Python so
+the native TURN client (native/rtc/turn.cc) is checked against a separate
+implementation. Supports Allocate (401 challenge -> authenticated), Refresh
+(incl. LIFETIME 0), CreatePermission, ChannelBind, Send/Data indications and
+ChannelData in both directions.
+"""
+from __future__ import annotations
+
+import hashlib
+import hmac
+import os
+import select
+import socket
+import struct
+import threading
+import zlib
+
+MAGIC = 0x2112A442
+
+
+def _pad(n):
+    return (4 - n % 4) % 4
+
+
+def parse(data: bytes):
+    if len(data) < 20 or data[0] >= 4:
+        return None
+    t, ln, magic = struct.unpack(">HHI", data[:8])
+    if magic != MAGIC or 20 + ln > len(data):
+        return None
+    tid = data[8:20]
+    attrs, off, mi_off = [], 20, None
+    while off + 4 <= 20 + ln:
+        at, al = struct.unpack(">HH", data[off:off + 4])
+        if at == 0x0008:
+            mi_off = off
+        attrs.append((at, data[off + 4:off + 4 + al]))
+        off += 4 + al + _pad(al)
+    return t, tid, attrs, mi_off
+
+
+def build(t, tid, attrs, key=None, fingerprint=True):
+    body = b"".join(struct.pack(">HH", a, len(v)) + v + b"\0" * _pad(len(v)) for a, v in attrs)
+    if key is not None:
+        hdr = struct.pack(">HHI", t, len(body) + 24, MAGIC) + tid
+        mac = hmac.new(key, hdr + body, hashlib.sha1).digest()
+        body += struct.pack(">HH", 0x0008, 20) + mac
+    if fingerprint:
+        hdr = struct.pack(">HHI", t, len(body) + 8, MAGIC) + tid
+        crc = (zlib.crc32(hdr + body) ^ 0x5354554E) & 0xFFFFFFFF
+        body += struct.pack(">HHI", 0x8028, 4, crc)
+    return struct.pack(">HHI", t, len(body), MAGIC) + tid + body
+
+
+def xor_addr(host: str, port: int) -> bytes:
+    ip = struct.unpack(">I", socket.inet_aton(host))[0] ^ MAGIC
+    return struct.pack(">BBHI", 0, 1, port ^ (MAGIC >> 16), ip)
+
+
+def unxor_addr(v: bytes):
+    _, fam, xp, xi = struct.unpack(">BBHI", v[:8])
+    return socket.inet_ntoa(struct.pack(">I", xi ^ MAGIC)), xp ^ (MAGIC >> 16)
+
+
+class TurnServer:
+    def __init__(self, user="user", password="pass", realm="p2pt.test", host="127.0.0.1"):
+        self.user, self.password, self.realm = user, password, realm
+        self.key = hashlib.md5(f"{user}:{realm}:{password}".encode()).digest()
+        self.nonce = os.urandom(8).hex().encode()
+        self.sock = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        self.sock.bind((host, 0))
+        self.host = host
+        self.port = self.sock.getsockname()[1]
+        self.allocs = {}     # client addr -> dict(relay=sock, perms=set(ip), chans={num: peer}, peers={peer: num})
+        self.by_relay = {}   # relay sock -> client addr
+        self.stats = {"allocations": 0, "relayed_to_peer": 0, "relayed_to_client": 0, "channel_binds": 0}
+        self._stop = False
+        self.thread = threading.Thread(target=self._run, daemon=True)
+
+    @property
+    def url(self):
+        return f"turn:{self.host}:{self.port}"
+
+    def start(self):
+        self.thread.start()
+        return self
+
+    def stop(self):
+        self._stop = True
+        self.thread.join(timeout=2)
+        for a in self.allocs.values():
+            a["relay"].close()
+        self.sock.close()
+
+    # ------------------------------------------------------------------
+    def _auth_ok(self, data, attrs, mi_off):
+        d = dict(attrs)
+        if mi_off is None or d.get(0x0006) != self.user.encode() or d.get(0x0014) != self.realm.encode():
+            return False
+        hdr = bytearray(data[:mi_off])
+        struct.pack_into(">H", hdr, 2, mi_off - 20 + 24)
+        mac = hmac.new(self.key, bytes(hdr), hashlib.sha1).digest()
+        return mac == data[mi_off + 4:mi_off + 24]
+
+    def _err(self, t, tid, code, reason, addr):
+        v = struct.pack(">HBB", 0, code // 100, code % 100) + reason.encode()
+        attrs = [(0x0009, v), (0x0014, self.realm.encode()), (0x0015, self.nonce)]
+        self.sock.sendto(build(t | 0x0110, tid, attrs), addr)
+
+    def _handle_client(self, data, addr):
+        if 0x40 <= data[0] <= 0x7F:  # ChannelData
+            ch, ln = struct.unpack(">HH", data[:4])
+            a = self.allocs.get(addr)
+            if a and ch in a["chans"]:
+                a["relay"].sendto(data[4:4 + ln], a["chans"][ch])
+                self.stats["relayed_to_peer"] += 1
+            return
+        m = parse(data)
+        if not m:
+            return
+        t, tid, attrs, mi_off = m
+        method = t & 0x3EEF
+        d = dict(attrs)
+        if t == 0x0016:  # Send indication
+            a = self.allocs.get(addr)
+            if a and 0x0012 in d and 0x0013 in d:
+                peer = unxor_addr(d[0x0012])
+                if peer[0] in a["perms"]:
+                    a["relay"].sendto(d[0x0013], peer)
+                    self.stats["relayed_to_peer"] += 1
+            return
+        if t & 0x0110:  # not a request
+            return
+        if method == 0x0001:  # Binding
+            self.sock.sendto(build(0x0101, tid, [(0x0020, xor_addr(*addr))]), addr)
+            return
+        if not self._auth_ok(data, attrs, mi_off):
+            self._err(method, tid, 401, "Unauthorized", addr)
+            return
+        if method == 0x0003:  # Allocate
+            if addr in self.allocs:
+                self._err(method, tid, 437, "Allocation Mismatch", addr)
+                return
+            r = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+            r.bind((self.host, 0))
+            self.allocs[addr] = {"relay": r, "perms": set(), "chans": {}, "peers": {}}
+            self.by_relay[r] = addr
+            self.stats["allocations"] += 1
+            rh, rp = r.getsockname()
+            self.sock.sendto(build(0x0103, tid, [(0x0016, xor_addr(rh, rp)), (0x0020, xor_addr(*addr)),
+                                                  (0x000D, struct.pack(">I", 600))], self.key), addr)
+        elif method == 0x0004:  # Refresh
+            lt = struct.unpack(">I", d.get(0x000D, b"\0\0\x02\x58"))[0]
+            if lt == 0 and addr in self.allocs:
+                a = self.allocs.pop(addr)
+                self.by_relay.pop(a["relay"], None)
+                a["relay"].close()
+            self.sock.sendto(build(0x0104, tid, [(0x000D, struct.pack(">I", lt))], self.key), addr)
+        elif method == 0x0008:  # CreatePermission
+            a = self.allocs.get(addr)
+            if a and 0x0012 in d:
+                a["perms"].add(unxor_addr(d[0x0012])[0])
+            self.sock.sendto(build(0x0108, tid, [], self.key), addr)
+        elif method == 0x0009:  # ChannelBind
+            a = self.allocs.get(addr)
+            ch = struct.unpack(">H", d[0x000C][:2])[0]
+            peer = unxor_addr(d[0x0012])
+            a["chans"][ch] = peer
+            a["peers"][peer] = ch
+            a["perms"].add(peer[0])
+            self.stats["channel_binds"] += 1
+            self.sock.sendto(build(0x0109, tid, [], self.key), addr)
+
+    def _handle_relay(self, r):
+        try:
+            data, peer = r.recvfrom(65536)
+        except OSError:
+            return
+        client = self.by_relay.get(r)
+        a = self.allocs.get(client)
+        if not a or peer[0] not in a["perms"]:
+            return
+        ch = a["peers"].get(peer)
+        if ch:
+            msg = struct.pack(">HH", ch, len(data)) + data + b"\0" * _pad(len(data))
+        else:
+            msg = build(0x0017, os.urandom(12), [(0x0012, xor_addr(*peer)), (0x0013, data)], fingerprint=False)
+        self.sock.sendto(msg, client)
+        self.stats["relayed_to_client"] += 1
+
+    def _run(self):
+        while not self._stop:
+            socks = [self.sock] + list(self.by_relay)
+            try:
+                ready, _, _ = select.select(socks, [], [], 0.1)
+            except (OSError, ValueError):
+                continue
+            for s in ready:
+                if s is self.sock:
+                    try:
+                        data, addr = s.recvfrom(65536)
+                    except OSError:
+                        continue
+                    self._handle_client(data, addr)
+                else:
+                    self._handle_relay(s)
