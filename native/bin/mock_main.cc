@@ -1,0 +1,151 @@
+// `tunnel-mock` — native implementation of the benchmark upstream.
+//
+// Same workload as the reference's tmp/mock_llm.py (and our Python
+// p2p_llm_tunnel_amd/utils/mock_llm.py): GET /v1/models, GET /health,
+// POST /v1/chat/completions with {"stream":true} -> 5 SSE token events written
+// --interval-ms apart (default 100), then a finish_reason:"stop" event and
+// "data: [DONE]"; HTTP/1.0 responses, no Content-Length on SSE, connection
+// closed at the end. Extras: POST /echo, GET /bulk?bytes=N. Written on the
+// reactor so it adds no GIL/thread-scheduling jitter to TTFT measurements.
+#include <signal.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <memory>
+#include <string>
+
+#include "core/net.h"
+#include "core/reactor.h"
+#include "http/http.h"
+
+using namespace p2pt;
+
+namespace {
+
+const char* kTokens[] = {"Hello", " from", " the", " tunnel", "!"};
+
+std::string chunk_event(const char* tok) {
+  std::string delta = tok ? std::string("{\"content\": \"") + tok + "\"}" : "{}";
+  std::string fin = tok ? "null" : "\"stop\"";
+  return "data: {\"id\": \"chatcmpl-test\", \"object\": \"chat.completion.chunk\", \"choices\": [{\"index\": 0, "
+         "\"delta\": " + delta + ", \"finish_reason\": " + fin + "}]}\n\n";
+}
+
+struct Server {
+  Reactor& r;
+  uint64_t interval_ms;
+  int tokens;
+  bool trace;
+  std::map<TcpConn*, std::shared_ptr<TcpConn>> conns;
+
+  void respond(const std::shared_ptr<TcpConn>& c, int status, const std::string& ctype, const std::string& body) {
+    std::string out = "HTTP/1.0 " + std::to_string(status) + " " + http::reason_phrase(status) +
+                      "\r\nServer: p2pt-mock\r\nDate: " + http::http_date_now() + "\r\nContent-Type: " + ctype +
+                      "\r\nContent-Length: " + std::to_string(body.size()) + "\r\n\r\n" + body;
+    c->write(std::move(out));
+    c->close_after_flush();
+  }
+
+  void sse(const std::shared_ptr<TcpConn>& c) {
+    c->write(std::string("HTTP/1.0 200 OK\r\nServer: p2pt-mock\r\nDate: ") + http::http_date_now() +
+             "\r\nContent-Type: text/event-stream\r\nCache-Control: no-cache\r\n\r\n");
+    auto step = std::make_shared<std::function<void(int)>>();
+    std::weak_ptr<TcpConn> w = c;
+    Reactor* rp = &r;
+    uint64_t iv = interval_ms;
+    int n = tokens;
+    *step = [w, rp, iv, n, step](int i) {
+      auto conn = w.lock();
+      if (!conn || conn->closed()) return;
+      if (i < n) {
+        conn->write(chunk_event(i < 5 ? kTokens[i] : " tok"));
+        rp->call_later_ms(iv, [step, i] { (*step)(i + 1); });
+        return;
+      }
+      conn->write(chunk_event(nullptr) + "data: [DONE]\n\n");
+      conn->close_after_flush();
+    };
+    (*step)(0);
+  }
+
+  void handle(const std::shared_ptr<TcpConn>& c, const http::Head& h, const std::string& body) {
+    std::string path = h.target.substr(0, h.target.find('?'));
+    if (h.method == "GET" && (path == "/v1/models" || path == "/models")) {
+      respond(c, 200, "application/json", R"({"object": "list", "data": [{"id": "test-model", "object": "model"}]})");
+    } else if (h.method == "GET" && path == "/health") {
+      respond(c, 200, "text/plain", "ok");
+    } else if (h.method == "GET" && path == "/bulk") {
+      size_t n = 1 << 20;
+      size_t q = h.target.find("bytes=");
+      if (q != std::string::npos) n = size_t(strtoull(h.target.c_str() + q + 6, nullptr, 10));
+      std::string b(n, '\0');
+      for (size_t i = 0; i < n; i++) b[i] = char(i & 0xFF);
+      respond(c, 200, "application/octet-stream", b);
+    } else if (h.method == "POST" && (path == "/v1/chat/completions" || path == "/chat/completions")) {
+      bool stream = body.find("\"stream\": true") != std::string::npos || body.find("\"stream\":true") != std::string::npos;
+      if (stream) sse(c);
+      else
+        respond(c, 200, "application/json",
+                R"({"id": "chatcmpl-test", "object": "chat.completion", "choices": [{"index": 0, "message": {"role": "assistant", "content": "Hello from the tunnel!"}, "finish_reason": "stop"}], "usage": {"prompt_tokens": 10, "completion_tokens": 5, "total_tokens": 15}})");
+    } else if (h.method == "POST" && path == "/echo") {
+      respond(c, 200, "application/octet-stream", body);
+    } else {
+      respond(c, 404, "text/plain", "not found");
+    }
+  }
+
+  void accept(int fd) {
+    auto c = TcpConn::adopt(r, fd);
+    conns[c.get()] = c;
+    auto buf = std::make_shared<std::string>();
+    auto done = std::make_shared<bool>(false);
+    std::weak_ptr<TcpConn> w = c;
+    c->on_data([this, w, buf, done](const uint8_t* p, size_t n) {
+      if (*done) return;
+      buf->append(reinterpret_cast<const char*>(p), n);
+      http::Head h;
+      size_t used = 0;
+      if (http::parse_request_head(*buf, h, used, nullptr) != http::ParseResult::Done) return;
+      uint64_t len = 0;
+      std::string err;
+      http::request_body_mode(h, len, &err);
+      if (buf->size() - used < len) return;
+      *done = true;
+      if (trace) fprintf(stderr, "mock_req %llu\n", static_cast<unsigned long long>(Reactor::now_us()));
+      if (auto s = w.lock()) handle(s, h, buf->substr(used, size_t(len)));
+    });
+    TcpConn* key = c.get();
+    c->on_close([this, key](const std::string&) { r.post([this, key] { conns.erase(key); }); });
+  }
+};
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  std::string listen = "127.0.0.1:3001";
+  uint64_t interval = 100;
+  int tokens = 5;
+  for (int i = 1; i + 1 < argc; i += 2) {
+    std::string a = argv[i];
+    if (a == "--listen") listen = argv[i + 1];
+    else if (a == "--port") listen = "127.0.0.1:" + std::string(argv[i + 1]);
+    else if (a == "--interval-ms") interval = strtoull(argv[i + 1], nullptr, 10);
+    else if (a == "--tokens") tokens = atoi(argv[i + 1]);
+  }
+  signal(SIGPIPE, SIG_IGN);
+  Reactor r;
+  Server s{r, interval, tokens, getenv("MOCK_TRACE") != nullptr, {}};
+  std::string err;
+  auto l = TcpListener::bind(r, listen, [&](int fd, SockAddr) { s.accept(fd); }, &err);
+  if (!l) {
+    fprintf(stderr, "mock: %s\n", err.c_str());
+    return 1;
+  }
+  printf("Mock LLM server running on %s\n", l->local_addr().str().c_str());
+  fflush(stdout);
+  r.on_signal(SIGINT, [&] { r.stop(); });
+  r.on_signal(SIGTERM, [&] { r.stop(); });
+  r.run();
+  return 0;
+}

@@ -76,6 +76,10 @@ const std::vector<Opt>& ext_opts() {
       {"handshake-timeout-ms", "TUNNEL_HANDSHAKE_TIMEOUT_MS", "300000", "HELLO/AGREE timeout"},
       {"listen-early", nullptr, nullptr, "proxy: bind before the tunnel is up and answer 503 until ready", true},
       {"metrics-listen", "TUNNEL_METRICS_LISTEN", "", "Serve Prometheus metrics on HOST:PORT"},
+      {"busy-poll-us", "TUNNEL_BUSY_POLL_US", "0",
+       "Keep polling for N us after I/O instead of sleeping (lower per-hop latency, more CPU)"},
+      {"upstream-prewarm", "TUNNEL_UPSTREAM_PREWARM", "4",
+       "serve: spare pre-connected upstream sockets (follows peak concurrency; 0=off)"},
   };
   return o;
 }
@@ -233,6 +237,8 @@ int main(int argc, char** argv) {
   cfg.handshake_timeout_ms = num(m, "handshake-timeout-ms");
   cfg.listen_early = m.count("listen-early") > 0;
   cfg.metrics_listen = m["metrics-listen"];
+  cfg.upstream_prewarm = num(m, "upstream-prewarm");
+  cfg.busy_poll_us = num(m, "busy-poll-us");
 
   if (cmd == "serve") {
     LOG_INFO("tunnel", "starting serve mode: signal=%s, room=%s, upstream=%s, advertise=%s", cfg.signal.c_str(),

@@ -321,13 +321,19 @@ void TcpConn::write(Bytes b) {
   if (fd_ < 0 || b.empty()) return;
   out_bytes_ += b.size();
   out_.push_back(std::move(b));
-  if (out_.size() == 1 && !handshaking_) {
-    // Fast path: try immediately. Errors are reported asynchronously so that
-    // the caller never sees its close callback re-enter write().
-    in_write_ = true;
-    do_write();
-    in_write_ = false;
-  } else {
+  // Writes issued while handling one reactor batch are coalesced into a single
+  // writev at the end of the batch (e.g. chunk header + payload + CRLF of a
+  // relayed SSE event go out as one syscall / one TCP segment).
+  if (!write_scheduled_ && !handshaking_ && out_.size() == 1) {
+    write_scheduled_ = true;
+    std::weak_ptr<TcpConn> w = shared_from_this();
+    r_.post([w] {
+      if (auto s = w.lock()) {
+        s->write_scheduled_ = false;
+        s->do_write();
+      }
+    });
+  } else if (!write_scheduled_) {
     update_interest();
   }
   if (low_water_ && out_bytes_ > low_water_) above_low_ = true;

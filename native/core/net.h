@@ -121,6 +121,7 @@ class TcpConn : public std::enable_shared_from_this<TcpConn> {
   bool paused_ = false;
   bool close_after_flush_ = false;
   bool in_write_ = false;
+  bool write_scheduled_ = false;
   std::deque<Bytes> out_;
   size_t out_off_ = 0;
   size_t out_bytes_ = 0;

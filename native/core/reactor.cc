@@ -181,8 +181,10 @@ void Reactor::run_flush() {
 
 void Reactor::run_once(int timeout_ms) {
   epoll_event evs[256];
+  if (busy_poll_us_ && timeout_ms > 0 && now_us() - last_io_us_ < busy_poll_us_) timeout_ms = 0;
   int n = epoll_wait(epfd_, evs, 256, timeout_ms);
   if (n < 0 && errno != EINTR) throw std::runtime_error(std::string("epoll_wait: ") + strerror(errno));
+  if (n > 0 && busy_poll_us_) last_io_us_ = now_us();
   for (int i = 0; i < n; i++) {
     uint64_t tag = evs[i].data.u64;
     if (tag == kWakeTag) {

@@ -4,7 +4,13 @@
 
 namespace p2pt::http {
 
-class ClientConnPool {
+// Keep-alive pool plus "warm" connections: fresh, already-established
+// sockets to the upstream origin opened ahead of demand. HTTP/1.0 upstreams
+// (the reference's mock, many simple servers) close after every response, so
+// keep-alive never helps them; a warm socket takes the TCP (and TLS)
+// handshake off every request's time-to-first-token. The warm target follows
+// the recent peak of concurrent requests (>= the configured minimum).
+class ClientConnPool : public std::enable_shared_from_this<ClientConnPool> {
  public:
   explicit ClientConnPool(Reactor& r) : r_(r) {}
   std::shared_ptr<TcpConn> take(const std::string& key) {
@@ -15,6 +21,130 @@ class ClientConnPool {
       if (!c->closed()) return c;
     }
     return nullptr;
+  }
+
+  struct Warm {
+    std::string host;
+    uint16_t port = 0;
+    bool tls = false;
+    size_t min = 0, max = 64;
+    size_t peak = 0;          // recent peak of in-flight requests
+    uint64_t peak_at_ms = 0;
+    size_t inflight = 0;
+    size_t connecting = 0;
+    int failures = 0;
+    uint64_t retry_timer = 0;
+    std::vector<std::shared_ptr<TcpConn>> ready;
+  };
+
+  void configure_warm(const std::string& key, const std::string& host, uint16_t port, bool tls, size_t min) {
+    Warm& w = warm_[key];
+    w.host = host;
+    w.port = port;
+    w.tls = tls;
+    w.min = min;
+    replenish(key);
+  }
+  bool has_warm(const std::string& key) const { return warm_.count(key) != 0; }
+
+  std::shared_ptr<TcpConn> take_warm(const std::string& key) {
+    auto it = warm_.find(key);
+    if (it == warm_.end()) return nullptr;
+    auto& v = it->second.ready;
+    std::shared_ptr<TcpConn> c;
+    while (!v.empty()) {
+      c = v.back();
+      v.pop_back();
+      if (!c->closed()) break;
+      c.reset();
+    }
+    if (c) {
+      c->on_data(nullptr);
+      c->on_close(nullptr);
+    }
+    return c;
+  }
+
+  void call_started(const std::string& key) {
+    auto it = warm_.find(key);
+    if (it == warm_.end()) return;
+    Warm& w = it->second;
+    w.inflight++;
+    uint64_t now = Reactor::now_ms();
+    if (w.inflight >= w.peak || now - w.peak_at_ms > 30000) {
+      w.peak = w.inflight;
+      w.peak_at_ms = now;
+    }
+    replenish(key);
+  }
+  void call_finished(const std::string& key) {
+    auto it = warm_.find(key);
+    if (it != warm_.end() && it->second.inflight) it->second.inflight--;
+  }
+
+  void replenish(const std::string& key) {
+    auto it = warm_.find(key);
+    if (it == warm_.end()) return;
+    Warm& w = it->second;
+    if (w.retry_timer) return;  // backing off after connect failures
+    size_t target = std::min(w.max, std::max(w.min, w.peak));
+    std::weak_ptr<ClientConnPool> self = shared_from_this();
+    while (w.ready.size() + w.connecting < target) {
+      w.connecting++;
+      TcpConn::connect(r_, w.host, w.port, w.tls, [self, key](std::shared_ptr<TcpConn> c, std::string err) {
+        auto p = self.lock();
+        if (!p) {
+          if (c) c->close();
+          return;
+        }
+        auto it2 = p->warm_.find(key);
+        if (it2 == p->warm_.end()) {
+          if (c) c->close();
+          return;
+        }
+        Warm& w2 = it2->second;
+        w2.connecting--;
+        if (!c) {
+          // Upstream down: back off (it is also reported per request as 502).
+          w2.failures++;
+          uint64_t delay = std::min<uint64_t>(100ull << std::min(w2.failures, 6), 5000);
+          w2.retry_timer = p->r_.call_later_ms(delay, [self, key] {
+            auto p2 = self.lock();
+            if (!p2) return;
+            auto it3 = p2->warm_.find(key);
+            if (it3 == p2->warm_.end()) return;
+            it3->second.retry_timer = 0;
+            p2->replenish(key);
+          });
+          return;
+        }
+        w2.failures = 0;
+        std::weak_ptr<TcpConn> wc = c;
+        // A warm socket that turns readable/closed was dropped by the server
+        // (idle timeout): discard it and top up again.
+        auto drop = [self, key, wc] {
+          auto p2 = self.lock();
+          auto conn = wc.lock();
+          if (!p2 || !conn) return;
+          auto it3 = p2->warm_.find(key);
+          if (it3 == p2->warm_.end()) return;
+          auto& v = it3->second.ready;
+          for (size_t i = 0; i < v.size(); i++)
+            if (v[i] == conn) {
+              v.erase(v.begin() + long(i));
+              break;
+            }
+          conn->on_close(nullptr);
+          conn->close();
+          p2->r_.post([self, key] {
+            if (auto p3 = self.lock()) p3->replenish(key);
+          });
+        };
+        c->on_data([drop](const uint8_t*, size_t) { drop(); });
+        c->on_close([drop](const std::string&) { drop(); });
+        w2.ready.push_back(std::move(c));
+      });
+    }
   }
   void put(const std::string& key, std::shared_ptr<TcpConn> c) {
     if (c->closed()) return;
@@ -56,16 +186,47 @@ class ClientConnPool {
         c->on_close(nullptr);
         c->close();
       }
+    auto warm = std::move(warm_);
+    warm_.clear();
+    for (auto& kv : warm) {
+      if (kv.second.retry_timer) r_.cancel(kv.second.retry_timer);
+      for (auto& c : kv.second.ready) {
+        c->on_close(nullptr);
+        c->close();
+      }
+    }
+  }
+  size_t warm_ready(const std::string& key) const {
+    auto it = warm_.find(key);
+    return it == warm_.end() ? 0 : it->second.ready.size();
   }
   Reactor& r_;
 
  private:
   std::map<std::string, std::vector<std::shared_ptr<TcpConn>>> idle_;
+  std::map<std::string, Warm> warm_;
 };
 
 HttpClient::HttpClient(Reactor& r) : r_(r), pool_(std::make_shared<ClientConnPool>(r)) {}
 HttpClient::~HttpClient() { pool_->clear(); }
 size_t HttpClient::idle_connections() const { return pool_->idle(); }
+
+bool HttpClient::prewarm(const std::string& url, size_t min_ready, std::string* err) {
+  Url u;
+  if (!parse_url(url, u, err)) return false;
+  if (u.scheme != "http" && u.scheme != "https") {
+    if (err) *err = "unsupported scheme";
+    return false;
+  }
+  pool_->configure_warm(u.scheme + "://" + u.host + ":" + std::to_string(u.port), u.host, u.port, u.tls(), min_ready);
+  return true;
+}
+
+size_t HttpClient::warm_connections(const std::string& url) const {
+  Url u;
+  if (!parse_url(url, u, nullptr)) return 0;
+  return pool_->warm_ready(u.scheme + "://" + u.host + ":" + std::to_string(u.port));
+}
 
 std::shared_ptr<ClientCall> HttpClient::request(ClientRequest req, ClientCallbacks cb) {
   auto call = std::shared_ptr<ClientCall>(new ClientCall());
@@ -103,7 +264,15 @@ void ClientCall::start() {
   }
   live_calls()[this] = shared_from_this();
   pool_key_ = url_.scheme + "://" + url_.host + ":" + std::to_string(url_.port);
+  pool_->call_started(pool_key_);
+  counted_ = true;
   if (auto c = pool_->take(pool_key_)) {
+    attach(c, true);
+    return;
+  }
+  // A warm socket may have been closed by the server an instant ago; it is
+  // treated like a reused keep-alive socket (one transparent retry).
+  if (auto c = pool_->take_warm(pool_key_)) {
     attach(c, true);
     return;
   }
@@ -151,9 +320,16 @@ void ClientCall::attach(std::shared_ptr<TcpConn> c, bool reused) {
   if (!has_accept) head += "accept: */*\r\n";
   if (req_.body_len > 0 || req_.force_content_length) head += "content-length: " + std::to_string(req_.body_len) + "\r\n";
   head += "\r\n";
-  conn_->write(std::move(head));
-  for (auto& b : req_.body) conn_->write(b);
+  // Small bodies ride in the same segment as the head.
+  if (req_.body_len <= 16384) {
+    for (auto& b : req_.body) head.append(reinterpret_cast<const char*>(b.data()), b.size());
+    conn_->write(std::move(head));
+  } else {
+    conn_->write(std::move(head));
+    for (auto& b : req_.body) conn_->write(b);
+  }
   if (paused_) conn_->pause_reading();
+  if (cb_.on_sent) cb_.on_sent(reused);
 }
 
 void ClientCall::on_data(const uint8_t* p, size_t n) {
@@ -254,6 +430,10 @@ void ClientCall::finish(const std::string& err) {
   if (finished_) return;
   finished_ = true;
   auto self = shared_from_this();
+  if (counted_) {
+    counted_ = false;
+    pool_->call_finished(pool_key_);
+  }
   if (conn_) {
     auto c = std::move(conn_);
     conn_.reset();

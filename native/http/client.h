@@ -30,6 +30,8 @@ struct ClientRequest {
 };
 
 struct ClientCallbacks {
+  // Request bytes handed to the socket (connection established or reused).
+  std::function<void(bool reused)> on_sent;
   std::function<void(const Head&)> on_head;
   std::function<void(const uint8_t*, size_t)> on_data;
   // err empty => complete body received. `before_head` tells whether any
@@ -69,6 +71,7 @@ class ClientCall : public std::enable_shared_from_this<ClientCall> {
   bool finished_ = false;
   bool paused_ = false;
   bool keep_alive_ = false;
+  bool counted_ = false;
   Head head_;
   BodyDecoder body_;
   std::string buf_;
@@ -83,6 +86,10 @@ class HttpClient {
   // handle may be dropped (the call keeps itself alive until done).
   std::shared_ptr<ClientCall> request(ClientRequest req, ClientCallbacks cb);
   size_t idle_connections() const;
+  // Keep >= min_ready established spare connections to url's origin (grows to
+  // the recent peak concurrency, max 64). 0 disables.
+  bool prewarm(const std::string& url, size_t min_ready, std::string* err = nullptr);
+  size_t warm_connections(const std::string& url) const;
 
  private:
   Reactor& r_;

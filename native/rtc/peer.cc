@@ -275,6 +275,7 @@ void PeerConnection::start_sctp() {
   if (jumbo) dtls_->set_record_limit(mtu_);
   SctpConfig sc;
   sc.mtu = mtu_;
+  sc.sack_delay_us = cfg_.sack_delay_us;
   sc.remote_port = remote_.sctp_port;
   if (jumbo) sc.initial_cwnd = cfg_.jumbo_initial_cwnd;
   std::weak_ptr<PeerConnection> w = shared_from_this();

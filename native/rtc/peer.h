@@ -36,6 +36,10 @@ struct PcConfig {
   bool allow_jumbo = true;   // advertise/use large SCTP packets on same-host paths
   size_t jumbo_mtu = 16000;
   size_t jumbo_initial_cwnd = 1 << 20;
+  // Delayed-SACK window for lone packets. Worth it on the side that usually
+  // answers what it receives (serve: a request's SACK rides on its response);
+  // 0 on the side that mostly receives streams (proxy).
+  uint64_t sack_delay_us = 0;
 };
 
 class PeerConnection;

@@ -96,6 +96,7 @@ SctpAssociation::SctpAssociation(Reactor& r, SctpConfig cfg, PacketOut out) : r_
 }
 
 SctpAssociation::~SctpAssociation() {
+  if (sack_timer_) r_.cancel(sack_timer_);
   if (t3_timer_) r_.cancel(t3_timer_);
   if (init_timer_) r_.cancel(init_timer_);
   for (auto* c : inflight_) delete c;
@@ -236,6 +237,14 @@ void SctpAssociation::on_packet(const uint8_t* p, size_t n) {
   auto self = shared_from_this();
   size_t off = kCommonHdr;
   bool first = true;
+  uint64_t data_before = stats_.data_chunks_received;
+  struct CountPkt {
+    SctpAssociation* s;
+    uint64_t before;
+    ~CountPkt() {
+      if (s->stats_.data_chunks_received != before) s->data_pkts_unacked_++;
+    }
+  } count_pkt{this, data_before};
   while (off + 4 <= n && !closed_fired_) {
     uint8_t type = p[off], flags = p[off + 1];
     size_t clen = rd16(p + off + 2);
@@ -761,8 +770,34 @@ void SctpAssociation::flush() {
     if (pkt.size() + ch.size() > mtu) flush_pkt();
     pkt.insert(pkt.end(), ch.begin(), ch.end());
   };
-  // SACK first (RFC 9260 §6.1: SACK goes before DATA when bundled).
-  if (sack_needed_ && have_peer_tsn_ && peer_vtag_) {
+  // SACK policy: immediate when >= 2 data packets are unacknowledged, on
+  // gaps/duplicates, or when DATA goes out now anyway (piggyback); otherwise
+  // delayed by sack_delay_us so a lone request frame is acknowledged by the
+  // response that follows instead of by a pure SACK (one less wakeup per
+  // request on each side). RFC 9260 §6.2 allows up to 500 ms.
+  bool data_ready = can_data && !sendq_.empty();
+  if (can_data && !data_ready)
+    for (Chunk* ch : inflight_)
+      if (ch->retransmit) {
+        data_ready = true;
+        break;
+      }
+  bool sack_now = sack_needed_ && (sack_urgent_ || data_pkts_unacked_ >= 2 || data_ready || cfg_.sack_delay_us == 0 ||
+                                   !ooo_.empty() || !dups_.empty());
+  if (sack_needed_ && !sack_now && !sack_timer_) {
+    std::weak_ptr<SctpAssociation> w = shared_from_this();
+    sack_timer_ = r_.call_later_us(cfg_.sack_delay_us, [w] {
+      if (auto s = w.lock()) {
+        s->sack_timer_ = 0;
+        s->sack_urgent_ = true;  // flushed at the end of this reactor iteration
+      }
+    });
+  }
+  if (sack_now && have_peer_tsn_ && peer_vtag_) {
+    if (sack_timer_) r_.cancel(sack_timer_);
+    sack_timer_ = 0;
+    sack_urgent_ = false;
+    data_pkts_unacked_ = 0;
     std::vector<uint8_t> b;
     build_sack(b);
     std::vector<uint8_t> ch;

@@ -41,6 +41,7 @@ struct SctpConfig {
   uint64_t rto_max_ms = 10000;
   int max_init_retrans = 8;
   int max_assoc_retrans = 20;
+  uint64_t sack_delay_us = 5000;    // delayed SACK for lone packets (0 = always immediate)
 };
 
 struct SctpStats {
@@ -164,6 +165,9 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   size_t ooo_bytes_ = 0;
   std::vector<uint32_t> dups_;
   bool sack_needed_ = false;
+  bool sack_urgent_ = false;
+  int data_pkts_unacked_ = 0;
+  uint64_t sack_timer_ = 0;
   struct Partial {
     uint32_t ppid = 0;
     std::vector<uint8_t> data;

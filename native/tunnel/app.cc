@@ -143,6 +143,7 @@ std::shared_ptr<void> connect_transport(Reactor& r, const AppConfig& cfg, Connec
 
 int run_app(const AppConfig& cfg) {
   Reactor r;
+  r.set_busy_poll_us(cfg.busy_poll_us);
   struct State {
     uint64_t attempt = 0;
     std::shared_ptr<void> transport;
@@ -230,6 +231,7 @@ int run_app(const AppConfig& cfg) {
         sc.handshake_timeout_ms = cfg.handshake_timeout_ms;
         sc.ping_interval_ms = cfg.ping_interval_ms;
         sc.pong_timeout_ms = cfg.pong_timeout_ms;
+        sc.upstream_prewarm = cfg.upstream_prewarm;
         st.serve = ServeSession::start(r, ch, sc, [&](const std::string& e) { on_fail(e); });
       } else {
         LOG_INFO(kT, "WebRTC connected, starting proxy...");

@@ -56,6 +56,8 @@ struct AppConfig {
   uint64_t handshake_timeout_ms = 300000;
   bool listen_early = false;
   std::string metrics_listen;
+  size_t upstream_prewarm = 4;
+  uint64_t busy_poll_us = 0;
 };
 
 // Establishes one MessageChannel (signalling + WebRTC, or a TCP debug link).

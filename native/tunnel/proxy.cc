@@ -566,6 +566,7 @@ void ProxySession::accept(int fd) {
     ::close(fd);
     return;
   }
+  trace::event("proxy", uint32_t(fd), "tcp_accept");
   auto tc = TcpConn::adopt(r_, fd);
   auto pc = std::make_shared<ProxyConn>(weak_from_this(), tc);
   conns_[pc.get()] = pc;

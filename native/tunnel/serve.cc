@@ -133,6 +133,11 @@ void ServeSession::on_hello(const proto::Frame& f) {
   sched_->send(proto::make_agree(agree));
   handshaken_ = true;
   LOG_INFO(kT, "sent AGREE, tunnel ready");
+  if (cfg_.upstream_prewarm) {
+    std::string perr;
+    if (!client_.prewarm(cfg_.upstream, cfg_.upstream_prewarm, &perr))
+      LOG_DEBUG(kT, "upstream prewarm disabled: %s", perr.c_str());
+  }
   last_pong_ms_ = Reactor::now_ms();
   send_ping();  // tokio::time::interval's first tick is immediate
 }
@@ -265,6 +270,7 @@ void ServeSession::start_request(uint32_t sid, Pending p) {
   std::weak_ptr<ServeSession> w = shared_from_this();
   metrics::counter_add("tunnel_upstream_requests_total");
   http::ClientCallbacks cb;
+  cb.on_sent = [sid](bool) { trace::event("serve", sid, "upstream_sent"); };
   cb.on_head = [w, sid](const http::Head& h) {
     auto s = w.lock();
     if (!s || s->stopped_) return;

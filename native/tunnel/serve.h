@@ -36,6 +36,8 @@ struct ServeConfig {
   uint64_t pong_timeout_ms = 0;  // 0 = reference behaviour (PONG only logged)
   size_t high_water = 4 << 20;
   size_t low_water = 1 << 20;
+  // Spare pre-connected upstream sockets (0 = connect per request like reqwest).
+  size_t upstream_prewarm = 4;
 };
 
 class ServeSession : public std::enable_shared_from_this<ServeSession> {

@@ -70,6 +70,7 @@ class WebrtcSession : public std::enable_shared_from_this<WebrtcSession> {
     pc.ice.failed_ms = cfg_.rtc.ice_failed_timeout_ms;
     pc.sctp_mtu = cfg_.rtc.sctp_mtu;
     pc.allow_jumbo = cfg_.rtc.allow_jumbo_loopback;
+    pc.sack_delay_us = cfg_.mode == "serve" ? 5000 : 0;
     return pc;
   }
 
