@@ -2,25 +2,30 @@
 """Headline benchmark: tunneled req/s + added p50 TTFT vs direct, mock-LLM SSE
 at 1/2/4/8 multiplexed streams (BASELINE.json "metric").
 
-Per rank (one rank per GPU of the node, launched by torch.distributed.run for
-N > 1): a mock OpenAI upstream (reference tmp/mock_llm.py workload: 5 SSE
-tokens 100 ms apart; threaded so concurrency is not capped by the mock),
-the local signal server, ``tunnel serve`` and ``tunnel proxy`` (native C++,
-WebRTC data channel over loopback by default). A *step* is one streamed
-completion on each of S concurrent keep-alive client connections (S = 8 for
-the headline; the 1/2/4 points are measured too and reported in "curve").
-``value`` is the whole-job aggregate tunneled requests/s over all ranks
-(weak scaling: every rank runs its own tunnel with S streams).
+Per rank (one rank per GPU of the node; torch.distributed.run launches N > 1):
+a mock OpenAI upstream serving the reference workload (tmp/mock_llm.py: 5 SSE
+tokens 100 ms apart, then a stop event and [DONE]; HTTP/1.0, no
+Content-Length), the local signal server, ``tunnel serve`` and ``tunnel proxy``
+(native C++; WebRTC data channel over the host's interfaces by default).
+A *step* = one streamed completion on each of S concurrent keep-alive client
+connections (S = 8 for the headline). ``value`` = whole-job tunneled
+requests/s over all ranks (weak scaling: every rank runs its own tunnel).
+
+The upstream and the client are native by default (``tunnel-mock``,
+``tunnel-loadgen``) so the TTFT numbers measure the tunnel rather than
+CPython; ``--mock python`` uses the Python mock instead. The untimed tail
+measures the 1/2/4-stream points and the direct (untunneled) baseline that
+"added TTFT" is computed against.
 
 The tunnel has no GPU compute: the measured path is
-host-side networking on the MI355X node, so "dtype" is reported as n/a.
+host-side networking on the MI355X node, so "dtype" is n/a.
 """
 from __future__ import annotations
 
 import argparse
-import asyncio
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -36,12 +41,12 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--streams", type=int, default=8, help="concurrent streams per rank for the headline")
-    ap.add_argument("--curve", default="1,2,4", help="extra stream counts measured for the scaling curve")
+    ap.add_argument("--curve", default="1,2,4", help="extra stream counts measured (untimed) for the curve")
     ap.add_argument("--curve-steps", type=int, default=3)
     ap.add_argument("--transport", default=os.environ.get("BENCH_TRANSPORT", "webrtc"))
+    ap.add_argument("--mock", choices=["native", "python"], default="native")
     ap.add_argument("--interval-ms", type=float, default=100.0)
-    ap.add_argument("--tokens", type=int, default=None)
-    ap.add_argument("--unthreaded-mock", action="store_true")
+    ap.add_argument("--tokens", type=int, default=5)
     ap.add_argument("--out", default=None, help="also write the JSON line here")
     return ap.parse_args()
 
@@ -66,11 +71,33 @@ def sync_device():
         pass
 
 
+def start_mock(kind, interval_ms, tokens):
+    from p2p_llm_tunnel_amd import binary
+    from p2p_llm_tunnel_amd.utils.procs import free_port, spawn
+    port = free_port()
+    if kind == "native":
+        p = spawn("mock", [binary("tunnel-mock"), "--port", str(port), "--interval-ms", str(int(interval_ms)),
+                           "--tokens", str(tokens)])
+    else:
+        p = spawn("mock", [sys.executable, "-m", "p2p_llm_tunnel_amd.utils.mock_llm", "--port", str(port),
+                           "--threaded", "--interval-ms", str(interval_ms), "--tokens", str(tokens)])
+    p.wait_for("Mock LLM server running", 30)
+    return p, port
+
+
+def loadgen(port, streams, steps, warmup=0):
+    from p2p_llm_tunnel_amd import binary
+    out = subprocess.run([binary("tunnel-loadgen"), "--target", f"127.0.0.1:{port}", "--streams", str(streams),
+                          "--steps", str(steps), "--warmup", str(warmup)], capture_output=True, text=True, timeout=600)
+    try:
+        return json.loads(out.stdout.strip().splitlines()[-1])
+    except (IndexError, ValueError):
+        raise RuntimeError(f"loadgen failed (rc={out.returncode}): {out.stdout[-500:]} {out.stderr[-500:]}")
+
+
 def main():
     a = parse()
     dist, rank, world = dist_init()
-    from p2p_llm_tunnel_amd.parallel.loadgen import run_steps, summarize
-    from p2p_llm_tunnel_amd.utils import mock_llm
     from p2p_llm_tunnel_amd.utils.build import ensure_native
     from p2p_llm_tunnel_amd.utils.procs import Tunnel
 
@@ -79,73 +106,63 @@ def main():
     if dist:
         dist.barrier()
 
-    srv, up_port = mock_llm.start_in_thread(threaded=not a.unthreaded_mock, tokens=a.tokens,
-                                            interval_ms=a.interval_ms)
+    mock, up_port = start_mock(a.mock, a.interval_ms, a.tokens)
     tun = Tunnel(f"http://127.0.0.1:{up_port}", transport=a.transport,
-                 env={"RUST_LOG": "warn,tunnel::serve=info,tunnel::proxy=info,tunnel::transport=info"})
+                 env={"RUST_LOG": "warn,tunnel::serve=info,tunnel::proxy=info,tunnel::transport=info,tunnel::rtc=info"})
     tun.start(timeout=60)
-    loop = asyncio.new_event_loop()
-
-    def run(port, streams, steps):
-        return loop.run_until_complete(run_steps("127.0.0.1", port, streams, steps))
 
     def barrier():
         if dist:
             dist.barrier()
 
-    # Warmup (untimed): connections, SCTP cwnd, pools.
+    # Warmup (untimed): connections, SCTP cwnd, upstream prewarm pool.
     if a.warmup:
-        run(tun.proxy_port, a.streams, a.warmup)
+        loadgen(tun.proxy_port, a.streams, a.warmup)
 
-    # ---- headline: timed K steps at S streams
+    # ---- headline: exactly K timed steps at S streams per rank
     barrier()
     sync_device()
     t0 = time.perf_counter()
-    dt_local, stats = run(tun.proxy_port, a.streams, a.steps)
+    head = loadgen(tun.proxy_port, a.streams, a.steps)
     barrier()
     sync_device()
     dt_wall = time.perf_counter() - t0
-    head = summarize(stats)
 
-    # ---- untimed extras: curve points and the direct (untunneled) baseline
+    # ---- untimed: curve points + direct baseline (same upstream, no tunnel)
     curve = {}
     for s in sorted({int(x) for x in a.curve.split(",") if x} | {a.streams}):
-        if s == a.streams:
-            tun_sum, tun_dt = head, dt_local
-        else:
-            tun_dt, st_ = run(tun.proxy_port, s, a.curve_steps)
-            tun_sum = summarize(st_)
-        d_dt, d_st = run(up_port, s, a.curve_steps)
-        d_sum = summarize(d_st)
+        tun_r = head if s == a.streams else loadgen(tun.proxy_port, s, a.curve_steps, warmup=1)
+        dir_r = loadgen(up_port, s, a.curve_steps, warmup=1)
         curve[str(s)] = {
-            "tunneled_req_s": tun_sum["requests"] / tun_dt if s != a.streams else head["requests"] / dt_local,
-            "direct_req_s": d_sum["requests"] / d_dt,
-            "tunneled_p50_ttft_ms": tun_sum["p50_ttft_ms"],
-            "direct_p50_ttft_ms": d_sum["p50_ttft_ms"],
-            "added_p50_ttft_ms": tun_sum["p50_ttft_ms"] - d_sum["p50_ttft_ms"],
-            "tunneled_p99_ttft_ms": tun_sum["p99_ttft_ms"],
-            "errors": tun_sum["errors"],
+            "tunneled_req_s": tun_r["req_s"],
+            "direct_req_s": dir_r["req_s"],
+            "tunneled_p50_ttft_ms": tun_r["p50_ttft_ms"],
+            "direct_p50_ttft_ms": dir_r["p50_ttft_ms"],
+            "added_p50_ttft_ms": tun_r["p50_ttft_ms"] - dir_r["p50_ttft_ms"],
+            "tunneled_p99_ttft_ms": tun_r["p99_ttft_ms"],
+            "direct_p99_ttft_ms": dir_r["p99_ttft_ms"],
+            "errors": tun_r["errors"],
         }
 
+    path = ""
+    for line in tun.serve.lines:
+        if "WebRTC connection established" in line:
+            path = line.split(" via ", 1)[-1]
     tun.stop()
-    srv.shutdown()
+    mock.stop()
 
     requests = head["requests"]
     errors = head["errors"]
     dt = dt_wall
+    added = curve[str(a.streams)]["added_p50_ttft_ms"]
     if dist:
         import torch
-        t = torch.tensor([dt], dtype=torch.float64)
+        t = torch.tensor([dt, added], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        dt, added = float(t[0].item()), float(t[1].item())
         r = torch.tensor([requests, errors], dtype=torch.float64)
         dist.all_reduce(r, op=dist.ReduceOp.SUM)
         requests, errors = int(r[0].item()), int(r[1].item())
-        added = torch.tensor([curve[str(a.streams)]["added_p50_ttft_ms"]], dtype=torch.float64)
-        dist.all_reduce(added, op=dist.ReduceOp.MAX)
-        added_max = float(added.item())
-    else:
-        added_max = curve[str(a.streams)]["added_p50_ttft_ms"]
 
     if rank == 0:
         out = {
@@ -160,16 +177,17 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "n/a",
-            "data": "synthetic: mock-LLM SSE upstream (5 tokens, %g ms apart, %s), no network/datasets" % (
-                a.interval_ms, "unthreaded" if a.unthreaded_mock else "threaded"),
+            "data": f"synthetic: mock-LLM SSE upstream ({a.mock}; {a.tokens} tokens, {a.interval_ms:g} ms apart), "
+                    "no network/datasets",
             "config": {
                 "model": "mock-llm-sse (reference tmp/mock_llm.py workload)",
                 "global_batch": a.streams * world,
-                "seq_len": len(mock_llm.TOKENS) if a.tokens is None else a.tokens,
+                "seq_len": a.tokens,
                 "parallelism": f"{world} tunnel(s) x {a.streams} multiplexed streams",
                 "transport": a.transport,
+                "path_rank0": path,
             },
-            "added_p50_ttft_ms": added_max,
+            "added_p50_ttft_ms": added,
             "p50_ttft_ms": head["p50_ttft_ms"],
             "p99_ttft_ms": head["p99_ttft_ms"],
             "errors": errors,

@@ -1,0 +1,131 @@
+#!/usr/bin/env python3
+"""Benchmark matrix for BASELINE.md (SURVEY §4.2 "Bench", BASELINE.json configs).
+
+  1. SSE streaming, 1/2/4/8 streams: tunneled vs direct req/s and TTFT, for the
+     native mock, the threaded Python mock, and the reference's unthreaded
+     (single-threaded, HTTP/1.0) Python mock; WebRTC and TCP transports.
+  2. 64 concurrent streams x 1 MB POST bodies (REQ_BODY chunking + back-pressure).
+  3. Idle then burst: the tunnel sits idle (PING/PONG keepalive running), then
+     16 concurrent streams (the 30-minute idle of config #5 is scaled down via
+     --idle-s; keepalive behaviour is identical for any idle length).
+
+Writes a JSON document (default: stdout) with every measured point.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT))
+
+from bench import loadgen, start_mock  # noqa: E402
+from p2p_llm_tunnel_amd.utils.build import ensure_native  # noqa: E402
+from p2p_llm_tunnel_amd.utils.procs import Tunnel  # noqa: E402
+
+
+def sse_matrix(transport, mock_kind, streams_list, steps, threaded=True):
+    mock, port = start_mock(mock_kind, 100, 5) if (mock_kind == "native" or threaded) else _unthreaded()
+    rows = []
+    try:
+        with Tunnel(f"http://127.0.0.1:{port}", transport=transport) as t:
+            for s in streams_list:
+                loadgen(t.proxy_port, s, 1)
+                tr = loadgen(t.proxy_port, s, steps)
+                dr = loadgen(port, s, steps)
+                rows.append({"transport": transport, "mock": mock_kind if threaded else "python-unthreaded",
+                             "streams": s, "tunneled_req_s": tr["req_s"], "direct_req_s": dr["req_s"],
+                             "tunneled_p50_ttft_ms": tr["p50_ttft_ms"], "direct_p50_ttft_ms": dr["p50_ttft_ms"],
+                             "added_p50_ttft_ms": tr["p50_ttft_ms"] - dr["p50_ttft_ms"],
+                             "tunneled_p99_ttft_ms": tr["p99_ttft_ms"], "errors": tr["errors"] + dr["errors"]})
+                print(json.dumps(rows[-1]), file=sys.stderr, flush=True)
+    finally:
+        mock.stop()
+    return rows
+
+
+def _unthreaded():
+    from p2p_llm_tunnel_amd.utils.procs import free_port, spawn
+    port = free_port()
+    p = spawn("mock", [sys.executable, "-m", "p2p_llm_tunnel_amd.utils.mock_llm", "--port", str(port)])
+    p.wait_for("Mock LLM server running", 30)
+    return p, port
+
+
+def post_1mb(transport, streams=64, mb=1, steps=2):
+    mock, port = start_mock("native", 100, 5)
+    try:
+        with Tunnel(f"http://127.0.0.1:{port}", transport=transport) as t:
+            from p2p_llm_tunnel_amd import binary
+            import subprocess
+            def run(target):
+                out = subprocess.run([binary("tunnel-loadgen"), "--target", f"127.0.0.1:{target}", "--streams",
+                                      str(streams), "--steps", str(steps), "--warmup", "1", "--post-bytes",
+                                      str(mb << 20)], capture_output=True, text=True, timeout=600)
+                return json.loads(out.stdout.strip().splitlines()[-1])
+            tr, dr = run(t.proxy_port), run(port)
+            # request + echoed response both cross the tunnel
+            row = {"transport": transport, "streams": streams, "body_mb": mb,
+                   "tunneled_req_s": tr["req_s"], "direct_req_s": dr["req_s"],
+                   "tunneled_MBps_each_way": tr["req_s"] * mb * 1.048576,
+                   "tunneled_p50_total_ms": tr["p50_total_ms"], "direct_p50_total_ms": dr["p50_total_ms"],
+                   "errors": tr["errors"] + dr["errors"]}
+            print(json.dumps(row), file=sys.stderr, flush=True)
+            return row
+    finally:
+        mock.stop()
+
+
+def idle_burst(transport, idle_s=30, burst=16):
+    mock, port = start_mock("native", 100, 5)
+    try:
+        with Tunnel(f"http://127.0.0.1:{port}", transport=transport,
+                    env={"RUST_LOG": "info,tunnel::serve=debug"}) as t:
+            loadgen(t.proxy_port, 1, 1)
+            pings0 = t.serve.count("sent keepalive ping")
+            time.sleep(idle_s)
+            pings = t.serve.count("sent keepalive ping") - pings0
+            r = loadgen(t.proxy_port, burst, 1)
+            d = loadgen(port, burst, 1)
+            row = {"transport": transport, "idle_s": idle_s, "burst_streams": burst, "pings_during_idle": pings,
+                   "tunneled_req_s": r["req_s"], "tunneled_p50_ttft_ms": r["p50_ttft_ms"],
+                   "direct_p50_ttft_ms": d["p50_ttft_ms"], "added_p50_ttft_ms": r["p50_ttft_ms"] - d["p50_ttft_ms"],
+                   "errors": r["errors"]}
+            print(json.dumps(row), file=sys.stderr, flush=True)
+            return row
+    finally:
+        mock.stop()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=6)
+    ap.add_argument("--idle-s", type=float, default=30)
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--quick", action="store_true", help="native mock + webrtc only")
+    a = ap.parse_args()
+    ensure_native()
+    res = {"host": os.uname().nodename, "time": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()), "sse": []}
+    streams = [1, 2, 4, 8]
+    res["sse"] += sse_matrix("webrtc", "native", streams, a.steps)
+    if not a.quick:
+        res["sse"] += sse_matrix("tcp", "native", streams, a.steps)
+        res["sse"] += sse_matrix("webrtc", "python", streams, a.steps)
+        res["sse"] += sse_matrix("webrtc", "python", [1, 2, 4, 8], 3, threaded=False)
+    res["post_64x1MB"] = [post_1mb("webrtc")]
+    if not a.quick:
+        res["post_64x1MB"].append(post_1mb("tcp"))
+    res["idle_burst"] = idle_burst("webrtc", a.idle_s)
+    doc = json.dumps(res, indent=1)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(doc + "\n")
+    print(doc)
+
+
+if __name__ == "__main__":
+    main()

@@ -99,7 +99,8 @@ class Stream : public std::enable_shared_from_this<Stream> {
       }
       buf_.erase(0, used);
       uint64_t len = 0;
-      body_.reset(http::response_body_mode(head_, "POST", len), len);
+      auto mode = http::response_body_mode(head_, "POST", len);  // sets len: evaluate before reset()
+      body_.reset(mode, len);
       keep_ = head_.version_minor >= 1 && !head_.has_token("connection", "close") &&
               body_.mode() != http::BodyDecoder::Mode::UntilClose;
       head_done_ = true;

@@ -854,13 +854,20 @@ void SctpAssociation::flush() {
     stats_.retransmits++;
     sent_any = true;
   }
-  // New data.
+  // New data. After each drain the producer (data channel -> frame scheduler)
+  // is told the queue emptied and may enqueue more right away; keep sending
+  // within this flush while the windows allow, instead of idling until the
+  // next SACK wakes the reactor (the producer keeps this queue shallow for
+  // fairness, so without this loop a flush would send at most one window).
+  for (int round = 0; round < 256; round++) {
+  bool progressed = false;
   while (!sendq_.empty()) {
     Msg& m = sendq_.front();
     size_t left = m.len - m.off;
     size_t take = std::min(left, max_payload);
     if (flight_size_ > 0 && (flight_size_ + take > cwnd_ || take > peer_rwnd_)) break;
     if (flight_size_ == 0 && peer_rwnd_ == 0 && !inflight_.empty()) break;  // wait for window / T3 probe
+    progressed = true;
     auto* ch = new Chunk();
     ch->tsn = next_tsn_++;
     ch->stream = m.stream;
@@ -884,6 +891,11 @@ void SctpAssociation::flush() {
     peer_rwnd_ = peer_rwnd_ > take ? peer_rwnd_ - take : 0;
     sent_any = true;
     if (m.off == m.len) sendq_.pop_front();
+  }
+  if (!progressed || !sendq_.empty() || !on_sent) break;
+  size_t before = unsent_bytes_;
+  on_sent();  // producer may refill the (now empty) queue
+  if (closed_fired_ || unsent_bytes_ == before) break;
   }
   flush_pkt();
   if (sent_any && !t3_timer_) start_t3();

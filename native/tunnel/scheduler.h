@@ -22,7 +22,7 @@ namespace p2pt {
 
 class FrameScheduler {
  public:
-  explicit FrameScheduler(std::shared_ptr<MessageChannel> ch, size_t window = 256 * 1024);
+  explicit FrameScheduler(std::shared_ptr<MessageChannel> ch, size_t window = 64 * 1024);
   ~FrameScheduler();
 
   // Stream 0 frames (HELLO/AGREE/PING/PONG) are control frames and jump the queue.

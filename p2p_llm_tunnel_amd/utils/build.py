@@ -23,15 +23,15 @@ def _newest_mtime(paths) -> float:
 
 def native_outputs() -> list[str]:
     import glob
-    outs = [os.path.join(BIN_DIR, "tunnel"), os.path.join(BIN_DIR, "tunnel-signal"),
-            os.path.join(BIN_DIR, "native_tests")]
+    outs = [os.path.join(BIN_DIR, n) for n in ("tunnel", "tunnel-signal", "tunnel-mock", "tunnel-loadgen",
+                                                "native_tests")]
     outs += glob.glob(os.path.join(PKG_DIR, "_native*.so"))
     return outs
 
 
 def native_up_to_date() -> bool:
     outs = native_outputs()
-    if len(outs) < 4 or not all(os.path.exists(o) for o in outs):
+    if len(outs) < 6 or not all(os.path.exists(o) for o in outs):
         return False
     src = _newest_mtime([os.path.join(REPO_ROOT, "native")])
     src = max(src, os.path.getmtime(os.path.join(REPO_ROOT, "CMakeLists.txt")))
