@@ -42,9 +42,12 @@ class Request:
 
 
 class Engine:
-    def __init__(self, device="cuda:0", config="tiny", max_batch=8, seed=0):
+    def __init__(self, device="cuda:0", config="tiny", max_batch=8, seed=0, use_graph=True):
         self.model = TinyLlama(config, device=device, max_batch=max_batch, seed=seed)
         self.device = self.model.device
+        self.use_graph = use_graph
+        if use_graph:
+            self.model.capture_graph()
         self.max_batch = max_batch
         self.pending: queue.Queue = queue.Queue()
         self.slots: list[dict | None] = [None] * max_batch
@@ -81,7 +84,9 @@ class Engine:
             if not active:
                 time.sleep(0.0005)
                 continue
-            n = max(active) + 1  # slots [0, n) run; idle slots feed token 0 at pos 0
+            # Graph mode replays the captured full-batch step; eager mode runs
+            # slots [0, n). Idle slots feed token 0 at position 0.
+            n = self.max_batch if self.use_graph else max(active) + 1
             toks, pos = [], []
             for i in range(n):
                 s = self.slots[i]
@@ -96,7 +101,10 @@ class Engine:
                     pos.append(s["pos"])
             t = torch.tensor(toks, dtype=torch.int64).to(self.device, non_blocking=True)
             p = torch.tensor(pos, dtype=torch.int32).to(self.device, non_blocking=True)
-            ids = self.model.decode_step(t, p, (min(pos), max(pos))).tolist()
+            if self.use_graph:
+                ids = self.model.graph_step(t, p).tolist()
+            else:
+                ids = self.model.decode_step(t, p, (min(pos), max(pos))).tolist()
             self.steps += 1
             for i in active:
                 s = self.slots[i]

@@ -89,8 +89,13 @@ class TinyLlama:
             raise ValueError("batch exceeds max_batch")
         if pos_range[1] >= c.max_seq:
             raise ValueError("sequence exceeds max_seq")
+        ids, logits = self._decode_impl(tokens, pos, pos_range, pos_range[1] + 1)
+        return (ids, logits) if return_logits else ids
+
+    def _decode_impl(self, tokens, pos, pos_range, max_len):
+        c = self.cfg
+        B = tokens.shape[0]
         lens = pos + 1
-        max_len = pos_range[1] + 1
         x = self.embed.index_select(0, tokens)
         h = ops.rmsnorm(x, self.layers[0]["attn_norm"], c.eps)
         residual = x
@@ -106,8 +111,39 @@ class TinyLlama:
             nxt = self.layers[i + 1]["attn_norm"] if i + 1 < len(self.layers) else self.final_norm
             h, residual = ops.rmsnorm(m, nxt, c.eps, residual=residual)
         logits = F.linear(h, self.lm_head)
-        ids = ops.argmax(logits)
-        return (ids, logits) if return_logits else ids
+        return ops.argmax(logits), logits
+
+    # ------------------------------------------------------------------ hipGraph
+    def capture_graph(self):
+        """Capture one full-batch decode step into a hipGraph (torch.cuda.CUDAGraph).
+
+        Decode at small batch is launch-bound (~10 kernels per layer, each a few
+        µs); replaying the captured graph removes the per-kernel launch cost.
+        The attention is captured for the cache capacity (its splits past each
+        sequence's length exit immediately), so one graph serves every step.
+        """
+        B, c = self.max_batch, self.cfg
+        self._g_tok = torch.zeros(B, dtype=torch.int64, device=self.device)
+        self._g_pos = torch.zeros(B, dtype=torch.int32, device=self.device)
+        full = (0, c.max_seq - 1)
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.no_grad(), torch.cuda.stream(side):
+            for _ in range(2):  # allocator + GEMM heuristics warm-up outside capture
+                self._decode_impl(self._g_tok, self._g_pos, full, c.max_seq)
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        self._graph = torch.cuda.CUDAGraph()
+        with torch.no_grad(), torch.cuda.graph(self._graph):
+            self._g_ids, self._g_logits = self._decode_impl(self._g_tok, self._g_pos, full, c.max_seq)
+        return self
+
+    @torch.no_grad()
+    def graph_step(self, tokens: torch.Tensor, pos: torch.Tensor, return_logits: bool = False):
+        """Replay the captured step. tokens/pos: [max_batch]; positions must be < max_seq."""
+        self._g_tok.copy_(tokens, non_blocking=True)
+        self._g_pos.copy_(pos, non_blocking=True)
+        self._graph.replay()
+        return (self._g_ids, self._g_logits) if return_logits else self._g_ids
 
     def cache_views_contiguous(self) -> bool:
         return all(self.k_cache[i, : self.max_batch].is_contiguous() for i in range(self.cfg.n_layers))

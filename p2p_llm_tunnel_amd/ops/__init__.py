@@ -136,8 +136,14 @@ def rope_qkv_cache(qkv: torch.Tensor, pos: torch.Tensor, k_cache: torch.Tensor, 
 
 
 def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, lens: torch.Tensor,
-                     chunk: int = 256, max_len: int | None = None, scale: float | None = None) -> torch.Tensor:
-    """Single-token GQA attention over the KV cache. q: [B, H, D]; lens: int32 [B] (>= 1)."""
+                     chunk: int = 64, max_len: int | None = None, scale: float | None = None) -> torch.Tensor:
+    """Single-token GQA attention over the KV cache. q: [B, H, D]; lens: int32 [B] (>= 1).
+
+    The sequence is split into `chunk`-token pieces, one workgroup each
+    (B * Hkv * ceil(max_len / chunk) workgroups), so even batch-1 decode
+    fills the 256 CUs. Splits past a sequence's length exit immediately, which
+    lets a captured graph use max_len = cache capacity for every step.
+    """
     _check(q, torch.bfloat16, "q")
     _check(k_cache, torch.bfloat16, "k_cache", q.device)
     _check(v_cache, torch.bfloat16, "v_cache", q.device)

@@ -183,6 +183,9 @@ __global__ __launch_bounds__(512) void k_decode_attn(const uint16_t* __restrict_
   const int start = split * chunk;
   const int stop = min(start + chunk, len);
   const int nthr = blockDim.x;
+  // Splits past this sequence's length do nothing (k_attn_reduce only reads
+  // the first ceil(len/chunk) partials), so graphs can launch for capacity.
+  if (start >= len) return;
 
   float qf[D];
   {

@@ -1,9 +1,10 @@
 """Decode-step microbenchmark of the on-node inference upstream (for rocprofv3).
 
-    python scripts/profile_decode.py --config tiny --batch 8 --ctx 1024 --steps 50
+    python scripts/profile_decode.py --config tiny --batch 8 --ctx 1024 --steps 50 [--eager]
 
-Prefills `ctx` positions by writing random KV (fast path), then times
-`steps` batched decode steps through the HIP kernels and prints tokens/s.
+Fills the KV cache with random values up to `ctx`, then times `steps`
+batched decode steps through the HIP kernels — replayed from a captured
+hipGraph by default, or launched eagerly with --eager — and prints tokens/s.
 """
 from __future__ import annotations
 
@@ -27,25 +28,29 @@ def main():
     ap.add_argument("--ctx", type=int, default=1024)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--eager", action="store_true")
     a = ap.parse_args()
     m = TinyLlama(a.config, device="cuda", max_batch=a.batch)
     m.k_cache.normal_()
     m.v_cache.normal_()
+    if not a.eager:
+        m.capture_graph()
     B = a.batch
     tok = torch.randint(0, m.cfg.vocab, (B,), device="cuda")
-    pos0 = a.ctx
+
+    def step(q):
+        p = torch.full((B,), q, dtype=torch.int32, device="cuda")
+        return m.decode_step(tok, p, (q, q)) if a.eager else m.graph_step(tok, p)
+
     for i in range(a.warmup):
-        p = torch.full((B,), pos0 + i, dtype=torch.int32, device="cuda")
-        tok = m.decode_step(tok, p, (pos0 + i, pos0 + i))
+        tok = step(a.ctx + i)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
-        q = pos0 + a.warmup + i
-        p = torch.full((B,), q, dtype=torch.int32, device="cuda")
-        tok = m.decode_step(tok, p, (q, q))
+        tok = step(a.ctx + a.warmup + i)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    print(json.dumps({"config": a.config, "batch": B, "ctx": a.ctx, "steps": a.steps,
+    print(json.dumps({"config": a.config, "batch": B, "ctx": a.ctx, "steps": a.steps, "graph": not a.eager,
                       "ms_per_step": dt * 1e3 / a.steps, "tokens_per_s": B * a.steps / dt}))
 
 

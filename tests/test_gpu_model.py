@@ -34,6 +34,26 @@ def test_decode_matches_fp32_reference(cfg):
 
 
 @cuda
+def test_graph_replay_matches_eager():
+    from p2p_llm_tunnel_amd.models.tiny_llm import TinyLlama
+    torch.manual_seed(3)
+    m = TinyLlama("micro", device="cuda", max_batch=4, seed=2)
+    m.k_cache.normal_()
+    m.v_cache.normal_()
+    m.capture_graph()
+    toks = torch.randint(0, m.cfg.vocab, (4,), device="cuda")
+    pos = torch.tensor([5, 130, 0, 300], dtype=torch.int32, device="cuda")
+    kc, vc = m.k_cache.clone(), m.v_cache.clone()
+    ids_g, logits_g = m.graph_step(toks, pos, return_logits=True)
+    logits_g = logits_g.clone()
+    m.k_cache.copy_(kc)
+    m.v_cache.copy_(vc)
+    ids_e, logits_e = m.decode_step(toks, pos, (0, 300), return_logits=True)
+    assert torch.equal(ids_g, ids_e)
+    assert (logits_g.float() - logits_e.float()).abs().max().item() < 1e-2
+
+
+@cuda
 def test_gpu_endpoint_through_tunnel():
     from p2p_llm_tunnel_amd.models.server import start_server
     from p2p_llm_tunnel_amd.utils.procs import Tunnel
