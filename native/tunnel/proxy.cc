@@ -30,7 +30,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
   }
 
   void on_res_headers(const proto::ResponseHeaders& rh) {
-    if (!conn_ || conn_->closed()) return;
+    if (!conn_ || conn_->closed() || aborted_) return;
     if (state_ != State::Awaiting && state_ != State::ReadingBody) {
       LOG_WARN(kT, "unexpected duplicate headers for stream %u", sid_);
       return;
@@ -41,7 +41,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
   }
 
   void on_res_body(const Bytes& payload) {
-    if (!conn_ || conn_->closed()) return;
+    if (!conn_ || conn_->closed() || aborted_) return;
     if (!head_written_) {
       LOG_WARN(kT, "received body chunk before headers for stream %u", sid_);
       return;
@@ -64,7 +64,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
   }
 
   void on_res_end() {
-    if (!conn_ || conn_->closed()) return;
+    if (!conn_ || conn_->closed() || aborted_) return;
     trace::event("proxy", sid_, "res_end");
     if (!head_written_) {
       fail_before_head("response ended before headers");
@@ -75,7 +75,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
   }
 
   void on_res_error(const std::string& msg) {
-    if (!conn_ || conn_->closed()) return;
+    if (!conn_ || conn_->closed() || aborted_) return;
     if (!head_written_) {
       fail_before_head(msg);
       return;
@@ -83,8 +83,13 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     // Q10: ending the body normally would hand the client a truncated body
     // that looks complete; abort the connection instead.
     LOG_WARN(kT, "tunnel error mid-stream for %u: %s", sid_, msg.c_str());
+    // The head and body bytes already queued are flushed first so the client
+    // sees the status and the partial body, then the connection ends without
+    // the length/terminating chunk it was promised.
     stream_registered_ = false;
-    conn_->close("tunnel error mid-stream");
+    aborted_ = true;
+    conn_->pause_reading();
+    conn_->close_after_flush();
   }
 
   void resume_reading() {
@@ -396,6 +401,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
   bool stream_registered_ = false;
   bool keep_alive_ = true;
   bool head_written_ = false;
+  bool aborted_ = false;
   bool chunked_ = false;
   bool no_body_ = false;
   bool first_body_ = false;
