@@ -2,6 +2,8 @@
 
 #include "core/log.h"
 
+#include <deque>
+
 namespace p2pt::http {
 
 // Keep-alive pool plus "warm" connections: fresh, already-established
@@ -10,6 +12,8 @@ namespace p2pt::http {
 // keep-alive never helps them; a warm socket takes the TCP (and TLS)
 // handshake off every request's time-to-first-token. The warm target follows
 // the recent peak of concurrent requests (>= the configured minimum).
+using WarmWaiter = std::function<bool(std::shared_ptr<TcpConn>, const std::string&)>;
+
 class ClientConnPool : public std::enable_shared_from_this<ClientConnPool> {
  public:
   explicit ClientConnPool(Reactor& r) : r_(r) {}
@@ -35,6 +39,7 @@ class ClientConnPool : public std::enable_shared_from_this<ClientConnPool> {
     int failures = 0;
     uint64_t retry_timer = 0;
     std::vector<std::shared_ptr<TcpConn>> ready;
+    std::deque<WarmWaiter> waiters;  // calls waiting for the next warm socket
   };
 
   void configure_warm(const std::string& key, const std::string& host, uint16_t port, bool tls, size_t min) {
@@ -47,14 +52,30 @@ class ClientConnPool : public std::enable_shared_from_this<ClientConnPool> {
   }
   bool has_warm(const std::string& key) const { return warm_.count(key) != 0; }
 
+  // With no warm socket ready, a call queues for the next one to finish
+  // connecting instead of opening its own: every upstream connection then
+  // comes from one FIFO, so use order follows connect (= accept) order even
+  // for a single-threaded upstream. False while backing off after connect
+  // failures (the caller connects directly and reports its own error).
+  bool wait_warm(const std::string& key, WarmWaiter fn) {
+    auto it = warm_.find(key);
+    if (it == warm_.end() || it->second.retry_timer) return false;
+    it->second.waiters.push_back(std::move(fn));
+    replenish(key);
+    return true;
+  }
+
   std::shared_ptr<TcpConn> take_warm(const std::string& key) {
     auto it = warm_.find(key);
     if (it == warm_.end()) return nullptr;
+    // Oldest first: a single-threaded upstream (the reference's own mock)
+    // accepts connections in connect order and blocks reading the first one,
+    // so handing out a newer warm socket would wait behind an idle one forever.
     auto& v = it->second.ready;
     std::shared_ptr<TcpConn> c;
     while (!v.empty()) {
-      c = v.back();
-      v.pop_back();
+      c = v.front();
+      v.erase(v.begin());
       if (!c->closed()) break;
       c.reset();
     }
@@ -87,7 +108,7 @@ class ClientConnPool : public std::enable_shared_from_this<ClientConnPool> {
     if (it == warm_.end()) return;
     Warm& w = it->second;
     if (w.retry_timer) return;  // backing off after connect failures
-    size_t target = std::min(w.max, std::max(w.min, w.peak));
+    size_t target = std::min(w.max, std::max(w.min, w.peak)) + w.waiters.size();
     std::weak_ptr<ClientConnPool> self = shared_from_this();
     while (w.ready.size() + w.connecting < target) {
       w.connecting++;
@@ -105,10 +126,17 @@ class ClientConnPool : public std::enable_shared_from_this<ClientConnPool> {
         Warm& w2 = it2->second;
         w2.connecting--;
         if (!c) {
-          // Upstream down: back off (it is also reported per request as 502).
-          w2.failures++;
-          uint64_t delay = std::min<uint64_t>(100ull << std::min(w2.failures, 6), 5000);
-          w2.retry_timer = p->r_.call_later_ms(delay, [self, key] {
+          // Upstream down: fail the waiting calls (each becomes a 502) and back off.
+          auto waiters = std::move(w2.waiters);
+          w2.waiters.clear();
+          for (auto& fn : waiters) fn(nullptr, err);
+          it2 = p->warm_.find(key);
+          if (it2 == p->warm_.end()) return;
+          Warm& w3 = it2->second;
+          if (w3.retry_timer) return;
+          w3.failures++;
+          uint64_t delay = std::min<uint64_t>(100ull << std::min(w3.failures, 6), 5000);
+          w3.retry_timer = p->r_.call_later_ms(delay, [self, key] {
             auto p2 = self.lock();
             if (!p2) return;
             auto it3 = p2->warm_.find(key);
@@ -119,6 +147,11 @@ class ClientConnPool : public std::enable_shared_from_this<ClientConnPool> {
           return;
         }
         w2.failures = 0;
+        while (!w2.waiters.empty()) {
+          WarmWaiter fn = std::move(w2.waiters.front());
+          w2.waiters.pop_front();
+          if (fn(c, "")) return;  // the call took it; a declined one (cancelled) tries the next
+        }
         std::weak_ptr<TcpConn> wc = c;
         // A warm socket that turns readable/closed was dropped by the server
         // (idle timeout): discard it and top up again.
@@ -190,6 +223,10 @@ class ClientConnPool : public std::enable_shared_from_this<ClientConnPool> {
     warm_.clear();
     for (auto& kv : warm) {
       if (kv.second.retry_timer) r_.cancel(kv.second.retry_timer);
+      if (!kv.second.waiters.empty())
+        r_.post([ws = std::move(kv.second.waiters)]() mutable {
+          for (auto& fn : ws) fn(nullptr, "client shut down");
+        });
       for (auto& c : kv.second.ready) {
         c->on_close(nullptr);
         c->close();
@@ -277,17 +314,19 @@ void ClientCall::start() {
     return;
   }
   std::weak_ptr<ClientCall> w = shared_from_this();
-  TcpConn::connect(*r_, url_.host, url_.port, url_.tls(), [w](std::shared_ptr<TcpConn> c, std::string e) {
+  auto deliver = [w](std::shared_ptr<TcpConn> c, const std::string& e) -> bool {
     auto self = w.lock();
-    if (!self || self->finished_) {
-      if (c) c->close();
-      return;
-    }
+    if (!self || self->finished_) return false;
     if (!c) {
       self->finish("error sending request for url (" + self->req_.url + "): " + e);
-      return;
+      return true;
     }
     self->attach(c, false);
+    return true;
+  };
+  if (pool_->wait_warm(pool_key_, deliver)) return;
+  TcpConn::connect(*r_, url_.host, url_.port, url_.tls(), [deliver](std::shared_ptr<TcpConn> c, std::string e) {
+    if (!deliver(c, e) && c) c->close();
   });
 }
 

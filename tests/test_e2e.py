@@ -6,6 +6,7 @@ exercised: SSE token-by-token, --advertise stripping, 502 on a
 dead upstream, 504 header timeout, mid-stream upstream failure, 1 MB POST,
 concurrent multiplexed streams, keep-alive reuse, HTTP/1.0 clients, PING cadence.
 """
+import concurrent.futures
 import http.client
 import json
 import socket
@@ -167,6 +168,23 @@ def test_advertise_prefix_stripping(transport):
             assert body == b"ok"
     finally:
         srv.shutdown()
+
+
+def test_single_threaded_upstream(transport):
+    # The reference's mock serves one connection at a time (socketserver.TCPServer,
+    # HTTP/1.0). Warm upstream sockets must be used in connect order or a
+    # request waits behind an idle socket the server is blocked on.
+    srv, port = mock_llm.start_in_thread(threaded=False)
+    try:
+        with Tunnel(f"http://127.0.0.1:{port}", transport=transport) as t:
+            for _ in range(6):
+                assert get(t.url + "/health", timeout=5)[2] == b"ok"
+            with concurrent.futures.ThreadPoolExecutor(6) as ex:
+                outs = list(ex.map(lambda _: get(t.url + "/v1/models", timeout=10)[2], range(6)))
+            assert all(b"test-model" in o for o in outs)
+    finally:
+        srv.shutdown()
+        srv.server_close()
 
 
 def test_dead_upstream_502(transport):
