@@ -2,10 +2,18 @@
 
 The tunnel's serve side fronts an OpenAI/Ollama-compatible endpoint running
 on the MI355X node (BASELINE.json north star). This module is that
-endpoint's model: random-init weights (no checkpoints offline), bf16, with
-the decode step built from the gfx950 HIP kernels in ``p2p_llm_tunnel_amd.ops``
-(fused residual+RMSNorm, fused RoPE+KV-append, GQA flash-decoding,
-SwiGLU, argmax) and hipBLASLt GEMMs via ``torch.nn.functional.linear``.
+endpoint's model: random-init weights (no checkpoints offline), bf16.
+
+Two decode paths over the same weights and caches:
+
+* fused (default, up to 16 tokens per step): ``ops.FusedLlamaDecoder`` — one
+  C++ call launching 5 kernels per layer + 2 (decode_fused.hip: MFMA skinny
+  GEMMs with RMSNorm prologues and RoPE/KV-append, SwiGLU, residual and
+  argmax epilogues; split-K attention with in-kernel merge);
+* unfused: the standalone kernels of kernels.hip (residual+RMSNorm,
+  RoPE+KV-append, flash-decoding, SwiGLU, argmax) around hipBLASLt GEMMs
+  (``torch.nn.functional.linear``) — kept as the cross-check and for batches
+  above 16.
 
 ``reference_logits`` recomputes the same network in fp32 PyTorch (full
 causal attention over the whole sequence) for numerics tests.
@@ -44,8 +52,11 @@ CONFIGS = {
 
 
 class TinyLlama:
-    def __init__(self, cfg: LlamaConfig | str = "tiny", device="cuda", max_batch: int = 8, seed: int = 0):
+    def __init__(self, cfg: LlamaConfig | str = "tiny", device="cuda", max_batch: int = 8, seed: int = 0,
+                 fused: bool = True):
         self.cfg = CONFIGS[cfg] if isinstance(cfg, str) else cfg
+        self.fused = fused
+        self._fused = None
         c = self.cfg
         self.device = torch.device(device)
         self.max_batch = max_batch
@@ -92,7 +103,28 @@ class TinyLlama:
         ids, logits = self._decode_impl(tokens, pos, pos_range, pos_range[1] + 1)
         return (ids, logits) if return_logits else ids
 
+    def fused_decoder(self) -> ops.FusedLlamaDecoder:
+        if self._fused is None:
+            c = self.cfg
+            dims = ops.LlamaDims(vocab=c.vocab, dim=c.dim, n_layers=c.n_layers, H=c.n_heads, Hkv=c.n_kv_heads,
+                                 D=c.head_dim, ffn=c.ffn, max_seq=c.max_seq, max_batch=self.max_batch, eps=c.eps,
+                                 theta=c.rope_theta)
+            ws = [self.embed, self.final_norm, self.lm_head]
+            for L in self.layers:
+                ws += [L[k] for k in ("attn_norm", "wqkv", "wo", "ffn_norm", "w_gate_up", "w_down")]
+            self._fused = ops.FusedLlamaDecoder(dims, ws, self.k_cache, self.v_cache)
+        return self._fused
+
     def _decode_impl(self, tokens, pos, pos_range, max_len):
+        B = tokens.shape[0]
+        if self.fused and B <= 16:
+            logits = torch.empty(B, self.cfg.vocab, dtype=torch.bfloat16, device=self.device)
+            ids = torch.empty(B, dtype=torch.int64, device=self.device)
+            self.fused_decoder().step(tokens, pos, max_len, logits, ids)
+            return ids, logits
+        return self._decode_unfused(tokens, pos, pos_range, max_len)
+
+    def _decode_unfused(self, tokens, pos, pos_range, max_len):
         c = self.cfg
         B = tokens.shape[0]
         lens = pos + 1

@@ -18,6 +18,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
 
 
+class LlamaDims(ctypes.Structure):
+    """Mirror of ``LlamaDims`` in decode_fused.hip."""
+    _fields_ = [(n, ctypes.c_int) for n in ("vocab", "dim", "n_layers", "H", "Hkv", "D", "ffn", "max_seq",
+                                           "max_batch")] + [("eps", ctypes.c_float), ("theta", ctypes.c_float)]
+
+
 def lib() -> ctypes.CDLL:
     global _LIB
     if _LIB is None:
@@ -32,7 +38,13 @@ def lib() -> ctypes.CDLL:
         _LIB.p2pt_rope_qkv_cache.argtypes = [vp, vp, vp, vp, vp, i, i, i, i, i, f, vp]
         _LIB.p2pt_decode_attention.argtypes = [vp, vp, vp, vp, vp, vp, i, i, i, i, i, i, i, f, vp]
         _LIB.p2pt_argmax.argtypes = [vp, vp, i, i, vp]
-        for fn in ("p2pt_rmsnorm", "p2pt_silu_mul", "p2pt_rope_qkv_cache", "p2pt_decode_attention", "p2pt_argmax"):
+        _LIB.p2pt_skinny_gemm.argtypes = [vp, vp, vp, i, i, i, vp]
+        _LIB.p2pt_llama_ws_bytes.argtypes = [ctypes.POINTER(LlamaDims)]
+        _LIB.p2pt_llama_ws_bytes.restype = ctypes.c_size_t
+        _LIB.p2pt_llama_decode.argtypes = [ctypes.POINTER(LlamaDims), ctypes.POINTER(vp), vp, vp, vp, vp, i, i, vp,
+                                           ctypes.c_size_t, vp, vp, vp]
+        for fn in ("p2pt_rmsnorm", "p2pt_silu_mul", "p2pt_rope_qkv_cache", "p2pt_decode_attention", "p2pt_argmax",
+                   "p2pt_skinny_gemm", "p2pt_llama_decode"):
             getattr(_LIB, fn).restype = ctypes.c_int
     return _LIB
 
@@ -182,3 +194,66 @@ def argmax(logits: torch.Tensor) -> torch.Tensor:
     out = torch.empty(B, dtype=torch.int64, device=logits.device)
     _ok(lib().p2pt_argmax(_p(logits), _p(out), B, V, _stream(logits)), "argmax")
     return out
+
+
+def skinny_gemm(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """bf16(x @ w.T) for a few rows on MFMA (decode-shaped GEMM). x: [M<=16, K]; w: [N, K]."""
+    _check(x, torch.bfloat16, "x")
+    _check(w, torch.bfloat16, "w", x.device)
+    if x.dim() != 2 or w.dim() != 2 or x.shape[1] != w.shape[1]:
+        raise ValueError("shapes must be x [M, K], w [N, K]")
+    M, K = x.shape
+    N = w.shape[0]
+    if not 1 <= M <= 16 or N % 32 or K % 128:
+        raise ValueError("need 1 <= M <= 16, N % 32 == 0, K % 128 == 0")
+    out = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    _ok(lib().p2pt_skinny_gemm(_p(x), _p(w), _p(out), M, N, K, _stream(x)), "skinny_gemm")
+    return out
+
+
+class FusedLlamaDecoder:
+    """Host handle for the fused decode step (decode_fused.hip): 5 kernels per layer + 2.
+
+    Holds the weight pointer table and a zero-initialised workspace; ``step``
+    validates the per-call tensors and launches on the current stream (capturable
+    into a hipGraph: no host sync, no allocation).
+    """
+
+    def __init__(self, dims: LlamaDims, weights: list, k_cache: torch.Tensor, v_cache: torch.Tensor):
+        self.dims = dims
+        dev = k_cache.device
+        for i, t in enumerate(weights):
+            _check(t, torch.bfloat16, f"weight[{i}]", dev)
+        L, Bmax, S, Hkv, D = k_cache.shape
+        if (L, Bmax, S, Hkv, D) != (dims.n_layers, dims.max_batch, dims.max_seq, dims.Hkv, dims.D):
+            raise ValueError("cache shape does not match dims")
+        _check(k_cache, torch.bfloat16, "k_cache", dev)
+        _check(v_cache, torch.bfloat16, "v_cache", dev)
+        if len(weights) != 3 + 6 * dims.n_layers:
+            raise ValueError("weight table: embed, final_norm, lm_head, then 6 per layer")
+        nbytes = lib().p2pt_llama_ws_bytes(ctypes.byref(dims))
+        if nbytes == 0:
+            raise ValueError("model dims not supported by the fused decode kernels")
+        self.weights = weights  # keep alive
+        self._wptr = (ctypes.c_void_p * len(weights))(*[t.data_ptr() for t in weights])
+        self.ws = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+        self.k_cache, self.v_cache = k_cache, v_cache
+        self.device = dev
+
+    def step(self, tokens: torch.Tensor, pos: torch.Tensor, max_len: int, logits: torch.Tensor,
+             ids: torch.Tensor) -> None:
+        d = self.dims
+        _check(tokens, torch.int64, "tokens", self.device)
+        _check(pos, torch.int32, "pos", self.device)
+        _check(logits, torch.bfloat16, "logits", self.device)
+        _check(ids, torch.int64, "ids", self.device)
+        B = tokens.shape[0]
+        if not 1 <= B <= min(16, d.max_batch) or pos.shape != (B,) or ids.shape != (B,):
+            raise ValueError("batch must be 1..min(16, max_batch) with matching pos/ids")
+        if logits.shape != (B, d.vocab):
+            raise ValueError("logits must be [B, vocab]")
+        if not 1 <= max_len <= d.max_seq:
+            raise ValueError("max_len out of range")
+        _ok(lib().p2pt_llama_decode(ctypes.byref(d), self._wptr, _p(self.k_cache), _p(self.v_cache), _p(tokens),
+                                    _p(pos), B, max_len, _p(self.ws), self.ws.numel(), _p(logits), _p(ids),
+                                    _stream(tokens)), "llama_decode")

@@ -1,6 +1,6 @@
 """Compile the HIP kernels in-tree for gfx950 (CDNA4 / MI355X).
 
-    hipcc -O3 --offload-arch=gfx950 -shared -fPIC kernels.hip -o _hip_ops.so
+    hipcc -O3 --offload-arch=gfx950 -shared -fPIC kernels.hip decode_fused.hip -o _hip_ops.so
 
 Cross-compiles on a CPU-only host; the .so travels with the repo snapshot to
 the GPU box.
@@ -12,7 +12,8 @@ import shutil
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRC = os.path.join(HERE, "kernels.hip")
+SRCS = [os.path.join(HERE, f) for f in ("kernels.hip", "decode_fused.hip")]
+DEPS = SRCS + [os.path.join(HERE, "bf16_common.h")]
 OUT = os.path.join(HERE, "_hip_ops.so")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
 
@@ -25,13 +26,13 @@ def hipcc() -> str:
 
 
 def up_to_date() -> bool:
-    return os.path.exists(OUT) and os.path.getmtime(OUT) >= os.path.getmtime(SRC)
+    return os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in DEPS)
 
 
 def build(verbose: bool = False, force: bool = False) -> str:
     if up_to_date() and not force:
         return OUT
-    cmd = [hipcc(), "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-shared", "-fPIC", "-o", OUT + ".tmp", SRC]
+    cmd = [hipcc(), "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-shared", "-fPIC", "-o", OUT + ".tmp", *SRCS]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)

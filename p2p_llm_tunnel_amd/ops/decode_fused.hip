@@ -1,0 +1,684 @@
+// Fused Llama decode step for gfx950 (CDNA4 / MI355X).
+//
+// The unfused step (kernels.hip + hipBLASLt) is ~50 kernels per token for a
+// 4-layer model; at decode batch sizes every one of them is a few-µs latency
+// chain (dispatch, one HBM round trip, write back) and the step is bound by
+// kernel count, not bytes. This file rebuilds the step as 5 kernels per layer
+// plus 2, each a weight-streaming MFMA GEMM with its neighbours fused in:
+//
+//   k_embed              token gather -> residual stream, per-row sum of squares
+//   per layer:
+//     k_skinny<ROPE>     RMSNorm prologue (attn_norm) -> QKV GEMM -> RoPE on q/k,
+//                        q to the attention buffer, k/v appended to the cache
+//     k_attn             GQA flash-decoding split-K; the last split to finish
+//                        for a (sequence, KV head) merges the partials in-kernel
+//     k_skinny<RESID>    O projection -> residual add -> per-row sum-of-squares
+//                        partials for the next norm
+//     k_skinny<SILU>     RMSNorm prologue (ffn_norm) -> gate/up GEMM -> SwiGLU
+//     k_skinny<RESID>    down projection -> residual add -> sum-of-squares
+//   k_skinny<ARGMAX>     RMSNorm prologue (final norm) -> LM head -> logits and
+//                        greedy argmax (last block merges the per-block winners)
+//
+// Skinny GEMM (M <= 16 tokens): Y[M,N] = A[M,K] * W[N,K]^T on
+// v_mfma_f32_16x16x32_bf16. A workgroup owns 16*TN output columns and splits K
+// over its NW waves; each lane streams its weight rows with 16-byte loads
+// straight into MFMA B fragments (no LDS staging: every weight byte is used
+// exactly once, by exactly one lane), the K-split partials are summed through
+// LDS and wave 0 runs the epilogue. Row RMSNorm needs the whole row, so the
+// producer of the residual writes per-block partial sums of squares and the
+// consumer folds them into 1/rms in its prologue (deterministic: fixed order,
+// no float atomics).
+//
+// Numerics mirror the unfused path: every value the unfused path stores as
+// bf16 (GEMM outputs, normed activations, residual) is rounded to bf16 at the
+// same point here; accumulation is fp32.
+#include "bf16_common.h"
+
+namespace {
+
+using namespace p2pt_gpu;
+
+constexpr int kMaxM = 16;  // tokens per step (one MFMA row tile)
+
+typedef short frag8 __attribute__((ext_vector_type(8)));
+typedef float frag4 __attribute__((ext_vector_type(4)));
+
+enum Epi : int { EPI_STORE = 0, EPI_ROPE = 1, EPI_SILU = 2, EPI_RESID = 3, EPI_ARGMAX = 4 };
+
+struct GemmArgs {
+  const uint16_t* x;  // A [M][K]
+  const uint16_t* w;  // W [N][K]
+  int M, N, K;
+  // RMSNorm prologue (norm_w == nullptr: A used as is)
+  const uint16_t* norm_w;
+  const float* ss_part;  // [ss_parts][16] partial row sums of squares
+  int ss_parts;
+  float eps;
+  // epilogue
+  uint16_t* out;   // STORE/ARGMAX: [M][N] logits; SILU: [M][N/2]; RESID: residual [M][N], in place
+  float* ss_out;   // RESID: [gridDim.x][16]
+  const int* pos;  // ROPE
+  uint16_t* q_out;
+  uint16_t* kc;
+  uint16_t* vc;
+  int H, Hkv, D, Smax;
+  float log2_theta;
+  float* am_val;  // ARGMAX: [gridDim.x][16]
+  int* am_idx;
+  unsigned* am_count;
+  int64_t* ids;
+};
+
+__device__ __forceinline__ frag8 as_frag(const uint4& v) { return __builtin_bit_cast(frag8, v); }
+
+// Output column of lane column c (0..15) in subtile t of block bx.
+template <int EPI, int TN>
+__device__ __forceinline__ int tile_col(const GemmArgs& a, int bx, int t, int c) {
+  if constexpr (EPI == EPI_ROPE) {
+    // TN == 2: subtile 0 = dims [i0, i0+16) of a head, subtile 1 = the RoPE
+    // partners [i0 + D/2, ...), so each lane holds both halves of its pairs.
+    const int half = a.D >> 1, per_head = half >> 4;
+    const int head = bx / per_head, i0 = (bx % per_head) << 4;
+    return head * a.D + t * half + i0 + c;
+  } else if constexpr (EPI == EPI_SILU) {
+    // TN == 2: subtile 0 = gate columns, subtile 1 = the matching up columns.
+    return t * (a.N >> 1) + (bx << 4) + c;
+  } else {
+    return ((bx * TN + t) << 4) + c;
+  }
+}
+
+template <int NW, int TN, int EPI>
+__global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
+  __shared__ float red[NW][TN][4][kWave];
+  __shared__ float s_rstd[kMaxM];
+  __shared__ float s_ss[NW][kMaxM];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int bx = blockIdx.x;
+  const bool norm = a.norm_w != nullptr;
+
+  if (norm) {
+    const int m = threadIdx.x & 15;
+    float s = 0.f;
+    for (int p = threadIdx.x >> 4; p < a.ss_parts; p += NW * 4) s += a.ss_part[p * kMaxM + m];
+    s += __shfl_xor(s, 16, kWave);
+    s += __shfl_xor(s, 32, kWave);
+    if (lane < 16) s_ss[wv][lane] = s;
+    __syncthreads();
+    if (threadIdx.x < kMaxM) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; w++) t += s_ss[w][threadIdx.x];
+      s_rstd[threadIdx.x] = rsqrtf(t * (1.f / float(a.K)) + a.eps);
+    }
+    __syncthreads();
+  }
+
+  // A fragment: row m_a, k = kb + 8*(lane>>4) + j. B fragment: W row n, same k.
+  const int m_a = lane & 15;
+  const bool a_ok = m_a < a.M;
+  const float rs = norm ? s_rstd[m_a] : 1.f;
+  const int kq = (lane >> 4) << 3;
+  const int Kw = a.K / NW;  // host guarantees K % (32 * NW) == 0
+  const int k0 = wv * Kw, k1 = k0 + Kw;
+  const uint16_t* xrow = a.x + size_t(m_a) * a.K + kq;
+  const uint16_t* gw = norm ? a.norm_w + kq : nullptr;
+  const uint16_t* wrow[TN];
+#pragma unroll
+  for (int t = 0; t < TN; t++) wrow[t] = a.w + size_t(tile_col<EPI, TN>(a, bx, t, lane & 15)) * a.K + kq;
+
+  frag4 acc[TN];
+#pragma unroll
+  for (int t = 0; t < TN; t++) acc[t] = frag4{0.f, 0.f, 0.f, 0.f};
+
+  auto load_a = [&](int k) -> uint4 {
+    if (!a_ok) return make_uint4(0, 0, 0, 0);
+    uint4 v = *reinterpret_cast<const uint4*>(xrow + k);
+    if (norm) {
+      float f[8], g[8];
+      unpack8(v, f);
+      unpack8(*reinterpret_cast<const uint4*>(gw + k), g);
+#pragma unroll
+      for (int j = 0; j < 8; j++) f[j] = f[j] * rs * g[j];
+      v = pack8(f);
+    }
+    return v;
+  };
+
+  constexpr int U = 4;
+  int k = k0;
+  for (; k + 32 * U <= k1; k += 32 * U) {
+    uint4 bv[U][TN], av[U];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int t = 0; t < TN; t++) bv[u][t] = *reinterpret_cast<const uint4*>(wrow[t] + k + 32 * u);
+#pragma unroll
+    for (int u = 0; u < U; u++) av[u] = load_a(k + 32 * u);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int t = 0; t < TN; t++)
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(av[u]), as_frag(bv[u][t]), acc[t], 0, 0, 0);
+  }
+  for (; k < k1; k += 32) {
+    uint4 bv[TN];
+#pragma unroll
+    for (int t = 0; t < TN; t++) bv[t] = *reinterpret_cast<const uint4*>(wrow[t] + k);
+    uint4 av = load_a(k);
+#pragma unroll
+    for (int t = 0; t < TN; t++)
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(av), as_frag(bv[t]), acc[t], 0, 0, 0);
+  }
+
+  // K-split reduction through LDS (lane-contiguous: conflict-free).
+#pragma unroll
+  for (int t = 0; t < TN; t++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) red[wv][t][r][lane] = acc[t][r];
+  __syncthreads();
+  if (wv != 0) return;
+  float v[TN][4];
+#pragma unroll
+  for (int t = 0; t < TN; t++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; w++) s += red[w][t][r][lane];
+      v[t][r] = s;
+    }
+
+  // C layout: row m = 4*(lane>>4) + r, column = tile_col(.., lane & 15).
+  const int mrow0 = (lane >> 4) << 2;
+  const int c = lane & 15;
+
+  if constexpr (EPI == EPI_STORE) {
+#pragma unroll
+    for (int t = 0; t < TN; t++) {
+      const int n = tile_col<EPI, TN>(a, bx, t, c);
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+        if (mrow0 + r < a.M) a.out[size_t(mrow0 + r) * a.N + n] = uint16_t(f2bf_bits(v[t][r]));
+    }
+  } else if constexpr (EPI == EPI_SILU) {
+    const int F = a.N >> 1;
+    const int n = tile_col<EPI, TN>(a, bx, 0, c);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      if (mrow0 + r >= a.M) continue;
+      const float g = bf_round(v[0][r]), u = bf_round(v[1][r]);
+      a.out[size_t(mrow0 + r) * F + n] = uint16_t(f2bf_bits(g / (1.f + __expf(-g)) * u));
+    }
+  } else if constexpr (EPI == EPI_ROPE) {
+    const int half = a.D >> 1;
+    const int col = tile_col<EPI, TN>(a, bx, 0, c);
+    const int head = col / a.D, i = col % a.D;  // i < half
+    const float inv_freq = exp2f(-a.log2_theta * (2.f * i) / a.D);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int m = mrow0 + r;
+      if (m >= a.M) continue;
+      const float x1 = bf_round(v[0][r]), x2 = bf_round(v[1][r]);
+      const int p = min(max(a.pos[m], 0), a.Smax - 1);  // host validates; never write outside the cache
+      if (head < a.H + a.Hkv) {
+        float sn, cs;
+        sincosf(float(p) * inv_freq, &sn, &cs);
+        const uint16_t o1 = uint16_t(f2bf_bits(x1 * cs - x2 * sn));
+        const uint16_t o2 = uint16_t(f2bf_bits(x2 * cs + x1 * sn));
+        uint16_t* dst;
+        if (head < a.H)
+          dst = a.q_out + (size_t(m) * a.H + head) * a.D;
+        else
+          dst = a.kc + ((size_t(m) * a.Smax + p) * a.Hkv + (head - a.H)) * a.D;
+        dst[i] = o1;
+        dst[i + half] = o2;
+      } else {
+        uint16_t* dst = a.vc + ((size_t(m) * a.Smax + p) * a.Hkv + (head - a.H - a.Hkv)) * a.D;
+        dst[i] = uint16_t(f2bf_bits(x1));
+        dst[i + half] = uint16_t(f2bf_bits(x2));
+      }
+    }
+  } else if constexpr (EPI == EPI_RESID) {
+    float sq[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < TN; t++) {
+      const int n = tile_col<EPI, TN>(a, bx, t, c);
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int m = mrow0 + r;
+        if (m >= a.M) continue;
+        uint16_t* p = a.out + size_t(m) * a.N + n;
+        const float nv = bf_round(bf2f(*p) + bf_round(v[t][r]));
+        *p = uint16_t(f2bf_bits(nv));
+        sq[r] += nv * nv;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) sq[r] += __shfl_xor(sq[r], o, kWave);
+      if (c == 0) a.ss_out[bx * kMaxM + mrow0 + r] = sq[r];
+    }
+  } else if constexpr (EPI == EPI_ARGMAX) {
+    float best[4];
+    int bi[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      best[r] = -INFINITY;
+      bi[r] = 0x7fffffff;
+    }
+#pragma unroll
+    for (int t = 0; t < TN; t++) {
+      const int n = tile_col<EPI, TN>(a, bx, t, c);
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int m = mrow0 + r;
+        const float lv = bf_round(v[t][r]);
+        if (m < a.M) a.out[size_t(m) * a.N + n] = uint16_t(f2bf_bits(lv));
+        if (lv > best[r] || (lv == best[r] && n < bi[r])) {
+          best[r] = lv;
+          bi[r] = n;
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const float ob = __shfl_xor(best[r], o, kWave);
+        const int oi = __shfl_xor(bi[r], o, kWave);
+        if (ob > best[r] || (ob == best[r] && oi < bi[r])) {
+          best[r] = ob;
+          bi[r] = oi;
+        }
+      }
+      if (c == 0) {
+        a.am_val[bx * kMaxM + mrow0 + r] = best[r];
+        a.am_idx[bx * kMaxM + mrow0 + r] = bi[r];
+      }
+    }
+    // Last block to finish merges every block's winners.
+    __threadfence();
+    unsigned ticket = 0;
+    if (lane == 0) ticket = atomicAdd(a.am_count, 1u);
+    ticket = __shfl(ticket, 0, kWave);
+    if (ticket != gridDim.x - 1) return;
+    __threadfence();
+    for (int m = 0; m < a.M; m++) {
+      float b = -INFINITY;
+      int i = 0x7fffffff;
+      for (int p = lane; p < int(gridDim.x); p += kWave) {
+        const float pv = __builtin_nontemporal_load(a.am_val + p * kMaxM + m);
+        const int pi = __builtin_nontemporal_load(a.am_idx + p * kMaxM + m);
+        if (pv > b || (pv == b && pi < i)) {
+          b = pv;
+          i = pi;
+        }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float ob = __shfl_xor(b, o, kWave);
+        const int oi = __shfl_xor(i, o, kWave);
+        if (ob > b || (ob == b && oi < i)) {
+          b = ob;
+          i = oi;
+        }
+      }
+      if (lane == 0) a.ids[m] = i;
+    }
+    if (lane == 0) *a.am_count = 0u;  // self-resetting for the next step / graph replay
+  }
+}
+
+// ------------------------------------------------------------ embedding gather
+// One block per token: residual row = embed[token]; ss_out[0][b] = sum of squares.
+__global__ __launch_bounds__(256) void k_embed(const uint16_t* __restrict__ embed, const int64_t* __restrict__ tok,
+                                               uint16_t* __restrict__ resid, float* __restrict__ ss_out, int dim,
+                                               int vocab) {
+  const int b = blockIdx.x;
+  int64_t t = tok[b];
+  t = t < 0 ? 0 : (t >= vocab ? vocab - 1 : t);
+  const uint4* src = reinterpret_cast<const uint4*>(embed + size_t(t) * dim);
+  uint4* dst = reinterpret_cast<uint4*>(resid + size_t(b) * dim);
+  float ss = 0.f;
+  for (int i = threadIdx.x; i < dim / 8; i += 256) {
+    const uint4 v = src[i];
+    dst[i] = v;
+    float f[8];
+    unpack8(v, f);
+#pragma unroll
+    for (int j = 0; j < 8; j++) ss += f[j] * f[j];
+  }
+  __shared__ float red[4];
+  ss = wave_sum(ss);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  if (threadIdx.x == 0) ss_out[b] = red[0] + red[1] + red[2] + red[3];
+}
+
+// ------------------------------------------------------------ attention
+// As k_decode_attn in kernels.hip (split-K over 64-token chunks, K/V tiles in
+// LDS shared by the GQA group, one wave per query head), plus: lens = pos + 1,
+// and the last split to finish for a (sequence, KV head) merges the partials
+// (arrival ticket, self-resetting) and writes the bf16 output [B][H*D].
+template <int D>
+__global__ __launch_bounds__(512) void k_attn(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+                                              const uint16_t* __restrict__ vc, const int* __restrict__ pos,
+                                              float* __restrict__ part_o, float* __restrict__ part_ml,
+                                              unsigned* __restrict__ counters, uint16_t* __restrict__ out, int H,
+                                              int Hkv, int Smax, int chunk, int nsplit, float scale) {
+  constexpr int TILE = 64;
+  constexpr int ROWB = D * 2 + 16;
+  constexpr int DPL = D / kWave;
+  __shared__ __attribute__((aligned(16))) uint8_t ks[TILE * ROWB];
+  __shared__ __attribute__((aligned(16))) uint8_t vs[TILE * ROWB];
+  __shared__ unsigned s_ticket;
+
+  const int split = blockIdx.x;
+  const int b = blockIdx.y / Hkv, kvh = blockIdx.y % Hkv;
+  const int G = H / Hkv;
+  const int len = min(max(pos[b], 0), Smax - 1) + 1;
+  const int g = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int start = split * chunk;
+  const int stop = min(start + chunk, len);
+  const int used = min(nsplit, (len + chunk - 1) / chunk);
+  if (start >= len) return;
+
+  float qf[D];
+  {
+    const uint16_t* qp = q + (size_t(b) * H + kvh * G + g) * D;
+#pragma unroll
+    for (int d = 0; d < D; d += 8) {
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4*>(qp + d), f);
+#pragma unroll
+      for (int k = 0; k < 8; k++) qf[d + k] = f[k] * scale;
+    }
+  }
+  float m = -INFINITY, l = 0.f, acc[DPL];
+#pragma unroll
+  for (int k = 0; k < DPL; k++) acc[k] = 0.f;
+
+  const size_t tok_stride = size_t(Hkv) * D;
+  const uint16_t* kbase = kc + (size_t(b) * Smax) * tok_stride + size_t(kvh) * D;
+  const uint16_t* vbase = vc + (size_t(b) * Smax) * tok_stride + size_t(kvh) * D;
+
+  for (int t0 = start; t0 < stop; t0 += TILE) {
+    const int nt = min(TILE, stop - t0);
+    constexpr int VPR = D / 8;
+    for (int e = threadIdx.x; e < TILE * VPR; e += blockDim.x) {
+      const int t = e / VPR, cc = e % VPR;
+      uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+      if (t < nt) {
+        kv = *reinterpret_cast<const uint4*>(kbase + size_t(t0 + t) * tok_stride + cc * 8);
+        vv = *reinterpret_cast<const uint4*>(vbase + size_t(t0 + t) * tok_stride + cc * 8);
+      }
+      *reinterpret_cast<uint4*>(ks + t * ROWB + cc * 16) = kv;
+      *reinterpret_cast<uint4*>(vs + t * ROWB + cc * 16) = vv;
+    }
+    __syncthreads();
+    float s = -INFINITY;
+    if (lane < nt) {
+      float dot = 0.f;
+#pragma unroll
+      for (int d = 0; d < D; d += 8) {
+        float f[8];
+        unpack8(*reinterpret_cast<const uint4*>(ks + lane * ROWB + d * 2), f);
+#pragma unroll
+        for (int k = 0; k < 8; k++) dot += qf[d + k] * f[k];
+      }
+      s = dot;
+    }
+    const float mnew = fmaxf(m, wave_max(s));
+    const float p = (lane < nt) ? __expf(s - mnew) : 0.f;
+    const float corr = __expf(m - mnew);
+    l = l * corr + wave_sum(p);
+    m = mnew;
+#pragma unroll
+    for (int k = 0; k < DPL; k++) acc[k] *= corr;
+    for (int t = 0; t < nt; t++) {
+      const float pt = __shfl(p, t, kWave);
+      const uint16_t* vrow = reinterpret_cast<const uint16_t*>(vs + t * ROWB);
+#pragma unroll
+      for (int k = 0; k < DPL; k++) acc[k] += pt * bf2f(vrow[lane + k * kWave]);
+    }
+    __syncthreads();
+  }
+  const size_t hb = size_t(b) * H + kvh * G + g;
+  const int nh = blockDim.x >> 6;  // == G
+  {
+    float* po = part_o + (hb * nsplit + split) * D;
+#pragma unroll
+    for (int k = 0; k < DPL; k++) po[lane + k * kWave] = acc[k];
+    if (lane == 0) {
+      part_ml[(hb * nsplit + split) * 2 + 0] = m;
+      part_ml[(hb * nsplit + split) * 2 + 1] = l;
+    }
+  }
+  if (used == 1) {  // single split: finish directly
+    const float inv = 1.f / l;
+#pragma unroll
+    for (int k = 0; k < DPL; k++) out[hb * D + lane + k * kWave] = uint16_t(f2bf_bits(acc[k] * inv));
+    return;
+  }
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) s_ticket = atomicAdd(&counters[blockIdx.y], 1u);
+  __syncthreads();
+  if (s_ticket != unsigned(used - 1)) return;
+  __threadfence();
+  (void)nh;
+  // Merge: lanes over splits for the max / weights, lanes over head dims for the output.
+  const float* ml = part_ml + hb * nsplit * 2;
+  float M = -INFINITY;
+  for (int s = lane; s < used; s += kWave) M = fmaxf(M, __builtin_nontemporal_load(ml + 2 * s));
+  M = wave_max(M);
+  float L = 0.f, o[DPL];
+#pragma unroll
+  for (int k = 0; k < DPL; k++) o[k] = 0.f;
+  for (int s0 = 0; s0 < used; s0 += kWave) {
+    const int s = s0 + lane;
+    float ws = 0.f;
+    if (s < used) {
+      ws = __expf(__builtin_nontemporal_load(ml + 2 * s) - M);
+      L += __builtin_nontemporal_load(ml + 2 * s + 1) * ws;
+    }
+    const int n = min(kWave, used - s0);
+    const float* pob = part_o + (hb * nsplit + s0) * D + lane;
+    for (int j = 0; j < n; j++) {
+      const float wj = __shfl(ws, j, kWave);
+#pragma unroll
+      for (int k = 0; k < DPL; k++) o[k] += wj * __builtin_nontemporal_load(pob + size_t(j) * D + k * kWave);
+    }
+  }
+  L = wave_sum(L);
+  const float inv = 1.f / L;
+#pragma unroll
+  for (int k = 0; k < DPL; k++) out[hb * D + lane + k * kWave] = uint16_t(f2bf_bits(o[k] * inv));
+  __syncthreads();
+  if (threadIdx.x == 0) counters[blockIdx.y] = 0u;
+}
+
+// ------------------------------------------------------------ host side
+struct LlamaDims {
+  int vocab, dim, n_layers, H, Hkv, D, ffn, max_seq, max_batch;
+  float eps, theta;
+};
+
+constexpr int kChunk = 64;
+constexpr int kTnResid = 1, kTnStore = 2;
+
+size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+struct Workspace {
+  uint16_t *resid, *q, *attn, *h;
+  float *ss, *part_o, *part_ml, *am_val;
+  int* am_idx;
+  unsigned* counters;  // [16 * Hkv] attention tickets, then 1 argmax ticket
+  size_t bytes;
+};
+
+Workspace carve(const LlamaDims& d, uint8_t* base) {
+  Workspace w{};
+  size_t off = 0;
+  auto take = [&](size_t n) {
+    uint8_t* p = base ? base + off : nullptr;
+    off += align256(n);
+    return p;
+  };
+  const int nsplit = (d.max_seq + kChunk - 1) / kChunk;
+  const int ss_parts = d.dim / (16 * kTnResid);
+  const int am_parts = d.vocab / (16 * kTnStore);
+  w.resid = reinterpret_cast<uint16_t*>(take(size_t(kMaxM) * d.dim * 2));
+  w.q = reinterpret_cast<uint16_t*>(take(size_t(kMaxM) * d.H * d.D * 2));
+  w.attn = reinterpret_cast<uint16_t*>(take(size_t(kMaxM) * d.H * d.D * 2));
+  w.h = reinterpret_cast<uint16_t*>(take(size_t(kMaxM) * d.ffn * 2));
+  w.ss = reinterpret_cast<float*>(take(size_t(ss_parts > 1 ? ss_parts : 1) * kMaxM * 4));
+  w.part_o = reinterpret_cast<float*>(take(size_t(kMaxM) * d.H * nsplit * d.D * 4));
+  w.part_ml = reinterpret_cast<float*>(take(size_t(kMaxM) * d.H * nsplit * 2 * 4));
+  w.am_val = reinterpret_cast<float*>(take(size_t(am_parts) * kMaxM * 4));
+  w.am_idx = reinterpret_cast<int*>(take(size_t(am_parts) * kMaxM * 4));
+  w.counters = reinterpret_cast<unsigned*>(take(size_t(kMaxM * d.Hkv + 1) * 4));
+  w.bytes = off;
+  return w;
+}
+
+int pick_nw(int K) {
+  if (K >= 2048 && K % (32 * 8) == 0) return 8;
+  if (K % (32 * 4) == 0) return 4;
+  return 0;
+}
+
+template <int EPI, int TN>
+hipError_t launch_gemm(const GemmArgs& a, int grid, hipStream_t s) {
+  const int nw = pick_nw(a.K);
+  if (nw == 8)
+    hipLaunchKernelGGL((k_skinny<8, TN, EPI>), dim3(grid), dim3(512), 0, s, a);
+  else if (nw == 4)
+    hipLaunchKernelGGL((k_skinny<4, TN, EPI>), dim3(grid), dim3(256), 0, s, a);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+bool dims_ok(const LlamaDims& d) {
+  if (d.D != 64 && d.D != 128) return false;
+  if (d.H % d.Hkv || d.H / d.Hkv > 8) return false;
+  if (!pick_nw(d.dim) || !pick_nw(d.H * d.D) || !pick_nw(d.ffn)) return false;
+  if (d.dim % (16 * kTnResid) || d.vocab % (16 * kTnStore) || d.ffn % 16) return false;
+  if (d.max_batch <= 0 || d.max_seq <= 0 || d.n_layers <= 0) return false;
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Workspace bytes for p2pt_llama_decode; it must be zero-filled once before first use
+// (the in-kernel arrival counters reset themselves afterwards).
+size_t p2pt_llama_ws_bytes(const LlamaDims* d) {
+  if (!dims_ok(*d)) return 0;
+  return carve(*d, nullptr).bytes;
+}
+
+// One decode step for B <= 16 sequences (slots 0..B-1 of the caches).
+//   w: embed, final_norm, lm_head, then per layer
+//      attn_norm, wqkv [(H+2Hkv)*D, dim], wo [dim, H*D], ffn_norm, w_gate_up [2*ffn, dim], w_down [dim, ffn]
+//   k_cache/v_cache: [n_layers][max_batch][max_seq][Hkv][D]
+//   tokens int64 [B], pos int32 [B] (< max_seq), logits bf16 [B][vocab], ids int64 [B]
+//   max_len: host bound on max(pos) + 1 (sizes the attention grid; use max_seq under graph capture)
+int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, void* v_cache, const int64_t* tokens,
+                      const int* pos, int B, int max_len, void* ws, size_t ws_bytes, void* logits, int64_t* ids,
+                      void* stream) {
+  const LlamaDims d = *dp;
+  if (!dims_ok(d) || B <= 0 || B > kMaxM || B > d.max_batch || max_len <= 0 || max_len > d.max_seq)
+    return int(hipErrorInvalidValue);
+  Workspace W = carve(d, static_cast<uint8_t*>(ws));
+  if (ws_bytes < W.bytes) return int(hipErrorInvalidValue);
+  auto s = static_cast<hipStream_t>(stream);
+  auto bf = [&](int i) { return static_cast<const uint16_t*>(w[i]); };
+  const int qkv_n = (d.H + 2 * d.Hkv) * d.D;
+  const size_t layer_cache = size_t(d.max_batch) * d.max_seq * d.Hkv * d.D;
+  const int nsplit = (max_len + kChunk - 1) / kChunk;
+  const int nsplit_ws = (d.max_seq + kChunk - 1) / kChunk;
+  const float log2_theta = log2f(d.theta);
+
+  hipLaunchKernelGGL(k_embed, dim3(B), dim3(256), 0, s, bf(0), tokens, W.resid, W.ss, d.dim, d.vocab);
+  int ss_parts = 1;
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return int(e);
+
+  for (int L = 0; L < d.n_layers; L++) {
+    const uint16_t* attn_norm = bf(3 + 6 * L);
+    const uint16_t* wqkv = bf(4 + 6 * L);
+    const uint16_t* wo = bf(5 + 6 * L);
+    const uint16_t* ffn_norm = bf(6 + 6 * L);
+    const uint16_t* wgu = bf(7 + 6 * L);
+    const uint16_t* wdown = bf(8 + 6 * L);
+    uint16_t* kc = static_cast<uint16_t*>(k_cache) + L * layer_cache;
+    uint16_t* vc = static_cast<uint16_t*>(v_cache) + L * layer_cache;
+
+    GemmArgs a{};
+    a.M = B;
+    a.eps = d.eps;
+    // QKV + RoPE + cache append
+    a.x = W.resid; a.w = wqkv; a.N = qkv_n; a.K = d.dim;
+    a.norm_w = attn_norm; a.ss_part = W.ss; a.ss_parts = ss_parts;
+    a.pos = pos; a.q_out = W.q; a.kc = kc; a.vc = vc;
+    a.H = d.H; a.Hkv = d.Hkv; a.D = d.D; a.Smax = d.max_seq; a.log2_theta = log2_theta;
+    if ((e = launch_gemm<EPI_ROPE, 2>(a, qkv_n / 32, s)) != hipSuccess) return int(e);
+
+    // attention
+    dim3 grid(nsplit, B * d.Hkv);
+    dim3 blk(64 * (d.H / d.Hkv));
+    const float scale = 1.f / sqrtf(float(d.D));
+    if (d.D == 64)
+      hipLaunchKernelGGL(k_attn<64>, grid, blk, 0, s, W.q, kc, vc, pos, W.part_o, W.part_ml, W.counters, W.attn, d.H,
+                         d.Hkv, d.max_seq, kChunk, nsplit_ws, scale);
+    else
+      hipLaunchKernelGGL(k_attn<128>, grid, blk, 0, s, W.q, kc, vc, pos, W.part_o, W.part_ml, W.counters, W.attn,
+                         d.H, d.Hkv, d.max_seq, kChunk, nsplit_ws, scale);
+    if ((e = hipGetLastError()) != hipSuccess) return int(e);
+
+    // O projection + residual
+    GemmArgs o{};
+    o.M = B; o.x = W.attn; o.w = wo; o.N = d.dim; o.K = d.H * d.D;
+    o.out = W.resid; o.ss_out = W.ss;
+    if ((e = launch_gemm<EPI_RESID, kTnResid>(o, d.dim / (16 * kTnResid), s)) != hipSuccess) return int(e);
+    ss_parts = d.dim / (16 * kTnResid);
+
+    // gate/up + SwiGLU
+    GemmArgs g{};
+    g.M = B; g.eps = d.eps; g.x = W.resid; g.w = wgu; g.N = 2 * d.ffn; g.K = d.dim;
+    g.norm_w = ffn_norm; g.ss_part = W.ss; g.ss_parts = ss_parts; g.out = W.h;
+    if ((e = launch_gemm<EPI_SILU, 2>(g, d.ffn / 16, s)) != hipSuccess) return int(e);
+
+    // down + residual
+    GemmArgs dn{};
+    dn.M = B; dn.x = W.h; dn.w = wdown; dn.N = d.dim; dn.K = d.ffn; dn.out = W.resid; dn.ss_out = W.ss;
+    if ((e = launch_gemm<EPI_RESID, kTnResid>(dn, d.dim / (16 * kTnResid), s)) != hipSuccess) return int(e);
+  }
+
+  // final norm + LM head + argmax
+  GemmArgs h{};
+  h.M = B; h.eps = d.eps; h.x = W.resid; h.w = bf(2); h.N = d.vocab; h.K = d.dim;
+  h.norm_w = bf(1); h.ss_part = W.ss; h.ss_parts = ss_parts;
+  h.out = static_cast<uint16_t*>(logits);
+  h.am_val = W.am_val; h.am_idx = W.am_idx; h.am_count = W.counters + kMaxM * d.Hkv; h.ids = ids;
+  if ((e = launch_gemm<EPI_ARGMAX, kTnStore>(h, d.vocab / (16 * kTnStore), s)) != hipSuccess) return int(e);
+  return int(hipSuccess);
+}
+
+// Standalone skinny GEMM (tests/benchmarks): out[M][N] = bf16(x[M][K] @ w[N][K]^T), M <= 16.
+int p2pt_skinny_gemm(const void* x, const void* w, void* out, int M, int N, int K, void* stream) {
+  if (M <= 0 || M > kMaxM || N % 32 || !pick_nw(K)) return int(hipErrorInvalidValue);
+  GemmArgs a{};
+  a.x = static_cast<const uint16_t*>(x);
+  a.w = static_cast<const uint16_t*>(w);
+  a.out = static_cast<uint16_t*>(out);
+  a.M = M; a.N = N; a.K = K;
+  return int(launch_gemm<EPI_STORE, 2>(a, N / 32, static_cast<hipStream_t>(stream)));
+}
+
+}  // extern "C"

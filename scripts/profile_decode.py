@@ -4,7 +4,9 @@
 
 Fills the KV cache with random values up to `ctx`, then times `steps`
 batched decode steps through the HIP kernels — replayed from a captured
-hipGraph by default, or launched eagerly with --eager — and prints tokens/s.
+hipGraph by default, or launched eagerly with --eager; the fused step
+(decode_fused.hip) by default, the unfused kernels + hipBLASLt with
+--unfused — and prints tokens/s.
 """
 from __future__ import annotations
 
@@ -29,8 +31,9 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--eager", action="store_true")
+    ap.add_argument("--unfused", action="store_true", help="kernels.hip + hipBLASLt path instead of decode_fused.hip")
     a = ap.parse_args()
-    m = TinyLlama(a.config, device="cuda", max_batch=a.batch)
+    m = TinyLlama(a.config, device="cuda", max_batch=a.batch, fused=not a.unfused)
     m.k_cache.normal_()
     m.v_cache.normal_()
     if not a.eager:
@@ -50,7 +53,7 @@ def main():
         tok = step(a.ctx + a.warmup + i)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    print(json.dumps({"config": a.config, "batch": B, "ctx": a.ctx, "steps": a.steps, "graph": not a.eager,
+    print(json.dumps({"config": a.config, "batch": B, "ctx": a.ctx, "steps": a.steps, "graph": not a.eager, "fused": not a.unfused,
                       "ms_per_step": dt * 1e3 / a.steps, "tokens_per_s": B * a.steps / dt}))
 
 

@@ -12,10 +12,11 @@ cuda = pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a HIP dev
 
 
 @cuda
+@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("cfg", ["micro", "tiny"])
-def test_decode_matches_fp32_reference(cfg):
+def test_decode_matches_fp32_reference(cfg, fused):
     from p2p_llm_tunnel_amd.models.tiny_llm import TinyLlama
-    m = TinyLlama(cfg, device="cuda", max_batch=3, seed=1)
+    m = TinyLlama(cfg, device="cuda", max_batch=3, seed=1, fused=fused)
     torch.manual_seed(0)
     T = 37
     seqs = torch.randint(0, m.cfg.vocab, (3, T), device="cuda")
@@ -31,6 +32,48 @@ def test_decode_matches_fp32_reference(cfg):
     top2 = ref.topk(2, -1).values
     confident = (top2[:, 0] - top2[:, 1]) > 0.05 * scale
     assert torch.equal(logits.float().argmax(-1)[confident], ref.argmax(-1)[confident])
+
+
+@cuda
+@pytest.mark.parametrize("cfg,B", [("micro", 5), ("tiny", 8), ("small", 2)])
+def test_fused_matches_unfused(cfg, B):
+    # Same weights, same token stream: the fused 5-kernels-per-layer step and the
+    # unfused kernels + hipBLASLt path agree on logits, caches and greedy ids.
+    from p2p_llm_tunnel_amd.models.tiny_llm import TinyLlama
+    mf = TinyLlama(cfg, device="cuda", max_batch=B, seed=4, fused=True)
+    mu = TinyLlama(cfg, device="cuda", max_batch=B, seed=4, fused=False)
+    torch.manual_seed(1)
+    T = 70  # crosses a 64-token attention split
+    seqs = torch.randint(0, mf.cfg.vocab, (B, T), device="cuda")
+    for p in range(T):
+        pos = torch.full((B,), p, dtype=torch.int32, device="cuda")
+        idf, lf = mf.decode_step(seqs[:, p], pos, (p, p), return_logits=True)
+        idu, lu = mu.decode_step(seqs[:, p], pos, (p, p), return_logits=True)
+    scale = lu.float().abs().max().item()
+    assert (lf.float() - lu.float()).abs().max().item() < 0.03 * scale
+    top2 = lu.float().topk(2, -1).values
+    confident = (top2[:, 0] - top2[:, 1]) > 0.03 * scale
+    assert torch.equal(idf[confident], idu[confident])
+    kdiff = (mf.k_cache[:, :B, :T].float() - mu.k_cache[:, :B, :T].float()).abs().max().item()
+    assert kdiff < 0.05 * mu.k_cache[:, :B, :T].float().abs().max().item()
+
+
+@cuda
+def test_fused_ragged_positions():
+    # Slots at different positions in one step (continuous batching).
+    from p2p_llm_tunnel_amd.models.tiny_llm import TinyLlama
+    mf = TinyLlama("micro", device="cuda", max_batch=4, seed=6, fused=True)
+    mu = TinyLlama("micro", device="cuda", max_batch=4, seed=6, fused=False)
+    torch.manual_seed(2)
+    mf.k_cache.normal_()
+    mf.v_cache.normal_()
+    mu.k_cache.copy_(mf.k_cache)
+    mu.v_cache.copy_(mf.v_cache)
+    toks = torch.randint(0, mf.cfg.vocab, (4,), device="cuda")
+    pos = torch.tensor([0, 63, 64, 300], dtype=torch.int32, device="cuda")
+    _, lf = mf.decode_step(toks, pos, (0, 300), return_logits=True)
+    _, lu = mu.decode_step(toks, pos, (0, 300), return_logits=True)
+    assert (lf.float() - lu.float()).abs().max().item() < 0.03 * lu.float().abs().max().item()
 
 
 @cuda

@@ -131,6 +131,26 @@ def test_argmax(ops, V):
 
 
 @cuda
+@pytest.mark.parametrize("M,N,K", [(1, 1536, 1024), (8, 2048, 2816), (16, 32000, 1024), (3, 64, 256), (16, 96, 4096)])
+def test_skinny_gemm(ops, M, N, K):
+    # Asymmetric operands: a transposed C write would not pass.
+    torch.manual_seed(M * 7 + K)
+    x = bf(torch.randn(M, K, device="cuda"))
+    w = bf(torch.randn(N, K, device="cuda") / math.sqrt(K))
+    got = ops.skinny_gemm(x, w)
+    ref = x.float() @ w.float().T
+    err = (got.float() - ref).abs().max().item()
+    assert err <= 0.01 * ref.abs().max().item() + 1e-3, err
+    # exact-integer check of the fragment layout (row/col mapping)
+    xi = bf(torch.randint(-3, 4, (M, K), device="cuda").float())
+    wi = bf(torch.randint(-3, 4, (N, K), device="cuda").float())
+    ref_i = (xi.float() @ wi.float().T)
+    got_i = ops.skinny_gemm(xi, wi).float()
+    exact = ref_i.abs() <= 256  # bf16 represents these integers exactly
+    assert torch.equal(got_i[exact], ref_i[exact])
+
+
+@cuda
 def test_host_side_shape_checks(ops):
     q = bf(torch.randn(2, 8, 64, device="cuda"))
     kc = bf(torch.randn(2, 10, 2, 64, device="cuda"))
@@ -141,6 +161,10 @@ def test_host_side_shape_checks(ops):
     with pytest.raises(ValueError):
         ops.rope_qkv_cache(bf(torch.randn(2, 5, device="cuda")), torch.zeros(2, dtype=torch.int32, device="cuda"),
                            kc, kc, 8, 2, 64)
+    with pytest.raises(ValueError):
+        ops.skinny_gemm(bf(torch.randn(17, 128, device="cuda")), bf(torch.randn(32, 128, device="cuda")))  # M > 16
+    with pytest.raises(ValueError):
+        ops.skinny_gemm(bf(torch.randn(2, 100, device="cuda")), bf(torch.randn(32, 100, device="cuda")))  # K % 128
 
 
 @cuda
