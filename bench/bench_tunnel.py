@@ -36,6 +36,8 @@ def sse_matrix(transport, mock_kind, streams_list, steps, threaded=True):
             for s in streams_list:
                 loadgen(t.proxy_port, s, 1)
                 tr = loadgen(t.proxy_port, s, steps)
+                if not threaded:
+                    time.sleep(1.3)  # let serve's spare upstream sockets expire (single-threaded upstream)
                 dr = loadgen(port, s, steps)
                 rows.append({"transport": transport, "mock": mock_kind if threaded else "python-unthreaded",
                              "streams": s, "tunneled_req_s": tr["req_s"], "direct_req_s": dr["req_s"],

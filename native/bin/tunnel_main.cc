@@ -80,6 +80,8 @@ const std::vector<Opt>& ext_opts() {
        "Keep polling for N us after I/O instead of sleeping (lower per-hop latency, more CPU)"},
       {"upstream-prewarm", "TUNNEL_UPSTREAM_PREWARM", "4",
        "serve: spare pre-connected upstream sockets (follows peak concurrency; 0=off)"},
+      {"upstream-prewarm-ttl-ms", "TUNNEL_UPSTREAM_PREWARM_TTL_MS", "1000",
+       "serve: close a spare upstream socket unused for this long"},
   };
   return o;
 }
@@ -238,6 +240,7 @@ int main(int argc, char** argv) {
   cfg.listen_early = m.count("listen-early") > 0;
   cfg.metrics_listen = m["metrics-listen"];
   cfg.upstream_prewarm = num(m, "upstream-prewarm");
+  cfg.upstream_prewarm_ttl_ms = num(m, "upstream-prewarm-ttl-ms");
   cfg.busy_poll_us = num(m, "busy-poll-us");
 
   if (cmd == "serve") {

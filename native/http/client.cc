@@ -11,7 +11,10 @@ namespace p2pt::http {
 // (the reference's mock, many simple servers) close after every response, so
 // keep-alive never helps them; a warm socket takes the TCP (and TLS)
 // handshake off every request's time-to-first-token. The warm target follows
-// the recent peak of concurrent requests (>= the configured minimum).
+// the recent peak of concurrent requests (>= the configured minimum) and is
+// topped up only when requests arrive. An unused warm socket is closed after
+// an idle TTL: a single-threaded upstream serves one connection at a time and
+// would otherwise sit blocked on our idle socket, starving its other clients.
 using WarmWaiter = std::function<bool(std::shared_ptr<TcpConn>, const std::string&)>;
 
 class ClientConnPool : public std::enable_shared_from_this<ClientConnPool> {
@@ -38,17 +41,56 @@ class ClientConnPool : public std::enable_shared_from_this<ClientConnPool> {
     size_t connecting = 0;
     int failures = 0;
     uint64_t retry_timer = 0;
+    uint64_t ttl_ms = 1000;
+    uint64_t expiry_timer = 0;
     std::vector<std::shared_ptr<TcpConn>> ready;
+    std::vector<uint64_t> ready_at;  // parallel to ready
     std::deque<WarmWaiter> waiters;  // calls waiting for the next warm socket
   };
 
-  void configure_warm(const std::string& key, const std::string& host, uint16_t port, bool tls, size_t min) {
+  void configure_warm(const std::string& key, const std::string& host, uint16_t port, bool tls, size_t min,
+                      uint64_t ttl_ms) {
     Warm& w = warm_[key];
     w.host = host;
     w.port = port;
     w.tls = tls;
     w.min = min;
+    w.ttl_ms = ttl_ms ? ttl_ms : 1;
     replenish(key);
+  }
+
+  void erase_ready(Warm& w, size_t i) {
+    w.ready.erase(w.ready.begin() + long(i));
+    w.ready_at.erase(w.ready_at.begin() + long(i));
+  }
+
+  // Close warm sockets idle for longer than the TTL (oldest first; ready is in
+  // connect order, so expired ones sit at the front).
+  void schedule_expiry(const std::string& key) {
+    auto it = warm_.find(key);
+    if (it == warm_.end()) return;
+    Warm& w = it->second;
+    if (w.expiry_timer || w.ready.empty()) return;
+    uint64_t now = Reactor::now_ms();
+    uint64_t due = w.ready_at.front() + w.ttl_ms;
+    std::weak_ptr<ClientConnPool> self = shared_from_this();
+    w.expiry_timer = r_.call_later_ms(due > now ? due - now : 0, [self, key] {
+      auto p = self.lock();
+      if (!p) return;
+      auto it2 = p->warm_.find(key);
+      if (it2 == p->warm_.end()) return;
+      Warm& w2 = it2->second;
+      w2.expiry_timer = 0;
+      uint64_t t = Reactor::now_ms();
+      while (!w2.ready.empty() && w2.ready_at.front() + w2.ttl_ms <= t) {
+        auto c = w2.ready.front();
+        p->erase_ready(w2, 0);
+        c->on_data(nullptr);
+        c->on_close(nullptr);
+        c->close();
+      }
+      p->schedule_expiry(key);
+    });
   }
   bool has_warm(const std::string& key) const { return warm_.count(key) != 0; }
 
@@ -71,11 +113,11 @@ class ClientConnPool : public std::enable_shared_from_this<ClientConnPool> {
     // Oldest first: a single-threaded upstream (the reference's own mock)
     // accepts connections in connect order and blocks reading the first one,
     // so handing out a newer warm socket would wait behind an idle one forever.
-    auto& v = it->second.ready;
+    Warm& w = it->second;
     std::shared_ptr<TcpConn> c;
-    while (!v.empty()) {
-      c = v.front();
-      v.erase(v.begin());
+    while (!w.ready.empty()) {
+      c = w.ready.front();
+      erase_ready(w, 0);
       if (!c->closed()) break;
       c.reset();
     }
@@ -154,7 +196,7 @@ class ClientConnPool : public std::enable_shared_from_this<ClientConnPool> {
         }
         std::weak_ptr<TcpConn> wc = c;
         // A warm socket that turns readable/closed was dropped by the server
-        // (idle timeout): discard it and top up again.
+        // (its idle timeout): discard it; the next request tops the pool up.
         auto drop = [self, key, wc] {
           auto p2 = self.lock();
           auto conn = wc.lock();
@@ -164,18 +206,17 @@ class ClientConnPool : public std::enable_shared_from_this<ClientConnPool> {
           auto& v = it3->second.ready;
           for (size_t i = 0; i < v.size(); i++)
             if (v[i] == conn) {
-              v.erase(v.begin() + long(i));
+              p2->erase_ready(it3->second, i);
               break;
             }
           conn->on_close(nullptr);
           conn->close();
-          p2->r_.post([self, key] {
-            if (auto p3 = self.lock()) p3->replenish(key);
-          });
         };
         c->on_data([drop](const uint8_t*, size_t) { drop(); });
         c->on_close([drop](const std::string&) { drop(); });
         w2.ready.push_back(std::move(c));
+        w2.ready_at.push_back(Reactor::now_ms());
+        p->schedule_expiry(key);
       });
     }
   }
@@ -223,6 +264,7 @@ class ClientConnPool : public std::enable_shared_from_this<ClientConnPool> {
     warm_.clear();
     for (auto& kv : warm) {
       if (kv.second.retry_timer) r_.cancel(kv.second.retry_timer);
+      if (kv.second.expiry_timer) r_.cancel(kv.second.expiry_timer);
       if (!kv.second.waiters.empty())
         r_.post([ws = std::move(kv.second.waiters)]() mutable {
           for (auto& fn : ws) fn(nullptr, "client shut down");
@@ -248,14 +290,15 @@ HttpClient::HttpClient(Reactor& r) : r_(r), pool_(std::make_shared<ClientConnPoo
 HttpClient::~HttpClient() { pool_->clear(); }
 size_t HttpClient::idle_connections() const { return pool_->idle(); }
 
-bool HttpClient::prewarm(const std::string& url, size_t min_ready, std::string* err) {
+bool HttpClient::prewarm(const std::string& url, size_t min_ready, uint64_t idle_ttl_ms, std::string* err) {
   Url u;
   if (!parse_url(url, u, err)) return false;
   if (u.scheme != "http" && u.scheme != "https") {
     if (err) *err = "unsupported scheme";
     return false;
   }
-  pool_->configure_warm(u.scheme + "://" + u.host + ":" + std::to_string(u.port), u.host, u.port, u.tls(), min_ready);
+  pool_->configure_warm(u.scheme + "://" + u.host + ":" + std::to_string(u.port), u.host, u.port, u.tls(), min_ready,
+                        idle_ttl_ms);
   return true;
 }
 

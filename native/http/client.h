@@ -88,7 +88,7 @@ class HttpClient {
   size_t idle_connections() const;
   // Keep >= min_ready established spare connections to url's origin (grows to
   // the recent peak concurrency, max 64). 0 disables.
-  bool prewarm(const std::string& url, size_t min_ready, std::string* err = nullptr);
+  bool prewarm(const std::string& url, size_t min_ready, uint64_t idle_ttl_ms = 1000, std::string* err = nullptr);
   size_t warm_connections(const std::string& url) const;
 
  private:

@@ -232,6 +232,7 @@ int run_app(const AppConfig& cfg) {
         sc.ping_interval_ms = cfg.ping_interval_ms;
         sc.pong_timeout_ms = cfg.pong_timeout_ms;
         sc.upstream_prewarm = cfg.upstream_prewarm;
+        sc.upstream_prewarm_ttl_ms = cfg.upstream_prewarm_ttl_ms;
         st.serve = ServeSession::start(r, ch, sc, [&](const std::string& e) { on_fail(e); });
       } else {
         LOG_INFO(kT, "WebRTC connected, starting proxy...");

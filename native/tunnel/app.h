@@ -57,6 +57,7 @@ struct AppConfig {
   bool listen_early = false;
   std::string metrics_listen;
   size_t upstream_prewarm = 4;
+  uint64_t upstream_prewarm_ttl_ms = 1000;
   uint64_t busy_poll_us = 0;
 };
 

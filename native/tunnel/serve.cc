@@ -135,7 +135,7 @@ void ServeSession::on_hello(const proto::Frame& f) {
   LOG_INFO(kT, "sent AGREE, tunnel ready");
   if (cfg_.upstream_prewarm) {
     std::string perr;
-    if (!client_.prewarm(cfg_.upstream, cfg_.upstream_prewarm, &perr))
+    if (!client_.prewarm(cfg_.upstream, cfg_.upstream_prewarm, cfg_.upstream_prewarm_ttl_ms, &perr))
       LOG_DEBUG(kT, "upstream prewarm disabled: %s", perr.c_str());
   }
   last_pong_ms_ = Reactor::now_ms();

@@ -38,6 +38,7 @@ struct ServeConfig {
   size_t low_water = 1 << 20;
   // Spare pre-connected upstream sockets (0 = connect per request like reqwest).
   size_t upstream_prewarm = 4;
+  uint64_t upstream_prewarm_ttl_ms = 1000;  // close unused warm sockets after this idle time
 };
 
 class ServeSession : public std::enable_shared_from_this<ServeSession> {

@@ -182,6 +182,10 @@ def test_single_threaded_upstream(transport):
             with concurrent.futures.ThreadPoolExecutor(6) as ex:
                 outs = list(ex.map(lambda _: get(t.url + "/v1/models", timeout=10)[2], range(6)))
             assert all(b"test-model" in o for o in outs)
+            # Spare upstream sockets expire after their idle TTL (1 s), so other
+            # clients of the single-threaded upstream are not starved.
+            time.sleep(1.3)
+            assert get(f"http://127.0.0.1:{port}/health", timeout=3)[2] == b"ok"
     finally:
         srv.shutdown()
         srv.server_close()
