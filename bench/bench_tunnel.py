@@ -28,11 +28,12 @@ from p2p_llm_tunnel_amd.utils.build import ensure_native  # noqa: E402
 from p2p_llm_tunnel_amd.utils.procs import Tunnel  # noqa: E402
 
 
-def sse_matrix(transport, mock_kind, streams_list, steps, threaded=True):
+def sse_matrix(transport, mock_kind, streams_list, steps, threaded=True, busy_poll_us=0):
     mock, port = start_mock(mock_kind, 100, 5) if (mock_kind == "native" or threaded) else _unthreaded()
     rows = []
+    extra = ["--busy-poll-us", str(busy_poll_us)] if busy_poll_us else []
     try:
-        with Tunnel(f"http://127.0.0.1:{port}", transport=transport) as t:
+        with Tunnel(f"http://127.0.0.1:{port}", transport=transport, serve_extra=extra, proxy_extra=extra) as t:
             for s in streams_list:
                 loadgen(t.proxy_port, s, 1)
                 tr = loadgen(t.proxy_port, s, steps)
@@ -40,6 +41,7 @@ def sse_matrix(transport, mock_kind, streams_list, steps, threaded=True):
                     time.sleep(1.3)  # let serve's spare upstream sockets expire (single-threaded upstream)
                 dr = loadgen(port, s, steps)
                 rows.append({"transport": transport, "mock": mock_kind if threaded else "python-unthreaded",
+                             "busy_poll_us": busy_poll_us,
                              "streams": s, "tunneled_req_s": tr["req_s"], "direct_req_s": dr["req_s"],
                              "tunneled_p50_ttft_ms": tr["p50_ttft_ms"], "direct_p50_ttft_ms": dr["p50_ttft_ms"],
                              "added_p50_ttft_ms": tr["p50_ttft_ms"] - dr["p50_ttft_ms"],
@@ -109,6 +111,7 @@ def main():
     ap.add_argument("--idle-s", type=float, default=30)
     ap.add_argument("--out", default=None)
     ap.add_argument("--quick", action="store_true", help="native mock + webrtc only")
+    ap.add_argument("--busy-poll", default="", help="comma-separated busy-poll µs values to add as extra SSE rows")
     a = ap.parse_args()
     ensure_native()
     res = {"host": os.uname().nodename, "time": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()), "sse": []}
@@ -118,6 +121,8 @@ def main():
         res["sse"] += sse_matrix("tcp", "native", streams, a.steps)
         res["sse"] += sse_matrix("webrtc", "python", streams, a.steps)
         res["sse"] += sse_matrix("webrtc", "python", [1, 2, 4, 8], 3, threaded=False)
+    for bp in [int(x) for x in a.busy_poll.split(",") if x]:
+        res["sse"] += sse_matrix("webrtc", "native", [1, 8], a.steps, busy_poll_us=bp)
     res["post_64x1MB"] = [post_1mb("webrtc")]
     if not a.quick:
         res["post_64x1MB"].append(post_1mb("tcp"))

@@ -179,24 +179,28 @@ void SctpAssociation::connect() {
   if (state_ != State::Closed) return;
   state_ = State::CookieWait;
   init_tries_ = 0;
-  std::weak_ptr<SctpAssociation> w = shared_from_this();
-  auto retry = std::make_shared<std::function<void()>>();
-  *retry = [w, retry] {
-    auto s = w.lock();
-    if (!s) return;
-    s->init_timer_ = 0;
-    if (s->state_ != State::CookieWait && s->state_ != State::CookieEchoed) return;
-    if (++s->init_tries_ > s->cfg_.max_init_retrans) {
-      s->closed("SCTP association setup timed out");
-      return;
-    }
-    if (s->state_ == State::CookieWait) s->send_init();
-    else s->send_control(kCookieEcho, 0, s->cookie_echo_, s->peer_vtag_);
-    uint64_t t = std::min<uint64_t>(s->cfg_.rto_initial_ms << std::min(s->init_tries_, 4), 5000);
-    s->init_timer_ = s->r_.call_later_ms(std::min<uint64_t>(t, 5000), *retry);
-  };
   send_init();
-  init_timer_ = r_.call_later_ms(cfg_.rto_initial_ms, *retry);
+  std::weak_ptr<SctpAssociation> w = shared_from_this();
+  init_timer_ = r_.call_later_ms(cfg_.rto_initial_ms, [w] {
+    if (auto s = w.lock()) s->on_init_timer();
+  });
+}
+
+// INIT / COOKIE-ECHO retransmission with exponential backoff (RFC 9260 §5.1, T1).
+void SctpAssociation::on_init_timer() {
+  init_timer_ = 0;
+  if (state_ != State::CookieWait && state_ != State::CookieEchoed) return;
+  if (++init_tries_ > cfg_.max_init_retrans) {
+    closed("SCTP association setup timed out");
+    return;
+  }
+  if (state_ == State::CookieWait) send_init();
+  else send_control(kCookieEcho, 0, cookie_echo_, peer_vtag_);
+  uint64_t t = std::min<uint64_t>(cfg_.rto_initial_ms << std::min(init_tries_, 4), 5000);
+  std::weak_ptr<SctpAssociation> w = shared_from_this();
+  init_timer_ = r_.call_later_ms(t, [w] {
+    if (auto s = w.lock()) s->on_init_timer();
+  });
 }
 
 std::string SctpAssociation::make_cookie(uint32_t peer_tag, uint32_t peer_tsn, uint32_t peer_rwnd, uint16_t peer_os,

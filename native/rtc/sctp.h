@@ -110,6 +110,7 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   std::string make_cookie(uint32_t peer_tag, uint32_t peer_tsn, uint32_t peer_rwnd, uint16_t peer_os, uint16_t peer_mis);
   void append_init_params(std::vector<uint8_t>& v);
   void send_init();
+  void on_init_timer();
   void send_control(uint8_t type, uint8_t flags, const std::vector<uint8_t>& body, uint32_t vtag);
   void queue_control(uint8_t type, uint8_t flags, std::vector<uint8_t> body);
   void build_sack(std::vector<uint8_t>& body);

@@ -118,6 +118,7 @@ class TinyLlama:
     def _decode_impl(self, tokens, pos, pos_range, max_len):
         B = tokens.shape[0]
         if self.fused and B <= 16:
+            tokens, pos = tokens.contiguous(), pos.contiguous()
             logits = torch.empty(B, self.cfg.vocab, dtype=torch.bfloat16, device=self.device)
             ids = torch.empty(B, dtype=torch.int64, device=self.device)
             self.fused_decoder().step(tokens, pos, max_len, logits, ids)
