@@ -55,12 +55,14 @@ struct Server {
     Reactor* rp = &r;
     uint64_t iv = interval_ms;
     int n = tokens;
-    *step = [w, rp, iv, n, step](int i) {
+    // The pending timer owns the step; the step refers to itself weakly.
+    std::weak_ptr<std::function<void(int)>> ws = step;
+    *step = [w, rp, iv, n, ws](int i) {
       auto conn = w.lock();
       if (!conn || conn->closed()) return;
       if (i < n) {
         conn->write(chunk_event(i < 5 ? kTokens[i] : " tok"));
-        rp->call_later_ms(iv, [step, i] { (*step)(i + 1); });
+        if (auto s = ws.lock()) rp->call_later_ms(iv, [s, i] { (*s)(i + 1); });
         return;
       }
       conn->write(chunk_event(nullptr) + "data: [DONE]\n\n");

@@ -80,34 +80,32 @@ void TurnClient::send_request(stun::Message m, std::function<void(const stun::Me
   pd.bytes = b;
   pd.tries = 1;
   raw_send(b.data(), b.size());
+  arm_retransmit(tid, 500);
+}
+
+// STUN request retransmission: RTO doubling from 500 ms (capped at 3.2 s), 6 tries.
+void TurnClient::arm_retransmit(const std::string& tid, uint64_t rto) {
+  auto it = pending_.find(tid);
+  if (it == pending_.end()) return;
   std::weak_ptr<TurnClient> w = shared_from_this();
-  std::function<void(uint64_t)> arm;
-  auto rearm = std::make_shared<std::function<void(uint64_t)>>();
-  *rearm = [w, tid, rearm, this](uint64_t rto) {
+  it->second.timer = r_.call_later_ms(rto, [w, tid, rto] {
     auto s = w.lock();
     if (!s) return;
-    auto it = pending_.find(tid);
-    if (it == pending_.end()) return;
-    it->second.timer = r_.call_later_ms(rto, [w, tid, rto, rearm, this] {
-      auto s2 = w.lock();
-      if (!s2) return;
-      auto it2 = pending_.find(tid);
-      if (it2 == pending_.end()) return;
-      if (it2->second.tries >= 6) {
-        auto cb2 = std::move(it2->second.cb);
-        pending_.erase(it2);
-        LOG_WARN(kT, "TURN request timed out");
-        stun::Message none;
-        none.type = 0;
-        if (cb2) cb2(none, nullptr, 0);
-        return;
-      }
-      it2->second.tries++;
-      raw_send(it2->second.bytes.data(), it2->second.bytes.size());
-      (*rearm)(std::min<uint64_t>(rto * 2, 3200));
-    });
-  };
-  (*rearm)(500);
+    auto it2 = s->pending_.find(tid);
+    if (it2 == s->pending_.end()) return;
+    if (it2->second.tries >= 6) {
+      auto cb2 = std::move(it2->second.cb);
+      s->pending_.erase(it2);
+      LOG_WARN(kT, "TURN request timed out");
+      stun::Message none;
+      none.type = 0;
+      if (cb2) cb2(none, nullptr, 0);
+      return;
+    }
+    it2->second.tries++;
+    s->raw_send(it2->second.bytes.data(), it2->second.bytes.size());
+    s->arm_retransmit(tid, std::min<uint64_t>(rto * 2, 3200));
+  });
 }
 
 void TurnClient::allocate() {

@@ -39,6 +39,7 @@ class TurnClient : public std::enable_shared_from_this<TurnClient> {
   TurnClient(Reactor& r, IceAgent* agent, int sock) : r_(r), agent_(agent), sock_(sock) {}
   void send_request(stun::Message m, std::function<void(const stun::Message&, const uint8_t*, size_t)> on_resp);
   void allocate();
+  void arm_retransmit(const std::string& tid, uint64_t rto);
   void refresh(uint32_t lifetime);
   void create_permission(const SockAddr& peer);
   void channel_bind(const SockAddr& peer);

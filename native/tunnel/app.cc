@@ -29,6 +29,7 @@ struct TcpLink {
   uint64_t retry_timer = 0;
   Reactor* r = nullptr;
   bool done = false;
+  std::shared_ptr<std::function<void()>> attempt;  // tcp-connect retry loop (owned here, weakly self-referenced)
   ~TcpLink() {
     if (retry_timer && r) r->cancel(retry_timer);
     if (ch) ch->close();
@@ -77,17 +78,21 @@ std::shared_ptr<void> connect_tcp(Reactor& r, const std::string& spec, ConnectCb
     if (host.size() > 1 && host.front() == '[') host = host.substr(1, host.size() - 2);
     auto deadline = Reactor::now_ms() + 30000;
     auto attempt = std::make_shared<std::function<void()>>();
+    link->attempt = attempt;
+    std::weak_ptr<std::function<void()>> wa = attempt;
     Reactor* rp = &r;
-    *attempt = [w, rp, host, port, deliver, deadline, attempt] {
-      TcpConn::connect(*rp, host, port, false, [w, rp, deliver, deadline, attempt](std::shared_ptr<TcpConn> c, std::string e) {
+    *attempt = [w, rp, host, port, deliver, deadline, wa] {
+      TcpConn::connect(*rp, host, port, false, [w, rp, deliver, deadline, wa](std::shared_ptr<TcpConn> c, std::string e) {
         auto l = w.lock();
         if (!l || l->done) return;
         if (!c) {
           if (Reactor::now_ms() < deadline) {
-            l->retry_timer = rp->call_later_ms(100, [w, attempt] {
-              if (auto l2 = w.lock()) {
+            l->retry_timer = rp->call_later_ms(100, [w, wa] {
+              auto l2 = w.lock();
+              auto a = wa.lock();
+              if (l2 && a) {
                 l2->retry_timer = 0;
-                (*attempt)();
+                (*a)();
               }
             });
             return;

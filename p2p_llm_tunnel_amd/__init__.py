@@ -20,7 +20,9 @@ __version__ = "0.2.0"
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_ROOT = os.path.dirname(PKG_DIR)
-BIN_DIR = os.path.join(REPO_ROOT, "build", "bin")
+# P2PT_BIN_DIR points the harness at another build (e.g. build-asan/bin to run
+# the end-to-end suite against sanitizer binaries).
+BIN_DIR = os.path.abspath(os.environ.get("P2PT_BIN_DIR") or os.path.join(REPO_ROOT, "build", "bin"))
 
 
 def native():
