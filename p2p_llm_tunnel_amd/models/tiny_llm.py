@@ -109,9 +109,15 @@ class TinyLlama:
             dims = ops.LlamaDims(vocab=c.vocab, dim=c.dim, n_layers=c.n_layers, H=c.n_heads, Hkv=c.n_kv_heads,
                                  D=c.head_dim, ffn=c.ffn, max_seq=c.max_seq, max_batch=self.max_batch, eps=c.eps,
                                  theta=c.rope_theta)
-            ws = [self.embed, self.final_norm, self.lm_head]
+            # The fused GEMMs take the RMSNorm weight folded into the following
+            # projection's columns (W[n][k] * g[k]); see decode_fused.hip.
+            def fold(w, g):
+                return (w.float() * g.float()[None, :]).to(torch.bfloat16)
+
+            ws = [self.embed, self.final_norm, fold(self.lm_head, self.final_norm)]
             for L in self.layers:
-                ws += [L[k] for k in ("attn_norm", "wqkv", "wo", "ffn_norm", "w_gate_up", "w_down")]
+                ws += [L["attn_norm"], fold(L["wqkv"], L["attn_norm"]), L["wo"], L["ffn_norm"],
+                       fold(L["w_gate_up"], L["ffn_norm"]), L["w_down"]]
             self._fused = ops.FusedLlamaDecoder(dims, ws, self.k_cache, self.v_cache)
         return self._fused
 

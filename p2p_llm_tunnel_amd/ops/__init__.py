@@ -204,8 +204,8 @@ def skinny_gemm(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         raise ValueError("shapes must be x [M, K], w [N, K]")
     M, K = x.shape
     N = w.shape[0]
-    if not 1 <= M <= 16 or N % 32 or K % 128:
-        raise ValueError("need 1 <= M <= 16, N % 32 == 0, K % 128 == 0")
+    if not 1 <= M <= 16 or N % 32 or K % 32:
+        raise ValueError("need 1 <= M <= 16, N % 32 == 0, K % 32 == 0")
     out = torch.empty(M, N, dtype=x.dtype, device=x.device)
     _ok(lib().p2pt_skinny_gemm(_p(x), _p(w), _p(out), M, N, K, _stream(x)), "skinny_gemm")
     return out
@@ -230,7 +230,8 @@ class FusedLlamaDecoder:
         _check(k_cache, torch.bfloat16, "k_cache", dev)
         _check(v_cache, torch.bfloat16, "v_cache", dev)
         if len(weights) != 3 + 6 * dims.n_layers:
-            raise ValueError("weight table: embed, final_norm, lm_head, then 6 per layer")
+            raise ValueError("weight table: embed, final_norm, lm_head, then 6 per layer "
+                             "(wqkv, w_gate_up and lm_head with the preceding norm weight folded in)")
         nbytes = lib().p2pt_llama_ws_bytes(ctypes.byref(dims))
         if nbytes == 0:
             raise ValueError("model dims not supported by the fused decode kernels")

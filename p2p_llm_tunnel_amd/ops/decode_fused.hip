@@ -8,15 +8,15 @@
 //
 //   k_embed              token gather -> residual stream, per-row sum of squares
 //   per layer:
-//     k_skinny<ROPE>     RMSNorm prologue (attn_norm) -> QKV GEMM -> RoPE on q/k,
+//     k_skinny<ROPE>     RMSNorm (attn_norm) -> QKV GEMM -> RoPE on q/k,
 //                        q to the attention buffer, k/v appended to the cache
 //     k_attn             GQA flash-decoding split-K; the last split to finish
 //                        for a (sequence, KV head) merges the partials in-kernel
 //     k_skinny<RESID>    O projection -> residual add -> per-row sum-of-squares
 //                        partials for the next norm
-//     k_skinny<SILU>     RMSNorm prologue (ffn_norm) -> gate/up GEMM -> SwiGLU
+//     k_skinny<SILU>     RMSNorm (ffn_norm) -> gate/up GEMM -> SwiGLU
 //     k_skinny<RESID>    down projection -> residual add -> sum-of-squares
-//   k_skinny<ARGMAX>     RMSNorm prologue (final norm) -> LM head -> logits and
+//   k_skinny<ARGMAX>     RMSNorm (final norm) -> LM head -> logits and
 //                        greedy argmax (last block merges the per-block winners)
 //
 // Skinny GEMM (M <= 16 tokens): Y[M,N] = A[M,K] * W[N,K]^T on
@@ -24,14 +24,18 @@
 // over its NW waves; each lane streams its weight rows with 16-byte loads
 // straight into MFMA B fragments (no LDS staging: every weight byte is used
 // exactly once, by exactly one lane), the K-split partials are summed through
-// LDS and wave 0 runs the epilogue. Row RMSNorm needs the whole row, so the
-// producer of the residual writes per-block partial sums of squares and the
-// consumer folds them into 1/rms in its prologue (deterministic: fixed order,
-// no float atomics).
+// LDS and wave 0 runs the epilogue. RMSNorm is folded away: its weight g is
+// multiplied into the columns of the following projection once at load time
+// (W'[n][k] = W[n][k] g[k]), and the per-row 1/rms factors out of the dot
+// product, so the GEMM streams the raw residual and the epilogue scales the
+// accumulator. 1/rms comes from per-block partial sums of squares written by
+// the residual producer (deterministic: fixed order, no float atomics).
+// Cross-workgroup merges (attention splits, argmax) use write-through stores
+// and an arrival ticket, never an L2 write-back fence.
 //
-// Numerics mirror the unfused path: every value the unfused path stores as
-// bf16 (GEMM outputs, normed activations, residual) is rounded to bf16 at the
-// same point here; accumulation is fp32.
+// Numerics: GEMM outputs, the residual and the attention output are rounded
+// to bf16 where the unfused path rounds them; the normed activation is not
+// materialised (rounding differs at the bf16-ulp level); fp32 accumulation.
 #include "bf16_common.h"
 
 namespace {
@@ -47,10 +51,11 @@ enum Epi : int { EPI_STORE = 0, EPI_ROPE = 1, EPI_SILU = 2, EPI_RESID = 3, EPI_A
 
 struct GemmArgs {
   const uint16_t* x;  // A [M][K]
-  const uint16_t* w;  // W [N][K]
+  const uint16_t* w;  // W [N][K]; for a normed input, W[n][k] * g[k] folded in
   int M, N, K;
-  // RMSNorm prologue (norm_w == nullptr: A used as is)
-  const uint16_t* norm_w;
+  // RMSNorm of A's rows (ss_part == nullptr: A used as is). The norm weight g
+  // is folded into W offline, so only the per-row 1/rms remains, and that
+  // factors out of the dot product: it scales the accumulator in the epilogue.
   const float* ss_part;  // [ss_parts][16] partial row sums of squares
   int ss_parts;
   float eps;
@@ -71,6 +76,25 @@ struct GemmArgs {
 
 __device__ __forceinline__ frag8 as_frag(const uint4& v) { return __builtin_bit_cast(frag8, v); }
 
+// Cross-workgroup hand-off without L2 write-back/invalidate fences: payload
+// stores are agent-scope relaxed atomics (write-through, `sc1`), drained with
+// s_waitcnt before the arrival ticket; the last arriver reads them back with
+// agent-scope loads that bypass stale cache lines (MI355X_MICROARCH handoff-flag).
+template <typename T>
+__device__ __forceinline__ void st_wt(T* p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+template <typename T>
+__device__ __forceinline__ T ld_wt(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void drain_stores() {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __builtin_amdgcn_s_waitcnt(0);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+__device__ __forceinline__ unsigned arrive(unsigned* ctr) {
+  return __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Output column of lane column c (0..15) in subtile t of block bx.
 template <int EPI, int TN>
 __device__ __forceinline__ int tile_col(const GemmArgs& a, int bx, int t, int c) {
@@ -88,41 +112,48 @@ __device__ __forceinline__ int tile_col(const GemmArgs& a, int bx, int t, int c)
   }
 }
 
+// UU consecutive 32-wide k-steps from step s: all loads issued, then the MFMAs.
+template <int UU, int TN>
+__device__ __forceinline__ void mma_steps(frag4 (&acc)[TN], const uint16_t* xrow, const uint16_t* const (&wrow)[TN],
+                                          bool a_ok, int s) {
+  uint4 bv[UU][TN], av[UU];
+#pragma unroll
+  for (int u = 0; u < UU; u++)
+#pragma unroll
+    for (int t = 0; t < TN; t++) bv[u][t] = *reinterpret_cast<const uint4*>(wrow[t] + (s + u) * 32);
+#pragma unroll
+  for (int u = 0; u < UU; u++)
+    av[u] = a_ok ? *reinterpret_cast<const uint4*>(xrow + (s + u) * 32) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int u = 0; u < UU; u++)
+#pragma unroll
+    for (int t = 0; t < TN; t++)
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(av[u]), as_frag(bv[u][t]), acc[t], 0, 0, 0);
+}
+
 template <int NW, int TN, int EPI>
 __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
   __shared__ float red[NW][TN][4][kWave];
-  __shared__ float s_rstd[kMaxM];
-  __shared__ float s_ss[NW][kMaxM];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int bx = blockIdx.x;
-  const bool norm = a.norm_w != nullptr;
+  const bool norm = a.ss_part != nullptr;
 
-  if (norm) {
-    const int m = threadIdx.x & 15;
-    float s = 0.f;
-    for (int p = threadIdx.x >> 4; p < a.ss_parts; p += NW * 4) s += a.ss_part[p * kMaxM + m];
-    s += __shfl_xor(s, 16, kWave);
-    s += __shfl_xor(s, 32, kWave);
-    if (lane < 16) s_ss[wv][lane] = s;
-    __syncthreads();
-    if (threadIdx.x < kMaxM) {
-      float t = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; w++) t += s_ss[w][threadIdx.x];
-      s_rstd[threadIdx.x] = rsqrtf(t * (1.f / float(a.K)) + a.eps);
-    }
-    __syncthreads();
+  // Row sums of squares (wave 0 only; it runs the epilogue): lane holds row
+  // lane & 15, summing every 4th partial; issued before the weight stream.
+  float ssum = 0.f;
+  if (norm && wv == 0) {
+#pragma unroll 8
+    for (int p = lane >> 4; p < a.ss_parts; p += 4) ssum += a.ss_part[p * kMaxM + (lane & 15)];
   }
 
-  // A fragment: row m_a, k = kb + 8*(lane>>4) + j. B fragment: W row n, same k.
+  // A fragment: row lane & 15, k = 32*s + 8*(lane>>4) + j; B fragment: W row n, same k.
+  // The K steps are split evenly over the NW waves.
   const int m_a = lane & 15;
   const bool a_ok = m_a < a.M;
-  const float rs = norm ? s_rstd[m_a] : 1.f;
   const int kq = (lane >> 4) << 3;
-  const int Kw = a.K / NW;  // host guarantees K % (32 * NW) == 0
-  const int k0 = wv * Kw, k1 = k0 + Kw;
+  const int S = a.K >> 5;
+  const int s0 = wv * S / NW, s1 = (wv + 1) * S / NW;
   const uint16_t* xrow = a.x + size_t(m_a) * a.K + kq;
-  const uint16_t* gw = norm ? a.norm_w + kq : nullptr;
   const uint16_t* wrow[TN];
 #pragma unroll
   for (int t = 0; t < TN; t++) wrow[t] = a.w + size_t(tile_col<EPI, TN>(a, bx, t, lane & 15)) * a.K + kq;
@@ -130,46 +161,14 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
   frag4 acc[TN];
 #pragma unroll
   for (int t = 0; t < TN; t++) acc[t] = frag4{0.f, 0.f, 0.f, 0.f};
-
-  auto load_a = [&](int k) -> uint4 {
-    if (!a_ok) return make_uint4(0, 0, 0, 0);
-    uint4 v = *reinterpret_cast<const uint4*>(xrow + k);
-    if (norm) {
-      float f[8], g[8];
-      unpack8(v, f);
-      unpack8(*reinterpret_cast<const uint4*>(gw + k), g);
-#pragma unroll
-      for (int j = 0; j < 8; j++) f[j] = f[j] * rs * g[j];
-      v = pack8(f);
-    }
-    return v;
-  };
-
-  constexpr int U = 4;
-  int k = k0;
-  for (; k + 32 * U <= k1; k += 32 * U) {
-    uint4 bv[U][TN], av[U];
-#pragma unroll
-    for (int u = 0; u < U; u++)
-#pragma unroll
-      for (int t = 0; t < TN; t++) bv[u][t] = *reinterpret_cast<const uint4*>(wrow[t] + k + 32 * u);
-#pragma unroll
-    for (int u = 0; u < U; u++) av[u] = load_a(k + 32 * u);
-#pragma unroll
-    for (int u = 0; u < U; u++)
-#pragma unroll
-      for (int t = 0; t < TN; t++)
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(av[u]), as_frag(bv[u][t]), acc[t], 0, 0, 0);
-  }
-  for (; k < k1; k += 32) {
-    uint4 bv[TN];
-#pragma unroll
-    for (int t = 0; t < TN; t++) bv[t] = *reinterpret_cast<const uint4*>(wrow[t] + k);
-    uint4 av = load_a(k);
-#pragma unroll
-    for (int t = 0; t < TN; t++)
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(av), as_frag(bv[t]), acc[t], 0, 0, 0);
-  }
+  // Up to 8 steps in flight per wave (4 for the 1024-thread, two-subtile
+  // variant, whose 128-VGPR budget would otherwise spill).
+  constexpr int UMAX = (NW >= 16 && TN >= 2) ? 4 : 8;
+  int s = s0;
+  for (; s + UMAX <= s1; s += UMAX) mma_steps<UMAX, TN>(acc, xrow, wrow, a_ok, s);
+  if (UMAX > 4 && s + 4 <= s1) { mma_steps<4, TN>(acc, xrow, wrow, a_ok, s); s += 4; }
+  if (s + 2 <= s1) { mma_steps<2, TN>(acc, xrow, wrow, a_ok, s); s += 2; }
+  if (s < s1) mma_steps<1, TN>(acc, xrow, wrow, a_ok, s);
 
   // K-split reduction through LDS (lane-contiguous: conflict-free).
 #pragma unroll
@@ -183,15 +182,26 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
   for (int t = 0; t < TN; t++)
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-      float s = 0.f;
+      float sum = 0.f;
 #pragma unroll
-      for (int w = 0; w < NW; w++) s += red[w][t][r][lane];
-      v[t][r] = s;
+      for (int w = 0; w < NW; w++) sum += red[w][t][r][lane];
+      v[t][r] = sum;
     }
 
   // C layout: row m = 4*(lane>>4) + r, column = tile_col(.., lane & 15).
   const int mrow0 = (lane >> 4) << 2;
   const int c = lane & 15;
+  if (norm) {
+    ssum += __shfl_xor(ssum, 16, kWave);
+    ssum += __shfl_xor(ssum, 32, kWave);
+    const float rs_row = rsqrtf(ssum * (1.f / float(a.K)) + a.eps);  // for row lane & 15
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const float rs = __shfl(rs_row, mrow0 + r, kWave);
+#pragma unroll
+      for (int t = 0; t < TN; t++) v[t][r] *= rs;
+    }
+  }
 
   if constexpr (EPI == EPI_STORE) {
 #pragma unroll
@@ -294,27 +304,34 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
         }
       }
       if (c == 0) {
-        a.am_val[bx * kMaxM + mrow0 + r] = best[r];
-        a.am_idx[bx * kMaxM + mrow0 + r] = bi[r];
+        st_wt(a.am_val + bx * kMaxM + mrow0 + r, best[r]);
+        st_wt(a.am_idx + bx * kMaxM + mrow0 + r, bi[r]);
       }
     }
     // Last block to finish merges every block's winners.
-    __threadfence();
+    drain_stores();
     unsigned ticket = 0;
-    if (lane == 0) ticket = atomicAdd(a.am_count, 1u);
+    if (lane == 0) ticket = arrive(a.am_count);
     ticket = __shfl(ticket, 0, kWave);
     if (ticket != gridDim.x - 1) return;
-    __threadfence();
     for (int m = 0; m < a.M; m++) {
       float b = -INFINITY;
       int i = 0x7fffffff;
-      for (int p = lane; p < int(gridDim.x); p += kWave) {
-        const float pv = __builtin_nontemporal_load(a.am_val + p * kMaxM + m);
-        const int pi = __builtin_nontemporal_load(a.am_idx + p * kMaxM + m);
-        if (pv > b || (pv == b && pi < i)) {
-          b = pv;
-          i = pi;
+      for (int p0 = lane; p0 < int(gridDim.x); p0 += 8 * kWave) {
+        float pv[8];
+        int pi[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {  // 8 loads in flight per lane
+          const int p = p0 + j * kWave;
+          pv[j] = p < int(gridDim.x) ? ld_wt(a.am_val + p * kMaxM + m) : -INFINITY;
+          pi[j] = p < int(gridDim.x) ? ld_wt(a.am_idx + p * kMaxM + m) : 0x7fffffff;
         }
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+          if (pv[j] > b || (pv[j] == b && pi[j] < i)) {
+            b = pv[j];
+            i = pi[j];
+          }
       }
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) {
@@ -327,7 +344,7 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
       }
       if (lane == 0) a.ids[m] = i;
     }
-    if (lane == 0) *a.am_count = 0u;  // self-resetting for the next step / graph replay
+    if (lane == 0) st_wt(a.am_count, 0u);  // self-resetting for the next step / graph replay
   }
 }
 
@@ -446,33 +463,30 @@ __global__ __launch_bounds__(512) void k_attn(const uint16_t* __restrict__ q, co
     __syncthreads();
   }
   const size_t hb = size_t(b) * H + kvh * G + g;
-  const int nh = blockDim.x >> 6;  // == G
-  {
-    float* po = part_o + (hb * nsplit + split) * D;
-#pragma unroll
-    for (int k = 0; k < DPL; k++) po[lane + k * kWave] = acc[k];
-    if (lane == 0) {
-      part_ml[(hb * nsplit + split) * 2 + 0] = m;
-      part_ml[(hb * nsplit + split) * 2 + 1] = l;
-    }
-  }
   if (used == 1) {  // single split: finish directly
     const float inv = 1.f / l;
 #pragma unroll
     for (int k = 0; k < DPL; k++) out[hb * D + lane + k * kWave] = uint16_t(f2bf_bits(acc[k] * inv));
     return;
   }
-  __threadfence();
+  {
+    float* po = part_o + (hb * nsplit + split) * D;
+#pragma unroll
+    for (int k = 0; k < DPL; k++) st_wt(po + lane + k * kWave, acc[k]);
+    if (lane == 0) {
+      st_wt(part_ml + (hb * nsplit + split) * 2 + 0, m);
+      st_wt(part_ml + (hb * nsplit + split) * 2 + 1, l);
+    }
+  }
+  drain_stores();
   __syncthreads();
-  if (threadIdx.x == 0) s_ticket = atomicAdd(&counters[blockIdx.y], 1u);
+  if (threadIdx.x == 0) s_ticket = arrive(&counters[blockIdx.y]);
   __syncthreads();
   if (s_ticket != unsigned(used - 1)) return;
-  __threadfence();
-  (void)nh;
   // Merge: lanes over splits for the max / weights, lanes over head dims for the output.
   const float* ml = part_ml + hb * nsplit * 2;
   float M = -INFINITY;
-  for (int s = lane; s < used; s += kWave) M = fmaxf(M, __builtin_nontemporal_load(ml + 2 * s));
+  for (int s = lane; s < used; s += kWave) M = fmaxf(M, ld_wt(ml + 2 * s));
   M = wave_max(M);
   float L = 0.f, o[DPL];
 #pragma unroll
@@ -481,15 +495,24 @@ __global__ __launch_bounds__(512) void k_attn(const uint16_t* __restrict__ q, co
     const int s = s0 + lane;
     float ws = 0.f;
     if (s < used) {
-      ws = __expf(__builtin_nontemporal_load(ml + 2 * s) - M);
-      L += __builtin_nontemporal_load(ml + 2 * s + 1) * ws;
+      ws = __expf(ld_wt(ml + 2 * s) - M);
+      L += ld_wt(ml + 2 * s + 1) * ws;
     }
     const int n = min(kWave, used - s0);
     const float* pob = part_o + (hb * nsplit + s0) * D + lane;
-    for (int j = 0; j < n; j++) {
-      const float wj = __shfl(ws, j, kWave);
+    // 8 splits' partials in flight at once (one wait per group, not per split).
+    for (int j0 = 0; j0 < n; j0 += 8) {
+      float pv[8][DPL];
 #pragma unroll
-      for (int k = 0; k < DPL; k++) o[k] += wj * __builtin_nontemporal_load(pob + size_t(j) * D + k * kWave);
+      for (int jj = 0; jj < 8; jj++)
+#pragma unroll
+        for (int k = 0; k < DPL; k++) pv[jj][k] = j0 + jj < n ? ld_wt(pob + size_t(j0 + jj) * D + k * kWave) : 0.f;
+#pragma unroll
+      for (int jj = 0; jj < 8; jj++) {
+        const float wj = __shfl(ws, (j0 + jj) & 63, kWave);
+#pragma unroll
+        for (int k = 0; k < DPL; k++) o[k] += wj * pv[jj][k];
+      }
     }
   }
   L = wave_sum(L);
@@ -497,7 +520,7 @@ __global__ __launch_bounds__(512) void k_attn(const uint16_t* __restrict__ q, co
 #pragma unroll
   for (int k = 0; k < DPL; k++) out[hb * D + lane + k * kWave] = uint16_t(f2bf_bits(o[k] * inv));
   __syncthreads();
-  if (threadIdx.x == 0) counters[blockIdx.y] = 0u;
+  if (threadIdx.x == 0) st_wt(&counters[blockIdx.y], 0u);
 }
 
 // ------------------------------------------------------------ host side
@@ -544,19 +567,20 @@ Workspace carve(const LlamaDims& d, uint8_t* base) {
   return w;
 }
 
+// Waves per workgroup: enough that each wave streams at most ~8 k-steps of
+// 32 (one round trip of loads), capped at 16 (1024 threads).
 int pick_nw(int K) {
-  if (K >= 2048 && K % (32 * 8) == 0) return 8;
-  if (K % (32 * 4) == 0) return 4;
-  return 0;
+  if (K <= 0 || K % 32) return 0;
+  return (K >> 5) <= 64 ? 8 : 16;
 }
 
 template <int EPI, int TN>
 hipError_t launch_gemm(const GemmArgs& a, int grid, hipStream_t s) {
   const int nw = pick_nw(a.K);
-  if (nw == 8)
+  if (nw == 16)
+    hipLaunchKernelGGL((k_skinny<16, TN, EPI>), dim3(grid), dim3(1024), 0, s, a);
+  else if (nw == 8)
     hipLaunchKernelGGL((k_skinny<8, TN, EPI>), dim3(grid), dim3(512), 0, s, a);
-  else if (nw == 4)
-    hipLaunchKernelGGL((k_skinny<4, TN, EPI>), dim3(grid), dim3(256), 0, s, a);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
@@ -585,6 +609,8 @@ size_t p2pt_llama_ws_bytes(const LlamaDims* d) {
 // One decode step for B <= 16 sequences (slots 0..B-1 of the caches).
 //   w: embed, final_norm, lm_head, then per layer
 //      attn_norm, wqkv [(H+2Hkv)*D, dim], wo [dim, H*D], ffn_norm, w_gate_up [2*ffn, dim], w_down [dim, ffn]
+//      where wqkv, w_gate_up and lm_head carry the preceding RMSNorm weight folded
+//      into their columns (W[n][k] * g[k]); the norm-weight slots are not read.
 //   k_cache/v_cache: [n_layers][max_batch][max_seq][Hkv][D]
 //   tokens int64 [B], pos int32 [B] (< max_seq), logits bf16 [B][vocab], ids int64 [B]
 //   max_len: host bound on max(pos) + 1 (sizes the attention grid; use max_seq under graph capture)
@@ -610,10 +636,8 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
   if (e != hipSuccess) return int(e);
 
   for (int L = 0; L < d.n_layers; L++) {
-    const uint16_t* attn_norm = bf(3 + 6 * L);
     const uint16_t* wqkv = bf(4 + 6 * L);
     const uint16_t* wo = bf(5 + 6 * L);
-    const uint16_t* ffn_norm = bf(6 + 6 * L);
     const uint16_t* wgu = bf(7 + 6 * L);
     const uint16_t* wdown = bf(8 + 6 * L);
     uint16_t* kc = static_cast<uint16_t*>(k_cache) + L * layer_cache;
@@ -624,7 +648,7 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
     a.eps = d.eps;
     // QKV + RoPE + cache append
     a.x = W.resid; a.w = wqkv; a.N = qkv_n; a.K = d.dim;
-    a.norm_w = attn_norm; a.ss_part = W.ss; a.ss_parts = ss_parts;
+    a.ss_part = W.ss; a.ss_parts = ss_parts;
     a.pos = pos; a.q_out = W.q; a.kc = kc; a.vc = vc;
     a.H = d.H; a.Hkv = d.Hkv; a.D = d.D; a.Smax = d.max_seq; a.log2_theta = log2_theta;
     if ((e = launch_gemm<EPI_ROPE, 2>(a, qkv_n / 32, s)) != hipSuccess) return int(e);
@@ -651,7 +675,7 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
     // gate/up + SwiGLU
     GemmArgs g{};
     g.M = B; g.eps = d.eps; g.x = W.resid; g.w = wgu; g.N = 2 * d.ffn; g.K = d.dim;
-    g.norm_w = ffn_norm; g.ss_part = W.ss; g.ss_parts = ss_parts; g.out = W.h;
+    g.ss_part = W.ss; g.ss_parts = ss_parts; g.out = W.h;
     if ((e = launch_gemm<EPI_SILU, 2>(g, d.ffn / 16, s)) != hipSuccess) return int(e);
 
     // down + residual
@@ -663,7 +687,7 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
   // final norm + LM head + argmax
   GemmArgs h{};
   h.M = B; h.eps = d.eps; h.x = W.resid; h.w = bf(2); h.N = d.vocab; h.K = d.dim;
-  h.norm_w = bf(1); h.ss_part = W.ss; h.ss_parts = ss_parts;
+  h.ss_part = W.ss; h.ss_parts = ss_parts;
   h.out = static_cast<uint16_t*>(logits);
   h.am_val = W.am_val; h.am_idx = W.am_idx; h.am_count = W.counters + kMaxM * d.Hkv; h.ids = ids;
   if ((e = launch_gemm<EPI_ARGMAX, kTnStore>(h, d.vocab / (16 * kTnStore), s)) != hipSuccess) return int(e);

@@ -131,7 +131,8 @@ def test_argmax(ops, V):
 
 
 @cuda
-@pytest.mark.parametrize("M,N,K", [(1, 1536, 1024), (8, 2048, 2816), (16, 32000, 1024), (3, 64, 256), (16, 96, 4096)])
+@pytest.mark.parametrize("M,N,K", [(1, 1536, 1024), (8, 2048, 2816), (16, 32000, 1024), (3, 64, 256), (16, 96, 4096),
+                                   (5, 256, 96), (16, 64, 8192)])
 def test_skinny_gemm(ops, M, N, K):
     # Asymmetric operands: a transposed C write would not pass.
     torch.manual_seed(M * 7 + K)
@@ -164,7 +165,7 @@ def test_host_side_shape_checks(ops):
     with pytest.raises(ValueError):
         ops.skinny_gemm(bf(torch.randn(17, 128, device="cuda")), bf(torch.randn(32, 128, device="cuda")))  # M > 16
     with pytest.raises(ValueError):
-        ops.skinny_gemm(bf(torch.randn(2, 100, device="cuda")), bf(torch.randn(32, 100, device="cuda")))  # K % 128
+        ops.skinny_gemm(bf(torch.randn(2, 100, device="cuda")), bf(torch.randn(32, 100, device="cuda")))  # K % 32
 
 
 @cuda
