@@ -42,18 +42,30 @@ class Request:
 
 
 class Engine:
-    def __init__(self, device="cuda:0", config="tiny", max_batch=8, seed=0, use_graph=True):
-        self.model = TinyLlama(config, device=device, max_batch=max_batch, seed=seed)
+    """Continuous batching with chunked prefill over the fused decode step.
+
+    Every step packs up to ``rows`` (16) token rows: first one decode row per
+    generating sequence, then prompt chunks of prefilling sequences, each row
+    tagged with its cache slot and position (``TinyLlama.decode_step(slots=)``).
+    A 512-byte prompt is thus prefilled in 32 steps instead of 512, while
+    generating sequences keep emitting a token every step. Padding rows point
+    at the model's scratch slot. The step is replayed from one hipGraph.
+    """
+
+    def __init__(self, device="cuda:0", config="tiny", max_batch=8, seed=0, use_graph=True, rows=16):
+        self.model = TinyLlama(config, device=device, max_batch=max_batch, seed=seed, fused=True)
         self.device = self.model.device
+        self.rows = rows
         self.use_graph = use_graph
         if use_graph:
-            self.model.capture_graph()
+            self.model.capture_graph(rows=rows)
         self.max_batch = max_batch
         self.pending: queue.Queue = queue.Queue()
         self.slots: list[dict | None] = [None] * max_batch
         self._stop = threading.Event()
         self.steps = 0
         self.tokens_out = 0
+        self.prefill_tokens = 0
         self.thread = threading.Thread(target=self._loop, daemon=True, name="engine")
         self.thread.start()
 
@@ -75,49 +87,57 @@ class Engine:
                 ids = req.prompt[: self.model.cfg.max_seq - req.max_new - 1] or [0]
                 self.slots[i] = {"req": req, "pos": 0, "ids": ids, "last": None}
 
+    def _plan(self):
+        """Rows for this step: [(slot, token, pos, emits)]."""
+        V = self.model.cfg.vocab
+        rows = []
+        for i, s in enumerate(self.slots):  # decode rows first: one token each
+            if s is not None and s["pos"] >= len(s["ids"]):
+                rows.append((i, s["last"], s["pos"], True))
+        for i, s in enumerate(self.slots):  # then prompt chunks
+            if s is None or s["pos"] >= len(s["ids"]):
+                continue
+            take = min(self.rows - len(rows), len(s["ids"]) - s["pos"])
+            for p in range(s["pos"], s["pos"] + take):
+                rows.append((i, s["ids"][p] % V, p, p == len(s["ids"]) - 1))
+            if len(rows) >= self.rows:
+                break
+        return rows
+
     def _loop(self):
         torch.cuda.set_device(self.device)
-        V = self.model.cfg.vocab
         while not self._stop.is_set():
             self._admit()
-            active = [i for i, s in enumerate(self.slots) if s is not None]
-            if not active:
+            rows = self._plan()
+            if not rows:
                 time.sleep(0.0005)
                 continue
-            # Graph mode replays the captured full-batch step; eager mode runs
-            # slots [0, n). Idle slots feed token 0 at position 0.
-            n = self.max_batch if self.use_graph else max(active) + 1
-            toks, pos = [], []
-            for i in range(n):
-                s = self.slots[i]
-                if s is None:
-                    toks.append(0)
-                    pos.append(0)
-                elif s["pos"] < len(s["ids"]):
-                    toks.append(s["ids"][s["pos"]] % V)
-                    pos.append(s["pos"])
-                else:
-                    toks.append(s["last"])
-                    pos.append(s["pos"])
-            t = torch.tensor(toks, dtype=torch.int64).to(self.device, non_blocking=True)
+            n = len(rows)
+            pad = self.rows - n if self.use_graph else 0
+            slot = [r[0] for r in rows] + [self.model.scratch_slot] * pad
+            tok = [r[1] for r in rows] + [0] * pad
+            pos = [r[2] for r in rows] + [0] * pad
+            t = torch.tensor(tok, dtype=torch.int64).to(self.device, non_blocking=True)
             p = torch.tensor(pos, dtype=torch.int32).to(self.device, non_blocking=True)
+            sl = torch.tensor(slot, dtype=torch.int32).to(self.device, non_blocking=True)
             if self.use_graph:
-                ids = self.model.graph_step(t, p).tolist()
+                out = self.model.graph_step(t, p, sl)[:n].tolist()
             else:
-                ids = self.model.decode_step(t, p, (min(pos), max(pos))).tolist()
+                out = self.model.decode_step(t, p, (min(pos), max(pos)), slots=sl).tolist()
             self.steps += 1
-            for i in active:
+            for (i, _, _, emits), nxt in zip(rows, out):
                 s = self.slots[i]
-                req = s["req"]
                 s["pos"] += 1
-                if s["pos"] < len(s["ids"]):
-                    continue  # still prefilling
-                s["last"] = ids[i]
+                if not emits:
+                    self.prefill_tokens += 1
+                    continue
+                req = s["req"]
+                s["last"] = nxt
                 if req.cancelled:
                     req.out.put(None)
                     self.slots[i] = None
                     continue
-                req.out.put(ids[i])
+                req.out.put(nxt)
                 req.generated += 1
                 self.tokens_out += 1
                 if req.generated >= req.max_new or s["pos"] >= self.model.cfg.max_seq - 1:

@@ -82,52 +82,68 @@ class TinyLlama:
             })
         self.final_norm = norm_w(c.dim)
         self.lm_head = w(c.vocab, c.dim, scale=1 / math.sqrt(c.dim))
-        cache_shape = (c.n_layers, max_batch, c.max_seq, c.n_kv_heads, c.head_dim)
+        # One spare slot (index max_batch) absorbs the K/V writes of padding rows.
+        self.scratch_slot = max_batch
+        cache_shape = (c.n_layers, max_batch + 1, c.max_seq, c.n_kv_heads, c.head_dim)
         self.k_cache = torch.zeros(cache_shape, dtype=torch.bfloat16, device=self.device)
         self.v_cache = torch.zeros(cache_shape, dtype=torch.bfloat16, device=self.device)
 
     # ------------------------------------------------------------------ HIP path
     @torch.no_grad()
     def decode_step(self, tokens: torch.Tensor, pos: torch.Tensor, pos_range: tuple[int, int],
-                    return_logits: bool = False):
-        """One token per slot. tokens: int64 [B]; pos: int32 [B] (cache position of this token).
+                    return_logits: bool = False, slots: torch.Tensor | None = None):
+        """One step of token rows. tokens: int64 [B]; pos: int32 [B] (cache position of
+        each token); slots: int32 [B] cache slot of each row (default: row b -> slot b).
+        With ``slots`` (fused path, B <= 16) several rows may feed one sequence at
+        consecutive positions: a causal prefill chunk.
 
         Returns next-token ids (int64 [B]) and optionally the bf16 logits.
         """
         c = self.cfg
         B = tokens.shape[0]
-        if B > self.max_batch:
+        if slots is None and B > self.max_batch:
             raise ValueError("batch exceeds max_batch")
-        if pos_range[1] >= c.max_seq:
-            raise ValueError("sequence exceeds max_seq")
-        ids, logits = self._decode_impl(tokens, pos, pos_range, pos_range[1] + 1)
+        if slots is not None and not (self.fused and B <= 16):
+            raise ValueError("row->slot mapping needs the fused path and at most 16 rows")
+        if pos_range[0] < 0 or pos_range[1] >= c.max_seq:
+            raise ValueError("positions out of [0, max_seq)")
+        ids, logits = self._decode_impl(tokens, pos, pos_range, pos_range[1] + 1, slots)
         return (ids, logits) if return_logits else ids
 
     def fused_decoder(self) -> ops.FusedLlamaDecoder:
         if self._fused is None:
             c = self.cfg
             dims = ops.LlamaDims(vocab=c.vocab, dim=c.dim, n_layers=c.n_layers, H=c.n_heads, Hkv=c.n_kv_heads,
-                                 D=c.head_dim, ffn=c.ffn, max_seq=c.max_seq, max_batch=self.max_batch, eps=c.eps,
+                                 D=c.head_dim, ffn=c.ffn, max_seq=c.max_seq, max_batch=self.max_batch + 1, eps=c.eps,
                                  theta=c.rope_theta)
             # The fused GEMMs take the RMSNorm weight folded into the following
-            # projection's columns (W[n][k] * g[k]); see decode_fused.hip.
+            # projection's columns (W[n][k] * g[k]), and QKV / gate-up rows
+            # interleaved in pairs so a 16-column tile holds both members of a
+            # RoPE pair or a SwiGLU pair; see decode_fused.hip.
             def fold(w, g):
                 return (w.float() * g.float()[None, :]).to(torch.bfloat16)
 
+            def pairs(n):  # [0, n, 1, n + 1, ...]
+                return torch.stack([torch.arange(n), torch.arange(n) + n], 1).flatten().to(self.device)
+
+            heads = c.n_heads + 2 * c.n_kv_heads
+            head_perm = (torch.arange(heads, device=self.device)[:, None] * c.head_dim
+                         + pairs(c.head_dim // 2)[None, :]).flatten()
             ws = [self.embed, self.final_norm, fold(self.lm_head, self.final_norm)]
             for L in self.layers:
-                ws += [L["attn_norm"], fold(L["wqkv"], L["attn_norm"]), L["wo"], L["ffn_norm"],
-                       fold(L["w_gate_up"], L["ffn_norm"]), L["w_down"]]
+                ws += [L["attn_norm"], fold(L["wqkv"], L["attn_norm"])[head_perm].contiguous(), L["wo"],
+                       L["ffn_norm"], fold(L["w_gate_up"], L["ffn_norm"])[pairs(c.ffn)].contiguous(), L["w_down"]]
             self._fused = ops.FusedLlamaDecoder(dims, ws, self.k_cache, self.v_cache)
         return self._fused
 
-    def _decode_impl(self, tokens, pos, pos_range, max_len):
+    def _decode_impl(self, tokens, pos, pos_range, max_len, slots=None):
         B = tokens.shape[0]
         if self.fused and B <= 16:
             tokens, pos = tokens.contiguous(), pos.contiguous()
+            slots = slots.contiguous() if slots is not None else None
             logits = torch.empty(B, self.cfg.vocab, dtype=torch.bfloat16, device=self.device)
             ids = torch.empty(B, dtype=torch.int64, device=self.device)
-            self.fused_decoder().step(tokens, pos, max_len, logits, ids)
+            self.fused_decoder().step(tokens, pos, max_len, logits, ids, slots)
             return ids, logits
         return self._decode_unfused(tokens, pos, pos_range, max_len)
 
@@ -153,34 +169,45 @@ class TinyLlama:
         return ops.argmax(logits), logits
 
     # ------------------------------------------------------------------ hipGraph
-    def capture_graph(self):
-        """Capture one full-batch decode step into a hipGraph (torch.cuda.CUDAGraph).
+    def capture_graph(self, rows: int | None = None):
+        """Capture one step of ``rows`` token rows into a hipGraph (torch.cuda.CUDAGraph).
 
-        Decode at small batch is launch-bound (~10 kernels per layer, each a few
-        µs); replaying the captured graph removes the per-kernel launch cost.
-        The attention is captured for the cache capacity (its splits past each
-        sequence's length exit immediately), so one graph serves every step.
+        Decode at small batch is bound by kernel count; replaying the captured
+        graph removes the per-kernel launch cost. The attention is captured for
+        the cache capacity (its splits past each row's length exit immediately),
+        so one graph serves every step. Fused path: 16 rows with a row->slot map
+        (padding rows point at the scratch slot); unfused: one row per slot.
         """
-        B, c = self.max_batch, self.cfg
-        self._g_tok = torch.zeros(B, dtype=torch.int64, device=self.device)
-        self._g_pos = torch.zeros(B, dtype=torch.int32, device=self.device)
+        c = self.cfg
+        R = rows or (16 if self.fused else self.max_batch)
+        self.graph_rows = R
+        self._g_tok = torch.zeros(R, dtype=torch.int64, device=self.device)
+        self._g_pos = torch.zeros(R, dtype=torch.int32, device=self.device)
+        self._g_slot = (torch.full((R,), self.scratch_slot, dtype=torch.int32, device=self.device)
+                        if self.fused else None)
         full = (0, c.max_seq - 1)
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.no_grad(), torch.cuda.stream(side):
             for _ in range(2):  # allocator + GEMM heuristics warm-up outside capture
-                self._decode_impl(self._g_tok, self._g_pos, full, c.max_seq)
+                self._decode_impl(self._g_tok, self._g_pos, full, c.max_seq, self._g_slot)
         torch.cuda.current_stream(self.device).wait_stream(side)
         self._graph = torch.cuda.CUDAGraph()
         with torch.no_grad(), torch.cuda.graph(self._graph):
-            self._g_ids, self._g_logits = self._decode_impl(self._g_tok, self._g_pos, full, c.max_seq)
+            self._g_ids, self._g_logits = self._decode_impl(self._g_tok, self._g_pos, full, c.max_seq, self._g_slot)
         return self
 
     @torch.no_grad()
-    def graph_step(self, tokens: torch.Tensor, pos: torch.Tensor, return_logits: bool = False):
-        """Replay the captured step. tokens/pos: [max_batch]; positions must be < max_seq."""
+    def graph_step(self, tokens: torch.Tensor, pos: torch.Tensor, slots: torch.Tensor | None = None,
+                   return_logits: bool = False):
+        """Replay the captured step. tokens/pos/slots: [graph_rows] (slots default to
+        row b -> slot b); positions must be < max_seq."""
         self._g_tok.copy_(tokens, non_blocking=True)
         self._g_pos.copy_(pos, non_blocking=True)
+        if self._g_slot is not None:
+            if slots is None:
+                slots = torch.arange(self.graph_rows, dtype=torch.int32).clamp_(max=self.scratch_slot)
+            self._g_slot.copy_(slots, non_blocking=True)
         self._graph.replay()
         return (self._g_ids, self._g_logits) if return_logits else self._g_ids
 

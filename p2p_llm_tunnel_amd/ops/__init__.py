@@ -41,8 +41,8 @@ def lib() -> ctypes.CDLL:
         _LIB.p2pt_skinny_gemm.argtypes = [vp, vp, vp, i, i, i, vp]
         _LIB.p2pt_llama_ws_bytes.argtypes = [ctypes.POINTER(LlamaDims)]
         _LIB.p2pt_llama_ws_bytes.restype = ctypes.c_size_t
-        _LIB.p2pt_llama_decode.argtypes = [ctypes.POINTER(LlamaDims), ctypes.POINTER(vp), vp, vp, vp, vp, i, i, vp,
-                                           ctypes.c_size_t, vp, vp, vp]
+        _LIB.p2pt_llama_decode.argtypes = [ctypes.POINTER(LlamaDims), ctypes.POINTER(vp), vp, vp, vp, vp, vp, i, i,
+                                           vp, ctypes.c_size_t, vp, vp, vp]
         for fn in ("p2pt_rmsnorm", "p2pt_silu_mul", "p2pt_rope_qkv_cache", "p2pt_decode_attention", "p2pt_argmax",
                    "p2pt_skinny_gemm", "p2pt_llama_decode"):
             getattr(_LIB, fn).restype = ctypes.c_int
@@ -242,19 +242,27 @@ class FusedLlamaDecoder:
         self.device = dev
 
     def step(self, tokens: torch.Tensor, pos: torch.Tensor, max_len: int, logits: torch.Tensor,
-             ids: torch.Tensor) -> None:
+             ids: torch.Tensor, slots: torch.Tensor | None = None) -> None:
+        """One step over B <= 16 token rows. Row b is token ``tokens[b]`` at cache
+        position ``pos[b]`` of cache slot ``slots[b]`` (default: slot b). Rows of one
+        slot at consecutive positions are a prefill chunk (causal within the step)."""
         d = self.dims
         _check(tokens, torch.int64, "tokens", self.device)
         _check(pos, torch.int32, "pos", self.device)
         _check(logits, torch.bfloat16, "logits", self.device)
         _check(ids, torch.int64, "ids", self.device)
         B = tokens.shape[0]
-        if not 1 <= B <= min(16, d.max_batch) or pos.shape != (B,) or ids.shape != (B,):
-            raise ValueError("batch must be 1..min(16, max_batch) with matching pos/ids")
+        if slots is not None:
+            _check(slots, torch.int32, "slots", self.device)
+            if slots.shape != (B,):
+                raise ValueError("slots must be [B]")
+        limit = 16 if slots is not None else min(16, d.max_batch)
+        if not 1 <= B <= limit or pos.shape != (B,) or ids.shape != (B,):
+            raise ValueError(f"rows must be 1..{limit} with matching pos/ids")
         if logits.shape != (B, d.vocab):
             raise ValueError("logits must be [B, vocab]")
         if not 1 <= max_len <= d.max_seq:
             raise ValueError("max_len out of range")
         _ok(lib().p2pt_llama_decode(ctypes.byref(d), self._wptr, _p(self.k_cache), _p(self.v_cache), _p(tokens),
-                                    _p(pos), B, max_len, _p(self.ws), self.ws.numel(), _p(logits), _p(ids),
-                                    _stream(tokens)), "llama_decode")
+                                    _p(pos), _p(slots), B, max_len, _p(self.ws), self.ws.numel(), _p(logits),
+                                    _p(ids), _stream(tokens)), "llama_decode")

@@ -17,7 +17,8 @@
 //     k_skinny<SILU>     RMSNorm (ffn_norm) -> gate/up GEMM -> SwiGLU
 //     k_skinny<RESID>    down projection -> residual add -> sum-of-squares
 //   k_skinny<ARGMAX>     RMSNorm (final norm) -> LM head -> logits and
-//                        greedy argmax (last block merges the per-block winners)
+//                        per-block greedy winners
+//   k_argmax_merge       one block per row merges the winners
 //
 // Skinny GEMM (M <= 16 tokens): Y[M,N] = A[M,K] * W[N,K]^T on
 // v_mfma_f32_16x16x32_bf16. A workgroup owns 16*TN output columns and splits K
@@ -30,8 +31,10 @@
 // product, so the GEMM streams the raw residual and the epilogue scales the
 // accumulator. 1/rms comes from per-block partial sums of squares written by
 // the residual producer (deterministic: fixed order, no float atomics).
-// Cross-workgroup merges (attention splits, argmax) use write-through stores
-// and an arrival ticket, never an L2 write-back fence.
+// The attention splits merge in-kernel through write-through stores and an
+// arrival ticket, never an L2 write-back fence. QKV and gate/up weights have
+// their rows interleaved in pairs (RoPE partners; gate_j/up_j) so that one
+// 16-column tile holds both members of every pair (lanes c, c^1).
 //
 // Numerics: GEMM outputs, the residual and the attention output are rounded
 // to bf16 where the unfused path rounds them; the normed activation is not
@@ -62,7 +65,9 @@ struct GemmArgs {
   // epilogue
   uint16_t* out;   // STORE/ARGMAX: [M][N] logits; SILU: [M][N/2]; RESID: residual [M][N], in place
   float* ss_out;   // RESID: [gridDim.x][16]
-  const int* pos;  // ROPE
+  const int* pos;   // ROPE: cache position of each row
+  const int* slot;  // ROPE: cache slot of each row (nullptr: row m -> slot m)
+  int nslots;
   uint16_t* q_out;
   uint16_t* kc;
   uint16_t* vc;
@@ -70,8 +75,6 @@ struct GemmArgs {
   float log2_theta;
   float* am_val;  // ARGMAX: [gridDim.x][16]
   int* am_idx;
-  unsigned* am_count;
-  int64_t* ids;
 };
 
 __device__ __forceinline__ frag8 as_frag(const uint4& v) { return __builtin_bit_cast(frag8, v); }
@@ -96,42 +99,43 @@ __device__ __forceinline__ unsigned arrive(unsigned* ctr) {
 }
 
 // Output column of lane column c (0..15) in subtile t of block bx.
-template <int EPI, int TN>
-__device__ __forceinline__ int tile_col(const GemmArgs& a, int bx, int t, int c) {
-  if constexpr (EPI == EPI_ROPE) {
-    // TN == 2: subtile 0 = dims [i0, i0+16) of a head, subtile 1 = the RoPE
-    // partners [i0 + D/2, ...), so each lane holds both halves of its pairs.
-    const int half = a.D >> 1, per_head = half >> 4;
-    const int head = bx / per_head, i0 = (bx % per_head) << 4;
-    return head * a.D + t * half + i0 + c;
-  } else if constexpr (EPI == EPI_SILU) {
-    // TN == 2: subtile 0 = gate columns, subtile 1 = the matching up columns.
-    return t * (a.N >> 1) + (bx << 4) + c;
-  } else {
-    return ((bx * TN + t) << 4) + c;
-  }
+template <int TN>
+__device__ __forceinline__ int tile_col(int bx, int t, int c) {
+  return ((bx * TN + t) << 4) + c;
 }
 
-// UU consecutive 32-wide k-steps from step s: all loads issued, then the MFMAs.
-template <int UU, int TN>
-__device__ __forceinline__ void mma_steps(frag4 (&acc)[TN], const uint16_t* xrow, const uint16_t* const (&wrow)[TN],
-                                          bool a_ok, int s) {
-  uint4 bv[UU][TN], av[UU];
+// One batch of up to UM consecutive 32-wide k-steps [s, min(s + UM, s1)): every
+// load is issued before the first MFMA (one memory round trip per batch).
+// Steps past s1 re-load the last step (cache hits) with a zeroed A fragment,
+// so the code is branch-free and the waits are static.
+template <int UM, int TN>
+__device__ __forceinline__ void mma_batch(frag4 (&acc)[TN], const uint16_t* xrow, const uint16_t* const (&wrow)[TN],
+                                          bool a_ok, int s, int s1) {
+  uint4 bv[UM][TN], av[UM];
 #pragma unroll
-  for (int u = 0; u < UU; u++)
+  for (int u = 0; u < UM; u++) {
+    const int su = min(s + u, s1 - 1) * 32;
 #pragma unroll
-    for (int t = 0; t < TN; t++) bv[u][t] = *reinterpret_cast<const uint4*>(wrow[t] + (s + u) * 32);
+    for (int t = 0; t < TN; t++) bv[u][t] = *reinterpret_cast<const uint4*>(wrow[t] + su);
+  }
 #pragma unroll
-  for (int u = 0; u < UU; u++)
-    av[u] = a_ok ? *reinterpret_cast<const uint4*>(xrow + (s + u) * 32) : make_uint4(0, 0, 0, 0);
+  for (int u = 0; u < UM; u++) {
+    const int su = min(s + u, s1 - 1) * 32;
+    const uint4 x = *reinterpret_cast<const uint4*>(xrow + su);
+    av[u] = (a_ok && s + u < s1) ? x : make_uint4(0, 0, 0, 0);
+  }
 #pragma unroll
-  for (int u = 0; u < UU; u++)
+  for (int u = 0; u < UM; u++)
 #pragma unroll
     for (int t = 0; t < TN; t++)
       acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(av[u]), as_frag(bv[u][t]), acc[t], 0, 0, 0);
 }
 
-template <int NW, int TN, int EPI>
+// Skinny GEMM + fused epilogue. NW waves split K; TN 16-column subtiles per
+// block; UM k-steps per load batch (host: >= each wave's share when possible).
+// ROPE and SILU take weights whose rows are interleaved in pairs (RoPE
+// partners d, d + D/2 of a head; gate_j, up_j), so a pair sits in lanes c, c^1.
+template <int NW, int TN, int EPI, int UM>
 __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
   __shared__ float red[NW][TN][4][kWave];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -156,19 +160,12 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
   const uint16_t* xrow = a.x + size_t(m_a) * a.K + kq;
   const uint16_t* wrow[TN];
 #pragma unroll
-  for (int t = 0; t < TN; t++) wrow[t] = a.w + size_t(tile_col<EPI, TN>(a, bx, t, lane & 15)) * a.K + kq;
+  for (int t = 0; t < TN; t++) wrow[t] = a.w + size_t(tile_col<TN>(bx, t, lane & 15)) * a.K + kq;
 
   frag4 acc[TN];
 #pragma unroll
   for (int t = 0; t < TN; t++) acc[t] = frag4{0.f, 0.f, 0.f, 0.f};
-  // Up to 8 steps in flight per wave (4 for the 1024-thread, two-subtile
-  // variant, whose 128-VGPR budget would otherwise spill).
-  constexpr int UMAX = (NW >= 16 && TN >= 2) ? 4 : 8;
-  int s = s0;
-  for (; s + UMAX <= s1; s += UMAX) mma_steps<UMAX, TN>(acc, xrow, wrow, a_ok, s);
-  if (UMAX > 4 && s + 4 <= s1) { mma_steps<4, TN>(acc, xrow, wrow, a_ok, s); s += 4; }
-  if (s + 2 <= s1) { mma_steps<2, TN>(acc, xrow, wrow, a_ok, s); s += 2; }
-  if (s < s1) mma_steps<1, TN>(acc, xrow, wrow, a_ok, s);
+  for (int s = s0; s < s1; s += UM) mma_batch<UM, TN>(acc, xrow, wrow, a_ok, s, s1);
 
   // K-split reduction through LDS (lane-contiguous: conflict-free).
 #pragma unroll
@@ -203,57 +200,91 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
     }
   }
 
-  if constexpr (EPI == EPI_STORE) {
-#pragma unroll
-    for (int t = 0; t < TN; t++) {
-      const int n = tile_col<EPI, TN>(a, bx, t, c);
-#pragma unroll
-      for (int r = 0; r < 4; r++)
-        if (mrow0 + r < a.M) a.out[size_t(mrow0 + r) * a.N + n] = uint16_t(f2bf_bits(v[t][r]));
-    }
-  } else if constexpr (EPI == EPI_SILU) {
-    const int F = a.N >> 1;
-    const int n = tile_col<EPI, TN>(a, bx, 0, c);
+  if constexpr (EPI == EPI_STORE || EPI == EPI_ARGMAX) {
+    // Logits (bf16) and, for ARGMAX, this block's per-row winner (first index on ties).
+    float best[4];
+    int bi[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-      if (mrow0 + r >= a.M) continue;
-      const float g = bf_round(v[0][r]), u = bf_round(v[1][r]);
-      a.out[size_t(mrow0 + r) * F + n] = uint16_t(f2bf_bits(g / (1.f + __expf(-g)) * u));
+      best[r] = -INFINITY;
+      bi[r] = 0x7fffffff;
+    }
+#pragma unroll
+    for (int t = 0; t < TN; t++) {
+      const int n = tile_col<TN>(bx, t, c);
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int m = mrow0 + r;
+        const float lv = bf_round(v[t][r]);
+        if (m < a.M) a.out[size_t(m) * a.N + n] = uint16_t(f2bf_bits(lv));
+        if (lv > best[r] || (lv == best[r] && n < bi[r])) {
+          best[r] = lv;
+          bi[r] = n;
+        }
+      }
+    }
+    if constexpr (EPI == EPI_ARGMAX) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          const float ob = __shfl_xor(best[r], o, kWave);
+          const int oi = __shfl_xor(bi[r], o, kWave);
+          if (ob > best[r] || (ob == best[r] && oi < bi[r])) {
+            best[r] = ob;
+            bi[r] = oi;
+          }
+        }
+        if (c == 0) {
+          a.am_val[bx * kMaxM + mrow0 + r] = best[r];
+          a.am_idx[bx * kMaxM + mrow0 + r] = bi[r];
+        }
+      }
+    }
+  } else if constexpr (EPI == EPI_SILU) {
+    // Interleaved rows: even lane = gate_j, odd lane = up_j, j = column / 2.
+    const int n = tile_col<TN>(bx, 0, c);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const float mine = bf_round(v[0][r]);
+      const float other = __shfl_xor(mine, 1, kWave);
+      if ((c & 1) || mrow0 + r >= a.M) continue;
+      a.out[size_t(mrow0 + r) * (a.N >> 1) + (n >> 1)] = uint16_t(f2bf_bits(mine / (1.f + __expf(-mine)) * other));
     }
   } else if constexpr (EPI == EPI_ROPE) {
+    // Interleaved rows within each head: column 2i = dim i, 2i+1 = dim i + D/2.
     const int half = a.D >> 1;
-    const int col = tile_col<EPI, TN>(a, bx, 0, c);
-    const int head = col / a.D, i = col % a.D;  // i < half
+    const int col = tile_col<TN>(bx, 0, c);
+    const int head = col / a.D, i = (col % a.D) >> 1;
+    const bool second = c & 1;
     const float inv_freq = exp2f(-a.log2_theta * (2.f * i) / a.D);
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const int m = mrow0 + r;
+      const float mine = bf_round(v[0][r]);
+      const float other = __shfl_xor(mine, 1, kWave);
       if (m >= a.M) continue;
-      const float x1 = bf_round(v[0][r]), x2 = bf_round(v[1][r]);
-      const int p = min(max(a.pos[m], 0), a.Smax - 1);  // host validates; never write outside the cache
+      // Host validates; clamped anyway so a bad index can never write outside the cache.
+      const int p = min(max(a.pos[m], 0), a.Smax - 1);
+      const int sl = a.slot ? min(max(a.slot[m], 0), a.nslots - 1) : m;
+      const int d = i + (second ? half : 0);
       if (head < a.H + a.Hkv) {
         float sn, cs;
         sincosf(float(p) * inv_freq, &sn, &cs);
-        const uint16_t o1 = uint16_t(f2bf_bits(x1 * cs - x2 * sn));
-        const uint16_t o2 = uint16_t(f2bf_bits(x2 * cs + x1 * sn));
-        uint16_t* dst;
-        if (head < a.H)
-          dst = a.q_out + (size_t(m) * a.H + head) * a.D;
-        else
-          dst = a.kc + ((size_t(m) * a.Smax + p) * a.Hkv + (head - a.H)) * a.D;
-        dst[i] = o1;
-        dst[i + half] = o2;
+        const float x1 = second ? other : mine, x2 = second ? mine : other;
+        const float o = second ? x2 * cs + x1 * sn : x1 * cs - x2 * sn;
+        uint16_t* dst = head < a.H ? a.q_out + (size_t(m) * a.H + head) * a.D
+                                   : a.kc + ((size_t(sl) * a.Smax + p) * a.Hkv + (head - a.H)) * a.D;
+        dst[d] = uint16_t(f2bf_bits(o));
       } else {
-        uint16_t* dst = a.vc + ((size_t(m) * a.Smax + p) * a.Hkv + (head - a.H - a.Hkv)) * a.D;
-        dst[i] = uint16_t(f2bf_bits(x1));
-        dst[i + half] = uint16_t(f2bf_bits(x2));
+        a.vc[((size_t(sl) * a.Smax + p) * a.Hkv + (head - a.H - a.Hkv)) * a.D + d] = uint16_t(f2bf_bits(mine));
       }
     }
   } else if constexpr (EPI == EPI_RESID) {
     float sq[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < TN; t++) {
-      const int n = tile_col<EPI, TN>(a, bx, t, c);
+      const int n = tile_col<TN>(bx, t, c);
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         const int m = mrow0 + r;
@@ -270,81 +301,55 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
       for (int o = 1; o < 16; o <<= 1) sq[r] += __shfl_xor(sq[r], o, kWave);
       if (c == 0) a.ss_out[bx * kMaxM + mrow0 + r] = sq[r];
     }
-  } else if constexpr (EPI == EPI_ARGMAX) {
-    float best[4];
-    int bi[4];
+  }
+}
+
+// Greedy sampling, second stage: one block per row merges the LM-head blocks'
+// winners (first index on ties).
+__global__ __launch_bounds__(256) void k_argmax_merge(const float* __restrict__ am_val, const int* __restrict__ am_idx,
+                                                      int parts, int64_t* __restrict__ ids) {
+  const int m = blockIdx.x;
+  float b = -INFINITY;
+  int i = 0x7fffffff;
+  for (int p0 = threadIdx.x; p0 < parts; p0 += 8 * 256) {
+    float pv[8];
+    int pi[8];
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
-      best[r] = -INFINITY;
-      bi[r] = 0x7fffffff;
+    for (int j = 0; j < 8; j++) {  // 8 loads in flight per thread
+      const int p = p0 + j * 256;
+      pv[j] = p < parts ? am_val[p * kMaxM + m] : -INFINITY;
+      pi[j] = p < parts ? am_idx[p * kMaxM + m] : 0x7fffffff;
     }
 #pragma unroll
-    for (int t = 0; t < TN; t++) {
-      const int n = tile_col<EPI, TN>(a, bx, t, c);
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int m = mrow0 + r;
-        const float lv = bf_round(v[t][r]);
-        if (m < a.M) a.out[size_t(m) * a.N + n] = uint16_t(f2bf_bits(lv));
-        if (lv > best[r] || (lv == best[r] && n < bi[r])) {
-          best[r] = lv;
-          bi[r] = n;
-        }
+    for (int j = 0; j < 8; j++)
+      if (pv[j] > b || (pv[j] == b && pi[j] < i)) {
+        b = pv[j];
+        i = pi[j];
       }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(b, o, kWave);
+    const int oi = __shfl_xor(i, o, kWave);
+    if (ob > b || (ob == b && oi < i)) {
+      b = ob;
+      i = oi;
     }
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        const float ob = __shfl_xor(best[r], o, kWave);
-        const int oi = __shfl_xor(bi[r], o, kWave);
-        if (ob > best[r] || (ob == best[r] && oi < bi[r])) {
-          best[r] = ob;
-          bi[r] = oi;
-        }
+  }
+  __shared__ float sb[4];
+  __shared__ int si[4];
+  if ((threadIdx.x & 63) == 0) {
+    sb[threadIdx.x >> 6] = b;
+    si[threadIdx.x >> 6] = i;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; w++)
+      if (sb[w] > b || (sb[w] == b && si[w] < i)) {
+        b = sb[w];
+        i = si[w];
       }
-      if (c == 0) {
-        st_wt(a.am_val + bx * kMaxM + mrow0 + r, best[r]);
-        st_wt(a.am_idx + bx * kMaxM + mrow0 + r, bi[r]);
-      }
-    }
-    // Last block to finish merges every block's winners.
-    drain_stores();
-    unsigned ticket = 0;
-    if (lane == 0) ticket = arrive(a.am_count);
-    ticket = __shfl(ticket, 0, kWave);
-    if (ticket != gridDim.x - 1) return;
-    for (int m = 0; m < a.M; m++) {
-      float b = -INFINITY;
-      int i = 0x7fffffff;
-      for (int p0 = lane; p0 < int(gridDim.x); p0 += 8 * kWave) {
-        float pv[8];
-        int pi[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) {  // 8 loads in flight per lane
-          const int p = p0 + j * kWave;
-          pv[j] = p < int(gridDim.x) ? ld_wt(a.am_val + p * kMaxM + m) : -INFINITY;
-          pi[j] = p < int(gridDim.x) ? ld_wt(a.am_idx + p * kMaxM + m) : 0x7fffffff;
-        }
-#pragma unroll
-        for (int j = 0; j < 8; j++)
-          if (pv[j] > b || (pv[j] == b && pi[j] < i)) {
-            b = pv[j];
-            i = pi[j];
-          }
-      }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const float ob = __shfl_xor(b, o, kWave);
-        const int oi = __shfl_xor(i, o, kWave);
-        if (ob > b || (ob == b && oi < i)) {
-          b = ob;
-          i = oi;
-        }
-      }
-      if (lane == 0) a.ids[m] = i;
-    }
-    if (lane == 0) st_wt(a.am_count, 0u);  // self-resetting for the next step / graph replay
+    ids[m] = i;
   }
 }
 
@@ -376,12 +381,14 @@ __global__ __launch_bounds__(256) void k_embed(const uint16_t* __restrict__ embe
 
 // ------------------------------------------------------------ attention
 // As k_decode_attn in kernels.hip (split-K over 64-token chunks, K/V tiles in
-// LDS shared by the GQA group, one wave per query head), plus: lens = pos + 1,
+// LDS shared by the GQA group, one wave per query head), plus: row b reads
+// cache slot slot[b] (several rows may share a slot: chunked prefill), lens = pos + 1,
 // and the last split to finish for a (sequence, KV head) merges the partials
 // (arrival ticket, self-resetting) and writes the bf16 output [B][H*D].
 template <int D>
 __global__ __launch_bounds__(512) void k_attn(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
                                               const uint16_t* __restrict__ vc, const int* __restrict__ pos,
+                                              const int* __restrict__ slot, int nslots,
                                               float* __restrict__ part_o, float* __restrict__ part_ml,
                                               unsigned* __restrict__ counters, uint16_t* __restrict__ out, int H,
                                               int Hkv, int Smax, int chunk, int nsplit, float scale) {
@@ -396,6 +403,7 @@ __global__ __launch_bounds__(512) void k_attn(const uint16_t* __restrict__ q, co
   const int b = blockIdx.y / Hkv, kvh = blockIdx.y % Hkv;
   const int G = H / Hkv;
   const int len = min(max(pos[b], 0), Smax - 1) + 1;
+  const int sb = slot ? min(max(slot[b], 0), nslots - 1) : b;  // cache slot of row b
   const int g = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int start = split * chunk;
   const int stop = min(start + chunk, len);
@@ -418,8 +426,8 @@ __global__ __launch_bounds__(512) void k_attn(const uint16_t* __restrict__ q, co
   for (int k = 0; k < DPL; k++) acc[k] = 0.f;
 
   const size_t tok_stride = size_t(Hkv) * D;
-  const uint16_t* kbase = kc + (size_t(b) * Smax) * tok_stride + size_t(kvh) * D;
-  const uint16_t* vbase = vc + (size_t(b) * Smax) * tok_stride + size_t(kvh) * D;
+  const uint16_t* kbase = kc + (size_t(sb) * Smax) * tok_stride + size_t(kvh) * D;
+  const uint16_t* vbase = vc + (size_t(sb) * Smax) * tok_stride + size_t(kvh) * D;
 
   for (int t0 = start; t0 < stop; t0 += TILE) {
     const int nt = min(TILE, stop - t0);
@@ -500,15 +508,15 @@ __global__ __launch_bounds__(512) void k_attn(const uint16_t* __restrict__ q, co
     }
     const int n = min(kWave, used - s0);
     const float* pob = part_o + (hb * nsplit + s0) * D + lane;
-    // 8 splits' partials in flight at once (one wait per group, not per split).
-    for (int j0 = 0; j0 < n; j0 += 8) {
-      float pv[8][DPL];
+    // 16 splits' partials in flight at once (one wait per group, not per split).
+    for (int j0 = 0; j0 < n; j0 += 16) {
+      float pv[16][DPL];
 #pragma unroll
-      for (int jj = 0; jj < 8; jj++)
+      for (int jj = 0; jj < 16; jj++)
 #pragma unroll
         for (int k = 0; k < DPL; k++) pv[jj][k] = j0 + jj < n ? ld_wt(pob + size_t(j0 + jj) * D + k * kWave) : 0.f;
 #pragma unroll
-      for (int jj = 0; jj < 8; jj++) {
+      for (int jj = 0; jj < 16; jj++) {
         const float wj = __shfl(ws, (j0 + jj) & 63, kWave);
 #pragma unroll
         for (int k = 0; k < DPL; k++) o[k] += wj * pv[jj][k];
@@ -530,7 +538,7 @@ struct LlamaDims {
 };
 
 constexpr int kChunk = 64;
-constexpr int kTnResid = 1, kTnStore = 2;
+constexpr int kTnResid = 1, kTnStore = 1;
 
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -574,16 +582,30 @@ int pick_nw(int K) {
   return (K >> 5) <= 64 ? 8 : 16;
 }
 
+template <int NW, int TN, int EPI>
+hipError_t launch_nw(const GemmArgs& a, int grid, hipStream_t s) {
+  // Load batch: each wave's share of k-steps, rounded up to a power of two,
+  // capped by the VGPR budget (8, or 4 for 1024-thread two-subtile blocks).
+  constexpr int kCap = (NW >= 16 && TN >= 2) ? 4 : 8;
+  const int per_wave = ((a.K >> 5) + NW - 1) / NW;
+  const dim3 g(grid), b(NW * 64);
+  if (per_wave <= 1)
+    hipLaunchKernelGGL((k_skinny<NW, TN, EPI, 1>), g, b, 0, s, a);
+  else if (per_wave <= 2)
+    hipLaunchKernelGGL((k_skinny<NW, TN, EPI, 2>), g, b, 0, s, a);
+  else if (per_wave <= 4 || kCap == 4)
+    hipLaunchKernelGGL((k_skinny<NW, TN, EPI, 4>), g, b, 0, s, a);
+  else
+    hipLaunchKernelGGL((k_skinny<NW, TN, EPI, (kCap > 4 ? 8 : 4)>), g, b, 0, s, a);
+  return hipGetLastError();
+}
+
 template <int EPI, int TN>
 hipError_t launch_gemm(const GemmArgs& a, int grid, hipStream_t s) {
   const int nw = pick_nw(a.K);
-  if (nw == 16)
-    hipLaunchKernelGGL((k_skinny<16, TN, EPI>), dim3(grid), dim3(1024), 0, s, a);
-  else if (nw == 8)
-    hipLaunchKernelGGL((k_skinny<8, TN, EPI>), dim3(grid), dim3(512), 0, s, a);
-  else
-    return hipErrorInvalidValue;
-  return hipGetLastError();
+  if (nw == 16) return launch_nw<16, TN, EPI>(a, grid, s);
+  if (nw == 8) return launch_nw<8, TN, EPI>(a, grid, s);
+  return hipErrorInvalidValue;
 }
 
 bool dims_ok(const LlamaDims& d) {
@@ -611,14 +633,19 @@ size_t p2pt_llama_ws_bytes(const LlamaDims* d) {
 //      attn_norm, wqkv [(H+2Hkv)*D, dim], wo [dim, H*D], ffn_norm, w_gate_up [2*ffn, dim], w_down [dim, ffn]
 //      where wqkv, w_gate_up and lm_head carry the preceding RMSNorm weight folded
 //      into their columns (W[n][k] * g[k]); the norm-weight slots are not read.
+//      wqkv rows are interleaved per head (dim i, dim i + D/2, ...) and w_gate_up
+//      rows per pair (gate_j, up_j, ...).
 //   k_cache/v_cache: [n_layers][max_batch][max_seq][Hkv][D]
 //   tokens int64 [B], pos int32 [B] (< max_seq), logits bf16 [B][vocab], ids int64 [B]
+//   slots int32 [B] or nullptr: cache slot of each row (< max_batch). Rows of one
+//     slot at consecutive positions form a prefill chunk: every row's K/V is
+//     appended before attention runs, and each row attends up to its own position.
 //   max_len: host bound on max(pos) + 1 (sizes the attention grid; use max_seq under graph capture)
 int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, void* v_cache, const int64_t* tokens,
-                      const int* pos, int B, int max_len, void* ws, size_t ws_bytes, void* logits, int64_t* ids,
-                      void* stream) {
+                      const int* pos, const int* slots, int B, int max_len, void* ws, size_t ws_bytes, void* logits,
+                      int64_t* ids, void* stream) {
   const LlamaDims d = *dp;
-  if (!dims_ok(d) || B <= 0 || B > kMaxM || B > d.max_batch || max_len <= 0 || max_len > d.max_seq)
+  if (!dims_ok(d) || B <= 0 || B > kMaxM || (!slots && B > d.max_batch) || max_len <= 0 || max_len > d.max_seq)
     return int(hipErrorInvalidValue);
   Workspace W = carve(d, static_cast<uint8_t*>(ws));
   if (ws_bytes < W.bytes) return int(hipErrorInvalidValue);
@@ -649,19 +676,19 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
     // QKV + RoPE + cache append
     a.x = W.resid; a.w = wqkv; a.N = qkv_n; a.K = d.dim;
     a.ss_part = W.ss; a.ss_parts = ss_parts;
-    a.pos = pos; a.q_out = W.q; a.kc = kc; a.vc = vc;
+    a.pos = pos; a.slot = slots; a.nslots = d.max_batch; a.q_out = W.q; a.kc = kc; a.vc = vc;
     a.H = d.H; a.Hkv = d.Hkv; a.D = d.D; a.Smax = d.max_seq; a.log2_theta = log2_theta;
-    if ((e = launch_gemm<EPI_ROPE, 2>(a, qkv_n / 32, s)) != hipSuccess) return int(e);
+    if ((e = launch_gemm<EPI_ROPE, 1>(a, qkv_n / 16, s)) != hipSuccess) return int(e);
 
     // attention
     dim3 grid(nsplit, B * d.Hkv);
     dim3 blk(64 * (d.H / d.Hkv));
     const float scale = 1.f / sqrtf(float(d.D));
     if (d.D == 64)
-      hipLaunchKernelGGL(k_attn<64>, grid, blk, 0, s, W.q, kc, vc, pos, W.part_o, W.part_ml, W.counters, W.attn, d.H,
+      hipLaunchKernelGGL(k_attn<64>, grid, blk, 0, s, W.q, kc, vc, pos, slots, d.max_batch, W.part_o, W.part_ml, W.counters, W.attn, d.H,
                          d.Hkv, d.max_seq, kChunk, nsplit_ws, scale);
     else
-      hipLaunchKernelGGL(k_attn<128>, grid, blk, 0, s, W.q, kc, vc, pos, W.part_o, W.part_ml, W.counters, W.attn,
+      hipLaunchKernelGGL(k_attn<128>, grid, blk, 0, s, W.q, kc, vc, pos, slots, d.max_batch, W.part_o, W.part_ml, W.counters, W.attn,
                          d.H, d.Hkv, d.max_seq, kChunk, nsplit_ws, scale);
     if ((e = hipGetLastError()) != hipSuccess) return int(e);
 
@@ -676,7 +703,7 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
     GemmArgs g{};
     g.M = B; g.eps = d.eps; g.x = W.resid; g.w = wgu; g.N = 2 * d.ffn; g.K = d.dim;
     g.ss_part = W.ss; g.ss_parts = ss_parts; g.out = W.h;
-    if ((e = launch_gemm<EPI_SILU, 2>(g, d.ffn / 16, s)) != hipSuccess) return int(e);
+    if ((e = launch_gemm<EPI_SILU, 1>(g, 2 * d.ffn / 16, s)) != hipSuccess) return int(e);
 
     // down + residual
     GemmArgs dn{};
@@ -689,9 +716,11 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
   h.M = B; h.eps = d.eps; h.x = W.resid; h.w = bf(2); h.N = d.vocab; h.K = d.dim;
   h.ss_part = W.ss; h.ss_parts = ss_parts;
   h.out = static_cast<uint16_t*>(logits);
-  h.am_val = W.am_val; h.am_idx = W.am_idx; h.am_count = W.counters + kMaxM * d.Hkv; h.ids = ids;
-  if ((e = launch_gemm<EPI_ARGMAX, kTnStore>(h, d.vocab / (16 * kTnStore), s)) != hipSuccess) return int(e);
-  return int(hipSuccess);
+  h.am_val = W.am_val; h.am_idx = W.am_idx;
+  const int parts = d.vocab / (16 * kTnStore);
+  if ((e = launch_gemm<EPI_ARGMAX, kTnStore>(h, parts, s)) != hipSuccess) return int(e);
+  hipLaunchKernelGGL(k_argmax_merge, dim3(B), dim3(256), 0, s, W.am_val, W.am_idx, parts, ids);
+  return int(hipGetLastError());
 }
 
 // Standalone skinny GEMM (tests/benchmarks): out[M][N] = bf16(x[M][K] @ w[N][K]^T), M <= 16.

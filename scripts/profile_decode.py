@@ -37,7 +37,7 @@ def main():
     m.k_cache.normal_()
     m.v_cache.normal_()
     if not a.eager:
-        m.capture_graph()
+        m.capture_graph(rows=a.batch)
     B = a.batch
     tok = torch.randint(0, m.cfg.vocab, (B,), device="cuda")
 
