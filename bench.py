@@ -85,10 +85,12 @@ def start_mock(kind, interval_ms, tokens):
     return p, port
 
 
-def loadgen(port, streams, steps, warmup=0):
+def loadgen(port, streams, steps, warmup=0, path=None):
     from p2p_llm_tunnel_amd import binary
+    extra = ["--path", path] if path else []
     out = subprocess.run([binary("tunnel-loadgen"), "--target", f"127.0.0.1:{port}", "--streams", str(streams),
-                          "--steps", str(steps), "--warmup", str(warmup)], capture_output=True, text=True, timeout=600)
+                          "--steps", str(steps), "--warmup", str(warmup)] + extra, capture_output=True, text=True,
+                         timeout=600)
     try:
         return json.loads(out.stdout.strip().splitlines()[-1])
     except (IndexError, ValueError):

@@ -28,20 +28,20 @@ from p2p_llm_tunnel_amd.utils.build import ensure_native  # noqa: E402
 from p2p_llm_tunnel_amd.utils.procs import Tunnel  # noqa: E402
 
 
-def sse_matrix(transport, mock_kind, streams_list, steps, threaded=True, busy_poll_us=0):
+def sse_matrix(transport, mock_kind, streams_list, steps, threaded=True, busy_poll_us=0, path=None):
     mock, port = start_mock(mock_kind, 100, 5) if (mock_kind == "native" or threaded) else _unthreaded()
     rows = []
     extra = ["--busy-poll-us", str(busy_poll_us)] if busy_poll_us else []
     try:
         with Tunnel(f"http://127.0.0.1:{port}", transport=transport, serve_extra=extra, proxy_extra=extra) as t:
             for s in streams_list:
-                loadgen(t.proxy_port, s, 1)
-                tr = loadgen(t.proxy_port, s, steps)
+                loadgen(t.proxy_port, s, 1, path=path)
+                tr = loadgen(t.proxy_port, s, steps, path=path)
                 if not threaded:
                     time.sleep(1.3)  # let serve's spare upstream sockets expire (single-threaded upstream)
-                dr = loadgen(port, s, steps)
+                dr = loadgen(port, s, steps, path=path)
                 rows.append({"transport": transport, "mock": mock_kind if threaded else "python-unthreaded",
-                             "busy_poll_us": busy_poll_us,
+                             "busy_poll_us": busy_poll_us, "path": path or "/v1/chat/completions",
                              "streams": s, "tunneled_req_s": tr["req_s"], "direct_req_s": dr["req_s"],
                              "tunneled_p50_ttft_ms": tr["p50_ttft_ms"], "direct_p50_ttft_ms": dr["p50_ttft_ms"],
                              "added_p50_ttft_ms": tr["p50_ttft_ms"] - dr["p50_ttft_ms"],
@@ -121,6 +121,8 @@ def main():
         res["sse"] += sse_matrix("tcp", "native", streams, a.steps)
         res["sse"] += sse_matrix("webrtc", "python", streams, a.steps)
         res["sse"] += sse_matrix("webrtc", "python", [1, 2, 4, 8], 3, threaded=False)
+    # BASELINE config #2: Ollama /api/generate NDJSON stream, up to 8 concurrent streams.
+    res["sse"] += sse_matrix("webrtc", "native", [1, 8], a.steps, path="/api/generate")
     for bp in [int(x) for x in a.busy_poll.split(",") if x]:
         res["sse"] += sse_matrix("webrtc", "native", [1, 8], a.steps, busy_poll_us=bp)
     res["post_64x1MB"] = [post_1mb("webrtc")]

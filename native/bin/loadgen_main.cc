@@ -184,7 +184,10 @@ int main(int argc, char** argv) {
     } else if (a == "--streams") o.streams = atoi(v.c_str());
     else if (a == "--steps") o.steps = atoi(v.c_str());
     else if (a == "--warmup") warmup = atoi(v.c_str());
-    else if (a == "--path") o.path = v;
+    else if (a == "--path") {
+      o.path = v;
+      if (v == "/api/generate") o.body = R"({"model": "test-model", "prompt": "hi", "stream": true})";
+    } else if (a == "--body") o.body = v;
     else if (a == "--post-bytes") o.post_bytes = size_t(strtoull(v.c_str(), nullptr, 10));
   }
   signal(SIGPIPE, SIG_IGN);

@@ -32,6 +32,15 @@ std::string chunk_event(const char* tok) {
          "\"delta\": " + delta + ", \"finish_reason\": " + fin + "}]}\n\n";
 }
 
+// Ollama /api/generate stream: one NDJSON object per token, then a done record.
+std::string ollama_line(const char* tok) {
+  if (!tok)
+    return "{\"model\": \"test-model\", \"created_at\": \"2026-01-01T00:00:00Z\", \"response\": \"\", \"done\": true, "
+           "\"done_reason\": \"stop\", \"eval_count\": 5}\n";
+  return std::string("{\"model\": \"test-model\", \"created_at\": \"2026-01-01T00:00:00Z\", \"response\": \"") + tok +
+         "\", \"done\": false}\n";
+}
+
 struct Server {
   Reactor& r;
   uint64_t interval_ms;
@@ -47,9 +56,11 @@ struct Server {
     c->close_after_flush();
   }
 
-  void sse(const std::shared_ptr<TcpConn>& c) {
+  // Token stream: SSE chat-completion chunks, or Ollama NDJSON when `ollama`.
+  void sse(const std::shared_ptr<TcpConn>& c, bool ollama = false) {
     c->write(std::string("HTTP/1.0 200 OK\r\nServer: p2pt-mock\r\nDate: ") + http::http_date_now() +
-             "\r\nContent-Type: text/event-stream\r\nCache-Control: no-cache\r\n\r\n");
+             (ollama ? "\r\nContent-Type: application/x-ndjson\r\n\r\n"
+                     : "\r\nContent-Type: text/event-stream\r\nCache-Control: no-cache\r\n\r\n"));
     auto step = std::make_shared<std::function<void(int)>>();
     std::weak_ptr<TcpConn> w = c;
     Reactor* rp = &r;
@@ -57,15 +68,16 @@ struct Server {
     int n = tokens;
     // The pending timer owns the step; the step refers to itself weakly.
     std::weak_ptr<std::function<void(int)>> ws = step;
-    *step = [w, rp, iv, n, ws](int i) {
+    *step = [w, rp, iv, n, ws, ollama](int i) {
       auto conn = w.lock();
       if (!conn || conn->closed()) return;
       if (i < n) {
-        conn->write(chunk_event(i < 5 ? kTokens[i] : " tok"));
+        const char* tok = i < 5 ? kTokens[i] : " tok";
+        conn->write(ollama ? ollama_line(tok) : chunk_event(tok));
         if (auto s = ws.lock()) rp->call_later_ms(iv, [s, i] { (*s)(i + 1); });
         return;
       }
-      conn->write(chunk_event(nullptr) + "data: [DONE]\n\n");
+      conn->write(ollama ? ollama_line(nullptr) : chunk_event(nullptr) + "data: [DONE]\n\n");
       conn->close_after_flush();
     };
     (*step)(0);
@@ -90,6 +102,15 @@ struct Server {
       else
         respond(c, 200, "application/json",
                 R"({"id": "chatcmpl-test", "object": "chat.completion", "choices": [{"index": 0, "message": {"role": "assistant", "content": "Hello from the tunnel!"}, "finish_reason": "stop"}], "usage": {"prompt_tokens": 10, "completion_tokens": 5, "total_tokens": 15}})");
+    } else if (h.method == "GET" && path == "/api/tags") {
+      respond(c, 200, "application/json", R"({"models": [{"name": "test-model", "model": "test-model"}]})");
+    } else if (h.method == "POST" && path == "/api/generate") {
+      // Ollama streams unless the request says "stream": false.
+      bool stream = body.find("\"stream\": false") == std::string::npos && body.find("\"stream\":false") == std::string::npos;
+      if (stream) sse(c, true);
+      else
+        respond(c, 200, "application/json",
+                R"({"model": "test-model", "response": "Hello from the tunnel!", "done": true, "done_reason": "stop"})");
     } else if (h.method == "POST" && path == "/echo") {
       respond(c, 200, "application/octet-stream", body);
     } else {

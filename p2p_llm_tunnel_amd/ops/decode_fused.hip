@@ -157,7 +157,9 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
   const int kq = (lane >> 4) << 3;
   const int S = a.K >> 5;
   const int s0 = wv * S / NW, s1 = (wv + 1) * S / NW;
-  const uint16_t* xrow = a.x + size_t(m_a) * a.K + kq;
+  // Rows past M are loaded from row M-1 (in bounds) and zeroed: the batch's
+  // loads are unconditional.
+  const uint16_t* xrow = a.x + size_t(min(m_a, a.M - 1)) * a.K + kq;
   const uint16_t* wrow[TN];
 #pragma unroll
   for (int t = 0; t < TN; t++) wrow[t] = a.w + size_t(tile_col<TN>(bx, t, lane & 15)) * a.K + kq;
