@@ -59,21 +59,33 @@ def test_fused_matches_unfused(cfg, B):
 
 
 @cuda
-def test_fused_ragged_positions():
+@pytest.mark.parametrize("cfg,positions", [("micro", [0, 63, 64, 300]),
+                                           # head_dim 128: 1024-token workgroup splits, merged across splits
+                                           ("small", [3, 1023, 1024, 2500])])
+def test_fused_ragged_positions(cfg, positions):
     # Slots at different positions in one step (continuous batching).
     from p2p_llm_tunnel_amd.models.tiny_llm import TinyLlama
-    mf = TinyLlama("micro", device="cuda", max_batch=4, seed=6, fused=True)
-    mu = TinyLlama("micro", device="cuda", max_batch=4, seed=6, fused=False)
+    mf = TinyLlama(cfg, device="cuda", max_batch=4, seed=6, fused=True)
+    mu = TinyLlama(cfg, device="cuda", max_batch=4, seed=6, fused=False)
     torch.manual_seed(2)
     mf.k_cache.normal_()
     mf.v_cache.normal_()
     mu.k_cache.copy_(mf.k_cache)
     mu.v_cache.copy_(mf.v_cache)
     toks = torch.randint(0, mf.cfg.vocab, (4,), device="cuda")
-    pos = torch.tensor([0, 63, 64, 300], dtype=torch.int32, device="cuda")
-    _, lf = mf.decode_step(toks, pos, (0, 300), return_logits=True)
-    _, lu = mu.decode_step(toks, pos, (0, 300), return_logits=True)
+    pos = torch.tensor(positions, dtype=torch.int32, device="cuda")
+    rng = (min(positions), max(positions))
+    _, lf = mf.decode_step(toks, pos, rng, return_logits=True)
+    _, lu = mu.decode_step(toks, pos, rng, return_logits=True)
     assert (lf.float() - lu.float()).abs().max().item() < 0.03 * lu.float().abs().max().item()
+    # the graph path launches for cache capacity (idle splits exit early)
+    mf.k_cache.copy_(mu.k_cache)
+    mf.v_cache.copy_(mu.v_cache)
+    mf.capture_graph(rows=4)
+    mf.k_cache.copy_(mu.k_cache)
+    mf.v_cache.copy_(mu.v_cache)
+    _, lg = mf.graph_step(toks, pos, return_logits=True)
+    assert (lg.float() - lu.float()).abs().max().item() < 0.03 * lu.float().abs().max().item()
 
 
 @cuda
