@@ -391,7 +391,6 @@ __global__ __launch_bounds__(256) void k_embed(const uint16_t* __restrict__ embe
 // tiles per wave) needs no cross-workgroup traffic; longer rows use several
 // splits whose last finisher merges them (write-through partials + arrival
 // ticket). Row b reads cache slot slot[b] (rows of one slot = prefill chunk).
-constexpr int kGMax = 8;
 
 template <int D>
 __device__ __forceinline__ void merge_splits(size_t hb, int used, int nsplit, const float* part_o, const float* part_ml,
@@ -439,18 +438,21 @@ __global__ __launch_bounds__(NWV * 64) void k_attn(const uint16_t* __restrict__ 
                                                    const int* __restrict__ slot, int nslots, float* __restrict__ part_o,
                                                    float* __restrict__ part_ml, unsigned* __restrict__ counters,
                                                    uint16_t* __restrict__ out, int H, int Hkv, int Smax, int split_tok,
-                                                   int nsplit, float scale) {
+                                                   int nsplit, float scale, int ngrp) {
   constexpr int TILE = 64;
   constexpr int VROW = D * 2 + 16;  // padded V row in LDS: conflict-free column reads
   constexpr int DPL = D / kWave;
   constexpr int VPR = D / 8;        // 16-byte pieces per K/V row
   __shared__ __attribute__((aligned(16))) uint8_t vs[NWV][TILE * VROW];
-  __shared__ float qs[kGMax][D];
   __shared__ unsigned s_ticket;
 
+  // blockIdx.y = g * ngrp + (b * Hkv + kvh): the G query heads of one KV head
+  // are ngrp blocks apart, i.e. on the same XCD when ngrp % 8 == 0 (K/V from L2).
   const int split = blockIdx.x;
-  const int b = blockIdx.y / Hkv, kvh = blockIdx.y % Hkv;
+  const int grp = blockIdx.y % ngrp, gq = blockIdx.y / ngrp;
+  const int b = grp / Hkv, kvh = grp % Hkv;
   const int G = H / Hkv;
+  const size_t hb = size_t(b) * H + size_t(kvh) * G + gq;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int len = min(max(pos[b], 0), Smax - 1) + 1;
   const int sb = slot ? min(max(slot[b], 0), nslots - 1) : b;
@@ -459,110 +461,81 @@ __global__ __launch_bounds__(NWV * 64) void k_attn(const uint16_t* __restrict__ 
   if (start >= len) return;  // splits past this row's length (graphs launch for capacity)
   const int stop = min(start + split_tok, len);
 
-  for (int e = threadIdx.x; e < G * D; e += NWV * kWave)
-    qs[e / D][e % D] = bf2f(q[(size_t(b) * H + size_t(kvh) * G) * D + e]) * scale;
-  __syncthreads();
+  uint4 qv[VPR];  // this head's query row (same for every lane)
+#pragma unroll
+  for (int c = 0; c < VPR; c++) qv[c] = *reinterpret_cast<const uint4*>(q + hb * D + c * 8);
 
   const size_t tok_stride = size_t(Hkv) * D;
   const uint16_t* kbase = kc + size_t(sb) * Smax * tok_stride + size_t(kvh) * D;
   const uint16_t* vbase = vc + size_t(sb) * Smax * tok_stride + size_t(kvh) * D;
   uint8_t* vw = vs[wv];
 
-  float m[kGMax], l[kGMax], acc[kGMax][DPL];
+  float m = -INFINITY, l = 0.f, acc[DPL];
 #pragma unroll
-  for (int g = 0; g < kGMax; g++) {
-    m[g] = -INFINITY;
-    l[g] = 0.f;
-#pragma unroll
-    for (int k = 0; k < DPL; k++) acc[g][k] = 0.f;
-  }
+  for (int k = 0; k < DPL; k++) acc[k] = 0.f;
 
   for (int t0 = start + wv * TILE; t0 < stop; t0 += NWV * TILE) {
     const int nt = min(TILE, stop - t0);
-    uint4 kr[VPR];
-    const int tr = t0 + min(lane, nt - 1);  // rows past nt re-read a valid row, masked below
+    const int tr = t0 + min(lane, nt - 1);  // lanes past nt re-read a valid row, masked below
+    float dot = 0.f;
 #pragma unroll
     for (int c = 0; c < VPR; c++) {
-      kr[c] = *reinterpret_cast<const uint4*>(kbase + size_t(tr) * tok_stride + c * 8);
+      const uint4 kr = *reinterpret_cast<const uint4*>(kbase + size_t(tr) * tok_stride + c * 8);
       *reinterpret_cast<uint4*>(vw + lane * VROW + c * 16) =
           *reinterpret_cast<const uint4*>(vbase + size_t(tr) * tok_stride + c * 8);
-    }
-    float sc[kGMax];
+      float kf[8], qf[8];
+      unpack8(kr, kf);
+      unpack8(qv[c], qf);
 #pragma unroll
-    for (int g = 0; g < kGMax; g++) sc[g] = 0.f;
-#pragma unroll
-    for (int c = 0; c < VPR; c++) {
-      float kf[8];
-      unpack8(kr[c], kf);
-#pragma unroll
-      for (int g = 0; g < kGMax; g++) {
-        if (g >= G) break;
-#pragma unroll
-        for (int j = 0; j < 8; j++) sc[g] += qs[g][c * 8 + j] * kf[j];
-      }
+      for (int j = 0; j < 8; j++) dot += qf[j] * kf[j];
     }
     // V rows staged by this wave are read back by other lanes of the same wave.
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    float p[kGMax];
+    const float s = lane < nt ? dot * scale : -INFINITY;
+    const float mnew = fmaxf(m, wave_max(s));
+    const float p = lane < nt ? __expf(s - mnew) : 0.f;
+    const float corr = __expf(m - mnew);
+    l = l * corr + wave_sum(p);
+    m = mnew;
 #pragma unroll
-    for (int g = 0; g < kGMax; g++) {
-      if (g >= G) break;
-      const float s = lane < nt ? sc[g] : -INFINITY;
-      const float mnew = fmaxf(m[g], wave_max(s));
-      p[g] = lane < nt ? __expf(s - mnew) : 0.f;
-      const float corr = __expf(m[g] - mnew);
-      l[g] = l[g] * corr + wave_sum(p[g]);
-      m[g] = mnew;
-#pragma unroll
-      for (int k = 0; k < DPL; k++) acc[g][k] *= corr;
-    }
+    for (int k = 0; k < DPL; k++) acc[k] *= corr;
     for (int t = 0; t < nt; t++) {
+      const float pt = __shfl(p, t, kWave);
       const uint16_t* vrow = reinterpret_cast<const uint16_t*>(vw + t * VROW);
-      float vv[DPL];
 #pragma unroll
-      for (int k = 0; k < DPL; k++) vv[k] = bf2f(vrow[lane + k * kWave]);
-#pragma unroll
-      for (int g = 0; g < kGMax; g++) {
-        if (g >= G) break;
-        const float pt = __shfl(p[g], t, kWave);
-#pragma unroll
-        for (int k = 0; k < DPL; k++) acc[g][k] += pt * vv[k];
-      }
+      for (int k = 0; k < DPL; k++) acc[k] += pt * bf2f(vrow[lane + k * kWave]);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
 
-  // Merge the waves through LDS (the V tiles are dead now).
+  // Merge the waves through LDS (the V tiles are dead now); wave 0 finishes.
   __syncthreads();
-  float* mlw = reinterpret_cast<float*>(&vs[0][0]);  // [NWV][kGMax][2]
-  float* accw = mlw + NWV * kGMax * 2;              // [NWV][kGMax][D]
-#pragma unroll
-  for (int g = 0; g < kGMax; g++) {
-    if (g >= G) break;
-    if (lane == 0) {
-      mlw[(wv * kGMax + g) * 2] = m[g];
-      mlw[(wv * kGMax + g) * 2 + 1] = l[g];
-    }
-#pragma unroll
-    for (int k = 0; k < DPL; k++) accw[(wv * kGMax + g) * D + lane + k * kWave] = acc[g][k];
+  float* mlw = reinterpret_cast<float*>(&vs[0][0]);  // [NWV][2]
+  float* accw = mlw + NWV * 2;                      // [NWV][D]
+  if (lane == 0) {
+    mlw[wv * 2] = m;
+    mlw[wv * 2 + 1] = l;
   }
+#pragma unroll
+  for (int k = 0; k < DPL; k++) accw[wv * D + lane + k * kWave] = acc[k];
   __syncthreads();
-  const size_t hb = size_t(b) * H + size_t(kvh) * G + wv;  // wave wv merges head wv of the group
-  if (wv < G) {
+  if (wv == 0) {
     float M = -INFINITY;
-    for (int w = 0; w < NWV; w++) M = fmaxf(M, mlw[(w * kGMax + wv) * 2]);
+#pragma unroll
+    for (int w = 0; w < NWV; w++) M = fmaxf(M, mlw[w * 2]);
     float L = 0.f, o[DPL];
 #pragma unroll
     for (int k = 0; k < DPL; k++) o[k] = 0.f;
-    for (int w = 0; w < NWV; w++) {
-      const float mw = mlw[(w * kGMax + wv) * 2];
-      const float e = mw == -INFINITY ? 0.f : __expf(mw - M);  // waves without tokens contribute nothing
-      L += mlw[(w * kGMax + wv) * 2 + 1] * e;
 #pragma unroll
-      for (int k = 0; k < DPL; k++) o[k] += accw[(w * kGMax + wv) * D + lane + k * kWave] * e;
+    for (int w = 0; w < NWV; w++) {
+      const float mw = mlw[w * 2];
+      const float e = mw == -INFINITY ? 0.f : __expf(mw - M);  // waves without tokens contribute nothing
+      L += mlw[w * 2 + 1] * e;
+#pragma unroll
+      for (int k = 0; k < DPL; k++) o[k] += accw[w * D + lane + k * kWave] * e;
     }
     if (used == 1) {
       const float inv = 1.f / L;
@@ -577,16 +550,16 @@ __global__ __launch_bounds__(NWV * 64) void k_attn(const uint16_t* __restrict__ 
         st_wt(part_ml + (hb * nsplit + split) * 2 + 1, L);
       }
       drain_stores();
+      unsigned ticket = 0;
+      if (lane == 0) ticket = arrive(&counters[hb]);
+      ticket = __shfl(ticket, 0, kWave);
+      if (ticket == unsigned(used - 1)) {
+        merge_splits<D>(hb, used, nsplit, part_o, part_ml, out, lane);
+        if (lane == 0) st_wt(&counters[hb], 0u);
+      }
     }
   }
-  if (used == 1) return;
-  __syncthreads();
-  if (threadIdx.x == 0) s_ticket = arrive(&counters[blockIdx.y]);
-  __syncthreads();
-  if (s_ticket != unsigned(used - 1)) return;
-  if (wv < G) merge_splits<D>(hb, used, nsplit, part_o, part_ml, out, lane);
-  __syncthreads();
-  if (threadIdx.x == 0) st_wt(&counters[blockIdx.y], 0u);
+  (void)s_ticket;
 }
 
 // ------------------------------------------------------------ host side
@@ -604,7 +577,7 @@ struct Workspace {
   uint16_t *resid, *q, *attn, *h;
   float *ss, *part_o, *part_ml, *am_val;
   int* am_idx;
-  unsigned* counters;  // [16 * Hkv] attention tickets, then 1 argmax ticket
+  unsigned* counters;  // [16 * H] attention split tickets (self-resetting)
   size_t bytes;
 };
 
@@ -628,7 +601,7 @@ Workspace carve(const LlamaDims& d, uint8_t* base) {
   w.part_ml = reinterpret_cast<float*>(take(size_t(kMaxM) * d.H * nsplit * 2 * 4));
   w.am_val = reinterpret_cast<float*>(take(size_t(am_parts) * kMaxM * 4));
   w.am_idx = reinterpret_cast<int*>(take(size_t(am_parts) * kMaxM * 4));
-  w.counters = reinterpret_cast<unsigned*>(take(size_t(kMaxM * d.Hkv + 1) * 4));
+  w.counters = reinterpret_cast<unsigned*>(take(size_t(kMaxM * d.H) * 4));
   w.bytes = off;
   return w;
 }
@@ -737,25 +710,26 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
     a.H = d.H; a.Hkv = d.Hkv; a.D = d.D; a.Smax = d.max_seq; a.log2_theta = log2_theta;
     if ((e = launch_gemm<EPI_ROPE, 1>(a, qkv_n / 16, s)) != hipSuccess) return int(e);
 
-    // attention: one workgroup per (row, KV head) up to split_tok tokens
-    const int gqa = d.H / d.Hkv;
-    if (d.D == 64) {
-      constexpr int NWV = 16;
-      const int split_tok = NWV * 64 * 2;
-      dim3 grid((max_len + split_tok - 1) / split_tok, B * d.Hkv);
-      hipLaunchKernelGGL((k_attn<64, NWV>), grid, dim3(NWV * 64), 0, s, W.q, kc, vc, pos, slots, d.max_batch,
-                         W.part_o, W.part_ml, W.counters, W.attn, d.H, d.Hkv, d.max_seq, split_tok, nsplit_ws,
-                         1.f / sqrtf(64.f));
-    } else {
-      constexpr int NWV = 8;
-      const int split_tok = NWV * 64 * 2;
-      dim3 grid((max_len + split_tok - 1) / split_tok, B * d.Hkv);
-      hipLaunchKernelGGL((k_attn<128, NWV>), grid, dim3(NWV * 64), 0, s, W.q, kc, vc, pos, slots, d.max_batch,
-                         W.part_o, W.part_ml, W.counters, W.attn, d.H, d.Hkv, d.max_seq, split_tok, nsplit_ws,
-                         1.f / sqrtf(128.f));
+    // attention: one workgroup per (row, query head) for up to split_tok tokens
+    {
+      const int ngrp = B * d.Hkv;
+      if (d.D == 64) {
+        constexpr int NWV = 16;
+        const int split_tok = NWV * 64 * 2;
+        dim3 grid((max_len + split_tok - 1) / split_tok, ngrp * (d.H / d.Hkv));
+        hipLaunchKernelGGL((k_attn<64, NWV>), grid, dim3(NWV * 64), 0, s, W.q, kc, vc, pos, slots, d.max_batch,
+                           W.part_o, W.part_ml, W.counters, W.attn, d.H, d.Hkv, d.max_seq, split_tok, nsplit_ws,
+                           1.f / sqrtf(64.f), ngrp);
+      } else {
+        constexpr int NWV = 8;
+        const int split_tok = NWV * 64 * 2;
+        dim3 grid((max_len + split_tok - 1) / split_tok, ngrp * (d.H / d.Hkv));
+        hipLaunchKernelGGL((k_attn<128, NWV>), grid, dim3(NWV * 64), 0, s, W.q, kc, vc, pos, slots, d.max_batch,
+                           W.part_o, W.part_ml, W.counters, W.attn, d.H, d.Hkv, d.max_seq, split_tok, nsplit_ws,
+                           1.f / sqrtf(128.f), ngrp);
+      }
+      if ((e = hipGetLastError()) != hipSuccess) return int(e);
     }
-    (void)gqa;
-    if ((e = hipGetLastError()) != hipSuccess) return int(e);
 
     // O projection + residual
     GemmArgs o{};
