@@ -382,20 +382,135 @@ __global__ __launch_bounds__(256) void k_embed(const uint16_t* __restrict__ embe
 }
 
 // ------------------------------------------------------------ attention
-// GQA decode attention, one workgroup per (row, KV head, split) with NWV waves.
-// Each wave streams 64-token tiles of its own (tiles wv, wv + NWV, ...): lane t
-// loads K row t straight into registers and scores it against all G query
-// heads of the group (q broadcast from LDS), then stages V row t in its private
-// LDS tile for the P.V pass (lane = head dim). The waves' online-softmax
-// partials are merged through LDS, so a split of up to split_tok tokens (2
-// tiles per wave) needs no cross-workgroup traffic; longer rows use several
-// splits whose last finisher merges them (write-through partials + arrival
-// ticket). Row b reads cache slot slot[b] (rows of one slot = prefill chunk).
-
-template <int D>
-__device__ __forceinline__ void merge_splits(size_t hb, int used, int nsplit, const float* part_o, const float* part_ml,
-                                             uint16_t* out, int lane) {
+// As k_decode_attn in kernels.hip (split-K over `chunk`-token pieces, K/V tiles
+// in LDS shared by the GQA group, one wave per query head; all TPB tiles of a
+// piece are loaded in one pass, so a workgroup makes one memory round trip),
+// plus: row b reads
+// cache slot slot[b] (several rows may share a slot: chunked prefill), lens = pos + 1,
+// and the last split to finish for a (sequence, KV head) merges the partials
+// (arrival ticket, self-resetting) and writes the bf16 output [B][H*D].
+template <int D, int TPB>
+__global__ __launch_bounds__(512) void k_attn(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+                                              const uint16_t* __restrict__ vc, const int* __restrict__ pos,
+                                              const int* __restrict__ slot, int nslots,
+                                              float* __restrict__ part_o, float* __restrict__ part_ml,
+                                              unsigned* __restrict__ counters, uint16_t* __restrict__ out, int H,
+                                              int Hkv, int Smax, int chunk, int nsplit, float scale) {
+  constexpr int TILE = 64;
+  constexpr int ROWB = D * 2 + 16;
   constexpr int DPL = D / kWave;
+  __shared__ __attribute__((aligned(16))) uint8_t ks[TPB * TILE * ROWB];
+  __shared__ __attribute__((aligned(16))) uint8_t vs[TPB * TILE * ROWB];
+  __shared__ unsigned s_ticket;
+
+  const int split = blockIdx.x;
+  const int b = blockIdx.y / Hkv, kvh = blockIdx.y % Hkv;
+  const int G = H / Hkv;
+  const int len = min(max(pos[b], 0), Smax - 1) + 1;
+  const int sb = slot ? min(max(slot[b], 0), nslots - 1) : b;  // cache slot of row b
+  const int g = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int start = split * chunk;
+  const int stop = min(start + chunk, len);
+  const int used = min(nsplit, (len + chunk - 1) / chunk);
+  if (start >= len) return;
+
+  float qf[D];
+  {
+    const uint16_t* qp = q + (size_t(b) * H + kvh * G + g) * D;
+#pragma unroll
+    for (int d = 0; d < D; d += 8) {
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4*>(qp + d), f);
+#pragma unroll
+      for (int k = 0; k < 8; k++) qf[d + k] = f[k] * scale;
+    }
+  }
+  float m = -INFINITY, l = 0.f, acc[DPL];
+#pragma unroll
+  for (int k = 0; k < DPL; k++) acc[k] = 0.f;
+
+  const size_t tok_stride = size_t(Hkv) * D;
+  const uint16_t* kbase = kc + (size_t(sb) * Smax) * tok_stride + size_t(kvh) * D;
+  const uint16_t* vbase = vc + (size_t(sb) * Smax) * tok_stride + size_t(kvh) * D;
+
+  // Cooperative 16-byte loads of every K and V row of this piece into LDS.
+  constexpr int VPR = D / 8;  // uint4 per row
+  const int ntok = stop - start;
+  const int nthr = blockDim.x;
+  constexpr int PER = TPB * TILE * VPR;
+  for (int e0 = threadIdx.x; e0 < PER; e0 += 4 * nthr) {
+    uint4 kv[4], vv[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {  // all loads of the batch in flight before the LDS stores
+      const int e = e0 + i * nthr, t = e / VPR, cc = e % VPR;
+      kv[i] = vv[i] = make_uint4(0, 0, 0, 0);
+      if (e < PER && t < ntok) {
+        kv[i] = *reinterpret_cast<const uint4*>(kbase + size_t(start + t) * tok_stride + cc * 8);
+        vv[i] = *reinterpret_cast<const uint4*>(vbase + size_t(start + t) * tok_stride + cc * 8);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int e = e0 + i * nthr, t = e / VPR, cc = e % VPR;
+      if (e < PER) {
+        *reinterpret_cast<uint4*>(ks + t * ROWB + cc * 16) = kv[i];
+        *reinterpret_cast<uint4*>(vs + t * ROWB + cc * 16) = vv[i];
+      }
+    }
+  }
+  __syncthreads();
+  for (int t0 = 0; t0 < ntok; t0 += TILE) {
+    const int nt = min(TILE, ntok - t0);
+    // Scores: lane = token.
+    float s = -INFINITY;
+    if (lane < nt) {
+      float dot = 0.f;
+#pragma unroll
+      for (int d = 0; d < D; d += 8) {
+        float f[8];
+        unpack8(*reinterpret_cast<const uint4*>(ks + (t0 + lane) * ROWB + d * 2), f);
+#pragma unroll
+        for (int k = 0; k < 8; k++) dot += qf[d + k] * f[k];
+      }
+      s = dot;
+    }
+    const float mnew = fmaxf(m, wave_max(s));
+    const float p = (lane < nt) ? __expf(s - mnew) : 0.f;
+    const float corr = __expf(m - mnew);
+    l = l * corr + wave_sum(p);
+    m = mnew;
+#pragma unroll
+    for (int k = 0; k < DPL; k++) acc[k] *= corr;
+    // P.V: lane = head dim; p_t broadcast across the wave.
+    for (int t = 0; t < nt; t++) {
+      const float pt = __shfl(p, t, kWave);
+      const uint16_t* vrow = reinterpret_cast<const uint16_t*>(vs + (t0 + t) * ROWB);
+#pragma unroll
+      for (int k = 0; k < DPL; k++) acc[k] += pt * bf2f(vrow[lane + k * kWave]);
+    }
+  }
+  const size_t hb = size_t(b) * H + kvh * G + g;
+  if (used == 1) {  // single split: finish directly
+    const float inv = 1.f / l;
+#pragma unroll
+    for (int k = 0; k < DPL; k++) out[hb * D + lane + k * kWave] = uint16_t(f2bf_bits(acc[k] * inv));
+    return;
+  }
+  {
+    float* po = part_o + (hb * nsplit + split) * D;
+#pragma unroll
+    for (int k = 0; k < DPL; k++) st_wt(po + lane + k * kWave, acc[k]);
+    if (lane == 0) {
+      st_wt(part_ml + (hb * nsplit + split) * 2 + 0, m);
+      st_wt(part_ml + (hb * nsplit + split) * 2 + 1, l);
+    }
+  }
+  drain_stores();
+  __syncthreads();
+  if (threadIdx.x == 0) s_ticket = arrive(&counters[blockIdx.y]);
+  __syncthreads();
+  if (s_ticket != unsigned(used - 1)) return;
+  // Merge: lanes over splits for the max / weights, lanes over head dims for the output.
   const float* ml = part_ml + hb * nsplit * 2;
   float M = -INFINITY;
   for (int s = lane; s < used; s += kWave) M = fmaxf(M, ld_wt(ml + 2 * s));
@@ -412,14 +527,15 @@ __device__ __forceinline__ void merge_splits(size_t hb, int used, int nsplit, co
     }
     const int n = min(kWave, used - s0);
     const float* pob = part_o + (hb * nsplit + s0) * D + lane;
-    for (int j0 = 0; j0 < n; j0 += 8) {  // 8 splits' partials in flight at once
-      float pv[8][DPL];
+    // 16 splits' partials in flight at once (one wait per group, not per split).
+    for (int j0 = 0; j0 < n; j0 += 16) {
+      float pv[16][DPL];
 #pragma unroll
-      for (int jj = 0; jj < 8; jj++)
+      for (int jj = 0; jj < 16; jj++)
 #pragma unroll
         for (int k = 0; k < DPL; k++) pv[jj][k] = j0 + jj < n ? ld_wt(pob + size_t(j0 + jj) * D + k * kWave) : 0.f;
 #pragma unroll
-      for (int jj = 0; jj < 8; jj++) {
+      for (int jj = 0; jj < 16; jj++) {
         const float wj = __shfl(ws, (j0 + jj) & 63, kWave);
 #pragma unroll
         for (int k = 0; k < DPL; k++) o[k] += wj * pv[jj][k];
@@ -430,136 +546,8 @@ __device__ __forceinline__ void merge_splits(size_t hb, int used, int nsplit, co
   const float inv = 1.f / L;
 #pragma unroll
   for (int k = 0; k < DPL; k++) out[hb * D + lane + k * kWave] = uint16_t(f2bf_bits(o[k] * inv));
-}
-
-template <int D, int NWV>
-__global__ __launch_bounds__(NWV * 64) void k_attn(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
-                                                   const uint16_t* __restrict__ vc, const int* __restrict__ pos,
-                                                   const int* __restrict__ slot, int nslots, float* __restrict__ part_o,
-                                                   float* __restrict__ part_ml, unsigned* __restrict__ counters,
-                                                   uint16_t* __restrict__ out, int H, int Hkv, int Smax, int split_tok,
-                                                   int nsplit, float scale, int ngrp) {
-  constexpr int TILE = 64;
-  constexpr int VROW = D * 2 + 16;  // padded V row in LDS: conflict-free column reads
-  constexpr int DPL = D / kWave;
-  constexpr int VPR = D / 8;        // 16-byte pieces per K/V row
-  __shared__ __attribute__((aligned(16))) uint8_t vs[NWV][TILE * VROW];
-  __shared__ unsigned s_ticket;
-
-  // blockIdx.y = g * ngrp + (b * Hkv + kvh): the G query heads of one KV head
-  // are ngrp blocks apart, i.e. on the same XCD when ngrp % 8 == 0 (K/V from L2).
-  const int split = blockIdx.x;
-  const int grp = blockIdx.y % ngrp, gq = blockIdx.y / ngrp;
-  const int b = grp / Hkv, kvh = grp % Hkv;
-  const int G = H / Hkv;
-  const size_t hb = size_t(b) * H + size_t(kvh) * G + gq;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int len = min(max(pos[b], 0), Smax - 1) + 1;
-  const int sb = slot ? min(max(slot[b], 0), nslots - 1) : b;
-  const int used = (len + split_tok - 1) / split_tok;
-  const int start = split * split_tok;
-  if (start >= len) return;  // splits past this row's length (graphs launch for capacity)
-  const int stop = min(start + split_tok, len);
-
-  uint4 qv[VPR];  // this head's query row (same for every lane)
-#pragma unroll
-  for (int c = 0; c < VPR; c++) qv[c] = *reinterpret_cast<const uint4*>(q + hb * D + c * 8);
-
-  const size_t tok_stride = size_t(Hkv) * D;
-  const uint16_t* kbase = kc + size_t(sb) * Smax * tok_stride + size_t(kvh) * D;
-  const uint16_t* vbase = vc + size_t(sb) * Smax * tok_stride + size_t(kvh) * D;
-  uint8_t* vw = vs[wv];
-
-  float m = -INFINITY, l = 0.f, acc[DPL];
-#pragma unroll
-  for (int k = 0; k < DPL; k++) acc[k] = 0.f;
-
-  for (int t0 = start + wv * TILE; t0 < stop; t0 += NWV * TILE) {
-    const int nt = min(TILE, stop - t0);
-    const int tr = t0 + min(lane, nt - 1);  // lanes past nt re-read a valid row, masked below
-    float dot = 0.f;
-#pragma unroll
-    for (int c = 0; c < VPR; c++) {
-      const uint4 kr = *reinterpret_cast<const uint4*>(kbase + size_t(tr) * tok_stride + c * 8);
-      *reinterpret_cast<uint4*>(vw + lane * VROW + c * 16) =
-          *reinterpret_cast<const uint4*>(vbase + size_t(tr) * tok_stride + c * 8);
-      float kf[8], qf[8];
-      unpack8(kr, kf);
-      unpack8(qv[c], qf);
-#pragma unroll
-      for (int j = 0; j < 8; j++) dot += qf[j] * kf[j];
-    }
-    // V rows staged by this wave are read back by other lanes of the same wave.
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const float s = lane < nt ? dot * scale : -INFINITY;
-    const float mnew = fmaxf(m, wave_max(s));
-    const float p = lane < nt ? __expf(s - mnew) : 0.f;
-    const float corr = __expf(m - mnew);
-    l = l * corr + wave_sum(p);
-    m = mnew;
-#pragma unroll
-    for (int k = 0; k < DPL; k++) acc[k] *= corr;
-    for (int t = 0; t < nt; t++) {
-      const float pt = __shfl(p, t, kWave);
-      const uint16_t* vrow = reinterpret_cast<const uint16_t*>(vw + t * VROW);
-#pragma unroll
-      for (int k = 0; k < DPL; k++) acc[k] += pt * bf2f(vrow[lane + k * kWave]);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-  }
-
-  // Merge the waves through LDS (the V tiles are dead now); wave 0 finishes.
   __syncthreads();
-  float* mlw = reinterpret_cast<float*>(&vs[0][0]);  // [NWV][2]
-  float* accw = mlw + NWV * 2;                      // [NWV][D]
-  if (lane == 0) {
-    mlw[wv * 2] = m;
-    mlw[wv * 2 + 1] = l;
-  }
-#pragma unroll
-  for (int k = 0; k < DPL; k++) accw[wv * D + lane + k * kWave] = acc[k];
-  __syncthreads();
-  if (wv == 0) {
-    float M = -INFINITY;
-#pragma unroll
-    for (int w = 0; w < NWV; w++) M = fmaxf(M, mlw[w * 2]);
-    float L = 0.f, o[DPL];
-#pragma unroll
-    for (int k = 0; k < DPL; k++) o[k] = 0.f;
-#pragma unroll
-    for (int w = 0; w < NWV; w++) {
-      const float mw = mlw[w * 2];
-      const float e = mw == -INFINITY ? 0.f : __expf(mw - M);  // waves without tokens contribute nothing
-      L += mlw[w * 2 + 1] * e;
-#pragma unroll
-      for (int k = 0; k < DPL; k++) o[k] += accw[w * D + lane + k * kWave] * e;
-    }
-    if (used == 1) {
-      const float inv = 1.f / L;
-#pragma unroll
-      for (int k = 0; k < DPL; k++) out[hb * D + lane + k * kWave] = uint16_t(f2bf_bits(o[k] * inv));
-    } else {
-      float* po = part_o + (hb * nsplit + split) * D;
-#pragma unroll
-      for (int k = 0; k < DPL; k++) st_wt(po + lane + k * kWave, o[k]);
-      if (lane == 0) {
-        st_wt(part_ml + (hb * nsplit + split) * 2 + 0, M);
-        st_wt(part_ml + (hb * nsplit + split) * 2 + 1, L);
-      }
-      drain_stores();
-      unsigned ticket = 0;
-      if (lane == 0) ticket = arrive(&counters[hb]);
-      ticket = __shfl(ticket, 0, kWave);
-      if (ticket == unsigned(used - 1)) {
-        merge_splits<D>(hb, used, nsplit, part_o, part_ml, out, lane);
-        if (lane == 0) st_wt(&counters[hb], 0u);
-      }
-    }
-  }
-  (void)s_ticket;
+  if (threadIdx.x == 0) st_wt(&counters[blockIdx.y], 0u);
 }
 
 // ------------------------------------------------------------ host side
@@ -568,7 +556,8 @@ struct LlamaDims {
   float eps, theta;
 };
 
-constexpr int kChunk = 64;
+constexpr int kChunk = 64;     // workspace granularity of attention partials
+constexpr int kAttnTok = 128;  // tokens per attention workgroup (2 tiles, one load pass)
 constexpr int kTnResid = 1, kTnStore = 1;
 
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -710,24 +699,18 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
     a.H = d.H; a.Hkv = d.Hkv; a.D = d.D; a.Smax = d.max_seq; a.log2_theta = log2_theta;
     if ((e = launch_gemm<EPI_ROPE, 1>(a, qkv_n / 16, s)) != hipSuccess) return int(e);
 
-    // attention: one workgroup per (row, query head) for up to split_tok tokens
+    // attention: split-K over kAttnTok-token pieces, one workgroup per (row, KV head, piece)
     {
-      const int ngrp = B * d.Hkv;
-      if (d.D == 64) {
-        constexpr int NWV = 16;
-        const int split_tok = NWV * 64 * 2;
-        dim3 grid((max_len + split_tok - 1) / split_tok, ngrp * (d.H / d.Hkv));
-        hipLaunchKernelGGL((k_attn<64, NWV>), grid, dim3(NWV * 64), 0, s, W.q, kc, vc, pos, slots, d.max_batch,
-                           W.part_o, W.part_ml, W.counters, W.attn, d.H, d.Hkv, d.max_seq, split_tok, nsplit_ws,
-                           1.f / sqrtf(64.f), ngrp);
-      } else {
-        constexpr int NWV = 8;
-        const int split_tok = NWV * 64 * 2;
-        dim3 grid((max_len + split_tok - 1) / split_tok, ngrp * (d.H / d.Hkv));
-        hipLaunchKernelGGL((k_attn<128, NWV>), grid, dim3(NWV * 64), 0, s, W.q, kc, vc, pos, slots, d.max_batch,
-                           W.part_o, W.part_ml, W.counters, W.attn, d.H, d.Hkv, d.max_seq, split_tok, nsplit_ws,
-                           1.f / sqrtf(128.f), ngrp);
-      }
+      const int nsplit = (max_len + kAttnTok - 1) / kAttnTok;
+      dim3 grid(nsplit, B * d.Hkv);
+      dim3 blk(64 * (d.H / d.Hkv));
+      const float scale = 1.f / sqrtf(float(d.D));
+      if (d.D == 64)
+        hipLaunchKernelGGL((k_attn<64, kAttnTok / 64>), grid, blk, 0, s, W.q, kc, vc, pos, slots, d.max_batch,
+                           W.part_o, W.part_ml, W.counters, W.attn, d.H, d.Hkv, d.max_seq, kAttnTok, nsplit_ws, scale);
+      else
+        hipLaunchKernelGGL((k_attn<128, kAttnTok / 64>), grid, blk, 0, s, W.q, kc, vc, pos, slots, d.max_batch,
+                           W.part_o, W.part_ml, W.counters, W.attn, d.H, d.Hkv, d.max_seq, kAttnTok, nsplit_ws, scale);
       if ((e = hipGetLastError()) != hipSuccess) return int(e);
     }
 
