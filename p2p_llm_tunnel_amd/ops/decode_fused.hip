@@ -402,6 +402,7 @@ __global__ __launch_bounds__(512) void k_attn(const uint16_t* __restrict__ q, co
   __shared__ __attribute__((aligned(16))) uint8_t ks[TPB * TILE * ROWB];
   __shared__ __attribute__((aligned(16))) uint8_t vs[TPB * TILE * ROWB];
   __shared__ unsigned s_ticket;
+  __shared__ __attribute__((aligned(16))) float ps[8][TILE];  // softmax weights, one row per wave
 
   const int split = blockIdx.x;
   const int b = blockIdx.y / Hkv, kvh = blockIdx.y % Hkv;
@@ -481,13 +482,28 @@ __global__ __launch_bounds__(512) void k_attn(const uint16_t* __restrict__ q, co
     m = mnew;
 #pragma unroll
     for (int k = 0; k < DPL; k++) acc[k] *= corr;
-    // P.V: lane = head dim; p_t broadcast across the wave.
-    for (int t = 0; t < nt; t++) {
-      const float pt = __shfl(p, t, kWave);
-      const uint16_t* vrow = reinterpret_cast<const uint16_t*>(vs + (t0 + t) * ROWB);
+    // P.V: lane = head dim. p goes through this wave's LDS row and is read back
+    // as broadcast float4s; the loop always covers the full tile (p = 0 and V
+    // rows zero-filled past the end) so it unrolls into independent LDS reads
+    // instead of a serial shuffle-per-token chain.
+    ps[g][lane] = p;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 2
+    for (int t = 0; t < TILE; t += 8) {
+      const float4 pa = *reinterpret_cast<const float4*>(&ps[g][t]);
+      const float4 pb = *reinterpret_cast<const float4*>(&ps[g][t + 4]);
+      const float pt[8] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
 #pragma unroll
-      for (int k = 0; k < DPL; k++) acc[k] += pt * bf2f(vrow[lane + k * kWave]);
+      for (int j = 0; j < 8; j++) {
+        const uint16_t* vrow = reinterpret_cast<const uint16_t*>(vs + (t0 + t + j) * ROWB);
+#pragma unroll
+        for (int k = 0; k < DPL; k++) acc[k] += pt[j] * bf2f(vrow[lane + k * kWave]);
+      }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
   }
   const size_t hb = size_t(b) * H + kvh * G + g;
   if (used == 1) {  // single split: finish directly

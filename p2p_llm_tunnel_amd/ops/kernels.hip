@@ -140,6 +140,7 @@ __global__ __launch_bounds__(512) void k_decode_attn(const uint16_t* __restrict_
   constexpr int DPL = D / kWave;    // head dims per lane in the P·V phase
   __shared__ __attribute__((aligned(16))) uint8_t ks[TILE * ROWB];
   __shared__ __attribute__((aligned(16))) uint8_t vs[TILE * ROWB];
+  __shared__ __attribute__((aligned(16))) float ps[8][TILE];  // softmax weights, one row per wave
 
   const int split = blockIdx.x;
   const int b = blockIdx.y / Hkv, kvh = blockIdx.y % Hkv;
@@ -207,12 +208,24 @@ __global__ __launch_bounds__(512) void k_decode_attn(const uint16_t* __restrict_
     m = mnew;
 #pragma unroll
     for (int k = 0; k < DPL; k++) acc[k] *= corr;
-    // P·V: lane = head dim; p_t broadcast across the wave.
-    for (int t = 0; t < nt; t++) {
-      const float pt = __shfl(p, t, kWave);
-      const uint16_t* vrow = reinterpret_cast<const uint16_t*>(vs + t * ROWB);
+    // P·V: lane = head dim. p goes through this wave's LDS row and is read back
+    // as broadcast float4s over the full (zero-filled) tile, so the loop unrolls
+    // into independent LDS reads instead of a shuffle-per-token chain.
+    ps[g][lane] = p;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 2
+    for (int t = 0; t < TILE; t += 8) {
+      const float4 pa = *reinterpret_cast<const float4*>(&ps[g][t]);
+      const float4 pb = *reinterpret_cast<const float4*>(&ps[g][t + 4]);
+      const float pt[8] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
 #pragma unroll
-      for (int k = 0; k < DPL; k++) acc[k] += pt * bf2f(vrow[lane + k * kWave]);
+      for (int j = 0; j < 8; j++) {
+        const uint16_t* vrow = reinterpret_cast<const uint16_t*>(vs + (t + j) * ROWB);
+#pragma unroll
+        for (int k = 0; k < DPL; k++) acc[k] += pt[j] * bf2f(vrow[lane + k * kWave]);
+      }
     }
     __syncthreads();
   }
