@@ -156,6 +156,9 @@ def _prompt_ids(body: dict) -> list[int]:
 def make_handler(engine: Engine, model_name: str):
     class H(http.server.BaseHTTPRequestHandler):
         protocol_version = "HTTP/1.1"
+        # Tokens leave as small chunked writes every decode step; with Nagle on,
+        # each would wait for the peer's (delayed) ACK of the previous one.
+        disable_nagle_algorithm = True
 
         def log_message(self, *a):
             pass
