@@ -263,6 +263,7 @@ def make_handler(engine: Engine, model_name: str):
 class _Server(socketserver.ThreadingMixIn, http.server.HTTPServer):
     daemon_threads = True
     allow_reuse_address = True
+    request_queue_size = 1024  # the default backlog of 5 drops SYNs of a connection burst (1 s retry)
 
 
 def start_server(host="127.0.0.1", port=0, device="cuda:0", config="tiny", max_batch=8, model_name=None):
