@@ -282,9 +282,14 @@ void ServeSession::start_request(uint32_t sid, Pending p) {
     s->sched_->send(proto::make_res_headers(rh));
     trace::event("serve", sid, "res_headers");
   };
-  cb.on_data = [w, sid](const uint8_t* d, size_t n) {
+  auto first = std::make_shared<bool>(true);
+  cb.on_data = [w, sid, first](const uint8_t* d, size_t n) {
     auto s = w.lock();
     if (!s || s->stopped_) return;
+    if (*first) {
+      *first = false;
+      trace::event("serve", sid, "first_body");
+    }
     Bytes chunk = Bytes::copy(d, n);  // the one user-space copy on this side
     for (size_t off = 0; off < n; off += proto::kMaxBodyChunk)
       s->sched_->send(proto::make_body(proto::MsgType::ResBody, sid, chunk.slice(off, proto::kMaxBodyChunk)));

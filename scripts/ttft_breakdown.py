@@ -1,0 +1,86 @@
+"""Where the tunnel's added time-to-first-token goes, hop by hop.
+
+    python scripts/ttft_breakdown.py [--requests 40] [--transport webrtc|tcp]
+
+Runs the native mock behind a tunnel with TUNNEL_TRACE (serve + proxy) and
+MOCK_TRACE on, sends sequential streamed requests with the native load
+generator, joins the per-stream events (all processes stamp CLOCK_MONOTONIC
+µs on one host) and prints the median and p90 of each hop:
+
+  proxy accept -> proxy req_end           proxy parses the request, queues the frames
+  proxy req_end -> serve req_headers      the request crosses the tunnel
+  serve req_headers -> req_end            serve receives the rest of the request
+  serve req_end -> upstream_sent          serve picks an upstream socket and writes
+  upstream_sent -> mock_req               upstream wakes up and parses
+  mock_req -> serve first_body            first event back at serve
+  serve first_body -> proxy first_body    response crosses the tunnel
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import subprocess
+import sys
+import tempfile
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from p2p_llm_tunnel_amd import binary  # noqa: E402
+from p2p_llm_tunnel_amd.utils.build import ensure_native  # noqa: E402
+from p2p_llm_tunnel_amd.utils.procs import Tunnel, free_port, spawn  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--requests", type=int, default=40)
+    ap.add_argument("--transport", default="webrtc")
+    ap.add_argument("--streams", type=int, default=1)
+    a = ap.parse_args()
+    ensure_native()
+    trace = tempfile.mktemp(suffix=".jsonl", prefix="p2pt-trace-")
+    port = free_port()
+    mock = spawn("mock", [binary("tunnel-mock"), "--port", str(port), "--interval-ms", "20"], env={"MOCK_TRACE": "1"})
+    mock.wait_for("Mock LLM server running", 10)
+    try:
+        with Tunnel(f"http://127.0.0.1:{port}", transport=a.transport, env={"TUNNEL_TRACE": trace}) as t:
+            subprocess.run([binary("tunnel-loadgen"), "--target", f"127.0.0.1:{t.proxy_port}", "--streams",
+                            str(a.streams), "--steps", str(a.requests // a.streams), "--warmup", "1"],
+                           check=True, capture_output=True)
+        ev = {}
+        with open(trace) as f:
+            for line in f:
+                e = json.loads(line)
+                ev.setdefault(e["sid"], {})[(e["role"], e["ev"])] = e["t_us"]
+        mock_t = sorted(int(l.split()[1]) for l in mock.lines if l.startswith("mock_req "))
+    finally:
+        mock.stop()
+        if os.path.exists(trace):
+            os.unlink(trace)
+    hops = [("proxy", "accept", "proxy", "req_end"), ("proxy", "req_end", "serve", "req_headers"),
+            ("serve", "req_headers", "serve", "req_end"), ("serve", "req_end", "serve", "upstream_sent"),
+            ("serve", "upstream_sent", "mock", "req"), ("mock", "req", "serve", "first_body"),
+            ("serve", "first_body", "proxy", "first_body")]
+    rows = {f"{a_}.{b_} -> {c_}.{d_}": [] for a_, b_, c_, d_ in hops}
+    for sid, e in sorted(ev.items()):
+        if ("serve", "upstream_sent") not in e or ("proxy", "first_body") not in e:
+            continue
+        up = e[("serve", "upstream_sent")]
+        m = next((x for x in mock_t if x >= up), None)  # the mock request that followed this send
+        if m is None:
+            continue
+        e[("mock", "req")] = m
+        for a_, b_, c_, d_ in hops:
+            if (a_, b_) in e and (c_, d_) in e:
+                rows[f"{a_}.{b_} -> {c_}.{d_}"].append(e[(c_, d_)] - e[(a_, b_)])
+    out = {}
+    for k, v in rows.items():
+        if v:
+            v.sort()
+            out[k] = {"n": len(v), "p50_us": statistics.median(v), "p90_us": v[int(0.9 * (len(v) - 1))]}
+    print(json.dumps({"transport": a.transport, "streams": a.streams, "hops": out}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
