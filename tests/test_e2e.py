@@ -79,6 +79,49 @@ def test_sse_token_by_token(tunnel):
     assert all(0.05 < g < 0.2 for g in gaps), gaps
 
 
+def _ndjson_stream(port, t0=None):
+    c = http.client.HTTPConnection("127.0.0.1", port, timeout=10)
+    t0 = time.perf_counter()
+    c.request("POST", "/api/generate", body=json.dumps({"model": "test-model", "prompt": "hi"}),
+              headers={"content-type": "application/json"})
+    r = c.getresponse()
+    lines = []
+    while True:
+        line = r.readline()
+        if not line:
+            break
+        lines.append((time.perf_counter() - t0, json.loads(line)))
+    c.close()
+    return r, lines
+
+
+def test_ollama_generate_ndjson_stream(tunnel):
+    # BASELINE config #2's upstream shape: Ollama /api/generate streams NDJSON.
+    r, lines = _ndjson_stream(tunnel.proxy_port)
+    assert r.status == 200 and r.getheader("content-type") == "application/x-ndjson"
+    assert "".join(o["response"] for _, o in lines) == "Hello from the tunnel!"
+    assert lines[-1][1]["done"] is True and not any(o["done"] for _, o in lines[:-1])
+    assert lines[0][0] < 0.09  # first token forwarded as produced
+    st, _, body = get(tunnel.url + "/api/tags")
+    assert st == 200 and b"test-model" in body
+
+
+def test_native_mock_ollama_through_tunnel(transport):
+    from p2p_llm_tunnel_amd import binary
+    from p2p_llm_tunnel_amd.utils.procs import spawn
+    port = free_port()
+    mock = spawn("mock", [binary("tunnel-mock"), "--port", str(port)])
+    try:
+        mock.wait_for("Mock LLM server running", 10)
+        with Tunnel(f"http://127.0.0.1:{port}", transport=transport) as t:
+            r, lines = _ndjson_stream(t.proxy_port)
+            assert r.status == 200 and r.getheader("content-type") == "application/x-ndjson"
+            assert "".join(o["response"] for _, o in lines) == "Hello from the tunnel!"
+            assert lines[-1][1]["done"] is True
+    finally:
+        mock.stop()
+
+
 def test_non_streaming_completion(tunnel):
     req = urllib.request.Request(tunnel.url + "/v1/chat/completions", data=b'{"stream": false}',
                                  headers={"content-type": "application/json"})
