@@ -2,7 +2,6 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-echo "== build"; timeout -k 10 300 python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { tail -30 gpurun_out/build.log; exit 1; }
 echo "== gpu tests"; timeout -k 10 900 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -15 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 echo "== decode variants"
 for args in "" "--unfused" "--eager" "--eager --unfused" "--batch 1" "--batch 1 --unfused" "--batch 16" "--config small --batch 8" "--config small --batch 8 --unfused"; do
