@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "core/log.h"
+#include "core/profiler.h"
 #include "tunnel/app.h"
 
 using namespace p2pt;
@@ -251,5 +252,6 @@ int main(int argc, char** argv) {
              cfg.listen.c_str());
   }
   if (cfg.rtc.turn.set()) LOG_INFO("tunnel", "TURN server configured: %s", cfg.rtc.turn.url.c_str());
+  profiler::start_from_env();
   return run_app(cfg);
 }

@@ -28,6 +28,15 @@ class Bytes {
     return Bytes(std::make_shared<std::vector<uint8_t>>(std::move(v)));
   }
   static Bytes take(std::string&& s) { return copy(s.data(), s.size()); }
+  // View of memory kept alive by an arbitrary owner (e.g. a pooled receive
+  // buffer that received datagrams are decrypted in place into).
+  static Bytes adopt(std::shared_ptr<const void> owner, const uint8_t* p, size_t n) {
+    Bytes b;
+    b.owner_ = std::move(owner);
+    b.ptr_ = p;
+    b.len_ = n;
+    return b;
+  }
 
   const uint8_t* data() const { return ptr_; }
   size_t size() const { return len_; }
@@ -53,12 +62,21 @@ class Bytes {
   }
 
  private:
-  explicit Bytes(std::shared_ptr<std::vector<uint8_t>> v)
-      : owner_(std::move(v)), ptr_(owner_->data()), len_(owner_->size()) {}
-  std::shared_ptr<const std::vector<uint8_t>> owner_;
+  explicit Bytes(std::shared_ptr<std::vector<uint8_t>> v) : ptr_(v->data()), len_(v->size()) { owner_ = std::move(v); }
+  std::shared_ptr<const void> owner_;
   const uint8_t* ptr_ = nullptr;
   size_t len_ = 0;
 };
+
+// Fixed-size, uninitialised, refcounted buffer (datagram receive/send pools).
+// A pool hands one out again once use_count() drops back to 1, i.e. once no
+// Bytes view into it is alive.
+struct RawBuf {
+  explicit RawBuf(size_t n) : data(new uint8_t[n]), cap(n) {}
+  std::unique_ptr<uint8_t[]> data;
+  size_t cap;
+};
+using RawBufPtr = std::shared_ptr<RawBuf>;
 
 // Append-only big-endian writer over a std::vector.
 class ByteWriter {

@@ -150,14 +150,71 @@ uint32_t crc32_ieee(const void* data, size_t n, uint32_t crc) {
   return ~crc;
 }
 
-// CRC-32c (Castagnoli) via the SSE4.2 crc32 instruction: 8 bytes/cycle-ish,
-// which keeps the SCTP checksum far below the AES-GCM cost per packet.
+// CRC-32c (Castagnoli) via the SSE4.2 crc32 instruction. One crc32q has a
+// 3-cycle latency but issues every cycle, so buffers of >= 3 lanes are
+// checksummed as three independent chains over adjacent blocks that are then
+// merged with a GF(2) multiply by x^(8*len) mod P (the zlib crc32_combine
+// identity on raw registers). That is ~3x the single-chain rate and keeps the
+// SCTP checksum of 16 KB packets well below the AES-GCM cost.
+namespace {
+constexpr uint32_t kCrc32cPoly = 0x82F63B78u;  // reflected
+
+uint32_t gf2_multmodp(uint32_t a, uint32_t b) {
+  uint32_t m = 1u << 31, p = 0;
+  for (;;) {
+    if (a & m) {
+      p ^= b;
+      if ((a & (m - 1)) == 0) break;
+    }
+    m >>= 1;
+    b = b & 1 ? (b >> 1) ^ kCrc32cPoly : b >> 1;
+  }
+  return p;
+}
+
+// x^(8*n) mod P.
+uint32_t gf2_x8n(size_t n) {
+  uint32_t x2n[32];
+  uint32_t p = 1u << 30;  // x^1
+  x2n[0] = p;
+  for (int k = 1; k < 32; k++) x2n[k] = p = gf2_multmodp(p, p);
+  p = 1u << 31;  // x^0
+  unsigned k = 3;
+  while (n) {
+    if (n & 1) p = gf2_multmodp(x2n[k & 31], p);
+    n >>= 1;
+    k++;
+  }
+  return p;
+}
+
+constexpr size_t kLane = 1024;  // bytes per chain per round
+const uint32_t kShift1 = gf2_x8n(kLane);
+const uint32_t kShift2 = gf2_x8n(2 * kLane);
+}  // namespace
+
 uint32_t crc32c(const void* data, size_t n, uint32_t crc) {
   const uint8_t* p = static_cast<const uint8_t*>(data);
   uint64_t c = ~crc;
   while (n && (reinterpret_cast<uintptr_t>(p) & 7)) {
     c = _mm_crc32_u8(uint32_t(c), *p++);
     n--;
+  }
+  while (n >= 3 * kLane) {
+    uint64_t c1 = 0, c2 = 0;
+    const uint8_t* q = p;
+    for (size_t i = 0; i < kLane; i += 8) {
+      uint64_t v0, v1, v2;
+      memcpy(&v0, q + i, 8);
+      memcpy(&v1, q + kLane + i, 8);
+      memcpy(&v2, q + 2 * kLane + i, 8);
+      c = _mm_crc32_u64(c, v0);
+      c1 = _mm_crc32_u64(c1, v1);
+      c2 = _mm_crc32_u64(c2, v2);
+    }
+    c = gf2_multmodp(kShift2, uint32_t(c)) ^ gf2_multmodp(kShift1, uint32_t(c1)) ^ uint32_t(c2);
+    p += 3 * kLane;
+    n -= 3 * kLane;
   }
   while (n >= 8) {
     uint64_t v;

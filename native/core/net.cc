@@ -268,14 +268,23 @@ void TcpConn::on_events(uint32_t ev) {
   }
 }
 
+Bytes TcpConn::rx_view(const uint8_t* p, size_t n) const {
+  constexpr size_t kMinView = 2048;  // smaller pieces are copied: never pin 64 KiB for a token
+  if (rx_ && n >= kMinView && p >= rx_->data.get() && p + n <= rx_->data.get() + rx_->cap)
+    return Bytes::adopt(rx_, p, n);
+  return Bytes::copy(p, n);
+}
+
 void TcpConn::do_read() {
-  uint8_t buf[65536];
+  constexpr size_t kRx = 65536;
   // Bounded number of reads per wakeup keeps the loop fair across sockets.
   for (int iter = 0; iter < 16 && fd_ >= 0 && !paused_; iter++) {
+    if (!rx_ || rx_.use_count() > 1) rx_ = std::make_shared<RawBuf>(kRx);
+    uint8_t* buf = rx_->data.get();
     ssize_t n;
     if (ssl_) {
       ERR_clear_error();
-      n = SSL_read(ssl_, buf, sizeof buf);
+      n = SSL_read(ssl_, buf, int(kRx));
       if (n <= 0) {
         int e = SSL_get_error(ssl_, int(n));
         if (e == SSL_ERROR_WANT_READ) return;
@@ -296,7 +305,7 @@ void TcpConn::do_read() {
         return;
       }
     } else {
-      n = ::read(fd_, buf, sizeof buf);
+      n = ::read(fd_, buf, kRx);
       if (n < 0) {
         if (errno == EAGAIN || errno == EINTR) return;
         fail(errno_str(errno));
@@ -308,7 +317,7 @@ void TcpConn::do_read() {
       }
     }
     if (auto cb = on_data_) (*cb)(buf, size_t(n));
-    if (size_t(n) < sizeof buf && !ssl_) return;
+    if (size_t(n) < kRx && !ssl_) return;
   }
 }
 

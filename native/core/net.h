@@ -101,6 +101,10 @@ class TcpConn : public std::enable_shared_from_this<TcpConn> {
   int fd() const { return fd_; }
   SockAddr peer() const { return peer_; }
   void set_nodelay(bool on);
+  // Inside an on_data callback: a Bytes for [p, p+n). Large ranges of the
+  // receive buffer become zero-copy views (the next read then uses a fresh
+  // buffer); small ones, and bytes from anywhere else, are copied.
+  Bytes rx_view(const uint8_t* p, size_t n) const;
 
  private:
   TcpConn(Reactor& r, int fd);
@@ -128,6 +132,7 @@ class TcpConn : public std::enable_shared_from_this<TcpConn> {
   bool above_low_ = false;
   size_t low_water_ = 0;
   std::shared_ptr<DataFn> on_data_;
+  RawBufPtr rx_;  // receive buffer; replaced when views into it are alive
   CloseFn on_close_;
   Fn on_drain_;
   uint32_t interest_ = 0;

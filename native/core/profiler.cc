@@ -1,0 +1,145 @@
+#include "core/profiler.h"
+
+#include <dlfcn.h>
+#include <pthread.h>
+#include <signal.h>
+#include <sys/time.h>
+#include <ucontext.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+namespace p2pt::profiler {
+namespace {
+
+constexpr int kDepth = 10;          // frames per sample: pc, [rsp], fp chain
+constexpr size_t kSlots = 1 << 15;  // distinct stacks kept
+
+struct Slot {
+  std::atomic<uint64_t> hash{0};
+  uint64_t pcs[kDepth];
+  std::atomic<uint64_t> count{0};
+};
+
+Slot* g_slots = nullptr;
+std::atomic<uint64_t> g_samples{0}, g_dropped{0};
+std::string g_path;
+uintptr_t g_stack_lo = 0, g_stack_hi = 0;
+std::atomic<bool> g_dumped{false};
+
+inline bool on_stack(uintptr_t p) { return p >= g_stack_lo && p + 16 <= g_stack_hi && (p & 7) == 0; }
+
+void on_sigprof(int, siginfo_t*, void* uc_) {
+  auto* uc = static_cast<ucontext_t*>(uc_);
+  uint64_t pcs[kDepth] = {};
+  int n = 0;
+#if defined(__x86_64__)
+  uintptr_t pc = uc->uc_mcontext.gregs[REG_RIP];
+  uintptr_t sp = uc->uc_mcontext.gregs[REG_RSP];
+  uintptr_t fp = uc->uc_mcontext.gregs[REG_RBP];
+  pcs[n++] = pc;
+  // Heuristic caller of a frameless leaf: the word at the stack pointer.
+  pcs[n++] = on_stack(sp) ? *reinterpret_cast<uint64_t*>(sp) : 0;
+  while (n < kDepth && on_stack(fp)) {
+    uintptr_t ret = reinterpret_cast<uint64_t*>(fp)[1];
+    uintptr_t next = reinterpret_cast<uint64_t*>(fp)[0];
+    if (!ret) break;
+    pcs[n++] = ret;
+    if (next <= fp) break;
+    fp = next;
+  }
+#else
+  (void)uc;
+#endif
+  uint64_t h = 1469598103934665603ull;
+  for (int i = 0; i < kDepth; i++) h = (h ^ pcs[i]) * 1099511628211ull;
+  if (h == 0) h = 1;
+  g_samples.fetch_add(1, std::memory_order_relaxed);
+  for (size_t probe = 0; probe < 64; probe++) {
+    Slot& s = g_slots[(h + probe) & (kSlots - 1)];
+    uint64_t cur = s.hash.load(std::memory_order_acquire);
+    if (cur == h) {
+      s.count.fetch_add(1, std::memory_order_relaxed);
+      return;
+    }
+    if (cur == 0) {
+      memcpy(s.pcs, pcs, sizeof pcs);
+      s.hash.store(h, std::memory_order_release);  // single sampled thread: no CAS race
+      s.count.fetch_add(1, std::memory_order_relaxed);
+      return;
+    }
+  }
+  g_dropped.fetch_add(1, std::memory_order_relaxed);
+}
+
+void resolve(FILE* f, uint64_t a) {
+  Dl_info di;
+  // Raw addresses; scripts/profile_report.py backs return addresses up by one
+  // byte so the symboliser attributes the call site.
+  if (a && dladdr(reinterpret_cast<void*>(a), &di) && di.dli_fname) {
+    fprintf(f, " %s+0x%lx", di.dli_fname, static_cast<unsigned long>(a - reinterpret_cast<uintptr_t>(di.dli_fbase)));
+  } else {
+    fprintf(f, " ?+0x%lx", static_cast<unsigned long>(a));
+  }
+}
+
+}  // namespace
+
+bool start_from_env() {
+  const char* p = getenv("TUNNEL_PROFILE");
+  if (!p || !*p) return false;
+  g_path = p;
+  if (size_t at = g_path.find("%p"); at != std::string::npos) g_path.replace(at, 2, std::to_string(getpid()));
+  int hz = 2000;
+  if (const char* h = getenv("TUNNEL_PROFILE_HZ")) hz = std::max(10, atoi(h));
+  g_slots = new Slot[kSlots];
+  pthread_attr_t attr;
+  if (pthread_getattr_np(pthread_self(), &attr) == 0) {
+    void* lo = nullptr;
+    size_t sz = 0;
+    pthread_attr_getstack(&attr, &lo, &sz);
+    g_stack_lo = reinterpret_cast<uintptr_t>(lo);
+    g_stack_hi = g_stack_lo + sz;
+    pthread_attr_destroy(&attr);
+  }
+  // Resolve dladdr's lazy state before the first signal.
+  Dl_info di;
+  dladdr(reinterpret_cast<void*>(&start_from_env), &di);
+  struct sigaction sa = {};
+  sa.sa_sigaction = on_sigprof;
+  sa.sa_flags = SA_SIGINFO | SA_RESTART;
+  sigemptyset(&sa.sa_mask);
+  sigaction(SIGPROF, &sa, nullptr);
+  struct itimerval it = {};
+  it.it_interval.tv_usec = 1000000 / hz;
+  it.it_value = it.it_interval;
+  setitimer(ITIMER_PROF, &it, nullptr);
+  atexit(dump);
+  return true;
+}
+
+void dump() {
+  if (!g_slots || g_dumped.exchange(true)) return;
+  struct itimerval off = {};
+  setitimer(ITIMER_PROF, &off, nullptr);
+  FILE* f = fopen(g_path.c_str(), "w");
+  if (!f) return;
+  fprintf(f, "# samples %llu dropped %llu\n", static_cast<unsigned long long>(g_samples.load()),
+          static_cast<unsigned long long>(g_dropped.load()));
+  for (size_t i = 0; i < kSlots; i++) {
+    Slot& s = g_slots[i];
+    if (!s.hash.load()) continue;
+    fprintf(f, "%llu", static_cast<unsigned long long>(s.count.load()));
+    for (int k = 0; k < kDepth && (k < 2 || s.pcs[k]); k++) resolve(f, s.pcs[k]);
+    fputc('\n', f);
+  }
+  fclose(f);
+}
+
+}  // namespace p2pt::profiler

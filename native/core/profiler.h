@@ -1,0 +1,22 @@
+// In-process sampling CPU profiler for the tunnel binaries (the
+// reference has no profiler hooks at all; this container has no `perf`).
+//
+// TUNNEL_PROFILE=<path> ("%p" = pid) arms ITIMER_PROF at TUNNEL_PROFILE_HZ (default 2000)
+// on the reactor thread. The SIGPROF handler records the interrupted PC, the
+// word at the stack pointer (the return address when a frameless leaf such as
+// memcpy or an AES routine was interrupted) and up to kDepth frame-pointer
+// links (our code is built with -fno-omit-frame-pointer), into a fixed,
+// lock-free table — no allocation in the handler. At exit the table is written
+// as text: one line per distinct stack, addresses resolved to
+// "module+0xoffset" with dladdr. scripts/profile_report.py symbolises it with
+// llvm-symbolizer and prints self/inclusive tables.
+#pragma once
+
+namespace p2pt::profiler {
+
+// Starts sampling when TUNNEL_PROFILE is set; returns whether it did.
+bool start_from_env();
+// Writes the report now (also registered with atexit).
+void dump();
+
+}  // namespace p2pt::profiler

@@ -416,6 +416,25 @@ void ClientCall::attach(std::shared_ptr<TcpConn> c, bool reused) {
 
 void ClientCall::on_data(const uint8_t* p, size_t n) {
   got_any_ = true;
+  if (head_done_ && buf_.empty() && !finished_ && !paused_ && !body_.done()) {
+    // Body bytes straight from the socket buffer (no staging copy).
+    auto self = shared_from_this();
+    size_t used = body_.feed(p, n, [this](const uint8_t* d, size_t k) {
+      if (cb_.on_data && !finished_) cb_.on_data(conn_ ? conn_->rx_view(d, k) : Bytes::copy(d, k));
+    });
+    if (used == SIZE_MAX) {
+      finish("error decoding response body: " + body_.error());
+      return;
+    }
+    if (finished_) return;
+    if (used < n) buf_.append(reinterpret_cast<const char*>(p + used), n - used);
+    if (body_.done() && buf_.empty()) {
+      finish("");
+      return;
+    }
+    process();
+    return;
+  }
   buf_.append(reinterpret_cast<const char*>(p), n);
   process();
 }
@@ -453,7 +472,7 @@ void ClientCall::process() {
     if (buf_.empty()) return;
     size_t used = body_.feed(reinterpret_cast<const uint8_t*>(buf_.data()), buf_.size(),
                              [this](const uint8_t* d, size_t k) {
-                               if (cb_.on_data && !finished_) cb_.on_data(d, k);
+                               if (cb_.on_data && !finished_) cb_.on_data(Bytes::copy(d, k));
                              });
     if (used == SIZE_MAX) {
       finish("error decoding response body: " + body_.error());

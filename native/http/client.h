@@ -33,7 +33,8 @@ struct ClientCallbacks {
   // Request bytes handed to the socket (connection established or reused).
   std::function<void(bool reused)> on_sent;
   std::function<void(const Head&)> on_head;
-  std::function<void(const uint8_t*, size_t)> on_data;
+  // Body bytes; large pieces are views of the socket's receive buffer.
+  std::function<void(Bytes)> on_data;
   // err empty => complete body received. `before_head` tells whether any
   // response head had been delivered (502 vs mid-stream ERROR semantics).
   std::function<void(const std::string& err, bool before_head)> on_done;

@@ -2,7 +2,9 @@
 
 #include <openssl/bio.h>
 #include <openssl/err.h>
+#include <openssl/core_names.h>
 #include <openssl/evp.h>
+#include <openssl/kdf.h>
 #include <openssl/ssl.h>
 #include <openssl/x509.h>
 
@@ -65,7 +67,7 @@ Identity& identity() {
     SSL_CTX_set1_groups_list(ctx, "X25519:P-256:P-384");
     SSL_CTX_set_verify(ctx, SSL_VERIFY_PEER | SSL_VERIFY_FAIL_IF_NO_PEER_CERT, verify_any);
     SSL_CTX_set_read_ahead(ctx, 1);
-    SSL_CTX_set_options(ctx, SSL_OP_NO_QUERY_MTU | SSL_OP_NO_TICKET);
+    SSL_CTX_set_options(ctx, SSL_OP_NO_QUERY_MTU | SSL_OP_NO_TICKET | SSL_OP_NO_RENEGOTIATION);
     id.ctx = ctx;
   });
   return id;
@@ -92,8 +94,7 @@ struct DtlsBio {
   }
   static int write(BIO* b, const char* data, int len) {
     auto* t = static_cast<DtlsTransport*>(BIO_get_data(b));
-    if (!t || t->closed_ || !t->write_) return len;
-    t->write_(reinterpret_cast<const uint8_t*>(data), size_t(len));
+    if (t) t->bio_wrote(reinterpret_cast<const uint8_t*>(data), size_t(len));
     return len;
   }
   static int read(BIO* b, char* out, int len) {
@@ -154,6 +155,8 @@ DtlsTransport::~DtlsTransport() {
     BIO_set_data(bio_, nullptr);
     SSL_free(ssl_);  // frees the BIO
   }
+  if (wctx_) EVP_CIPHER_CTX_free(wctx_);
+  if (rctx_) EVP_CIPHER_CTX_free(rctx_);
 }
 
 void DtlsTransport::start() {
@@ -194,8 +197,204 @@ bool DtlsTransport::verify_peer() {
   return true;
 }
 
+namespace {
+constexpr size_t kRecHdr = 13;     // type, version(2), epoch(2), seq(6), length(2)
+constexpr size_t kExplicit = 8;    // GCM explicit nonce
+constexpr size_t kTag = 16;
+constexpr uint8_t kAppData = 23, kAlert = 21;
+
+uint64_t rd48(const uint8_t* p) {
+  uint64_t v = 0;
+  for (int i = 0; i < 6; i++) v = v << 8 | p[i];
+  return v;
+}
+void wr48(uint8_t* p, uint64_t v) {
+  for (int i = 5; i >= 0; i--) {
+    p[i] = uint8_t(v);
+    v >>= 8;
+  }
+}
+}  // namespace
+
+// Every datagram OpenSSL emits passes here: remember the highest epoch-1
+// sequence number it used (our record layer continues after it), capture the
+// probe record, and mute OpenSSL once our layer owns the epoch.
+void DtlsTransport::bio_wrote(const uint8_t* p, size_t n) {
+  for (size_t off = 0; off + kRecHdr <= n;) {
+    size_t len = rd16(p + off + 11);
+    if (rd16(p + off + 3) == 1) ossl_max_wseq_ = std::max(ossl_max_wseq_, rd48(p + off + 5));
+    off += kRecHdr + len;
+  }
+  if (capture_) {
+    captured_.append(reinterpret_cast<const char*>(p), n);
+    return;
+  }
+  if (closed_ || fast_tx_ || !write_) return;
+  write_(p, n);
+}
+
+// TLS 1.2 key block for the AES-GCM suites (RFC 5246 §6.3, RFC 5288 §3):
+// client_write_key | server_write_key | client_write_IV[4] | server_write_IV[4].
+void DtlsTransport::setup_fast_path() {
+  if (getenv("TUNNEL_DTLS_OPENSSL_RECORDS")) return;  // diagnostics: keep OpenSSL's record layer
+  const SSL_CIPHER* c = SSL_get_current_cipher(ssl_);
+  if (!c) return;
+  uint16_t id = SSL_CIPHER_get_protocol_id(c);
+  const EVP_CIPHER* ciph;
+  const char* md;
+  size_t klen;
+  if (id == 0xC02B) {  // ECDHE-ECDSA-AES128-GCM-SHA256
+    ciph = EVP_aes_128_gcm();
+    md = "SHA256";
+    klen = 16;
+  } else if (id == 0xC02C) {  // ECDHE-ECDSA-AES256-GCM-SHA384
+    ciph = EVP_aes_256_gcm();
+    md = "SHA384";
+    klen = 32;
+  } else {
+    LOG_DEBUG(kT, "DTLS suite %s: OpenSSL record layer", cipher().c_str());
+    return;
+  }
+  uint8_t master[48], cr[32], sr[32];
+  size_t mlen = SSL_SESSION_get_master_key(SSL_get_session(ssl_), master, sizeof master);
+  if (mlen != 48 || SSL_get_client_random(ssl_, cr, 32) != 32 || SSL_get_server_random(ssl_, sr, 32) != 32) return;
+  uint8_t seed[13 + 64];
+  memcpy(seed, "key expansion", 13);
+  memcpy(seed + 13, sr, 32);
+  memcpy(seed + 45, cr, 32);
+  uint8_t kb[2 * 32 + 2 * 4];
+  size_t kblen = 2 * klen + 8;
+  EVP_KDF* kdf = EVP_KDF_fetch(nullptr, "TLS1-PRF", nullptr);
+  EVP_KDF_CTX* kctx = kdf ? EVP_KDF_CTX_new(kdf) : nullptr;
+  OSSL_PARAM params[] = {
+      OSSL_PARAM_construct_utf8_string(OSSL_KDF_PARAM_DIGEST, const_cast<char*>(md), 0),
+      OSSL_PARAM_construct_octet_string(OSSL_KDF_PARAM_SECRET, master, mlen),
+      OSSL_PARAM_construct_octet_string(OSSL_KDF_PARAM_SEED, seed, sizeof seed),
+      OSSL_PARAM_construct_end()};
+  bool ok = kctx && EVP_KDF_derive(kctx, kb, kblen, params) == 1;
+  EVP_KDF_CTX_free(kctx);
+  EVP_KDF_free(kdf);
+  OPENSSL_cleanse(master, sizeof master);
+  if (!ok) return;
+  const uint8_t* ckey = kb;
+  const uint8_t* skey = kb + klen;
+  const uint8_t* civ = kb + 2 * klen;
+  const uint8_t* siv = civ + 4;
+  const uint8_t* wkey = client_ ? ckey : skey;
+  const uint8_t* rkey = client_ ? skey : ckey;
+  memcpy(wiv_, client_ ? civ : siv, 4);
+  memcpy(riv_, client_ ? siv : civ, 4);
+  wctx_ = EVP_CIPHER_CTX_new();
+  rctx_ = EVP_CIPHER_CTX_new();
+  EVP_EncryptInit_ex(wctx_, ciph, nullptr, wkey, nullptr);
+  EVP_DecryptInit_ex(rctx_, ciph, nullptr, rkey, nullptr);
+  // Known-answer check of the derivation: OpenSSL encrypts a probe record
+  // (captured, never sent); our write key must open it.
+  static const char kProbe[] = "p2pt-record-probe";
+  capture_ = true;
+  captured_.clear();
+  ERR_clear_error();
+  int rc = SSL_write(ssl_, kProbe, int(sizeof kProbe - 1));
+  capture_ = false;
+  bool probe_ok = false;
+  if (rc > 0 && captured_.size() >= kRecHdr + kExplicit + kTag) {
+    auto* rec = reinterpret_cast<uint8_t*>(captured_.data());
+    size_t ctlen = captured_.size() - kRecHdr - kExplicit - kTag;
+    EVP_CIPHER_CTX* t = EVP_CIPHER_CTX_new();
+    uint8_t nonce[12], aad[13], out[64];
+    memcpy(nonce, wiv_, 4);
+    memcpy(nonce + 4, rec + kRecHdr, 8);
+    memcpy(aad, rec + 3, 8);
+    aad[8] = rec[0];
+    aad[9] = rec[1];
+    aad[10] = rec[2];
+    wr16(aad + 11, uint16_t(ctlen));
+    int l = 0, l2 = 0;
+    probe_ok = ctlen == sizeof kProbe - 1 && EVP_DecryptInit_ex(t, ciph, nullptr, wkey, nonce) == 1 &&
+               EVP_DecryptUpdate(t, nullptr, &l, aad, 13) == 1 &&
+               EVP_DecryptUpdate(t, out, &l, rec + kRecHdr + kExplicit, int(ctlen)) == 1 &&
+               EVP_CIPHER_CTX_ctrl(t, EVP_CTRL_GCM_SET_TAG, 16, rec + kRecHdr + kExplicit + ctlen) == 1 &&
+               EVP_DecryptFinal_ex(t, out + l, &l2) == 1 && memcmp(out, kProbe, ctlen) == 0;
+    EVP_CIPHER_CTX_free(t);
+  }
+  OPENSSL_cleanse(kb, sizeof kb);
+  if (!probe_ok) {
+    LOG_WARN(kT, "DTLS key derivation self-check failed; staying on OpenSSL's record layer");
+    return;
+  }
+  fast_rx_ = true;
+  LOG_DEBUG(kT, "DTLS own record layer armed (%s)", cipher().c_str());
+}
+
+bool DtlsTransport::fast_decrypt(uint8_t* rec, size_t len, uint8_t type, uint64_t seq, uint8_t** pt, size_t* pt_len) {
+  if (len < kRecHdr + kExplicit + kTag) return false;
+  if (rx_any_ && seq <= rx_max_) {
+    uint64_t d = rx_max_ - seq;
+    if (d >= 64 || (rx_bitmap_ >> d) & 1) return false;  // replayed or too old
+  }
+  size_t ctlen = len - kRecHdr - kExplicit - kTag;
+  uint8_t* ct = rec + kRecHdr + kExplicit;
+  uint8_t nonce[12], aad[13];
+  memcpy(nonce, riv_, 4);
+  memcpy(nonce + 4, rec + kRecHdr, 8);
+  memcpy(aad, rec + 3, 8);
+  aad[8] = type;
+  aad[9] = rec[1];
+  aad[10] = rec[2];
+  wr16(aad + 11, uint16_t(ctlen));
+  int l = 0, l2 = 0;
+  if (EVP_DecryptInit_ex(rctx_, nullptr, nullptr, nullptr, nonce) != 1 ||
+      EVP_DecryptUpdate(rctx_, nullptr, &l, aad, 13) != 1 || EVP_DecryptUpdate(rctx_, ct, &l, ct, int(ctlen)) != 1 ||
+      EVP_CIPHER_CTX_ctrl(rctx_, EVP_CTRL_GCM_SET_TAG, 16, ct + ctlen) != 1 ||
+      EVP_DecryptFinal_ex(rctx_, ct + l, &l2) != 1)
+    return false;
+  if (!rx_any_ || seq > rx_max_) {
+    uint64_t sh = rx_any_ ? seq - rx_max_ : 64;
+    rx_bitmap_ = sh >= 64 ? 1 : (rx_bitmap_ << sh) | 1;
+    rx_max_ = seq;
+    rx_any_ = true;
+  } else {
+    rx_bitmap_ |= uint64_t(1) << (rx_max_ - seq);
+  }
+  *pt = ct;
+  *pt_len = ctlen;
+  return true;
+}
+
+bool DtlsTransport::fast_encrypt_into(uint8_t* out, uint8_t type, const iovec* iov, int cnt, size_t total) {
+  out[0] = type;
+  out[1] = 0xFE;  // DTLS 1.2
+  out[2] = 0xFD;
+  wr16(out + 3, 1);  // epoch
+  wr48(out + 5, wseq_++);
+  wr16(out + 11, uint16_t(kExplicit + total + kTag));
+  memcpy(out + kRecHdr, out + 3, 8);  // explicit nonce = epoch || seq (as OpenSSL does)
+  uint8_t nonce[12], aad[13];
+  memcpy(nonce, wiv_, 4);
+  memcpy(nonce + 4, out + 3, 8);
+  memcpy(aad, out + 3, 8);
+  aad[8] = type;
+  aad[9] = 0xFE;
+  aad[10] = 0xFD;
+  wr16(aad + 11, uint16_t(total));
+  int l = 0;
+  if (EVP_EncryptInit_ex(wctx_, nullptr, nullptr, nullptr, nonce) != 1 ||
+      EVP_EncryptUpdate(wctx_, nullptr, &l, aad, 13) != 1)
+    return false;
+  uint8_t* o = out + kRecHdr + kExplicit;
+  for (int i = 0; i < cnt; i++) {
+    if (!iov[i].iov_len) continue;
+    if (EVP_EncryptUpdate(wctx_, o, &l, static_cast<const uint8_t*>(iov[i].iov_base), int(iov[i].iov_len)) != 1)
+      return false;
+    o += l;
+  }
+  if (EVP_EncryptFinal_ex(wctx_, o, &l) != 1) return false;
+  o += l;
+  return EVP_CIPHER_CTX_ctrl(wctx_, EVP_CTRL_GCM_GET_TAG, 16, o) == 1;
+}
+
 void DtlsTransport::drive() {
-  if (closed_) return;
+  if (closed_ || fast_tx_) return;
   auto self = shared_from_this();
   if (!connected_) {
     ERR_clear_error();
@@ -209,6 +408,7 @@ void DtlsTransport::drive() {
       if (timer_) r_.cancel(timer_);
       timer_ = 0;
       LOG_DEBUG(kT, "DTLS handshake complete (%s, %s)", client_ ? "client" : "server", cipher().c_str());
+      setup_fast_path();
       if (on_connected) on_connected();
       if (closed_) return;
     } else {
@@ -221,13 +421,14 @@ void DtlsTransport::drive() {
       return;
     }
   }
-  // Application data: one record per SSL_read.
+  // Application data through OpenSSL (before our layer is armed, or for
+  // records OpenSSL buffered during the handshake).
   uint8_t buf[17 * 1024];
   while (!closed_) {
     ERR_clear_error();
     int n = SSL_read(ssl_, buf, sizeof buf);
     if (n > 0) {
-      if (on_data) on_data(buf, size_t(n));
+      if (on_data) on_data(Bytes::copy(buf, size_t(n)));
       continue;
     }
     int e = SSL_get_error(ssl_, n);
@@ -256,7 +457,7 @@ void DtlsTransport::arm_timer() {
   std::weak_ptr<DtlsTransport> w = shared_from_this();
   timer_ = r_.call_later_us(us ? us : 1, [w] {
     auto s = w.lock();
-    if (!s || s->closed_) return;
+    if (!s || s->closed_ || s->fast_tx_) return;
     s->timer_ = 0;
     if (DTLSv1_handle_timeout(s->ssl_) < 0) {
       s->fail("DTLS handshake timed out");
@@ -266,8 +467,7 @@ void DtlsTransport::arm_timer() {
   });
 }
 
-void DtlsTransport::on_datagram(const uint8_t* p, size_t n) {
-  if (closed_) return;
+void DtlsTransport::feed_openssl(const uint8_t* p, size_t n) {
   in_ = p;
   in_len_ = n;
   drive();
@@ -275,10 +475,87 @@ void DtlsTransport::on_datagram(const uint8_t* p, size_t n) {
   in_len_ = 0;
 }
 
+void DtlsTransport::on_datagram(const uint8_t* p, size_t n) {
+  auto buf = std::make_shared<RawBuf>(n ? n : 1);
+  memcpy(buf->data.get(), p, n);
+  uint8_t* d = buf->data.get();
+  on_datagram(std::move(buf), d, n);
+}
+
+void DtlsTransport::on_datagram(std::shared_ptr<const void> owner, uint8_t* p, size_t n) {
+  if (closed_) return;
+  auto self = shared_from_this();
+  size_t off = 0;
+  while (off + kRecHdr <= n && !closed_) {
+    uint8_t* rec = p + off;
+    uint8_t type = rec[0];
+    uint16_t epoch = rd16(rec + 3);
+    size_t len = kRecHdr + rd16(rec + 11);
+    if (off + len > n) break;  // truncated record: drop the rest
+    off += len;
+    if (fast_rx_ && epoch == 1 && (type == kAppData || type == kAlert)) {
+      uint8_t* pt;
+      size_t ptl;
+      if (!fast_decrypt(rec, len, type, rd48(rec + 5), &pt, &ptl)) {
+        LOG_TRACE(kT, "dropping DTLS record that fails authentication or replay check");
+        continue;
+      }
+      if (type == kAlert) {
+        if (ptl >= 2 && (pt[0] == 2 || pt[1] == 0)) {
+          fail(pt[1] == 0 ? "DTLS close_notify received" : "DTLS fatal alert received");
+          return;
+        }
+        continue;
+      }
+      if (!fast_tx_) {
+        // The peer finished its handshake: OpenSSL has nothing left to send.
+        fast_tx_ = true;
+        wseq_ = ossl_max_wseq_ + 1;
+        if (timer_) r_.cancel(timer_);
+        timer_ = 0;
+      }
+      if (on_data) on_data(Bytes::adopt(owner, pt, ptl));
+      continue;
+    }
+    if (fast_tx_) continue;  // stale handshake retransmissions: OpenSSL is retired
+    feed_openssl(rec, len);
+  }
+}
+
 bool DtlsTransport::send(const uint8_t* p, size_t n) {
+  iovec v{const_cast<uint8_t*>(p), n};
+  return send(&v, 1);
+}
+
+bool DtlsTransport::send(const iovec* iov, int cnt) {
   if (!connected_ || closed_) return false;
+  size_t total = 0;
+  for (int i = 0; i < cnt; i++) total += iov[i].iov_len;
+  if (fast_tx_) {
+    size_t rec = kRecHdr + kExplicit + total + kTag;
+    if (reserve_) {
+      uint8_t* o = reserve_(rec);
+      if (!fast_encrypt_into(o, kAppData, iov, cnt, total)) return false;
+      commit_(rec);
+    } else {
+      if (scratch_.size() < rec) scratch_.resize(rec);
+      if (!fast_encrypt_into(scratch_.data(), kAppData, iov, cnt, total)) return false;
+      if (write_) write_(scratch_.data(), rec);
+    }
+    return true;
+  }
+  const void* p = iov[0].iov_base;
+  if (cnt > 1) {
+    scratch_.resize(total);
+    size_t o = 0;
+    for (int i = 0; i < cnt; i++) {
+      memcpy(scratch_.data() + o, iov[i].iov_base, iov[i].iov_len);
+      o += iov[i].iov_len;
+    }
+    p = scratch_.data();
+  }
   ERR_clear_error();
-  int rc = SSL_write(ssl_, p, int(n));
+  int rc = SSL_write(ssl_, p, int(total));
   if (rc <= 0) {
     LOG_DEBUG(kT, "DTLS write failed: %s", ssl_errors().c_str());
     return false;
@@ -301,7 +578,14 @@ std::string DtlsTransport::cipher() const {
 
 void DtlsTransport::close() {
   if (closed_) return;
-  if (ssl_ && connected_) SSL_shutdown(ssl_);
+  if (fast_tx_ && connected_) {
+    static const uint8_t kCloseNotify[2] = {1, 0};
+    iovec v{const_cast<uint8_t*>(kCloseNotify), 2};
+    uint8_t rec[kRecHdr + kExplicit + 2 + kTag];
+    if (fast_encrypt_into(rec, kAlert, &v, 1, 2) && write_) write_(rec, sizeof rec);
+  } else if (ssl_ && connected_) {
+    SSL_shutdown(ssl_);
+  }
   closed_ = true;
   if (timer_) r_.cancel(timer_);
   timer_ = 0;

@@ -3,26 +3,55 @@
 // Replaces webrtc-dtls 0.10 in the reference stack. Each peer uses an
 // ephemeral ECDSA P-256 self-signed certificate whose SHA-256 fingerprint is
 // advertised in SDP (a=fingerprint); the handshake verifies the peer's
-// certificate against the fingerprint from the remote SDP. I/O goes through a
-// custom datagram BIO (one BIO write == one UDP datagram) wired to the ICE
-// agent's batched send path, and OpenSSL's retransmission timer is driven by
-// the reactor.
+// certificate against the fingerprint from the remote SDP. OpenSSL runs the
+// handshake through a custom datagram BIO (one BIO read == one record) wired
+// to the ICE agent's batched send path, and its retransmission timer is
+// driven by the reactor.
+//
+// Application data takes a zero-copy record layer of our own once the
+// handshake is done and the suite is AES-GCM (what every WebRTC stack
+// negotiates first):
+//   - keys come from the session's master secret through the TLS 1.2 PRF
+//     ("key expansion", RFC 5246 §6.3) and are checked against a probe record
+//     OpenSSL itself encrypts before the switch;
+//   - send: the SCTP packet arrives as an iovec gather list (headers plus
+//     slices of the frames) and is encrypted straight into the outgoing
+//     datagram buffer — no plaintext copy, several records per datagram on
+//     same-host jumbo paths;
+//   - receive: records are authenticated and decrypted in place inside the
+//     pooled receive buffer and handed up as Bytes views into it;
+//   - RFC 6347 §4.1.2.6 anti-replay window.
+// Records from OpenSSL and ours never share a sequence number: our send side
+// starts after the highest epoch-1 sequence OpenSSL wrote, and only once the
+// peer has proven it finished the handshake (its first application record
+// decrypted), after which OpenSSL never writes again.
 #pragma once
+
+#include <sys/uio.h>
 
 #include <functional>
 #include <memory>
 #include <string>
+#include <vector>
 
+#include "core/buf.h"
 #include "core/reactor.h"
 
 typedef struct ssl_st SSL;
 typedef struct bio_st BIO;
+typedef struct evp_cipher_ctx_st EVP_CIPHER_CTX;
 
 namespace p2pt::rtc {
 
 class DtlsTransport : public std::enable_shared_from_this<DtlsTransport> {
  public:
   using WriteFn = std::function<void(const uint8_t*, size_t)>;
+  // Space for one record appended to the datagram being assembled
+  // (reserve(max) -> pointer, commit(used)). Optional: without it records are
+  // built in a scratch buffer and handed to WriteFn.
+  using ReserveFn = std::function<uint8_t*(size_t)>;
+  using CommitFn = std::function<void(size_t)>;
+
   static std::shared_ptr<DtlsTransport> create(Reactor& r, bool is_client, std::string remote_fingerprint,
                                                WriteFn write_datagram);
   ~DtlsTransport();
@@ -30,18 +59,28 @@ class DtlsTransport : public std::enable_shared_from_this<DtlsTransport> {
   // "sha-256 AB:CD:..." value for a=fingerprint (process-wide certificate).
   static const std::string& local_fingerprint();
 
+  void set_record_sink(ReserveFn reserve, CommitFn commit) {
+    reserve_ = std::move(reserve);
+    commit_ = std::move(commit);
+  }
   void start();
-  void on_datagram(const uint8_t* p, size_t n);
-  // Encrypt and send one application record (one SCTP packet).
+  // One received datagram (may hold several records). The buffer is owned by
+  // `owner` and is decrypted in place; plaintext is handed up as views into it.
+  void on_datagram(std::shared_ptr<const void> owner, uint8_t* p, size_t n);
+  void on_datagram(const uint8_t* p, size_t n);  // copies first
+  // Encrypt and send one application record (one SCTP packet) given as a
+  // gather list.
+  bool send(const iovec* iov, int cnt);
   bool send(const uint8_t* p, size_t n);
   void close();
   bool connected() const { return connected_; }
+  bool fast_path() const { return fast_tx_; }  // own record layer carries sends
   // Largest application record (plaintext) after the handshake.
   void set_record_limit(size_t n);
   std::string cipher() const;
 
   std::function<void()> on_connected;
-  std::function<void(const uint8_t*, size_t)> on_data;
+  std::function<void(Bytes)> on_data;
   std::function<void(const std::string&)> on_closed;
 
  private:
@@ -50,6 +89,11 @@ class DtlsTransport : public std::enable_shared_from_this<DtlsTransport> {
   void arm_timer();
   void fail(const std::string& why);
   bool verify_peer();
+  void setup_fast_path();
+  bool fast_decrypt(uint8_t* rec, size_t len, uint8_t type, uint64_t seq48, uint8_t** pt, size_t* pt_len);
+  bool fast_encrypt_into(uint8_t* out, uint8_t type, const iovec* iov, int cnt, size_t total);
+  void feed_openssl(const uint8_t* p, size_t n);
+  void bio_wrote(const uint8_t* p, size_t n);
 
   Reactor& r_;
   SSL* ssl_ = nullptr;
@@ -59,11 +103,28 @@ class DtlsTransport : public std::enable_shared_from_this<DtlsTransport> {
   bool closed_ = false;
   std::string remote_fp_;
   WriteFn write_;
+  ReserveFn reserve_;
+  CommitFn commit_;
   uint64_t timer_ = 0;
-  // current inbound datagram (read by the BIO)
+  // current inbound record (read by the BIO)
   const uint8_t* in_ = nullptr;
   size_t in_len_ = 0;
   size_t mtu_ = 1200;
+
+  // --- own record layer
+  bool fast_rx_ = false;   // decrypt epoch-1 application records ourselves
+  bool fast_tx_ = false;   // encrypt ourselves; OpenSSL is muted from here on
+  bool capture_ = false;   // BIO writes are captured (probe record), not sent
+  std::string captured_;
+  EVP_CIPHER_CTX* wctx_ = nullptr;
+  EVP_CIPHER_CTX* rctx_ = nullptr;
+  uint8_t wiv_[4] = {}, riv_[4] = {};
+  uint64_t wseq_ = 0;              // next epoch-1 sequence number we send
+  uint64_t ossl_max_wseq_ = 0;     // highest epoch-1 sequence OpenSSL wrote
+  uint64_t rx_max_ = 0;            // anti-replay: highest authenticated seq
+  uint64_t rx_bitmap_ = 0;         // bit i = rx_max_ - i seen
+  bool rx_any_ = false;
+  std::vector<uint8_t> scratch_;
   friend struct DtlsBio;
 };
 

@@ -93,7 +93,7 @@ IceAgent::IceAgent(Reactor& r, IceConfig cfg, bool controlling)
     : r_(r), cfg_(std::move(cfg)), controlling_(controlling), tiebreaker_(random_u64()) {
   ufrag_ = random_ice_chars(16);
   pwd_ = random_ice_chars(32);
-  rxbuf_.resize(size_t(32) * 65536);
+  rxpool_.resize(32);
 }
 
 IceAgent::~IceAgent() { close(); }
@@ -407,8 +407,46 @@ void IceAgent::send_raw(int local_idx, const SockAddr& to, const uint8_t* p, siz
   Out o;
   o.local = local_idx;
   o.to = to;
+  if (!spare_.empty()) {
+    o.data = std::move(spare_.back());
+    spare_.pop_back();
+  }
   o.data.assign(p, p + n);
   outq_.push_back(std::move(o));
+}
+
+uint8_t* IceAgent::reserve_append(size_t max) {
+  if (sel_local_ < 0 || closed_) {
+    drop_.resize(max);
+    append_at_ = SIZE_MAX;
+    return drop_.data();
+  }
+  if (!outq_.empty()) {
+    Out& b = outq_.back();
+    if (b.coalesce && b.local == sel_local_ && b.to == sel_remote_ && b.data.size() + max <= coalesce_limit_) {
+      append_at_ = b.data.size();
+      b.data.resize(append_at_ + max);
+      return b.data.data() + append_at_;
+    }
+  }
+  Out o;
+  o.local = sel_local_;
+  o.to = sel_remote_;
+  o.coalesce = coalesce_limit_ > 0 && !locals_[sel_local_].relay;
+  if (!spare_.empty()) {
+    o.data = std::move(spare_.back());
+    spare_.pop_back();
+  }
+  o.data.reserve(std::max(coalesce_limit_, max));
+  o.data.resize(max);
+  outq_.push_back(std::move(o));
+  append_at_ = 0;
+  return outq_.back().data.data();
+}
+
+void IceAgent::commit_append(size_t used) {
+  if (append_at_ == SIZE_MAX || outq_.empty()) return;
+  outq_.back().data.resize(append_at_ + used);
 }
 
 void IceAgent::send(const uint8_t* p, size_t n) {
@@ -447,10 +485,18 @@ FaultCfg& fault() {
 }  // namespace
 
 void IceAgent::flush() {
-  if (outq_.empty() || closed_) {
-    outq_.clear();
-    return;
-  }
+  struct Recycle {
+    IceAgent* a;
+    ~Recycle() {
+      for (auto& o : a->outq_)
+        if (a->spare_.size() < 64 && o.data.capacity() >= 2048) {
+          o.data.clear();
+          a->spare_.push_back(std::move(o.data));
+        }
+      a->outq_.clear();
+    }
+  } recycle{this};
+  if (outq_.empty() || closed_) return;
   if (fault().on) {
     std::vector<Out> keep;
     for (auto& o : outq_) {
@@ -525,7 +571,6 @@ void IceAgent::flush() {
     }
     i = j;
   }
-  outq_.clear();
 }
 
 int IceAgent::local_for_socket(int si, bool relay) const {
@@ -543,8 +588,11 @@ void IceAgent::on_readable(int si) {
   sockaddr_storage from[kBatch];
   for (int round = 0; round < 8 && !closed_; round++) {
     for (int i = 0; i < kBatch; i++) {
+      // A slot whose previous datagram is still referenced (zero-copy views
+      // handed up the stack) gets a fresh buffer.
+      if (!rxpool_[i] || rxpool_[i].use_count() > 1) rxpool_[i] = std::make_shared<RawBuf>(65536);
       memset(&msgs[i], 0, sizeof msgs[i]);
-      iovs[i].iov_base = rxbuf_.data() + size_t(i) * 65536;
+      iovs[i].iov_base = rxpool_[i]->data.get();
       iovs[i].iov_len = 65536;
       msgs[i].msg_hdr.msg_iov = &iovs[i];
       msgs[i].msg_hdr.msg_iovlen = 1;
@@ -557,19 +605,20 @@ void IceAgent::on_readable(int si) {
       SockAddr a;
       memcpy(&a.ss, &from[i], msgs[i].msg_hdr.msg_namelen);
       a.len = msgs[i].msg_hdr.msg_namelen;
-      const uint8_t* p = rxbuf_.data() + size_t(i) * 65536;
+      const uint8_t* p = rxpool_[i]->data.get();
       size_t len = msgs[i].msg_len;
       if (turn_ && turn_->is_server(si, a)) {
         turn_->on_packet(p, len);
         continue;
       }
-      handle_datagram(-1, si, a, p, len, false);
+      handle_datagram(-1, si, a, p, len, false, rxpool_[i]);
     }
     if (n < kBatch) return;
   }
 }
 
-void IceAgent::handle_datagram(int, int si, const SockAddr& from, const uint8_t* p, size_t n, bool via_relay) {
+void IceAgent::handle_datagram(int, int si, const SockAddr& from, const uint8_t* p, size_t n, bool via_relay,
+                               const RawBufPtr& owner) {
   if (n == 0) return;
   last_rx_ = Reactor::now_ms();
   if (stun::looks_like_stun(p, n)) {
@@ -585,7 +634,15 @@ void IceAgent::handle_datagram(int, int si, const SockAddr& from, const uint8_t*
       sel_remote_ = from;
     }
   }
-  if (on_data) on_data(p, n);
+  if (!on_data) return;
+  if (owner && p == owner->data.get()) {
+    on_data(owner, owner->data.get(), n);
+  } else {  // relayed (inside a TURN message): private copy
+    auto b = std::make_shared<RawBuf>(n ? n : 1);
+    memcpy(b->data.get(), p, n);
+    uint8_t* d = b->data.get();
+    on_data(std::move(b), d, n);
+  }
 }
 
 void IceAgent::handle_stun(int si, const SockAddr& from, const uint8_t* p, size_t n, bool via_relay) {

@@ -27,6 +27,28 @@
 
 namespace p2pt::rtc {
 
+// Byte vector whose resize() leaves new bytes uninitialised (datagram
+// buffers are always fully written before use).
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = NoInitAlloc<U>;
+  };
+  NoInitAlloc() = default;
+  template <class U>
+  NoInitAlloc(const NoInitAlloc<U>&) {}
+  template <class U>
+  void construct(U* p) noexcept {
+    ::new (static_cast<void*>(p)) U;
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+  }
+};
+using DgVec = std::vector<uint8_t, NoInitAlloc<uint8_t>>;
+
 struct Candidate {
   std::string foundation;
   int component = 1;
@@ -88,6 +110,14 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   // Datagram path (valid once a pair is usable). Queued and flushed with one
   // sendmmsg per reactor iteration.
   void send(const uint8_t* p, size_t n);
+  // Zero-copy record assembly on the selected path: space for `max` bytes at
+  // the end of the datagram being built (a new one when it would exceed the
+  // coalescing limit), then commit how many were written.
+  uint8_t* reserve_append(size_t max);
+  void commit_append(size_t used);
+  // Pack several DTLS records into one datagram up to this size (0 = one per
+  // datagram). Only for same-host jumbo paths, where IP never fragments.
+  void set_coalesce_limit(size_t n) { coalesce_limit_ = n; }
   bool has_path() const { return sel_local_ >= 0; }
   // True when both ends of the selected pair are on this host.
   bool selected_same_host() const;
@@ -99,7 +129,9 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   std::function<void(const Candidate&)> on_candidate;
   std::function<void()> on_gathering_done;
   std::function<void(IceState)> on_state;
-  std::function<void(const uint8_t*, size_t)> on_data;  // non-STUN datagrams (DTLS)
+  // Non-STUN datagrams (DTLS), in a pooled buffer the receiver may modify in
+  // place and keep views into (via `owner`).
+  std::function<void(std::shared_ptr<const void> owner, uint8_t*, size_t)> on_data;
 
  private:
   struct Sock {
@@ -127,7 +159,8 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   IceAgent(Reactor& r, IceConfig cfg, bool controlling);
   void open_sockets();
   void on_readable(int si);
-  void handle_datagram(int local_idx_hint, int si, const SockAddr& from, const uint8_t* p, size_t n, bool via_relay);
+  void handle_datagram(int local_idx_hint, int si, const SockAddr& from, const uint8_t* p, size_t n, bool via_relay,
+                       const RawBufPtr& owner = nullptr);
   void handle_stun(int si, const SockAddr& from, const uint8_t* p, size_t n, bool via_relay);
   void handle_request(int si, const SockAddr& from, const stun::Message& m, const uint8_t* p, size_t n, bool via_relay);
   void handle_response(const SockAddr& from, const stun::Message& m, const uint8_t* p, size_t n);
@@ -183,11 +216,16 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   struct Out {
     int local;
     SockAddr to;
-    std::vector<uint8_t> data;
+    DgVec data;
     bool faulted = false;  // already passed the fault injector
+    bool coalesce = false; // more records may be appended
   };
   std::vector<Out> outq_;
-  std::vector<uint8_t> rxbuf_;
+  std::vector<DgVec> spare_;        // recycled datagram buffers
+  size_t coalesce_limit_ = 0;
+  size_t append_at_ = 0;
+  std::vector<RawBufPtr> rxpool_;   // recvmmsg slots; replaced while views into them live
+  DgVec drop_;                      // reserve_append target with no path
   friend class TurnClient;
 };
 

@@ -11,7 +11,8 @@
 // Bring-up order: ICE pair selected -> DTLS handshake (role from a=setup) ->
 // SCTP association (both sides INIT) -> DCEP OPEN/ACK (RFC 8832) -> open.
 // Datagrams produced in a reactor batch are flushed together: SCTP bundles,
-// DTLS encrypts one record per packet, ICE sends them with one sendmmsg.
+// DTLS encrypts one record per packet (into ICE's datagram buffers), ICE
+// sends them with one sendmmsg.
 #pragma once
 
 #include <functional>
@@ -34,7 +35,8 @@ struct PcConfig {
   IceConfig ice;
   size_t sctp_mtu = 1200;
   bool allow_jumbo = true;   // advertise/use large SCTP packets on same-host paths
-  size_t jumbo_mtu = 16000;
+  size_t jumbo_mtu = 16384;       // = max DTLS plaintext record (2^14)
+  size_t jumbo_datagram = 65000;  // records packed per same-host datagram (UDP max 65507)
   size_t jumbo_initial_cwnd = 1 << 20;
   // Delayed-SACK window for lone packets. Worth it on the side that usually
   // answers what it receives (serve: a request's SACK rides on its response);
@@ -52,6 +54,7 @@ class DataChannel : public MessageChannel, public std::enable_shared_from_this<D
   bool is_open() const override { return open_ && !closed_; }
   void close() override;
   std::string describe() const override;
+  size_t body_chunk() const override;
   const std::string& label() const { return label_; }
   int stream() const { return stream_; }
 

@@ -72,8 +72,13 @@ struct SctpAssociation::InChunk {
   uint8_t flags;
   uint16_t stream;
   uint32_t ppid;
-  std::vector<uint8_t> data;
+  Bytes data;
 };
+
+namespace {
+constexpr size_t kInlineMax = 512;      // payload pieces below this are copied into the packet buffer
+constexpr size_t kZeroCopyMin = 2048;   // received messages at least this big are delivered as views
+}  // namespace
 
 std::shared_ptr<SctpAssociation> SctpAssociation::create(Reactor& r, SctpConfig cfg, PacketOut out) {
   return std::shared_ptr<SctpAssociation>(new SctpAssociation(r, cfg, std::move(out)));
@@ -120,7 +125,43 @@ void SctpAssociation::emit_packet(std::vector<uint8_t>& pkt) {
   pkt[10] = uint8_t(crc >> 16);
   pkt[11] = uint8_t(crc >> 24);
   stats_.packets_sent++;
-  if (out_) out_(pkt.data(), pkt.size());
+  iovec v{pkt.data(), pkt.size()};
+  if (out_) out_(&v, 1);
+}
+
+void SctpAssociation::begin_gather() {
+  if (pkt_.capacity() < cfg_.mtu + 64) pkt_.reserve(cfg_.mtu + 64);  // no pointers into pkt_ exist yet
+  pkt_.clear();
+  put16(pkt_, cfg_.local_port);
+  put16(pkt_, cfg_.remote_port);
+  put32(pkt_, peer_vtag_);
+  put32(pkt_, 0);
+  iov_.clear();
+  run_start_ = 0;
+  pkt_len_ = kCommonHdr;
+}
+
+void SctpAssociation::close_run() {
+  if (pkt_.size() > run_start_) iov_.push_back(iovec{pkt_.data() + run_start_, pkt_.size() - run_start_});
+  run_start_ = pkt_.size();
+}
+
+// CRC32c over the gather list (checksum field zeroed), then hand it to DTLS.
+void SctpAssociation::emit_gather() {
+  close_run();
+  pkt_[8] = pkt_[9] = pkt_[10] = pkt_[11] = 0;
+  uint32_t crc = 0;
+  // Both sides accept zero checksums over DTLS (RFC 9653): skip the pass.
+  bool zero = cfg_.zero_checksum && peer_zero_checksum_ && state_ != State::CookieWait &&
+              state_ != State::CookieEchoed && state_ != State::Closed;
+  if (!zero)
+    for (auto& v : iov_) crc = crc32c(v.iov_base, v.iov_len, crc);
+  pkt_[8] = uint8_t(crc);
+  pkt_[9] = uint8_t(crc >> 8);
+  pkt_[10] = uint8_t(crc >> 16);
+  pkt_[11] = uint8_t(crc >> 24);
+  stats_.packets_sent++;
+  if (out_) out_(iov_.data(), int(iov_.size()));
 }
 
 static void begin_packet(std::vector<uint8_t>& pkt, uint16_t sport, uint16_t dport, uint32_t vtag) {
@@ -162,6 +203,21 @@ void SctpAssociation::append_init_params(std::vector<uint8_t>& v) {
   // Forward-TSN-Supported.
   put16(v, 0xC000);
   put16(v, 4);
+  if (cfg_.zero_checksum) {  // Zero Checksum Acceptable, EDMID 1 = DTLS (RFC 9653 §4)
+    put16(v, 0x8001);
+    put16(v, 8);
+    put32(v, 1);
+  }
+}
+
+bool SctpAssociation::peer_offers_zero_checksum(const uint8_t* c, size_t len) const {
+  for (size_t off = 0; off + 4 <= len;) {
+    uint16_t pt = rd16(c + off), pl = rd16(c + off + 2);
+    if (pl < 4 || off + pl > len) break;
+    if (pt == 0x8001 && pl >= 8 && rd32(c + off + 4) == 1) return true;
+    off += (pl + 3u) & ~3u;
+  }
+  return false;
 }
 
 void SctpAssociation::send_init() {
@@ -204,7 +260,7 @@ void SctpAssociation::on_init_timer() {
 }
 
 std::string SctpAssociation::make_cookie(uint32_t peer_tag, uint32_t peer_tsn, uint32_t peer_rwnd, uint16_t peer_os,
-                                         uint16_t peer_mis) {
+                                         uint16_t peer_mis, uint32_t peer_flags) {
   std::vector<uint8_t> c;
   put32(c, peer_tag);
   put32(c, peer_tsn);
@@ -212,6 +268,7 @@ std::string SctpAssociation::make_cookie(uint32_t peer_tag, uint32_t peer_tsn, u
   put16(c, peer_os);
   put16(c, peer_mis);
   put32(c, my_vtag_);
+  put32(c, peer_flags);
   uint64_t now = Reactor::now_ms();
   put32(c, uint32_t(now >> 32));
   put32(c, uint32_t(now));
@@ -224,17 +281,21 @@ std::string SctpAssociation::make_cookie(uint32_t peer_tag, uint32_t peer_tsn, u
 
 // ------------------------------------------------------------------ input
 
-void SctpAssociation::on_packet(const uint8_t* p, size_t n) {
+void SctpAssociation::on_packet(const Bytes& pkt) {
+  const uint8_t* p = pkt.data();
+  size_t n = pkt.size();
   if (n < kCommonHdr + 4) return;
   uint32_t got = uint32_t(p[8]) | uint32_t(p[9]) << 8 | uint32_t(p[10]) << 16 | uint32_t(p[11]) << 24;
-  uint8_t hdr[kCommonHdr];
-  memcpy(hdr, p, kCommonHdr);
-  hdr[8] = hdr[9] = hdr[10] = hdr[11] = 0;
-  // crc32c() chains: the header (checksum zeroed) then the chunks.
-  uint32_t crc = crc32c(p + kCommonHdr, n - kCommonHdr, crc32c(hdr, kCommonHdr));
-  if (crc != got) {
-    LOG_TRACE(kT, "dropping SCTP packet with bad checksum");
-    return;
+  if (!(cfg_.zero_checksum && got == 0)) {  // RFC 9653 §5.2: accept zero, verify anything else
+    uint8_t hdr[kCommonHdr];
+    memcpy(hdr, p, kCommonHdr);
+    hdr[8] = hdr[9] = hdr[10] = hdr[11] = 0;
+    // crc32c() chains: the header (checksum zeroed) then the chunks.
+    uint32_t crc = crc32c(p + kCommonHdr, n - kCommonHdr, crc32c(hdr, kCommonHdr));
+    if (crc != got) {
+      LOG_TRACE(kT, "dropping SCTP packet with bad checksum");
+      return;
+    }
   }
   uint32_t vtag = rd32(p + 4);
   stats_.packets_received++;
@@ -265,7 +326,7 @@ void SctpAssociation::on_packet(const uint8_t* p, size_t n) {
       return;
     }
     switch (type) {
-      case kData: handle_data(flags, body, blen); break;
+      case kData: handle_data(flags, body, blen, pkt); break;
       case kInit: handle_init(body, blen, vtag); break;
       case kInitAck: handle_init_ack(body, blen); break;
       case kSack: handle_sack(body, blen); break;
@@ -301,7 +362,8 @@ void SctpAssociation::handle_init(const uint8_t* c, size_t len, uint32_t) {
   uint16_t os = rd16(c + 8), mis = rd16(c + 10);
   uint32_t tsn = rd32(c + 12);
   if (tag == 0) return;
-  std::string cookie = make_cookie(tag, tsn, rwnd, os, mis);
+  uint32_t flags = peer_offers_zero_checksum(c + 16, len - 16) ? 1 : 0;
+  std::string cookie = make_cookie(tag, tsn, rwnd, os, mis, flags);
   std::vector<uint8_t> b;
   put32(b, my_vtag_);
   put32(b, cfg_.rwnd);
@@ -334,6 +396,7 @@ void SctpAssociation::handle_init_ack(const uint8_t* c, size_t len) {
     off += (pl + 3u) & ~3u;
   }
   if (!cookie) return;
+  peer_zero_checksum_ = peer_offers_zero_checksum(c + 16, len - 16);
   if (!have_peer_tsn_) {
     peer_cum_tsn_ = tsn - 1;
     have_peer_tsn_ = true;
@@ -345,22 +408,25 @@ void SctpAssociation::handle_init_ack(const uint8_t* c, size_t len) {
 }
 
 void SctpAssociation::handle_cookie_echo(const uint8_t* c, size_t len) {
-  if (len != 28 + 32) return;
+  constexpr size_t kBody = 32;  // tag, tsn, rwnd, os, mis, my tag, flags, time
+  if (len != kBody + 32) return;
   unsigned int mlen = 0;
   uint8_t mac[32];
-  HMAC(EVP_sha256(), cookie_key_, sizeof cookie_key_, c, 28, mac, &mlen);
-  if (memcmp(mac, c + 28, 32) != 0) {
+  HMAC(EVP_sha256(), cookie_key_, sizeof cookie_key_, c, kBody, mac, &mlen);
+  if (memcmp(mac, c + kBody, 32) != 0) {
     LOG_DEBUG(kT, "invalid SCTP cookie");
     return;
   }
   uint32_t peer_tag = rd32(c), peer_tsn = rd32(c + 4), peer_rwnd = rd32(c + 8);
   uint32_t my_tag = rd32(c + 16);
   if (my_tag != my_vtag_) return;
+  bool peer_zero = rd32(c + 20) & 1;
   if (state_ == State::Established || state_ == State::ShutdownPending) {
     if (peer_tag == peer_vtag_) queue_control(kCookieAck, 0, {});
     return;
   }
   peer_vtag_ = peer_tag;
+  peer_zero_checksum_ = peer_zero;
   if (!have_peer_tsn_) {
     peer_cum_tsn_ = peer_tsn - 1;
     have_peer_tsn_ = true;
@@ -427,7 +493,7 @@ void SctpAssociation::abort(const std::string& reason) {
   closed(reason);
 }
 
-void SctpAssociation::handle_data(uint8_t flags, const uint8_t* c, size_t len) {
+void SctpAssociation::handle_data(uint8_t flags, const uint8_t* c, size_t len, const Bytes& pkt) {
   if (len < 12 || !have_peer_tsn_) return;
   uint32_t tsn = rd32(c);
   uint16_t stream = rd16(c + 4);
@@ -442,10 +508,19 @@ void SctpAssociation::handle_data(uint8_t flags, const uint8_t* c, size_t len) {
     if (dups_.size() < 32) dups_.push_back(tsn);
     return;
   }
-  auto deliver_chunk = [this](uint8_t fl, uint16_t st, uint32_t pp, const uint8_t* dp, size_t dn) {
+  // A view of this chunk's payload: zero-copy for big payloads, a private
+  // copy for small ones (or when the packet is not a view we may keep).
+  auto hold = [&pkt](const uint8_t* dp, size_t dn) {
+    if (dn >= kZeroCopyMin && dp >= pkt.data() && dp + dn <= pkt.data() + pkt.size())
+      return pkt.slice(size_t(dp - pkt.data()), dn);
+    return Bytes::copy(dp, dn);
+  };
+  auto deliver_chunk = [this](uint8_t fl, uint16_t st, uint32_t pp, const Bytes& d) {
     bool B = fl & 2, E = fl & 1, U = fl & 4;
+    const uint8_t* dp = d.data();
+    size_t dn = d.size();
     if (B && E) {
-      if (on_message) on_message(st, pp, Bytes::copy(dp, dn));
+      if (on_message) on_message(st, pp, d);
       return;
     }
     Partial& pa = U ? partial_u_[st] : partial_[st];
@@ -465,7 +540,8 @@ void SctpAssociation::handle_data(uint8_t flags, const uint8_t* c, size_t len) {
   };
   if (d == 1) {
     peer_cum_tsn_ = tsn;
-    deliver_chunk(flags, stream, ppid, data, dlen);
+    bool whole = (flags & 3) == 3;
+    deliver_chunk(flags, stream, ppid, whole ? hold(data, dlen) : Bytes::adopt(nullptr, data, dlen));
     // Drain now-contiguous out-of-order chunks.
     while (!ooo_.empty()) {
       auto it = ooo_.find(peer_cum_tsn_ + 1);
@@ -474,7 +550,7 @@ void SctpAssociation::handle_data(uint8_t flags, const uint8_t* c, size_t len) {
       ooo_.erase(it);
       ooo_bytes_ -= ic->data.size();
       peer_cum_tsn_ = ic->tsn;
-      deliver_chunk(ic->flags, ic->stream, ic->ppid, ic->data.data(), ic->data.size());
+      deliver_chunk(ic->flags, ic->stream, ic->ppid, ic->data);
       delete ic;
     }
     return;
@@ -484,7 +560,7 @@ void SctpAssociation::handle_data(uint8_t flags, const uint8_t* c, size_t len) {
     return;
   }
   if (ooo_bytes_ + dlen > cfg_.rwnd) return;  // window exceeded: drop, peer retransmits
-  auto* ic = new InChunk{tsn, flags, stream, ppid, std::vector<uint8_t>(data, data + dlen)};
+  auto* ic = new InChunk{tsn, flags, stream, ppid, hold(data, dlen)};
   ooo_[tsn] = ic;
   ooo_bytes_ += dlen;
 }
@@ -644,7 +720,7 @@ void SctpAssociation::handle_forward_tsn(const uint8_t* c, size_t len) {
     InChunk* ic = it->second;
     ooo_.erase(it);
     ooo_bytes_ -= ic->data.size();
-    std::vector<uint8_t> tmp = std::move(ic->data);
+    Bytes tmp = std::move(ic->data);
     uint8_t fl = ic->flags;
     uint16_t st = ic->stream;
     uint32_t pp = ic->ppid;
@@ -655,7 +731,8 @@ void SctpAssociation::handle_forward_tsn(const uint8_t* c, size_t len) {
     wr16(hdr.data() + 4, st);
     wr32(hdr.data() + 8, pp);
     hdr.insert(hdr.end(), tmp.begin(), tmp.end());
-    handle_data(fl, hdr.data(), hdr.size());
+    Bytes whole = Bytes::take(std::move(hdr));
+    handle_data(fl, whole.data(), whole.size(), whole);
   }
 }
 
@@ -764,15 +841,15 @@ void SctpAssociation::flush() {
   if (!can_data && ctrl_.empty()) return;
   const size_t mtu = cfg_.mtu;
   size_t max_payload = mtu - kCommonHdr - kDataHdr;
-  std::vector<uint8_t>& pkt = pkt_;
-  begin_packet(pkt, cfg_.local_port, cfg_.remote_port, peer_vtag_);
+  begin_gather();
   auto flush_pkt = [&] {
-    if (pkt.size() > kCommonHdr) emit_packet(pkt);
-    begin_packet(pkt, cfg_.local_port, cfg_.remote_port, peer_vtag_);
+    if (pkt_len_ > kCommonHdr) emit_gather();
+    begin_gather();
   };
   auto add_raw = [&](const std::vector<uint8_t>& ch) {
-    if (pkt.size() + ch.size() > mtu) flush_pkt();
-    pkt.insert(pkt.end(), ch.begin(), ch.end());
+    if (pkt_len_ + ch.size() > mtu) flush_pkt();
+    pkt_.insert(pkt_.end(), ch.begin(), ch.end());
+    pkt_len_ += ch.size();
   };
   // SACK policy: immediate when >= 2 data packets are unacknowledged, on
   // gaps/duplicates, or when DATA goes out now anyway (piggyback); otherwise
@@ -821,9 +898,10 @@ void SctpAssociation::flush() {
   }
   uint64_t now = Reactor::now_us();
   auto add_data = [&](Chunk* ch) {
-    size_t need = kDataHdr + ((ch->len + 3) & ~size_t(3));
-    if (pkt.size() + need > mtu) flush_pkt();
-    size_t start = pkt.size();
+    size_t padded = (ch->len + 3) & ~size_t(3);
+    size_t need = kDataHdr + padded;
+    if (pkt_len_ + need > mtu) flush_pkt();
+    std::vector<uint8_t>& pkt = pkt_;
     pkt.push_back(kData);
     pkt.push_back(ch->flags);
     put16(pkt, uint16_t(kDataHdr + ch->len));
@@ -831,9 +909,18 @@ void SctpAssociation::flush() {
     put16(pkt, ch->stream);
     put16(pkt, ch->ssn);
     put32(pkt, ch->ppid);
-    for (auto& b : ch->data) pkt.insert(pkt.end(), b.begin(), b.end());
-    pad4(pkt);
-    (void)start;
+    // Small pieces are copied inline; large ones are referenced in place
+    // (the chunk keeps its slices alive until acknowledged).
+    for (auto& b : ch->data) {
+      if (b.size() < kInlineMax) {
+        pkt.insert(pkt.end(), b.begin(), b.end());
+      } else {
+        close_run();
+        iov_.push_back(iovec{const_cast<uint8_t*>(b.data()), b.size()});
+      }
+    }
+    pkt.insert(pkt.end(), padded - ch->len, 0);
+    pkt_len_ += need;
     ch->sent_us = now;
     ch->tx++;
     if (!ch->in_flight) {

@@ -17,6 +17,8 @@
 //     and initial cwnd on same-host paths.
 #pragma once
 
+#include <sys/uio.h>
+
 #include <cstdint>
 #include <deque>
 #include <functional>
@@ -42,6 +44,11 @@ struct SctpConfig {
   int max_init_retrans = 8;
   int max_assoc_retrans = 20;
   uint64_t sack_delay_us = 5000;    // delayed SACK for lone packets (0 = always immediate)
+  // RFC 9653 zero checksum with Error Detection Method 1 (the lower layer is
+  // DTLS, which already authenticates every packet): advertised in INIT /
+  // INIT-ACK; once both sides did, packets after setup carry checksum 0 and a
+  // received checksum of 0 is not verified.
+  bool zero_checksum = false;
 };
 
 struct SctpStats {
@@ -56,15 +63,29 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
  public:
   enum class State { Closed, CookieWait, CookieEchoed, Established, ShutdownPending, ShutdownSent, ShutdownReceived,
                      ShutdownAckSent };
-  using PacketOut = std::function<void(const uint8_t*, size_t)>;
+  // One outbound SCTP packet as a gather list: common/chunk headers and small
+  // payloads live in an internal assembly buffer, large payload slices are
+  // referenced in place (the DTLS layer encrypts straight from them).
+  using PacketOut = std::function<void(const iovec*, int)>;
 
   static std::shared_ptr<SctpAssociation> create(Reactor& r, SctpConfig cfg, PacketOut out);
+  // Contiguous view of a gathered packet (tests, fallbacks).
+  static std::vector<uint8_t> flatten(const iovec* iov, int cnt) {
+    std::vector<uint8_t> v;
+    for (int i = 0; i < cnt; i++)
+      v.insert(v.end(), static_cast<const uint8_t*>(iov[i].iov_base),
+               static_cast<const uint8_t*>(iov[i].iov_base) + iov[i].iov_len);
+    return v;
+  }
   ~SctpAssociation();
 
   // Active open (send INIT). Safe to call on both peers (simultaneous open).
   void connect();
-  // Feed one decrypted SCTP packet.
-  void on_packet(const uint8_t* p, size_t n);
+  // Feed one decrypted SCTP packet. Large single-chunk messages are delivered
+  // as views into `pkt` (no copy); small ones are copied so a tiny message
+  // never pins a whole receive buffer.
+  void on_packet(const Bytes& pkt);
+  void on_packet(const uint8_t* p, size_t n) { on_packet(Bytes::copy(p, n)); }
   // Queue a message made of gathered pieces (no copy until packetisation).
   bool send(uint16_t stream, uint32_t ppid, const std::vector<Bytes>& pieces, bool unordered = false);
   // Build and emit packets (bundled). Called once per reactor batch.
@@ -98,7 +119,7 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   void handle_init(const uint8_t* c, size_t len, uint32_t vtag);
   void handle_init_ack(const uint8_t* c, size_t len);
   void handle_cookie_echo(const uint8_t* c, size_t len);
-  void handle_data(uint8_t flags, const uint8_t* c, size_t len);
+  void handle_data(uint8_t flags, const uint8_t* c, size_t len, const Bytes& pkt);
   void handle_sack(const uint8_t* c, size_t len);
   void handle_forward_tsn(const uint8_t* c, size_t len);
   void handle_reconfig(const uint8_t* c, size_t len);
@@ -107,7 +128,9 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   void enter_established();
   void closed(const std::string& why);
 
-  std::string make_cookie(uint32_t peer_tag, uint32_t peer_tsn, uint32_t peer_rwnd, uint16_t peer_os, uint16_t peer_mis);
+  std::string make_cookie(uint32_t peer_tag, uint32_t peer_tsn, uint32_t peer_rwnd, uint16_t peer_os, uint16_t peer_mis,
+                          uint32_t peer_flags);
+  bool peer_offers_zero_checksum(const uint8_t* params, size_t len) const;
   void append_init_params(std::vector<uint8_t>& v);
   void send_init();
   void on_init_timer();
@@ -120,6 +143,9 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   void stop_t3();
   void on_t3();
   void emit_packet(std::vector<uint8_t>& pkt);
+  void begin_gather();
+  void close_run();
+  void emit_gather();
   void maybe_finish_shutdown();
 
   Reactor& r_;
@@ -160,6 +186,7 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   bool retransmit_pending_ = false;
 
   // --- receiver
+  bool peer_zero_checksum_ = false;  // peer advertised RFC 9653 EDMID 1
   bool have_peer_tsn_ = false;
   uint32_t peer_cum_tsn_ = 0;  // highest in-order TSN received
   std::map<uint32_t, InChunk*> ooo_;  // out-of-order (by TSN, serial order via custom cmp)
@@ -182,7 +209,11 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   bool closed_fired_ = false;
   uint32_t reconfig_seq_;
   SctpStats stats_;
-  std::vector<uint8_t> pkt_;
+  // gather assembly of the packet being built by flush()
+  std::vector<uint8_t> pkt_;  // inline bytes; reserved so it never reallocates mid-packet
+  std::vector<iovec> iov_;
+  size_t run_start_ = 0;      // start of the inline run not yet in iov_
+  size_t pkt_len_ = 0;        // total packet bytes (inline + referenced)
 };
 
 }  // namespace p2pt::rtc

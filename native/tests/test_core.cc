@@ -1,5 +1,6 @@
 // Core: JSON, checksums, encodings, reactor timers, frame codec, HTTP parser.
 #include <cstring>
+#include <vector>
 
 #include "core/crypto.h"
 #include "core/json.h"
@@ -61,6 +62,29 @@ TEST(crc32c_vectors) {
   CHECK_EQ(crc32c("123456789", 9), 0xE3069283u);
   // Chaining equals one pass.
   CHECK_EQ(crc32c("456789", 6, crc32c("123", 3)), 0xE3069283u);
+}
+
+TEST(crc32c_multilane_matches_bitwise) {
+  // The 3-lane path (>= 3 KiB) against a bitwise reference, at odd lengths,
+  // misaligned starts and chained calls.
+  auto ref = [](const uint8_t* p, size_t n, uint32_t crc) {
+    crc = ~crc;
+    for (size_t i = 0; i < n; i++) {
+      crc ^= p[i];
+      for (int k = 0; k < 8; k++) crc = crc & 1 ? (crc >> 1) ^ 0x82F63B78u : crc >> 1;
+    }
+    return ~crc;
+  };
+  std::vector<uint8_t> buf(70000);
+  uint32_t x = 12345;
+  for (auto& b : buf) b = uint8_t((x = x * 1103515245u + 12345u) >> 16);
+  for (size_t n : {size_t(3071), size_t(3072), size_t(3073), size_t(6150), size_t(16384), size_t(65536)}) {
+    for (size_t off : {size_t(0), size_t(1), size_t(5)}) {
+      CHECK_EQ(crc32c(buf.data() + off, n), ref(buf.data() + off, n, 0));
+      size_t cut = n / 3 + 1;
+      CHECK_EQ(crc32c(buf.data() + off + cut, n - cut, crc32c(buf.data() + off, cut)), ref(buf.data() + off, n, 0));
+    }
+  }
 }
 
 TEST(crc32_ieee_vector) { CHECK_EQ(crc32_ieee("123456789", 9), 0xCBF43926u); }

@@ -295,12 +295,18 @@ TEST(fuzz_sctp_packets) {
   std::shared_ptr<SctpAssociation> a, b;
   SctpConfig cfg;
   cfg.sack_delay_us = 0;
-  a = SctpAssociation::create(r, cfg, [&](const uint8_t* p, size_t n) {
+  a = SctpAssociation::create(r, cfg, [&](const iovec* iov, int cnt) {
+    auto flat = SctpAssociation::flatten(iov, cnt);
+    const uint8_t* p = flat.data();
+    size_t n = flat.size();
     captured.emplace_back(p, p + n);
     auto pkt = std::make_shared<Buf>(p, p + n);
     r.post([&b, pkt] { if (b) b->on_packet(pkt->data(), pkt->size()); });
   });
-  b = SctpAssociation::create(r, cfg, [&](const uint8_t* p, size_t n) {
+  b = SctpAssociation::create(r, cfg, [&](const iovec* iov, int cnt) {
+    auto flat = SctpAssociation::flatten(iov, cnt);
+    const uint8_t* p = flat.data();
+    size_t n = flat.size();
     captured.emplace_back(p, p + n);
     auto pkt = std::make_shared<Buf>(p, p + n);
     r.post([&a, pkt] { if (a) a->on_packet(pkt->data(), pkt->size()); });

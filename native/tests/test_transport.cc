@@ -43,13 +43,26 @@ struct SctpPair {
   std::shared_ptr<SctpAssociation> a, b;
   LossyLink link;
   std::vector<std::pair<uint16_t, std::string>> got_a, got_b;
-  SctpPair(double loss, double dup, uint64_t delay, size_t mtu = 1200) : link(r, loss, dup, delay) {
+  size_t zero_sums_a = 0, zero_sums_b = 0;  // packets sent with checksum 0
+  SctpPair(double loss, double dup, uint64_t delay, size_t mtu = 1200, bool zc_a = false, bool zc_b = false)
+      : link(r, loss, dup, delay) {
     SctpConfig cfg;
     cfg.mtu = mtu;
     cfg.rto_initial_ms = 100;
     cfg.rto_min_ms = 20;
-    a = SctpAssociation::create(r, cfg, [this](const uint8_t* p, size_t n) { link.carry(b, p, n); });
-    b = SctpAssociation::create(r, cfg, [this](const uint8_t* p, size_t n) { link.carry(a, p, n); });
+    auto zero = [](const std::vector<uint8_t>& f) { return f[8] == 0 && f[9] == 0 && f[10] == 0 && f[11] == 0; };
+    cfg.zero_checksum = zc_a;
+    a = SctpAssociation::create(r, cfg, [this, zero](const iovec* v, int c) {
+      auto f = SctpAssociation::flatten(v, c);
+      zero_sums_a += zero(f);
+      link.carry(b, f.data(), f.size());
+    });
+    cfg.zero_checksum = zc_b;
+    b = SctpAssociation::create(r, cfg, [this, zero](const iovec* v, int c) {
+      auto f = SctpAssociation::flatten(v, c);
+      zero_sums_b += zero(f);
+      link.carry(a, f.data(), f.size());
+    });
     a->on_message = [this](uint16_t s, uint32_t, Bytes m) { got_a.emplace_back(s, m.str()); };
     b->on_message = [this](uint16_t s, uint32_t, Bytes m) { got_b.emplace_back(s, m.str()); };
     r.add_flush_hook([this] {
@@ -83,6 +96,26 @@ TEST(sctp_simultaneous_open_and_messages) {
   for (size_t i = 0; i < p.got_b.size() && i < sent.size(); i++) CHECK(p.got_b[i].second == sent[i]);
   CHECK(!p.got_a.empty() && p.got_a[0].second == "xyz");
   CHECK_EQ(p.a->stats().retransmits, uint64_t(0));
+}
+
+TEST(sctp_zero_checksum_negotiation) {
+  // RFC 9653: zero checksums only once both sides advertised EDMID 1; a peer
+  // without support keeps receiving (and sending) real CRC32c.
+  for (int both = 0; both < 2; both++) {
+    SctpPair p(0, 0, 0, 16384, true, both == 1);
+    p.a->connect();
+    CHECK(p.r.run_until([&] { return p.a->established() && p.b->established(); }, 2000));
+    for (int i = 0; i < 20; i++) p.a->send(1, 53, {Bytes::copy(payload(5000 + size_t(i), uint32_t(i)))});
+    p.b->send(1, 53, {Bytes::copy("back")});
+    CHECK(p.r.run_until([&] { return p.got_b.size() == 20 && p.got_a.size() == 1; }, 3000));
+    CHECK(p.got_b.size() == 20 && p.got_b[19].second == payload(5019, 19));
+    if (both) {
+      CHECK(p.zero_sums_a > 0 && p.zero_sums_b > 0);
+    } else {
+      CHECK_EQ(p.zero_sums_a, size_t(0));
+      CHECK_EQ(p.zero_sums_b, size_t(0));
+    }
+  }
 }
 
 TEST(sctp_loss_reorder_dup_recovery) {
@@ -136,7 +169,7 @@ TEST(dtls_pair_handshake_and_data) {
     r.post([&c, v] { c->on_datagram(v->data(), v->size()); });
   });
   std::string got;
-  s->on_data = [&](const uint8_t* p, size_t n) { got.append(reinterpret_cast<const char*>(p), n); };
+  s->on_data = [&](Bytes b) { got.append(b.view()); };
   bool cc = false, sc = false;
   c->on_connected = [&] { cc = true; };
   s->on_connected = [&] { sc = true; };
@@ -146,6 +179,62 @@ TEST(dtls_pair_handshake_and_data) {
   CHECK(c->send(reinterpret_cast<const uint8_t*>("hello"), 5));
   CHECK(r.run_until([&] { return got == "hello"; }, 1000));
   CHECK(c->cipher().find("GCM") != std::string::npos || !c->cipher().empty());
+}
+
+TEST(dtls_own_record_layer_roundtrip_and_replay) {
+  // OpenSSL-encrypted records open with our derived read keys, our records
+  // (gathered from several pieces) open on the other side, both sides switch
+  // their send path once the peer's first record arrives, and a replayed
+  // datagram is dropped by the anti-replay window.
+  Reactor r;
+  std::shared_ptr<DtlsTransport> c, s;
+  std::string fp = DtlsTransport::local_fingerprint();
+  std::vector<std::vector<uint8_t>> c_sent;
+  c = DtlsTransport::create(r, true, fp, [&](const uint8_t* p, size_t n) {
+    c_sent.emplace_back(p, p + n);
+    auto v = std::make_shared<std::vector<uint8_t>>(p, p + n);
+    r.post([&s, v] { s->on_datagram(v->data(), v->size()); });
+  });
+  s = DtlsTransport::create(r, false, fp, [&](const uint8_t* p, size_t n) {
+    auto v = std::make_shared<std::vector<uint8_t>>(p, p + n);
+    r.post([&c, v] { c->on_datagram(v->data(), v->size()); });
+  });
+  std::vector<std::string> at_s, at_c;
+  s->on_data = [&](Bytes b) { at_s.push_back(b.str()); };
+  c->on_data = [&](Bytes b) { at_c.push_back(b.str()); };
+  bool cc = false, sc = false;
+  c->on_connected = [&] { cc = true; };
+  s->on_connected = [&] { sc = true; };
+  c->start();
+  s->start();
+  CHECK(r.run_until([&] { return cc && sc; }, 3000));
+  CHECK(!c->fast_path() && !s->fast_path());
+  CHECK(c->send(reinterpret_cast<const uint8_t*>("one"), 3));  // OpenSSL record
+  CHECK(r.run_until([&] { return at_s.size() == 1; }, 1000));
+  CHECK(s->fast_path());  // server saw the client's record: it now encrypts itself
+  std::string big(9000, 'x');
+  for (size_t i = 0; i < big.size(); i++) big[i] = char('a' + i % 26);
+  iovec parts[3] = {{const_cast<char*>("hdr:"), 4}, {big.data(), big.size()}, {const_cast<char*>(":end"), 4}};
+  CHECK(s->send(parts, 3));
+  CHECK(r.run_until([&] { return at_c.size() == 1; }, 1000));
+  CHECK(at_c[0] == "hdr:" + big + ":end");
+  CHECK(c->fast_path());
+  size_t before = c_sent.size();
+  CHECK(c->send(reinterpret_cast<const uint8_t*>("two"), 3));  // our record
+  CHECK(r.run_until([&] { return at_s.size() == 2; }, 1000));
+  CHECK(at_s[1] == "two");
+  CHECK(c_sent.size() == before + 1);
+  auto replay = c_sent.back();
+  s->on_datagram(replay.data(), replay.size());
+  replay[replay.size() - 1] ^= 1;  // and a forged tag
+  s->on_datagram(replay.data(), replay.size());
+  r.run_until([&] { return false; }, 50);
+  CHECK(at_s.size() == 2);
+  c->close();
+  std::string why;
+  s->on_closed = [&](const std::string& w) { why = w; };
+  CHECK(r.run_until([&] { return !why.empty(); }, 1000));
+  CHECK(why.find("close_notify") != std::string::npos);
 }
 
 TEST(dtls_fingerprint_mismatch_fails) {

@@ -16,6 +16,7 @@
 #include "core/buf.h"
 #include "core/net.h"
 #include "core/reactor.h"
+#include "proto/frame.h"
 
 namespace p2pt {
 
@@ -30,6 +31,10 @@ class MessageChannel {
   virtual bool is_open() const = 0;
   virtual void close() = 0;
   virtual std::string describe() const = 0;
+  // Largest REQ_BODY/RES_BODY payload per frame. The wire limit is 65408
+  // (reference protocol.rs:10-12); a transport whose packets are smaller may
+  // ask for frames that fit one packet so they are never fragmented/reassembled.
+  virtual size_t body_chunk() const { return proto::kMaxBodyChunk; }
 
   // Message arrived (whole message, zero-copy view where possible).
   std::function<void(Bytes)> on_message;

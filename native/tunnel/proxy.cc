@@ -101,6 +101,17 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
   enum class State { Head, ReadingBody, Awaiting, Responding };
 
   void on_data(const uint8_t* p, size_t n) {
+    if (state_ == State::ReadingBody && inbuf_.empty() && conn_) {
+      // Request body straight from the socket buffer: REQ_BODY frames are
+      // views of it (no staging copy into inbuf_).
+      auto keep = shared_from_this();
+      size_t used = 0;
+      bool more = feed_body(p, n, &used);
+      if (used == SIZE_MAX) return;
+      if (used < n) inbuf_.append(reinterpret_cast<const char*>(p + used), n - used);
+      if (more) process();
+      return;
+    }
     inbuf_.append(reinterpret_cast<const char*>(p), n);
     process();
   }
@@ -115,7 +126,10 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
       }
       if (state_ == State::ReadingBody) {
         if (inbuf_.empty()) return;
-        if (!feed_body()) return;
+        size_t used = 0;
+        bool more = feed_body(reinterpret_cast<const uint8_t*>(inbuf_.data()), inbuf_.size(), &used);
+        if (used != SIZE_MAX) inbuf_.erase(0, used);
+        if (!more) return;
         continue;
       }
       // Awaiting / Responding: further bytes belong to the next (pipelined)
@@ -193,23 +207,28 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     return true;
   }
 
-  bool feed_body() {
+  // Feeds request-body bytes; *used = bytes consumed (SIZE_MAX on a framing
+  // error, after which the connection is closed). Returns whether processing
+  // should continue (the body completed).
+  bool feed_body(const uint8_t* data, size_t len, size_t* used_out) {
+    *used_out = 0;
     auto sess = sess_.lock();
     if (!sess) return false;
     uint32_t sid = sid_;
     bool reject = reject_not_ready_;
-    size_t used = body_.feed(reinterpret_cast<const uint8_t*>(inbuf_.data()), inbuf_.size(),
-                             [&](const uint8_t* d, size_t n) {
-                               if (reject) return;
-                               Bytes b = Bytes::copy(d, n);
-                               for (size_t off = 0; off < n; off += proto::kMaxBodyChunk)
-                                 sess->send(proto::make_body(proto::MsgType::ReqBody, sid, b.slice(off, proto::kMaxBodyChunk)));
-                             });
+    size_t cs = sess->body_chunk();
+    auto conn = conn_;
+    size_t used = body_.feed(data, len, [&](const uint8_t* d, size_t n) {
+      if (reject) return;
+      Bytes b = conn ? conn->rx_view(d, n) : Bytes::copy(d, n);
+      for (size_t off = 0; off < n; off += cs)
+        sess->send(proto::make_body(proto::MsgType::ReqBody, sid, b.slice(off, cs)));
+    });
+    *used_out = used;
     if (used == SIZE_MAX) {
       simple_and_close(400, "text/plain", "Failed to read body");
       return false;
     }
-    inbuf_.erase(0, used);
     if (body_.done()) {
       finish_request_body();
       return true;

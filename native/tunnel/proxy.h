@@ -63,6 +63,7 @@ class ProxySession : public std::enable_shared_from_this<ProxySession> {
   void unregister_stream(uint32_t sid) { streams_.erase(sid); }
   void send(proto::Frame f) { sched_->send(std::move(f)); }
   bool congested() const { return sched_->over_high(); }
+  size_t body_chunk() const { return sched_->body_chunk(); }
   void add_paused_reader(std::weak_ptr<ProxyConn> c) { paused_readers_.push_back(std::move(c)); }
   bool cancel_feature() const { return cancel_feature_; }
   const ProxyConfig& config() const { return cfg_; }

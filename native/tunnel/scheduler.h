@@ -36,6 +36,7 @@ class FrameScheduler {
   bool over_high() const { return pending_bytes() > high_; }
   void pump();
   MessageChannel* channel() const { return ch_.get(); }
+  size_t body_chunk() const { return ch_ ? ch_->body_chunk() : proto::kMaxBodyChunk; }
 
  private:
   bool emit(const proto::Frame& f);

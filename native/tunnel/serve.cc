@@ -283,16 +283,19 @@ void ServeSession::start_request(uint32_t sid, Pending p) {
     trace::event("serve", sid, "res_headers");
   };
   auto first = std::make_shared<bool>(true);
-  cb.on_data = [w, sid, first](const uint8_t* d, size_t n) {
+  cb.on_data = [w, sid, first](Bytes chunk) {
     auto s = w.lock();
     if (!s || s->stopped_) return;
     if (*first) {
       *first = false;
       trace::event("serve", sid, "first_body");
     }
-    Bytes chunk = Bytes::copy(d, n);  // the one user-space copy on this side
-    for (size_t off = 0; off < n; off += proto::kMaxBodyChunk)
-      s->sched_->send(proto::make_body(proto::MsgType::ResBody, sid, chunk.slice(off, proto::kMaxBodyChunk)));
+    // `chunk` views the upstream socket's receive buffer (large reads) or is a
+    // private copy (small ones, e.g. SSE tokens); frames slice it, no copy.
+    size_t n = chunk.size();
+    size_t cs = s->sched_->body_chunk();
+    for (size_t off = 0; off < n; off += cs)
+      s->sched_->send(proto::make_body(proto::MsgType::ResBody, sid, chunk.slice(off, cs)));
     if (s->sched_->over_high() && !s->upstream_paused_) {
       s->upstream_paused_ = true;
       for (auto& kv : s->inflight_)
