@@ -5,6 +5,9 @@
      native mock, the threaded Python mock, and the reference's unthreaded
      (single-threaded, HTTP/1.0) Python mock; WebRTC and TCP transports.
   2. 64 concurrent streams x 1 MB POST bodies (REQ_BODY chunking + back-pressure).
+  4. NAT traversal (config #4): both peers behind emulated port-restricted
+     cone NATs (TUNNEL_NAT, native/rtc/ice.h), STUN-only ICE against a local
+     STUN server, SSE at 1/8 streams through the hole-punched srflx path.
   3. Idle then burst: the tunnel sits idle (PING/PONG keepalive running), then
      16 concurrent streams (the 30-minute idle of config #5 is scaled down via
      --idle-s; keepalive behaviour is identical for any idle length).
@@ -28,19 +31,28 @@ from p2p_llm_tunnel_amd.utils.build import ensure_native  # noqa: E402
 from p2p_llm_tunnel_amd.utils.procs import Tunnel  # noqa: E402
 
 
-def sse_matrix(transport, mock_kind, streams_list, steps, threaded=True, busy_poll_us=0, path=None):
+def sse_matrix(transport, mock_kind, streams_list, steps, threaded=True, busy_poll_us=0, path=None, nat=None):
     mock, port = start_mock(mock_kind, 100, 5) if (mock_kind == "native" or threaded) else _unthreaded()
     rows = []
     extra = ["--busy-poll-us", str(busy_poll_us)] if busy_poll_us else []
+    env = None
+    stun = None
+    if nat:
+        from p2p_llm_tunnel_amd.utils.turn_server import TurnServer
+        stun = TurnServer().start()
+        extra += ["--stun", f"stun:127.0.0.1:{stun.port}"]
+        env = {"TUNNEL_NAT": nat}
     try:
-        with Tunnel(f"http://127.0.0.1:{port}", transport=transport, serve_extra=extra, proxy_extra=extra) as t:
+        with Tunnel(f"http://127.0.0.1:{port}", transport=transport, serve_extra=extra, proxy_extra=extra,
+                    env=env) as t:
             for s in streams_list:
                 loadgen(t.proxy_port, s, 1, path=path)
                 tr = loadgen(t.proxy_port, s, steps, path=path)
                 if not threaded:
                     time.sleep(1.3)  # let serve's spare upstream sockets expire (single-threaded upstream)
                 dr = loadgen(port, s, steps, path=path)
-                rows.append({"transport": transport, "mock": mock_kind if threaded else "python-unthreaded",
+                rows.append({"transport": transport + (f"+nat:{nat}" if nat else ""),
+                             "mock": mock_kind if threaded else "python-unthreaded",
                              "busy_poll_us": busy_poll_us, "path": path or "/v1/chat/completions",
                              "streams": s, "tunneled_req_s": tr["req_s"], "direct_req_s": dr["req_s"],
                              "tunneled_p50_ttft_ms": tr["p50_ttft_ms"], "direct_p50_ttft_ms": dr["p50_ttft_ms"],
@@ -49,6 +61,8 @@ def sse_matrix(transport, mock_kind, streams_list, steps, threaded=True, busy_po
                 print(json.dumps(rows[-1]), file=sys.stderr, flush=True)
     finally:
         mock.stop()
+        if stun:
+            stun.stop()
     return rows
 
 
@@ -123,6 +137,8 @@ def main():
         res["sse"] += sse_matrix("webrtc", "python", [1, 2, 4, 8], 3, threaded=False)
     # BASELINE config #2: Ollama /api/generate NDJSON stream, up to 8 concurrent streams.
     res["sse"] += sse_matrix("webrtc", "native", [1, 8], a.steps, path="/api/generate")
+    # BASELINE config #4: NAT traversal (emulated port-restricted NATs, STUN-only ICE).
+    res["sse"] += sse_matrix("webrtc", "native", [1, 8], a.steps, nat="port-restricted")
     for bp in [int(x) for x in a.busy_poll.split(",") if x]:
         res["sse"] += sse_matrix("webrtc", "native", [1, 8], a.steps, busy_poll_us=bp)
     res["post_64x1MB"] = [post_1mb("webrtc")]

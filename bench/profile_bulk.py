@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""64 streams x 1 MB POST echoed through a tunnel (BASELINE config #3), with
+per-process CPU accounting, SCTP gauges and optional sampling profiles.
+
+    python bench/profile_bulk.py [--transport webrtc|tcp] [--streams 64] [--steps 3]
+                                 [--profile-dir DIR]   # TUNNEL_PROFILE dumps + reports
+
+The profile dumps come from native/core/profiler.cc and are symbolised with
+scripts/profile_report.py.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import subprocess
+import sys
+import time
+import urllib.request
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from bench import start_mock  # noqa: E402
+from p2p_llm_tunnel_amd import binary  # noqa: E402
+from p2p_llm_tunnel_amd.utils.procs import Tunnel, free_port  # noqa: E402
+
+
+def cpu_s(pid: int) -> float:
+    st = open(f"/proc/{pid}/stat").read().rsplit(")", 1)[1].split()
+    return (int(st[11]) + int(st[12])) / os.sysconf("SC_CLK_TCK")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--transport", default="webrtc")
+    ap.add_argument("--streams", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--mb", type=int, default=1)
+    ap.add_argument("--profile-dir", default=None)
+    a = ap.parse_args()
+    env = None
+    if a.profile_dir:
+        os.makedirs(a.profile_dir, exist_ok=True)
+        env = {"TUNNEL_PROFILE": os.path.join(os.path.abspath(a.profile_dir), "tunnel.%p.prof")}
+    mock, port = start_mock("native", 100, 5)
+    ms, mp = free_port(), free_port()
+    out = {}
+    try:
+        with Tunnel(f"http://127.0.0.1:{port}", transport=a.transport, env=env,
+                    serve_extra=["--metrics-listen", f"127.0.0.1:{ms}"],
+                    proxy_extra=["--metrics-listen", f"127.0.0.1:{mp}"]) as t:
+            def run(target):
+                r = subprocess.run([binary("tunnel-loadgen"), "--target", f"127.0.0.1:{target}", "--streams",
+                                    str(a.streams), "--steps", str(a.steps), "--warmup", "1", "--post-bytes",
+                                    str(a.mb << 20)], capture_output=True, text=True, timeout=600)
+                return json.loads(r.stdout.strip().splitlines()[-1])
+            pids = {"serve": t.serve.popen.pid, "proxy": t.proxy.popen.pid, "mock": mock.popen.pid}
+            c0 = {k: cpu_s(v) for k, v in pids.items()}
+            t0 = time.time()
+            tr = run(t.proxy_port)
+            wall = time.time() - t0
+            c1 = {k: cpu_s(v) for k, v in pids.items()}
+            dr = run(port)
+            out = {"transport": a.transport, "streams": a.streams, "body_mb": a.mb, "steps": a.steps,
+                   "tunneled_req_s": tr["req_s"], "direct_req_s": dr["req_s"],
+                   "tunneled_MBps_each_way": tr["req_s"] * a.mb * 1.048576, "errors": tr["errors"] + dr["errors"],
+                   "wall_s_incl_warmup": round(wall, 3),
+                   "cpu_s_incl_warmup": {k: round(c1[k] - c0[k], 3) for k in pids}}
+            for name, p in (("serve", ms), ("proxy", mp)):
+                txt = urllib.request.urlopen(f"http://127.0.0.1:{p}/metrics", timeout=5).read().decode()
+                out[f"{name}_sctp"] = {l.split()[0]: float(l.split()[1]) for l in txt.splitlines()
+                                       if l.startswith("tunnel_sctp")}
+    finally:
+        mock.stop()
+    print(json.dumps(out))
+    if a.profile_dir:
+        for f in sorted(glob.glob(os.path.join(a.profile_dir, "tunnel.*.prof"))):
+            rep = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "profile_report.py"), f, "--top", "25"],
+                                 capture_output=True, text=True).stdout
+            with open(f[:-5] + ".txt", "w") as fh:
+                fh.write(rep)
+
+
+if __name__ == "__main__":
+    main()

@@ -94,6 +94,11 @@ IceAgent::IceAgent(Reactor& r, IceConfig cfg, bool controlling)
   ufrag_ = random_ice_chars(16);
   pwd_ = random_ice_chars(32);
   rxpool_.resize(32);
+  if (const char* e = getenv("TUNNEL_NAT")) {
+    std::string m = e;
+    nat_mode_ = m == "port-restricted" ? 1 : m == "symmetric" ? 2 : 0;
+    if (nat_mode_) LOG_INFO(kT, "NAT emulation: %s", m.c_str());
+  }
 }
 
 IceAgent::~IceAgent() { close(); }
@@ -114,6 +119,14 @@ void IceAgent::close() {
       s.fd = -1;
     }
   }
+  for (auto& np : nat_ports_) {
+    if (np.fd >= 0) {
+      r_.remove(np.fd);
+      ::close(np.fd);
+      np.fd = -1;
+    }
+  }
+  if (nat_mode_) LOG_INFO(kT, "NAT emulation: %llu inbound datagrams filtered", (unsigned long long)nat_dropped_);
   state_ = IceState::Closed;
 }
 
@@ -239,24 +252,18 @@ void IceAgent::start_srflx() {
     }
     pending_gather_++;
     // Bound the whole srflx attempt (DNS included) so gathering can finish
-    // offline without waiting for the resolver.
-    auto done = std::make_shared<bool>(false);
-    r_.call_later_ms(cfg_.stun_timeout_ms, [w, done] {
-      if (*done) return;
-      *done = true;
-      if (auto s = w.lock()) {
-        s->pending_gather_--;
-        s->maybe_gathering_done();
-      }
+    // offline without waiting for the resolver; it closes earlier once every
+    // request to this server has been answered.
+    auto win = std::make_shared<SrflxWindow>();
+    r_.call_later_ms(cfg_.stun_timeout_ms, [w, win] {
+      if (auto s = w.lock()) s->srflx_window_done(win);
     });
-    resolve_async(r_, host, port, [w, done, url](std::vector<SockAddr> addrs, std::string err) {
+    resolve_async(r_, host, port, [w, win, url](std::vector<SockAddr> addrs, std::string err) {
       auto s = w.lock();
-      if (!s || *done) return;
+      if (!s || win->done) return;
       if (addrs.empty()) {
         LOG_DEBUG(kT, "STUN server %s unresolvable: %s", url.c_str(), err.c_str());
-        *done = true;
-        s->pending_gather_--;
-        s->maybe_gathering_done();
+        s->srflx_window_done(win);
         return;
       }
       for (int si = 0; si < int(s->socks_.size()); si++) {
@@ -264,18 +271,25 @@ void IceAgent::start_srflx() {
         for (auto& a : addrs) {
           if (a.family() != s->socks_[si].addr.family()) continue;
           auto m = stun::Message::make(stun::kBindingRequest);
-          SrflxReq rq{si, a, m.tid_key(), 1};
+          SrflxReq rq{si, a, m.tid_key(), 1, win};
           auto bytes = m.serialize(nullptr, true);
           s->send_raw(-1 - si, a, bytes.data(), bytes.size());
           s->srflx_.push_back(rq);
+          win->outstanding++;
           break;
         }
       }
-      // srflx responses are matched in handle_response; the timeout above
-      // closes the gathering window.
-      (void)done;
+      // Responses are matched in handle_response.
+      if (win->outstanding == 0) s->srflx_window_done(win);
     });
   }
+}
+
+void IceAgent::srflx_window_done(const std::shared_ptr<SrflxWindow>& win) {
+  if (win->done) return;
+  win->done = true;
+  pending_gather_--;
+  maybe_gathering_done();
 }
 
 void IceAgent::start_relay() {
@@ -540,7 +554,7 @@ void IceAgent::flush() {
       continue;
     }
     int si = li >= 0 ? locals_[li].sock : (-1 - li);
-    int fd = socks_[si].fd;
+    int fd = nat_mode_ ? nat_fd_for(si, outq_[i].to) : socks_[si].fd;
     int cnt = 0;
     size_t j = i;
     while (j < outq_.size() && cnt < kBatch) {
@@ -548,6 +562,7 @@ void IceAgent::flush() {
       if (lj >= 0 && locals_[lj].relay) break;
       int sj = lj >= 0 ? locals_[lj].sock : (-1 - lj);
       if (sj != si) break;
+      if (nat_mode_ && nat_fd_for(sj, outq_[j].to) != fd) break;
       memset(&msgs[cnt], 0, sizeof msgs[cnt]);
       iovs[cnt].iov_base = outq_[j].data.data();
       iovs[cnt].iov_len = outq_[j].data.size();
@@ -602,18 +617,75 @@ void IceAgent::on_readable(int si) {
     int n = recvmmsg(socks_[si].fd, msgs, kBatch, MSG_DONTWAIT, nullptr);
     if (n <= 0) return;
     for (int i = 0; i < n && !closed_; i++) {
+      if (nat_mode_) {  // private address: unreachable from outside the emulated NAT
+        nat_dropped_++;
+        continue;
+      }
       SockAddr a;
       memcpy(&a.ss, &from[i], msgs[i].msg_hdr.msg_namelen);
       a.len = msgs[i].msg_hdr.msg_namelen;
-      const uint8_t* p = rxpool_[i]->data.get();
-      size_t len = msgs[i].msg_len;
-      if (turn_ && turn_->is_server(si, a)) {
-        turn_->on_packet(p, len);
-        continue;
-      }
-      handle_datagram(-1, si, a, p, len, false, rxpool_[i]);
+      dispatch_rx(si, a, rxpool_[i], msgs[i].msg_len);
     }
     if (n < kBatch) return;
+  }
+}
+
+void IceAgent::dispatch_rx(int si, const SockAddr& a, const RawBufPtr& owner, size_t len) {
+  const uint8_t* p = owner->data.get();
+  if (turn_ && turn_->is_server(si, a)) {
+    turn_->on_packet(p, len);
+    return;
+  }
+  handle_datagram(-1, si, a, p, len, false, owner);
+}
+
+int IceAgent::nat_fd_for(int si, const SockAddr& to) {
+  std::string key = std::to_string(si);
+  if (nat_mode_ == 2) key += "|" + to.str();
+  auto it = nat_map_.find(key);
+  int pi;
+  if (it != nat_map_.end()) {
+    pi = it->second;
+  } else {
+    NatPort np;
+    np.si = si;
+    np.fd = ::socket(socks_[si].addr.family(), SOCK_DGRAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+    SockAddr a = socks_[si].addr;
+    a.set_port(0);
+    int buf = 4 << 20;
+    setsockopt(np.fd, SOL_SOCKET, SO_RCVBUF, &buf, sizeof buf);
+    setsockopt(np.fd, SOL_SOCKET, SO_SNDBUF, &buf, sizeof buf);
+    if (np.fd < 0 || ::bind(np.fd, a.sa(), a.len) < 0) return socks_[si].fd;
+    np.ext.len = sizeof np.ext.ss;
+    getsockname(np.fd, np.ext.sa(), &np.ext.len);
+    pi = int(nat_ports_.size());
+    nat_ports_.push_back(np);
+    nat_map_[key] = pi;
+    std::weak_ptr<IceAgent> w = shared_from_this();
+    r_.add(np.fd, EPOLLIN, [w, pi](uint32_t) {
+      if (auto self = w.lock()) self->on_nat_readable(pi);
+    });
+    LOG_DEBUG(kT, "NAT emulation: %s -> external %s%s", socks_[si].addr.str().c_str(), np.ext.str().c_str(),
+              nat_mode_ == 2 ? (" for " + to.str()).c_str() : "");
+  }
+  nat_ports_[pi].sent.insert(to.str());
+  return nat_ports_[pi].fd;
+}
+
+void IceAgent::on_nat_readable(int pi) {
+  if (closed_) return;
+  auto self = shared_from_this();
+  for (int round = 0; round < 64 && !closed_; round++) {
+    if (!rxpool_[0] || rxpool_[0].use_count() > 1) rxpool_[0] = std::make_shared<RawBuf>(65536);
+    SockAddr a;
+    a.len = sizeof a.ss;
+    ssize_t n = recvfrom(nat_ports_[pi].fd, rxpool_[0]->data.get(), 65536, MSG_DONTWAIT, a.sa(), &a.len);
+    if (n < 0) return;
+    if (!nat_ports_[pi].sent.count(a.str())) {  // address+port-dependent filtering
+      nat_dropped_++;
+      continue;
+    }
+    dispatch_rx(nat_ports_[pi].si, a, rxpool_[0], size_t(n));
   }
 }
 
@@ -762,7 +834,9 @@ void IceAgent::handle_response(const SockAddr& from, const stun::Message& m, con
         add_local(c, si, false);
       }
     }
+    auto win = srflx_[i].win;
     srflx_.erase(srflx_.begin() + long(i));
+    if (win && --win->outstanding == 0) srflx_window_done(win);
     return;
   }
   auto it = tx_pairs_.find(tid);

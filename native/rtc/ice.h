@@ -17,6 +17,7 @@
 #include <deque>
 #include <functional>
 #include <map>
+#include <set>
 #include <memory>
 #include <string>
 #include <vector>
@@ -159,12 +160,25 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   IceAgent(Reactor& r, IceConfig cfg, bool controlling);
   void open_sockets();
   void on_readable(int si);
+  void dispatch_rx(int si, const SockAddr& from, const RawBufPtr& owner, size_t len);
+  // Test-only NAT emulation (TUNNEL_NAT=port-restricted|symmetric; SURVEY
+  // §4.2, BASELINE config #4 without two real NATs). Every datagram leaves
+  // through an emulated external socket: one per host socket (endpoint-
+  // independent mapping) or one per destination (symmetric). Inbound traffic
+  // is accepted only on external sockets and only from destinations that
+  // socket has sent to (address+port-dependent filtering); the private host
+  // sockets drop everything. STUN servers therefore see the external address
+  // (a real srflx candidate), and peers must hole-punch or relay.
+  int nat_fd_for(int si, const SockAddr& to);
+  void on_nat_readable(int pi);
   void handle_datagram(int local_idx_hint, int si, const SockAddr& from, const uint8_t* p, size_t n, bool via_relay,
                        const RawBufPtr& owner = nullptr);
   void handle_stun(int si, const SockAddr& from, const uint8_t* p, size_t n, bool via_relay);
   void handle_request(int si, const SockAddr& from, const stun::Message& m, const uint8_t* p, size_t n, bool via_relay);
   void handle_response(const SockAddr& from, const stun::Message& m, const uint8_t* p, size_t n);
   void start_srflx();
+  struct SrflxWindow;
+  void srflx_window_done(const std::shared_ptr<SrflxWindow>& win);
   void start_relay();
   void maybe_gathering_done();
   void add_local(Candidate c, int sock, bool relay);
@@ -191,11 +205,16 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   std::vector<Candidate> remotes_;
   std::vector<Pair> pairs_;
   std::map<std::string, int> tx_pairs_;  // STUN tid -> pair index
+  struct SrflxWindow {  // one STUN server's gathering window
+    bool done = false;
+    int outstanding = 0;
+  };
   struct SrflxReq {
     int sock;
     SockAddr server;
     std::string tid;
     int tries = 0;
+    std::shared_ptr<SrflxWindow> win;
   };
   std::vector<SrflxReq> srflx_;
   int pending_gather_ = 0;
@@ -221,6 +240,16 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
     bool coalesce = false; // more records may be appended
   };
   std::vector<Out> outq_;
+  struct NatPort {
+    int fd = -1;
+    int si = -1;                   // host socket it translates for
+    SockAddr ext;                  // external (mapped) address
+    std::set<std::string> sent;    // destinations sent to (filter)
+  };
+  int nat_mode_ = 0;               // 0 off, 1 port-restricted cone, 2 symmetric
+  std::vector<NatPort> nat_ports_;
+  std::map<std::string, int> nat_map_;  // "si|dest" (symmetric) or "si" -> nat_ports_ index
+  uint64_t nat_dropped_ = 0;
   std::vector<DgVec> spare_;        // recycled datagram buffers
   size_t coalesce_limit_ = 0;
   size_t append_at_ = 0;

@@ -75,7 +75,7 @@ class TurnServer:
         self.port = self.sock.getsockname()[1]
         self.allocs = {}     # client addr -> dict(relay=sock, perms=set(ip), chans={num: peer}, peers={peer: num})
         self.by_relay = {}   # relay sock -> client addr
-        self.stats = {"allocations": 0, "relayed_to_peer": 0, "relayed_to_client": 0, "channel_binds": 0}
+        self.stats = {"bindings": 0, "allocations": 0, "relayed_to_peer": 0, "relayed_to_client": 0, "channel_binds": 0}
         self._stop = False
         self.thread = threading.Thread(target=self._run, daemon=True)
 
@@ -134,6 +134,7 @@ class TurnServer:
         if t & 0x0110:  # not a request
             return
         if method == 0x0001:  # Binding
+            self.stats["bindings"] += 1
             self.sock.sendto(build(0x0101, tid, [(0x0020, xor_addr(*addr))]), addr)
             return
         if not self._auth_ok(data, attrs, mi_off):
