@@ -470,20 +470,33 @@ void IceAgent::send(const uint8_t* p, size_t n) {
 
 // Test-only fault injection on the datagram path (SURVEY §4.2 "fault
 // injection"): TUNNEL_FAULT_DROP / TUNNEL_FAULT_DUP are probabilities,
-// TUNNEL_FAULT_DELAY_MS a uniform random extra delay (which also reorders).
-// STUN (connectivity checks) is exempt so the path still comes up.
+// TUNNEL_FAULT_DELAY_MS a uniform random extra delay (which also reorders);
+// STUN (connectivity checks) is exempt from those so the path still comes up.
+// TUNNEL_FAULT_BLACKHOLE=<start_ms>:<duration_ms> drops every outbound
+// datagram, STUN included, in that window after the first send (a path that
+// dies and later comes back).
 namespace {
 struct FaultCfg {
   double drop = 0, dup = 0;
   uint64_t delay_us = 0;
+  uint64_t bh_start_ms = 0, bh_len_ms = 0, t0_ms = 0;
   bool on = false;
   uint64_t rng = 0x9E3779B97F4A7C15ull;
   FaultCfg() {
     if (const char* e = getenv("TUNNEL_FAULT_DROP")) drop = atof(e);
     if (const char* e = getenv("TUNNEL_FAULT_DUP")) dup = atof(e);
     if (const char* e = getenv("TUNNEL_FAULT_DELAY_MS")) delay_us = uint64_t(atof(e) * 1000);
-    on = drop > 0 || dup > 0 || delay_us > 0;
+    if (const char* e = getenv("TUNNEL_FAULT_BLACKHOLE")) {
+      bh_start_ms = strtoull(e, nullptr, 10);
+      if (const char* c = strchr(e, ':')) bh_len_ms = strtoull(c + 1, nullptr, 10);
+    }
+    t0_ms = Reactor::now_ms();
+    on = drop > 0 || dup > 0 || delay_us > 0 || bh_len_ms > 0;
     rng ^= uint64_t(getpid()) << 20;
+  }
+  bool blackholed() const {
+    uint64_t t = Reactor::now_ms() - t0_ms;
+    return bh_len_ms && t >= bh_start_ms && t < bh_start_ms + bh_len_ms;
   }
   double uni() {
     rng ^= rng << 13;
@@ -512,6 +525,7 @@ void IceAgent::flush() {
   } recycle{this};
   if (outq_.empty() || closed_) return;
   if (fault().on) {
+    if (fault().blackholed()) return;
     std::vector<Out> keep;
     for (auto& o : outq_) {
       if (o.faulted || stun::looks_like_stun(o.data.data(), o.data.size()) || o.local < 0) {
