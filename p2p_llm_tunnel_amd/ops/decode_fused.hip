@@ -41,6 +41,9 @@
 // materialised (rounding differs at the bf16-ulp level); fp32 accumulation.
 #include "bf16_common.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace {
 
 using namespace p2pt_gpu;
@@ -75,9 +78,22 @@ struct GemmArgs {
   float log2_theta;
   float* am_val;  // ARGMAX: [gridDim.x][16]
   int* am_idx;
+  // Split-K over workgroups (ks > 1): the ks workgroups of a column tile each
+  // reduce a K range, publish a 16 x 16*TN fp32 slab write-through, and the
+  // last to arrive sums the slabs in fixed order (deterministic) and runs the
+  // epilogue. Small-N projections (N = d_model) otherwise leave CUs idle.
+  int ks;
+  float* kpart;     // [tiles][ks][TN][4][64]
+  unsigned* kctr;   // [tiles] arrival tickets (self-resetting)
 };
 
 __device__ __forceinline__ frag8 as_frag(const uint4& v) { return __builtin_bit_cast(frag8, v); }
+
+// Weights use the default cache policy on purpose: a decode step replays the
+// same weights back to back, and models up to the 256 MB MALL keep them
+// resident between steps (non-temporal loads measured 1.75x slower on the
+// 4-layer config, and no faster on the 0.85 GB one).
+__device__ __forceinline__ uint4 ld_stream(const uint16_t* p) { return *reinterpret_cast<const uint4*>(p); }
 
 // Cross-workgroup hand-off without L2 write-back/invalidate fences: payload
 // stores are agent-scope relaxed atomics (write-through, `sc1`), drained with
@@ -116,7 +132,7 @@ __device__ __forceinline__ void mma_batch(frag4 (&acc)[TN], const uint16_t* xrow
   for (int u = 0; u < UM; u++) {
     const int su = min(s + u, s1 - 1) * 32;
 #pragma unroll
-    for (int t = 0; t < TN; t++) bv[u][t] = *reinterpret_cast<const uint4*>(wrow[t] + su);
+    for (int t = 0; t < TN; t++) bv[u][t] = ld_stream(wrow[t] + su);
   }
 #pragma unroll
   for (int u = 0; u < UM; u++) {
@@ -139,7 +155,8 @@ template <int NW, int TN, int EPI, int UM>
 __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
   __shared__ float red[NW][TN][4][kWave];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int bx = blockIdx.x;
+  const int bx = blockIdx.x / a.ks;  // column tile
+  const int kslice = blockIdx.x % a.ks;
   const bool norm = a.ss_part != nullptr;
 
   // Row sums of squares (wave 0 only; it runs the epilogue): lane holds row
@@ -156,7 +173,8 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
   const bool a_ok = m_a < a.M;
   const int kq = (lane >> 4) << 3;
   const int S = a.K >> 5;
-  const int s0 = wv * S / NW, s1 = (wv + 1) * S / NW;
+  const int b0 = kslice * S / a.ks, bs = (kslice + 1) * S / a.ks - b0;  // this workgroup's k-steps
+  const int s0 = b0 + wv * bs / NW, s1 = b0 + (wv + 1) * bs / NW;
   // Rows past M are loaded from row M-1 (in bounds) and zeroed: the batch's
   // loads are unconditional.
   const uint16_t* xrow = a.x + size_t(min(m_a, a.M - 1)) * a.K + kq;
@@ -186,6 +204,27 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
       for (int w = 0; w < NW; w++) sum += red[w][t][r][lane];
       v[t][r] = sum;
     }
+  if (a.ks > 1) {
+    float* slab = a.kpart + size_t(bx) * a.ks * (TN * 4 * kWave);
+#pragma unroll
+    for (int t = 0; t < TN; t++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) st_wt(slab + size_t(kslice) * (TN * 4 * kWave) + (t * 4 + r) * kWave + lane, v[t][r]);
+    drain_stores();
+    unsigned tk = 0;
+    if (lane == 0) tk = arrive(&a.kctr[bx]);
+    tk = __shfl(tk, 0, kWave);
+    if (tk != unsigned(a.ks - 1)) return;
+#pragma unroll
+    for (int t = 0; t < TN; t++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        float sum = 0.f;
+        for (int j = 0; j < a.ks; j++) sum += ld_wt(slab + size_t(j) * (TN * 4 * kWave) + (t * 4 + r) * kWave + lane);
+        v[t][r] = sum;
+      }
+    if (lane == 0) st_wt(&a.kctr[bx], 0u);
+  }
 
   // C layout: row m = 4*(lane>>4) + r, column = tile_col(.., lane & 15).
   const int mrow0 = (lane >> 4) << 2;
@@ -382,187 +421,231 @@ __global__ __launch_bounds__(256) void k_embed(const uint16_t* __restrict__ embe
 }
 
 // ------------------------------------------------------------ attention
-// As k_decode_attn in kernels.hip (split-K over `chunk`-token pieces, K/V tiles
-// in LDS shared by the GQA group, one wave per query head; all TPB tiles of a
-// piece are loaded in one pass, so a workgroup makes one memory round trip),
-// plus: row b reads
-// cache slot slot[b] (several rows may share a slot: chunked prefill), lens = pos + 1,
-// and the last split to finish for a (sequence, KV head) merges the partials
-// (arrival ticket, self-resetting) and writes the bf16 output [B][H*D].
-template <int D, int TPB>
-__global__ __launch_bounds__(512) void k_attn(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+// GQA flash-decoding. A workgroup owns a (row b, KV head, 256-token chunk);
+// each of its 4 waves takes a 64-token piece and loads all of it straight
+// into registers with 16-byte loads whose lanes tile whole K/V rows (D/8 lanes
+// per row, so every instruction reads full cache lines), so a piece's bytes
+// are in flight at once and never staged through LDS. A lane keeps one 8-dim
+// group of every query head of the KV head (K/V are read once per GQA group),
+// finishes its dot products with in-row xor shuffles, and ends up holding the
+// softmax weights of exactly the tokens whose V it loaded: P.V needs no data
+// exchange until the final cross-row sum. Scores and P.V are fp32 VALU FMAs:
+// with G <= 8 query rows an MFMA tile would be >= half padding, and the
+// kernel is bound by the K/V stream and by latency, not arithmetic.
+// Merges are latency, so they are kept off the global round-trip path where
+// possible: the 4 pieces of a chunk merge through LDS; only contexts longer
+// than one chunk publish a per-chunk partial (write-through + arrival ticket)
+// and the last chunk to finish merges them, its waves taking different heads
+// and issuing every partial load of a head before the first use.
+// Row b reads cache slot slot[b] (rows may share a slot: chunked prefill) and
+// attends to positions 0..pos[b]; the output is bf16 [B][H*D].
+template <int D, int G>
+__global__ __launch_bounds__(256) void k_attn(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
                                               const uint16_t* __restrict__ vc, const int* __restrict__ pos,
-                                              const int* __restrict__ slot, int nslots,
-                                              float* __restrict__ part_o, float* __restrict__ part_ml,
-                                              unsigned* __restrict__ counters, uint16_t* __restrict__ out, int H,
-                                              int Hkv, int Smax, int chunk, int nsplit, float scale) {
-  constexpr int TILE = 64;
-  constexpr int ROWB = D * 2 + 16;
-  constexpr int DPL = D / kWave;
-  __shared__ __attribute__((aligned(16))) uint8_t ks[TPB * TILE * ROWB];
-  __shared__ __attribute__((aligned(16))) uint8_t vs[TPB * TILE * ROWB];
+                                              const int* __restrict__ slot, int nslots, float* __restrict__ part_o,
+                                              float* __restrict__ part_ml, unsigned* __restrict__ counters,
+                                              uint16_t* __restrict__ out, int H, int Hkv, int Smax, int nsplit,
+                                              float scale) {
+  constexpr int TOK = 64, NWV = 4, CHUNK = TOK * NWV;
+  constexpr int DPL = D / kWave;  // merges: dims per lane
+  constexpr int MAXC = 16;        // chunks merged per load batch
+  __shared__ __attribute__((aligned(16))) float pacc[NWV][G][D];
+  __shared__ float pml[NWV][G][2];
   __shared__ unsigned s_ticket;
-  __shared__ __attribute__((aligned(16))) float ps[8][TILE];  // softmax weights, one row per wave
 
-  const int split = blockIdx.x;
+  const int chunk = blockIdx.x;
   const int b = blockIdx.y / Hkv, kvh = blockIdx.y % Hkv;
-  const int G = H / Hkv;
   const int len = min(max(pos[b], 0), Smax - 1) + 1;
-  const int sb = slot ? min(max(slot[b], 0), nslots - 1) : b;  // cache slot of row b
-  const int g = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int start = split * chunk;
-  const int stop = min(start + chunk, len);
-  const int used = min(nsplit, (len + chunk - 1) / chunk);
-  if (start >= len) return;
-
-  float qf[D];
-  {
-    const uint16_t* qp = q + (size_t(b) * H + kvh * G + g) * D;
-#pragma unroll
-    for (int d = 0; d < D; d += 8) {
-      float f[8];
-      unpack8(*reinterpret_cast<const uint4*>(qp + d), f);
-#pragma unroll
-      for (int k = 0; k < 8; k++) qf[d + k] = f[k] * scale;
-    }
-  }
-  float m = -INFINITY, l = 0.f, acc[DPL];
-#pragma unroll
-  for (int k = 0; k < DPL; k++) acc[k] = 0.f;
+  if (chunk * CHUNK >= len) return;
+  const int nchunks = (len + CHUNK - 1) / CHUNK;
+  const int sb = slot ? min(max(slot[b], 0), nslots - 1) : b;
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int start = chunk * CHUNK + wv * TOK;
+  const int ntok = max(0, min(TOK, len - start));  // 0: this wave's piece is past the end
 
   const size_t tok_stride = size_t(Hkv) * D;
-  const uint16_t* kbase = kc + (size_t(sb) * Smax) * tok_stride + size_t(kvh) * D;
-  const uint16_t* vbase = vc + (size_t(sb) * Smax) * tok_stride + size_t(kvh) * D;
+  const int t_last = max(ntok - 1, 0);
+  const uint16_t* kbase = kc + (size_t(sb) * Smax + min(start, len - 1)) * tok_stride + size_t(kvh) * D;
+  const uint16_t* vbase = vc + (size_t(sb) * Smax + min(start, len - 1)) * tok_stride + size_t(kvh) * D;
 
-  // Cooperative 16-byte loads of every K and V row of this piece into LDS.
-  constexpr int VPR = D / 8;  // uint4 per row
-  const int ntok = stop - start;
-  const int nthr = blockDim.x;
-  constexpr int PER = TPB * TILE * VPR;
-  for (int e0 = threadIdx.x; e0 < PER; e0 += 4 * nthr) {
-    uint4 kv[4], vv[4];
+  // Lane layout for K and V alike: LPR lanes cover one D-wide row with 16-byte
+  // loads (dim group dg = 8 dims), so one instruction reads RPI whole rows
+  // (contiguous 128/256-byte runs: full cache lines) and NI instructions cover
+  // the piece. Lanes past the end re-read the last valid row (in bounds).
+  constexpr int LPR = D / 8, RPI = kWave / LPR, NI = TOK / RPI;
+  const int dg = lane % LPR, ri = lane / LPR;
+  uint4 kr[NI], vr[NI];
 #pragma unroll
-    for (int i = 0; i < 4; i++) {  // all loads of the batch in flight before the LDS stores
-      const int e = e0 + i * nthr, t = e / VPR, cc = e % VPR;
-      kv[i] = vv[i] = make_uint4(0, 0, 0, 0);
-      if (e < PER && t < ntok) {
-        kv[i] = *reinterpret_cast<const uint4*>(kbase + size_t(start + t) * tok_stride + cc * 8);
-        vv[i] = *reinterpret_cast<const uint4*>(vbase + size_t(start + t) * tok_stride + cc * 8);
-      }
+  for (int j = 0; j < NI; j++) {
+    const size_t t = size_t(min(j * RPI + ri, t_last));
+    kr[j] = *reinterpret_cast<const uint4*>(kbase + t * tok_stride + 8 * dg);
+  }
+#pragma unroll
+  for (int j = 0; j < NI; j++) {
+    const size_t t = size_t(min(j * RPI + ri, t_last));
+    vr[j] = *reinterpret_cast<const uint4*>(vbase + t * tok_stride + 8 * dg);
+  }
+  // This lane's 8 query dims of every head, pre-scaled.
+  float qf[G][8];
+  {
+    const uint16_t* qp = q + (size_t(b) * H + size_t(kvh) * G) * D + 8 * dg;
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+      unpack8(*reinterpret_cast<const uint4*>(qp + size_t(g) * D), qf[g]);
+#pragma unroll
+      for (int k = 0; k < 8; k++) qf[g][k] *= scale;
+    }
+  }
+
+  // Scores: partial dots over the lane's 8 dims, summed across the LPR lanes
+  // of the row (DPP-able xor shuffles inside 8/16-lane rows). Every lane of a
+  // row ends up with the row's score: lane (ri, dg) holds token j*RPI + ri.
+  float sc[G][NI];
+#pragma unroll
+  for (int j = 0; j < NI; j++) {
+    float f[8];
+    unpack8(kr[j], f);
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+      float d = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; k++) d += qf[g][k] * f[k];
+#pragma unroll
+      for (int o = 1; o < LPR; o <<= 1) d += __shfl_xor(d, o, kWave);
+      sc[g][j] = (j * RPI + ri < ntok) ? d : -INFINITY;
+    }
+  }
+  // Softmax statistics per head: max/sum over the lane's tokens, then across
+  // rows (lanes differing in ri; lanes of one row hold the same values).
+  float mg[G], lg[G];
+#pragma unroll
+  for (int g = 0; g < G; g++) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < NI; j++) m = fmaxf(m, sc[g][j]);
+#pragma unroll
+    for (int o = LPR; o < kWave; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, kWave));
+    mg[g] = m;
+    float l = 0.f;
+#pragma unroll
+    for (int j = 0; j < NI; j++) {
+      sc[g][j] = ntok ? __expf(sc[g][j] - m) : 0.f;  // now p
+      l += sc[g][j];
     }
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const int e = e0 + i * nthr, t = e / VPR, cc = e % VPR;
-      if (e < PER) {
-        *reinterpret_cast<uint4*>(ks + t * ROWB + cc * 16) = kv[i];
-        *reinterpret_cast<uint4*>(vs + t * ROWB + cc * 16) = vv[i];
-      }
+    for (int o = LPR; o < kWave; o <<= 1) l += __shfl_xor(l, o, kWave);
+    lg[g] = l;
+  }
+  // P.V: the lane's own tokens times its 8 dims, then summed across rows.
+  float acc[G][8];
+#pragma unroll
+  for (int g = 0; g < G; g++)
+#pragma unroll
+    for (int k = 0; k < 8; k++) acc[g][k] = 0.f;
+#pragma unroll
+  for (int j = 0; j < NI; j++) {
+    float f[8];
+    unpack8(vr[j], f);
+#pragma unroll
+    for (int g = 0; g < G; g++)
+#pragma unroll
+      for (int k = 0; k < 8; k++) acc[g][k] += sc[g][j] * f[k];
+  }
+#pragma unroll
+  for (int g = 0; g < G; g++)
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+#pragma unroll
+      for (int o = LPR; o < kWave; o <<= 1) acc[g][k] += __shfl_xor(acc[g][k], o, kWave);
+  // Publish this piece to the workgroup (empty pieces: m = -inf, l = 0).
+  if (ri == 0) {
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+      *reinterpret_cast<float4*>(&pacc[wv][g][8 * dg]) = make_float4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
+      *reinterpret_cast<float4*>(&pacc[wv][g][8 * dg + 4]) = make_float4(acc[g][4], acc[g][5], acc[g][6], acc[g][7]);
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+      pml[wv][g][0] = ntok ? mg[g] : -INFINITY;
+      pml[wv][g][1] = ntok ? lg[g] : 0.f;
     }
   }
   __syncthreads();
-  for (int t0 = 0; t0 < ntok; t0 += TILE) {
-    const int nt = min(TILE, ntok - t0);
-    // Scores: lane = token.
-    float s = -INFINITY;
-    if (lane < nt) {
-      float dot = 0.f;
+
+  // Chunk merge through LDS: wave w takes heads w, w + 4, ...
+  const size_t hb0 = size_t(b) * H + size_t(kvh) * G;
+  for (int g = wv; g < G; g += NWV) {
+    float M = -INFINITY;
 #pragma unroll
-      for (int d = 0; d < D; d += 8) {
-        float f[8];
-        unpack8(*reinterpret_cast<const uint4*>(ks + (t0 + lane) * ROWB + d * 2), f);
+    for (int w = 0; w < NWV; w++) M = fmaxf(M, pml[w][g][0]);
+    float L = 0.f, o[DPL];
 #pragma unroll
-        for (int k = 0; k < 8; k++) dot += qf[d + k] * f[k];
-      }
-      s = dot;
+    for (int k = 0; k < DPL; k++) o[k] = 0.f;
+#pragma unroll
+    for (int w = 0; w < NWV; w++) {
+      const float ww = pml[w][g][1] > 0.f ? __expf(pml[w][g][0] - M) : 0.f;
+      L += pml[w][g][1] * ww;
+#pragma unroll
+      for (int k = 0; k < DPL; k++) o[k] += ww * pacc[w][g][lane + k * kWave];
     }
-    const float mnew = fmaxf(m, wave_max(s));
-    const float p = (lane < nt) ? __expf(s - mnew) : 0.f;
-    const float corr = __expf(m - mnew);
-    l = l * corr + wave_sum(p);
-    m = mnew;
+    const size_t hb = hb0 + g;
+    if (nchunks == 1) {
+      const float inv = 1.f / L;
 #pragma unroll
-    for (int k = 0; k < DPL; k++) acc[k] *= corr;
-    // P.V: lane = head dim. p goes through this wave's LDS row and is read back
-    // as broadcast float4s; the loop always covers the full tile (p = 0 and V
-    // rows zero-filled past the end) so it unrolls into independent LDS reads
-    // instead of a serial shuffle-per-token chain.
-    ps[g][lane] = p;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll 2
-    for (int t = 0; t < TILE; t += 8) {
-      const float4 pa = *reinterpret_cast<const float4*>(&ps[g][t]);
-      const float4 pb = *reinterpret_cast<const float4*>(&ps[g][t + 4]);
-      const float pt[8] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
+      for (int k = 0; k < DPL; k++) out[hb * D + lane + k * kWave] = uint16_t(f2bf_bits(o[k] * inv));
+    } else {
+      float* po = part_o + (hb * nsplit + chunk) * D;
 #pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const uint16_t* vrow = reinterpret_cast<const uint16_t*>(vs + (t0 + t + j) * ROWB);
-#pragma unroll
-        for (int k = 0; k < DPL; k++) acc[k] += pt[j] * bf2f(vrow[lane + k * kWave]);
+      for (int k = 0; k < DPL; k++) st_wt(po + lane + k * kWave, o[k]);
+      if (lane == 0) {
+        st_wt(part_ml + (hb * nsplit + chunk) * 2 + 0, M);
+        st_wt(part_ml + (hb * nsplit + chunk) * 2 + 1, L);
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
   }
-  const size_t hb = size_t(b) * H + kvh * G + g;
-  if (used == 1) {  // single split: finish directly
-    const float inv = 1.f / l;
-#pragma unroll
-    for (int k = 0; k < DPL; k++) out[hb * D + lane + k * kWave] = uint16_t(f2bf_bits(acc[k] * inv));
-    return;
-  }
-  {
-    float* po = part_o + (hb * nsplit + split) * D;
-#pragma unroll
-    for (int k = 0; k < DPL; k++) st_wt(po + lane + k * kWave, acc[k]);
-    if (lane == 0) {
-      st_wt(part_ml + (hb * nsplit + split) * 2 + 0, m);
-      st_wt(part_ml + (hb * nsplit + split) * 2 + 1, l);
-    }
-  }
+  if (nchunks == 1) return;
   drain_stores();
   __syncthreads();
   if (threadIdx.x == 0) s_ticket = arrive(&counters[blockIdx.y]);
   __syncthreads();
-  if (s_ticket != unsigned(used - 1)) return;
-  // Merge: lanes over splits for the max / weights, lanes over head dims for the output.
-  const float* ml = part_ml + hb * nsplit * 2;
-  float M = -INFINITY;
-  for (int s = lane; s < used; s += kWave) M = fmaxf(M, ld_wt(ml + 2 * s));
-  M = wave_max(M);
-  float L = 0.f, o[DPL];
+  if (s_ticket != unsigned(nchunks - 1)) return;
+
+  // Last chunk: merge the chunk partials, heads spread over the waves; each
+  // batch of up to MAXC chunks is loaded before any of it is used.
+  for (int g = wv; g < G; g += NWV) {
+    const size_t hb = hb0 + g;
+    const float* ml = part_ml + hb * nsplit * 2;
+    float M = -INFINITY;
+    for (int c = lane; c < nchunks; c += kWave) M = fmaxf(M, ld_wt(ml + 2 * c));
+    M = wave_max(M);
+    float L = 0.f, o[DPL];
 #pragma unroll
-  for (int k = 0; k < DPL; k++) o[k] = 0.f;
-  for (int s0 = 0; s0 < used; s0 += kWave) {
-    const int s = s0 + lane;
-    float ws = 0.f;
-    if (s < used) {
-      ws = __expf(ld_wt(ml + 2 * s) - M);
-      L += ld_wt(ml + 2 * s + 1) * ws;
-    }
-    const int n = min(kWave, used - s0);
-    const float* pob = part_o + (hb * nsplit + s0) * D + lane;
-    // 16 splits' partials in flight at once (one wait per group, not per split).
-    for (int j0 = 0; j0 < n; j0 += 16) {
-      float pv[16][DPL];
+    for (int k = 0; k < DPL; k++) o[k] = 0.f;
+    for (int c0 = 0; c0 < nchunks; c0 += MAXC) {
+      float pv[MAXC][DPL], wl[MAXC], ll[MAXC];
 #pragma unroll
-      for (int jj = 0; jj < 16; jj++)
+      for (int j = 0; j < MAXC; j++) {
+        const bool ok = c0 + j < nchunks;
+        const int c = min(c0 + j, nchunks - 1);
+        wl[j] = ld_wt(ml + 2 * c);
+        ll[j] = ok ? ld_wt(ml + 2 * c + 1) : 0.f;
 #pragma unroll
-        for (int k = 0; k < DPL; k++) pv[jj][k] = j0 + jj < n ? ld_wt(pob + size_t(j0 + jj) * D + k * kWave) : 0.f;
+        for (int k = 0; k < DPL; k++) pv[j][k] = ld_wt(part_o + (hb * nsplit + c) * D + lane + k * kWave);
+      }
 #pragma unroll
-      for (int jj = 0; jj < 16; jj++) {
-        const float wj = __shfl(ws, (j0 + jj) & 63, kWave);
+      for (int j = 0; j < MAXC; j++) {
+        const float ww = ll[j] > 0.f ? __expf(wl[j] - M) : 0.f;
+        L += ll[j] * ww;
 #pragma unroll
-        for (int k = 0; k < DPL; k++) o[k] += wj * pv[jj][k];
+        for (int k = 0; k < DPL; k++) o[k] += ww * pv[j][k];
       }
     }
-  }
-  L = wave_sum(L);
-  const float inv = 1.f / L;
+    const float inv = 1.f / L;
 #pragma unroll
-  for (int k = 0; k < DPL; k++) out[hb * D + lane + k * kWave] = uint16_t(f2bf_bits(o[k] * inv));
-  __syncthreads();
+    for (int k = 0; k < DPL; k++) out[hb * D + lane + k * kWave] = uint16_t(f2bf_bits(o[k] * inv));
+  }
   if (threadIdx.x == 0) st_wt(&counters[blockIdx.y], 0u);
 }
 
@@ -572,9 +655,9 @@ struct LlamaDims {
   float eps, theta;
 };
 
-constexpr int kChunk = 64;     // workspace granularity of attention partials
-constexpr int kAttnTok = 128;  // tokens per attention workgroup (2 tiles, one load pass)
+constexpr int kChunk = 64;  // tokens per attention workgroup = workspace granularity of its partials
 constexpr int kTnResid = 1, kTnStore = 1;
+constexpr int kMaxKs = 8;    // split-K ways over workgroups
 
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -583,6 +666,8 @@ struct Workspace {
   float *ss, *part_o, *part_ml, *am_val;
   int* am_idx;
   unsigned* counters;  // [16 * H] attention split tickets (self-resetting)
+  float* kpart;        // split-K slabs of the widest split GEMM
+  unsigned* kctr;      // split-K tickets per column tile (self-resetting)
   size_t bytes;
 };
 
@@ -607,15 +692,38 @@ Workspace carve(const LlamaDims& d, uint8_t* base) {
   w.am_val = reinterpret_cast<float*>(take(size_t(am_parts) * kMaxM * 4));
   w.am_idx = reinterpret_cast<int*>(take(size_t(am_parts) * kMaxM * 4));
   w.counters = reinterpret_cast<unsigned*>(take(size_t(kMaxM * d.H) * 4));
+  const int qkv_n = (d.H + 2 * d.Hkv) * d.D;
+  const int max_n = std::max(std::max(qkv_n, d.dim), 2 * d.ffn);
+  w.kpart = reinterpret_cast<float*>(take(size_t(max_n / 16) * kMaxKs * 4 * kWave * 4));
+  w.kctr = reinterpret_cast<unsigned*>(take(size_t(max_n / 16) * 4));
   w.bytes = off;
   return w;
 }
 
-// Waves per workgroup: enough that each wave streams at most ~8 k-steps of
-// 32 (one round trip of loads), capped at 16 (1024 threads).
-int pick_nw(int K) {
-  if (K <= 0 || K % 32) return 0;
-  return (K >> 5) <= 64 ? 8 : 16;
+// Waves per workgroup for `steps` 32-wide k-steps per workgroup: enough that
+// each wave streams at most ~8 k-steps (one round trip of loads), capped at
+// 16 (1024 threads).
+int pick_nw(int steps) {
+  if (steps <= 0) return 0;
+  return steps <= 16 ? 4 : steps <= 64 ? 8 : 16;
+}
+
+// Split-K ways. Off by default: on MI355X the seam (write-through slabs,
+// drain, arrival ticket, slab reads by the last arriver) costs more latency
+// than the extra workgroups win back at d_model <= 2048 (QKV 8.7 -> 13.5 us,
+// O 7.4 -> 12.0 us, down 17.3 -> 17.3 us on the 2048-wide config, batch 8).
+// P2PT_DECODE_SPLITK=1 enables it (grid grown toward 512 workgroups while
+// every workgroup keeps >= 8 k-steps) for wider models / experiments.
+int pick_ks(int tiles, int K) {
+  static const bool on = [] {
+    const char* e = getenv("P2PT_DECODE_SPLITK");
+    return e && *e == '1';
+  }();
+  if (!on) return 1;
+  const int S = K >> 5;
+  int ks = 1;
+  while (ks < kMaxKs && tiles * ks < 512 && S / (ks * 2) >= 8) ks *= 2;
+  return ks;
 }
 
 template <int NW, int TN, int EPI>
@@ -623,8 +731,8 @@ hipError_t launch_nw(const GemmArgs& a, int grid, hipStream_t s) {
   // Load batch: each wave's share of k-steps, rounded up to a power of two,
   // capped by the VGPR budget (8, or 4 for 1024-thread two-subtile blocks).
   constexpr int kCap = (NW >= 16 && TN >= 2) ? 4 : 8;
-  const int per_wave = ((a.K >> 5) + NW - 1) / NW;
-  const dim3 g(grid), b(NW * 64);
+  const int per_wave = ((a.K >> 5) / a.ks + NW - 1) / NW;
+  const dim3 g(grid * a.ks), b(NW * 64);
   if (per_wave <= 1)
     hipLaunchKernelGGL((k_skinny<NW, TN, EPI, 1>), g, b, 0, s, a);
   else if (per_wave <= 2)
@@ -636,18 +744,21 @@ hipError_t launch_nw(const GemmArgs& a, int grid, hipStream_t s) {
   return hipGetLastError();
 }
 
+// grid = column tiles; the launch has grid * a.ks workgroups (a.ks == 0: pick).
 template <int EPI, int TN>
-hipError_t launch_gemm(const GemmArgs& a, int grid, hipStream_t s) {
-  const int nw = pick_nw(a.K);
+hipError_t launch_gemm(GemmArgs a, int grid, hipStream_t s) {
+  if (a.ks <= 0) a.ks = (a.kpart && a.kctr) ? pick_ks(grid, a.K) : 1;
+  const int nw = pick_nw((a.K >> 5) / a.ks);
   if (nw == 16) return launch_nw<16, TN, EPI>(a, grid, s);
   if (nw == 8) return launch_nw<8, TN, EPI>(a, grid, s);
+  if (nw == 4) return launch_nw<4, TN, EPI>(a, grid, s);
   return hipErrorInvalidValue;
 }
 
 bool dims_ok(const LlamaDims& d) {
   if (d.D != 64 && d.D != 128) return false;
-  if (d.H % d.Hkv || d.H / d.Hkv > 8) return false;
-  if (!pick_nw(d.dim) || !pick_nw(d.H * d.D) || !pick_nw(d.ffn)) return false;
+  if (d.H % d.Hkv || (d.H / d.Hkv != 1 && d.H / d.Hkv != 2 && d.H / d.Hkv != 4 && d.H / d.Hkv != 8)) return false;
+  if (d.dim % 32 || (d.H * d.D) % 32 || d.ffn % 32) return false;
   if (d.dim % (16 * kTnResid) || d.vocab % (16 * kTnStore) || d.ffn % 16) return false;
   if (d.max_batch <= 0 || d.max_seq <= 0 || d.n_layers <= 0) return false;
   return true;
@@ -713,39 +824,44 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
     a.ss_part = W.ss; a.ss_parts = ss_parts;
     a.pos = pos; a.slot = slots; a.nslots = d.max_batch; a.q_out = W.q; a.kc = kc; a.vc = vc;
     a.H = d.H; a.Hkv = d.Hkv; a.D = d.D; a.Smax = d.max_seq; a.log2_theta = log2_theta;
+    a.kpart = W.kpart; a.kctr = W.kctr;
     if ((e = launch_gemm<EPI_ROPE, 1>(a, qkv_n / 16, s)) != hipSuccess) return int(e);
 
-    // attention: split-K over kAttnTok-token pieces, one workgroup per (row, KV head, piece)
+    // attention: one 4-wave workgroup per (row, KV head, 256-token chunk)
     {
-      const int nsplit = (max_len + kAttnTok - 1) / kAttnTok;
+      const int nsplit = (max_len + 4 * kChunk - 1) / (4 * kChunk);
       dim3 grid(nsplit, B * d.Hkv);
-      dim3 blk(64 * (d.H / d.Hkv));
       const float scale = 1.f / sqrtf(float(d.D));
-      if (d.D == 64)
-        hipLaunchKernelGGL((k_attn<64, kAttnTok / 64>), grid, blk, 0, s, W.q, kc, vc, pos, slots, d.max_batch,
-                           W.part_o, W.part_ml, W.counters, W.attn, d.H, d.Hkv, d.max_seq, kAttnTok, nsplit_ws, scale);
-      else
-        hipLaunchKernelGGL((k_attn<128, kAttnTok / 64>), grid, blk, 0, s, W.q, kc, vc, pos, slots, d.max_batch,
-                           W.part_o, W.part_ml, W.counters, W.attn, d.H, d.Hkv, d.max_seq, kAttnTok, nsplit_ws, scale);
+      const int G = d.H / d.Hkv;
+#define P2PT_ATTN(DD, GG)                                                                                          \
+  hipLaunchKernelGGL((k_attn<DD, GG>), grid, dim3(256), 0, s, W.q, kc, vc, pos, slots, d.max_batch, W.part_o,    \
+                     W.part_ml, W.counters, W.attn, d.H, d.Hkv, d.max_seq, nsplit_ws, scale)
+      if (d.D == 64) {
+        if (G == 1) P2PT_ATTN(64, 1); else if (G == 2) P2PT_ATTN(64, 2); else if (G == 4) P2PT_ATTN(64, 4); else P2PT_ATTN(64, 8);
+      } else {
+        if (G == 1) P2PT_ATTN(128, 1); else if (G == 2) P2PT_ATTN(128, 2); else if (G == 4) P2PT_ATTN(128, 4); else P2PT_ATTN(128, 8);
+      }
+#undef P2PT_ATTN
       if ((e = hipGetLastError()) != hipSuccess) return int(e);
     }
 
     // O projection + residual
     GemmArgs o{};
     o.M = B; o.x = W.attn; o.w = wo; o.N = d.dim; o.K = d.H * d.D;
-    o.out = W.resid; o.ss_out = W.ss;
+    o.out = W.resid; o.ss_out = W.ss; o.kpart = W.kpart; o.kctr = W.kctr;
     if ((e = launch_gemm<EPI_RESID, kTnResid>(o, d.dim / (16 * kTnResid), s)) != hipSuccess) return int(e);
     ss_parts = d.dim / (16 * kTnResid);
 
     // gate/up + SwiGLU
     GemmArgs g{};
     g.M = B; g.eps = d.eps; g.x = W.resid; g.w = wgu; g.N = 2 * d.ffn; g.K = d.dim;
-    g.ss_part = W.ss; g.ss_parts = ss_parts; g.out = W.h;
+    g.ss_part = W.ss; g.ss_parts = ss_parts; g.out = W.h; g.kpart = W.kpart; g.kctr = W.kctr;
     if ((e = launch_gemm<EPI_SILU, 1>(g, 2 * d.ffn / 16, s)) != hipSuccess) return int(e);
 
     // down + residual
     GemmArgs dn{};
     dn.M = B; dn.x = W.h; dn.w = wdown; dn.N = d.dim; dn.K = d.ffn; dn.out = W.resid; dn.ss_out = W.ss;
+    dn.kpart = W.kpart; dn.kctr = W.kctr;
     if ((e = launch_gemm<EPI_RESID, kTnResid>(dn, d.dim / (16 * kTnResid), s)) != hipSuccess) return int(e);
   }
 
@@ -763,12 +879,12 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
 
 // Standalone skinny GEMM (tests/benchmarks): out[M][N] = bf16(x[M][K] @ w[N][K]^T), M <= 16.
 int p2pt_skinny_gemm(const void* x, const void* w, void* out, int M, int N, int K, void* stream) {
-  if (M <= 0 || M > kMaxM || N % 32 || !pick_nw(K)) return int(hipErrorInvalidValue);
+  if (M <= 0 || M > kMaxM || N % 32 || K <= 0 || K % 32) return int(hipErrorInvalidValue);
   GemmArgs a{};
   a.x = static_cast<const uint16_t*>(x);
   a.w = static_cast<const uint16_t*>(w);
   a.out = static_cast<uint16_t*>(out);
-  a.M = M; a.N = N; a.K = K;
+  a.M = M; a.N = N; a.K = K; a.ks = 1;
   return int(launch_gemm<EPI_STORE, 2>(a, N / 32, static_cast<hipStream_t>(stream)));
 }
 
