@@ -230,8 +230,7 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
   const int mrow0 = (lane >> 4) << 2;
   const int c = lane & 15;
   if (norm) {
-    ssum += __shfl_xor(ssum, 16, kWave);
-    ssum += __shfl_xor(ssum, 32, kWave);
+    ssum = xor32_sum(xor16_sum(ssum));
     const float rs_row = rsqrtf(ssum * (1.f / float(a.K)) + a.eps);  // for row lane & 15
 #pragma unroll
     for (int r = 0; r < 4; r++) {
@@ -267,15 +266,7 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
     if constexpr (EPI == EPI_ARGMAX) {
 #pragma unroll
       for (int r = 0; r < 4; r++) {
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          const float ob = __shfl_xor(best[r], o, kWave);
-          const int oi = __shfl_xor(bi[r], o, kWave);
-          if (ob > best[r] || (ob == best[r] && oi < bi[r])) {
-            best[r] = ob;
-            bi[r] = oi;
-          }
-        }
+        row16_argmax(best[r], bi[r]);
         if (c == 0) {
           a.am_val[bx * kMaxM + mrow0 + r] = best[r];
           a.am_idx[bx * kMaxM + mrow0 + r] = bi[r];
@@ -288,7 +279,7 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const float mine = bf_round(v[0][r]);
-      const float other = __shfl_xor(mine, 1, kWave);
+      const float other = dpp<kDppXor1>(mine);
       if ((c & 1) || mrow0 + r >= a.M) continue;
       a.out[size_t(mrow0 + r) * (a.N >> 1) + (n >> 1)] = uint16_t(f2bf_bits(mine / (1.f + __expf(-mine)) * other));
     }
@@ -303,7 +294,7 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
     for (int r = 0; r < 4; r++) {
       const int m = mrow0 + r;
       const float mine = bf_round(v[0][r]);
-      const float other = __shfl_xor(mine, 1, kWave);
+      const float other = dpp<kDppXor1>(mine);
       if (m >= a.M) continue;
       // Host validates; clamped anyway so a bad index can never write outside the cache.
       const int p = min(max(a.pos[m], 0), a.Smax - 1);
@@ -338,8 +329,7 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
     }
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) sq[r] += __shfl_xor(sq[r], o, kWave);
+      sq[r] = row16_sum(sq[r]);
       if (c == 0) a.ss_out[bx * kMaxM + mrow0 + r] = sq[r];
     }
   }
@@ -368,15 +358,7 @@ __global__ __launch_bounds__(256) void k_argmax_merge(const float* __restrict__ 
         i = pi[j];
       }
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float ob = __shfl_xor(b, o, kWave);
-    const int oi = __shfl_xor(i, o, kWave);
-    if (ob > b || (ob == b && oi < i)) {
-      b = ob;
-      i = oi;
-    }
-  }
+  wave_argmax(b, i);
   __shared__ float sb[4];
   __shared__ int si[4];
   if ((threadIdx.x & 63) == 0) {
@@ -510,8 +492,7 @@ __global__ __launch_bounds__(256) void k_attn(const uint16_t* __restrict__ q, co
       float d = 0.f;
 #pragma unroll
       for (int k = 0; k < 8; k++) d += qf[g][k] * f[k];
-#pragma unroll
-      for (int o = 1; o < LPR; o <<= 1) d += __shfl_xor(d, o, kWave);
+      d = LPR == 16 ? row16_sum(d) : row8_sum(d);
       sc[g][j] = (j * RPI + ri < ntok) ? d : -INFINITY;
     }
   }
@@ -523,8 +504,8 @@ __global__ __launch_bounds__(256) void k_attn(const uint16_t* __restrict__ q, co
     float m = -INFINITY;
 #pragma unroll
     for (int j = 0; j < NI; j++) m = fmaxf(m, sc[g][j]);
-#pragma unroll
-    for (int o = LPR; o < kWave; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, kWave));
+    if constexpr (LPR == 8) m = xor8_max(m);
+    m = xor32_max(xor16_max(m));
     mg[g] = m;
     float l = 0.f;
 #pragma unroll
@@ -532,8 +513,8 @@ __global__ __launch_bounds__(256) void k_attn(const uint16_t* __restrict__ q, co
       sc[g][j] = ntok ? __expf(sc[g][j] - m) : 0.f;  // now p
       l += sc[g][j];
     }
-#pragma unroll
-    for (int o = LPR; o < kWave; o <<= 1) l += __shfl_xor(l, o, kWave);
+    if constexpr (LPR == 8) l = xor8_sum(l);
+    l = xor32_sum(xor16_sum(l));
     lg[g] = l;
   }
   // P.V: the lane's own tokens times its 8 dims, then summed across rows.
@@ -554,9 +535,11 @@ __global__ __launch_bounds__(256) void k_attn(const uint16_t* __restrict__ q, co
 #pragma unroll
   for (int g = 0; g < G; g++)
 #pragma unroll
-    for (int k = 0; k < 8; k++)
-#pragma unroll
-      for (int o = LPR; o < kWave; o <<= 1) acc[g][k] += __shfl_xor(acc[g][k], o, kWave);
+    for (int k = 0; k < 8; k++) {
+      float v = acc[g][k];
+      if constexpr (LPR == 8) v = xor8_sum(v);
+      acc[g][k] = xor32_sum(xor16_sum(v));
+    }
   // Publish this piece to the workgroup (empty pieces: m = -inf, l = 0).
   if (ri == 0) {
 #pragma unroll
@@ -656,7 +639,7 @@ struct LlamaDims {
 };
 
 constexpr int kChunk = 64;  // tokens per attention workgroup = workspace granularity of its partials
-constexpr int kTnResid = 1, kTnStore = 1;
+constexpr int kTnResid = 1, kTnStore = 2;  // LM head: two 16-column subtiles per block
 constexpr int kMaxKs = 8;    // split-K ways over workgroups
 
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -700,12 +683,13 @@ Workspace carve(const LlamaDims& d, uint8_t* base) {
   return w;
 }
 
-// Waves per workgroup for `steps` 32-wide k-steps per workgroup: enough that
-// each wave streams at most ~8 k-steps (one round trip of loads), capped at
-// 16 (1024 threads).
+// Waves per workgroup for `steps` 32-wide k-steps per workgroup. Measured on
+// MI355X (scripts/bench_skinny.py, M = 8): 4 and 8 waves tie up to K = 2048,
+// 8 beats 16 by 20-30 % at K = 5632 (a 16-wave block's reduction and barrier
+// cost more than its extra loads in flight win back).
 int pick_nw(int steps) {
   if (steps <= 0) return 0;
-  return steps <= 16 ? 4 : steps <= 64 ? 8 : 16;
+  return steps <= 16 ? 4 : 8;
 }
 
 // Split-K ways. Off by default: on MI355X the seam (write-through slabs,
@@ -746,9 +730,9 @@ hipError_t launch_nw(const GemmArgs& a, int grid, hipStream_t s) {
 
 // grid = column tiles; the launch has grid * a.ks workgroups (a.ks == 0: pick).
 template <int EPI, int TN>
-hipError_t launch_gemm(GemmArgs a, int grid, hipStream_t s) {
+hipError_t launch_gemm(GemmArgs a, int grid, hipStream_t s, int nw_override = 0) {
   if (a.ks <= 0) a.ks = (a.kpart && a.kctr) ? pick_ks(grid, a.K) : 1;
-  const int nw = pick_nw((a.K >> 5) / a.ks);
+  const int nw = nw_override ? nw_override : pick_nw((a.K >> 5) / a.ks);
   if (nw == 16) return launch_nw<16, TN, EPI>(a, grid, s);
   if (nw == 8) return launch_nw<8, TN, EPI>(a, grid, s);
   if (nw == 4) return launch_nw<4, TN, EPI>(a, grid, s);
@@ -872,7 +856,8 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
   h.out = static_cast<uint16_t*>(logits);
   h.am_val = W.am_val; h.am_idx = W.am_idx;
   const int parts = d.vocab / (16 * kTnStore);
-  if ((e = launch_gemm<EPI_ARGMAX, kTnStore>(h, parts, s)) != hipSuccess) return int(e);
+  // 4 waves x 2 subtiles: the fastest LM-head shape measured (vocab 32000, K 2048: 22.6 vs 29.6 us).
+  if ((e = launch_gemm<EPI_ARGMAX, kTnStore>(h, parts, s, 4)) != hipSuccess) return int(e);
   hipLaunchKernelGGL(k_argmax_merge, dim3(B), dim3(256), 0, s, W.am_val, W.am_idx, parts, ids);
   return int(hipGetLastError());
 }
@@ -886,6 +871,62 @@ int p2pt_skinny_gemm(const void* x, const void* w, void* out, int M, int N, int 
   a.out = static_cast<uint16_t*>(out);
   a.M = M; a.N = N; a.K = K; a.ks = 1;
   return int(launch_gemm<EPI_STORE, 2>(a, N / 32, static_cast<hipStream_t>(stream)));
+}
+
+// Microbenchmark hook (scripts/bench_skinny.py --attn): `reps` back-to-back
+// launches of the decode attention kernel. part_o / part_ml / counters as in
+// the workspace (counters zeroed); q [B][H*D], caches [B][Smax][Hkv][D].
+int p2pt_attn_bench(const void* q, const void* kc, const void* vc, const int* pos, int B, int H, int Hkv, int D,
+                    int Smax, int max_len, float* part_o, float* part_ml, unsigned* counters, void* out, int reps,
+                    void* stream) {
+  const int G = Hkv > 0 ? H / Hkv : 0;
+  if (B <= 0 || B > kMaxM || (D != 64 && D != 128) || G != 4 || max_len <= 0 || max_len > Smax || reps <= 0)
+    return int(hipErrorInvalidValue);
+  auto st = static_cast<hipStream_t>(stream);
+  const int nsplit_ws = (Smax + kChunk - 1) / kChunk;
+  const int nsplit = (max_len + 4 * kChunk - 1) / (4 * kChunk);
+  const float scale = 1.f / sqrtf(float(D));
+  for (int r = 0; r < reps; r++) {
+    dim3 grid(nsplit, B * Hkv);
+    auto qq = static_cast<const uint16_t*>(q);
+    auto kk = static_cast<const uint16_t*>(kc);
+    auto vv = static_cast<const uint16_t*>(vc);
+    auto oo = static_cast<uint16_t*>(out);
+    if (D == 64)
+      hipLaunchKernelGGL((k_attn<64, 4>), grid, dim3(256), 0, st, qq, kk, vv, pos, nullptr, B, part_o, part_ml,
+                         counters, oo, H, Hkv, Smax, nsplit_ws, scale);
+    else
+      hipLaunchKernelGGL((k_attn<128, 4>), grid, dim3(256), 0, st, qq, kk, vv, pos, nullptr, B, part_o, part_ml,
+                         counters, oo, H, Hkv, Smax, nsplit_ws, scale);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return int(e);
+  }
+  return 0;
+}
+
+// Microbenchmark hook (scripts/bench_skinny.py): `reps` back-to-back launches
+// of the skinny GEMM with an explicit waves-per-block / subtile choice.
+int p2pt_skinny_bench(const void* x, const void* w, void* out, int M, int N, int K, int nw, int tn, int reps,
+                      void* stream) {
+  if (M <= 0 || M > kMaxM || N % (16 * tn) || K <= 0 || K % 32 || reps <= 0) return int(hipErrorInvalidValue);
+  GemmArgs a{};
+  a.x = static_cast<const uint16_t*>(x);
+  a.w = static_cast<const uint16_t*>(w);
+  a.out = static_cast<uint16_t*>(out);
+  a.M = M; a.N = N; a.K = K; a.ks = 1;
+  auto st = static_cast<hipStream_t>(stream);
+  for (int r = 0; r < reps; r++) {
+    hipError_t e;
+    const int grid = N / (16 * tn);
+    if (tn == 1)
+      e = nw == 4 ? launch_nw<4, 1, EPI_STORE>(a, grid, st) : nw == 8 ? launch_nw<8, 1, EPI_STORE>(a, grid, st)
+                                                          : launch_nw<16, 1, EPI_STORE>(a, grid, st);
+    else
+      e = nw == 4 ? launch_nw<4, 2, EPI_STORE>(a, grid, st) : nw == 8 ? launch_nw<8, 2, EPI_STORE>(a, grid, st)
+                                                          : launch_nw<16, 2, EPI_STORE>(a, grid, st);
+    if (e != hipSuccess) return int(e);
+  }
+  return 0;
 }
 
 }  // extern "C"

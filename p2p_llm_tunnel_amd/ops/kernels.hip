@@ -289,15 +289,7 @@ __global__ __launch_bounds__(256) void k_argmax(const uint16_t* __restrict__ log
       bi = i;
     }
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    float ob = __shfl_xor(best, o, kWave);
-    int oi = __shfl_xor(bi, o, kWave);
-    if (ob > best || (ob == best && oi < bi)) {
-      best = ob;
-      bi = oi;
-    }
-  }
+  wave_argmax(best, bi);
   __shared__ float sb[4];
   __shared__ int si[4];
   if ((threadIdx.x & 63) == 0) {
