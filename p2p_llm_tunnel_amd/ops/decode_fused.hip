@@ -89,6 +89,12 @@ struct GemmArgs {
 
 __device__ __forceinline__ frag8 as_frag(const uint4& v) { return __builtin_bit_cast(frag8, v); }
 
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+// v_dot2_f32_bf16: c + a.lo * b.lo + a.hi * b.hi, products and sum in fp32.
+__device__ __forceinline__ float dot2_bf16(uint32_t a, uint32_t b, float c) {
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, a), __builtin_bit_cast(bf16x2_t, b), c, false);
+}
+
 // Weights use the default cache policy on purpose: a decode step replays the
 // same weights back to back, and models up to the 256 MB MALL keep them
 // resident between steps (non-temporal loads measured 1.75x slower on the
@@ -403,144 +409,144 @@ __global__ __launch_bounds__(256) void k_embed(const uint16_t* __restrict__ embe
 }
 
 // ------------------------------------------------------------ attention
-// GQA flash-decoding. A workgroup owns a (row b, KV head, 256-token chunk);
-// each of its 4 waves takes a 64-token piece and loads all of it straight
-// into registers with 16-byte loads whose lanes tile whole K/V rows (D/8 lanes
-// per row, so every instruction reads full cache lines), so a piece's bytes
-// are in flight at once and never staged through LDS. A lane keeps one 8-dim
-// group of every query head of the KV head (K/V are read once per GQA group),
-// finishes its dot products with in-row xor shuffles, and ends up holding the
-// softmax weights of exactly the tokens whose V it loaded: P.V needs no data
-// exchange until the final cross-row sum. Scores and P.V are fp32 VALU FMAs:
-// with G <= 8 query rows an MFMA tile would be >= half padding, and the
-// kernel is bound by the K/V stream and by latency, not arithmetic.
-// Merges are latency, so they are kept off the global round-trip path where
-// possible: the 4 pieces of a chunk merge through LDS; only contexts longer
-// than one chunk publish a per-chunk partial (write-through + arrival ticket)
-// and the last chunk to finish merges them, its waves taking different heads
-// and issuing every partial load of a head before the first use.
+// GQA flash-decoding with a fixed grid of (span slot, row b, KV head)
+// workgroups: graph-captured steps launch the same grid whatever the context
+// length, so the grid is sized by the batch (about one round of workgroups on
+// the chip), not by the cache capacity — idle workgroups were a third of the
+// kernel at 1k tokens. Each slot covers a span of >= 256 tokens of row b; its
+// 8 waves walk the span in 32-token pieces with an online softmax.
+// A piece is loaded straight into registers with 16-byte loads whose lanes
+// tile whole K/V rows (D/8 lanes per row: every instruction reads full cache
+// lines); nothing is staged through LDS. A lane keeps one 8-dim group of every
+// query head of the KV head (K/V are read once per GQA group), computes its
+// dot products with v_dot2_f32_bf16 and finishes them with in-row DPP sums,
+// and ends up holding the softmax weights of exactly the tokens whose V it
+// loaded: P.V needs no data exchange until the final cross-row sum. Scores and
+// P.V are fp32 VALU: with G <= 8 query rows an MFMA tile would be >= half
+// padding; the kernel is bound by the K/V stream and latency.
+// The 8 waves of a slot merge through LDS; only spans split over several
+// slots publish a partial (write-through + arrival ticket) that the last slot
+// to finish merges, its waves taking different heads.
 // Row b reads cache slot slot[b] (rows may share a slot: chunked prefill) and
 // attends to positions 0..pos[b]; the output is bf16 [B][H*D].
 template <int D, int G>
-__global__ __launch_bounds__(256) void k_attn(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+__global__ __launch_bounds__(512) void k_attn(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
                                               const uint16_t* __restrict__ vc, const int* __restrict__ pos,
                                               const int* __restrict__ slot, int nslots, float* __restrict__ part_o,
                                               float* __restrict__ part_ml, unsigned* __restrict__ counters,
                                               uint16_t* __restrict__ out, int H, int Hkv, int Smax, int nsplit,
                                               float scale) {
-  constexpr int TOK = 64, NWV = 4, CHUNK = TOK * NWV;
+  constexpr int TOK = 32, NWV = 8, MINSPAN = TOK * NWV;
   constexpr int DPL = D / kWave;  // merges: dims per lane
-  constexpr int MAXC = 16;        // chunks merged per load batch
+  constexpr int MAXC = 16;        // partials merged per load batch
+  constexpr int LPR = D / 8, RPI = kWave / LPR, NI = TOK / RPI;
   __shared__ __attribute__((aligned(16))) float pacc[NWV][G][D];
   __shared__ float pml[NWV][G][2];
   __shared__ unsigned s_ticket;
 
-  const int chunk = blockIdx.x;
   const int b = blockIdx.y / Hkv, kvh = blockIdx.y % Hkv;
   const int len = min(max(pos[b], 0), Smax - 1) + 1;
-  if (chunk * CHUNK >= len) return;
-  const int nchunks = (len + CHUNK - 1) / CHUNK;
+  int span = (len + gridDim.x - 1) / gridDim.x;
+  span = max(MINSPAN, (span + TOK - 1) / TOK * TOK);
+  const int nact = (len + span - 1) / span;  // slots with tokens
+  const int sl = blockIdx.x;
+  if (sl >= nact) return;
+  const int s0 = sl * span, s1 = min(len, s0 + span);
   const int sb = slot ? min(max(slot[b], 0), nslots - 1) : b;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int start = chunk * CHUNK + wv * TOK;
-  const int ntok = max(0, min(TOK, len - start));  // 0: this wave's piece is past the end
+  const int dg = lane % LPR, ri = lane / LPR;
 
   const size_t tok_stride = size_t(Hkv) * D;
-  const int t_last = max(ntok - 1, 0);
-  const uint16_t* kbase = kc + (size_t(sb) * Smax + min(start, len - 1)) * tok_stride + size_t(kvh) * D;
-  const uint16_t* vbase = vc + (size_t(sb) * Smax + min(start, len - 1)) * tok_stride + size_t(kvh) * D;
-
-  // Lane layout for K and V alike: LPR lanes cover one D-wide row with 16-byte
-  // loads (dim group dg = 8 dims), so one instruction reads RPI whole rows
-  // (contiguous 128/256-byte runs: full cache lines) and NI instructions cover
-  // the piece. Lanes past the end re-read the last valid row (in bounds).
-  constexpr int LPR = D / 8, RPI = kWave / LPR, NI = TOK / RPI;
-  const int dg = lane % LPR, ri = lane / LPR;
-  uint4 kr[NI], vr[NI];
-#pragma unroll
-  for (int j = 0; j < NI; j++) {
-    const size_t t = size_t(min(j * RPI + ri, t_last));
-    kr[j] = *reinterpret_cast<const uint4*>(kbase + t * tok_stride + 8 * dg);
-  }
-#pragma unroll
-  for (int j = 0; j < NI; j++) {
-    const size_t t = size_t(min(j * RPI + ri, t_last));
-    vr[j] = *reinterpret_cast<const uint4*>(vbase + t * tok_stride + 8 * dg);
-  }
-  // This lane's 8 query dims of every head, pre-scaled.
-  float qf[G][8];
+  const uint16_t* kbase = kc + size_t(sb) * Smax * tok_stride + size_t(kvh) * D + 8 * dg;
+  const uint16_t* vbase = vc + size_t(sb) * Smax * tok_stride + size_t(kvh) * D + 8 * dg;
+  // This lane's 8 query dims of every head as bf16 pairs (v_dot2 operands).
+  uint4 qpk[G];
   {
     const uint16_t* qp = q + (size_t(b) * H + size_t(kvh) * G) * D + 8 * dg;
 #pragma unroll
-    for (int g = 0; g < G; g++) {
-      unpack8(*reinterpret_cast<const uint4*>(qp + size_t(g) * D), qf[g]);
-#pragma unroll
-      for (int k = 0; k < 8; k++) qf[g][k] *= scale;
-    }
+    for (int g = 0; g < G; g++) qpk[g] = *reinterpret_cast<const uint4*>(qp + size_t(g) * D);
   }
 
-  // Scores: partial dots over the lane's 8 dims, summed across the LPR lanes
-  // of the row (DPP-able xor shuffles inside 8/16-lane rows). Every lane of a
-  // row ends up with the row's score: lane (ri, dg) holds token j*RPI + ri.
-  float sc[G][NI];
-#pragma unroll
-  for (int j = 0; j < NI; j++) {
-    float f[8];
-    unpack8(kr[j], f);
-#pragma unroll
-    for (int g = 0; g < G; g++) {
-      float d = 0.f;
-#pragma unroll
-      for (int k = 0; k < 8; k++) d += qf[g][k] * f[k];
-      d = LPR == 16 ? row16_sum(d) : row8_sum(d);
-      sc[g][j] = (j * RPI + ri < ntok) ? d : -INFINITY;
-    }
-  }
-  // Softmax statistics per head: max/sum over the lane's tokens, then across
-  // rows (lanes differing in ri; lanes of one row hold the same values).
-  float mg[G], lg[G];
+  // Running state over this wave's pieces. m is wave-uniform per head; l and
+  // acc hold this lane's tokens only and are summed across rows at the end.
+  float mg[G], lg[G], acc[G][8];
 #pragma unroll
   for (int g = 0; g < G; g++) {
-    float m = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < NI; j++) m = fmaxf(m, sc[g][j]);
-    if constexpr (LPR == 8) m = xor8_max(m);
-    m = xor32_max(xor16_max(m));
-    mg[g] = m;
-    float l = 0.f;
-#pragma unroll
-    for (int j = 0; j < NI; j++) {
-      sc[g][j] = ntok ? __expf(sc[g][j] - m) : 0.f;  // now p
-      l += sc[g][j];
-    }
-    if constexpr (LPR == 8) l = xor8_sum(l);
-    l = xor32_sum(xor16_sum(l));
-    lg[g] = l;
-  }
-  // P.V: the lane's own tokens times its 8 dims, then summed across rows.
-  float acc[G][8];
-#pragma unroll
-  for (int g = 0; g < G; g++)
+    mg[g] = -INFINITY;
+    lg[g] = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; k++) acc[g][k] = 0.f;
-#pragma unroll
-  for (int j = 0; j < NI; j++) {
-    float f[8];
-    unpack8(vr[j], f);
-#pragma unroll
-    for (int g = 0; g < G; g++)
-#pragma unroll
-      for (int k = 0; k < 8; k++) acc[g][k] += sc[g][j] * f[k];
   }
+  for (int p0 = s0 + wv * TOK; p0 < s1; p0 += NWV * TOK) {
+    const int ntok = min(TOK, s1 - p0);
+    // Issue the piece (lanes past the end re-read the last valid row).
+    uint4 kr[NI], vr[NI];
 #pragma unroll
-  for (int g = 0; g < G; g++)
+    for (int j = 0; j < NI; j++)
+      kr[j] = *reinterpret_cast<const uint4*>(kbase + size_t(p0 + min(j * RPI + ri, ntok - 1)) * tok_stride);
+#pragma unroll
+    for (int j = 0; j < NI; j++)
+      vr[j] = *reinterpret_cast<const uint4*>(vbase + size_t(p0 + min(j * RPI + ri, ntok - 1)) * tok_stride);
+    // Scores: lane (ri, dg) ends with token j*RPI + ri's score for every head.
+    float sc[G][NI];
+#pragma unroll
+    for (int j = 0; j < NI; j++) {
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        float d = 0.f;
+        d = dot2_bf16(qpk[g].x, kr[j].x, d);
+        d = dot2_bf16(qpk[g].y, kr[j].y, d);
+        d = dot2_bf16(qpk[g].z, kr[j].z, d);
+        d = dot2_bf16(qpk[g].w, kr[j].w, d);
+        d = (LPR == 16 ? row16_sum(d) : row8_sum(d)) * scale;
+        sc[g][j] = (j * RPI + ri < ntok) ? d : -INFINITY;
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+      float pm = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < NI; j++) pm = fmaxf(pm, sc[g][j]);
+      if constexpr (LPR == 8) pm = xor8_max(pm);
+      pm = xor32_max(xor16_max(pm));
+      const float mnew = fmaxf(mg[g], pm);
+      const float corr = __expf(mg[g] - mnew);  // 0 on the first piece (mg = -inf)
+      mg[g] = mnew;
+      float ls = 0.f;
+#pragma unroll
+      for (int j = 0; j < NI; j++) {
+        sc[g][j] = __expf(sc[g][j] - mnew);  // now p (0 for masked tokens)
+        ls += sc[g][j];
+      }
+      lg[g] = lg[g] * corr + ls;
+#pragma unroll
+      for (int k = 0; k < 8; k++) acc[g][k] *= corr;
+    }
+    // P.V: the lane's own tokens times its 8 dims.
+#pragma unroll
+    for (int j = 0; j < NI; j++) {
+      float f[8];
+      unpack8(vr[j], f);
+#pragma unroll
+      for (int g = 0; g < G; g++)
+#pragma unroll
+        for (int k = 0; k < 8; k++) acc[g][k] += sc[g][j] * f[k];
+    }
+  }
+  // Sum across rows (lanes with the same dim group).
+#pragma unroll
+  for (int g = 0; g < G; g++) {
+    float l = lg[g];
+    if constexpr (LPR == 8) l = xor8_sum(l);
+    lg[g] = xor32_sum(xor16_sum(l));
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       float v = acc[g][k];
       if constexpr (LPR == 8) v = xor8_sum(v);
       acc[g][k] = xor32_sum(xor16_sum(v));
     }
-  // Publish this piece to the workgroup (empty pieces: m = -inf, l = 0).
+  }
+  // Publish this wave to the workgroup (waves without pieces: m = -inf, l = 0).
   if (ri == 0) {
 #pragma unroll
     for (int g = 0; g < G; g++) {
@@ -551,13 +557,13 @@ __global__ __launch_bounds__(256) void k_attn(const uint16_t* __restrict__ q, co
   if (lane == 0) {
 #pragma unroll
     for (int g = 0; g < G; g++) {
-      pml[wv][g][0] = ntok ? mg[g] : -INFINITY;
-      pml[wv][g][1] = ntok ? lg[g] : 0.f;
+      pml[wv][g][0] = mg[g];
+      pml[wv][g][1] = lg[g];
     }
   }
   __syncthreads();
 
-  // Chunk merge through LDS: wave w takes heads w, w + 4, ...
+  // Slot merge through LDS: wave w takes heads w, w + 8, ...
   const size_t hb0 = size_t(b) * H + size_t(kvh) * G;
   for (int g = wv; g < G; g += NWV) {
     float M = -INFINITY;
@@ -574,44 +580,44 @@ __global__ __launch_bounds__(256) void k_attn(const uint16_t* __restrict__ q, co
       for (int k = 0; k < DPL; k++) o[k] += ww * pacc[w][g][lane + k * kWave];
     }
     const size_t hb = hb0 + g;
-    if (nchunks == 1) {
+    if (nact == 1) {
       const float inv = 1.f / L;
 #pragma unroll
       for (int k = 0; k < DPL; k++) out[hb * D + lane + k * kWave] = uint16_t(f2bf_bits(o[k] * inv));
     } else {
-      float* po = part_o + (hb * nsplit + chunk) * D;
+      float* po = part_o + (hb * nsplit + sl) * D;
 #pragma unroll
       for (int k = 0; k < DPL; k++) st_wt(po + lane + k * kWave, o[k]);
       if (lane == 0) {
-        st_wt(part_ml + (hb * nsplit + chunk) * 2 + 0, M);
-        st_wt(part_ml + (hb * nsplit + chunk) * 2 + 1, L);
+        st_wt(part_ml + (hb * nsplit + sl) * 2 + 0, M);
+        st_wt(part_ml + (hb * nsplit + sl) * 2 + 1, L);
       }
     }
   }
-  if (nchunks == 1) return;
+  if (nact == 1) return;
   drain_stores();
   __syncthreads();
   if (threadIdx.x == 0) s_ticket = arrive(&counters[blockIdx.y]);
   __syncthreads();
-  if (s_ticket != unsigned(nchunks - 1)) return;
+  if (s_ticket != unsigned(nact - 1)) return;
 
-  // Last chunk: merge the chunk partials, heads spread over the waves; each
-  // batch of up to MAXC chunks is loaded before any of it is used.
+  // Last slot: merge the slot partials, heads spread over the waves; each
+  // batch of up to MAXC partials is loaded before any of it is used.
   for (int g = wv; g < G; g += NWV) {
     const size_t hb = hb0 + g;
     const float* ml = part_ml + hb * nsplit * 2;
     float M = -INFINITY;
-    for (int c = lane; c < nchunks; c += kWave) M = fmaxf(M, ld_wt(ml + 2 * c));
+    for (int c = lane; c < nact; c += kWave) M = fmaxf(M, ld_wt(ml + 2 * c));
     M = wave_max(M);
     float L = 0.f, o[DPL];
 #pragma unroll
     for (int k = 0; k < DPL; k++) o[k] = 0.f;
-    for (int c0 = 0; c0 < nchunks; c0 += MAXC) {
+    for (int c0 = 0; c0 < nact; c0 += MAXC) {
       float pv[MAXC][DPL], wl[MAXC], ll[MAXC];
 #pragma unroll
       for (int j = 0; j < MAXC; j++) {
-        const bool ok = c0 + j < nchunks;
-        const int c = min(c0 + j, nchunks - 1);
+        const bool ok = c0 + j < nact;
+        const int c = min(c0 + j, nact - 1);
         wl[j] = ld_wt(ml + 2 * c);
         ll[j] = ok ? ld_wt(ml + 2 * c + 1) : 0.f;
 #pragma unroll
@@ -630,6 +636,13 @@ __global__ __launch_bounds__(256) void k_attn(const uint16_t* __restrict__ q, co
     for (int k = 0; k < DPL; k++) out[hb * D + lane + k * kWave] = uint16_t(f2bf_bits(o[k] * inv));
   }
   if (threadIdx.x == 0) st_wt(&counters[blockIdx.y], 0u);
+}
+
+// Span slots per (row, KV head): about one round of workgroups on the chip,
+// at most the workspace's partial slots.
+int attn_slots(int B, int Hkv, int nsplit_ws) {
+  int sl = 256 / std::max(1, B * Hkv);
+  return std::max(1, std::min({sl, 16, nsplit_ws}));
 }
 
 // ------------------------------------------------------------ host side
@@ -811,14 +824,14 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
     a.kpart = W.kpart; a.kctr = W.kctr;
     if ((e = launch_gemm<EPI_ROPE, 1>(a, qkv_n / 16, s)) != hipSuccess) return int(e);
 
-    // attention: one 4-wave workgroup per (row, KV head, 256-token chunk)
+    // attention: (span slot, row, KV head) workgroups of 8 waves
     {
-      const int nsplit = (max_len + 4 * kChunk - 1) / (4 * kChunk);
-      dim3 grid(nsplit, B * d.Hkv);
+      (void)max_len;  // the grid no longer depends on the context length
+      dim3 grid(attn_slots(B, d.Hkv, nsplit_ws), B * d.Hkv);
       const float scale = 1.f / sqrtf(float(d.D));
       const int G = d.H / d.Hkv;
 #define P2PT_ATTN(DD, GG)                                                                                          \
-  hipLaunchKernelGGL((k_attn<DD, GG>), grid, dim3(256), 0, s, W.q, kc, vc, pos, slots, d.max_batch, W.part_o,    \
+  hipLaunchKernelGGL((k_attn<DD, GG>), grid, dim3(512), 0, s, W.q, kc, vc, pos, slots, d.max_batch, W.part_o,    \
                      W.part_ml, W.counters, W.attn, d.H, d.Hkv, d.max_seq, nsplit_ws, scale)
       if (d.D == 64) {
         if (G == 1) P2PT_ATTN(64, 1); else if (G == 2) P2PT_ATTN(64, 2); else if (G == 4) P2PT_ATTN(64, 4); else P2PT_ATTN(64, 8);
@@ -884,19 +897,18 @@ int p2pt_attn_bench(const void* q, const void* kc, const void* vc, const int* po
     return int(hipErrorInvalidValue);
   auto st = static_cast<hipStream_t>(stream);
   const int nsplit_ws = (Smax + kChunk - 1) / kChunk;
-  const int nsplit = (max_len + 4 * kChunk - 1) / (4 * kChunk);
   const float scale = 1.f / sqrtf(float(D));
   for (int r = 0; r < reps; r++) {
-    dim3 grid(nsplit, B * Hkv);
+    dim3 grid(attn_slots(B, Hkv, nsplit_ws), B * Hkv);
     auto qq = static_cast<const uint16_t*>(q);
     auto kk = static_cast<const uint16_t*>(kc);
     auto vv = static_cast<const uint16_t*>(vc);
     auto oo = static_cast<uint16_t*>(out);
     if (D == 64)
-      hipLaunchKernelGGL((k_attn<64, 4>), grid, dim3(256), 0, st, qq, kk, vv, pos, nullptr, B, part_o, part_ml,
+      hipLaunchKernelGGL((k_attn<64, 4>), grid, dim3(512), 0, st, qq, kk, vv, pos, nullptr, B, part_o, part_ml,
                          counters, oo, H, Hkv, Smax, nsplit_ws, scale);
     else
-      hipLaunchKernelGGL((k_attn<128, 4>), grid, dim3(256), 0, st, qq, kk, vv, pos, nullptr, B, part_o, part_ml,
+      hipLaunchKernelGGL((k_attn<128, 4>), grid, dim3(512), 0, st, qq, kk, vv, pos, nullptr, B, part_o, part_ml,
                          counters, oo, H, Hkv, Smax, nsplit_ws, scale);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return int(e);

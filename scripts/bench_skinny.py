@@ -93,10 +93,10 @@ def attn(a):
             part_o = torch.empty(16 * H * (Smax // 64) * D, device="cuda", dtype=torch.float32)
             part_ml = torch.empty(16 * H * (Smax // 64) * 2, device="cuda", dtype=torch.float32)
             ctr = torch.zeros(16 * H, device="cuda", dtype=torch.int32)
-            for ctx in (64, 256, 1024, 4000):
+            for ctx, ml in ((64, Smax), (64, 64), (256, Smax), (1024, Smax), (1024, 1024), (4000, Smax)):
                 pos = torch.full((B,), ctx - 1, device="cuda", dtype=torch.int32)
                 st = torch.cuda.current_stream().cuda_stream
-                args = (q.data_ptr(), kc.data_ptr(), vc.data_ptr(), pos.data_ptr(), B, H, Hkv, D, Smax, Smax,
+                args = (q.data_ptr(), kc.data_ptr(), vc.data_ptr(), pos.data_ptr(), B, H, Hkv, D, Smax, ml,
                         part_o.data_ptr(), part_ml.data_ptr(), ctr.data_ptr(), out.data_ptr())
                 assert lib.p2pt_attn_bench(*args, 3, st) == 0
                 torch.cuda.synchronize()
@@ -113,7 +113,7 @@ def attn(a):
                 p = torch.softmax(qf @ kf.transpose(-1, -2), -1)
                 ref = (p @ vf).reshape(B, H * D)
                 err = (out.float() - ref).abs().max().item()
-                print(json.dumps({"attn_D": D, "B": B, "ctx": ctx, "us": round(us, 2), "kv_MB": round(kv / 1e6, 2),
+                print(json.dumps({"attn_D": D, "B": B, "ctx": ctx, "max_len": ml, "us": round(us, 2), "kv_MB": round(kv / 1e6, 2),
                                   "TBps": round(kv / us / 1e6, 2), "max_abs_err": round(err, 4)}), flush=True)
 
 
