@@ -8,6 +8,7 @@
 #include <netinet/tcp.h>
 #include <openssl/err.h>
 #include <openssl/ssl.h>
+#include <openssl/x509v3.h>
 #include <sys/epoll.h>
 #include <sys/uio.h>
 #include <unistd.h>
@@ -562,9 +563,14 @@ struct ConnectOp : std::enable_shared_from_this<ConnectOp> {
     }
     conn->ssl_ = SSL_new(tls_client_ctx());
     SSL_set_fd(conn->ssl_, cfd);
-    SSL_set_tlsext_host_name(conn->ssl_, host.c_str());
     SockAddr dummy;
-    if (!SockAddr::parse(host, 0, dummy)) SSL_set1_host(conn->ssl_, host.c_str());
+    if (SockAddr::parse(host, 0, dummy)) {
+      // IP literal: no SNI (RFC 6066 §3); the certificate must carry it as an IP SAN.
+      X509_VERIFY_PARAM_set1_ip_asc(SSL_get0_param(conn->ssl_), host.c_str());
+    } else {
+      SSL_set_tlsext_host_name(conn->ssl_, host.c_str());
+      SSL_set1_host(conn->ssl_, host.c_str());
+    }
     conn->handshaking_ = true;
     auto self = shared_from_this();
     conn->handshake_cb_ = [self, conn](std::string err) {
