@@ -36,7 +36,7 @@ const std::vector<Opt>& serve_opts() {
   static const std::vector<Opt> o = {
       {"signal", "TUNNEL_SIGNAL", "wss://signal-server.fly.dev", "WebSocket URL of the signaling server"},
       {"room", "TUNNEL_ROOM", nullptr, "Room name to join"},
-      {"upstream", "TUNNEL_UPSTREAM", nullptr, "Upstream HTTP URL to forward requests to"},
+      {"upstream", "TUNNEL_UPSTREAM", nullptr, "Upstream HTTP URL to forward requests to (comma-separated: least-loaded across several)"},
       {"advertise", nullptr, "/", "Path prefix to advertise (e.g. /v1)"},
       {"turn", "TUNNEL_TURN", "", "TURN server URL (e.g. turn:turn.example.com:3478)"},
       {"turn-user", "TUNNEL_TURN_USER", "", "TURN server username"},

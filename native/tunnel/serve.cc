@@ -38,6 +38,14 @@ std::shared_ptr<ServeSession> ServeSession::start(Reactor& r, std::shared_ptr<Me
 ServeSession::ServeSession(Reactor& r, std::shared_ptr<MessageChannel> ch, ServeConfig cfg)
     : r_(r), ch_(std::move(ch)), cfg_(std::move(cfg)), client_(r) {
   sched_ = std::make_unique<FrameScheduler>(ch_);
+  for (size_t a = 0; a <= cfg_.upstream.size();) {
+    size_t c = cfg_.upstream.find(',', a);
+    if (c == std::string::npos) c = cfg_.upstream.size();
+    if (c > a) upstreams_.push_back(cfg_.upstream.substr(a, c - a));
+    a = c + 1;
+  }
+  if (upstreams_.empty()) upstreams_.push_back(cfg_.upstream);
+  outstanding_.assign(upstreams_.size(), 0);
   std::weak_ptr<ServeSession> w;  // set after construction via on_open
   ch_->on_buffered_low = [this] { sched_->pump(); };
 }
@@ -63,6 +71,7 @@ void ServeSession::stop(const std::string& why) {
   hello_timer_ = ping_timer_ = 0;
   auto inflight = std::move(inflight_);
   inflight_.clear();
+  std::fill(outstanding_.begin(), outstanding_.end(), 0);
   for (auto& kv : inflight)
     if (kv.second.call) kv.second.call->cancel();
   streams_.clear();
@@ -134,9 +143,11 @@ void ServeSession::on_hello(const proto::Frame& f) {
   handshaken_ = true;
   LOG_INFO(kT, "sent AGREE, tunnel ready");
   if (cfg_.upstream_prewarm) {
-    std::string perr;
-    if (!client_.prewarm(cfg_.upstream, cfg_.upstream_prewarm, cfg_.upstream_prewarm_ttl_ms, &perr))
-      LOG_DEBUG(kT, "upstream prewarm disabled: %s", perr.c_str());
+    for (auto& u : upstreams_) {
+      std::string perr;
+      if (!client_.prewarm(u, cfg_.upstream_prewarm, cfg_.upstream_prewarm_ttl_ms, &perr))
+        LOG_DEBUG(kT, "upstream prewarm disabled for %s: %s", u.c_str(), perr.c_str());
+    }
   }
   last_pong_ms_ = Reactor::now_ms();
   send_ping();  // tokio::time::interval's first tick is immediate
@@ -204,6 +215,7 @@ void ServeSession::handle_frame(const proto::Frame& f) {
       if (it != inflight_.end()) {
         LOG_DEBUG(kT, "stream %u cancelled by peer", f.stream_id);
         auto call = it->second.call;
+        release_upstream(it->second);
         inflight_.erase(it);
         if (call) call->cancel();
         metrics::counter_add("tunnel_streams_cancelled_total");
@@ -241,8 +253,19 @@ static bool valid_method(const std::string& m) {
   return true;
 }
 
+size_t ServeSession::pick_upstream() {
+  size_t n = upstreams_.size(), best = rr_ % n;
+  for (size_t k = 1; k < n; k++) {
+    size_t i = (rr_ + k) % n;
+    if (outstanding_[i] < outstanding_[best]) best = i;
+  }
+  rr_ = best + 1;
+  return best;
+}
+
 void ServeSession::start_request(uint32_t sid, Pending p) {
-  std::string url = proto::build_upstream_url(cfg_.upstream, cfg_.advertise, p.headers.path);
+  const size_t up = pick_upstream();
+  std::string url = proto::build_upstream_url(upstreams_[up], cfg_.advertise, p.headers.path);
   LOG_DEBUG(kT, "forwarding %s %s -> %s", p.headers.method.c_str(), p.headers.path.c_str(), url.c_str());
   if (!valid_method(p.headers.method)) {
     LOG_ERROR(kT, "failed to handle request: invalid HTTP method");
@@ -307,6 +330,7 @@ void ServeSession::start_request(uint32_t sid, Pending p) {
     if (!s) return;
     auto it = s->inflight_.find(sid);
     if (it == s->inflight_.end()) return;  // cancelled
+    s->release_upstream(it->second);
     s->inflight_.erase(it);
     if (s->stopped_) return;
     if (!err.empty()) {
@@ -323,7 +347,10 @@ void ServeSession::start_request(uint32_t sid, Pending p) {
     trace::event("serve", sid, "res_end");
     LOG_DEBUG(kT, "response %u complete", sid);
   };
-  inflight_[sid] = Inflight{};
+  Inflight fl;
+  fl.up = up;
+  inflight_[sid] = fl;
+  outstanding_[up]++;
   auto call = client_.request(std::move(req), std::move(cb));
   auto it = inflight_.find(sid);
   if (it != inflight_.end()) {

@@ -19,6 +19,7 @@
 #include <functional>
 #include <memory>
 #include <string>
+#include <vector>
 #include <unordered_map>
 
 #include "http/client.h"
@@ -29,6 +30,9 @@
 namespace p2pt {
 
 struct ServeConfig {
+  // One upstream base URL, or several separated by commas (extension: e.g. one
+  // inference endpoint per GPU of the node); each request goes to the one
+  // with the fewest requests in flight, ties round-robin.
   std::string upstream;
   std::string advertise = "/";
   uint64_t handshake_timeout_ms = 300000;
@@ -60,7 +64,12 @@ class ServeSession : public std::enable_shared_from_this<ServeSession> {
   struct Inflight {
     std::shared_ptr<http::ClientCall> call;
     bool cancelled = false;
+    size_t up = 0;  // index into upstreams_
   };
+  size_t pick_upstream();
+  void release_upstream(const Inflight& f) {
+    if (f.up < outstanding_.size() && outstanding_[f.up]) outstanding_[f.up]--;
+  }
 
   ServeSession(Reactor& r, std::shared_ptr<MessageChannel> ch, ServeConfig cfg);
   void on_open();
@@ -87,6 +96,9 @@ class ServeSession : public std::enable_shared_from_this<ServeSession> {
   std::unordered_map<uint32_t, Pending> streams_;
   std::unordered_map<uint32_t, Inflight> inflight_;
   bool upstream_paused_ = false;
+  std::vector<std::string> upstreams_;
+  std::vector<size_t> outstanding_;
+  size_t rr_ = 0;
 };
 
 }  // namespace p2pt

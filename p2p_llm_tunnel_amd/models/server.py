@@ -273,6 +273,39 @@ def start_server(host="127.0.0.1", port=0, device="cuda:0", config="tiny", max_b
     return srv, srv.server_address[1], engine
 
 
+def _replicas(a) -> int:
+    """--gpus N: one endpoint process per GPU on ports port..port+N-1 (data-
+    parallel replicas: the model fits one MI355X many times over, so replicas
+    scale throughput with no cross-GPU traffic). `tunnel serve --upstream`
+    takes the printed comma-separated list and balances requests over them by
+    fewest in flight. Each child is a fresh interpreter pinned to its device;
+    the parent never touches the GPU and exits with the first child that dies."""
+    import subprocess
+    import sys
+    base = a.port
+    procs = []
+    for i in range(a.gpus):
+        cmd = [sys.executable, "-m", "p2p_llm_tunnel_amd.models.server", "--host", a.host, "--port", str(base + i),
+               "--device", f"cuda:{i}", "--config", a.config, "--max-batch", str(a.max_batch)]
+        procs.append(subprocess.Popen(cmd))
+    ups = ",".join(f"http://{a.host}:{base + i}" for i in range(a.gpus))
+    print(f"{a.gpus} inference endpoints; use: tunnel serve --upstream {ups}", flush=True)
+    try:
+        while True:
+            for p in procs:
+                rc = p.poll()
+                if rc is not None:
+                    for q in procs:
+                        if q.poll() is None:
+                            q.terminate()
+                    return rc
+            time.sleep(0.5)
+    except KeyboardInterrupt:
+        for p in procs:
+            p.terminate()
+        return 0
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description="GPU-backed OpenAI/Ollama-compatible endpoint")
     ap.add_argument("--host", default="127.0.0.1")
@@ -280,7 +313,11 @@ def main(argv=None):
     ap.add_argument("--device", default="cuda:0")
     ap.add_argument("--config", default="tiny")
     ap.add_argument("--max-batch", type=int, default=8)
+    ap.add_argument("--gpus", type=int, default=0,
+                    help="spawn one endpoint per GPU (cuda:0..N-1) on consecutive ports instead of serving here")
     a = ap.parse_args(argv)
+    if a.gpus > 0:
+        raise SystemExit(_replicas(a))
     srv, port, engine = start_server(a.host, a.port, a.device, a.config, a.max_batch)
     print(f"inference endpoint on http://{a.host}:{port} ({a.config}, {a.device})", flush=True)
     try:

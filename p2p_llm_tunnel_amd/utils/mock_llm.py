@@ -109,6 +109,7 @@ class MockHandler(http.server.BaseHTTPRequestHandler):
             self.wfile.write(b"not found")
 
     def do_POST(self):
+        self.server.posts = getattr(self.server, "posts", 0) + 1  # test hook: requests served (approximate)
         url = urllib.parse.urlparse(self.path)
         body = self._read_body()
         if url.path in ("/v1/chat/completions", "/chat/completions"):

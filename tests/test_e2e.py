@@ -271,3 +271,34 @@ def test_keepalive_ping_pong(mock_upstream, transport):
         assert t.serve.count("sent keepalive ping") >= 4
         assert t.proxy.count("received ping, sent pong") >= 4
         assert t.serve.count("received pong") >= 4
+
+
+def test_multiple_upstreams_least_loaded():
+    """Extension: `--upstream a,b` (e.g. one inference endpoint per GPU of the
+    node) spreads requests over the upstreams by fewest in flight."""
+    import threading
+    from p2p_llm_tunnel_amd.utils import mock_llm
+    servers = [mock_llm.start_in_thread(threaded=True) for _ in range(2)]
+    ups = ",".join(f"http://127.0.0.1:{port}" for _, port in servers)
+    try:
+        with Tunnel(ups, transport="webrtc", serve_extra=["--upstream-prewarm", "0"]) as t:
+            results = []
+
+            def one():
+                c = http.client.HTTPConnection("127.0.0.1", t.proxy_port, timeout=30)
+                c.request("POST", "/v1/chat/completions", body=json.dumps({"stream": True}))
+                r = c.getresponse()
+                results.append((r.status, r.read().count(b"data: ")))
+
+            ths = [threading.Thread(target=one) for _ in range(8)]
+            for th in ths:
+                th.start()
+            for th in ths:
+                th.join()
+            assert results == [(200, 7)] * 8
+        counts = [getattr(srv, "posts", 0) for srv, _ in servers]
+        assert sum(counts) == 8 and min(counts) >= 3, counts  # 8 concurrent streams split ~4/4
+    finally:
+        for srv, _ in servers:
+            srv.shutdown()
+            srv.server_close()
