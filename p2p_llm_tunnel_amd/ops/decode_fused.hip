@@ -160,17 +160,25 @@ __device__ __forceinline__ void mma_batch(frag4 (&acc)[TN], const uint16_t* xrow
 template <int NW, int TN, int EPI, int UM>
 __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
   __shared__ float red[NW][TN][4][kWave];
+  __shared__ float red_ss[NW][kWave];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int bx = blockIdx.x / a.ks;  // column tile
   const int kslice = blockIdx.x % a.ks;
   const bool norm = a.ss_part != nullptr;
 
-  // Row sums of squares (wave 0 only; it runs the epilogue): lane holds row
-  // lane & 15, summing every 4th partial; issued before the weight stream.
-  float ssum = 0.f;
-  if (norm && wv == 0) {
-#pragma unroll 8
-    for (int p = lane >> 4; p < a.ss_parts; p += 4) ssum += a.ss_part[p * kMaxM + (lane & 15)];
+  // Row sums of squares for the folded RMSNorm, spread over every wave (lane:
+  // row lane & 15, partials (lane >> 4) + 4 * wave + 4 * NW * i): up to 8
+  // loads per lane issued ahead of the weight stream and summed only after
+  // it, so they never stall it; combined through LDS before the epilogue.
+  constexpr int kSsRegs = 8;
+  float ssv[kSsRegs];
+  const int ss_p0 = (lane >> 4) + 4 * wv;
+  if (norm) {
+#pragma unroll
+    for (int i = 0; i < kSsRegs; i++) {
+      const int p = ss_p0 + 4 * NW * i;
+      ssv[i] = p < a.ss_parts ? a.ss_part[p * kMaxM + (lane & 15)] : 0.f;
+    }
   }
 
   // A fragment: row lane & 15, k = 32*s + 8*(lane>>4) + j; B fragment: W row n, same k.
@@ -193,6 +201,13 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
   for (int t = 0; t < TN; t++) acc[t] = frag4{0.f, 0.f, 0.f, 0.f};
   for (int s = s0; s < s1; s += UM) mma_batch<UM, TN>(acc, xrow, wrow, a_ok, s, s1);
 
+  if (norm) {
+    float ssum = 0.f;
+#pragma unroll
+    for (int i = 0; i < kSsRegs; i++) ssum += ssv[i];
+    for (int p = ss_p0 + 4 * NW * kSsRegs; p < a.ss_parts; p += 4 * NW) ssum += a.ss_part[p * kMaxM + (lane & 15)];
+    red_ss[wv][lane] = ssum;
+  }
   // K-split reduction through LDS (lane-contiguous: conflict-free).
 #pragma unroll
   for (int t = 0; t < TN; t++)
@@ -236,6 +251,9 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
   const int mrow0 = (lane >> 4) << 2;
   const int c = lane & 15;
   if (norm) {
+    float ssum = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; w++) ssum += red_ss[w][lane];
     ssum = xor32_sum(xor16_sum(ssum));
     const float rs_row = rsqrtf(ssum * (1.f / float(a.K)) + a.eps);  // for row lane & 15
 #pragma unroll
