@@ -7,6 +7,9 @@
 //   proxy: --signal --room --listen (TUNNEL_LISTEN, 127.0.0.1:8000) --turn...
 // Logging filter from RUST_LOG (or TUNNEL_LOG), default info (main.rs:21-25).
 // Extra opt-in flags (defaults keep reference behaviour) are listed in --help.
+#include <sched.h>
+
+#include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -83,6 +86,10 @@ const std::vector<Opt>& ext_opts() {
        "serve: spare pre-connected upstream sockets (follows peak concurrency; 0=off)"},
       {"upstream-prewarm-ttl-ms", "TUNNEL_UPSTREAM_PREWARM_TTL_MS", "1000",
        "serve: close a spare upstream socket unused for this long"},
+      {"secret", "TUNNEL_SECRET", "",
+       "Pre-shared secret both peers must prove (HMAC bound to the DTLS fingerprints); prefer the env var"},
+      {"cpu-affinity", "TUNNEL_CPU_AFFINITY", "",
+       "Pin the process to these CPUs, e.g. 0-3,64 (the NIC's NUMA node, away from inference threads)"},
   };
   return o;
 }
@@ -168,6 +175,44 @@ bool parse_sub(int argc, char** argv, const char* cmd, const std::vector<Opt>& o
   return true;
 }
 
+// "0-3,8,10-11" -> sched_setaffinity. The tunnel is one reactor thread: pin it
+// next to the NIC (same NUMA node) and away from the inference server's cores.
+bool pin_cpus(const std::string& list, std::string* err) {
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  size_t a = 0;
+  while (a < list.size()) {
+    size_t c = list.find(',', a);
+    if (c == std::string::npos) c = list.size();
+    std::string part = list.substr(a, c - a);
+    char* end = nullptr;
+    long lo = strtol(part.c_str(), &end, 10), hi = lo;
+    if (end == part.c_str()) {
+      *err = "expected a CPU number in '" + part + "'";
+      return false;
+    }
+    if (*end == '-') {
+      const char* h = end + 1;
+      hi = strtol(h, &end, 10);
+      if (end == h) {
+        *err = "expected a range end in '" + part + "'";
+        return false;
+      }
+    }
+    if (*end || lo < 0 || hi < lo || hi >= CPU_SETSIZE) {
+      *err = "bad CPU range '" + part + "'";
+      return false;
+    }
+    for (long i = lo; i <= hi; i++) CPU_SET(i, &set);
+    a = c + 1;
+  }
+  if (sched_setaffinity(0, sizeof set, &set) != 0) {
+    *err = strerror(errno);
+    return false;
+  }
+  return true;
+}
+
 uint64_t num(const std::map<std::string, std::string>& m, const char* k) {
   auto it = m.find(k);
   return it == m.end() ? 0 : strtoull(it->second.c_str(), nullptr, 10);
@@ -243,6 +288,15 @@ int main(int argc, char** argv) {
   cfg.upstream_prewarm = num(m, "upstream-prewarm");
   cfg.upstream_prewarm_ttl_ms = num(m, "upstream-prewarm-ttl-ms");
   cfg.busy_poll_us = num(m, "busy-poll-us");
+  cfg.secret = m["secret"];
+  if (!m["cpu-affinity"].empty()) {
+    std::string err;
+    if (!pin_cpus(m["cpu-affinity"], &err)) {
+      fprintf(stderr, "error: --cpu-affinity %s: %s\n", m["cpu-affinity"].c_str(), err.c_str());
+      return 2;
+    }
+    LOG_INFO("tunnel", "pinned to CPUs %s", m["cpu-affinity"].c_str());
+  }
 
   if (cmd == "serve") {
     LOG_INFO("tunnel", "starting serve mode: signal=%s, room=%s, upstream=%s, advertise=%s", cfg.signal.c_str(),

@@ -31,6 +31,17 @@ std::array<uint8_t, 20> hmac_sha1(const void* key, size_t klen, const void* p, s
   return out;
 }
 
+std::array<uint8_t, 32> hmac_sha256(const void* key, size_t klen, const void* p, size_t n) {
+  std::array<uint8_t, 32> out{};
+  unsigned int len = 0;
+  HMAC(EVP_sha256(), key, int(klen), static_cast<const uint8_t*>(p), n, out.data(), &len);
+  return out;
+}
+
+bool equal_ct(std::string_view a, std::string_view b) {
+  return a.size() == b.size() && CRYPTO_memcmp(a.data(), b.data(), a.size()) == 0;
+}
+
 static const char kB64[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
 
 std::string base64_encode(const void* data, size_t n) {

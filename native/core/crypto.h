@@ -18,6 +18,9 @@ namespace p2pt {
 std::array<uint8_t, 20> sha1(const void* p, size_t n);
 std::array<uint8_t, 32> sha256(const void* p, size_t n);
 std::array<uint8_t, 20> hmac_sha1(const void* key, size_t klen, const void* p, size_t n);
+std::array<uint8_t, 32> hmac_sha256(const void* key, size_t klen, const void* p, size_t n);
+// Constant-time equality (MAC comparison).
+bool equal_ct(std::string_view a, std::string_view b);
 std::array<uint8_t, 16> md5(const void* p, size_t n);
 
 std::string base64_encode(const void* p, size_t n);

@@ -3,6 +3,8 @@
 #include <algorithm>
 #include <cstring>
 
+#include "core/crypto.h"
+
 namespace p2pt::proto {
 
 std::optional<MsgType> msg_type_from_u8(uint8_t v) {
@@ -144,7 +146,21 @@ Json Hello::to_json() const {
   j.set("min_version", Json(min_version));
   j.set("max_version", Json(max_version));
   j.set("features", str_array(features));
+  if (!psk_nonce.empty()) j.set("psk_nonce", Json(psk_nonce));
+  if (!psk_mac.empty()) j.set("psk_mac", Json(psk_mac));
   return j;
+}
+
+// Optional string member (absent is fine; present must be a string).
+static bool opt_str(const Json& j, const char* k, std::string& out, std::string* err) {
+  const Json* v = j.get(k);
+  if (!v) return true;
+  if (!v->is_string()) {
+    if (err) *err = std::string("field '") + k + "' must be a string";
+    return false;
+  }
+  out = v->as_string();
+  return true;
 }
 
 bool Hello::from_json(const Json& j, Hello& out, std::string* err) {
@@ -153,13 +169,15 @@ bool Hello::from_json(const Json& j, Hello& out, std::string* err) {
     return false;
   }
   return get_str(j, "proto", out.proto, err) && get_u32(j, "min_version", out.min_version, err) &&
-         get_u32(j, "max_version", out.max_version, err) && get_str_array(j, "features", out.features, err);
+         get_u32(j, "max_version", out.max_version, err) && get_str_array(j, "features", out.features, err) &&
+         opt_str(j, "psk_nonce", out.psk_nonce, err) && opt_str(j, "psk_mac", out.psk_mac, err);
 }
 
 Json Agree::to_json() const {
   Json j = Json::object();
   j.set("version", Json(version));
   j.set("features", str_array(features));
+  if (!psk_mac.empty()) j.set("psk_mac", Json(psk_mac));
   return j;
 }
 
@@ -168,7 +186,15 @@ bool Agree::from_json(const Json& j, Agree& out, std::string* err) {
     if (err) *err = "expected object";
     return false;
   }
-  return get_u32(j, "version", out.version, err) && get_str_array(j, "features", out.features, err);
+  return get_u32(j, "version", out.version, err) && get_str_array(j, "features", out.features, err) &&
+         opt_str(j, "psk_mac", out.psk_mac, err);
+}
+
+std::string psk_mac(const std::string& secret, const char* role, const std::string& nonce,
+                    const std::string& binding) {
+  std::string msg = std::string("p2pt-psk|") + role + "|" + nonce + "|" + binding;
+  auto mac = hmac_sha256(secret.data(), secret.size(), msg.data(), msg.size());
+  return hex_encode(mac.data(), mac.size());
 }
 
 const std::vector<std::string>& our_features() {

@@ -74,6 +74,9 @@ struct Hello {
   uint32_t min_version = 1;
   uint32_t max_version = kProtocolVersion;
   std::vector<std::string> features{"sse"};
+  // "psk" extension (only with --secret; serialised only when set, so a
+  // reference peer sees the reference's HELLO): nonce and proof of the secret.
+  std::string psk_nonce, psk_mac;
   Json to_json() const;
   static bool from_json(const Json& j, Hello& out, std::string* err);
 };
@@ -81,9 +84,19 @@ struct Hello {
 struct Agree {
   uint32_t version = 1;
   std::vector<std::string> features;
+  std::string psk_mac;  // "psk" extension: the serve side's proof
   Json to_json() const;
   static bool from_json(const Json& j, Agree& out, std::string* err);
 };
+
+// Pre-shared-secret proof (extension "psk", the reference README's planned
+// `--secret`): hex HMAC-SHA256(secret, "p2pt-psk|" role "|" nonce "|" binding),
+// role "hello" (proxy) or "agree" (serve). `binding` names the secured channel
+// (both DTLS certificate fingerprints, sorted), so a proof observed on one
+// channel is useless on another and a man in the middle — who must terminate
+// DTLS with its own certificate on each leg — cannot relay it.
+std::string psk_mac(const std::string& secret, const char* role, const std::string& nonce,
+                    const std::string& binding);
 
 // Features this build understands. "sse" is the reference's only feature;
 // "cancel" (client-disconnect propagation) is only *acted on* when

@@ -65,6 +65,22 @@ size_t DataChannel::body_chunk() const {
   return mtu - 12 - 16 - proto::kHeaderLen;  // SCTP common + DATA chunk headers, frame header
 }
 
+// Both DTLS certificate fingerprints (ours and the one the remote SDP pinned
+// and the handshake verified), normalised and sorted: the same string on both
+// peers, different on each leg of a man-in-the-middle.
+std::string DataChannel::channel_binding() const {
+  auto pc = pc_.lock();
+  if (!pc) return "";
+  auto norm = [](std::string fp) {
+    size_t sp = fp.find(' ');
+    if (sp != std::string::npos) fp = fp.substr(sp + 1);
+    for (auto& c : fp) c = char(toupper(static_cast<unsigned char>(c)));
+    return fp;
+  };
+  std::string a = norm(DtlsTransport::local_fingerprint()), b = norm(pc->remote_.fingerprint);
+  return a < b ? a + "|" + b : b + "|" + a;
+}
+
 std::string DataChannel::describe() const {
   auto pc = pc_.lock();
   return "webrtc:" + label_ + (pc ? " " + pc->describe_path() : "");

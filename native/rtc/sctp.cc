@@ -458,6 +458,9 @@ void SctpAssociation::closed(const std::string& why) {
 }
 
 void SctpAssociation::handle_heartbeat(const uint8_t* c, size_t len) {
+  // The echo must fit one packet (the peer chose its size; flush() never
+  // splits a chunk): oversized probes go unanswered.
+  if (len + 4 + kCommonHdr > cfg_.mtu) return;
   queue_control(kHeartbeatAck, 0, std::vector<uint8_t>(c, c + len));
 }
 

@@ -238,6 +238,7 @@ int run_app(const AppConfig& cfg) {
         sc.pong_timeout_ms = cfg.pong_timeout_ms;
         sc.upstream_prewarm = cfg.upstream_prewarm;
         sc.upstream_prewarm_ttl_ms = cfg.upstream_prewarm_ttl_ms;
+        sc.secret = cfg.secret;
         st.serve = ServeSession::start(r, ch, sc, [&](const std::string& e) { on_fail(e); });
       } else {
         LOG_INFO(kT, "WebRTC connected, starting proxy...");
@@ -248,6 +249,7 @@ int run_app(const AppConfig& cfg) {
         pc.ping_interval_ms = cfg.ping_interval_ms;
         pc.pong_timeout_ms = cfg.pong_timeout_ms;
         pc.listen_early = cfg.listen_early;
+        pc.secret = cfg.secret;
         st.proxy = ProxySession::start(r, ch, pc, [&](const std::string& e) { on_fail(e); });
         st.early.session = st.proxy;
       }

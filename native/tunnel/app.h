@@ -59,6 +59,7 @@ struct AppConfig {
   size_t upstream_prewarm = 4;
   uint64_t upstream_prewarm_ttl_ms = 1000;
   uint64_t busy_poll_us = 0;
+  std::string secret;  // "psk" extension; empty = reference behaviour
 };
 
 // Establishes one MessageChannel (signalling + WebRTC, or a TCP debug link).

@@ -35,6 +35,10 @@ class MessageChannel {
   // (reference protocol.rs:10-12); a transport whose packets are smaller may
   // ask for frames that fit one packet so they are never fragmented/reassembled.
   virtual size_t body_chunk() const { return proto::kMaxBodyChunk; }
+  // Identifies the secured channel for handshake proofs (psk extension): both
+  // peers compute the same string. Empty when the transport has no such
+  // identity (the TCP debug transport).
+  virtual std::string channel_binding() const { return ""; }
 
   // Message arrived (whole message, zero-copy view where possible).
   std::function<void(Bytes)> on_message;

@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cstdio>
 
+#include "core/crypto.h"
 #include "core/log.h"
 #include "core/net.h"
 #include "http/http.h"
@@ -504,6 +505,14 @@ void ProxySession::on_open() {
   LOG_INFO(kT, "data channel ready, performing handshake...");
   proto::Hello hello;
   hello.features = proto::our_features();
+  if (!cfg_.secret.empty()) {  // psk extension: prove the shared secret on this channel
+    uint8_t nonce[16];
+    random_bytes(nonce, sizeof nonce);
+    psk_nonce_ = hex_encode(nonce, sizeof nonce);
+    hello.features.push_back("psk");
+    hello.psk_nonce = psk_nonce_;
+    hello.psk_mac = proto::psk_mac(cfg_.secret, "hello", psk_nonce_, ch_->channel_binding());
+  }
   sched_->send(proto::make_hello(hello));
   hello_sent_ = true;
   LOG_INFO(kT, "sent HELLO");
@@ -557,6 +566,16 @@ void ProxySession::on_agree(const proto::Frame& f) {
     return;
   }
   LOG_INFO(kT, "received AGREE: %s", j.dump().c_str());
+  if (!cfg_.secret.empty()) {
+    bool agreed = std::find(agree.features.begin(), agree.features.end(), "psk") != agree.features.end();
+    if (!agreed ||
+        !equal_ct(agree.psk_mac, proto::psk_mac(cfg_.secret, "agree", psk_nonce_, ch_->channel_binding()))) {
+      LOG_ERROR(kT, "authentication failed: peer did not prove the shared secret");
+      metrics::counter_add("tunnel_auth_failures_total");
+      stop("authentication failed: peer did not prove the shared secret");
+      return;
+    }
+  }
   cancel_feature_ = std::find(agree.features.begin(), agree.features.end(), "cancel") != agree.features.end();
   ready_ = true;
   last_pong_ms_ = Reactor::now_ms();

@@ -39,6 +39,9 @@ struct ProxyConfig {
   bool listen_early = false;
   size_t high_water = 4 << 20;
   size_t low_water = 1 << 20;
+  // Pre-shared secret ("psk" extension, --secret): HELLO carries a proof and
+  // an AGREE without the serve side's proof ends the session.
+  std::string secret;
   // Called with the bound address once listening (tests/bench use port 0).
   std::function<void(const std::string&)> on_listening;
 };
@@ -93,6 +96,7 @@ class ProxySession : public std::enable_shared_from_this<ProxySession> {
   bool ready_ = false;
   bool stopped_ = false;
   bool cancel_feature_ = false;
+  std::string psk_nonce_;  // psk extension: the nonce our HELLO carried
   uint64_t agree_timer_ = 0;
   uint64_t ping_timer_ = 0;
   uint64_t last_pong_ms_ = 0;

@@ -2,6 +2,7 @@
 
 #include <algorithm>
 
+#include "core/crypto.h"
 #include "core/log.h"
 #include "tunnel/metrics.h"
 
@@ -134,10 +135,25 @@ void ServeSession::on_hello(const proto::Frame& f) {
   }
   LOG_INFO(kT, "received HELLO: %s", j.dump().c_str());
   proto::Agree agree;
-  if (!proto::agree_from_hello(hello, agree, &err)) {
+  std::vector<std::string> ours = proto::our_features();
+  const std::string binding = ch_->channel_binding();
+  if (!cfg_.secret.empty()) {
+    // psk extension: the proxy must prove the shared secret on this channel.
+    bool offered = std::find(hello.features.begin(), hello.features.end(), "psk") != hello.features.end();
+    if (!offered || hello.psk_nonce.size() < 32 ||
+        !equal_ct(hello.psk_mac, proto::psk_mac(cfg_.secret, "hello", hello.psk_nonce, binding))) {
+      LOG_ERROR(kT, "authentication failed: HELLO without a valid shared-secret proof");
+      metrics::counter_add("tunnel_auth_failures_total");
+      stop("authentication failed: HELLO without a valid shared-secret proof");
+      return;
+    }
+    ours.push_back("psk");
+  }
+  if (!proto::agree_from_hello(hello, agree, &err, ours)) {
     stop("handshake failed: " + err);
     return;
   }
+  if (!cfg_.secret.empty()) agree.psk_mac = proto::psk_mac(cfg_.secret, "agree", hello.psk_nonce, binding);
   cancel_feature_ = std::find(agree.features.begin(), agree.features.end(), "cancel") != agree.features.end();
   sched_->send(proto::make_agree(agree));
   handshaken_ = true;

@@ -43,6 +43,9 @@ struct ServeConfig {
   // Spare pre-connected upstream sockets (0 = connect per request like reqwest).
   size_t upstream_prewarm = 4;
   uint64_t upstream_prewarm_ttl_ms = 1000;  // close unused warm sockets after this idle time
+  // Pre-shared secret ("psk" extension, --secret): when set, a HELLO without a
+  // valid proof ends the session; empty = room name only (reference).
+  std::string secret;
 };
 
 class ServeSession : public std::enable_shared_from_this<ServeSession> {

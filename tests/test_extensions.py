@@ -117,5 +117,21 @@ def test_cli_help_version_and_missing_args():
     assert "connecting to signaling server: ws://127.0.0.1:1" in out.stdout  # env fallbacks honoured
 
 
+def test_cpu_affinity(mock_upstream):
+    """--cpu-affinity pins the reactor thread (NUMA placement next to the NIC)."""
+    import os
+    import subprocess
+    cpu = sorted(os.sched_getaffinity(0))[-1]
+    with Tunnel(mock_upstream, transport="webrtc", serve_extra=["--cpu-affinity", str(cpu)]) as t:
+        assert urllib.request.urlopen(t.url + "/health", timeout=10).read() == b"ok"
+        status = open(f"/proc/{t.serve.popen.pid}/status").read()
+        allowed = [l.split(":", 1)[1].strip() for l in status.splitlines() if l.startswith("Cpus_allowed_list")]
+        assert allowed == [str(cpu)]
+        assert f"pinned to CPUs {cpu}" in t.serve.text()
+    out = subprocess.run([binary("tunnel"), "serve", "--room", "r", "--upstream", "http://x", "--cpu-affinity", "3-1"],
+                         capture_output=True, text=True)
+    assert out.returncode == 2 and "bad CPU range" in out.stderr
+
+
 def test_backoff_schedule(native):
     assert [native.backoff_secs(n) for n in range(1, 9)] == [2, 4, 8, 16, 32, 60, 60, 60]
