@@ -137,6 +137,8 @@ def main():
         res["sse"] += sse_matrix("webrtc", "python", [1, 2, 4, 8], 3, threaded=False)
     # BASELINE config #2: Ollama /api/generate NDJSON stream, up to 8 concurrent streams.
     res["sse"] += sse_matrix("webrtc", "native", [1, 8], a.steps, path="/api/generate")
+    # Beyond the 1-8 stream curve: 64 and 256 concurrent SSE streams on one tunnel.
+    res["sse"] += sse_matrix("webrtc", "native", [64, 256], max(2, a.steps // 2))
     # BASELINE config #4: NAT traversal (emulated port-restricted NATs, STUN-only ICE).
     res["sse"] += sse_matrix("webrtc", "native", [1, 8], a.steps, nat="port-restricted")
     for bp in [int(x) for x in a.busy_poll.split(",") if x]:
