@@ -34,7 +34,7 @@ class ClientConnPool : public std::enable_shared_from_this<ClientConnPool> {
     std::string host;
     uint16_t port = 0;
     bool tls = false;
-    size_t min = 0, max = 64;
+    size_t min = 0, max = 512;  // warm-socket cap: follows peaks of up to 512 concurrent requests
     size_t peak = 0;          // recent peak of in-flight requests
     uint64_t peak_at_ms = 0;
     size_t inflight = 0;
@@ -43,6 +43,7 @@ class ClientConnPool : public std::enable_shared_from_this<ClientConnPool> {
     uint64_t retry_timer = 0;
     uint64_t ttl_ms = 1000;
     uint64_t expiry_timer = 0;
+    uint64_t topup_timer = 0;
     std::vector<std::shared_ptr<TcpConn>> ready;
     std::vector<uint64_t> ready_at;  // parallel to ready
     std::deque<WarmWaiter> waiters;  // calls waiting for the next warm socket
@@ -138,11 +139,30 @@ class ClientConnPool : public std::enable_shared_from_this<ClientConnPool> {
       w.peak = w.inflight;
       w.peak_at_ms = now;
     }
-    replenish(key);
+    schedule_topup(key, w);
   }
   void call_finished(const std::string& key) {
     auto it = warm_.find(key);
-    if (it != warm_.end() && it->second.inflight) it->second.inflight--;
+    if (it == warm_.end()) return;
+    if (it->second.inflight) it->second.inflight--;
+    // Refill toward the recent peak between bursts, so the next burst of
+    // requests finds connected sockets instead of queueing for connects.
+    schedule_topup(key, it->second);
+  }
+  // Top up a little later, not inside the burst that is taking the sockets:
+  // connect() calls would sit on the critical path of the requests still being
+  // parsed in this and the next reactor iterations.
+  void schedule_topup(const std::string& key, Warm& w) {
+    if (w.topup_timer) return;
+    std::weak_ptr<ClientConnPool> self = shared_from_this();
+    w.topup_timer = r_.call_later_ms(2, [self, key] {
+      auto p = self.lock();
+      if (!p) return;
+      auto it2 = p->warm_.find(key);
+      if (it2 == p->warm_.end()) return;
+      it2->second.topup_timer = 0;
+      p->replenish(key);
+    });
   }
 
   void replenish(const std::string& key) {
@@ -265,6 +285,7 @@ class ClientConnPool : public std::enable_shared_from_this<ClientConnPool> {
     for (auto& kv : warm) {
       if (kv.second.retry_timer) r_.cancel(kv.second.retry_timer);
       if (kv.second.expiry_timer) r_.cancel(kv.second.expiry_timer);
+      if (kv.second.topup_timer) r_.cancel(kv.second.topup_timer);
       if (!kv.second.waiters.empty())
         r_.post([ws = std::move(kv.second.waiters)]() mutable {
           for (auto& fn : ws) fn(nullptr, "client shut down");
