@@ -316,6 +316,19 @@ void DtlsTransport::setup_fast_path() {
                EVP_CIPHER_CTX_ctrl(t, EVP_CTRL_GCM_SET_TAG, 16, rec + kRecHdr + kExplicit + ctlen) == 1 &&
                EVP_DecryptFinal_ex(t, out + l, &l2) == 1 && memcmp(out, kProbe, ctlen) == 0;
     EVP_CIPHER_CTX_free(t);
+    // The vector AES-GCM must open OpenSSL's probe too, or it stays unused.
+    if (probe_ok && AesGcm::supported() && !getenv("TUNNEL_DTLS_EVP")) {
+      auto w = std::make_unique<AesGcm>(), r = std::make_unique<AesGcm>();
+      uint8_t ct[sizeof kProbe];
+      if (w->init(wkey, klen) && r->init(rkey, klen) &&
+          w->open(nonce, aad, 13, rec + kRecHdr + kExplicit, ct, ctlen, rec + kRecHdr + kExplicit + ctlen) &&
+          memcmp(ct, kProbe, ctlen) == 0) {
+        wgcm_ = std::move(w);
+        rgcm_ = std::move(r);
+      } else {
+        LOG_WARN(kT, "vector AES-GCM self-check failed; using OpenSSL's EVP for records");
+      }
+    }
   }
   OPENSSL_cleanse(kb, sizeof kb);
   if (!probe_ok) {
@@ -323,7 +336,7 @@ void DtlsTransport::setup_fast_path() {
     return;
   }
   fast_rx_ = true;
-  LOG_DEBUG(kT, "DTLS own record layer armed (%s)", cipher().c_str());
+  LOG_DEBUG(kT, "DTLS own record layer armed (%s, %s)", cipher().c_str(), wgcm_ ? "VAES AES-GCM" : "EVP AES-GCM");
 }
 
 bool DtlsTransport::fast_decrypt(uint8_t* rec, size_t len, uint8_t type, uint64_t seq, uint8_t** pt, size_t* pt_len) {
@@ -342,12 +355,16 @@ bool DtlsTransport::fast_decrypt(uint8_t* rec, size_t len, uint8_t type, uint64_
   aad[9] = rec[1];
   aad[10] = rec[2];
   wr16(aad + 11, uint16_t(ctlen));
-  int l = 0, l2 = 0;
-  if (EVP_DecryptInit_ex(rctx_, nullptr, nullptr, nullptr, nonce) != 1 ||
-      EVP_DecryptUpdate(rctx_, nullptr, &l, aad, 13) != 1 || EVP_DecryptUpdate(rctx_, ct, &l, ct, int(ctlen)) != 1 ||
-      EVP_CIPHER_CTX_ctrl(rctx_, EVP_CTRL_GCM_SET_TAG, 16, ct + ctlen) != 1 ||
-      EVP_DecryptFinal_ex(rctx_, ct + l, &l2) != 1)
-    return false;
+  if (rgcm_) {
+    if (!rgcm_->open(nonce, aad, 13, ct, ct, ctlen, ct + ctlen)) return false;
+  } else {
+    int l = 0, l2 = 0;
+    if (EVP_DecryptInit_ex(rctx_, nullptr, nullptr, nullptr, nonce) != 1 ||
+        EVP_DecryptUpdate(rctx_, nullptr, &l, aad, 13) != 1 || EVP_DecryptUpdate(rctx_, ct, &l, ct, int(ctlen)) != 1 ||
+        EVP_CIPHER_CTX_ctrl(rctx_, EVP_CTRL_GCM_SET_TAG, 16, ct + ctlen) != 1 ||
+        EVP_DecryptFinal_ex(rctx_, ct + l, &l2) != 1)
+      return false;
+  }
   if (!rx_any_ || seq > rx_max_) {
     uint64_t sh = rx_any_ ? seq - rx_max_ : 64;
     rx_bitmap_ = sh >= 64 ? 1 : (rx_bitmap_ << sh) | 1;
@@ -377,6 +394,16 @@ bool DtlsTransport::fast_encrypt_into(uint8_t* out, uint8_t type, const iovec* i
   aad[9] = 0xFE;
   aad[10] = 0xFD;
   wr16(aad + 11, uint16_t(total));
+  if (wgcm_) {  // gather, then encrypt in place (the copy is L1-resident)
+    uint8_t* o = out + kRecHdr + kExplicit;
+    for (int i = 0; i < cnt; i++) {
+      memcpy(o, iov[i].iov_base, iov[i].iov_len);
+      o += iov[i].iov_len;
+    }
+    o = out + kRecHdr + kExplicit;
+    wgcm_->seal(nonce, aad, 13, o, o, total, o + total);
+    return true;
+  }
   int l = 0;
   if (EVP_EncryptInit_ex(wctx_, nullptr, nullptr, nullptr, nonce) != 1 ||
       EVP_EncryptUpdate(wctx_, nullptr, &l, aad, 13) != 1)

@@ -34,6 +34,7 @@
 #include <string>
 #include <vector>
 
+#include "core/aesgcm.h"
 #include "core/buf.h"
 #include "core/reactor.h"
 
@@ -118,6 +119,8 @@ class DtlsTransport : public std::enable_shared_from_this<DtlsTransport> {
   std::string captured_;
   EVP_CIPHER_CTX* wctx_ = nullptr;
   EVP_CIPHER_CTX* rctx_ = nullptr;
+  // VAES/VPCLMULQDQ AES-GCM (core/aesgcm.h) when the CPU has it; EVP otherwise.
+  std::unique_ptr<AesGcm> wgcm_, rgcm_;
   uint8_t wiv_[4] = {}, riv_[4] = {};
   uint64_t wseq_ = 0;              // next epoch-1 sequence number we send
   uint64_t ossl_max_wseq_ = 0;     // highest epoch-1 sequence OpenSSL wrote

@@ -2,6 +2,9 @@
 #include <cstring>
 #include <vector>
 
+#include <openssl/evp.h>
+
+#include "core/aesgcm.h"
 #include "core/crypto.h"
 #include "core/json.h"
 #include "core/reactor.h"
@@ -214,4 +217,104 @@ TEST(ws_frame_codec) {
   ws::FrameParser strict(true);
   std::string unmasked = ws::encode_frame(ws::Op::Text, "a", false);
   CHECK(!strict.feed(reinterpret_cast<const uint8_t*>(unmasked.data()), unmasked.size(), [](ws::Op, bool, std::string&&) {}));
+}
+
+// ---------------------------------------------------------------- AES-GCM
+namespace {
+bool evp_gcm(bool enc, const std::vector<uint8_t>& key, const uint8_t* iv, const std::vector<uint8_t>& aad,
+             const std::vector<uint8_t>& in, std::vector<uint8_t>& out, uint8_t tag[16]) {
+  EVP_CIPHER_CTX* c = EVP_CIPHER_CTX_new();
+  const EVP_CIPHER* ci = key.size() == 16 ? EVP_aes_128_gcm() : EVP_aes_256_gcm();
+  int l = 0;
+  out.assign(in.size() + 16, 0);
+  bool ok = (enc ? EVP_EncryptInit_ex(c, ci, nullptr, key.data(), iv) : EVP_DecryptInit_ex(c, ci, nullptr, key.data(), iv)) == 1;
+  if (!aad.empty()) ok = ok && EVP_CipherUpdate(c, nullptr, &l, aad.data(), int(aad.size())) == 1;
+  ok = ok && EVP_CipherUpdate(c, out.data(), &l, in.data(), int(in.size())) == 1;
+  if (!enc) ok = ok && EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_SET_TAG, 16, tag) == 1;
+  int l2 = 0;
+  ok = ok && EVP_CipherFinal_ex(c, out.data() + l, &l2) == 1;
+  if (enc) ok = ok && EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_GET_TAG, 16, tag) == 1;
+  out.resize(in.size());
+  EVP_CIPHER_CTX_free(c);
+  return ok;
+}
+std::vector<uint8_t> unhex(const char* h) {
+  std::vector<uint8_t> v;
+  for (; h[0] && h[1]; h += 2) v.push_back(uint8_t(std::stoi(std::string(h, 2), nullptr, 16)));
+  return v;
+}
+}  // namespace
+
+TEST(aesgcm_spec_vectors) {
+  if (!AesGcm::supported()) return;  // EVP path only on this CPU
+  // GCM specification test cases 1-2 (zero key, zero IV) and 3 (no AAD, 64 B).
+  AesGcm g;
+  std::vector<uint8_t> k0(16, 0);
+  CHECK(g.init(k0.data(), 16));
+  uint8_t iv[12] = {}, tag[16];
+  g.seal(iv, nullptr, 0, nullptr, nullptr, 0, tag);
+  CHECK(memcmp(tag, unhex("58e2fccefa7e3061367f1d57a4e7455a").data(), 16) == 0);
+  uint8_t z[16] = {}, c[16];
+  g.seal(iv, nullptr, 0, z, c, 16, tag);
+  CHECK(memcmp(c, unhex("0388dace60b6a392f328c2b971b2fe78").data(), 16) == 0);
+  CHECK(memcmp(tag, unhex("ab6e47d42cec13bdf53a67b21257bddf").data(), 16) == 0);
+  auto k3 = unhex("feffe9928665731c6d6a8f9467308308");
+  auto iv3 = unhex("cafebabefacedbaddecaf888");
+  auto p3 = unhex("d9313225f88406e5a55909c5aff5269a86a7a9531534f7da2e4c303d8a318a721c3c0c95956809532fcf0e2449a6b525b16aedf5aa0de657ba637b391aafd255");
+  CHECK(g.init(k3.data(), 16));
+  std::vector<uint8_t> c3(p3.size());
+  g.seal(iv3.data(), nullptr, 0, p3.data(), c3.data(), p3.size(), tag);
+  CHECK(c3 == unhex("42831ec2217774244b7221b784d0d49ce3aa212f2c02a4e035c17e2329aca12e21d514b25466931c7d8f6a5aac84aa051ba30b396a0aac973d58e091473f5985"));
+  CHECK(memcmp(tag, unhex("4d5c2af327cd64a62cf35abd2ba6fab4").data(), 16) == 0);
+  std::vector<uint8_t> back(p3.size());
+  CHECK(g.open(iv3.data(), nullptr, 0, c3.data(), back.data(), c3.size(), tag));
+  CHECK(back == p3);
+}
+
+TEST(aesgcm_matches_evp_and_rejects_tampering) {
+  if (!AesGcm::supported()) return;
+  uint32_t seed = 12345;
+  auto rnd = [&] { return seed = seed * 1103515245u + 12345u, seed >> 8; };
+  std::vector<size_t> sizes;
+  for (size_t n = 0; n <= 600; n++) sizes.push_back(n);
+  for (size_t n : {1023, 1024, 1025, 1200, 4095, 4096, 16383, 16384, 16385, 65000}) sizes.push_back(n);
+  for (size_t klen : {16, 32}) {
+    for (size_t n : sizes) {
+      std::vector<uint8_t> key(klen), aad(rnd() % 3 == 0 ? 0 : (rnd() % 40)), pt(n);
+      uint8_t iv[12];
+      for (auto& b : key) b = uint8_t(rnd());
+      for (auto& b : aad) b = uint8_t(rnd());
+      for (auto& b : pt) b = uint8_t(rnd());
+      for (auto& b : iv) b = uint8_t(rnd());
+      if (n % 7 == 0) memset(iv + 8, 0xff, 4);  // counter bytes next to the IV stay the IV's
+      AesGcm g;
+      CHECK(g.init(key.data(), klen));
+      std::vector<uint8_t> ref;
+      uint8_t rtag[16], tag[16];
+      CHECK(evp_gcm(true, key, iv, aad, pt, ref, rtag));
+      std::vector<uint8_t> ct(n + 1);
+      g.seal(iv, aad.data(), aad.size(), pt.data(), ct.data() + (n & 1), n, tag);  // odd/even alignment
+      CHECK(memcmp(ct.data() + (n & 1), ref.data(), n) == 0);
+      CHECK(memcmp(tag, rtag, 16) == 0);
+      // in-place round trip
+      std::vector<uint8_t> buf = pt;
+      g.seal(iv, aad.data(), aad.size(), buf.data(), buf.data(), n, tag);
+      CHECK(memcmp(buf.data(), ref.data(), n) == 0);
+      CHECK(g.open(iv, aad.data(), aad.size(), buf.data(), buf.data(), n, tag));
+      CHECK(buf == pt);
+      // tampering: one flipped bit anywhere -> rejected, output zeroed
+      if (n) {
+        std::vector<uint8_t> bad = ref;
+        bad[rnd() % n] ^= uint8_t(1u << (rnd() % 8));
+        std::vector<uint8_t> o(n, 0xAA);
+        CHECK(!g.open(iv, aad.data(), aad.size(), bad.data(), o.data(), n, rtag));
+        CHECK(o == std::vector<uint8_t>(n, 0));
+      }
+      uint8_t btag[16];
+      memcpy(btag, rtag, 16);
+      btag[rnd() % 16] ^= 0x80;
+      std::vector<uint8_t> o(n);
+      CHECK(!g.open(iv, aad.data(), aad.size(), ref.data(), o.data(), n, btag));
+    }
+  }
 }
