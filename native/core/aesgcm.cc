@@ -186,57 +186,90 @@ __m128i ghash(const uint8_t (*hp)[16], __m128i y, const uint8_t* p, size_t n) {
 }
 
 // ---------------------------------------------------------------- CTR
-// out = in ^ E(IV || ctr), E(IV || ctr+1), ... (32-bit big-endian counter).
-void ctr_xor(const uint8_t (*rk)[64], int nr, const uint8_t iv[12], uint32_t ctr, const uint8_t* in, uint8_t* out,
-             size_t n) {
-  alignas(16) uint8_t b[16];
-  memcpy(b, iv, 12);
-  memcpy(b + 12, &ctr, 4);  // native (little-endian) counter word; byte-swapped per block below
-  const __m512i base = _mm512_broadcast_i32x4(_mm_load_si128(reinterpret_cast<const __m128i*>(b)));
-  const __m512i cmask =
-      _mm512_broadcast_i32x4(_mm_set_epi8(12, 13, 14, 15, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0));
-  const __m512i inc4 = _mm512_set_epi32(4, 0, 0, 0, 4, 0, 0, 0, 4, 0, 0, 0, 4, 0, 0, 0);
-  __m512i c = _mm512_add_epi32(base, _mm512_set_epi32(3, 0, 0, 0, 2, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0));
-  const __m512i k0 = rk512(rk, 0), klast = rk512(rk, nr);
-  while (n >= 256) {
-    const __m512i c1 = _mm512_add_epi32(c, inc4), c2 = _mm512_add_epi32(c1, inc4), c3 = _mm512_add_epi32(c2, inc4);
-    __m512i b0 = _mm512_xor_si512(_mm512_shuffle_epi8(c, cmask), k0);
-    __m512i b1 = _mm512_xor_si512(_mm512_shuffle_epi8(c1, cmask), k0);
-    __m512i b2 = _mm512_xor_si512(_mm512_shuffle_epi8(c2, cmask), k0);
-    __m512i b3 = _mm512_xor_si512(_mm512_shuffle_epi8(c3, cmask), k0);
-    c = _mm512_add_epi32(c3, inc4);
-    for (int r = 1; r < nr; r++) {
-      const __m512i k = rk512(rk, r);
-      b0 = _mm512_aesenc_epi128(b0, k);
-      b1 = _mm512_aesenc_epi128(b1, k);
-      b2 = _mm512_aesenc_epi128(b2, k);
-      b3 = _mm512_aesenc_epi128(b3, k);
-    }
-    b0 = _mm512_aesenclast_epi128(b0, klast);
-    b1 = _mm512_aesenclast_epi128(b1, klast);
-    b2 = _mm512_aesenclast_epi128(b2, klast);
-    b3 = _mm512_aesenclast_epi128(b3, klast);
-    _mm512_storeu_si512(out, _mm512_xor_si512(b0, _mm512_loadu_si512(in)));
-    _mm512_storeu_si512(out + 64, _mm512_xor_si512(b1, _mm512_loadu_si512(in + 64)));
-    _mm512_storeu_si512(out + 128, _mm512_xor_si512(b2, _mm512_loadu_si512(in + 128)));
-    _mm512_storeu_si512(out + 192, _mm512_xor_si512(b3, _mm512_loadu_si512(in + 192)));
-    in += 256;
-    out += 256;
-    n -= 256;
+// Plaintext/ciphertext sources for the CTR passes: a flat buffer, or the
+// gather list of an outgoing record (SCTP headers inline, payload slices
+// referenced), read 64 bytes at a time so sealing needs no gather copy.
+struct FlatSrc {
+  const uint8_t* p;
+  __m512i next64() {
+    const __m512i v = _mm512_loadu_si512(p);
+    p += 64;
+    return v;
   }
-  while (n) {
-    __m512i b0 = _mm512_xor_si512(_mm512_shuffle_epi8(c, cmask), k0);
+  __m512i last(size_t n) { return _mm512_maskz_loadu_epi8(~0ULL >> (64 - n), p); }  // 0 < n < 64
+};
+
+struct GatherSrc {
+  const iovec* iov;
+  int cnt;
+  int i = 0;
+  size_t pos = 0;
+  __m512i next64() {
+    while (i < cnt && pos == iov[i].iov_len) {
+      i++;
+      pos = 0;
+    }
+    if (i < cnt && iov[i].iov_len - pos >= 64) {  // common case: inside one piece
+      const __m512i v = _mm512_loadu_si512(static_cast<const uint8_t*>(iov[i].iov_base) + pos);
+      pos += 64;
+      return v;
+    }
+    return assemble(64);
+  }
+  __m512i last(size_t n) { return assemble(n); }
+  __m512i assemble(size_t want) {  // across piece boundaries (a few times per record)
+    alignas(64) uint8_t t[64] = {};
+    size_t got = 0;
+    while (got < want && i < cnt) {
+      const size_t avail = iov[i].iov_len - pos;
+      if (!avail) {
+        i++;
+        pos = 0;
+        continue;
+      }
+      const size_t take = avail < want - got ? avail : want - got;
+      memcpy(t + got, static_cast<const uint8_t*>(iov[i].iov_base) + pos, take);
+      got += take;
+      pos += take;
+    }
+    return _mm512_load_si512(t);
+  }
+};
+
+struct CtrState {
+  __m512i c, cmask, inc4, k0, klast;
+  CtrState(const uint8_t (*rk)[64], int nr, const uint8_t iv[12], uint32_t ctr) {
+    alignas(16) uint8_t b[16];
+    memcpy(b, iv, 12);
+    memcpy(b + 12, &ctr, 4);  // native (little-endian) counter word; byte-swapped per block
+    const __m512i base = _mm512_broadcast_i32x4(_mm_load_si128(reinterpret_cast<const __m128i*>(b)));
+    cmask = _mm512_broadcast_i32x4(_mm_set_epi8(12, 13, 14, 15, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0));
+    inc4 = _mm512_set_epi32(4, 0, 0, 0, 4, 0, 0, 0, 4, 0, 0, 0, 4, 0, 0, 0);
+    c = _mm512_add_epi32(base, _mm512_set_epi32(3, 0, 0, 0, 2, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0));
+    k0 = rk512(rk, 0);
+    klast = rk512(rk, nr);
+  }
+  __m512i next_block4() {  // 4 counter blocks, whitened with round key 0
+    const __m512i b = _mm512_xor_si512(_mm512_shuffle_epi8(c, cmask), k0);
     c = _mm512_add_epi32(c, inc4);
+    return b;
+  }
+};
+
+// out = src ^ E(IV || ctr), E(IV || ctr+1), ... (32-bit big-endian counter),
+// for the sub-512-byte tail.
+template <class Src>
+void ctr_xor(const uint8_t (*rk)[64], int nr, CtrState& st, Src& src, uint8_t* out, size_t n) {
+  while (n) {
+    __m512i b0 = st.next_block4();
     for (int r = 1; r < nr; r++) b0 = _mm512_aesenc_epi128(b0, rk512(rk, r));
-    b0 = _mm512_aesenclast_epi128(b0, klast);
+    b0 = _mm512_aesenclast_epi128(b0, st.klast);
     if (n >= 64) {
-      _mm512_storeu_si512(out, _mm512_xor_si512(b0, _mm512_loadu_si512(in)));
-      in += 64;
+      _mm512_storeu_si512(out, _mm512_xor_si512(b0, src.next64()));
       out += 64;
       n -= 64;
     } else {
-      const __mmask64 m = ~0ULL >> (64 - n);
-      _mm512_mask_storeu_epi8(out, m, _mm512_xor_si512(b0, _mm512_maskz_loadu_epi8(m, in)));
+      _mm512_mask_storeu_epi8(out, ~0ULL >> (64 - n), _mm512_xor_si512(b0, src.last(n)));
       n = 0;
     }
   }
@@ -263,27 +296,15 @@ inline void gh_chunk512(const uint8_t (*hp)[16], const uint8_t* p, __m128i y, __
 // (VAES) and carry-less multiply (VPCLMULQDQ) streams overlap. Decryption
 // hashes the chunk it decrypts (its loads precede the stores, so in == out
 // works); encryption hashes the ciphertext one chunk behind. hp = H^32..H^1.
-template <bool ENC>
-__m128i ctr_ghash512(const uint8_t (*rk)[64], int nr, const uint8_t (*hp)[16], const uint8_t iv[12], uint32_t ctr,
+template <bool ENC, class Src>
+__m128i ctr_ghash512(const uint8_t (*rk)[64], int nr, const uint8_t (*hp)[16], CtrState& st, Src& src,
                      const uint8_t* in, uint8_t* out, size_t n, __m128i y) {
-  alignas(16) uint8_t b[16];
-  memcpy(b, iv, 12);
-  memcpy(b + 12, &ctr, 4);
-  const __m512i base = _mm512_broadcast_i32x4(_mm_load_si128(reinterpret_cast<const __m128i*>(b)));
-  const __m512i cmask =
-      _mm512_broadcast_i32x4(_mm_set_epi8(12, 13, 14, 15, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0));
-  const __m512i inc4 = _mm512_set_epi32(4, 0, 0, 0, 4, 0, 0, 0, 4, 0, 0, 0, 4, 0, 0, 0);
   const __m512i bsw = bswap_mask512();
-  __m512i c = _mm512_add_epi32(base, _mm512_set_epi32(3, 0, 0, 0, 2, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0));
-  const __m512i k0 = rk512(rk, 0), klast = rk512(rk, nr);
   for (size_t off = 0; off < n; off += 512) {
     const uint8_t* gp = ENC ? (off ? out + off - 512 : nullptr) : in + off;
     __m512i blk[8];
 #pragma GCC unroll 8
-    for (int j = 0; j < 8; j++) {
-      blk[j] = _mm512_xor_si512(_mm512_shuffle_epi8(c, cmask), k0);
-      c = _mm512_add_epi32(c, inc4);
-    }
+    for (int j = 0; j < 8; j++) blk[j] = st.next_block4();
     __m512i lo, mid, hi;
     if (gp) gh_chunk512(hp, gp, y, bsw, lo, mid, hi);
     for (int r = 1; r < nr; r++) {
@@ -293,8 +314,8 @@ __m128i ctr_ghash512(const uint8_t (*rk)[64], int nr, const uint8_t (*hp)[16], c
     }
 #pragma GCC unroll 8
     for (int j = 0; j < 8; j++)
-      _mm512_storeu_si512(out + off + 64 * j, _mm512_xor_si512(_mm512_aesenclast_epi128(blk[j], klast),
-                                                               _mm512_loadu_si512(in + off + 64 * j)));
+      _mm512_storeu_si512(out + off + 64 * j, _mm512_xor_si512(_mm512_aesenclast_epi128(blk[j], st.klast),
+                                                               src.next64()));
     if (gp) y = gf_reduce(fold4(lo), fold4(mid), fold4(hi));
   }
   if (ENC) {
@@ -345,14 +366,16 @@ void setup(const uint8_t* key, size_t key_len, uint8_t (*rk)[64], uint8_t (*hp)[
   for (int r = 0; r < 15; r++) vk[r] = _mm_setzero_si128();
 }
 
+template <class Src>
 void seal_impl(const uint8_t (*rk)[64], const uint8_t (*hp)[16], int nr, const uint8_t iv[12], const uint8_t* aad,
-               size_t aad_len, const uint8_t* in, uint8_t* out, size_t n, uint8_t tag[16]) {
+               size_t aad_len, Src& src, uint8_t* out, size_t n, uint8_t tag[16]) {
   const uint8_t (*hp16)[16] = hp + 16;
   const __m128i ej0 = enc_block(rk, nr, j0_block(iv));
   __m128i y = ghash(hp16, _mm_setzero_si128(), aad, aad_len);
+  CtrState st(rk, nr, iv, 2);
   const size_t big = n & ~size_t(511);
-  if (big) y = ctr_ghash512<true>(rk, nr, hp, iv, 2, in, out, big, y);
-  ctr_xor(rk, nr, iv, uint32_t(2 + big / 16), in + big, out + big, n - big);
+  if (big) y = ctr_ghash512<true>(rk, nr, hp, st, src, nullptr, out, big, y);
+  ctr_xor(rk, nr, st, src, out + big, n - big);
   y = ghash_len(hp16, ghash(hp16, y, out + big, n - big), aad_len, n);
   _mm_storeu_si128(reinterpret_cast<__m128i*>(tag), _mm_xor_si128(bswap128(y), ej0));
 }
@@ -362,10 +385,12 @@ bool open_impl(const uint8_t (*rk)[64], const uint8_t (*hp)[16], int nr, const u
   const uint8_t (*hp16)[16] = hp + 16;
   const __m128i ej0 = enc_block(rk, nr, j0_block(iv));
   __m128i y = ghash(hp16, _mm_setzero_si128(), aad, aad_len);
+  CtrState st(rk, nr, iv, 2);
+  FlatSrc src{in};
   const size_t big = n & ~size_t(511);
-  if (big) y = ctr_ghash512<false>(rk, nr, hp, iv, 2, in, out, big, y);
+  if (big) y = ctr_ghash512<false>(rk, nr, hp, st, src, in, out, big, y);
   y = ghash_len(hp16, ghash(hp16, y, in + big, n - big), aad_len, n);  // hash the tail before decrypting it
-  ctr_xor(rk, nr, iv, uint32_t(2 + big / 16), in + big, out + big, n - big);
+  ctr_xor(rk, nr, st, src, out + big, n - big);
   alignas(16) uint8_t want[16];
   _mm_store_si128(reinterpret_cast<__m128i*>(want), _mm_xor_si128(bswap128(y), ej0));
   if (CRYPTO_memcmp(want, tag, 16) == 0) return true;
@@ -403,7 +428,14 @@ bool AesGcm::init(const uint8_t* key, size_t key_len) {
 
 void AesGcm::seal(const uint8_t iv[12], const uint8_t* aad, size_t aad_len, const uint8_t* in, uint8_t* out, size_t n,
                   uint8_t tag[16]) const {
-  seal_impl(rk_, hpow_, rounds_, iv, aad, aad_len, in, out, n, tag);
+  FlatSrc src{in};
+  seal_impl(rk_, hpow_, rounds_, iv, aad, aad_len, src, out, n, tag);
+}
+
+void AesGcm::seal_gather(const uint8_t iv[12], const uint8_t* aad, size_t aad_len, const iovec* iov, int cnt,
+                         uint8_t* out, size_t n, uint8_t tag[16]) const {
+  GatherSrc src{iov, cnt};
+  seal_impl(rk_, hpow_, rounds_, iv, aad, aad_len, src, out, n, tag);
 }
 
 bool AesGcm::open(const uint8_t iv[12], const uint8_t* aad, size_t aad_len, const uint8_t* in, uint8_t* out, size_t n,

@@ -12,6 +12,8 @@
 // against a record OpenSSL itself encrypted (native/rtc/dtls.cc).
 #pragma once
 
+#include <sys/uio.h>
+
 #include <cstddef>
 #include <cstdint>
 
@@ -32,6 +34,10 @@ class AesGcm {
   // in == out is allowed.
   void seal(const uint8_t iv[12], const uint8_t* aad, size_t aad_len, const uint8_t* in, uint8_t* out, size_t n,
             uint8_t tag[16]) const;
+  // Same, reading the plaintext from a gather list totalling n bytes (no
+  // gather copy); out must not overlap the pieces.
+  void seal_gather(const uint8_t iv[12], const uint8_t* aad, size_t aad_len, const iovec* iov, int cnt, uint8_t* out,
+                   size_t n, uint8_t tag[16]) const;
   // Decrypts in -> out (in == out allowed) and checks the tag; on failure
   // returns false with out zeroed.
   bool open(const uint8_t iv[12], const uint8_t* aad, size_t aad_len, const uint8_t* in, uint8_t* out, size_t n,

@@ -394,14 +394,9 @@ bool DtlsTransport::fast_encrypt_into(uint8_t* out, uint8_t type, const iovec* i
   aad[9] = 0xFE;
   aad[10] = 0xFD;
   wr16(aad + 11, uint16_t(total));
-  if (wgcm_) {  // gather, then encrypt in place (the copy is L1-resident)
+  if (wgcm_) {  // straight from the gather list into the datagram
     uint8_t* o = out + kRecHdr + kExplicit;
-    for (int i = 0; i < cnt; i++) {
-      memcpy(o, iov[i].iov_base, iov[i].iov_len);
-      o += iov[i].iov_len;
-    }
-    o = out + kRecHdr + kExplicit;
-    wgcm_->seal(nonce, aad, 13, o, o, total, o + total);
+    wgcm_->seal_gather(nonce, aad, 13, iov, cnt, o, total, o + total);
     return true;
   }
   int l = 0;

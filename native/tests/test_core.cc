@@ -1,4 +1,5 @@
 // Core: JSON, checksums, encodings, reactor timers, frame codec, HTTP parser.
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -296,6 +297,22 @@ TEST(aesgcm_matches_evp_and_rejects_tampering) {
       g.seal(iv, aad.data(), aad.size(), pt.data(), ct.data() + (n & 1), n, tag);  // odd/even alignment
       CHECK(memcmp(ct.data() + (n & 1), ref.data(), n) == 0);
       CHECK(memcmp(tag, rtag, 16) == 0);
+      // gather source: random split into pieces (some empty, some tiny)
+      {
+        std::vector<iovec> iov;
+        size_t at = 0;
+        while (at < n) {
+          size_t take = std::min(n - at, size_t(rnd() % 4 == 0 ? rnd() % 5 : rnd() % 700));
+          iov.push_back({pt.data() + at, take});
+          at += take;
+        }
+        if (rnd() % 2) iov.push_back({pt.data(), 0});
+        std::vector<uint8_t> g2(n);
+        uint8_t gtag[16];
+        g.seal_gather(iv, aad.data(), aad.size(), iov.data(), int(iov.size()), g2.data(), n, gtag);
+        CHECK(memcmp(g2.data(), ref.data(), n) == 0);
+        CHECK(memcmp(gtag, rtag, 16) == 0);
+      }
       // in-place round trip
       std::vector<uint8_t> buf = pt;
       g.seal(iv, aad.data(), aad.size(), buf.data(), buf.data(), n, tag);
