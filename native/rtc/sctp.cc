@@ -581,7 +581,7 @@ void SctpAssociation::build_sack(std::vector<uint8_t>& b) {
   std::vector<std::pair<uint16_t, uint16_t>> gaps;
   for (uint32_t o : offs) {
     if (o > 0xFFFF) break;
-    if (!gaps.empty() && gaps.back().second + 1 == o) gaps.back().second = uint16_t(o);
+    if (!gaps.empty() && uint32_t(gaps.back().second) + 1 == o) gaps.back().second = uint16_t(o);
     else gaps.emplace_back(uint16_t(o), uint16_t(o));
     if (gaps.size() > 64) break;
   }
