@@ -43,7 +43,8 @@ def main():
     env = None
     if a.profile_dir:
         os.makedirs(a.profile_dir, exist_ok=True)
-        env = {"TUNNEL_PROFILE": os.path.join(os.path.abspath(a.profile_dir), "tunnel.%p.prof")}
+        env = {"TUNNEL_PROFILE": os.path.join(os.path.abspath(a.profile_dir), "tunnel.%p.prof"),
+               "TUNNEL_PROFILE_HZ": os.environ.get("TUNNEL_PROFILE_HZ", "2000")}
     mock, port = start_mock("native", 100, 5)
     ms, mp = free_port(), free_port()
     out = {}
