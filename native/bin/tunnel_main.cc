@@ -20,6 +20,7 @@
 
 #include "core/log.h"
 #include "core/profiler.h"
+#include "rtc/dtls.h"
 #include "tunnel/app.h"
 
 using namespace p2pt;
@@ -91,6 +92,10 @@ const std::vector<Opt>& ext_opts() {
        "Pre-shared secret both peers must prove (HMAC bound to the DTLS fingerprints); prefer the env var"},
       {"cpu-affinity", "TUNNEL_CPU_AFFINITY", "",
        "Pin the process to these CPUs, e.g. 0-3,64 (the NIC's NUMA node, away from inference threads)"},
+      {"identity", "TUNNEL_IDENTITY", "",
+       "PEM file with this peer's DTLS key + certificate (created if missing): a stable fingerprint to pin"},
+      {"pin-peer", "TUNNEL_PIN_PEER", "",
+       "Only accept a peer whose DTLS certificate SHA-256 is listed (comma-separated; see `tunnel fingerprint`)"},
   };
   return o;
 }
@@ -99,6 +104,7 @@ void usage_main() {
   printf("P2P HTTP tunnel over WebRTC\n\nUsage: tunnel <COMMAND>\n\nCommands:\n"
          "  serve  Serve an upstream HTTP service through the tunnel\n"
          "  proxy  Create a local HTTP proxy that tunnels to a remote provider\n"
+         "  fingerprint  Print the DTLS fingerprint of an --identity file (for --pin-peer)\n"
          "  help   Print this message or the help of the given subcommand(s)\n\n"
          "Options:\n  -h, --help     Print help\n  -V, --version  Print version\n");
 }
@@ -243,6 +249,21 @@ int main(int argc, char** argv) {
     else usage_main();
     return 0;
   }
+  if (cmd == "fingerprint") {  // print (creating if needed) the identity's fingerprint for --pin-peer
+    std::string path = argc > 3 && std::string(argv[2]) == "--identity" ? argv[3] : "";
+    if (path.empty() && getenv("TUNNEL_IDENTITY")) path = getenv("TUNNEL_IDENTITY");
+    if (path.empty()) {
+      fprintf(stderr, "Usage: tunnel fingerprint --identity <PEM FILE>  [env: TUNNEL_IDENTITY=]\n");
+      return 2;
+    }
+    std::string err;
+    if (!rtc::set_identity_file(path, &err)) {
+      fprintf(stderr, "error: --identity %s: %s\n", path.c_str(), err.c_str());
+      return 2;
+    }
+    printf("%s\n", rtc::DtlsTransport::local_fingerprint().c_str());
+    return 0;
+  }
   if (cmd != "serve" && cmd != "proxy") {
     fprintf(stderr, "error: unrecognized subcommand '%s'\n\n", cmd.c_str());
     usage_main();
@@ -302,6 +323,31 @@ int main(int argc, char** argv) {
       return 2;
     }
     LOG_INFO("tunnel", "pinned to CPUs %s", m["cpu-affinity"].c_str());
+  }
+
+  if (!m["identity"].empty()) {
+    std::string err;
+    if (!rtc::set_identity_file(m["identity"], &err)) {
+      fprintf(stderr, "error: --identity %s: %s\n", m["identity"].c_str(), err.c_str());
+      return 2;
+    }
+    LOG_INFO("tunnel", "DTLS identity %s: %s", m["identity"].c_str(), rtc::DtlsTransport::local_fingerprint().c_str());
+  }
+  if (!m["pin-peer"].empty()) {
+    std::vector<std::string> pins;
+    const std::string& s = m["pin-peer"];
+    for (size_t a = 0; a < s.size();) {
+      size_t c = s.find(',', a);
+      if (c == std::string::npos) c = s.size();
+      if (c > a) pins.push_back(s.substr(a, c - a));
+      a = c + 1;
+    }
+    std::string bad;
+    if (pins.empty() || !rtc::set_pinned_fingerprints(pins, &bad)) {
+      fprintf(stderr, "error: --pin-peer: '%s' is not a SHA-256 fingerprint\n", bad.c_str());
+      return 2;
+    }
+    LOG_INFO("tunnel", "accepting only %zu pinned peer certificate(s)", pins.size());
   }
 
   if (cmd == "serve") {

@@ -5,9 +5,15 @@
 #include <openssl/core_names.h>
 #include <openssl/evp.h>
 #include <openssl/kdf.h>
+#include <openssl/pem.h>
 #include <openssl/ssl.h>
 #include <openssl/x509.h>
 
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 
@@ -38,21 +44,88 @@ std::string fp_of(X509* cert) {
 
 int verify_any(int, X509_STORE_CTX*) { return 1; }  // self-signed: checked against the SDP fingerprint
 
+// Process-wide settings, fixed before the first session (set_identity_file,
+// set_pinned_fingerprints; see dtls.h).
+std::string g_identity_path;
+std::vector<std::string> g_pins;
+
+void make_cert(Identity& id, long days) {
+  id.key = EVP_EC_gen("P-256");
+  id.cert = X509_new();
+  X509_set_version(id.cert, 2);
+  ASN1_INTEGER_set(X509_get_serialNumber(id.cert), long(random_u32() & 0x7fffffff));
+  X509_gmtime_adj(X509_getm_notBefore(id.cert), -86400);
+  X509_gmtime_adj(X509_getm_notAfter(id.cert), days * 86400);
+  X509_set_pubkey(id.cert, id.key);
+  X509_NAME* name = X509_get_subject_name(id.cert);
+  X509_NAME_add_entry_by_txt(name, "CN", MBSTRING_ASC, reinterpret_cast<const unsigned char*>("WebRTC"), -1, -1, 0);
+  X509_set_issuer_name(id.cert, name);
+  X509_sign(id.cert, id.key, EVP_sha256());
+}
+
+// PEM private key + certificate. A missing file is created (mode 0600) with a
+// fresh long-lived key pair, so the fingerprint stays stable across restarts
+// and the peer can pin it.
+bool load_or_create(const std::string& path, Identity& id, std::string* err) {
+  if (FILE* f = fopen(path.c_str(), "r")) {
+    id.key = PEM_read_PrivateKey(f, nullptr, nullptr, nullptr);
+    id.cert = id.key ? PEM_read_X509(f, nullptr, nullptr, nullptr) : nullptr;
+    fclose(f);
+    if (!id.key || !id.cert || X509_check_private_key(id.cert, id.key) != 1) {
+      *err = "not a PEM private key followed by its certificate";
+      return false;
+    }
+    return true;
+  }
+  if (errno != ENOENT) {
+    *err = strerror(errno);
+    return false;
+  }
+  make_cert(id, 3650);
+  int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_EXCL, 0600);
+  FILE* f = fd >= 0 ? fdopen(fd, "w") : nullptr;
+  if (!f) {
+    *err = std::string("cannot create: ") + strerror(errno);
+    if (fd >= 0) ::close(fd);
+    return false;
+  }
+  bool ok = PEM_write_PrivateKey(f, id.key, nullptr, nullptr, 0, nullptr, nullptr) == 1 &&
+            PEM_write_X509(f, id.cert) == 1;
+  ok = fclose(f) == 0 && ok;
+  if (!ok) *err = "write failed";
+  return ok;
+}
+
+// "sha-256 ab:cd..." / "AB:CD..." / "abcd..." -> "AB:CD:..." (empty if not a
+// SHA-256 fingerprint).
+std::string normalize_fp(std::string s) {
+  size_t sp = s.find_last_of(' ');
+  if (sp != std::string::npos) s = s.substr(sp + 1);
+  std::string hex;
+  for (char c : s)
+    if (c != ':') hex += char(toupper(static_cast<unsigned char>(c)));
+  if (hex.size() != 64 || hex.find_first_not_of("0123456789ABCDEF") != std::string::npos) return "";
+  std::string out;
+  for (size_t i = 0; i < hex.size(); i += 2) {
+    if (i) out += ':';
+    out += hex.substr(i, 2);
+  }
+  return out;
+}
+
 Identity& identity() {
   static Identity id;
   static std::once_flag once;
   std::call_once(once, [] {
-    id.key = EVP_EC_gen("P-256");
-    id.cert = X509_new();
-    X509_set_version(id.cert, 2);
-    ASN1_INTEGER_set(X509_get_serialNumber(id.cert), long(random_u32() & 0x7fffffff));
-    X509_gmtime_adj(X509_getm_notBefore(id.cert), -86400);
-    X509_gmtime_adj(X509_getm_notAfter(id.cert), 30L * 86400);
-    X509_set_pubkey(id.cert, id.key);
-    X509_NAME* name = X509_get_subject_name(id.cert);
-    X509_NAME_add_entry_by_txt(name, "CN", MBSTRING_ASC, reinterpret_cast<const unsigned char*>("WebRTC"), -1, -1, 0);
-    X509_set_issuer_name(id.cert, name);
-    X509_sign(id.cert, id.key, EVP_sha256());
+    std::string err;
+    if (!g_identity_path.empty() && !load_or_create(g_identity_path, id, &err)) {
+      // set_identity_file() validated the file already; reaching this means
+      // it changed underneath us. Never fall back to a different identity
+      // silently: pinned peers would reject it anyway.
+      LOG_ERROR(kT, "DTLS identity %s: %s", g_identity_path.c_str(), err.c_str());
+      abort();
+    }
+    if (g_identity_path.empty()) make_cert(id, 30);
     id.fingerprint = "sha-256 " + fp_of(id.cert);
 
     SSL_CTX* ctx = SSL_CTX_new(DTLS_method());
@@ -128,6 +201,35 @@ struct DtlsBio {
 
 const std::string& DtlsTransport::local_fingerprint() { return identity().fingerprint; }
 
+bool set_identity_file(const std::string& path, std::string* err) {
+  Identity probe;  // validate (or create) now, so a bad file fails at startup
+  bool ok = load_or_create(path, probe, err);
+  EVP_PKEY_free(probe.key);
+  X509_free(probe.cert);
+  if (ok) g_identity_path = path;
+  return ok;
+}
+
+bool set_pinned_fingerprints(const std::vector<std::string>& fps, std::string* bad) {
+  std::vector<std::string> pins;
+  for (auto& f : fps) {
+    std::string n = normalize_fp(f);
+    if (n.empty()) {
+      if (bad) *bad = f;
+      return false;
+    }
+    pins.push_back(n);
+  }
+  g_pins = std::move(pins);
+  return true;
+}
+
+bool fingerprint_pinned(const std::string& fp) {
+  if (g_pins.empty()) return true;
+  std::string n = normalize_fp(fp);
+  return std::find(g_pins.begin(), g_pins.end(), n) != g_pins.end();
+}
+
 std::shared_ptr<DtlsTransport> DtlsTransport::create(Reactor& r, bool is_client, std::string remote_fp,
                                                      WriteFn write) {
   auto t = std::shared_ptr<DtlsTransport>(new DtlsTransport(r));
@@ -192,6 +294,10 @@ bool DtlsTransport::verify_peer() {
   X509_free(peer);
   if (fp != remote_fp_) {
     LOG_ERROR(kT, "DTLS fingerprint mismatch: got %s, SDP says %s", fp.c_str(), remote_fp_.c_str());
+    return false;
+  }
+  if (!fingerprint_pinned(fp)) {
+    LOG_ERROR(kT, "DTLS peer certificate sha-256 %s is not pinned (--pin-peer)", fp.c_str());
     return false;
   }
   return true;
@@ -423,7 +529,7 @@ void DtlsTransport::drive() {
     int rc = SSL_do_handshake(ssl_);
     if (rc == 1) {
       if (!verify_peer()) {
-        fail("DTLS peer certificate does not match the SDP fingerprint");
+        fail("DTLS peer certificate rejected (SDP fingerprint mismatch or not pinned)");
         return;
       }
       connected_ = true;

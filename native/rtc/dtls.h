@@ -44,6 +44,20 @@ typedef struct evp_cipher_ctx_st EVP_CIPHER_CTX;
 
 namespace p2pt::rtc {
 
+// Process-wide DTLS identity and peer pinning, set before the first session
+// (reference README "Future options": certificate pinning via the DTLS
+// fingerprints). Without an identity file every process start has a fresh
+// ephemeral certificate.
+//   set_identity_file: load a PEM key + certificate, creating it (0600, fresh
+//     P-256 key, 10-year self-signed certificate) if missing.
+//   set_pinned_fingerprints: only peers whose certificate SHA-256 is listed are
+//     accepted (checked against the SDP offer/answer and again after the DTLS
+//     handshake). Accepts "sha-256 AB:CD:..", "AB:CD:.." or bare hex; false
+//     (with *bad set) on a malformed entry.
+bool set_identity_file(const std::string& path, std::string* err);
+bool set_pinned_fingerprints(const std::vector<std::string>& fps, std::string* bad = nullptr);
+bool fingerprint_pinned(const std::string& fp);  // true when nothing is pinned
+
 class DtlsTransport : public std::enable_shared_from_this<DtlsTransport> {
  public:
   using WriteFn = std::function<void(const uint8_t*, size_t)>;

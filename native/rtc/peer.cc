@@ -196,6 +196,10 @@ std::string PeerConnection::local_description() const {
 bool PeerConnection::set_remote_description(const std::string& sdp, std::string* err) {
   SessionDesc d;
   if (!SessionDesc::parse(sdp, d, err)) return false;
+  if (!fingerprint_pinned(d.fingerprint)) {  // fail before ICE/DTLS; re-checked on the certificate
+    if (err) *err = "remote fingerprint " + d.fingerprint + " is not pinned (--pin-peer)";
+    return false;
+  }
   remote_ = d;
   have_remote_ = true;
   // DTLS role (RFC 8842 §5): the answerer picks "active" when offered actpass.

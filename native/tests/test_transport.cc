@@ -258,6 +258,36 @@ TEST(dtls_fingerprint_mismatch_fails) {
   CHECK(!c->connected());
 }
 
+TEST(dtls_unpinned_certificate_fails_after_handshake) {
+  // SDP fingerprints match, but the pin set excludes the peer: the DTLS-level
+  // check (not only the SDP one) rejects it.
+  Reactor r;
+  std::shared_ptr<DtlsTransport> c, s;
+  std::string fp = DtlsTransport::local_fingerprint();
+  CHECK(!set_pinned_fingerprints({"sha-256 12:34"}));
+  std::string other;
+  for (int i = 0; i < 32; i++) other += i ? ":AB" : "AB";
+  CHECK(set_pinned_fingerprints({other}));
+  CHECK(!fingerprint_pinned(fp));
+  CHECK(fingerprint_pinned("sha-256 " + other));
+  c = DtlsTransport::create(r, true, fp, [&](const uint8_t* p, size_t n) {
+    auto v = std::make_shared<std::vector<uint8_t>>(p, p + n);
+    r.post([&s, v] { if (s) s->on_datagram(v->data(), v->size()); });
+  });
+  s = DtlsTransport::create(r, false, fp, [&](const uint8_t* p, size_t n) {
+    auto v = std::make_shared<std::vector<uint8_t>>(p, p + n);
+    r.post([&c, v] { if (c) c->on_datagram(v->data(), v->size()); });
+  });
+  std::string why;
+  c->on_closed = [&](const std::string& w) { why = w; };
+  c->start();
+  CHECK(r.run_until([&] { return !why.empty(); }, 3000));
+  CHECK(why.find("not pinned") != std::string::npos);
+  CHECK(!c->connected());
+  CHECK(set_pinned_fingerprints({}));  // process-wide: restore "no pinning"
+  CHECK(fingerprint_pinned(fp));
+}
+
 TEST(peerconnection_pair_loopback) {
   Reactor r;
   PcConfig cfg;
