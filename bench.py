@@ -100,6 +100,8 @@ def loadgen(port, streams, steps, warmup=0, path=None):
 def main():
     a = parse()
     dist, rank, world = dist_init()
+    if world > 1:  # disjoint port blocks: ranks start their tunnels concurrently
+        os.environ.setdefault("P2PT_PORT_BASE", str(20000 + 500 * int(os.environ.get("LOCAL_RANK", rank))))
     from p2p_llm_tunnel_amd.utils.build import ensure_native
     from p2p_llm_tunnel_amd.utils.procs import Tunnel
 

@@ -19,7 +19,25 @@ from dataclasses import dataclass, field
 from p2p_llm_tunnel_amd import binary
 
 
+_next_port = [0]
+
+
 def free_port(host: str = "127.0.0.1") -> int:
+    """A currently free TCP port. With P2PT_PORT_BASE set (bench.py sets a
+    disjoint block per rank), ports are taken in order from that block, so
+    ranks starting tunnels at the same instant never race for one the kernel
+    handed to both between our close() and the child's bind()."""
+    base = int(os.environ.get("P2PT_PORT_BASE", "0"))
+    if base:
+        for _ in range(500):
+            port = base + _next_port[0] % 500
+            _next_port[0] += 1
+            with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+                try:
+                    s.bind((host, port))
+                except OSError:
+                    continue
+                return port
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind((host, 0))
         return s.getsockname()[1]
