@@ -54,18 +54,39 @@ class Request:
         self.state = None  # front-end bookkeeping for batched requests
 
 
+class _StepBuf:
+    """Host staging of one in-flight step (two alternate: step k+1 is planned
+    and launched while step k runs). Rows: token (prompt rows), position,
+    slot, decode flag, slot to record the sampled id under (scratch for rows
+    that emit nothing)."""
+
+    def __init__(self, rows: int, cuda: bool):
+        self.h_in = torch.zeros((5, rows), dtype=torch.int64, pin_memory=cuda)
+        self.np = self.h_in.numpy()
+        self.h_out = torch.zeros(rows, dtype=torch.int64, pin_memory=cuda)
+        self.ev = torch.cuda.Event() if cuda else None
+        self.n = 0
+        self.emits = []  # (row, req, finished)
+
+
 class Engine:
-    """Continuous batching with chunked prefill over the fused decode step.
+    """Continuous batching with chunked prefill over the fused decode step,
+    one step in flight ahead of the host.
 
     Every step packs up to ``rows`` (16) token rows: first one decode row per
     generating sequence, then prompt chunks of prefilling sequences, each row
     tagged with its cache slot and position (``TinyLlama.decode_step(slots=)``).
     A 512-byte prompt is thus prefilled in 32 steps instead of 512, while
     generating sequences keep emitting a token every step. Padding rows point
-    at the model's scratch slot. The step is replayed from one hipGraph whose
-    inputs arrive in one pinned host->device copy and whose sampled ids leave
-    through one pinned device->host copy; the engine waits on an event with
-    the GIL released.
+    at the model's scratch slot.
+
+    The schedule never depends on token values (no stop tokens; lengths are
+    known), so the host plans step k+1 while step k runs: a decode row's input
+    token is read on the device from ``last[slot]``, which every emitting row
+    updates after the step, and the sampled ids come back through a pinned
+    buffer and an event per step. The host waits on step k (GIL released, so
+    the HTTP thread writes meanwhile) only after step k+1 is queued behind it.
+    The step itself is replayed from one hipGraph.
 
     ``model`` injects a model object (tests use a CPU stand-in with the same
     ``decode_step`` / ``cfg`` / ``scratch_slot`` / ``device`` surface).
@@ -81,13 +102,13 @@ class Engine:
         self.device = self.model.device
         self.rows = rows
         self.use_graph = use_graph
+        cuda = self.device.type == "cuda"
         if use_graph:
             self.model.capture_graph(rows=rows)
-            self._h_in = torch.zeros((3, rows), dtype=torch.int64, pin_memory=True)
-            self._h_in_np = self._h_in.numpy()
-            self._d_in = torch.zeros((3, rows), dtype=torch.int64, device=self.device)
-            self._h_out = torch.zeros(rows, dtype=torch.int64, pin_memory=True)
-            self._ev = torch.cuda.Event()
+        self._bufs = [_StepBuf(rows, cuda), _StepBuf(rows, cuda)]
+        self._k = 0
+        self._d_in = torch.zeros((5, rows), dtype=torch.int64, device=self.device) if cuda else None
+        self._d_last = torch.zeros(max_batch + 1, dtype=torch.int64, device=self.device)
         self.max_batch = max_batch
         self.pending: queue.Queue = queue.Queue()
         self.slots: list[dict | None] = [None] * max_batch
@@ -118,87 +139,120 @@ class Engine:
                 except queue.Empty:
                     return
                 ids = req.prompt[: self.model.cfg.max_seq - req.max_new - 1] or [0]
-                self.slots[i] = {"req": req, "pos": 0, "ids": ids, "last": None}
+                self.slots[i] = {"req": req, "pos": 0, "ids": ids, "gen": 0}
 
-    def _plan(self):
-        """Rows for this step: [(slot, token, pos, emits)]."""
+    def _plan(self, batch: list):
+        """Rows of the next step [(slot, token, pos, is_decode, emits)], with the
+        host-side state advanced past them (it does not depend on the tokens)
+        and the emitting rows' (row, req, finished) list."""
         V = self.model.cfg.vocab
-        rows = []
+        rows, emits = [], []
         for i, s in enumerate(self.slots):  # decode rows first: one token each
-            if s is not None and s["pos"] >= len(s["ids"]):
-                rows.append((i, s["last"], s["pos"], True))
+            if s is None or s["pos"] < len(s["ids"]):
+                continue
+            if s["req"].cancelled:
+                self._emit(s["req"], None, batch)
+                self.slots[i] = None
+                continue
+            rows.append((i, 0, s["pos"], 1, True))
         for i, s in enumerate(self.slots):  # then prompt chunks
             if s is None or s["pos"] >= len(s["ids"]):
                 continue
             take = min(self.rows - len(rows), len(s["ids"]) - s["pos"])
             for p in range(s["pos"], s["pos"] + take):
-                rows.append((i, s["ids"][p] % V, p, p == len(s["ids"]) - 1))
+                rows.append((i, s["ids"][p] % V, p, 0, p == len(s["ids"]) - 1))
             if len(rows) >= self.rows:
                 break
-        return rows
+        max_seq = self.model.cfg.max_seq
+        for r, (i, _, _, _, emit) in enumerate(rows):
+            s = self.slots[i]
+            s["pos"] += 1
+            if not emit:
+                self.prefill_tokens += 1
+                continue
+            s["gen"] += 1
+            fin = s["gen"] >= s["req"].max_new or s["pos"] >= max_seq - 1
+            emits.append((r, s["req"], fin))
+            if fin:
+                self.slots[i] = None
+        return rows, emits
 
-    def _run(self, rows) -> list[int]:
-        n = len(rows)
+    def _launch(self, rows, emits) -> _StepBuf:
+        b = self._bufs[self._k % 2]
+        self._k += 1
+        n, R, scratch = len(rows), self.rows, self.model.scratch_slot
+        h = b.np
+        h[0, :n] = [r[1] for r in rows]
+        h[1, :n] = [r[2] for r in rows]
+        h[2, :n] = [r[0] for r in rows]
+        h[3, :n] = [r[3] for r in rows]
+        h[4, :n] = [r[0] if r[4] else scratch for r in rows]
+        if n < R:  # padding rows: scratch slot, nothing recorded
+            h[0:2, n:] = 0
+            h[2, n:] = scratch
+            h[3, n:] = 0
+            h[4, n:] = scratch
+        b.n, b.emits = n, emits
+        m = R if self.use_graph else n
+        if self._d_in is not None:
+            self._d_in.copy_(b.h_in, non_blocking=True)
+            d = self._d_in
+        else:
+            d = b.h_in
+        tok = torch.where(d[3, :m] != 0, self._d_last[d[2, :m]], d[0, :m])
         if self.use_graph:
-            h = self._h_in_np
-            h[0, :n] = [r[1] for r in rows]
-            h[1, :n] = [r[2] for r in rows]
-            h[2, :n] = [r[0] for r in rows]
-            if n < self.rows:  # padding rows -> scratch slot
-                h[0, n:] = 0
-                h[1, n:] = 0
-                h[2, n:] = self.model.scratch_slot
-            self._d_in.copy_(self._h_in, non_blocking=True)
-            ids = self.model.graph_step(self._d_in[0], self._d_in[1], self._d_in[2])
-            self._h_out.copy_(ids, non_blocking=True)
-            self._ev.record()
-            self._ev.synchronize()  # GIL released: the I/O thread writes meanwhile
-            return self._h_out[:n].tolist()
-        tok = torch.tensor([r[1] for r in rows], dtype=torch.int64).to(self.device)
-        pos = torch.tensor([r[2] for r in rows], dtype=torch.int32).to(self.device)
-        sl = torch.tensor([r[0] for r in rows], dtype=torch.int32).to(self.device)
-        lo, hi = min(r[2] for r in rows), max(r[2] for r in rows)
-        return self.model.decode_step(tok, pos, (lo, hi), slots=sl).tolist()
+            ids = self.model.graph_step(tok, d[1], d[2])
+        else:
+            lo, hi = min(r[2] for r in rows), max(r[2] for r in rows)
+            ids = self.model.decode_step(tok, d[1, :m].to(torch.int32), (lo, hi), slots=d[2, :m].to(torch.int32))
+        self._d_last.index_copy_(0, d[4, :m], ids[:m].to(torch.int64))
+        b.h_out[:m].copy_(ids[:m], non_blocking=True)
+        if b.ev is not None:
+            b.ev.record()
+        self.steps += 1
+        return b
+
+    def _drain(self, b: _StepBuf, batch: list):
+        if b.ev is not None:
+            b.ev.synchronize()  # GIL released: the HTTP thread writes meanwhile
+        out = b.h_out[: b.n].tolist() if b.emits else []
+        for r, req, fin in b.emits:
+            if req.cancelled:
+                continue
+            self._emit(req, out[r], batch)
+            req.generated += 1
+            self.tokens_out += 1
+            if fin:
+                self._emit(req, None, batch)
 
     def _loop(self):
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
-        while not self._stop.is_set():
-            self._admit()
-            rows = self._plan()
-            if not rows:
-                self._wake.wait(0.05)
-                self._wake.clear()
-                continue
-            out = self._run(rows)
-            self.steps += 1
-            batch = []
-            for (i, _, _, emits), nxt in zip(rows, out):
-                s = self.slots[i]
-                s["pos"] += 1
-                if not emits:
-                    self.prefill_tokens += 1
-                    continue
-                req = s["req"]
-                s["last"] = nxt
-                if req.cancelled:
-                    self._emit(req, None, batch)
-                    self.slots[i] = None
-                    continue
-                self._emit(req, nxt, batch)
-                req.generated += 1
-                self.tokens_out += 1
-                if req.generated >= req.max_new or s["pos"] >= self.model.cfg.max_seq - 1:
-                    self._emit(req, None, batch)
-                    self.slots[i] = None
-            if batch:
-                self.deliver(batch)
+        inflight: list[_StepBuf] = []
+        with torch.no_grad():
+            while not self._stop.is_set():
+                batch = []
+                self._admit()
+                rows, emits = self._plan(batch)
+                if rows:
+                    inflight.append(self._launch(rows, emits))
+                if inflight and (len(inflight) >= 2 or not rows):
+                    self._drain(inflight.pop(0), batch)
+                if batch:
+                    self._flush(batch)
+                if not rows and not inflight:
+                    self._wake.wait(0.05)
+                    self._wake.clear()
 
     def _emit(self, req: Request, tok, batch: list):
         if req.batched and self.deliver is not None:
             batch.append((req, tok))
         else:
             req.out.put(tok)
+
+    def _flush(self, batch: list):
+        if self.deliver is not None:
+            self.deliver(batch)
 
 
 def _prompt_ids(body: dict) -> list[int]:
