@@ -58,10 +58,16 @@ def main():
         body = json.dumps({"model": "p2pt", "stream": True, "max_tokens": a.max_tokens,
                            "messages": [{"role": "user", "content": "x" * a.prompt_bytes}]})
         rows = []
+        counts = [int(x) for x in a.streams.split(",")]
+        # Direct baselines first, with no tunnel attached: with serve's idle
+        # upstream pool connected, the first direct step at 16 streams stalled
+        # ~190 ms (one TCP retransmission timeout) on the MI355X box
+        # (scripts/gpu/diag_direct16.py), which is not a property of either path.
+        direct = {s: loadgen(port, s, a.steps, body) for s in counts}
         with Tunnel(f"http://127.0.0.1:{port}", transport=os.environ.get("P2PT_TRANSPORT", "webrtc")) as t:
-            for s in [int(x) for x in a.streams.split(",")]:
+            for s in counts:
                 tr = loadgen(t.proxy_port, s, a.steps, body)
-                dr = loadgen(port, s, a.steps, body)
+                dr = direct[s]
                 row = {"streams": s, "max_tokens": a.max_tokens, "prompt_bytes": a.prompt_bytes,
                        "tunneled_req_s": tr["req_s"], "direct_req_s": dr["req_s"],
                        "tunneled_tok_s": tr["req_s"] * a.max_tokens, "direct_tok_s": dr["req_s"] * a.max_tokens,

@@ -204,6 +204,7 @@ int main(int argc, char** argv) {
     live.push_back(std::make_shared<Stream>(r, o, res));
     warmers.push_back(std::make_shared<Stream>(r, o, warm_res));
   }
+  std::vector<uint64_t> step_end;  // timed steps' completion times (per-step durations in the output)
   launch = [&] {
     auto& set = step < warmup ? warmers : live;
     if (step == warmup) t_start = Reactor::now_us();
@@ -214,6 +215,7 @@ int main(int argc, char** argv) {
     for (auto& s : *set)
       s->on_done = [&] {
         if (--pending == 0) {
+          if (step >= warmup) step_end.push_back(Reactor::now_us());
           step++;
           if (step >= total_steps) {
             t_end = Reactor::now_us();
@@ -227,14 +229,20 @@ int main(int argc, char** argv) {
   launch();
   r.run();
   double secs = double(t_end - t_start) / 1e6;
+  std::string steps_ms;
+  for (size_t i = 0; i < step_end.size(); i++) {
+    char b[32];
+    snprintf(b, sizeof b, "%s%.3f", i ? ", " : "", double(step_end[i] - (i ? step_end[i - 1] : t_start)) / 1e3);
+    steps_ms += b;
+  }
   printf("{\"streams\": %d, \"steps\": %d, \"requests\": %zu, \"errors\": %d, \"seconds\": %.6f, \"req_s\": %.4f, "
          "\"p50_ttft_ms\": %.4f, \"p90_ttft_ms\": %.4f, \"p99_ttft_ms\": %.4f, \"mean_ttft_ms\": %.4f, "
-         "\"p50_total_ms\": %.4f, \"body_bytes\": %llu, \"MBps\": %.2f}\n",
+         "\"p50_total_ms\": %.4f, \"body_bytes\": %llu, \"MBps\": %.2f, \"step_ms\": [%s]}\n",
          o.streams, o.steps, res.ttft_us.size(), res.errors + warm_res.errors, secs,
          secs > 0 ? double(res.ttft_us.size()) / secs : 0.0, pct(res.ttft_us, 50) / 1e3, pct(res.ttft_us, 90) / 1e3,
          pct(res.ttft_us, 99) / 1e3,
          res.ttft_us.empty() ? 0.0 : [&] { double s = 0; for (double x : res.ttft_us) s += x; return s / double(res.ttft_us.size()) / 1e3; }(),
          pct(res.total_us, 50) / 1e3, static_cast<unsigned long long>(res.body_bytes),
-         secs > 0 ? double(res.body_bytes) / secs / 1e6 : 0.0);
+         secs > 0 ? double(res.body_bytes) / secs / 1e6 : 0.0, steps_ms.c_str());
   return res.errors ? 1 : 0;
 }
