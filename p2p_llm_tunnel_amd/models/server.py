@@ -73,11 +73,12 @@ class Engine:
     """Continuous batching with chunked prefill over the fused decode step,
     one step in flight ahead of the host.
 
-    Every step packs up to ``rows`` (16) token rows: first one decode row per
+    Every step packs up to ``rows`` (64) token rows: first one decode row per
     generating sequence, then prompt chunks of prefilling sequences, each row
     tagged with its cache slot and position (``TinyLlama.decode_step(slots=)``).
-    A 512-byte prompt is thus prefilled in 32 steps instead of 512, while
-    generating sequences keep emitting a token every step. Padding rows point
+    A 512-byte prompt is thus prefilled in 8 steps instead of 512, while
+    generating sequences keep emitting a token every step. Steps of up to 16
+    rows replay a 16-row graph, larger ones a 64-row graph; padding rows point
     at the model's scratch slot.
 
     The schedule never depends on token values (no stop tokens; lengths are
@@ -92,19 +93,28 @@ class Engine:
     ``decode_step`` / ``cfg`` / ``scratch_slot`` / ``device`` surface).
     """
 
-    def __init__(self, device="cuda:0", config="tiny", max_batch=8, seed=0, use_graph=True, rows=16, model=None):
+    def __init__(self, device="cuda:0", config="tiny", max_batch=8, seed=0, use_graph=True, rows=64, model=None,
+                 small_rows=16):
         if model is None:
             from p2p_llm_tunnel_amd.models.tiny_llm import TinyLlama
             model = TinyLlama(config, device=device, max_batch=max_batch, seed=seed, fused=True)
         else:
             use_graph = False
+        if not 1 <= max_batch <= small_rows <= rows:
+            raise ValueError("need 1 <= max_batch <= small_rows <= rows")
         self.model = model
         self.device = self.model.device
         self.rows = rows
+        self.small_rows = small_rows
         self.use_graph = use_graph
         cuda = self.device.type == "cuda"
         if use_graph:
-            self.model.capture_graph(rows=rows)
+            # Two graphs: decode-heavy steps replay the 16-row one; prefill-heavy
+            # steps the 64-row one (4 MFMA row tiles), whose LM head covers only
+            # the leading rows that sample (at most one per slot).
+            self.model.capture_graph(rows=small_rows)
+            if rows > small_rows:
+                self.model.capture_graph(rows=rows, emit_rows=max_batch)
         self._bufs = [_StepBuf(rows, cuda), _StepBuf(rows, cuda)]
         self._k = 0
         self._d_in = torch.zeros((5, rows), dtype=torch.int64, device=self.device) if cuda else None
@@ -163,6 +173,9 @@ class Engine:
                 rows.append((i, s["ids"][p] % V, p, 0, p == len(s["ids"]) - 1))
             if len(rows) >= self.rows:
                 break
+        # Rows that sample go first: the 64-row graph's LM head covers only the
+        # first max_batch rows (each slot samples at most once per step).
+        rows.sort(key=lambda r: not r[4])
         max_seq = self.model.cfg.max_seq
         for r, (i, _, _, _, emit) in enumerate(rows):
             s = self.slots[i]
@@ -180,7 +193,8 @@ class Engine:
     def _launch(self, rows, emits) -> _StepBuf:
         b = self._bufs[self._k % 2]
         self._k += 1
-        n, R, scratch = len(rows), self.rows, self.model.scratch_slot
+        n, scratch = len(rows), self.model.scratch_slot
+        R = self.small_rows if n <= self.small_rows else self.rows
         h = b.np
         h[0, :n] = [r[1] for r in rows]
         h[1, :n] = [r[2] for r in rows]
@@ -188,10 +202,10 @@ class Engine:
         h[3, :n] = [r[3] for r in rows]
         h[4, :n] = [r[0] if r[4] else scratch for r in rows]
         if n < R:  # padding rows: scratch slot, nothing recorded
-            h[0:2, n:] = 0
-            h[2, n:] = scratch
-            h[3, n:] = 0
-            h[4, n:] = scratch
+            h[0:2, n:R] = 0
+            h[2, n:R] = scratch
+            h[3, n:R] = 0
+            h[4, n:R] = scratch
         b.n, b.emits = n, emits
         m = R if self.use_graph else n
         if self._d_in is not None:
@@ -201,7 +215,7 @@ class Engine:
             d = b.h_in
         tok = torch.where(d[3, :m] != 0, self._d_last[d[2, :m]], d[0, :m])
         if self.use_graph:
-            ids = self.model.graph_step(tok, d[1], d[2])
+            ids = self.model.graph_step(tok, d[1, :m], d[2, :m])
         else:
             lo, hi = min(r[2] for r in rows), max(r[2] for r in rows)
             ids = self.model.decode_step(tok, d[1, :m].to(torch.int32), (lo, hi), slots=d[2, :m].to(torch.int32))

@@ -6,14 +6,14 @@ endpoint's model: random-init weights (no checkpoints offline), bf16.
 
 Two decode paths over the same weights and caches:
 
-* fused (default, up to 16 tokens per step): ``ops.FusedLlamaDecoder`` — one
+* fused (default, up to 64 token rows per step): ``ops.FusedLlamaDecoder`` — one
   C++ call launching 5 kernels per layer + 2 (decode_fused.hip: MFMA skinny
   GEMMs with RMSNorm prologues and RoPE/KV-append, SwiGLU, residual and
   argmax epilogues; split-K attention with in-kernel merge);
 * unfused: the standalone kernels of kernels.hip (residual+RMSNorm,
   RoPE+KV-append, flash-decoding, SwiGLU, argmax) around hipBLASLt GEMMs
   (``torch.nn.functional.linear``) — kept as the cross-check and for batches
-  above 16.
+  above 64.
 
 ``reference_logits`` recomputes the same network in fp32 PyTorch (full
 causal attention over the whole sequence) for numerics tests.
@@ -91,11 +91,12 @@ class TinyLlama:
     # ------------------------------------------------------------------ HIP path
     @torch.no_grad()
     def decode_step(self, tokens: torch.Tensor, pos: torch.Tensor, pos_range: tuple[int, int],
-                    return_logits: bool = False, slots: torch.Tensor | None = None):
+                    return_logits: bool = False, slots: torch.Tensor | None = None, emit_rows: int = 0):
         """One step of token rows. tokens: int64 [B]; pos: int32 [B] (cache position of
         each token); slots: int32 [B] cache slot of each row (default: row b -> slot b).
-        With ``slots`` (fused path, B <= 16) several rows may feed one sequence at
-        consecutive positions: a causal prefill chunk.
+        With ``slots`` (fused path, B <= 64) several rows may feed one sequence at
+        consecutive positions: a causal prefill chunk. ``emit_rows`` > 0: only the
+        first rows get ids/logits (fused path; the LM head skips the rest).
 
         Returns next-token ids (int64 [B]) and optionally the bf16 logits.
         """
@@ -103,11 +104,11 @@ class TinyLlama:
         B = tokens.shape[0]
         if slots is None and B > self.max_batch:
             raise ValueError("batch exceeds max_batch")
-        if slots is not None and not (self.fused and B <= 16):
-            raise ValueError("row->slot mapping needs the fused path and at most 16 rows")
+        if slots is not None and not (self.fused and B <= ops.MAX_ROWS):
+            raise ValueError(f"row->slot mapping needs the fused path and at most {ops.MAX_ROWS} rows")
         if pos_range[0] < 0 or pos_range[1] >= c.max_seq:
             raise ValueError("positions out of [0, max_seq)")
-        ids, logits = self._decode_impl(tokens, pos, pos_range, pos_range[1] + 1, slots)
+        ids, logits = self._decode_impl(tokens, pos, pos_range, pos_range[1] + 1, slots, emit_rows)
         return (ids, logits) if return_logits else ids
 
     def fused_decoder(self) -> ops.FusedLlamaDecoder:
@@ -136,14 +137,14 @@ class TinyLlama:
             self._fused = ops.FusedLlamaDecoder(dims, ws, self.k_cache, self.v_cache)
         return self._fused
 
-    def _decode_impl(self, tokens, pos, pos_range, max_len, slots=None):
+    def _decode_impl(self, tokens, pos, pos_range, max_len, slots=None, emit_rows=0):
         B = tokens.shape[0]
-        if self.fused and B <= 16:
+        if self.fused and B <= ops.MAX_ROWS:
             tokens, pos = tokens.contiguous(), pos.contiguous()
             slots = slots.contiguous() if slots is not None else None
             logits = torch.empty(B, self.cfg.vocab, dtype=torch.bfloat16, device=self.device)
             ids = torch.empty(B, dtype=torch.int64, device=self.device)
-            self.fused_decoder().step(tokens, pos, max_len, logits, ids, slots)
+            self.fused_decoder().step(tokens, pos, max_len, logits, ids, slots, emit_rows)
             return ids, logits
         return self._decode_unfused(tokens, pos, pos_range, max_len)
 
@@ -169,47 +170,55 @@ class TinyLlama:
         return ops.argmax(logits), logits
 
     # ------------------------------------------------------------------ hipGraph
-    def capture_graph(self, rows: int | None = None):
+    def capture_graph(self, rows: int | None = None, emit_rows: int = 0):
         """Capture one step of ``rows`` token rows into a hipGraph (torch.cuda.CUDAGraph).
 
         Decode at small batch is bound by kernel count; replaying the captured
         graph removes the per-kernel launch cost. The attention is captured for
         the cache capacity (its splits past each row's length exit immediately),
-        so one graph serves every step. Fused path: 16 rows with a row->slot map
-        (padding rows point at the scratch slot); unfused: one row per slot.
+        so one graph serves every step. Fused path: up to 64 rows with a
+        row->slot map (padding rows point at the scratch slot); unfused: one row
+        per slot. Several row counts may be captured (e.g. 16 for decode-heavy
+        steps, 64 for prefill-heavy ones); ``graph_step`` picks the graph by the
+        number of rows it is given. ``emit_rows``: rows that get ids (0: all).
         """
         c = self.cfg
         R = rows or (16 if self.fused else self.max_batch)
         self.graph_rows = R
-        self._g_tok = torch.zeros(R, dtype=torch.int64, device=self.device)
-        self._g_pos = torch.zeros(R, dtype=torch.int32, device=self.device)
-        self._g_slot = (torch.full((R,), self.scratch_slot, dtype=torch.int32, device=self.device)
-                        if self.fused else None)
+        g_tok = torch.zeros(R, dtype=torch.int64, device=self.device)
+        g_pos = torch.zeros(R, dtype=torch.int32, device=self.device)
+        g_slot = (torch.full((R,), self.scratch_slot, dtype=torch.int32, device=self.device)
+                  if self.fused else None)
         full = (0, c.max_seq - 1)
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.no_grad(), torch.cuda.stream(side):
             for _ in range(2):  # allocator + GEMM heuristics warm-up outside capture
-                self._decode_impl(self._g_tok, self._g_pos, full, c.max_seq, self._g_slot)
+                self._decode_impl(g_tok, g_pos, full, c.max_seq, g_slot, emit_rows)
         torch.cuda.current_stream(self.device).wait_stream(side)
-        self._graph = torch.cuda.CUDAGraph()
-        with torch.no_grad(), torch.cuda.graph(self._graph):
-            self._g_ids, self._g_logits = self._decode_impl(self._g_tok, self._g_pos, full, c.max_seq, self._g_slot)
+        graph = torch.cuda.CUDAGraph()
+        with torch.no_grad(), torch.cuda.graph(graph):
+            g_ids, g_logits = self._decode_impl(g_tok, g_pos, full, c.max_seq, g_slot, emit_rows)
+        if not hasattr(self, "_graphs"):
+            self._graphs = {}
+        self._graphs[R] = (graph, g_tok, g_pos, g_slot, g_ids, g_logits)
         return self
 
     @torch.no_grad()
     def graph_step(self, tokens: torch.Tensor, pos: torch.Tensor, slots: torch.Tensor | None = None,
                    return_logits: bool = False):
-        """Replay the captured step. tokens/pos/slots: [graph_rows] (slots default to
-        row b -> slot b); positions must be < max_seq."""
-        self._g_tok.copy_(tokens, non_blocking=True)
-        self._g_pos.copy_(pos, non_blocking=True)
-        if self._g_slot is not None:
+        """Replay the graph captured for ``tokens.shape[0]`` rows. tokens/pos/slots:
+        [rows] (slots default to row b -> slot b); positions must be < max_seq."""
+        R = tokens.shape[0]
+        graph, g_tok, g_pos, g_slot, g_ids, g_logits = self._graphs[R]
+        g_tok.copy_(tokens, non_blocking=True)
+        g_pos.copy_(pos, non_blocking=True)
+        if g_slot is not None:
             if slots is None:
-                slots = torch.arange(self.graph_rows, dtype=torch.int32).clamp_(max=self.scratch_slot)
-            self._g_slot.copy_(slots, non_blocking=True)
-        self._graph.replay()
-        return (self._g_ids, self._g_logits) if return_logits else self._g_ids
+                slots = torch.arange(R, dtype=torch.int32).clamp_(max=self.scratch_slot)
+            g_slot.copy_(slots, non_blocking=True)
+        graph.replay()
+        return (g_ids, g_logits) if return_logits else g_ids
 
     def cache_views_contiguous(self) -> bool:
         return all(self.k_cache[i, : self.max_batch].is_contiguous() for i in range(self.cfg.n_layers))

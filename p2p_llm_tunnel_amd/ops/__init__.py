@@ -42,12 +42,15 @@ def lib() -> ctypes.CDLL:
         _LIB.p2pt_llama_ws_bytes.argtypes = [ctypes.POINTER(LlamaDims)]
         _LIB.p2pt_llama_ws_bytes.restype = ctypes.c_size_t
         _LIB.p2pt_llama_decode.argtypes = [ctypes.POINTER(LlamaDims), ctypes.POINTER(vp), vp, vp, vp, vp, vp, i, i,
-                                           vp, ctypes.c_size_t, vp, vp, vp]
+                                           i, vp, ctypes.c_size_t, vp, vp, vp]
         for fn in ("p2pt_rmsnorm", "p2pt_silu_mul", "p2pt_rope_qkv_cache", "p2pt_decode_attention", "p2pt_argmax",
                    "p2pt_skinny_gemm", "p2pt_llama_decode"):
             getattr(_LIB, fn).restype = ctypes.c_int
     return _LIB
 
+
+
+MAX_ROWS = 64  # token rows per fused step (decode_fused.hip kMaxM)
 
 def loaded_path() -> str:
     lib()
@@ -197,15 +200,15 @@ def argmax(logits: torch.Tensor) -> torch.Tensor:
 
 
 def skinny_gemm(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """bf16(x @ w.T) for a few rows on MFMA (decode-shaped GEMM). x: [M<=16, K]; w: [N, K]."""
+    """bf16(x @ w.T) for a few rows on MFMA (decode-shaped GEMM). x: [M<=64, K]; w: [N, K]."""
     _check(x, torch.bfloat16, "x")
     _check(w, torch.bfloat16, "w", x.device)
     if x.dim() != 2 or w.dim() != 2 or x.shape[1] != w.shape[1]:
         raise ValueError("shapes must be x [M, K], w [N, K]")
     M, K = x.shape
     N = w.shape[0]
-    if not 1 <= M <= 16 or N % 32 or K % 32:
-        raise ValueError("need 1 <= M <= 16, N % 32 == 0, K % 32 == 0")
+    if not 1 <= M <= MAX_ROWS or N % 32 or K % 32:
+        raise ValueError(f"need 1 <= M <= {MAX_ROWS}, N % 32 == 0, K % 32 == 0")
     out = torch.empty(M, N, dtype=x.dtype, device=x.device)
     _ok(lib().p2pt_skinny_gemm(_p(x), _p(w), _p(out), M, N, K, _stream(x)), "skinny_gemm")
     return out
@@ -242,10 +245,12 @@ class FusedLlamaDecoder:
         self.device = dev
 
     def step(self, tokens: torch.Tensor, pos: torch.Tensor, max_len: int, logits: torch.Tensor,
-             ids: torch.Tensor, slots: torch.Tensor | None = None) -> None:
-        """One step over B <= 16 token rows. Row b is token ``tokens[b]`` at cache
-        position ``pos[b]`` of cache slot ``slots[b]`` (default: slot b). Rows of one
-        slot at consecutive positions are a prefill chunk (causal within the step)."""
+             ids: torch.Tensor, slots: torch.Tensor | None = None, emit_rows: int = 0) -> None:
+        """One step over B <= 64 token rows (16-row MFMA tiles). Row b is token
+        ``tokens[b]`` at cache position ``pos[b]`` of cache slot ``slots[b]``
+        (default: slot b). Rows of one slot at consecutive positions are a prefill
+        chunk (causal within the step). Only rows [0, emit_rows) get logits and
+        ids (0: all): the LM head skips prefill rows that sample nothing."""
         d = self.dims
         _check(tokens, torch.int64, "tokens", self.device)
         _check(pos, torch.int32, "pos", self.device)
@@ -256,7 +261,9 @@ class FusedLlamaDecoder:
             _check(slots, torch.int32, "slots", self.device)
             if slots.shape != (B,):
                 raise ValueError("slots must be [B]")
-        limit = 16 if slots is not None else min(16, d.max_batch)
+        limit = MAX_ROWS if slots is not None else min(MAX_ROWS, d.max_batch)
+        if not 0 <= emit_rows <= B:
+            raise ValueError("emit_rows must be in 0..B")
         if not 1 <= B <= limit or pos.shape != (B,) or ids.shape != (B,):
             raise ValueError(f"rows must be 1..{limit} with matching pos/ids")
         if logits.shape != (B, d.vocab):
@@ -264,5 +271,5 @@ class FusedLlamaDecoder:
         if not 1 <= max_len <= d.max_seq:
             raise ValueError("max_len out of range")
         _ok(lib().p2pt_llama_decode(ctypes.byref(d), self._wptr, _p(self.k_cache), _p(self.v_cache), _p(tokens),
-                                    _p(pos), _p(slots), B, max_len, _p(self.ws), self.ws.numel(), _p(logits),
+                                    _p(pos), _p(slots), B, emit_rows, max_len, _p(self.ws), self.ws.numel(), _p(logits),
                                     _p(ids), _stream(tokens)), "llama_decode")

@@ -20,8 +20,9 @@
 //                        per-block greedy winners
 //   k_argmax_merge       one block per row merges the winners
 //
-// Skinny GEMM (M <= 16 tokens): Y[M,N] = A[M,K] * W[N,K]^T on
-// v_mfma_f32_16x16x32_bf16. A workgroup owns 16*TN output columns and splits K
+// Skinny GEMM (M <= 64 tokens): Y[M,N] = A[M,K] * W[N,K]^T on
+// v_mfma_f32_16x16x32_bf16. A workgroup owns 16*TN output columns of one
+// 16-row tile (blockIdx.y; prefill-heavy steps carry up to 4) and splits K
 // over its NW waves; each lane streams its weight rows with 16-byte loads
 // straight into MFMA B fragments (no LDS staging: every weight byte is used
 // exactly once, by exactly one lane), the K-split partials are summed through
@@ -48,7 +49,7 @@ namespace {
 
 using namespace p2pt_gpu;
 
-constexpr int kMaxM = 16;  // tokens per step (one MFMA row tile)
+constexpr int kMaxM = 64;  // token rows per step: up to 4 MFMA row tiles (blockIdx.y)
 
 typedef short frag8 __attribute__((ext_vector_type(8)));
 typedef float frag4 __attribute__((ext_vector_type(4)));
@@ -162,6 +163,7 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
   __shared__ float red[NW][TN][4][kWave];
   __shared__ float red_ss[NW][kWave];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int m0 = blockIdx.y << 4;    // first row of this workgroup's 16-row tile
   const int bx = blockIdx.x / a.ks;  // column tile
   const int kslice = blockIdx.x % a.ks;
   const bool norm = a.ss_part != nullptr;
@@ -177,21 +179,21 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
 #pragma unroll
     for (int i = 0; i < kSsRegs; i++) {
       const int p = ss_p0 + 4 * NW * i;
-      ssv[i] = p < a.ss_parts ? a.ss_part[p * kMaxM + (lane & 15)] : 0.f;
+      ssv[i] = p < a.ss_parts ? a.ss_part[p * kMaxM + m0 + (lane & 15)] : 0.f;
     }
   }
 
   // A fragment: row lane & 15, k = 32*s + 8*(lane>>4) + j; B fragment: W row n, same k.
   // The K steps are split evenly over the NW waves.
   const int m_a = lane & 15;
-  const bool a_ok = m_a < a.M;
+  const bool a_ok = m0 + m_a < a.M;
   const int kq = (lane >> 4) << 3;
   const int S = a.K >> 5;
   const int b0 = kslice * S / a.ks, bs = (kslice + 1) * S / a.ks - b0;  // this workgroup's k-steps
   const int s0 = b0 + wv * bs / NW, s1 = b0 + (wv + 1) * bs / NW;
   // Rows past M are loaded from row M-1 (in bounds) and zeroed: the batch's
   // loads are unconditional.
-  const uint16_t* xrow = a.x + size_t(min(m_a, a.M - 1)) * a.K + kq;
+  const uint16_t* xrow = a.x + size_t(min(m0 + m_a, a.M - 1)) * a.K + kq;
   const uint16_t* wrow[TN];
 #pragma unroll
   for (int t = 0; t < TN; t++) wrow[t] = a.w + size_t(tile_col<TN>(bx, t, lane & 15)) * a.K + kq;
@@ -205,7 +207,7 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
     float ssum = 0.f;
 #pragma unroll
     for (int i = 0; i < kSsRegs; i++) ssum += ssv[i];
-    for (int p = ss_p0 + 4 * NW * kSsRegs; p < a.ss_parts; p += 4 * NW) ssum += a.ss_part[p * kMaxM + (lane & 15)];
+    for (int p = ss_p0 + 4 * NW * kSsRegs; p < a.ss_parts; p += 4 * NW) ssum += a.ss_part[p * kMaxM + m0 + (lane & 15)];
     red_ss[wv][lane] = ssum;
   }
   // K-split reduction through LDS (lane-contiguous: conflict-free).
@@ -247,18 +249,18 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
     if (lane == 0) st_wt(&a.kctr[bx], 0u);
   }
 
-  // C layout: row m = 4*(lane>>4) + r, column = tile_col(.., lane & 15).
-  const int mrow0 = (lane >> 4) << 2;
+  // C layout: row m = m0 + 4*(lane>>4) + r, column = tile_col(.., lane & 15).
+  const int lrow0 = (lane >> 4) << 2, mrow0 = m0 + lrow0;
   const int c = lane & 15;
   if (norm) {
     float ssum = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; w++) ssum += red_ss[w][lane];
     ssum = xor32_sum(xor16_sum(ssum));
-    const float rs_row = rsqrtf(ssum * (1.f / float(a.K)) + a.eps);  // for row lane & 15
+    const float rs_row = rsqrtf(ssum * (1.f / float(a.K)) + a.eps);  // for row m0 + (lane & 15)
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-      const float rs = __shfl(rs_row, mrow0 + r, kWave);
+      const float rs = __shfl(rs_row, lrow0 + r, kWave);
 #pragma unroll
       for (int t = 0; t < TN; t++) v[t][r] *= rs;
     }
@@ -679,7 +681,7 @@ struct Workspace {
   uint16_t *resid, *q, *attn, *h;
   float *ss, *part_o, *part_ml, *am_val;
   int* am_idx;
-  unsigned* counters;  // [16 * H] attention split tickets (self-resetting)
+  unsigned* counters;  // [kMaxM * H] attention split tickets (self-resetting)
   float* kpart;        // split-K slabs of the widest split GEMM
   unsigned* kctr;      // split-K tickets per column tile (self-resetting)
   size_t bytes;
@@ -747,7 +749,7 @@ hipError_t launch_nw(const GemmArgs& a, int grid, hipStream_t s) {
   // capped by the VGPR budget (8, or 4 for 1024-thread two-subtile blocks).
   constexpr int kCap = (NW >= 16 && TN >= 2) ? 4 : 8;
   const int per_wave = ((a.K >> 5) / a.ks + NW - 1) / NW;
-  const dim3 g(grid * a.ks), b(NW * 64);
+  const dim3 g(grid * a.ks, (a.M + 15) >> 4), b(NW * 64);
   if (per_wave <= 1)
     hipLaunchKernelGGL((k_skinny<NW, TN, EPI, 1>), g, b, 0, s, a);
   else if (per_wave <= 2)
@@ -763,6 +765,7 @@ hipError_t launch_nw(const GemmArgs& a, int grid, hipStream_t s) {
 template <int EPI, int TN>
 hipError_t launch_gemm(GemmArgs a, int grid, hipStream_t s, int nw_override = 0) {
   if (a.ks <= 0) a.ks = (a.kpart && a.kctr) ? pick_ks(grid, a.K) : 1;
+  if (a.M > 16) a.ks = 1;  // split-K slabs and tickets are per column tile: one row tile only
   const int nw = nw_override ? nw_override : pick_nw((a.K >> 5) / a.ks);
   if (nw == 16) return launch_nw<16, TN, EPI>(a, grid, s);
   if (nw == 8) return launch_nw<8, TN, EPI>(a, grid, s);
@@ -798,17 +801,20 @@ size_t p2pt_llama_ws_bytes(const LlamaDims* d) {
 //      wqkv rows are interleaved per head (dim i, dim i + D/2, ...) and w_gate_up
 //      rows per pair (gate_j, up_j, ...).
 //   k_cache/v_cache: [n_layers][max_batch][max_seq][Hkv][D]
-//   tokens int64 [B], pos int32 [B] (< max_seq), logits bf16 [B][vocab], ids int64 [B]
+//   tokens int64 [B <= 64], pos int32 [B] (< max_seq), logits bf16 [B][vocab], ids int64 [B]
+//   emit_rows: only rows [0, emit_rows) get logits and ids (the LM head runs on
+//     them alone: prefill rows that sample nothing go last); <= 0 means B
 //   slots int32 [B] or nullptr: cache slot of each row (< max_batch). Rows of one
 //     slot at consecutive positions form a prefill chunk: every row's K/V is
 //     appended before attention runs, and each row attends up to its own position.
 //   max_len: host bound on max(pos) + 1 (sizes the attention grid; use max_seq under graph capture)
 int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, void* v_cache, const int64_t* tokens,
-                      const int* pos, const int* slots, int B, int max_len, void* ws, size_t ws_bytes, void* logits,
-                      int64_t* ids, void* stream) {
+                      const int* pos, const int* slots, int B, int emit_rows, int max_len, void* ws, size_t ws_bytes,
+                      void* logits, int64_t* ids, void* stream) {
   const LlamaDims d = *dp;
   if (!dims_ok(d) || B <= 0 || B > kMaxM || (!slots && B > d.max_batch) || max_len <= 0 || max_len > d.max_seq)
     return int(hipErrorInvalidValue);
+  if (emit_rows <= 0 || emit_rows > B) emit_rows = B;
   Workspace W = carve(d, static_cast<uint8_t*>(ws));
   if (ws_bytes < W.bytes) return int(hipErrorInvalidValue);
   auto s = static_cast<hipStream_t>(stream);
@@ -882,18 +888,18 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
 
   // final norm + LM head + argmax
   GemmArgs h{};
-  h.M = B; h.eps = d.eps; h.x = W.resid; h.w = bf(2); h.N = d.vocab; h.K = d.dim;
+  h.M = emit_rows; h.eps = d.eps; h.x = W.resid; h.w = bf(2); h.N = d.vocab; h.K = d.dim;
   h.ss_part = W.ss; h.ss_parts = ss_parts;
   h.out = static_cast<uint16_t*>(logits);
   h.am_val = W.am_val; h.am_idx = W.am_idx;
   const int parts = d.vocab / (16 * kTnStore);
   // 4 waves x 2 subtiles: the fastest LM-head shape measured (vocab 32000, K 2048: 22.6 vs 29.6 us).
   if ((e = launch_gemm<EPI_ARGMAX, kTnStore>(h, parts, s, 4)) != hipSuccess) return int(e);
-  hipLaunchKernelGGL(k_argmax_merge, dim3(B), dim3(256), 0, s, W.am_val, W.am_idx, parts, ids);
+  hipLaunchKernelGGL(k_argmax_merge, dim3(emit_rows), dim3(256), 0, s, W.am_val, W.am_idx, parts, ids);
   return int(hipGetLastError());
 }
 
-// Standalone skinny GEMM (tests/benchmarks): out[M][N] = bf16(x[M][K] @ w[N][K]^T), M <= 16.
+// Standalone skinny GEMM (tests/benchmarks): out[M][N] = bf16(x[M][K] @ w[N][K]^T), M <= 64.
 int p2pt_skinny_gemm(const void* x, const void* w, void* out, int M, int N, int K, void* stream) {
   if (M <= 0 || M > kMaxM || N % 32 || K <= 0 || K % 32) return int(hipErrorInvalidValue);
   GemmArgs a{};

@@ -180,3 +180,47 @@ def test_gpu_endpoint_through_tunnel():
     finally:
         engine.stop()
         srv.shutdown()
+
+
+@cuda
+def test_64_row_prefill_chunk_matches_16_row_chunks():
+    # One 64-row step (4 MFMA row tiles: a 57-token prompt chunk plus decode
+    # rows of other slots) equals the same prompt fed as 16-row chunks; with
+    # emit_rows the LM head covers only the leading rows and their ids match.
+    from p2p_llm_tunnel_amd.models.tiny_llm import TinyLlama
+    m1 = TinyLlama("micro", device="cuda", max_batch=3, seed=9)
+    m2 = TinyLlama("micro", device="cuda", max_batch=3, seed=9)
+    torch.manual_seed(5)
+    T = 57
+    prompt = torch.randint(0, m1.cfg.vocab, (T,), device="cuda")
+    two = lambda n: torch.full((n,), 2, dtype=torch.int32, device="cuda")
+    for c0 in range(0, T, 16):
+        c1 = min(c0 + 16, T)
+        ids1, l1 = m1.decode_step(prompt[c0:c1], torch.arange(c0, c1, dtype=torch.int32, device="cuda"), (c0, c1 - 1),
+                                  return_logits=True, slots=two(c1 - c0))
+    # 64 rows: two decode rows first (slots 0, 1 at position 0), then the chunk, then padding to the scratch slot
+    toks = torch.cat([torch.tensor([11, 12], device="cuda"), prompt,
+                      torch.zeros(64 - 2 - T, dtype=torch.int64, device="cuda")])
+    pos = torch.cat([torch.zeros(2, dtype=torch.int32, device="cuda"), torch.arange(T, dtype=torch.int32, device="cuda"),
+                     torch.zeros(64 - 2 - T, dtype=torch.int32, device="cuda")])
+    slots = torch.cat([torch.tensor([0, 1], dtype=torch.int32, device="cuda"), two(T),
+                       torch.full((64 - 2 - T,), m2.scratch_slot, dtype=torch.int32, device="cuda")])
+    ids2, l2 = m2.decode_step(toks, pos, (0, T - 1), return_logits=True, slots=slots)
+    ref = l1[-1].float()
+    assert (l2[2 + T - 1].float() - ref).abs().max().item() <= 1e-6 + 0.01 * ref.abs().max().item()
+    assert int(ids2[2 + T - 1]) == int(ids1[-1])
+    # the KV cache written by the 64-row step matches the chunked one
+    assert torch.equal(m1.k_cache[:, 2, :T], m2.k_cache[:, 2, :T])
+    # emit_rows: LM head on the first rows only; same ids there
+    m3 = TinyLlama("micro", device="cuda", max_batch=3, seed=9)
+    order = torch.cat([torch.tensor([0, 1, 2 + T - 1], device="cuda"), torch.arange(2, 2 + T - 1, device="cuda"),
+                       torch.arange(2 + T, 64, device="cuda")])
+    ids3 = m3.decode_step(toks[order], pos[order], (0, T - 1), slots=slots[order], emit_rows=3)
+    assert torch.equal(ids3[:3], ids2[order[:3]])
+    # both graphs of the engine's pair replay correctly
+    m3.capture_graph(rows=16)
+    m3.capture_graph(rows=64, emit_rows=3)
+    m3.k_cache.zero_()
+    m3.v_cache.zero_()
+    g = m3.graph_step(toks[order], pos[order], slots[order])
+    assert torch.equal(g[:3], ids2[order[:3]])

@@ -132,7 +132,9 @@ def test_argmax(ops, V):
 
 @cuda
 @pytest.mark.parametrize("M,N,K", [(1, 1536, 1024), (8, 2048, 2816), (16, 32000, 1024), (3, 64, 256), (16, 96, 4096),
-                                   (5, 256, 96), (16, 64, 8192)])
+                                   (5, 256, 96), (16, 64, 8192),
+                                   # several 16-row MFMA tiles (blockIdx.y), partial last tile
+                                   (17, 1536, 1024), (40, 2048, 2816), (64, 32000, 1024), (33, 96, 4096)])
 def test_skinny_gemm(ops, M, N, K):
     # Asymmetric operands: a transposed C write would not pass.
     torch.manual_seed(M * 7 + K)
@@ -163,7 +165,7 @@ def test_host_side_shape_checks(ops):
         ops.rope_qkv_cache(bf(torch.randn(2, 5, device="cuda")), torch.zeros(2, dtype=torch.int32, device="cuda"),
                            kc, kc, 8, 2, 64)
     with pytest.raises(ValueError):
-        ops.skinny_gemm(bf(torch.randn(17, 128, device="cuda")), bf(torch.randn(32, 128, device="cuda")))  # M > 16
+        ops.skinny_gemm(bf(torch.randn(65, 128, device="cuda")), bf(torch.randn(32, 128, device="cuda")))  # M > 64
     with pytest.raises(ValueError):
         ops.skinny_gemm(bf(torch.randn(2, 100, device="cuda")), bf(torch.randn(32, 100, device="cuda")))  # K % 32
 
