@@ -30,9 +30,13 @@ from p2p_llm_tunnel_amd.utils.procs import Tunnel, free_port, spawn  # noqa: E40
 
 
 def loadgen(port, streams, steps, body, warmup=1):
+    # --warm-conns 1: the warmup runs on the timed keep-alive connections, so
+    # connection setup stays out of the timed steps for both paths (a burst of
+    # 32+ fresh connections to the Python endpoint costs its first step
+    # 130-210 ms on the MI355X box; serve's upstream pool is connected ahead).
     out = subprocess.run([binary("tunnel-loadgen"), "--target", f"127.0.0.1:{port}", "--streams", str(streams),
                           "--steps", str(steps), "--warmup", str(warmup), "--path", "/v1/chat/completions",
-                          "--body", body], capture_output=True, text=True, timeout=900)
+                          "--body", body, "--warm-conns", "1"], capture_output=True, text=True, timeout=900)
     try:
         return json.loads(out.stdout.strip().splitlines()[-1])
     except (IndexError, ValueError):
@@ -59,10 +63,7 @@ def main():
                            "messages": [{"role": "user", "content": "x" * a.prompt_bytes}]})
         rows = []
         counts = [int(x) for x in a.streams.split(",")]
-        # Direct baselines first, with no tunnel attached: with serve's idle
-        # upstream pool connected, the first direct step at 16 streams stalled
-        # ~190 ms (one TCP retransmission timeout) on the MI355X box
-        # (scripts/gpu/diag_direct16.py), which is not a property of either path.
+        # Direct baselines first, with no tunnel attached.
         direct = {s: loadgen(port, s, a.steps, body) for s in counts}
         with Tunnel(f"http://127.0.0.1:{port}", transport=os.environ.get("P2PT_TRANSPORT", "webrtc")) as t:
             for s in counts:
@@ -75,7 +76,8 @@ def main():
                        "added_p50_ttft_ms": round(tr["p50_ttft_ms"] - dr["p50_ttft_ms"], 3),
                        "tunneled_p99_ttft_ms": tr["p99_ttft_ms"], "direct_p99_ttft_ms": dr["p99_ttft_ms"],
                        "tunneled_p50_total_ms": tr["p50_total_ms"], "direct_p50_total_ms": dr["p50_total_ms"],
-                       "errors": tr["errors"] + dr["errors"]}
+                       "errors": tr["errors"] + dr["errors"],
+                       "tunneled_step_ms": tr.get("step_ms"), "direct_step_ms": dr.get("step_ms")}
                 rows.append(row)
                 print(json.dumps(row), file=sys.stderr, flush=True)
         doc = {"upstream": f"p2p_llm_tunnel_amd.models.server ({a.config}, fused gfx950 decode, hipGraph)",

@@ -175,6 +175,7 @@ double pct(std::vector<double> v, double q) {
 int main(int argc, char** argv) {
   Opts o;
   int warmup = 1;
+  bool warm_conns = false;  // --warm-conns 1: warmup on the timed steps' own connections
   for (int i = 1; i + 1 < argc; i += 2) {
     std::string a = argv[i], v = argv[i + 1];
     if (a == "--target") {
@@ -189,6 +190,7 @@ int main(int argc, char** argv) {
       if (v == "/api/generate") o.body = R"({"model": "test-model", "prompt": "hi", "stream": true})";
     } else if (a == "--body") o.body = v;
     else if (a == "--post-bytes") o.post_bytes = size_t(strtoull(v.c_str(), nullptr, 10));
+    else if (a == "--warm-conns") warm_conns = v == "1";
   }
   signal(SIGPIPE, SIG_IGN);
   Reactor r;
@@ -199,6 +201,8 @@ int main(int argc, char** argv) {
   std::function<void()> launch;
   // Warmup steps run on their own connections (results discarded); the timed
   // steps reuse one keep-alive connection per stream when the server allows.
+  // --warm-conns 1 warms up on the timed connections instead, so connection
+  // setup stays out of the timed steps (steady-state keep-alive serving).
   std::vector<std::shared_ptr<Stream>> live, warmers;
   for (int i = 0; i < o.streams; i++) {
     live.push_back(std::make_shared<Stream>(r, o, res));
@@ -206,8 +210,14 @@ int main(int argc, char** argv) {
   }
   std::vector<uint64_t> step_end;  // timed steps' completion times (per-step durations in the output)
   launch = [&] {
-    auto& set = step < warmup ? warmers : live;
-    if (step == warmup) t_start = Reactor::now_us();
+    auto& set = step < warmup && !warm_conns ? warmers : live;
+    if (step == warmup) {
+      t_start = Reactor::now_us();
+      if (warm_conns) {  // drop what the warmup recorded on the live streams
+        warm_res.errors += res.errors;
+        res = Result{};
+      }
+    }
     pending = o.streams;
     for (auto& s : set) s->request();
   };

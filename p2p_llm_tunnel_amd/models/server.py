@@ -32,6 +32,7 @@ import asyncio
 import json
 import queue
 import socket
+import sys
 import threading
 import time
 import uuid
@@ -100,8 +101,8 @@ class Engine:
             model = TinyLlama(config, device=device, max_batch=max_batch, seed=seed, fused=True)
         else:
             use_graph = False
-        if not 1 <= max_batch <= small_rows <= rows:
-            raise ValueError("need 1 <= max_batch <= small_rows <= rows")
+        if not (1 <= max_batch <= rows and 1 <= small_rows <= rows):
+            raise ValueError("need 1 <= max_batch <= rows and small_rows <= rows")
         self.model = model
         self.device = self.model.device
         self.rows = rows
@@ -109,9 +110,10 @@ class Engine:
         self.use_graph = use_graph
         cuda = self.device.type == "cuda"
         if use_graph:
-            # Two graphs: decode-heavy steps replay the 16-row one; prefill-heavy
-            # steps the 64-row one (4 MFMA row tiles), whose LM head covers only
-            # the leading rows that sample (at most one per slot).
+            # Two graphs: steps of up to 16 rows replay the 16-row one, larger
+            # (prefill-heavy, or more than 16 generating slots) the 64-row one (4
+            # MFMA row tiles), whose LM head covers only the leading rows that
+            # sample (at most one per slot, so max_batch rows).
             self.model.capture_graph(rows=small_rows)
             if rows > small_rows:
                 self.model.capture_graph(rows=rows, emit_rows=max_batch)
@@ -254,6 +256,11 @@ class Engine:
                     self._drain(inflight.pop(0), batch)
                 if batch:
                     self._flush(batch)
+                # Hand the GIL over once per step: when the host is the slower
+                # side the event wait above returns at once, and the HTTP thread
+                # (accepting a burst of new connections, say) would otherwise get
+                # the GIL only at the interpreter's forced-switch interval.
+                time.sleep(0)
                 if not rows and not inflight:
                     self._wake.wait(0.05)
                     self._wake.clear()
@@ -504,6 +511,7 @@ def start_server(host="127.0.0.1", port=0, device="cuda:0", config="tiny", max_b
                  engine: Engine | None = None):
     """Engine + HTTP front-end; returns (server, port, engine). ``server.shutdown()``
     stops the HTTP side, ``engine.stop()`` the GPU side."""
+    sys.setswitchinterval(0.0005)  # two busy threads: bound a GIL wait at 0.5 ms, not 5
     engine = engine or Engine(device=device, config=config, max_batch=max_batch)
     srv = FrontEnd(engine, host, port, model_name or f"p2pt-{config}")
     return srv, srv.server_address[1], engine
@@ -517,7 +525,6 @@ def _replicas(a) -> int:
     fewest in flight. Each child is a fresh interpreter pinned to its device;
     the parent never touches the GPU and exits with the first child that dies."""
     import subprocess
-    import sys
     base = a.port
     procs = []
     for i in range(a.gpus):
