@@ -88,7 +88,9 @@ class Engine:
     updates after the step, and the sampled ids come back through a pinned
     buffer and an event per step. The host waits on step k (GIL released, so
     the HTTP thread writes meanwhile) only after step k+1 is queued behind it.
-    The step itself is replayed from one hipGraph.
+    Each step is one hipGraph replay: input copy from pinned staging, decode
+    token gather, the fused step, last-token scatter, ids back to pinned
+    memory.
 
     ``model`` injects a model object (tests use a CPU stand-in with the same
     ``decode_step`` / ``cfg`` / ``scratch_slot`` / ``device`` surface).
@@ -109,18 +111,26 @@ class Engine:
         self.small_rows = small_rows
         self.use_graph = use_graph
         cuda = self.device.type == "cuda"
-        if use_graph:
-            # Two graphs: steps of up to 16 rows replay the 16-row one, larger
-            # (prefill-heavy, or more than 16 generating slots) the 64-row one (4
-            # MFMA row tiles), whose LM head covers only the leading rows that
-            # sample (at most one per slot, so max_batch rows).
-            self.model.capture_graph(rows=small_rows)
-            if rows > small_rows:
-                self.model.capture_graph(rows=rows, emit_rows=max_batch)
-        self._bufs = [_StepBuf(rows, cuda), _StepBuf(rows, cuda)]
         self._k = 0
-        self._d_in = torch.zeros((5, rows), dtype=torch.int64, device=self.device) if cuda else None
         self._d_last = torch.zeros(max_batch + 1, dtype=torch.int64, device=self.device)
+        self._graphs = {}
+        if use_graph:
+            # Two row counts: steps of up to 16 rows replay the 16-row graphs,
+            # larger ones (prefill-heavy, or more than 16 generating slots) the
+            # 64-row graphs (4 MFMA row tiles), whose LM head covers only the
+            # leading rows that sample (at most one per slot: max_batch rows).
+            # Each graph holds the whole step: input copy from its pinned
+            # staging buffer, decode-row token gather, the fused step, the
+            # last-token scatter and the copy of the ids back to pinned memory;
+            # one per staging buffer of the pair, so a step is one replay.
+            sizes = [small_rows] + ([rows] if rows > small_rows else [])
+            self._bufs = {R: [_StepBuf(R, cuda), _StepBuf(R, cuda)] for R in sizes}
+            self._d_in = {R: torch.zeros((5, R), dtype=torch.int64, device=self.device) for R in sizes}
+            for R in sizes:
+                for par in (0, 1):
+                    self._graphs[(R, par)] = self._capture(self._bufs[R][par], R, 0 if R == small_rows else max_batch)
+        else:
+            self._bufs = {rows: [_StepBuf(rows, cuda), _StepBuf(rows, cuda)]}
         self.max_batch = max_batch
         self.pending: queue.Queue = queue.Queue()
         self.slots: list[dict | None] = [None] * max_batch
@@ -192,11 +202,43 @@ class Engine:
                 self.slots[i] = None
         return rows, emits
 
+    def _step_body(self, b: _StepBuf, R: int, emit_rows: int):
+        """The captured step: staging -> device, token gather, fused step,
+        last-token scatter, ids -> pinned staging."""
+        d = self._d_in[R]
+        d.copy_(b.h_in, non_blocking=True)
+        tok = torch.where(d[3] != 0, self._d_last[d[2]], d[0])
+        S = self.model.cfg.max_seq
+        ids, _ = self.model._decode_impl(tok, d[1].to(torch.int32), (0, S - 1), S, d[2].to(torch.int32), emit_rows)
+        self._d_last.index_copy_(0, d[4], ids)
+        b.h_out.copy_(ids, non_blocking=True)
+
+    def _capture(self, b: _StepBuf, R: int, emit_rows: int):
+        scratch = self.model.scratch_slot
+        b.np[:] = 0
+        b.np[2, :] = scratch  # warm-up and capture touch the scratch slot only
+        b.np[4, :] = scratch
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.no_grad(), torch.cuda.stream(side):
+            for _ in range(2):  # allocator + kernel warm-up outside capture
+                self._step_body(b, R, emit_rows)
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.no_grad(), torch.cuda.graph(graph):
+            self._step_body(b, R, emit_rows)
+        torch.cuda.synchronize(self.device)
+        return graph
+
     def _launch(self, rows, emits) -> _StepBuf:
-        b = self._bufs[self._k % 2]
-        self._k += 1
         n, scratch = len(rows), self.model.scratch_slot
-        R = self.small_rows if n <= self.small_rows else self.rows
+        if self.use_graph:
+            R = self.small_rows if n <= self.small_rows else self.rows
+        else:
+            R = self.rows
+        par = self._k % 2
+        self._k += 1
+        b = self._bufs[R][par]
         h = b.np
         h[0, :n] = [r[1] for r in rows]
         h[1, :n] = [r[2] for r in rows]
@@ -209,20 +251,15 @@ class Engine:
             h[3, n:R] = 0
             h[4, n:R] = scratch
         b.n, b.emits = n, emits
-        m = R if self.use_graph else n
-        if self._d_in is not None:
-            self._d_in.copy_(b.h_in, non_blocking=True)
-            d = self._d_in
-        else:
-            d = b.h_in
-        tok = torch.where(d[3, :m] != 0, self._d_last[d[2, :m]], d[0, :m])
         if self.use_graph:
-            ids = self.model.graph_step(tok, d[1, :m], d[2, :m])
-        else:
+            self._graphs[(R, par)].replay()
+        else:  # injected model (tests): the same step, eagerly, on its n rows
+            d = b.h_in.to(self.device)
+            tok = torch.where(d[3, :n] != 0, self._d_last[d[2, :n]], d[0, :n])
             lo, hi = min(r[2] for r in rows), max(r[2] for r in rows)
-            ids = self.model.decode_step(tok, d[1, :m].to(torch.int32), (lo, hi), slots=d[2, :m].to(torch.int32))
-        self._d_last.index_copy_(0, d[4, :m], ids[:m].to(torch.int64))
-        b.h_out[:m].copy_(ids[:m], non_blocking=True)
+            ids = self.model.decode_step(tok, d[1, :n].to(torch.int32), (lo, hi), slots=d[2, :n].to(torch.int32))
+            self._d_last.index_copy_(0, d[4, :n], ids.to(torch.int64))
+            b.h_out[:n].copy_(ids)
         if b.ev is not None:
             b.ev.record()
         self.steps += 1
