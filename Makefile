@@ -15,6 +15,9 @@
 #   make proxy ROOM=r [LISTEN=127.0.0.1:8000]
 #   make signal [PORT=8787]
 #   make docker-signal    container image for the signal server (deploy/)
+#   make deploy-signal    deploy the signal server to Fly.io (deploy/fly.toml; needs flyctl)
+#   make signal-status    Fly.io status of the signal server app
+#   make signal-logs      Fly.io logs of the signal server app
 #   make clean
 
 BUILD ?= build
@@ -25,7 +28,7 @@ LISTEN ?= 127.0.0.1:8000
 SIGNAL_FLAG := $(if $(SIGNAL),--signal $(SIGNAL),)
 
 .PHONY: build build-tunnel build-signal build-ops test test-unit test-local test-public test-gpu \
-        sanitize tsan bench serve proxy signal docker-signal clean
+        sanitize tsan bench serve proxy signal docker-signal deploy-signal signal-status signal-logs clean
 
 build:
 	cmake -S . -B $(BUILD) -G Ninja -DCMAKE_BUILD_TYPE=Release
@@ -79,6 +82,18 @@ signal: build
 
 docker-signal:
 	docker build -f deploy/Dockerfile.signal -t p2pt-signal .
+
+FLY ?= fly
+FLY_CONFIG := deploy/fly.toml
+
+deploy-signal:
+	$(FLY) deploy --config $(FLY_CONFIG) --dockerfile deploy/Dockerfile.signal .
+
+signal-status:
+	$(FLY) status --config $(FLY_CONFIG)
+
+signal-logs:
+	$(FLY) logs --config $(FLY_CONFIG)
 
 clean:
 	rm -rf $(BUILD) $(BUILD)-asan $(BUILD)-tsan

@@ -157,6 +157,7 @@ int run_app(const AppConfig& cfg) {
     uint64_t backoff_timer = 0;
     uint64_t session_start_ms = 0;
     int exit_code = 0;
+    bool interrupted = false;  // Ctrl-C / SIGTERM, as opposed to giving up after --max-retries
     bool in_attempt = false;
     EarlyListener early;
   } st;
@@ -265,6 +266,7 @@ int run_app(const AppConfig& cfg) {
       LOG_INFO(kT, "received Ctrl+C, exiting");
     }
     st.exit_code = 1;
+    st.interrupted = true;
     st.in_attempt = false;
     r.stop();
   };
@@ -280,7 +282,9 @@ int run_app(const AppConfig& cfg) {
   st.transport.reset();
   // Let queued close/bye frames go out.
   r.run_until([] { return false; }, 50);
-  if (st.exit_code) fprintf(stderr, "Error: interrupted by user\n");
+  if (st.interrupted) fprintf(stderr, "Error: interrupted by user\n");
+  else if (st.exit_code) fprintf(stderr, "Error: %s failed after %llu attempts\n", cfg.mode.c_str(),
+                                 static_cast<unsigned long long>(cfg.max_retries));
   return st.exit_code;
 }
 

@@ -160,7 +160,11 @@ class Engine:
                     req = self.pending.get_nowait()
                 except queue.Empty:
                     return
-                ids = req.prompt[: self.model.cfg.max_seq - req.max_new - 1] or [0]
+                # Keep at least the prompt's first token: max_new is clamped
+                # so prompt + generated rows fit max_seq.
+                max_seq = self.model.cfg.max_seq
+                req.max_new = max(1, min(req.max_new, max_seq - 2))
+                ids = req.prompt[: max_seq - req.max_new - 1] or [0]
                 self.slots[i] = {"req": req, "pos": 0, "ids": ids, "gen": 0}
 
     def _plan(self, batch: list):
@@ -188,18 +192,26 @@ class Engine:
         # Rows that sample go first: the 64-row graph's LM head covers only the
         # first max_batch rows (each slot samples at most once per step).
         rows.sort(key=lambda r: not r[4])
+        # Advance every row's slot first: after the sort a slot's sampling row
+        # can precede its other prompt rows, so slots are only freed once all
+        # rows of the step are accounted for.
         max_seq = self.model.cfg.max_seq
-        for r, (i, _, _, _, emit) in enumerate(rows):
-            s = self.slots[i]
-            s["pos"] += 1
+        for i, _, _, _, emit in rows:
+            self.slots[i]["pos"] += 1
             if not emit:
                 self.prefill_tokens += 1
+        done = []
+        for r, (i, _, _, _, emit) in enumerate(rows):
+            if not emit:
                 continue
+            s = self.slots[i]
             s["gen"] += 1
             fin = s["gen"] >= s["req"].max_new or s["pos"] >= max_seq - 1
             emits.append((r, s["req"], fin))
             if fin:
-                self.slots[i] = None
+                done.append(i)
+        for i in done:
+            self.slots[i] = None
         return rows, emits
 
     def _step_body(self, b: _StepBuf, R: int, emit_rows: int):
@@ -528,7 +540,12 @@ class FrontEnd:
                 req_body = {}
         except ValueError:
             req_body = {}
-        max_new = int(req_body.get("max_tokens", req_body.get("num_predict", 16)) or 16)
+        raw_max = req_body.get("max_tokens", req_body.get("num_predict", 16))
+        try:
+            max_new = int(raw_max if raw_max is not None else 16)
+        except (TypeError, ValueError):
+            writer.write(self._json_response({"error": f"max_tokens must be an integer, got {raw_max!r}"}, 400))
+            return True
         ollama = path == "/api/generate"
         kind = "ollama" if ollama else ("chat" if "chat" in path else "text")
         stream = bool(req_body.get("stream", ollama))

@@ -130,6 +130,38 @@ def test_concurrent_streams_are_batched_and_independent():
         eng.stop()
 
 
+def test_single_token_requests_with_multibyte_prompts():
+    """max_tokens=1 finishes a request on its prompt's sampling row, which the
+    step plan orders before that prompt's other rows; the engine must survive
+    it (stream and non-stream), and bad/edge max_tokens values get answers."""
+    srv, port, eng = _server(max_seq=64)
+    try:
+        for stream in (True, False):
+            for mt in (1, 0, -5, None):
+                body = {"stream": stream, "prompt": "hello world", "max_tokens": mt}
+                st, _, data, _ = _post(port, "/v1/completions", body)
+                assert st == 200, data
+                if stream:
+                    objs = [json.loads(l[6:]) for l in data.split(b"\n") if l.startswith(b"data: {")]
+                    text = "".join(o["choices"][0]["text"] for o in objs)
+                else:
+                    text = json.loads(data)["choices"][0]["text"]
+                n = 16 if mt is None else 1
+                assert text == "".join(f" t{t}" for t in expected(b"hello world", n)), (stream, mt, text)
+        assert eng.thread.is_alive()
+        # max_tokens beyond the context: clamped, the prompt's head is kept
+        st, _, data, _ = _post(port, "/v1/completions", {"stream": False, "prompt": "abc", "max_tokens": 1000})
+        assert st == 200 and json.loads(data)["choices"][0]["text"].count(" t") == 62
+        for bad in ("lots", [3], {"x": 1}):
+            st, _, data, _ = _post(port, "/v1/completions", {"prompt": "a", "max_tokens": bad})
+            assert st == 400 and b"max_tokens" in data
+        st, _, data, _ = _post(port, "/v1/completions", {"stream": False, "prompt": "ok", "max_tokens": 2})
+        assert st == 200 and eng.thread.is_alive()
+    finally:
+        srv.shutdown()
+        eng.stop()
+
+
 def test_client_disconnect_frees_the_slot():
     srv, port, eng = _server(delay_s=0.005)
     try:
