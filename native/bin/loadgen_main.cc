@@ -1,19 +1,30 @@
 // `tunnel-loadgen` — native streamed-completion load generator.
 //
 // S client connections (keep-alive when the server allows it) each issue K
-// back-to-back `POST /v1/chat/completions {"stream": true}` requests; a
-// "step" is one request on every connection, all in flight together (the
-// multiplexing dimension of the tunnel). TTFT = time from
-// writing the request to the first byte of the first `data:` event. Runs on
-// the reactor (no interpreter jitter), so µs-scale tunnel overhead is visible.
-// Output: one JSON object on stdout.
+// back-to-back requests (default `POST /v1/chat/completions {"stream": true}`);
+// a "step" is one request on every connection of a thread, all in flight
+// together (the multiplexing dimension of the tunnel).
+//
+// Measured per request: TTFT = time from writing the request to the first
+// body byte; per streamed event (SSE "\n\n"-terminated, NDJSON "\n"-terminated)
+// its arrival time, from which the inter-token latency (ITL: gap between
+// consecutive events of one response) is derived — the number that shows
+// head-of-line blocking behind other streams' bulk frames.
+//
+// --threads T spreads the streams over T reactor threads (one node-scale
+// client must not be the bottleneck it measures); --target takes a comma-
+// separated list (stream i uses target i mod n: the direct baseline against
+// several upstreams). Runs on the reactor (no interpreter jitter), so µs-scale
+// tunnel overhead is visible. Output: one JSON object on stdout.
 #include <signal.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "core/net.h"
@@ -24,33 +35,47 @@ using namespace p2pt;
 
 namespace {
 
-struct Opts {
+struct Target {
   std::string host = "127.0.0.1";
   uint16_t port = 8000;
+};
+
+struct Opts {
+  std::vector<Target> targets{Target{}};
   int streams = 8;
   int steps = 10;
+  int warmup = 1;
+  int threads = 1;
+  bool warm_conns = false;
+  std::string method = "POST";
   std::string path = "/v1/chat/completions";
   std::string body = R"({"model": "test-model", "stream": true, "messages": [{"role": "user", "content": "hi"}]})";
   size_t post_bytes = 0;  // >0: POST /echo with this many bytes instead
+  char event_sep = 0;     // 0: auto from content-type (SSE "\n\n", NDJSON "\n"); 'n' none
+  uint64_t read_rate = 0; // >0: read at most this many body bytes/s per stream (slow client)
 };
 
 struct Result {
-  std::vector<double> ttft_us, total_us;
+  std::vector<double> ttft_us, total_us, itl_us;
   int errors = 0;
   uint64_t body_bytes = 0;
+  uint64_t events = 0;
+  std::vector<uint64_t> step_end;
+  uint64_t t_start = 0, t_end = 0;
 };
 
 class Stream : public std::enable_shared_from_this<Stream> {
  public:
-  Stream(Reactor& r, const Opts& o, Result& res) : r_(r), o_(o), res_(res) {}
+  Stream(Reactor& r, const Opts& o, const Target& t, Result* res) : r_(r), o_(o), t_(t), res_(res) {}
   std::function<void()> on_done;  // one request finished
+  void set_result(Result* r) { res_ = r; }
 
   void request() {
     if (!conn_ || conn_->closed()) {
       auto self = shared_from_this();
-      TcpConn::connect(r_, o_.host, o_.port, false, [self](std::shared_ptr<TcpConn> c, std::string err) {
+      TcpConn::connect(r_, t_.host, t_.port, false, [self](std::shared_ptr<TcpConn> c, std::string err) {
         if (!c) {
-          self->res_.errors++;
+          self->res_->errors++;
           self->finish();
           return;
         }
@@ -71,17 +96,38 @@ class Stream : public std::enable_shared_from_this<Stream> {
 
  private:
   void send() {
-    std::string body = o_.post_bytes ? std::string(o_.post_bytes, 'x') : o_.body;
+    std::string body = o_.post_bytes ? std::string(o_.post_bytes, 'x') : (o_.method == "GET" ? "" : o_.body);
     std::string path = o_.post_bytes ? "/echo" : o_.path;
-    std::string req = "POST " + path + " HTTP/1.1\r\nHost: " + o_.host + ":" + std::to_string(o_.port) +
-                      "\r\nContent-Type: application/json\r\nContent-Length: " + std::to_string(body.size()) +
-                      "\r\n\r\n" + body;
+    std::string method = o_.post_bytes ? "POST" : o_.method;
+    std::string req = method + " " + path + " HTTP/1.1\r\nHost: " + t_.host + ":" + std::to_string(t_.port) + "\r\n";
+    if (method != "GET") req += "Content-Type: application/json\r\nContent-Length: " + std::to_string(body.size()) + "\r\n";
+    req += "\r\n" + body;
     buf_.clear();
     head_done_ = false;
     first_ = 0;
+    last_ev_ = 0;
+    sep_run_ = 0;
     active_ = true;
     t0_ = Reactor::now_us();
     conn_->write(std::move(req));
+  }
+
+  // Event boundaries inside the decoded body bytes; records ITL gaps.
+  void scan_events(const uint8_t* d, size_t k, uint64_t now) {
+    if (sep_ == 'n') return;
+    for (size_t i = 0; i < k; i++) {
+      if (d[i] == '\n') {
+        sep_run_++;
+        if ((sep_ == 'l' && sep_run_ >= 1) || (sep_ == 's' && sep_run_ == 2)) {
+          res_->events++;
+          if (last_ev_) res_->itl_us.push_back(double(now - last_ev_));
+          last_ev_ = now;
+          if (sep_ == 'l') sep_run_ = 0;
+        }
+      } else if (d[i] != '\r') {
+        sep_run_ = 0;
+      }
+    }
   }
 
   void on_data(const uint8_t* p, size_t n) {
@@ -92,31 +138,58 @@ class Stream : public std::enable_shared_from_this<Stream> {
       auto rs = http::parse_response_head(buf_, head_, used, nullptr);
       if (rs == http::ParseResult::Incomplete) return;
       if (rs == http::ParseResult::Error || head_.status != 200) {
-        res_.errors++;
+        res_->errors++;
         active_ = false;
         conn_->close();
         return;
       }
       buf_.erase(0, used);
       uint64_t len = 0;
-      auto mode = http::response_body_mode(head_, "POST", len);  // sets len: evaluate before reset()
+      auto mode = http::response_body_mode(head_, o_.post_bytes ? "POST" : o_.method.c_str(), len);  // sets len
       body_.reset(mode, len);
       keep_ = head_.version_minor >= 1 && !head_.has_token("connection", "close") &&
               body_.mode() != http::BodyDecoder::Mode::UntilClose;
       head_done_ = true;
+      sep_ = o_.event_sep;
+      if (!sep_) {
+        const std::string* ct = head_.get("content-type");
+        if (ct && ct->find("event-stream") != std::string::npos) sep_ = 's';
+        else if (ct && ct->find("ndjson") != std::string::npos) sep_ = 'l';
+        else sep_ = 'n';
+      }
     }
+    uint64_t now = Reactor::now_us();
     size_t used = body_.feed(reinterpret_cast<const uint8_t*>(buf_.data()), buf_.size(), [&](const uint8_t* d, size_t k) {
-      if (!first_ && k) first_ = Reactor::now_us();
-      res_.body_bytes += k;
+      if (!first_ && k) first_ = now;
+      res_->body_bytes += k;
+      got_ += k;
+      scan_events(d, k, now);
     });
     if (used == SIZE_MAX) {
-      res_.errors++;
+      res_->errors++;
       active_ = false;
       conn_->close();
       return;
     }
     buf_.erase(0, used);
-    if (body_.done()) complete();
+    if (body_.done()) {
+      complete();
+      return;
+    }
+    throttle(now);
+  }
+
+  // Slow client: stop reading once ahead of read_rate, resume when due.
+  void throttle(uint64_t now) {
+    if (!o_.read_rate || !conn_ || conn_->closed()) return;
+    uint64_t due_us = t0_ + got_ * 1000000 / o_.read_rate;
+    if (due_us <= now) return;
+    conn_->pause_reading();
+    std::weak_ptr<Stream> w = shared_from_this();
+    r_.call_at(due_us, [w] {
+      if (auto s = w.lock())
+        if (s->conn_ && !s->conn_->closed()) s->conn_->resume_reading();
+    });
   }
 
   void on_close() {
@@ -126,7 +199,7 @@ class Stream : public std::enable_shared_from_this<Stream> {
       return;
     }
     if (active_) {
-      res_.errors++;
+      res_->errors++;
       active_ = false;
       finish();
     }
@@ -134,9 +207,10 @@ class Stream : public std::enable_shared_from_this<Stream> {
 
   void complete() {
     active_ = false;
+    got_ = 0;
     uint64_t now = Reactor::now_us();
-    res_.ttft_us.push_back(double((first_ ? first_ : now) - t0_));
-    res_.total_us.push_back(double(now - t0_));
+    res_->ttft_us.push_back(double((first_ ? first_ : now) - t0_));
+    res_->total_us.push_back(double(now - t0_));
     if (!keep_ && conn_) {
       conn_->on_close(nullptr);
       conn_->close();
@@ -154,19 +228,69 @@ class Stream : public std::enable_shared_from_this<Stream> {
 
   Reactor& r_;
   const Opts& o_;
-  Result& res_;
+  Target t_;
+  Result* res_;
   std::shared_ptr<TcpConn> conn_;
   std::string buf_;
   http::Head head_;
   http::BodyDecoder body_;
   bool head_done_ = false, keep_ = false, active_ = false;
-  uint64_t t0_ = 0, first_ = 0;
+  uint64_t t0_ = 0, first_ = 0, last_ev_ = 0, got_ = 0;
+  char sep_ = 0;
+  int sep_run_ = 0;
 };
 
-double pct(std::vector<double> v, double q) {
+// One reactor thread driving streams [first, first + count).
+void run_thread(const Opts& o, int first, int count, Result& res, Result& warm_res) {
+  Reactor r;
+  int total_steps = o.warmup + o.steps;
+  int step = 0, pending = 0;
+  std::vector<std::shared_ptr<Stream>> live, warmers;
+  for (int i = first; i < first + count; i++) {
+    const Target& t = o.targets[size_t(i) % o.targets.size()];
+    live.push_back(std::make_shared<Stream>(r, o, t, &res));
+    warmers.push_back(std::make_shared<Stream>(r, o, t, &warm_res));
+  }
+  // Warmup steps run on their own connections (results discarded); the timed
+  // steps reuse one keep-alive connection per stream when the server allows.
+  // --warm-conns 1 warms up on the timed connections instead, so connection
+  // setup stays out of the timed steps (steady-state keep-alive serving).
+  if (o.warm_conns)
+    for (auto& s : live) s->set_result(&warm_res);
+  std::function<void()> launch = [&] {
+    auto& set = step < o.warmup && !o.warm_conns ? warmers : live;
+    if (step == o.warmup) {
+      res.t_start = Reactor::now_us();
+      if (o.warm_conns)
+        for (auto& s : live) s->set_result(&res);
+    }
+    pending = count;
+    for (auto& s : set) s->request();
+  };
+  for (auto* set : {&warmers, &live})
+    for (auto& s : *set)
+      s->on_done = [&] {
+        if (--pending == 0) {
+          if (step >= o.warmup) res.step_end.push_back(Reactor::now_us());
+          step++;
+          if (step >= total_steps) {
+            res.t_end = Reactor::now_us();
+            r.stop();
+            return;
+          }
+          launch();
+        }
+      };
+  if (o.warmup == 0) res.t_start = Reactor::now_us();
+  if (count == 0) return;
+  launch();
+  r.run();
+}
+
+double pct(std::vector<double>& v, double q) {
   if (v.empty()) return 0;
-  std::sort(v.begin(), v.end());
   size_t k = size_t(q / 100.0 * double(v.size() - 1) + 0.5);
+  std::nth_element(v.begin(), v.begin() + long(std::min(k, v.size() - 1)), v.end());
   return v[std::min(k, v.size() - 1)];
 }
 
@@ -174,85 +298,86 @@ double pct(std::vector<double> v, double q) {
 
 int main(int argc, char** argv) {
   Opts o;
-  int warmup = 1;
-  bool warm_conns = false;  // --warm-conns 1: warmup on the timed steps' own connections
   for (int i = 1; i + 1 < argc; i += 2) {
     std::string a = argv[i], v = argv[i + 1];
     if (a == "--target") {
-      size_t c = v.rfind(':');
-      o.host = v.substr(0, c);
-      o.port = uint16_t(atoi(v.c_str() + c + 1));
+      o.targets.clear();
+      for (size_t s = 0; s <= v.size();) {
+        size_t e = v.find(',', s);
+        if (e == std::string::npos) e = v.size();
+        std::string hp = v.substr(s, e - s);
+        s = e + 1;
+        if (hp.empty()) continue;
+        size_t c = hp.rfind(':');
+        Target t;
+        t.host = hp.substr(0, c);
+        t.port = uint16_t(atoi(hp.c_str() + c + 1));
+        o.targets.push_back(t);
+      }
+      if (o.targets.empty()) o.targets.push_back(Target{});
     } else if (a == "--streams") o.streams = atoi(v.c_str());
     else if (a == "--steps") o.steps = atoi(v.c_str());
-    else if (a == "--warmup") warmup = atoi(v.c_str());
+    else if (a == "--warmup") o.warmup = atoi(v.c_str());
+    else if (a == "--threads") o.threads = std::max(1, atoi(v.c_str()));
+    else if (a == "--method") o.method = v;
     else if (a == "--path") {
       o.path = v;
       if (v == "/api/generate") o.body = R"({"model": "test-model", "prompt": "hi", "stream": true})";
     } else if (a == "--body") o.body = v;
     else if (a == "--post-bytes") o.post_bytes = size_t(strtoull(v.c_str(), nullptr, 10));
-    else if (a == "--warm-conns") warm_conns = v == "1";
+    else if (a == "--warm-conns") o.warm_conns = v == "1";
+    else if (a == "--events") o.event_sep = v == "sse" ? 's' : v == "ndjson" ? 'l' : v == "none" ? 'n' : 0;
+    else if (a == "--read-rate") o.read_rate = strtoull(v.c_str(), nullptr, 10);
   }
   signal(SIGPIPE, SIG_IGN);
-  Reactor r;
-  Result warm_res, res;
-  int total_steps = warmup + o.steps;
-  int step = 0, pending = 0;
-  uint64_t t_start = 0, t_end = 0;
-  std::function<void()> launch;
-  // Warmup steps run on their own connections (results discarded); the timed
-  // steps reuse one keep-alive connection per stream when the server allows.
-  // --warm-conns 1 warms up on the timed connections instead, so connection
-  // setup stays out of the timed steps (steady-state keep-alive serving).
-  std::vector<std::shared_ptr<Stream>> live, warmers;
-  for (int i = 0; i < o.streams; i++) {
-    live.push_back(std::make_shared<Stream>(r, o, res));
-    warmers.push_back(std::make_shared<Stream>(r, o, warm_res));
+  int T = std::min(o.threads, std::max(1, o.streams));
+  std::vector<Result> res(static_cast<size_t>(T)), warm(static_cast<size_t>(T));
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; t++) {
+    int first = o.streams * t / T, last = o.streams * (t + 1) / T;
+    th.emplace_back(run_thread, std::cref(o), first, last - first, std::ref(res[size_t(t)]), std::ref(warm[size_t(t)]));
   }
-  std::vector<uint64_t> step_end;  // timed steps' completion times (per-step durations in the output)
-  launch = [&] {
-    auto& set = step < warmup && !warm_conns ? warmers : live;
-    if (step == warmup) {
-      t_start = Reactor::now_us();
-      if (warm_conns) {  // drop what the warmup recorded on the live streams
-        warm_res.errors += res.errors;
-        res = Result{};
-      }
-    }
-    pending = o.streams;
-    for (auto& s : set) s->request();
-  };
-  for (auto* set : {&warmers, &live})
-    for (auto& s : *set)
-      s->on_done = [&] {
-        if (--pending == 0) {
-          if (step >= warmup) step_end.push_back(Reactor::now_us());
-          step++;
-          if (step >= total_steps) {
-            t_end = Reactor::now_us();
-            r.stop();
-            return;
-          }
-          launch();
-        }
-      };
-  if (warmup == 0) t_start = Reactor::now_us();
-  launch();
-  r.run();
-  double secs = double(t_end - t_start) / 1e6;
+  for (auto& x : th) x.join();
+  Result all;
+  int warm_errors = 0;
+  all.t_start = UINT64_MAX;
+  for (int t = 0; t < T; t++) {
+    auto& r = res[size_t(t)];
+    all.ttft_us.insert(all.ttft_us.end(), r.ttft_us.begin(), r.ttft_us.end());
+    all.total_us.insert(all.total_us.end(), r.total_us.begin(), r.total_us.end());
+    all.itl_us.insert(all.itl_us.end(), r.itl_us.begin(), r.itl_us.end());
+    all.errors += r.errors;
+    all.body_bytes += r.body_bytes;
+    all.events += r.events;
+    warm_errors += warm[size_t(t)].errors;
+    if (r.t_start && r.t_start < all.t_start) all.t_start = r.t_start;
+    all.t_end = std::max(all.t_end, r.t_end);
+  }
+  if (all.t_start == UINT64_MAX) all.t_start = all.t_end;
+  double secs = double(all.t_end - all.t_start) / 1e6;
+  // Per-step durations (thread 0's steps; every thread runs the same count).
   std::string steps_ms;
-  for (size_t i = 0; i < step_end.size(); i++) {
+  auto& se = res[0].step_end;
+  for (size_t i = 0; i < se.size(); i++) {
     char b[32];
-    snprintf(b, sizeof b, "%s%.3f", i ? ", " : "", double(step_end[i] - (i ? step_end[i - 1] : t_start)) / 1e3);
+    snprintf(b, sizeof b, "%s%.3f", i ? ", " : "", double(se[i] - (i ? se[i - 1] : res[0].t_start)) / 1e3);
     steps_ms += b;
   }
-  printf("{\"streams\": %d, \"steps\": %d, \"requests\": %zu, \"errors\": %d, \"seconds\": %.6f, \"req_s\": %.4f, "
-         "\"p50_ttft_ms\": %.4f, \"p90_ttft_ms\": %.4f, \"p99_ttft_ms\": %.4f, \"mean_ttft_ms\": %.4f, "
-         "\"p50_total_ms\": %.4f, \"body_bytes\": %llu, \"MBps\": %.2f, \"step_ms\": [%s]}\n",
-         o.streams, o.steps, res.ttft_us.size(), res.errors + warm_res.errors, secs,
-         secs > 0 ? double(res.ttft_us.size()) / secs : 0.0, pct(res.ttft_us, 50) / 1e3, pct(res.ttft_us, 90) / 1e3,
-         pct(res.ttft_us, 99) / 1e3,
-         res.ttft_us.empty() ? 0.0 : [&] { double s = 0; for (double x : res.ttft_us) s += x; return s / double(res.ttft_us.size()) / 1e3; }(),
-         pct(res.total_us, 50) / 1e3, static_cast<unsigned long long>(res.body_bytes),
-         secs > 0 ? double(res.body_bytes) / secs / 1e6 : 0.0, steps_ms.c_str());
-  return res.errors ? 1 : 0;
+  double mean = 0;
+  for (double x : all.ttft_us) mean += x;
+  if (!all.ttft_us.empty()) mean /= double(all.ttft_us.size());
+  double itl_max = all.itl_us.empty() ? 0 : *std::max_element(all.itl_us.begin(), all.itl_us.end());
+  printf("{\"streams\": %d, \"steps\": %d, \"threads\": %d, \"requests\": %zu, \"errors\": %d, \"seconds\": %.6f, "
+         "\"req_s\": %.4f, \"p50_ttft_ms\": %.4f, \"p90_ttft_ms\": %.4f, \"p99_ttft_ms\": %.4f, \"mean_ttft_ms\": %.4f, "
+         "\"p50_total_ms\": %.4f, \"body_bytes\": %llu, \"MBps\": %.2f, \"events\": %llu, \"events_s\": %.1f, "
+         "\"p50_itl_ms\": %.4f, \"p90_itl_ms\": %.4f, \"p99_itl_ms\": %.4f, \"p999_itl_ms\": %.4f, \"max_itl_ms\": %.4f, "
+         "\"step_ms\": [%s]}\n",
+         o.streams, o.steps, T, all.ttft_us.size(), all.errors + warm_errors, secs,
+         secs > 0 ? double(all.ttft_us.size()) / secs : 0.0, pct(all.ttft_us, 50) / 1e3, pct(all.ttft_us, 90) / 1e3,
+         pct(all.ttft_us, 99) / 1e3, mean / 1e3, pct(all.total_us, 50) / 1e3,
+         static_cast<unsigned long long>(all.body_bytes), secs > 0 ? double(all.body_bytes) / secs / 1e6 : 0.0,
+         static_cast<unsigned long long>(all.events), secs > 0 ? double(all.events) / secs : 0.0,
+         pct(all.itl_us, 50) / 1e3, pct(all.itl_us, 90) / 1e3, pct(all.itl_us, 99) / 1e3, pct(all.itl_us, 99.9) / 1e3,
+         itl_max / 1e3, steps_ms.c_str());
+  return all.errors + warm_errors ? 1 : 0;
 }

@@ -14,6 +14,8 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "core/net.h"
 #include "core/reactor.h"
@@ -43,7 +45,7 @@ std::string ollama_line(const char* tok) {
 
 struct Server {
   Reactor& r;
-  uint64_t interval_ms;
+  uint64_t interval_us;
   int tokens;
   bool trace;
   std::map<TcpConn*, std::shared_ptr<TcpConn>> conns;
@@ -64,7 +66,7 @@ struct Server {
     auto step = std::make_shared<std::function<void(int)>>();
     std::weak_ptr<TcpConn> w = c;
     Reactor* rp = &r;
-    uint64_t iv = interval_ms;
+    uint64_t iv = interval_us;
     int n = tokens;
     // The pending timer owns the step; the step refers to itself weakly.
     std::weak_ptr<std::function<void(int)>> ws = step;
@@ -74,7 +76,7 @@ struct Server {
       if (i < n) {
         const char* tok = i < 5 ? kTokens[i] : " tok";
         conn->write(ollama ? ollama_line(tok) : chunk_event(tok));
-        if (auto s = ws.lock()) rp->call_later_ms(iv, [s, i] { (*s)(i + 1); });
+        if (auto s = ws.lock()) rp->call_later_us(iv, [s, i] { (*s)(i + 1); });
         return;
       }
       conn->write(ollama ? ollama_line(nullptr) : chunk_event(nullptr) + "data: [DONE]\n\n");
@@ -147,20 +149,42 @@ struct Server {
 
 int main(int argc, char** argv) {
   std::string listen = "127.0.0.1:3001";
-  uint64_t interval = 100;
+  uint64_t interval_us = 100000;
   int tokens = 5;
+  int threads = 1;
   for (int i = 1; i + 1 < argc; i += 2) {
     std::string a = argv[i];
     if (a == "--listen") listen = argv[i + 1];
     else if (a == "--port") listen = "127.0.0.1:" + std::string(argv[i + 1]);
-    else if (a == "--interval-ms") interval = strtoull(argv[i + 1], nullptr, 10);
+    else if (a == "--interval-ms") interval_us = strtoull(argv[i + 1], nullptr, 10) * 1000;
+    else if (a == "--interval-us") interval_us = strtoull(argv[i + 1], nullptr, 10);
     else if (a == "--tokens") tokens = atoi(argv[i + 1]);
+    else if (a == "--threads") threads = std::max(1, atoi(argv[i + 1]));
   }
   signal(SIGPIPE, SIG_IGN);
-  Reactor r;
-  Server s{r, interval, tokens, getenv("MOCK_TRACE") != nullptr, {}};
+  // Accepts on one listener; with --threads N, accepted sockets are handed
+  // round-robin to N reactor threads (a node-scale upstream that is not itself
+  // the bottleneck of a many-stream benchmark).
+  std::vector<std::unique_ptr<Reactor>> rs;
+  std::vector<std::unique_ptr<Server>> servers;
+  for (int t = 0; t < threads; t++) {
+    rs.push_back(std::make_unique<Reactor>());
+    servers.push_back(std::make_unique<Server>(Server{*rs.back(), interval_us, tokens, getenv("MOCK_TRACE") != nullptr, {}}));
+  }
+  Reactor& r = *rs[0];
   std::string err;
-  auto l = TcpListener::bind(r, listen, [&](int fd, SockAddr) { s.accept(fd); }, &err);
+  size_t next = 0;
+  auto l = TcpListener::bind(
+      r, listen,
+      [&](int fd, SockAddr) {
+        size_t k = next++ % servers.size();
+        if (k == 0) servers[0]->accept(fd);
+        else {
+          Server* sv = servers[k].get();
+          rs[k]->post_threadsafe([sv, fd] { sv->accept(fd); });
+        }
+      },
+      &err);
   if (!l) {
     fprintf(stderr, "mock: %s\n", err.c_str());
     return 1;
@@ -169,6 +193,10 @@ int main(int argc, char** argv) {
   fflush(stdout);
   r.on_signal(SIGINT, [&] { r.stop(); });
   r.on_signal(SIGTERM, [&] { r.stop(); });
+  std::vector<std::thread> th;
+  for (int t = 1; t < threads; t++) th.emplace_back([&rs, t] { rs[size_t(t)]->run(); });
   r.run();
+  for (int t = 1; t < threads; t++) rs[size_t(t)]->post_threadsafe([&rs, t] { rs[size_t(t)]->stop(); });
+  for (auto& x : th) x.join();
   return 0;
 }

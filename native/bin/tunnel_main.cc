@@ -84,6 +84,10 @@ const std::vector<Opt>& ext_opts() {
       {"metrics-listen", "TUNNEL_METRICS_LISTEN", "", "Serve Prometheus metrics on HOST:PORT"},
       {"busy-poll-us", "TUNNEL_BUSY_POLL_US", "0",
        "Keep polling for N us after I/O instead of sleeping (lower per-hop latency, more CPU)"},
+      {"workers", "TUNNEL_WORKERS", "auto",
+       "HTTP worker threads beside the association thread (auto: one per spare CPU, max 8; 0: single thread)"},
+      {"inline-streams", "TUNNEL_INLINE_STREAMS", "16",
+       "Concurrent streams handled on the association thread before new ones go to workers"},
       {"upstream-prewarm", "TUNNEL_UPSTREAM_PREWARM", "4",
        "serve: spare pre-connected upstream sockets (follows peak concurrency; 0=off)"},
       {"upstream-prewarm-ttl-ms", "TUNNEL_UPSTREAM_PREWARM_TTL_MS", "1000",
@@ -315,6 +319,8 @@ int main(int argc, char** argv) {
   cfg.upstream_prewarm = num(m, "upstream-prewarm");
   cfg.upstream_prewarm_ttl_ms = num(m, "upstream-prewarm-ttl-ms");
   cfg.busy_poll_us = num(m, "busy-poll-us");
+  cfg.workers = m["workers"] == "auto" ? -1 : int(num(m, "workers"));
+  cfg.inline_streams = num(m, "inline-streams");
   cfg.secret = m["secret"];
   if (!m["cpu-affinity"].empty()) {
     std::string err;

@@ -5,6 +5,7 @@
 // into a shared, immutable allocation: slicing never copies.
 #pragma once
 
+#include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <memory>
@@ -77,6 +78,67 @@ struct RawBuf {
   size_t cap;
 };
 using RawBufPtr = std::shared_ptr<RawBuf>;
+// Call after seeing use_count() == 1 and before writing into the buffer again:
+// views may live on worker threads (tunnel/workers.h), and use_count() is a
+// relaxed load, so this orders the reuse after their last reads.
+inline void reuse_fence() { std::atomic_thread_fence(std::memory_order_acquire); }
+
+// Recycling pool of fixed-size receive buffers whose contents are handed up
+// the stack as zero-copy views (datagram receive: DTLS decrypts in place and
+// SCTP messages are views of the datagram). A buffer goes back into service
+// once no view of it is alive (use_count() == 1: only the pool holds it),
+// wherever the last view was dropped — on a worker thread, typically. Without
+// it every receive slot whose previous datagram is still being written to a
+// client would need a fresh 64 KiB allocation (and a cross-thread free later).
+class BufPool {
+ public:
+  explicit BufPool(size_t buf_size, size_t max_keep = 512) : size_(buf_size), max_keep_(max_keep) {}
+  RawBufPtr get() {
+    size_t n = bufs_.size();
+    for (size_t k = 0; k < n && k < 128; k++) {
+      size_t i = next_ + k < n ? next_ + k : next_ + k - n;
+      if (bufs_[i].use_count() == 1) {
+        reuse_fence();
+        next_ = i + 1 < n ? i + 1 : 0;
+        return bufs_[i];
+      }
+    }
+    auto b = std::make_shared<RawBuf>(size_);
+    if (n < max_keep_) bufs_.push_back(b);
+    return b;
+  }
+  size_t size() const { return bufs_.size(); }
+
+ private:
+  size_t size_, max_keep_;
+  std::vector<RawBufPtr> bufs_;
+  size_t next_ = 0;
+};
+
+// Copies of small byte ranges (SSE tokens read from an upstream socket, chunk
+// headers) packed into per-thread 64 KiB blocks instead of one heap
+// allocation each: the block is shared by the views and recycled once they
+// are all gone. Frames cross threads (tunnel/workers.h), so per-piece mallocs
+// would be freed on another thread's arena — the contention this avoids.
+inline Bytes slab_copy(const void* p, size_t n) {
+  constexpr size_t kBlock = 64 * 1024, kMax = 2048;
+  if (n == 0 || n > kMax) return Bytes::copy(p, n);
+  struct Slab {
+    BufPool pool{kBlock, 64};
+    RawBufPtr cur;
+    size_t off = kBlock;
+  };
+  thread_local Slab s;
+  if (s.off + n > kBlock) {
+    s.cur.reset();  // a block in use stays alive through its views, then returns to the pool
+    s.cur = s.pool.get();
+    s.off = 0;
+  }
+  uint8_t* d = s.cur->data.get() + s.off;
+  memcpy(d, p, n);
+  s.off += (n + 15) & ~size_t(15);
+  return Bytes::adopt(s.cur, d, n);
+}
 
 // Append-only big-endian writer over a std::vector.
 class ByteWriter {

@@ -273,7 +273,7 @@ Bytes TcpConn::rx_view(const uint8_t* p, size_t n) const {
   constexpr size_t kMinView = 2048;  // smaller pieces are copied: never pin 64 KiB for a token
   if (rx_ && n >= kMinView && p >= rx_->data.get() && p + n <= rx_->data.get() + rx_->cap)
     return Bytes::adopt(rx_, p, n);
-  return Bytes::copy(p, n);
+  return slab_copy(p, n);
 }
 
 void TcpConn::do_read() {
@@ -281,6 +281,7 @@ void TcpConn::do_read() {
   // Bounded number of reads per wakeup keeps the loop fair across sockets.
   for (int iter = 0; iter < 16 && fd_ >= 0 && !paused_; iter++) {
     if (!rx_ || rx_.use_count() > 1) rx_ = std::make_shared<RawBuf>(kRx);
+    else reuse_fence();  // the last view may have been dropped on another thread
     uint8_t* buf = rx_->data.get();
     ssize_t n;
     if (ssl_) {

@@ -23,6 +23,7 @@ constexpr size_t kSlots = 1 << 15;  // distinct stacks kept
 
 struct Slot {
   std::atomic<uint64_t> hash{0};
+  uint64_t tag;
   uint64_t pcs[kDepth];
   std::atomic<uint64_t> count{0};
 };
@@ -30,10 +31,13 @@ struct Slot {
 Slot* g_slots = nullptr;
 std::atomic<uint64_t> g_samples{0}, g_dropped{0};
 std::string g_path;
-uintptr_t g_stack_lo = 0, g_stack_hi = 0;
+// Stack bounds of the interrupted thread (the process timer samples whichever
+// thread is running: the main reactor or a worker, see register_thread()).
+thread_local uintptr_t t_stack_lo = 0, t_stack_hi = 0;
+thread_local uint64_t t_tag = 0;  // 0 = main reactor thread, k = worker k
 std::atomic<bool> g_dumped{false};
 
-inline bool on_stack(uintptr_t p) { return p >= g_stack_lo && p + 16 <= g_stack_hi && (p & 7) == 0; }
+inline bool on_stack(uintptr_t p) { return p >= t_stack_lo && p + 16 <= t_stack_hi && (p & 7) == 0; }
 
 void on_sigprof(int, siginfo_t*, void* uc_) {
   auto* uc = static_cast<ucontext_t*>(uc_);
@@ -59,6 +63,7 @@ void on_sigprof(int, siginfo_t*, void* uc_) {
 #endif
   uint64_t h = 1469598103934665603ull;
   for (int i = 0; i < kDepth; i++) h = (h ^ pcs[i]) * 1099511628211ull;
+  h = (h ^ t_tag) * 1099511628211ull;
   if (h == 0) h = 1;
   g_samples.fetch_add(1, std::memory_order_relaxed);
   for (size_t probe = 0; probe < 64; probe++) {
@@ -69,8 +74,15 @@ void on_sigprof(int, siginfo_t*, void* uc_) {
       return;
     }
     if (cur == 0) {
+      // Claim the slot (several threads may be sampled at once); a loser
+      // re-reads it and either matches or probes on.
+      if (!s.hash.compare_exchange_strong(cur, h, std::memory_order_acq_rel)) {
+        if (cur == h) s.count.fetch_add(1, std::memory_order_relaxed);
+        else continue;
+        return;
+      }
       memcpy(s.pcs, pcs, sizeof pcs);
-      s.hash.store(h, std::memory_order_release);  // single sampled thread: no CAS race
+      s.tag = t_tag;
       s.count.fetch_add(1, std::memory_order_relaxed);
       return;
     }
@@ -91,6 +103,19 @@ void resolve(FILE* f, uint64_t a) {
 
 }  // namespace
 
+void register_thread(int tag) {
+  t_tag = uint64_t(tag);
+  pthread_attr_t attr;
+  if (pthread_getattr_np(pthread_self(), &attr) == 0) {
+    void* lo = nullptr;
+    size_t sz = 0;
+    pthread_attr_getstack(&attr, &lo, &sz);
+    t_stack_lo = reinterpret_cast<uintptr_t>(lo);
+    t_stack_hi = t_stack_lo + sz;
+    pthread_attr_destroy(&attr);
+  }
+}
+
 bool start_from_env() {
   const char* p = getenv("TUNNEL_PROFILE");
   if (!p || !*p) return false;
@@ -99,15 +124,7 @@ bool start_from_env() {
   int hz = 2000;
   if (const char* h = getenv("TUNNEL_PROFILE_HZ")) hz = std::max(10, atoi(h));
   g_slots = new Slot[kSlots];
-  pthread_attr_t attr;
-  if (pthread_getattr_np(pthread_self(), &attr) == 0) {
-    void* lo = nullptr;
-    size_t sz = 0;
-    pthread_attr_getstack(&attr, &lo, &sz);
-    g_stack_lo = reinterpret_cast<uintptr_t>(lo);
-    g_stack_hi = g_stack_lo + sz;
-    pthread_attr_destroy(&attr);
-  }
+  register_thread(0);
   // Resolve dladdr's lazy state before the first signal.
   Dl_info di;
   dladdr(reinterpret_cast<void*>(&start_from_env), &di);
@@ -135,7 +152,7 @@ void dump() {
   for (size_t i = 0; i < kSlots; i++) {
     Slot& s = g_slots[i];
     if (!s.hash.load()) continue;
-    fprintf(f, "%llu", static_cast<unsigned long long>(s.count.load()));
+    fprintf(f, "%llu T%llu", static_cast<unsigned long long>(s.count.load()), static_cast<unsigned long long>(s.tag));
     for (int k = 0; k < kDepth && (k < 2 || s.pcs[k]); k++) resolve(f, s.pcs[k]);
     fputc('\n', f);
   }

@@ -2,7 +2,7 @@
 // reference has no profiler hooks at all; this container has no `perf`).
 //
 // TUNNEL_PROFILE=<path> ("%p" = pid) arms ITIMER_PROF at TUNNEL_PROFILE_HZ (default 2000)
-// on the reactor thread. The SIGPROF handler records the interrupted PC, the
+// (process CPU time: whichever thread runs gets sampled). The SIGPROF handler records the interrupted PC, the
 // word at the stack pointer (the return address when a frameless leaf such as
 // memcpy or an AES routine was interrupted) and up to kDepth frame-pointer
 // links (our code is built with -fno-omit-frame-pointer), into a fixed,
@@ -18,5 +18,9 @@ namespace p2pt::profiler {
 bool start_from_env();
 // Writes the report now (also registered with atexit).
 void dump();
+// Records the calling thread's stack bounds so its samples get a frame-
+// pointer walk (worker threads call this when they start).
+// `tag` labels the thread's samples in the dump ("T<tag>"; 0 = main).
+void register_thread(int tag);
 
 }  // namespace p2pt::profiler

@@ -94,10 +94,16 @@ void Reactor::cancel(TimerId id) {
 void Reactor::post(Fn fn) { posted_.push_back(std::move(fn)); }
 
 void Reactor::post_threadsafe(Fn fn) {
+  bool wake;
   {
     std::lock_guard<std::mutex> lk(ts_mu_);
+    // The loop drains the eventfd before it takes the whole queue, so only the
+    // push into an empty queue needs to wake it: posts that land while a batch
+    // is still waiting ride along without a syscall.
+    wake = ts_posted_.empty();
     ts_posted_.push_back(std::move(fn));
   }
+  if (!wake) return;
   uint64_t one = 1;
   ssize_t r = write(evfd_, &one, sizeof one);
   (void)r;
@@ -189,8 +195,8 @@ void Reactor::run_once(int timeout_ms) {
     uint64_t tag = evs[i].data.u64;
     if (tag == kWakeTag) {
       uint64_t v;
-      while (read(evfd_, &v, sizeof v) > 0) {
-      }
+      ssize_t rd = read(evfd_, &v, sizeof v);  // one read resets the counter
+      (void)rd;
       std::vector<Fn> fns;
       {
         std::lock_guard<std::mutex> lk(ts_mu_);

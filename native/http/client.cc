@@ -349,7 +349,7 @@ ClientCall::~ClientCall() {
 namespace {
 // Calls keep themselves alive until finished (fire-and-forget semantics like tokio::spawn).
 std::map<ClientCall*, std::shared_ptr<ClientCall>>& live_calls() {
-  static std::map<ClientCall*, std::shared_ptr<ClientCall>> m;
+  thread_local std::map<ClientCall*, std::shared_ptr<ClientCall>> m;  // per reactor thread
   return m;
 }
 }  // namespace

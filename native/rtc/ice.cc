@@ -616,10 +616,12 @@ void IceAgent::on_readable(int si) {
   iovec iovs[kBatch];
   sockaddr_storage from[kBatch];
   for (int round = 0; round < 8 && !closed_; round++) {
+    for (int i = 0; i < kBatch; i++) rxpool_[i].reset();
     for (int i = 0; i < kBatch; i++) {
-      // A slot whose previous datagram is still referenced (zero-copy views
-      // handed up the stack) gets a fresh buffer.
-      if (!rxpool_[i] || rxpool_[i].use_count() > 1) rxpool_[i] = std::make_shared<RawBuf>(65536);
+      // Buffers whose datagrams are still referenced (zero-copy views handed
+      // up the stack, possibly to worker threads) stay out of the pool's
+      // rotation until the views are gone.
+      rxpool_[i] = rxbufs_.get();
       memset(&msgs[i], 0, sizeof msgs[i]);
       iovs[i].iov_base = rxpool_[i]->data.get();
       iovs[i].iov_len = 65536;
@@ -690,7 +692,8 @@ void IceAgent::on_nat_readable(int pi) {
   if (closed_) return;
   auto self = shared_from_this();
   for (int round = 0; round < 64 && !closed_; round++) {
-    if (!rxpool_[0] || rxpool_[0].use_count() > 1) rxpool_[0] = std::make_shared<RawBuf>(65536);
+    rxpool_[0].reset();
+    rxpool_[0] = rxbufs_.get();
     SockAddr a;
     a.len = sizeof a.ss;
     ssize_t n = recvfrom(nat_ports_[pi].fd, rxpool_[0]->data.get(), 65536, MSG_DONTWAIT, a.sa(), &a.len);

@@ -253,7 +253,8 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   std::vector<DgVec> spare_;        // recycled datagram buffers
   size_t coalesce_limit_ = 0;
   size_t append_at_ = 0;
-  std::vector<RawBufPtr> rxpool_;   // recvmmsg slots; replaced while views into them live
+  std::vector<RawBufPtr> rxpool_;   // recvmmsg slots, filled from rxbufs_ each round
+  BufPool rxbufs_{65536};
   DgVec drop_;                      // reserve_append target with no path
   friend class TurnClient;
 };

@@ -29,11 +29,7 @@ const char* pc_state_name(PcState s) {
 bool DataChannel::send(const uint8_t* hdr, size_t hlen, const Bytes& payload) {
   auto pc = pc_.lock();
   if (!pc || !is_open() || !pc->sctp_) return false;
-  std::vector<Bytes> pieces;
-  pieces.reserve(2);
-  pieces.push_back(Bytes::copy(hdr, hlen));
-  if (!payload.empty()) pieces.push_back(payload);
-  bool ok = pc->sctp_->send(uint16_t(stream_), kPpidBinary, pieces);
+  bool ok = pc->sctp_->send_framed(uint16_t(stream_), kPpidBinary, hdr, hlen, payload);
   if (ok && buffered_amount() > buffered_low_threshold) above_low_ = true;
   return ok;
 }

@@ -51,12 +51,18 @@ void pad4(std::vector<uint8_t>& v) {
 }
 }  // namespace
 
+// An outbound DATA fragment: a few inline bytes (the tunnel frame header)
+// followed by up to two zero-copy payload slices. Pooled (chunk_free_): a
+// frame in flight costs no heap allocation on the association thread.
 struct SctpAssociation::Chunk {
   uint32_t tsn;
   uint16_t stream, ssn;
   uint32_t ppid;
   uint8_t flags;  // B=2, E=1, U=4
-  std::vector<Bytes> data;
+  uint8_t ilen = 0;
+  uint8_t np = 0;
+  uint8_t inl[SctpAssociation::kMsgHdrMax];
+  Bytes piece[2];
   size_t len;
   uint64_t sent_us = 0;
   int tx = 0;
@@ -105,7 +111,26 @@ SctpAssociation::~SctpAssociation() {
   if (t3_timer_) r_.cancel(t3_timer_);
   if (init_timer_) r_.cancel(init_timer_);
   for (auto* c : inflight_) delete c;
+  for (auto* c : chunk_free_) delete c;
   for (auto& kv : ooo_) delete kv.second;
+}
+
+SctpAssociation::Chunk* SctpAssociation::new_chunk() {
+  if (chunk_free_.empty()) return new Chunk();
+  Chunk* c = chunk_free_.back();
+  chunk_free_.pop_back();
+  return c;
+}
+
+void SctpAssociation::free_chunk(Chunk* c) {
+  c->piece[0] = Bytes();
+  c->piece[1] = Bytes();
+  if (chunk_free_.size() >= 8192) {
+    delete c;
+    return;
+  }
+  *c = Chunk();
+  chunk_free_.push_back(c);
 }
 
 void SctpAssociation::set_mtu(size_t mtu) {
@@ -516,7 +541,7 @@ void SctpAssociation::handle_data(uint8_t flags, const uint8_t* c, size_t len, c
   auto hold = [&pkt](const uint8_t* dp, size_t dn) {
     if (dn >= kZeroCopyMin && dp >= pkt.data() && dp + dn <= pkt.data() + pkt.size())
       return pkt.slice(size_t(dp - pkt.data()), dn);
-    return Bytes::copy(dp, dn);
+    return slab_copy(dp, dn);  // packed with other small messages (core/buf.h)
   };
   auto deliver_chunk = [this](uint8_t fl, uint16_t st, uint32_t pp, const Bytes& d) {
     bool B = fl & 2, E = fl & 1, U = fl & 4;
@@ -631,7 +656,7 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
       newly_acked += ch->len;
       if (ch->tx == 1) rtt_sample = now - ch->sent_us;
     }
-    delete ch;
+    free_chunk(ch);
   }
   cum_acked_ = cum;
   uint32_t highest_gap = cum;
@@ -784,9 +809,36 @@ bool SctpAssociation::send(uint16_t stream, uint32_t ppid, const std::vector<Byt
   m.stream = stream;
   m.ppid = ppid;
   m.unordered = unordered;
-  m.pieces = pieces;
   m.len = 0;
   for (auto& p : pieces) m.len += p.size();
+  if (m.len == 0) return false;
+  // Generic gather list: one contiguous copy unless it is a single piece.
+  if (pieces.size() == 1) {
+    m.body = pieces[0];
+  } else {
+    std::vector<uint8_t> v;
+    v.reserve(m.len);
+    for (auto& p : pieces) v.insert(v.end(), p.begin(), p.end());
+    m.body = Bytes::take(std::move(v));
+  }
+  m.ssn = unordered ? 0 : next_ssn_[stream]++;
+  unsent_bytes_ += m.len;
+  sendq_.push_back(std::move(m));
+  return true;
+}
+
+bool SctpAssociation::send_framed(uint16_t stream, uint32_t ppid, const uint8_t* hdr, size_t hlen, const Bytes& payload,
+                                  bool unordered) {
+  if (closed_fired_ || state_ == State::ShutdownPending || state_ == State::ShutdownSent) return false;
+  if (hlen > kMsgHdrMax) return send(stream, ppid, {Bytes::copy(hdr, hlen), payload}, unordered);
+  Msg m;
+  m.stream = stream;
+  m.ppid = ppid;
+  m.unordered = unordered;
+  memcpy(m.hdr, hdr, hlen);
+  m.hlen = uint8_t(hlen);
+  m.body = payload;
+  m.len = hlen + payload.size();
   if (m.len == 0) return false;
   m.ssn = unordered ? 0 : next_ssn_[stream]++;
   unsent_bytes_ += m.len;
@@ -912,9 +964,12 @@ void SctpAssociation::flush() {
     put16(pkt, ch->stream);
     put16(pkt, ch->ssn);
     put32(pkt, ch->ppid);
-    // Small pieces are copied inline; large ones are referenced in place
-    // (the chunk keeps its slices alive until acknowledged).
-    for (auto& b : ch->data) {
+    // Inline header bytes and small pieces are copied into the packet buffer;
+    // large pieces are referenced in place (the chunk keeps its slices alive
+    // until acknowledged).
+    pkt.insert(pkt.end(), ch->inl, ch->inl + ch->ilen);
+    for (int k = 0; k < ch->np; k++) {
+      const Bytes& b = ch->piece[k];
       if (b.size() < kInlineMax) {
         pkt.insert(pkt.end(), b.begin(), b.end());
       } else {
@@ -962,21 +1017,23 @@ void SctpAssociation::flush() {
     if (flight_size_ > 0 && (flight_size_ + take > cwnd_ || take > peer_rwnd_)) break;
     if (flight_size_ == 0 && peer_rwnd_ == 0 && !inflight_.empty()) break;  // wait for window / T3 probe
     progressed = true;
-    auto* ch = new Chunk();
+    Chunk* ch = new_chunk();
     ch->tsn = next_tsn_++;
     ch->stream = m.stream;
     ch->ssn = m.ssn;
     ch->ppid = m.ppid;
     ch->flags = uint8_t((m.off == 0 ? 2 : 0) | (take == left ? 1 : 0) | (m.unordered ? 4 : 0));
     ch->len = take;
-    // Slice [off, off+take) out of the gathered pieces without copying.
-    size_t pos = 0, want_lo = m.off, want_hi = m.off + take;
-    for (auto& piece : m.pieces) {
-      size_t lo = pos, hi = pos + piece.size();
-      pos = hi;
-      if (hi <= want_lo || lo >= want_hi) continue;
-      size_t a = std::max(lo, want_lo) - lo, b = std::min(hi, want_hi) - lo;
-      ch->data.push_back(piece.slice(a, b - a));
+    // Slice [off, off+take) out of header + body without copying the body.
+    size_t want_lo = m.off, want_hi = m.off + take;
+    if (want_lo < m.hlen) {
+      size_t e = std::min<size_t>(m.hlen, want_hi);
+      memcpy(ch->inl, m.hdr + want_lo, e - want_lo);
+      ch->ilen = uint8_t(e - want_lo);
+    }
+    if (want_hi > m.hlen) {
+      size_t a = want_lo > m.hlen ? want_lo - m.hlen : 0, b = want_hi - m.hlen;
+      ch->piece[ch->np++] = m.body.slice(a, b - a);
     }
     m.off += take;
     unsent_bytes_ -= take;

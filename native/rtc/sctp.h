@@ -86,8 +86,13 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   // never pins a whole receive buffer.
   void on_packet(const Bytes& pkt);
   void on_packet(const uint8_t* p, size_t n) { on_packet(Bytes::copy(p, n)); }
-  // Queue a message made of gathered pieces (no copy until packetisation).
+  // Queue a message made of gathered pieces (a single piece is never copied).
   bool send(uint16_t stream, uint32_t ppid, const std::vector<Bytes>& pieces, bool unordered = false);
+  // Queue a message = a short header (copied, <= kMsgHdrMax bytes) followed by
+  // a payload view (never copied): the tunnel's frame header + body.
+  static constexpr size_t kMsgHdrMax = 16;
+  bool send_framed(uint16_t stream, uint32_t ppid, const uint8_t* hdr, size_t hlen, const Bytes& payload,
+                   bool unordered = false);
   // Build and emit packets (bundled). Called once per reactor batch.
   void flush();
   void shutdown();
@@ -165,10 +170,15 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
     uint32_t ppid;
     bool unordered;
     uint16_t ssn;
-    std::vector<Bytes> pieces;
+    uint8_t hlen = 0;
+    uint8_t hdr[kMsgHdrMax];
+    Bytes body;      // message = hdr[0, hlen) ++ body
     size_t len;
     size_t off = 0;  // bytes already fragmented
   };
+  Chunk* new_chunk();
+  void free_chunk(Chunk* c);
+  std::vector<Chunk*> chunk_free_;
   std::deque<Msg> sendq_;
   std::map<uint16_t, uint16_t> next_ssn_;
   std::deque<Chunk*> inflight_;  // ordered by TSN

@@ -149,6 +149,11 @@ std::shared_ptr<void> connect_transport(Reactor& r, const AppConfig& cfg, Connec
 int run_app(const AppConfig& cfg) {
   Reactor r;
   r.set_busy_poll_us(cfg.busy_poll_us);
+  // Worker threads for per-stream HTTP work (tunnel/workers.h); they outlive
+  // sessions, so reconnects reuse them.
+  WorkerPool pool(cfg.workers);
+  if (pool.size()) LOG_INFO(kT, "%zu worker threads (streams beyond %zu per session spill onto them)", pool.size(),
+                            cfg.inline_streams);
   struct State {
     uint64_t attempt = 0;
     std::shared_ptr<void> transport;
@@ -240,7 +245,8 @@ int run_app(const AppConfig& cfg) {
         sc.upstream_prewarm = cfg.upstream_prewarm;
         sc.upstream_prewarm_ttl_ms = cfg.upstream_prewarm_ttl_ms;
         sc.secret = cfg.secret;
-        st.serve = ServeSession::start(r, ch, sc, [&](const std::string& e) { on_fail(e); });
+        sc.inline_streams = cfg.inline_streams;
+        st.serve = ServeSession::start(r, ch, sc, [&](const std::string& e) { on_fail(e); }, &pool);
       } else {
         LOG_INFO(kT, "WebRTC connected, starting proxy...");
         ProxyConfig pc;
@@ -251,7 +257,8 @@ int run_app(const AppConfig& cfg) {
         pc.pong_timeout_ms = cfg.pong_timeout_ms;
         pc.listen_early = cfg.listen_early;
         pc.secret = cfg.secret;
-        st.proxy = ProxySession::start(r, ch, pc, [&](const std::string& e) { on_fail(e); });
+        pc.inline_streams = cfg.inline_streams;
+        st.proxy = ProxySession::start(r, ch, pc, [&](const std::string& e) { on_fail(e); }, &pool);
         st.early.session = st.proxy;
       }
     });

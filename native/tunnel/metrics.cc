@@ -2,7 +2,9 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <atomic>
 #include <map>
+#include <mutex>
 #include <string_view>
 
 #include "http/http.h"
@@ -10,14 +12,18 @@
 
 namespace p2pt::metrics {
 namespace {
+// Frame counters are bumped on the association thread; named counters and
+// gauges may also come from worker threads (tunnel/workers.h): a mutex guards
+// the maps, relaxed atomics the per-type arrays.
 struct Registry {
+  std::mutex mu;
   std::map<std::string, double> counters;
   std::map<std::string, double> gauges;
   std::map<std::string, std::function<double()>> gauge_fns;
-  uint64_t frames_sent[256] = {};
-  uint64_t bytes_sent[256] = {};
-  uint64_t frames_recv[256] = {};
-  uint64_t bytes_recv[256] = {};
+  std::atomic<uint64_t> frames_sent[256] = {};
+  std::atomic<uint64_t> bytes_sent[256] = {};
+  std::atomic<uint64_t> frames_recv[256] = {};
+  std::atomic<uint64_t> bytes_recv[256] = {};
 };
 Registry& reg() {
   static Registry r;
@@ -31,24 +37,38 @@ std::string type_label(int t) {
 }  // namespace
 
 void frame_sent(uint8_t type, size_t bytes) {
-  reg().frames_sent[type]++;
-  reg().bytes_sent[type] += bytes;
+  reg().frames_sent[type].fetch_add(1, std::memory_order_relaxed);
+  reg().bytes_sent[type].fetch_add(bytes, std::memory_order_relaxed);
 }
 void frame_recv(uint8_t type, size_t bytes) {
-  reg().frames_recv[type]++;
-  reg().bytes_recv[type] += bytes;
+  reg().frames_recv[type].fetch_add(1, std::memory_order_relaxed);
+  reg().bytes_recv[type].fetch_add(bytes, std::memory_order_relaxed);
 }
-void counter_add(const std::string& name, double v) { reg().counters[name] += v; }
-void gauge_set(const std::string& name, double v) { reg().gauges[name] = v; }
-void gauge_fn(const std::string& name, std::function<double()> fn) { reg().gauge_fns[name] = std::move(fn); }
-void gauge_fn_remove(const std::string& name) { reg().gauge_fns.erase(name); }
+void counter_add(const std::string& name, double v) {
+  std::lock_guard<std::mutex> lk(reg().mu);
+  reg().counters[name] += v;
+}
+void gauge_set(const std::string& name, double v) {
+  std::lock_guard<std::mutex> lk(reg().mu);
+  reg().gauges[name] = v;
+}
+void gauge_fn(const std::string& name, std::function<double()> fn) {
+  std::lock_guard<std::mutex> lk(reg().mu);
+  reg().gauge_fns[name] = std::move(fn);
+}
+void gauge_fn_remove(const std::string& name) {
+  std::lock_guard<std::mutex> lk(reg().mu);
+  reg().gauge_fns.erase(name);
+}
 double counter_get(const std::string& name) {
+  std::lock_guard<std::mutex> lk(reg().mu);
   auto it = reg().counters.find(name);
   return it == reg().counters.end() ? 0 : it->second;
 }
 
 std::string render_prometheus() {
   auto& r = reg();
+  std::lock_guard<std::mutex> lk(r.mu);
   std::string out;
   char buf[256];
   auto line = [&](const std::string& name, const std::string& labels, double v) {

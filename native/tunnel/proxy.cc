@@ -13,11 +13,65 @@ namespace p2pt {
 
 static const char* kT = "tunnel::proxy";
 
+// The client connections of one reactor thread (the association thread's own
+// or a worker's): stream registration, frames towards the session, and the
+// RES_* frames the session routes back. Created, used and destroyed on its
+// reactor's thread only.
+class ProxyWorker : public std::enable_shared_from_this<ProxyWorker> {
+ public:
+  ProxyWorker(Reactor& r, Reactor& assoc, std::weak_ptr<ProxySession> sess,
+              std::shared_ptr<ProxySession::Shared> shared, size_t index)
+      : r_(r), assoc_(assoc), sess_(std::move(sess)), shared_(std::move(shared)), index_(index) {}
+  ~ProxyWorker();
+  void init() {
+    std::weak_ptr<ProxySession> w = sess_;
+    size_t k = index_;
+    out_ = std::make_unique<Pipe<ProxySession::Ev>>(r_, assoc_, [w, k](ProxySession::Ev& ev) {
+      if (auto s = w.lock()) s->on_event(k, ev);
+    });
+  }
+  void handle(ProxySession::Cmd& c);
+  // Fails every registered stream (the tunnel went away).
+  void fail_all(const std::string& why);
+
+  // ---- used by ProxyConn
+  uint32_t next_stream_id() { return shared_->next_sid.fetch_add(1, std::memory_order_relaxed); }
+  void register_stream(uint32_t sid, std::weak_ptr<ProxyConn> c) {
+    streams_[sid] = std::move(c);
+    out_->push(ProxySession::Ev{ProxySession::Ev::Route, sid});
+  }
+  void unregister_stream(uint32_t sid) {
+    if (streams_.erase(sid)) out_->push(ProxySession::Ev{ProxySession::Ev::Unroute, sid});
+  }
+  void send(proto::Frame f) {
+    ProxySession::Ev ev(ProxySession::Ev::Frame, f.stream_id);
+    ev.frame = std::move(f);
+    out_->push(std::move(ev));
+  }
+  bool ready() const { return shared_->ready.load(std::memory_order_relaxed); }
+  size_t body_chunk() const { return shared_->body_chunk; }
+  bool cancel_feature() const { return shared_->cancel_feature.load(std::memory_order_relaxed); }
+  const ProxyConfig& config() const { return shared_->cfg; }
+  Reactor& reactor() { return r_; }
+  void conn_closed(ProxyConn* c);
+
+ private:
+  void adopt(int fd);
+  Reactor& r_;
+  Reactor& assoc_;
+  std::weak_ptr<ProxySession> sess_;
+  std::shared_ptr<ProxySession::Shared> shared_;
+  size_t index_;
+  std::unique_ptr<Pipe<ProxySession::Ev>> out_;
+  std::unordered_map<uint32_t, std::weak_ptr<ProxyConn>> streams_;
+  std::unordered_map<ProxyConn*, std::shared_ptr<ProxyConn>> conns_;
+};
+
 // One accepted client connection. Requests on a connection are handled one
 // at a time (HTTP/1.1 keep-alive; pipelined requests wait in the buffer).
 class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
  public:
-  ProxyConn(std::weak_ptr<ProxySession> s, std::shared_ptr<TcpConn> c) : sess_(std::move(s)), conn_(std::move(c)) {}
+  ProxyConn(std::weak_ptr<ProxyWorker> s, std::shared_ptr<TcpConn> c) : sess_(std::move(s)), conn_(std::move(c)) {}
   ~ProxyConn() { cancel_timer(); }
 
   void start() {
@@ -56,9 +110,18 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     if (chunked_) {
       char hdr[24];
       int n = snprintf(hdr, sizeof hdr, "%zx\r\n", payload.size());
-      conn_->write(Bytes::copy(hdr, size_t(n)));
-      conn_->write(payload);  // zero-copy from the received message
-      conn_->write(Bytes::copy("\r\n", 2));
+      if (payload.size() <= 1024) {
+        // A token event: chunk header, data and CRLF as one small slab piece.
+        char ev[1024 + 32];
+        memcpy(ev, hdr, size_t(n));
+        memcpy(ev + n, payload.data(), payload.size());
+        memcpy(ev + n + payload.size(), "\r\n", 2);
+        conn_->write(slab_copy(ev, size_t(n) + payload.size() + 2));
+      } else {
+        conn_->write(slab_copy(hdr, size_t(n)));
+        conn_->write(payload);  // zero-copy from the received message
+        conn_->write(slab_copy("\r\n", 2));
+      }
     } else {
       conn_->write(payload);
     }
@@ -93,7 +156,13 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     conn_->close_after_flush();
   }
 
-  void resume_reading() {
+  // Per-stream back-pressure from the session: this upload's frames pile up.
+  void flow_pause() {
+    flow_paused_ = true;
+    if (conn_ && !conn_->closed()) conn_->pause_reading();
+  }
+  void flow_resume() {
+    flow_paused_ = false;
     if (conn_ && !conn_->closed() && !pipelined_hold_) conn_->resume_reading();
     if (conn_ && !inbuf_.empty()) process();
   }
@@ -234,10 +303,6 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
       finish_request_body();
       return true;
     }
-    if (sess->congested() && !conn_->reading_paused()) {
-      conn_->pause_reading();
-      sess->add_paused_reader(weak_from_this());
-    }
     return false;
   }
 
@@ -366,6 +431,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     }
     state_ = State::Head;
     req_ = http::Head{};
+    flow_paused_ = false;
     if (pipelined_hold_) {
       pipelined_hold_ = false;
       conn_->resume_reading();
@@ -401,7 +467,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
       stream_registered_ = false;
     }
     conn_.reset();
-    if (sess) sess->conns_.erase(this);
+    if (sess) sess->conn_closed(this);
   }
 
   void cancel_timer() {
@@ -411,7 +477,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     }
   }
 
-  std::weak_ptr<ProxySession> sess_;
+  std::weak_ptr<ProxyWorker> sess_;  // this connection's thread
   std::shared_ptr<TcpConn> conn_;
   std::string inbuf_;
   State state_ = State::Head;
@@ -428,17 +494,83 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
   bool response_complete_ = false;
   bool pipelined_hold_ = false;
   bool reject_not_ready_ = false;
+  bool flow_paused_ = false;
   uint64_t body_sent_ = 0;
   uint64_t timer_ = 0;
-  friend class ProxySession;
+  friend class ProxyWorker;
 };
+
+ProxyWorker::~ProxyWorker() {
+  auto conns = std::move(conns_);
+  for (auto& kv : conns)
+    if (kv.second->conn_) {
+      kv.second->conn_->on_close(nullptr);
+      kv.second->conn_->close();
+    }
+  out_.reset();
+}
+
+void ProxyWorker::adopt(int fd) {
+  trace::event("proxy", uint32_t(fd), "tcp_accept");
+  auto tc = TcpConn::adopt(r_, fd);
+  auto pc = std::make_shared<ProxyConn>(weak_from_this(), tc);
+  conns_[pc.get()] = pc;
+  pc->start();
+}
+
+void ProxyWorker::conn_closed(ProxyConn* c) {
+  if (conns_.erase(c)) out_->push(ProxySession::Ev{ProxySession::Ev::ConnClosed, 0});
+}
+
+void ProxyWorker::fail_all(const std::string& why) {
+  auto streams = std::move(streams_);
+  streams_.clear();
+  for (auto& kv : streams)
+    if (auto c = kv.second.lock()) c->on_res_error(why);
+}
+
+void ProxyWorker::handle(ProxySession::Cmd& c) {
+  using Cmd = ProxySession::Cmd;
+  if (c.kind == Cmd::Adopt) {
+    adopt(c.fd);
+    return;
+  }
+  auto it = streams_.find(c.sid);
+  if (it == streams_.end()) return;
+  auto conn = it->second.lock();
+  switch (c.kind) {
+    case Cmd::Headers:
+      if (conn) conn->on_res_headers(*c.rh);
+      break;
+    case Cmd::Body:
+      if (conn) conn->on_res_body(c.data);
+      break;
+    case Cmd::End:
+      streams_.erase(it);
+      if (conn) conn->on_res_end();
+      break;
+    case Cmd::Error:
+      streams_.erase(it);
+      if (conn) conn->on_res_error(c.data.str());
+      break;
+    case Cmd::Pause:
+      if (conn) conn->flow_pause();
+      break;
+    case Cmd::Resume:
+      if (conn) conn->flow_resume();
+      break;
+    case Cmd::Adopt:
+      break;
+  }
+}
 
 // ---------------------------------------------------------------- session
 
 std::shared_ptr<ProxySession> ProxySession::start(Reactor& r, std::shared_ptr<MessageChannel> ch, ProxyConfig cfg,
-                                                  std::function<void(const std::string&)> done) {
+                                                  std::function<void(const std::string&)> done, WorkerPool* pool) {
   auto s = std::shared_ptr<ProxySession>(new ProxySession(r, ch, std::move(cfg)));
   s->done_ = std::move(done);
+  s->init_links(pool);
   std::weak_ptr<ProxySession> w = s;
   ch->on_message = [w](Bytes b) {
     if (auto x = w.lock()) x->on_message(std::move(b));
@@ -448,6 +580,9 @@ std::shared_ptr<ProxySession> ProxySession::start(Reactor& r, std::shared_ptr<Me
   };
   ch->on_buffered_low = [w] {
     if (auto x = w.lock()) x->sched_->pump();
+  };
+  s->sched_->on_progress = [w] {
+    if (auto x = w.lock()) x->check_paused();
   };
   if (ch->is_open()) {
     LOG_INFO(kT, "data channel already open");
@@ -462,8 +597,50 @@ std::shared_ptr<ProxySession> ProxySession::start(Reactor& r, std::shared_ptr<Me
 }
 
 ProxySession::ProxySession(Reactor& r, std::shared_ptr<MessageChannel> ch, ProxyConfig cfg)
-    : r_(r), ch_(std::move(ch)), cfg_(std::move(cfg)) {
+    : r_(r), ch_(std::move(ch)), cfg_(std::move(cfg)), shared_(std::make_shared<Shared>()) {
   sched_ = std::make_unique<FrameScheduler>(ch_);
+  shared_->cfg = cfg_;
+  shared_->cfg.on_listening = nullptr;
+}
+
+void ProxySession::init_links(WorkerPool* pool) {
+  size_t n = 1 + (pool ? pool->size() : 0);
+  place_ = std::make_unique<Placement>(n, cfg_.inline_streams);
+  std::weak_ptr<ProxySession> self = shared_from_this();
+  for (size_t k = 0; k < n; k++) {
+    Reactor& wr = k == 0 ? r_ : pool->reactor(k - 1);
+    auto worker = std::make_shared<ProxyWorker>(wr, r_, self, shared_, k);
+    std::weak_ptr<ProxyWorker> ww = worker;
+    Link l;
+    l.r = &wr;
+    l.to = std::make_unique<Pipe<Cmd>>(r_, wr, [ww](Cmd& c) {
+      if (auto x = ww.lock()) x->handle(c);
+    });
+    if (k == 0) worker->init();
+    else wr.post_threadsafe([worker] { worker->init(); });  // init before any Cmd batch (FIFO)
+    l.worker = std::move(worker);
+    links_.push_back(std::move(l));
+  }
+}
+
+// Drops the links: pending commands are discarded; each worker fails its
+// in-flight streams (`fail_why`, if any) and is destroyed on its own thread
+// one loop iteration later, after those error responses were written.
+void ProxySession::release_links(const std::string& fail_why) {
+  auto links = std::move(links_);
+  links_.clear();
+  for (size_t k = 0; k < links.size(); k++) {
+    links[k].to.reset();
+    std::shared_ptr<ProxyWorker> w = std::move(links[k].worker);
+    auto finish = [w, fail_why]() mutable {
+      if (!fail_why.empty()) w->fail_all(fail_why);
+      Reactor& wr = w->reactor();
+      wr.post([w]() mutable { w.reset(); });
+      w.reset();
+    };
+    if (k == 0) finish();
+    else links[k].r->post_threadsafe(std::move(finish));
+  }
 }
 
 ProxySession::~ProxySession() {
@@ -475,26 +652,22 @@ ProxySession::~ProxySession() {
     ch_->on_open = nullptr;
     ch_->on_buffered_low = nullptr;
   }
-  auto conns = std::move(conns_);
-  for (auto& kv : conns)
-    if (kv.second->conn_) {
-      kv.second->conn_->on_close(nullptr);
-      kv.second->conn_->close();
-    }
+  release_links("");
 }
 
 void ProxySession::stop(const std::string& why) {
   if (stopped_) return;
   stopped_ = true;
+  ready_ = false;
+  shared_->ready = false;
   if (agree_timer_) r_.cancel(agree_timer_);
   if (ping_timer_) r_.cancel(ping_timer_);
   agree_timer_ = ping_timer_ = 0;
   listener_.reset();  // like the reference, the listener dies with the session
+  routes_.clear();
+  paused_.clear();
   // Fail in-flight requests so clients are not left hanging.
-  auto streams = std::move(streams_);
-  streams_.clear();
-  for (auto& kv : streams)
-    if (auto c = kv.second.lock()) c->on_res_error("tunnel disconnected");
+  release_links("tunnel disconnected");
   auto done = std::move(done_);
   done_ = nullptr;
   if (done) done(why);
@@ -503,6 +676,7 @@ void ProxySession::stop(const std::string& why) {
 void ProxySession::on_open() {
   if (stopped_ || hello_sent_) return;
   LOG_INFO(kT, "data channel ready, performing handshake...");
+  shared_->body_chunk = sched_->body_chunk();  // path MTU known now; read by connection threads later
   proto::Hello hello;
   hello.features = proto::our_features();
   if (!cfg_.secret.empty()) {  // psk extension: prove the shared secret on this channel
@@ -524,7 +698,7 @@ void ProxySession::on_open() {
     }
   });
   sched_->set_watermarks(cfg_.high_water, cfg_.low_water, [w] {
-    if (auto s = w.lock()) s->on_relief();
+    if (auto s = w.lock()) s->check_paused();
   });
 }
 
@@ -576,8 +750,10 @@ void ProxySession::on_agree(const proto::Frame& f) {
       return;
     }
   }
-  cancel_feature_ = std::find(agree.features.begin(), agree.features.end(), "cancel") != agree.features.end();
+  shared_->cancel_feature =
+      std::find(agree.features.begin(), agree.features.end(), "cancel") != agree.features.end();
   ready_ = true;
+  shared_->ready = true;
   last_pong_ms_ = Reactor::now_ms();
   send_ping();
   if (!listener_ && !cfg_.listen_early) {
@@ -606,15 +782,14 @@ bool ProxySession::bind_listener() {
 }
 
 void ProxySession::accept(int fd) {
-  if (stopped_) {
+  if (stopped_ || links_.empty()) {
     ::close(fd);
     return;
   }
-  trace::event("proxy", uint32_t(fd), "tcp_accept");
-  auto tc = TcpConn::adopt(r_, fd);
-  auto pc = std::make_shared<ProxyConn>(weak_from_this(), tc);
-  conns_[pc.get()] = pc;
-  pc->start();
+  size_t k = place_->pick();
+  Cmd c{Cmd::Adopt};
+  c.fd = fd;
+  command(k, std::move(c));
 }
 
 void ProxySession::send_ping() {
@@ -634,46 +809,107 @@ void ProxySession::send_ping() {
   });
 }
 
+void ProxySession::on_event(size_t thread, Ev& ev) {
+  if (stopped_) return;
+  switch (ev.kind) {
+    case Ev::Route:
+      routes_[ev.sid] = Route{thread, false};
+      return;
+    case Ev::Unroute:
+      routes_.erase(ev.sid);
+      paused_.erase(ev.sid);
+      return;
+    case Ev::ConnClosed:
+      place_->release(thread);
+      return;
+    case Ev::Frame:
+      break;
+  }
+  bool body = ev.frame.type == proto::MsgType::ReqBody;
+  uint32_t sid = ev.frame.stream_id;
+  sched_->send(std::move(ev.frame));
+  if (!body) return;
+  auto it = routes_.find(sid);
+  if (it == routes_.end() || it->second.paused) return;
+  // Per-stream back-pressure for uploads: pause just this client's reads.
+  size_t q = sched_->stream_queued(sid);
+  if (q > cfg_.stream_budget || (q > FrameScheduler::kInteractive && sched_->over_high())) {
+    it->second.paused = true;
+    paused_.insert(sid);
+    command(it->second.thread, Cmd{Cmd::Pause, sid});
+  }
+}
+
+void ProxySession::check_paused() {
+  if (paused_.empty() || stopped_ || sched_->over_high()) return;
+  for (auto p = paused_.begin(); p != paused_.end();) {
+    uint32_t sid = *p;
+    auto it = routes_.find(sid);
+    if (it == routes_.end()) {
+      p = paused_.erase(p);
+      continue;
+    }
+    if (sched_->stream_queued(sid) <= cfg_.stream_budget / 4) {
+      it->second.paused = false;
+      p = paused_.erase(p);
+      command(it->second.thread, Cmd{Cmd::Resume, sid});
+      continue;
+    }
+    ++p;
+  }
+}
+
 void ProxySession::route(const proto::Frame& f) {
   using proto::MsgType;
   switch (f.type) {
     case MsgType::ResHeaders: {
       Json j;
       std::string err;
-      proto::ResponseHeaders rh;
-      if (!proto::json_parse_bytes(f.payload, j, &err) || !proto::ResponseHeaders::from_json(j, rh, &err)) {
+      auto rh = std::make_shared<proto::ResponseHeaders>();
+      if (!proto::json_parse_bytes(f.payload, j, &err) || !proto::ResponseHeaders::from_json(j, *rh, &err)) {
         LOG_ERROR(kT, "failed to parse response headers: %s", err.c_str());
         return;
       }
-      LOG_DEBUG(kT, "response headers for stream %u: status=%u", rh.stream_id, rh.status);
-      auto it = streams_.find(rh.stream_id);  // routed by the JSON stream_id (proxy.rs:131)
-      if (it != streams_.end())
-        if (auto c = it->second.lock()) c->on_res_headers(rh);
+      LOG_DEBUG(kT, "response headers for stream %u: status=%u", rh->stream_id, rh->status);
+      uint32_t sid = rh->stream_id;  // routed by the JSON stream_id (proxy.rs:131)
+      auto it = routes_.find(sid);
+      if (it != routes_.end()) {
+        Cmd c{Cmd::Headers, sid};
+        c.rh = std::move(rh);
+        command(it->second.thread, std::move(c));
+      }
       break;
     }
     case MsgType::ResBody: {
-      auto it = streams_.find(f.stream_id);
-      if (it != streams_.end())
-        if (auto c = it->second.lock()) c->on_res_body(f.payload);
+      auto it = routes_.find(f.stream_id);
+      if (it != routes_.end()) {
+        Cmd c{Cmd::Body, f.stream_id};
+        c.data = f.payload;
+        command(it->second.thread, std::move(c));
+      }
       break;
     }
     case MsgType::ResEnd: {
-      auto it = streams_.find(f.stream_id);
-      if (it != streams_.end()) {
-        auto c = it->second.lock();
-        streams_.erase(it);
-        if (c) c->on_res_end();
+      auto it = routes_.find(f.stream_id);
+      if (it != routes_.end()) {
+        size_t k = it->second.thread;
+        routes_.erase(it);
+        paused_.erase(f.stream_id);
+        command(k, Cmd{Cmd::End, f.stream_id});
       }
       break;
     }
     case MsgType::Error: {
       std::string msg = f.payload.str();
       LOG_ERROR(kT, "tunnel error for stream %u: %s", f.stream_id, msg.c_str());
-      auto it = streams_.find(f.stream_id);
-      if (it != streams_.end()) {
-        auto c = it->second.lock();
-        streams_.erase(it);
-        if (c) c->on_res_error(msg);
+      auto it = routes_.find(f.stream_id);
+      if (it != routes_.end()) {
+        size_t k = it->second.thread;
+        routes_.erase(it);
+        paused_.erase(f.stream_id);
+        Cmd c{Cmd::Error, f.stream_id};
+        c.data = f.payload;
+        command(k, std::move(c));
       }
       break;
     }
@@ -688,13 +924,6 @@ void ProxySession::route(const proto::Frame& f) {
     default:
       LOG_DEBUG(kT, "proxy ignoring message type %s", proto::msg_type_name(f.type));
   }
-}
-
-void ProxySession::on_relief() {
-  auto readers = std::move(paused_readers_);
-  paused_readers_.clear();
-  for (auto& w : readers)
-    if (auto c = w.lock()) c->resume_reading();
 }
 
 }  // namespace p2pt

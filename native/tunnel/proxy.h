@@ -13,20 +13,31 @@
 //     END before headers -> 502 "Tunnel error: ..."                       (:339-376)
 //   - response minus transfer-encoding/connection, body streamed per frame (:379-419)
 // Differences (local only, wire-compatible): request bodies are streamed
-// instead of fully buffered; a mid-stream ERROR aborts the client connection
-// instead of ending the body as if complete (Q10); a client disconnect sends
-// CANCEL when the peer negotiated it (Q12); --listen-early binds before the
-// handshake and answers 503 "Tunnel not ready" until it completes (Q8).
+// instead of fully buffered, and a stream whose REQ_BODY frames pile up has
+// just its own client read paused; a mid-stream ERROR aborts the client
+// connection instead of ending the body as if complete (Q10); a client
+// disconnect sends CANCEL when the peer negotiated it (Q12); --listen-early
+// binds before the handshake and answers 503 "Tunnel not ready" until it
+// completes (Q8).
+//
+// Threads (tunnel/workers.h): the session (handshake, keepalive, routing of
+// RES_* frames by stream id) lives on the association thread; each client
+// connection lives on one reactor — the association thread's own for the
+// first `inline_streams` connections, a worker's beyond that (the reference's
+// task per connection, proxy.rs:196-217).
 #pragma once
 
+#include <atomic>
 #include <functional>
 #include <memory>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 
 #include "proto/frame.h"
 #include "tunnel/channel.h"
 #include "tunnel/scheduler.h"
+#include "tunnel/workers.h"
 
 namespace p2pt {
 
@@ -39,68 +50,100 @@ struct ProxyConfig {
   bool listen_early = false;
   size_t high_water = 4 << 20;
   size_t low_water = 1 << 20;
+  size_t stream_budget = 256 << 10;  // one upload's queued bytes before its client read pauses
   // Pre-shared secret ("psk" extension, --secret): HELLO carries a proof and
   // an AGREE without the serve side's proof ends the session.
   std::string secret;
+  // Client connections kept on the association thread before new ones go to
+  // worker threads (see tunnel/workers.h).
+  size_t inline_streams = 16;
   // Called with the bound address once listening (tests/bench use port 0).
   std::function<void(const std::string&)> on_listening;
 };
 
 class ProxyConn;
+class ProxyWorker;
 class TcpListener;
 
 class ProxySession : public std::enable_shared_from_this<ProxySession> {
  public:
   static std::shared_ptr<ProxySession> start(Reactor& r, std::shared_ptr<MessageChannel> ch, ProxyConfig cfg,
-                                             std::function<void(const std::string&)> done);
+                                             std::function<void(const std::string&)> done,
+                                             WorkerPool* pool = nullptr);
   ~ProxySession();
-  // Hand an accepted client socket to this session (used by the early
+  // Hand an accepted client socket to this session (also used by the early
   // listener, which outlives sessions; see tunnel/app.cc).
   void accept(int fd);
   void stop(const std::string& why);
   bool ready() const { return ready_; }
 
-  // ---- used by ProxyConn
-  uint32_t next_stream_id() { return next_sid_++; }
-  void register_stream(uint32_t sid, std::weak_ptr<ProxyConn> c) { streams_[sid] = std::move(c); }
-  void unregister_stream(uint32_t sid) { streams_.erase(sid); }
-  void send(proto::Frame f) { sched_->send(std::move(f)); }
-  bool congested() const { return sched_->over_high(); }
-  size_t body_chunk() const { return sched_->body_chunk(); }
-  void add_paused_reader(std::weak_ptr<ProxyConn> c) { paused_readers_.push_back(std::move(c)); }
-  bool cancel_feature() const { return cancel_feature_; }
-  const ProxyConfig& config() const { return cfg_; }
-  Reactor& reactor() { return r_; }
+  // State the connection threads read.
+  struct Shared {
+    ProxyConfig cfg;
+    std::atomic<uint32_t> next_sid{1};
+    std::atomic<bool> ready{false};
+    std::atomic<bool> cancel_feature{false};
+    size_t body_chunk = proto::kMaxBodyChunk;
+  };
+  // Association thread -> a connection thread.
+  struct Cmd {
+    enum Kind : uint8_t { Adopt, Headers, Body, End, Error, Pause, Resume } kind;
+    explicit Cmd(Kind k, uint32_t s = 0) : kind(k), sid(s) {}
+    uint32_t sid = 0;
+    int fd = -1;                                  // Adopt
+    Bytes data;                                   // Body / Error message
+    std::shared_ptr<proto::ResponseHeaders> rh;   // Headers
+  };
+  // A connection thread -> association thread.
+  struct Ev {
+    enum Kind : uint8_t { Route, Unroute, Frame, ConnClosed } kind;
+    explicit Ev(Kind k, uint32_t s = 0) : kind(k), sid(s) {}
+    uint32_t sid = 0;
+    proto::Frame frame{proto::MsgType::Ping, 0, Bytes()};
+  };
 
  private:
+  struct Link {
+    Reactor* r = nullptr;
+    std::unique_ptr<Pipe<Cmd>> to;
+    std::shared_ptr<ProxyWorker> worker;  // owned here; released on its own thread
+  };
+  struct Route {
+    size_t thread = 0;
+    bool paused = false;
+  };
   ProxySession(Reactor& r, std::shared_ptr<MessageChannel> ch, ProxyConfig cfg);
+  void init_links(WorkerPool* pool);
+  void release_links(const std::string& fail_why);
   void on_open();
   void on_message(Bytes raw);
   void on_agree(const proto::Frame& f);
   void route(const proto::Frame& f);
   void send_ping();
   bool bind_listener();
-  void on_relief();
+  void on_event(size_t thread, Ev& ev);
+  void check_paused();
+  void command(size_t thread, Cmd c) { links_[thread].to->push(std::move(c)); }
 
   Reactor& r_;
   std::shared_ptr<MessageChannel> ch_;
   std::unique_ptr<FrameScheduler> sched_;
   ProxyConfig cfg_;
+  std::shared_ptr<Shared> shared_;
   std::function<void(const std::string&)> done_;
   std::unique_ptr<TcpListener> listener_;
-  std::unordered_map<uint32_t, std::weak_ptr<ProxyConn>> streams_;
-  std::unordered_map<ProxyConn*, std::shared_ptr<ProxyConn>> conns_;
-  std::vector<std::weak_ptr<ProxyConn>> paused_readers_;
-  uint32_t next_sid_ = 1;
+  std::unordered_map<uint32_t, Route> routes_;
+  std::unordered_set<uint32_t> paused_;
+  std::vector<Link> links_;
+  std::unique_ptr<Placement> place_;
   bool hello_sent_ = false;
   bool ready_ = false;
   bool stopped_ = false;
-  bool cancel_feature_ = false;
   std::string psk_nonce_;  // psk extension: the nonce our HELLO carried
   uint64_t agree_timer_ = 0;
   uint64_t ping_timer_ = 0;
   uint64_t last_pong_ms_ = 0;
-  friend class ProxyConn;
+  friend class ProxyWorker;
 };
 
 }  // namespace p2pt

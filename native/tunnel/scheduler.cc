@@ -24,6 +24,11 @@ bool FrameScheduler::emit(const proto::Frame& f) {
   return ch_->send(hdr, sizeof hdr, f.payload);
 }
 
+void FrameScheduler::list(uint32_t sid, StreamQ& s) {
+  s.listed = true;
+  (s.bytes <= kInteractive ? interactive_ : bulk_).push_back(sid);
+}
+
 void FrameScheduler::send(proto::Frame f) {
   if (!ch_ || !ch_->is_open()) return;
   // Fast path: nothing queued and the channel has room.
@@ -32,46 +37,72 @@ void FrameScheduler::send(proto::Frame f) {
     if (pending_bytes() > high_) was_high_ = true;
     return;
   }
-  queued_ += f.wire_size();
+  size_t sz = f.wire_size();
+  queued_ += sz;
   if (f.stream_id == 0) {
     control_.push_back(std::move(f));
   } else {
-    auto& q = streams_[f.stream_id];
-    if (q.empty()) rr_.push_back(f.stream_id);
-    q.push_back(std::move(f));
+    uint32_t sid = f.stream_id;
+    auto& s = streams_[sid];
+    s.q.push_back(std::move(f));
+    s.bytes += sz;
+    if (!s.listed) list(sid, s);
   }
   if (pending_bytes() > high_) was_high_ = true;
   pump();
 }
 
+// Releases the head frame of the first stream in `lane`; false if the lane is empty.
+bool FrameScheduler::pop_from(std::deque<uint32_t>& lane) {
+  while (!lane.empty()) {
+    uint32_t sid = lane.front();
+    lane.pop_front();
+    auto it = streams_.find(sid);
+    if (it == streams_.end()) continue;
+    StreamQ& s = it->second;
+    s.listed = false;
+    if (s.q.empty()) {
+      streams_.erase(it);
+      continue;
+    }
+    proto::Frame f = std::move(s.q.front());
+    s.q.pop_front();
+    size_t sz = f.wire_size();
+    s.bytes -= sz;
+    queued_ -= sz;
+    if (s.q.empty()) streams_.erase(it);
+    else list(sid, s);  // re-queued behind the others, in the lane its backlog now calls for
+    emit(f);
+    return true;
+  }
+  return false;
+}
+
 void FrameScheduler::pump() {
   if (pumping_ || !ch_) return;
   pumping_ = true;
+  bool progressed = false;
   while (ch_->is_open() && queued_ && ch_->buffered_amount() < window_) {
     if (!control_.empty()) {
       proto::Frame f = std::move(control_.front());
       control_.pop_front();
       queued_ -= f.wire_size();
       emit(f);
+      progressed = true;
       continue;
     }
-    if (rr_.empty()) break;
-    uint32_t sid = rr_.front();
-    rr_.pop_front();
-    auto it = streams_.find(sid);
-    if (it == streams_.end() || it->second.empty()) continue;
-    proto::Frame f = std::move(it->second.front());
-    it->second.pop_front();
-    queued_ -= f.wire_size();
-    if (it->second.empty()) streams_.erase(it);
-    else rr_.push_back(sid);
-    emit(f);
+    if (pop_from(interactive_) || pop_from(bulk_)) {
+      progressed = true;
+      continue;
+    }
+    break;
   }
   pumping_ = false;
   if (was_high_ && pending_bytes() <= low_) {
     was_high_ = false;
     if (low_cb_) low_cb_();
   }
+  if (progressed && on_progress) on_progress();
 }
 
 }  // namespace p2pt

@@ -3,11 +3,19 @@
 // The reference writes every frame straight into the data channel with no
 // back-pressure (reference serve.rs:274, proxy.rs:324), so
 // a 1 MB body queued ahead of an SSE token delays that token by the whole
-// body. Here frames wait in per-stream FIFOs and are released round-robin
-// (one frame per stream per turn, control frames first) only while the
-// channel's buffered amount is below a window. Head-of-line delay for a
-// token is therefore bounded by the window, not by other streams' bodies.
-// Wire format is unchanged: per-stream frame order is preserved.
+// body. Here frames wait in per-stream FIFOs and are released into the channel
+// only while its buffered amount is below a window, in this order:
+//
+//   1. control frames (stream 0: HELLO/AGREE/PING/PONG/credit);
+//   2. the "interactive" lane: streams with little queued (<= kInteractive
+//      bytes, e.g. an SSE stream with its next token), one frame per turn;
+//   3. the bulk lane: backlogged streams, round-robin one frame per turn.
+//
+// So a token waits for at most the channel window plus one frame, never for
+// other streams' queued bodies. Per-stream FIFO order is preserved (the wire
+// format is unchanged: frames of one stream never reorder). Per-stream queue
+// sizes are exposed so producers can pause just the streams that are over
+// their budget instead of everyone.
 #pragma once
 
 #include <deque>
@@ -22,29 +30,46 @@ namespace p2pt {
 
 class FrameScheduler {
  public:
+  static constexpr size_t kInteractive = 4096;
+
   explicit FrameScheduler(std::shared_ptr<MessageChannel> ch, size_t window = 64 * 1024);
   ~FrameScheduler();
 
-  // Stream 0 frames (HELLO/AGREE/PING/PONG) are control frames and jump the queue.
   void send(proto::Frame f);
   // Bytes held here plus bytes buffered in the channel.
   size_t pending_bytes() const { return queued_ + (ch_ ? ch_->buffered_amount() : 0); }
   size_t queued_bytes() const { return queued_; }
-  // Back-pressure hook: `cb` fires when pending_bytes() drops below `low`
-  // after having exceeded `high`. Producers pause when pending_bytes() > high.
+  // Bytes of `sid` held in the scheduler (not yet handed to the channel).
+  size_t stream_queued(uint32_t sid) const {
+    auto it = streams_.find(sid);
+    return it == streams_.end() ? 0 : it->second.bytes;
+  }
+  // Global watermarks: `cb` fires when pending_bytes() drops to `low` after
+  // having exceeded `high`.
   void set_watermarks(size_t high, size_t low, std::function<void()> cb);
   bool over_high() const { return pending_bytes() > high_; }
+  // Fires after a pump that released frames (producers re-check paused streams).
+  std::function<void()> on_progress;
   void pump();
   MessageChannel* channel() const { return ch_.get(); }
   size_t body_chunk() const { return ch_ ? ch_->body_chunk() : proto::kMaxBodyChunk; }
+  size_t window() const { return window_; }
 
  private:
+  struct StreamQ {
+    std::deque<proto::Frame> q;
+    size_t bytes = 0;
+    bool listed = false;
+  };
   bool emit(const proto::Frame& f);
+  void list(uint32_t sid, StreamQ& s);
+  bool pop_from(std::deque<uint32_t>& lane);
+
   std::shared_ptr<MessageChannel> ch_;
   size_t window_;
   std::deque<proto::Frame> control_;
-  std::unordered_map<uint32_t, std::deque<proto::Frame>> streams_;
-  std::deque<uint32_t> rr_;
+  std::unordered_map<uint32_t, StreamQ> streams_;
+  std::deque<uint32_t> interactive_, bulk_;
   size_t queued_ = 0;
   size_t high_ = SIZE_MAX, low_ = 0;
   bool was_high_ = false;

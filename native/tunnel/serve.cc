@@ -10,10 +10,160 @@ namespace p2pt {
 
 static const char* kT = "tunnel::serve";
 
+// Runs upstream calls on one reactor (the association thread's own or a
+// worker's) and reports frames back to the session through a Pipe. Created,
+// used and destroyed on its reactor's thread only.
+class ServeWorker : public std::enable_shared_from_this<ServeWorker> {
+ public:
+  ServeWorker(Reactor& r, Reactor& assoc, std::weak_ptr<ServeSession> sess, const ServeConfig& cfg,
+              std::vector<std::string> upstreams, bool is_inline)
+      : r_(r), assoc_(assoc), sess_(std::move(sess)), cfg_(cfg), upstreams_(std::move(upstreams)),
+        inline_(is_inline) {}
+
+  ~ServeWorker() {
+    auto calls = std::move(calls_);
+    for (auto& kv : calls)
+      if (kv.second) kv.second->cancel();
+    client_.reset();
+    out_.reset();
+  }
+
+  void init() {
+    client_ = std::make_unique<http::HttpClient>(r_);
+    std::weak_ptr<ServeSession> w = sess_;
+    out_ = std::make_unique<Pipe<ServeSession::Ev>>(r_, assoc_, [w](ServeSession::Ev& ev) {
+      if (auto s = w.lock()) s->on_event(ev);
+    });
+  }
+
+  void handle(ServeSession::Cmd& c) {
+    using Cmd = ServeSession::Cmd;
+    switch (c.kind) {
+      case Cmd::Start: start(c.sid, std::move(c.req), c.body_chunk); break;
+      case Cmd::Cancel: {
+        auto it = calls_.find(c.sid);
+        if (it == calls_.end()) break;
+        auto call = it->second;
+        calls_.erase(it);
+        if (call) call->cancel();
+        break;
+      }
+      case Cmd::Pause:
+      case Cmd::Resume: {
+        auto it = calls_.find(c.sid);
+        if (it != calls_.end() && it->second) {
+          if (c.kind == Cmd::Pause) it->second->pause();
+          else it->second->resume();
+        }
+        break;
+      }
+      case Cmd::Prewarm: prewarm(); break;
+    }
+  }
+
+ private:
+  void prewarm() {
+    if (prewarmed_ || !cfg_.upstream_prewarm) return;
+    prewarmed_ = true;
+    for (auto& u : upstreams_) {
+      std::string perr;
+      if (!client_->prewarm(u, cfg_.upstream_prewarm, cfg_.upstream_prewarm_ttl_ms, &perr))
+        LOG_DEBUG(kT, "upstream prewarm disabled for %s: %s", u.c_str(), perr.c_str());
+    }
+  }
+
+  void emit(uint32_t sid, proto::Frame f) {
+    ServeSession::Ev ev(ServeSession::Ev::Frame, sid);
+    ev.frame = std::move(f);
+    out_->push(std::move(ev));
+  }
+
+  void simple_response(uint32_t sid, uint16_t status, const std::string& body) {
+    proto::ResponseHeaders rh;
+    rh.stream_id = sid;
+    rh.status = status;
+    rh.headers.emplace_back("content-type", "text/plain");
+    emit(sid, proto::make_res_headers(rh));
+    emit(sid, proto::make_body(proto::MsgType::ResBody, sid, Bytes::copy(body)));
+    emit(sid, proto::make_empty(proto::MsgType::ResEnd, sid));
+  }
+
+  void start(uint32_t sid, http::ClientRequest req, size_t body_chunk) {
+    if (!inline_) prewarm();  // workers warm their own pools on first use
+    std::weak_ptr<ServeWorker> w = shared_from_this();
+    http::ClientCallbacks cb;
+    cb.on_sent = [sid](bool) { trace::event("serve", sid, "upstream_sent"); };
+    cb.on_head = [w, sid](const http::Head& h) {
+      auto s = w.lock();
+      if (!s) return;
+      proto::ResponseHeaders rh;
+      rh.stream_id = sid;
+      rh.status = uint16_t(h.status);
+      for (auto& hd : h.headers)
+        if (http::is_visible_ascii(hd.value)) proto::header_set(rh.headers, http::to_lower(hd.name), hd.value);
+      s->emit(sid, proto::make_res_headers(rh));
+      trace::event("serve", sid, "res_headers");
+    };
+    auto first = std::make_shared<bool>(true);
+    size_t cs = body_chunk ? body_chunk : proto::kMaxBodyChunk;
+    cb.on_data = [w, sid, first, cs](Bytes chunk) {
+      auto s = w.lock();
+      if (!s) return;
+      if (*first) {
+        *first = false;
+        trace::event("serve", sid, "first_body");
+      }
+      // `chunk` views the upstream socket's receive buffer (large reads) or is a
+      // private copy (small ones, e.g. SSE tokens); frames slice it, no copy.
+      size_t n = chunk.size();
+      for (size_t off = 0; off < n; off += cs)
+        s->emit(sid, proto::make_body(proto::MsgType::ResBody, sid, chunk.slice(off, cs)));
+    };
+    cb.on_done = [w, sid](const std::string& err, bool before_head) {
+      auto s = w.lock();
+      if (!s) return;
+      auto it = s->calls_.find(sid);
+      if (it == s->calls_.end()) return;  // cancelled
+      s->calls_.erase(it);
+      if (!err.empty() && before_head) {
+        LOG_ERROR(kT, "upstream request failed: %s", err.c_str());
+        metrics::counter_add("tunnel_upstream_errors_total");
+        s->simple_response(sid, 502, "Bad Gateway: " + err);
+      } else {
+        if (!err.empty()) {
+          LOG_ERROR(kT, "upstream stream error for stream %u: %s", sid, err.c_str());
+          s->emit(sid, proto::make_error(sid, "upstream error: " + err));
+        }
+        s->emit(sid, proto::make_empty(proto::MsgType::ResEnd, sid));
+        trace::event("serve", sid, "res_end");
+        LOG_DEBUG(kT, "response %u complete", sid);
+      }
+      ServeSession::Ev done{ServeSession::Ev::Done, sid};
+      s->out_->push(std::move(done));
+    };
+    calls_[sid] = nullptr;  // present while the call runs (on_done may fire inside request())
+    auto call = client_->request(std::move(req), std::move(cb));
+    auto it = calls_.find(sid);
+    if (it != calls_.end()) it->second = call;
+  }
+
+  Reactor& r_;
+  Reactor& assoc_;
+  std::weak_ptr<ServeSession> sess_;
+  ServeConfig cfg_;
+  std::vector<std::string> upstreams_;
+  bool inline_;
+  bool prewarmed_ = false;
+  std::unique_ptr<http::HttpClient> client_;
+  std::unique_ptr<Pipe<ServeSession::Ev>> out_;
+  std::unordered_map<uint32_t, std::shared_ptr<http::ClientCall>> calls_;
+};
+
 std::shared_ptr<ServeSession> ServeSession::start(Reactor& r, std::shared_ptr<MessageChannel> ch, ServeConfig cfg,
-                                                  std::function<void(const std::string&)> done) {
+                                                  std::function<void(const std::string&)> done, WorkerPool* pool) {
   auto s = std::shared_ptr<ServeSession>(new ServeSession(r, ch, std::move(cfg)));
   s->done_ = std::move(done);
+  s->init_links(pool);
   std::weak_ptr<ServeSession> w = s;
   ch->on_message = [w](Bytes b) {
     if (auto x = w.lock()) x->on_message(std::move(b));
@@ -23,6 +173,12 @@ std::shared_ptr<ServeSession> ServeSession::start(Reactor& r, std::shared_ptr<Me
       LOG_INFO(kT, "data channel closed, serve ending");
       x->stop("data channel closed: " + why);
     }
+  };
+  ch->on_buffered_low = [w] {
+    if (auto x = w.lock()) x->sched_->pump();
+  };
+  s->sched_->on_progress = [w] {
+    if (auto x = w.lock()) x->check_paused();
   };
   if (ch->is_open()) {
     LOG_INFO(kT, "data channel already open");
@@ -37,7 +193,7 @@ std::shared_ptr<ServeSession> ServeSession::start(Reactor& r, std::shared_ptr<Me
 }
 
 ServeSession::ServeSession(Reactor& r, std::shared_ptr<MessageChannel> ch, ServeConfig cfg)
-    : r_(r), ch_(std::move(ch)), cfg_(std::move(cfg)), client_(r) {
+    : r_(r), ch_(std::move(ch)), cfg_(std::move(cfg)) {
   sched_ = std::make_unique<FrameScheduler>(ch_);
   for (size_t a = 0; a <= cfg_.upstream.size();) {
     size_t c = cfg_.upstream.find(',', a);
@@ -47,15 +203,48 @@ ServeSession::ServeSession(Reactor& r, std::shared_ptr<MessageChannel> ch, Serve
   }
   if (upstreams_.empty()) upstreams_.push_back(cfg_.upstream);
   outstanding_.assign(upstreams_.size(), 0);
-  std::weak_ptr<ServeSession> w;  // set after construction via on_open
-  ch_->on_buffered_low = [this] { sched_->pump(); };
+}
+
+void ServeSession::init_links(WorkerPool* pool) {
+  size_t n = 1 + (pool ? pool->size() : 0);
+  place_ = std::make_unique<Placement>(n, cfg_.inline_streams);
+  std::weak_ptr<ServeSession> self = shared_from_this();
+  for (size_t k = 0; k < n; k++) {
+    Reactor& wr = k == 0 ? r_ : pool->reactor(k - 1);
+    auto worker = std::make_shared<ServeWorker>(wr, r_, self, cfg_, upstreams_, k == 0);
+    std::weak_ptr<ServeWorker> ww = worker;
+    Link l;
+    l.r = &wr;
+    l.to = std::make_unique<Pipe<Cmd>>(r_, wr, [ww](Cmd& c) {
+      if (auto x = ww.lock()) x->handle(c);
+    });
+    if (k == 0) worker->init();
+    else wr.post_threadsafe([worker] { worker->init(); });  // init before any Cmd batch (FIFO)
+    l.worker = std::move(worker);
+    links_.push_back(std::move(l));
+  }
+}
+
+// Drops the links: pending commands are discarded and each worker object is
+// destroyed on its own thread (cancelling its upstream calls there).
+void ServeSession::release_links() {
+  auto links = std::move(links_);
+  links_.clear();
+  for (size_t k = 0; k < links.size(); k++) {
+    links[k].to.reset();
+    if (k == 0) {
+      links[k].worker.reset();
+    } else {
+      std::shared_ptr<ServeWorker> w = std::move(links[k].worker);
+      links[k].r->post_threadsafe([w]() mutable { w.reset(); });
+    }
+  }
 }
 
 ServeSession::~ServeSession() {
   if (hello_timer_) r_.cancel(hello_timer_);
   if (ping_timer_) r_.cancel(ping_timer_);
-  for (auto& kv : inflight_)
-    if (kv.second.call) kv.second.call->cancel();
+  release_links();
   if (ch_) {
     ch_->on_message = nullptr;
     ch_->on_closed = nullptr;
@@ -70,12 +259,11 @@ void ServeSession::stop(const std::string& why) {
   if (hello_timer_) r_.cancel(hello_timer_);
   if (ping_timer_) r_.cancel(ping_timer_);
   hello_timer_ = ping_timer_ = 0;
-  auto inflight = std::move(inflight_);
   inflight_.clear();
+  paused_.clear();
   std::fill(outstanding_.begin(), outstanding_.end(), 0);
-  for (auto& kv : inflight)
-    if (kv.second.call) kv.second.call->cancel();
   streams_.clear();
+  release_links();
   auto done = std::move(done_);
   done_ = nullptr;
   if (done) done(why);
@@ -92,7 +280,7 @@ void ServeSession::on_open() {
     }
   });
   sched_->set_watermarks(cfg_.high_water, cfg_.low_water, [w] {
-    if (auto s = w.lock()) s->on_backpressure_relief();
+    if (auto s = w.lock()) s->check_paused();
   });
 }
 
@@ -158,13 +346,7 @@ void ServeSession::on_hello(const proto::Frame& f) {
   sched_->send(proto::make_agree(agree));
   handshaken_ = true;
   LOG_INFO(kT, "sent AGREE, tunnel ready");
-  if (cfg_.upstream_prewarm) {
-    for (auto& u : upstreams_) {
-      std::string perr;
-      if (!client_.prewarm(u, cfg_.upstream_prewarm, cfg_.upstream_prewarm_ttl_ms, &perr))
-        LOG_DEBUG(kT, "upstream prewarm disabled for %s: %s", u.c_str(), perr.c_str());
-    }
-  }
+  if (cfg_.upstream_prewarm) command(0, Cmd{Cmd::Prewarm});
   last_pong_ms_ = Reactor::now_ms();
   send_ping();  // tokio::time::interval's first tick is immediate
 }
@@ -230,10 +412,12 @@ void ServeSession::handle_frame(const proto::Frame& f) {
       auto it = inflight_.find(f.stream_id);
       if (it != inflight_.end()) {
         LOG_DEBUG(kT, "stream %u cancelled by peer", f.stream_id);
-        auto call = it->second.call;
-        release_upstream(it->second);
+        Inflight fl = it->second;
+        release_upstream(fl);
+        place_->release(fl.thread);
         inflight_.erase(it);
-        if (call) call->cancel();
+        paused_.erase(f.stream_id);
+        command(fl.thread, Cmd{Cmd::Cancel, f.stream_id});
         metrics::counter_add("tunnel_streams_cancelled_total");
       }
       streams_.erase(f.stream_id);
@@ -280,17 +464,21 @@ size_t ServeSession::pick_upstream() {
 }
 
 void ServeSession::start_request(uint32_t sid, Pending p) {
-  const size_t up = pick_upstream();
-  std::string url = proto::build_upstream_url(upstreams_[up], cfg_.advertise, p.headers.path);
-  LOG_DEBUG(kT, "forwarding %s %s -> %s", p.headers.method.c_str(), p.headers.path.c_str(), url.c_str());
   if (!valid_method(p.headers.method)) {
     LOG_ERROR(kT, "failed to handle request: invalid HTTP method");
     send_simple_response(sid, 400, "Bad Request: invalid HTTP method");
     return;
   }
-  http::ClientRequest req;
+  if (inflight_.count(sid)) {
+    LOG_WARN(kT, "stream %u reused while its response is in flight; ignoring the new request", sid);
+    return;
+  }
+  const size_t up = pick_upstream();
+  Cmd c{Cmd::Start, sid};
+  http::ClientRequest& req = c.req;
   req.method = p.headers.method;
-  req.url = url;
+  req.url = proto::build_upstream_url(upstreams_[up], cfg_.advertise, p.headers.path);
+  LOG_DEBUG(kT, "forwarding %s %s -> %s", p.headers.method.c_str(), p.headers.path.c_str(), req.url.c_str());
   bool had_cl = false;
   for (auto& kv : p.headers.headers) {
     const std::string& k = kv.first;
@@ -305,81 +493,60 @@ void ServeSession::start_request(uint32_t sid, Pending p) {
   req.body = std::move(p.body);
   req.body_len = p.body_len;
   req.force_content_length = had_cl;
-
-  std::weak_ptr<ServeSession> w = shared_from_this();
+  c.body_chunk = sched_->body_chunk();
   metrics::counter_add("tunnel_upstream_requests_total");
-  http::ClientCallbacks cb;
-  cb.on_sent = [sid](bool) { trace::event("serve", sid, "upstream_sent"); };
-  cb.on_head = [w, sid](const http::Head& h) {
-    auto s = w.lock();
-    if (!s || s->stopped_) return;
-    proto::ResponseHeaders rh;
-    rh.stream_id = sid;
-    rh.status = uint16_t(h.status);
-    for (auto& hd : h.headers)
-      if (http::is_visible_ascii(hd.value)) proto::header_set(rh.headers, http::to_lower(hd.name), hd.value);
-    s->sched_->send(proto::make_res_headers(rh));
-    trace::event("serve", sid, "res_headers");
-  };
-  auto first = std::make_shared<bool>(true);
-  cb.on_data = [w, sid, first](Bytes chunk) {
-    auto s = w.lock();
-    if (!s || s->stopped_) return;
-    if (*first) {
-      *first = false;
-      trace::event("serve", sid, "first_body");
-    }
-    // `chunk` views the upstream socket's receive buffer (large reads) or is a
-    // private copy (small ones, e.g. SSE tokens); frames slice it, no copy.
-    size_t n = chunk.size();
-    size_t cs = s->sched_->body_chunk();
-    for (size_t off = 0; off < n; off += cs)
-      s->sched_->send(proto::make_body(proto::MsgType::ResBody, sid, chunk.slice(off, cs)));
-    if (s->sched_->over_high() && !s->upstream_paused_) {
-      s->upstream_paused_ = true;
-      for (auto& kv : s->inflight_)
-        if (kv.second.call) kv.second.call->pause();
-    }
-  };
-  cb.on_done = [w, sid, url](const std::string& err, bool before_head) {
-    auto s = w.lock();
-    if (!s) return;
-    auto it = s->inflight_.find(sid);
-    if (it == s->inflight_.end()) return;  // cancelled
-    s->release_upstream(it->second);
-    s->inflight_.erase(it);
-    if (s->stopped_) return;
-    if (!err.empty()) {
-      if (before_head) {
-        LOG_ERROR(kT, "upstream request failed: %s", err.c_str());
-        metrics::counter_add("tunnel_upstream_errors_total");
-        s->send_simple_response(sid, 502, "Bad Gateway: " + err);
-        return;
-      }
-      LOG_ERROR(kT, "upstream stream error for stream %u: %s", sid, err.c_str());
-      s->sched_->send(proto::make_error(sid, "upstream error: " + err));
-    }
-    s->sched_->send(proto::make_empty(proto::MsgType::ResEnd, sid));
-    trace::event("serve", sid, "res_end");
-    LOG_DEBUG(kT, "response %u complete", sid);
-  };
   Inflight fl;
   fl.up = up;
+  fl.thread = place_->pick();
   inflight_[sid] = fl;
   outstanding_[up]++;
-  auto call = client_.request(std::move(req), std::move(cb));
-  auto it = inflight_.find(sid);
-  if (it != inflight_.end()) {
-    it->second.call = call;
-    if (upstream_paused_) call->pause();
+  command(fl.thread, std::move(c));
+}
+
+void ServeSession::on_event(Ev& ev) {
+  if (stopped_) return;
+  auto it = inflight_.find(ev.sid);
+  if (it == inflight_.end()) return;  // cancelled: drop its late frames
+  if (ev.kind == Ev::Done) {
+    release_upstream(it->second);
+    place_->release(it->second.thread);
+    inflight_.erase(it);
+    paused_.erase(ev.sid);
+    return;
+  }
+  bool body = ev.frame.type == proto::MsgType::ResBody;
+  sched_->send(std::move(ev.frame));
+  if (!body || it->second.paused) return;
+  // Per-stream back-pressure: only the stream whose frames pile up stops
+  // reading its upstream; a congested channel (over the global high water)
+  // also pauses every stream that has a backlog, but never an interactive
+  // (SSE-like) one with nothing queued.
+  size_t q = sched_->stream_queued(ev.sid);
+  if (q > cfg_.stream_budget || (q > FrameScheduler::kInteractive && sched_->over_high())) {
+    it->second.paused = true;
+    paused_.insert(ev.sid);
+    metrics::counter_add("tunnel_stream_pauses_total");
+    command(it->second.thread, Cmd{Cmd::Pause, ev.sid});
   }
 }
 
-void ServeSession::on_backpressure_relief() {
-  if (!upstream_paused_) return;
-  upstream_paused_ = false;
-  for (auto& kv : inflight_)
-    if (kv.second.call) kv.second.call->resume();
+void ServeSession::check_paused() {
+  if (paused_.empty() || stopped_ || sched_->over_high()) return;
+  for (auto p = paused_.begin(); p != paused_.end();) {
+    uint32_t sid = *p;
+    auto it = inflight_.find(sid);
+    if (it == inflight_.end()) {
+      p = paused_.erase(p);
+      continue;
+    }
+    if (sched_->stream_queued(sid) <= cfg_.stream_budget / 4) {
+      it->second.paused = false;
+      p = paused_.erase(p);
+      command(it->second.thread, Cmd{Cmd::Resume, sid});
+      continue;
+    }
+    ++p;
+  }
 }
 
 }  // namespace p2pt

@@ -11,21 +11,29 @@
 //   - mid-stream upstream failure -> ERROR "upstream error: ..." + END    (:278-290)
 // Local robustness fixes (wire-compatible): malformed
 // REQ_HEADERS (Q3) and unparseable methods (Q4) answer 400 instead of killing
-// the session / hanging the client; back-pressure pauses upstream reads
-// while the channel is congested (Q11); a negotiated CANCEL aborts the
-// upstream request (Q12).
+// the session / hanging the client; a stream whose frames queue up beyond its
+// budget has just its own upstream read paused (Q11); a negotiated CANCEL
+// aborts the upstream request (Q12).
+//
+// Threads (tunnel/workers.h): the session, frame scheduler and stream table
+// live on the association thread; each upstream call runs on one reactor —
+// the association thread's own for the first `inline_streams` concurrent
+// requests, a worker's beyond that (the reference's task per request,
+// serve.rs:131-137).
 #pragma once
 
 #include <functional>
 #include <memory>
 #include <string>
-#include <vector>
 #include <unordered_map>
+#include <unordered_set>
+#include <vector>
 
 #include "http/client.h"
 #include "proto/frame.h"
 #include "tunnel/channel.h"
 #include "tunnel/scheduler.h"
+#include "tunnel/workers.h"
 
 namespace p2pt {
 
@@ -38,25 +46,49 @@ struct ServeConfig {
   uint64_t handshake_timeout_ms = 300000;
   uint64_t ping_interval_ms = 10000;
   uint64_t pong_timeout_ms = 0;  // 0 = reference behaviour (PONG only logged)
-  size_t high_water = 4 << 20;
+  size_t high_water = 4 << 20;   // all streams: above this, backlogged streams pause
   size_t low_water = 1 << 20;
+  size_t stream_budget = 256 << 10;  // one stream's queued bytes before its upstream read pauses
   // Spare pre-connected upstream sockets (0 = connect per request like reqwest).
   size_t upstream_prewarm = 4;
   uint64_t upstream_prewarm_ttl_ms = 1000;  // close unused warm sockets after this idle time
   // Pre-shared secret ("psk" extension, --secret): when set, a HELLO without a
   // valid proof ends the session; empty = room name only (reference).
   std::string secret;
+  // Concurrent upstream calls kept on the association thread before new ones
+  // go to worker threads (see tunnel/workers.h).
+  size_t inline_streams = 16;
 };
+
+class ServeWorker;
 
 class ServeSession : public std::enable_shared_from_this<ServeSession> {
  public:
   // `done` fires once with the reason the session ended (always an error:
-  // like the reference, a session only ends on failure).
+  // like the reference, a session only ends on failure). `pool` (may be null)
+  // supplies the worker threads.
   static std::shared_ptr<ServeSession> start(Reactor& r, std::shared_ptr<MessageChannel> ch, ServeConfig cfg,
-                                             std::function<void(const std::string&)> done);
+                                             std::function<void(const std::string&)> done,
+                                             WorkerPool* pool = nullptr);
   ~ServeSession();
   void stop(const std::string& why);
   size_t active_streams() const { return streams_.size() + inflight_.size(); }
+
+  // Association thread -> the reactor running a call.
+  struct Cmd {
+    enum Kind : uint8_t { Start, Cancel, Pause, Resume, Prewarm } kind;
+    explicit Cmd(Kind k, uint32_t s = 0) : kind(k), sid(s) {}
+    uint32_t sid = 0;
+    http::ClientRequest req;  // Start
+    size_t body_chunk = 0;    // Start: RES_BODY payload size for this channel
+  };
+  // A call's reactor -> association thread.
+  struct Ev {
+    enum Kind : uint8_t { Frame, Done } kind;
+    explicit Ev(Kind k, uint32_t s = 0) : kind(k), sid(s) {}
+    uint32_t sid = 0;
+    proto::Frame frame{proto::MsgType::Ping, 0, Bytes()};
+  };
 
  private:
   struct Pending {
@@ -65,9 +97,14 @@ class ServeSession : public std::enable_shared_from_this<ServeSession> {
     uint64_t body_len = 0;
   };
   struct Inflight {
-    std::shared_ptr<http::ClientCall> call;
-    bool cancelled = false;
-    size_t up = 0;  // index into upstreams_
+    size_t up = 0;      // index into upstreams_
+    size_t thread = 0;  // index into links_
+    bool paused = false;
+  };
+  struct Link {
+    Reactor* r = nullptr;
+    std::unique_ptr<Pipe<Cmd>> to;
+    std::shared_ptr<ServeWorker> worker;  // owned here; released on its own thread
   };
   size_t pick_upstream();
   void release_upstream(const Inflight& f) {
@@ -75,6 +112,8 @@ class ServeSession : public std::enable_shared_from_this<ServeSession> {
   }
 
   ServeSession(Reactor& r, std::shared_ptr<MessageChannel> ch, ServeConfig cfg);
+  void init_links(WorkerPool* pool);
+  void release_links();
   void on_open();
   void on_message(Bytes raw);
   void on_hello(const proto::Frame& f);
@@ -82,14 +121,15 @@ class ServeSession : public std::enable_shared_from_this<ServeSession> {
   void start_request(uint32_t sid, Pending p);
   void send_simple_response(uint32_t sid, uint16_t status, const std::string& body);
   void send_ping();
-  void on_backpressure_relief();
+  void on_event(Ev& ev);
+  void check_paused();
+  void command(size_t thread, Cmd c) { links_[thread].to->push(std::move(c)); }
 
   Reactor& r_;
   std::shared_ptr<MessageChannel> ch_;
   std::unique_ptr<FrameScheduler> sched_;
   ServeConfig cfg_;
   std::function<void(const std::string&)> done_;
-  http::HttpClient client_;
   bool handshaken_ = false;
   bool stopped_ = false;
   bool cancel_feature_ = false;
@@ -98,10 +138,13 @@ class ServeSession : public std::enable_shared_from_this<ServeSession> {
   uint64_t last_pong_ms_ = 0;
   std::unordered_map<uint32_t, Pending> streams_;
   std::unordered_map<uint32_t, Inflight> inflight_;
-  bool upstream_paused_ = false;
+  std::unordered_set<uint32_t> paused_;
   std::vector<std::string> upstreams_;
   std::vector<size_t> outstanding_;
   size_t rr_ = 0;
+  std::vector<Link> links_;
+  std::unique_ptr<Placement> place_;
+  friend class ServeWorker;
 };
 
 }  // namespace p2pt

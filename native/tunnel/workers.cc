@@ -1,0 +1,64 @@
+#include "tunnel/workers.h"
+
+#include <pthread.h>
+#include <signal.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <future>
+
+#include "core/profiler.h"
+
+namespace p2pt {
+
+WorkerThread::WorkerThread(int index) : index_(index) {
+  std::promise<Reactor*> ready;
+  auto fut = ready.get_future();
+  // The reactor is created on its own thread so thread-affine state (the
+  // thread_local current reactor) belongs to that thread.
+  th_ = std::thread([this, &ready] {
+    // Process signals (Ctrl-C, SIGTERM) belong to the main reactor's signalfd;
+    // a worker must never take them with the default action. SIGPROF stays
+    // open so the sampling profiler sees worker time too.
+    sigset_t mask;
+    sigemptyset(&mask);
+    for (int sig : {SIGINT, SIGTERM, SIGHUP, SIGQUIT, SIGUSR1, SIGUSR2, SIGPIPE}) sigaddset(&mask, sig);
+    pthread_sigmask(SIG_BLOCK, &mask, nullptr);
+    auto r = std::make_unique<Reactor>();
+    Reactor* rp = r.get();
+    r_ = std::move(r);
+    char name[16];
+    snprintf(name, sizeof name, "p2pt-w%d", index_);
+    pthread_setname_np(pthread_self(), name);
+    profiler::register_thread(index_);
+    ready.set_value(rp);
+    rp->run();
+  });
+  fut.get();
+}
+
+WorkerThread::~WorkerThread() {
+  Reactor* r = r_.get();
+  r->post_threadsafe([r] { r->stop(); });
+  th_.join();
+  // Work posted by sessions torn down in the meantime (their last references
+  // to worker-side state) still has to run: drain it here.
+  r_->run_until([] { return false; }, 20);
+}
+
+int WorkerPool::auto_count() {
+  long n = sysconf(_SC_NPROCESSORS_ONLN);
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
+  return int(std::clamp<long>(n - 1, 0, 8));
+}
+
+WorkerPool::WorkerPool(int n) {
+  if (n < 0) n = auto_count();
+  for (int i = 0; i < n; i++) threads_.push_back(std::make_unique<WorkerThread>(i + 1));
+}
+
+WorkerPool::~WorkerPool() = default;
+
+}  // namespace p2pt

@@ -1,0 +1,156 @@
+// Worker threads for the tunnel roles.
+//
+// The reference runs on tokio's multi-threaded runtime and spawns a task per
+// request (reference tunnel/src/main.rs:18, serve.rs:131-137, proxy.rs:196-217),
+// so HTTP parsing and socket I/O for many streams spread over all cores. Here
+// the association thread owns the one thing that must stay ordered — the data
+// channel (ICE/DTLS/SCTP, the frame scheduler, the stream table) — and the
+// per-stream HTTP work (upstream calls on serve, client connections on proxy:
+// one read or write syscall per SSE token) runs on worker reactors:
+//
+//   serve:  channel -> [assoc] --Start/Cancel/Pause--> [worker k] -> upstream
+//           upstream -> [worker k] --frames (RES_*), Done--> [assoc] -> channel
+//   proxy:  client -> [worker k] --Route, frames (REQ_*)--> [assoc] -> channel
+//           channel -> [assoc] --RES_* by stream id--> [worker k] -> client
+//
+// Streams start on the association thread itself (no hand-off latency) and
+// only spill onto workers once more than `inline_streams` are active, so low
+// concurrency keeps the single-thread TTFT and node-scale load uses the cores.
+//
+// Threads talk through Pipe<M>: an ordered queue from one reactor's thread to
+// another's, batched per event-loop iteration (one lock + one eventfd write per
+// batch, whatever the number of frames). Frame payloads are refcounted Bytes
+// views, so crossing a thread never copies a body.
+#pragma once
+
+#include <atomic>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "core/reactor.h"
+
+namespace p2pt {
+
+// A Reactor running on its own thread until destroyed.
+class WorkerThread {
+ public:
+  explicit WorkerThread(int index);
+  ~WorkerThread();
+  Reactor& reactor() { return *r_; }
+  int index() const { return index_; }
+
+ private:
+  int index_;
+  std::unique_ptr<Reactor> r_;
+  std::thread th_;
+};
+
+// The process's worker threads; they outlive sessions (reconnects reuse them).
+class WorkerPool {
+ public:
+  // n < 0: one per CPU beyond the first, at most 8.
+  explicit WorkerPool(int n);
+  ~WorkerPool();
+  size_t size() const { return threads_.size(); }
+  Reactor& reactor(size_t i) { return threads_[i]->reactor(); }
+  static int auto_count();
+
+ private:
+  std::vector<std::unique_ptr<WorkerThread>> threads_;
+};
+
+// Ordered, batched messages from the thread of `src` to the thread of `dst`.
+// push() runs on src's thread; the sink runs on dst's thread, once per message,
+// in push order. When src == dst the sink runs synchronously inside push().
+// The Pipe itself must be destroyed on src's thread (it owns a flush hook
+// there); messages still queued are delivered unless the pipe was close()d.
+template <class M>
+class Pipe {
+ public:
+  using Sink = std::function<void(M&)>;
+  Pipe(Reactor& src, Reactor& dst, Sink sink)
+      : src_(src), dst_(dst), state_(std::make_shared<State>()) {
+    state_->sink = std::move(sink);
+    if (&src != &dst) {
+      std::weak_ptr<State> w = state_;
+      Reactor* d = &dst_;
+      hook_ = src_.add_flush_hook([w, d] {
+        auto st = w.lock();
+        if (!st || st->buf.empty()) return;
+        auto batch = std::make_shared<std::vector<M>>(std::move(st->buf));
+        st->buf.clear();
+        st->buf.reserve(batch->size());
+        d->post_threadsafe([st, batch] {
+          if (st->closed) return;
+          for (auto& m : *batch) st->sink(m);
+        });
+      });
+    }
+  }
+  ~Pipe() {
+    if (hook_) src_.remove_flush_hook(hook_);
+  }
+  Pipe(const Pipe&) = delete;
+  Pipe& operator=(const Pipe&) = delete;
+
+  void push(M m) {
+    if (state_->closed) return;
+    if (!hook_) {
+      state_->sink(m);
+      return;
+    }
+    state_->buf.push_back(std::move(m));
+  }
+  // Stop delivering (also batches already posted). src thread only; the flag
+  // is read on dst's thread, so it is atomic.
+  void close() { state_->closed = true; }
+  bool same_thread() const { return hook_ == 0; }
+  Reactor& dst() const { return dst_; }
+
+ private:
+  struct State {
+    Sink sink;
+    std::vector<M> buf;  // src thread only
+    std::atomic<bool> closed{false};
+  };
+  Reactor& src_;
+  Reactor& dst_;
+  std::shared_ptr<State> state_;
+  uint64_t hook_ = 0;
+};
+
+// Picks the thread for a new stream/connection: the association thread
+// (index 0) while fewer than `inline_max` are active there, otherwise the
+// least-loaded worker (ties round-robin).
+class Placement {
+ public:
+  Placement(size_t threads, size_t inline_max) : active_(threads, 0), inline_max_(inline_max) {}
+  size_t pick() {
+    size_t n = active_.size(), best = 0;
+    if (n > 1 && active_[0] >= inline_max_) {
+      best = 1 + rr_ % (n - 1);
+      for (size_t k = 0; k + 1 < n; k++) {
+        size_t i = 1 + (rr_ + k) % (n - 1);
+        if (active_[i] < active_[best]) best = i;
+      }
+      rr_ = best;
+    }
+    active_[best]++;
+    return best;
+  }
+  void release(size_t i) {
+    if (i < active_.size() && active_[i]) active_[i]--;
+  }
+  size_t active(size_t i) const { return active_[i]; }
+  size_t threads() const { return active_.size(); }
+
+ private:
+  std::vector<size_t> active_;
+  size_t inline_max_;
+  size_t rr_ = 0;
+};
+
+}  // namespace p2pt

@@ -56,7 +56,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dump")
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--thread", default=None,
+                    help="only samples of this thread tag (0 = main reactor, k = worker k; 'workers' = all k > 0)")
     a = ap.parse_args()
+    per_thread = collections.Counter()
     stacks = []
     header = ""
     for line in open(a.dump):
@@ -65,6 +68,13 @@ def main():
             continue
         parts = line.split()
         cnt = int(parts[0])
+        tag = 0
+        if len(parts) > 1 and parts[1].startswith("T") and "+" not in parts[1]:
+            tag = int(parts[1][1:])
+            parts = [parts[0]] + parts[2:]
+        per_thread[tag] += cnt
+        if a.thread is not None and not (a.thread == "workers" and tag > 0) and a.thread != str(tag):
+            continue
         frames = []
         for i, tok in enumerate(parts[1:]):
             mod, off = tok.rsplit("+", 1)
@@ -93,6 +103,10 @@ def main():
         if len(fr) > 1:
             leaf_caller[(leaf, names[fr[1]])] += cnt
     print(header)
+    allt = sum(per_thread.values()) or 1
+    print("threads (samples %): " + ", ".join(f"T{t} {100 * c / allt:.1f}" for t, c in sorted(per_thread.items())))
+    if a.thread is not None:
+        print(f"(tables below: thread {a.thread} only)")
     print(f"\n{'self %':>7}  function")
     for n, c in self_t.most_common(a.top):
         print(f"{100 * c / total:7.2f}  {n}")
