@@ -39,7 +39,9 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--mb", type=int, default=1)
     ap.add_argument("--profile-dir", default=None)
+    ap.add_argument("--extra", default="", help="extra flags for both tunnel processes, e.g. --no-jumbo-loopback")
     a = ap.parse_args()
+    extra = [x for x in a.extra.split() if x]
     env = None
     if a.profile_dir:
         os.makedirs(a.profile_dir, exist_ok=True)
@@ -50,8 +52,8 @@ def main():
     out = {}
     try:
         with Tunnel(f"http://127.0.0.1:{port}", transport=a.transport, env=env,
-                    serve_extra=["--metrics-listen", f"127.0.0.1:{ms}"],
-                    proxy_extra=["--metrics-listen", f"127.0.0.1:{mp}"]) as t:
+                    serve_extra=["--metrics-listen", f"127.0.0.1:{ms}"] + extra,
+                    proxy_extra=["--metrics-listen", f"127.0.0.1:{mp}"] + extra) as t:
             def run(target):
                 r = subprocess.run([binary("tunnel-loadgen"), "--target", f"127.0.0.1:{target}", "--streams",
                                     str(a.streams), "--steps", str(a.steps), "--warmup", "1", "--post-bytes",
@@ -64,7 +66,8 @@ def main():
             wall = time.time() - t0
             c1 = {k: cpu_s(v) for k, v in pids.items()}
             dr = run(port)
-            out = {"transport": a.transport, "streams": a.streams, "body_mb": a.mb, "steps": a.steps,
+            out = {"transport": a.transport, "extra": a.extra, "path": t.serve.wait_for("connection established", 1)
+                   .split(" via ", 1)[-1] if a.transport == "webrtc" else "", "streams": a.streams, "body_mb": a.mb, "steps": a.steps,
                    "tunneled_req_s": tr["req_s"], "direct_req_s": dr["req_s"],
                    "tunneled_MBps_each_way": tr["req_s"] * a.mb * 1.048576, "errors": tr["errors"] + dr["errors"],
                    "wall_s_incl_warmup": round(wall, 3),

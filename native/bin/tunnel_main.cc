@@ -85,7 +85,7 @@ const std::vector<Opt>& ext_opts() {
       {"busy-poll-us", "TUNNEL_BUSY_POLL_US", "0",
        "Keep polling for N us after I/O instead of sleeping (lower per-hop latency, more CPU)"},
       {"workers", "TUNNEL_WORKERS", "auto",
-       "HTTP worker threads beside the association thread (auto: one per spare CPU, max 8; 0: single thread)"},
+       "HTTP worker threads beside the association thread (auto: one per 4 CPUs, 1..4; 0: single thread)"},
       {"inline-streams", "TUNNEL_INLINE_STREAMS", "16",
        "Concurrent streams handled on the association thread before new ones go to workers"},
       {"upstream-prewarm", "TUNNEL_UPSTREAM_PREWARM", "4",

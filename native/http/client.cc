@@ -382,6 +382,7 @@ void ClientCall::start() {
     auto self = w.lock();
     if (!self || self->finished_) return false;
     if (!c) {
+      if (self->cb_.on_connect_failed) self->cb_.on_connect_failed();
       self->finish("error sending request for url (" + self->req_.url + "): " + e);
       return true;
     }
@@ -524,6 +525,7 @@ void ClientCall::on_close(const std::string& err) {
         return;
       }
       if (!c) {
+        if (s->cb_.on_connect_failed) s->cb_.on_connect_failed();
         s->finish("error sending request for url (" + s->req_.url + "): " + e);
         return;
       }

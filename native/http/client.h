@@ -38,6 +38,10 @@ struct ClientCallbacks {
   // err empty => complete body received. `before_head` tells whether any
   // response head had been delivered (502 vs mid-stream ERROR semantics).
   std::function<void(const std::string& err, bool before_head)> on_done;
+  // No TCP (or TLS) connection to the origin could be established: the
+  // request never reached it (fires right before on_done). Safe to retry on
+  // another origin.
+  std::function<void()> on_connect_failed;
 };
 
 class ClientConnPool;

@@ -60,7 +60,7 @@ struct AppConfig {
   uint64_t upstream_prewarm_ttl_ms = 1000;
   uint64_t busy_poll_us = 0;
   // HTTP worker threads next to the association thread (-1 = auto: one per
-  // spare CPU, at most 8; 0 = everything on one reactor thread).
+  // 4 CPUs, 1..4; 0 = everything on one reactor thread).
   int workers = -1;
   // Streams kept on the association thread before new ones go to workers.
   size_t inline_streams = 16;

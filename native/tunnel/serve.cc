@@ -39,7 +39,7 @@ class ServeWorker : public std::enable_shared_from_this<ServeWorker> {
   void handle(ServeSession::Cmd& c) {
     using Cmd = ServeSession::Cmd;
     switch (c.kind) {
-      case Cmd::Start: start(c.sid, std::move(c.req), c.body_chunk); break;
+      case Cmd::Start: start(c.sid, std::move(c.req), c.body_chunk, c.retryable); break;
       case Cmd::Cancel: {
         auto it = calls_.find(c.sid);
         if (it == calls_.end()) break;
@@ -88,10 +88,19 @@ class ServeWorker : public std::enable_shared_from_this<ServeWorker> {
     emit(sid, proto::make_empty(proto::MsgType::ResEnd, sid));
   }
 
-  void start(uint32_t sid, http::ClientRequest req, size_t body_chunk) {
+  void start(uint32_t sid, http::ClientRequest req, size_t body_chunk, bool retryable) {
     if (!inline_) prewarm();  // workers warm their own pools on first use
     std::weak_ptr<ServeWorker> w = shared_from_this();
     http::ClientCallbacks cb;
+    // Unreachable upstream: with other upstreams to try, the request goes back
+    // to the session untouched (it never left this host).
+    std::shared_ptr<ServeSession::Unreachable> back;
+    if (retryable) {
+      back = std::make_shared<ServeSession::Unreachable>();
+      back->req = req;  // header strings + body views: no body copy
+    }
+    auto unreachable = std::make_shared<bool>(false);
+    cb.on_connect_failed = [unreachable] { *unreachable = true; };
     cb.on_sent = [sid](bool) { trace::event("serve", sid, "upstream_sent"); };
     cb.on_head = [w, sid](const http::Head& h) {
       auto s = w.lock();
@@ -119,12 +128,24 @@ class ServeWorker : public std::enable_shared_from_this<ServeWorker> {
       for (size_t off = 0; off < n; off += cs)
         s->emit(sid, proto::make_body(proto::MsgType::ResBody, sid, chunk.slice(off, cs)));
     };
-    cb.on_done = [w, sid](const std::string& err, bool before_head) {
+    cb.on_done = [w, sid, back, unreachable](const std::string& err, bool before_head) {
       auto s = w.lock();
       if (!s) return;
       auto it = s->calls_.find(sid);
       if (it == s->calls_.end()) return;  // cancelled
       s->calls_.erase(it);
+      ServeSession::Ev done(ServeSession::Ev::Done, sid);
+      done.responded = !before_head;
+      if (*unreachable && before_head) {
+        if (back) {  // the session retries elsewhere or answers 502 itself
+          back->err = err;
+          done.unreachable = back;
+          s->out_->push(std::move(done));
+          return;
+        }
+        done.unreachable = std::make_shared<ServeSession::Unreachable>();  // health bookkeeping only
+        done.unreachable->err = err;
+      }
       if (!err.empty() && before_head) {
         LOG_ERROR(kT, "upstream request failed: %s", err.c_str());
         metrics::counter_add("tunnel_upstream_errors_total");
@@ -138,7 +159,6 @@ class ServeWorker : public std::enable_shared_from_this<ServeWorker> {
         trace::event("serve", sid, "res_end");
         LOG_DEBUG(kT, "response %u complete", sid);
       }
-      ServeSession::Ev done{ServeSession::Ev::Done, sid};
       s->out_->push(std::move(done));
     };
     calls_[sid] = nullptr;  // present while the call runs (on_done may fire inside request())
@@ -198,20 +218,21 @@ ServeSession::ServeSession(Reactor& r, std::shared_ptr<MessageChannel> ch, Serve
   for (size_t a = 0; a <= cfg_.upstream.size();) {
     size_t c = cfg_.upstream.find(',', a);
     if (c == std::string::npos) c = cfg_.upstream.size();
-    if (c > a) upstreams_.push_back(cfg_.upstream.substr(a, c - a));
+    if (c > a) ups_.push_back(Upstream{cfg_.upstream.substr(a, c - a)});
     a = c + 1;
   }
-  if (upstreams_.empty()) upstreams_.push_back(cfg_.upstream);
-  outstanding_.assign(upstreams_.size(), 0);
+  if (ups_.empty()) ups_.push_back(Upstream{cfg_.upstream});
 }
 
 void ServeSession::init_links(WorkerPool* pool) {
   size_t n = 1 + (pool ? pool->size() : 0);
   place_ = std::make_unique<Placement>(n, cfg_.inline_streams);
   std::weak_ptr<ServeSession> self = shared_from_this();
+  std::vector<std::string> bases;
+  for (auto& u : ups_) bases.push_back(u.base);
   for (size_t k = 0; k < n; k++) {
     Reactor& wr = k == 0 ? r_ : pool->reactor(k - 1);
-    auto worker = std::make_shared<ServeWorker>(wr, r_, self, cfg_, upstreams_, k == 0);
+    auto worker = std::make_shared<ServeWorker>(wr, r_, self, cfg_, bases, k == 0);
     std::weak_ptr<ServeWorker> ww = worker;
     Link l;
     l.r = &wr;
@@ -261,7 +282,7 @@ void ServeSession::stop(const std::string& why) {
   hello_timer_ = ping_timer_ = 0;
   inflight_.clear();
   paused_.clear();
-  std::fill(outstanding_.begin(), outstanding_.end(), 0);
+  for (auto& u : ups_) u.outstanding = 0;
   streams_.clear();
   release_links();
   auto done = std::move(done_);
@@ -453,14 +474,40 @@ static bool valid_method(const std::string& m) {
   return true;
 }
 
-size_t ServeSession::pick_upstream() {
-  size_t n = upstreams_.size(), best = rr_ % n;
-  for (size_t k = 1; k < n; k++) {
+// Fewest requests in flight among the healthy upstreams (ties round-robin);
+// when every upstream is ejected, the one whose ejection ends first (a probe).
+size_t ServeSession::pick_upstream(size_t avoid) {
+  size_t n = ups_.size(), best = SIZE_MAX;
+  uint64_t now = Reactor::now_ms();
+  for (size_t k = 0; k < n; k++) {
     size_t i = (rr_ + k) % n;
-    if (outstanding_[i] < outstanding_[best]) best = i;
+    if (i == avoid && n > 1) continue;
+    if (ups_[i].down_until_ms > now) continue;
+    if (best == SIZE_MAX || ups_[i].outstanding < ups_[best].outstanding) best = i;
+  }
+  if (best == SIZE_MAX) {
+    for (size_t i = 0; i < n; i++)
+      if (best == SIZE_MAX || ups_[i].down_until_ms < ups_[best].down_until_ms) best = i;
   }
   rr_ = best + 1;
   return best;
+}
+
+bool ServeSession::any_healthy(size_t except) const {
+  uint64_t now = Reactor::now_ms();
+  for (size_t i = 0; i < ups_.size(); i++)
+    if (i != except && ups_[i].down_until_ms <= now) return true;
+  return false;
+}
+
+void ServeSession::send_start(uint32_t sid, Inflight& fl, http::ClientRequest req) {
+  req.url = proto::build_upstream_url(ups_[fl.up].base, cfg_.advertise, fl.path);
+  Cmd c{Cmd::Start, sid};
+  c.req = std::move(req);
+  c.body_chunk = sched_->body_chunk();
+  c.retryable = ups_.size() > 1 && fl.tries + 1u < ups_.size();
+  ups_[fl.up].outstanding++;
+  command(fl.thread, std::move(c));
 }
 
 void ServeSession::start_request(uint32_t sid, Pending p) {
@@ -473,12 +520,9 @@ void ServeSession::start_request(uint32_t sid, Pending p) {
     LOG_WARN(kT, "stream %u reused while its response is in flight; ignoring the new request", sid);
     return;
   }
-  const size_t up = pick_upstream();
-  Cmd c{Cmd::Start, sid};
-  http::ClientRequest& req = c.req;
+  http::ClientRequest req;
   req.method = p.headers.method;
-  req.url = proto::build_upstream_url(upstreams_[up], cfg_.advertise, p.headers.path);
-  LOG_DEBUG(kT, "forwarding %s %s -> %s", p.headers.method.c_str(), p.headers.path.c_str(), req.url.c_str());
+  LOG_DEBUG(kT, "forwarding %s %s", p.headers.method.c_str(), p.headers.path.c_str());
   bool had_cl = false;
   for (auto& kv : p.headers.headers) {
     const std::string& k = kv.first;
@@ -493,14 +537,12 @@ void ServeSession::start_request(uint32_t sid, Pending p) {
   req.body = std::move(p.body);
   req.body_len = p.body_len;
   req.force_content_length = had_cl;
-  c.body_chunk = sched_->body_chunk();
   metrics::counter_add("tunnel_upstream_requests_total");
-  Inflight fl;
-  fl.up = up;
+  Inflight& fl = inflight_[sid];
+  fl.up = pick_upstream();
   fl.thread = place_->pick();
-  inflight_[sid] = fl;
-  outstanding_[up]++;
-  command(fl.thread, std::move(c));
+  fl.path = std::move(p.headers.path);
+  send_start(sid, fl, std::move(req));
 }
 
 void ServeSession::on_event(Ev& ev) {
@@ -508,8 +550,35 @@ void ServeSession::on_event(Ev& ev) {
   auto it = inflight_.find(ev.sid);
   if (it == inflight_.end()) return;  // cancelled: drop its late frames
   if (ev.kind == Ev::Done) {
-    release_upstream(it->second);
-    place_->release(it->second.thread);
+    Inflight& fl = it->second;
+    release_upstream(fl);
+    Upstream& u = ups_[fl.up];
+    if (ev.unreachable) {
+      u.fails++;
+      uint64_t ms = std::min<uint64_t>(1000ull << std::min<uint32_t>(u.fails - 1, 5), 30000);
+      u.down_until_ms = Reactor::now_ms() + ms;
+      metrics::counter_add("tunnel_upstream_ejections_total");
+      if (ups_.size() > 1)
+        LOG_WARN(kT, "upstream %s unreachable, ejected for %llu ms: %s", u.base.c_str(),
+                 static_cast<unsigned long long>(ms), ev.unreachable->err.c_str());
+      // Never connected, nothing sent: try another healthy upstream.
+      if (!ev.unreachable->req.method.empty() && any_healthy(fl.up)) {
+        fl.tries++;
+        fl.up = pick_upstream(fl.up);
+        metrics::counter_add("tunnel_upstream_retries_total");
+        send_start(ev.sid, fl, std::move(ev.unreachable->req));
+        return;
+      }
+      if (!ev.unreachable->req.method.empty()) {  // handed back, but nowhere left to go
+        LOG_ERROR(kT, "upstream request failed: %s", ev.unreachable->err.c_str());
+        metrics::counter_add("tunnel_upstream_errors_total");
+        send_simple_response(ev.sid, 502, "Bad Gateway: " + ev.unreachable->err);
+      }
+    } else if (ev.responded) {
+      u.fails = 0;
+      u.down_until_ms = 0;
+    }
+    place_->release(fl.thread);
     inflight_.erase(it);
     paused_.erase(ev.sid);
     return;

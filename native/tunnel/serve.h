@@ -81,6 +81,12 @@ class ServeSession : public std::enable_shared_from_this<ServeSession> {
     uint32_t sid = 0;
     http::ClientRequest req;  // Start
     size_t body_chunk = 0;    // Start: RES_BODY payload size for this channel
+    bool retryable = false;   // Start: hand the request back if the upstream is unreachable
+  };
+  // An upstream call that never connected, handed back for another upstream.
+  struct Unreachable {
+    http::ClientRequest req;
+    std::string err;
   };
   // A call's reactor -> association thread.
   struct Ev {
@@ -88,6 +94,8 @@ class ServeSession : public std::enable_shared_from_this<ServeSession> {
     explicit Ev(Kind k, uint32_t s = 0) : kind(k), sid(s) {}
     uint32_t sid = 0;
     proto::Frame frame{proto::MsgType::Ping, 0, Bytes()};
+    bool responded = false;                    // Done: the upstream answered (any status)
+    std::shared_ptr<Unreachable> unreachable;  // Done: no connection, nothing sent yet
   };
 
  private:
@@ -97,19 +105,32 @@ class ServeSession : public std::enable_shared_from_this<ServeSession> {
     uint64_t body_len = 0;
   };
   struct Inflight {
-    size_t up = 0;      // index into upstreams_
+    size_t up = 0;      // index into ups_
     size_t thread = 0;  // index into links_
     bool paused = false;
+    uint8_t tries = 0;  // upstreams tried after connect failures
+    std::string path;   // request path (the URL is rebuilt for another upstream)
+  };
+  // One upstream origin (one inference endpoint, e.g. one per GPU) and its
+  // passive health: an origin that refuses connections is ejected for an
+  // exponentially growing time (1 s .. 30 s) and requests go to the others.
+  struct Upstream {
+    std::string base;
+    size_t outstanding = 0;
+    uint64_t down_until_ms = 0;
+    uint32_t fails = 0;
   };
   struct Link {
     Reactor* r = nullptr;
     std::unique_ptr<Pipe<Cmd>> to;
     std::shared_ptr<ServeWorker> worker;  // owned here; released on its own thread
   };
-  size_t pick_upstream();
+  size_t pick_upstream(size_t avoid = SIZE_MAX);
   void release_upstream(const Inflight& f) {
-    if (f.up < outstanding_.size() && outstanding_[f.up]) outstanding_[f.up]--;
+    if (f.up < ups_.size() && ups_[f.up].outstanding) ups_[f.up].outstanding--;
   }
+  void send_start(uint32_t sid, Inflight& fl, http::ClientRequest req);
+  bool any_healthy(size_t except) const;
 
   ServeSession(Reactor& r, std::shared_ptr<MessageChannel> ch, ServeConfig cfg);
   void init_links(WorkerPool* pool);
@@ -139,8 +160,7 @@ class ServeSession : public std::enable_shared_from_this<ServeSession> {
   std::unordered_map<uint32_t, Pending> streams_;
   std::unordered_map<uint32_t, Inflight> inflight_;
   std::unordered_set<uint32_t> paused_;
-  std::vector<std::string> upstreams_;
-  std::vector<size_t> outstanding_;
+  std::vector<Upstream> ups_;
   size_t rr_ = 0;
   std::vector<Link> links_;
   std::unique_ptr<Placement> place_;

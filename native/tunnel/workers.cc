@@ -47,11 +47,15 @@ WorkerThread::~WorkerThread() {
   r_->run_until([] { return false; }, 20);
 }
 
+// One worker per 4 CPUs the process may use, 1..4: measured on the MI355X
+// host (bench/bench_node.py, profiles/node_r02/), 4 workers carried 1024
+// 1 ms-token streams at direct speed while 8 lost to contention with the
+// association thread, and a single worker already halves the 256-stream TTFT.
 int WorkerPool::auto_count() {
   long n = sysconf(_SC_NPROCESSORS_ONLN);
   cpu_set_t set;
   if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
-  return int(std::clamp<long>(n - 1, 0, 8));
+  return int(std::clamp<long>(n / 4, 1, 4));
 }
 
 WorkerPool::WorkerPool(int n) {

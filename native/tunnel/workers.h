@@ -51,7 +51,7 @@ class WorkerThread {
 // The process's worker threads; they outlive sessions (reconnects reuse them).
 class WorkerPool {
  public:
-  // n < 0: one per CPU beyond the first, at most 8.
+  // n < 0: auto_count().
   explicit WorkerPool(int n);
   ~WorkerPool();
   size_t size() const { return threads_.size(); }
