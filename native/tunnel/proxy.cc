@@ -431,9 +431,11 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     }
     state_ = State::Head;
     req_ = http::Head{};
-    flow_paused_ = false;
-    if (pipelined_hold_) {
+    // A flow pause belonged to the stream that just ended (its Resume may
+    // never come: the session drops a finished stream's pause state).
+    if (pipelined_hold_ || flow_paused_) {
       pipelined_hold_ = false;
+      flow_paused_ = false;
       conn_->resume_reading();
     }
     if (!inbuf_.empty()) {
@@ -584,6 +586,18 @@ std::shared_ptr<ProxySession> ProxySession::start(Reactor& r, std::shared_ptr<Me
   s->sched_->on_progress = [w] {
     if (auto x = w.lock()) x->check_paused();
   };
+  auto gauge = [w](double (*f)(ProxySession&)) {
+    return [w, f]() -> double {
+      auto x = w.lock();
+      return x ? f(*x) : 0.0;
+    };
+  };
+  metrics::gauge_fn("tunnel_streams_inflight", gauge([](ProxySession& x) { return double(x.routes_.size()); }));
+  metrics::gauge_fn("tunnel_streams_paused", gauge([](ProxySession& x) { return double(x.paused_.size()); }));
+  metrics::gauge_fn("tunnel_scheduler_queued_bytes",
+                    gauge([](ProxySession& x) { return double(x.sched_->queued_bytes()); }));
+  metrics::gauge_fn("tunnel_channel_buffered_bytes",
+                    gauge([](ProxySession& x) { return double(x.ch_->buffered_amount()); }));
   if (ch->is_open()) {
     LOG_INFO(kT, "data channel already open");
     s->on_open();

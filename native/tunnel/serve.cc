@@ -200,6 +200,18 @@ std::shared_ptr<ServeSession> ServeSession::start(Reactor& r, std::shared_ptr<Me
   s->sched_->on_progress = [w] {
     if (auto x = w.lock()) x->check_paused();
   };
+  auto gauge = [w](double (*f)(ServeSession&)) {
+    return [w, f]() -> double {
+      auto x = w.lock();
+      return x ? f(*x) : 0.0;
+    };
+  };
+  metrics::gauge_fn("tunnel_streams_inflight", gauge([](ServeSession& x) { return double(x.inflight_.size()); }));
+  metrics::gauge_fn("tunnel_streams_paused", gauge([](ServeSession& x) { return double(x.paused_.size()); }));
+  metrics::gauge_fn("tunnel_scheduler_queued_bytes",
+                    gauge([](ServeSession& x) { return double(x.sched_->queued_bytes()); }));
+  metrics::gauge_fn("tunnel_channel_buffered_bytes",
+                    gauge([](ServeSession& x) { return double(x.ch_->buffered_amount()); }));
   if (ch->is_open()) {
     LOG_INFO(kT, "data channel already open");
     s->on_open();

@@ -38,9 +38,9 @@ def _mocks(n, interval_us=2000, tokens=8, trace=False):
     return ms, ports
 
 
-def _loadgen(port, streams, steps, threads=2):
+def _loadgen(port, streams, steps, threads=2, extra=()):
     out = subprocess.run([binary("tunnel-loadgen"), "--target", f"127.0.0.1:{port}", "--streams", str(streams),
-                          "--steps", str(steps), "--warmup", "0", "--threads", str(threads)],
+                          "--steps", str(steps), "--warmup", "0", "--threads", str(threads), *extra],
                          capture_output=True, text=True, timeout=120)
     return json.loads(out.stdout.strip().splitlines()[-1])
 
@@ -72,6 +72,10 @@ def test_request_paths_on_worker_threads(transport):
             assert r.status == 200 and len(data) == 3000000 and data[:256] == bytes(range(256))
             res = _loadgen(t.proxy_port, 48, 3)
             assert res["errors"] == 0 and res["requests"] == 144 and res["events"] == 144 * 7
+            # back-to-back uploads on keep-alive connections: per-stream upload
+            # pauses must not outlive their stream (a later request would hang)
+            res = _loadgen(t.proxy_port, 32, 4, extra=("--post-bytes", str(1 << 20)))
+            assert res["errors"] == 0 and res["requests"] == 128
     finally:
         for m in ms:
             m.stop()
