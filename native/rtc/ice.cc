@@ -1,5 +1,7 @@
 #include "rtc/ice.h"
 
+#include <netinet/udp.h>
+
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <sys/epoll.h>
@@ -140,6 +142,23 @@ void IceAgent::set_state(IceState s) {
   }
 }
 
+void IceAgent::enable_gro(int fd) {
+  if (getenv("TUNNEL_NO_GRO")) return;
+  int one = 1;
+  if (setsockopt(fd, SOL_UDP, UDP_GRO, &one, sizeof one) == 0) gro_enabled_ = true;
+}
+
+size_t IceAgent::gro_segment(const msghdr* mh) {
+  for (cmsghdr* c = CMSG_FIRSTHDR(const_cast<msghdr*>(mh)); c; c = CMSG_NXTHDR(const_cast<msghdr*>(mh), c)) {
+    if (c->cmsg_level == SOL_UDP && c->cmsg_type == UDP_GRO) {
+      int v = 0;
+      memcpy(&v, CMSG_DATA(c), sizeof v);
+      return v > 0 ? size_t(v) : 0;
+    }
+  }
+  return 0;
+}
+
 void IceAgent::open_sockets() {
   auto addrs = local_addresses(cfg_.include_loopback, cfg_.include_ipv6);
   // Non-loopback first so they get the higher local preference.
@@ -156,6 +175,7 @@ void IceAgent::open_sockets() {
     int buf = 4 << 20;
     setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &buf, sizeof buf);
     setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &buf, sizeof buf);
+    enable_gro(fd);
     SockAddr a = ia.addr;
     a.set_port(0);
     if (::bind(fd, a.sa(), a.len) < 0) {
@@ -554,10 +574,15 @@ void IceAgent::flush() {
     outq_.swap(keep);
     if (outq_.empty()) return;
   }
-  // Group consecutive datagrams by socket for sendmmsg.
-  constexpr int kBatch = 64;
+  // Group consecutive datagrams by socket for sendmmsg; within a group, runs
+  // of equal-size datagrams to one destination become one UDP GSO message
+  // (UDP_SEGMENT): one skb through the stack instead of one per datagram,
+  // delivered whole to a GRO-enabled receiver on the same host. Standard-MTU
+  // bulk traffic is exactly that: full SCTP packets -> equal DTLS records.
+  constexpr int kBatch = 64, kIov = 512;
   mmsghdr msgs[kBatch];
-  iovec iovs[kBatch];
+  iovec iovs[kIov];
+  alignas(cmsghdr) char ctrl[kBatch][CMSG_SPACE(sizeof(uint16_t))];
   size_t i = 0;
   while (i < outq_.size()) {
     // Resolve the socket (relay locals go through TURN).
@@ -569,29 +594,71 @@ void IceAgent::flush() {
     }
     int si = li >= 0 ? locals_[li].sock : (-1 - li);
     int fd = nat_mode_ ? nat_fd_for(si, outq_[i].to) : socks_[si].fd;
-    int cnt = 0;
+    int cnt = 0, niov = 0;
     size_t j = i;
-    while (j < outq_.size() && cnt < kBatch) {
+    while (j < outq_.size() && cnt < kBatch && niov < kIov) {
       int lj = outq_[j].local;
       if (lj >= 0 && locals_[lj].relay) break;
       int sj = lj >= 0 ? locals_[lj].sock : (-1 - lj);
       if (sj != si) break;
       if (nat_mode_ && nat_fd_for(sj, outq_[j].to) != fd) break;
-      memset(&msgs[cnt], 0, sizeof msgs[cnt]);
-      iovs[cnt].iov_base = outq_[j].data.data();
-      iovs[cnt].iov_len = outq_[j].data.size();
-      msgs[cnt].msg_hdr.msg_iov = &iovs[cnt];
-      msgs[cnt].msg_hdr.msg_iovlen = 1;
-      msgs[cnt].msg_hdr.msg_name = const_cast<sockaddr*>(outq_[j].to.sa());
-      msgs[cnt].msg_hdr.msg_namelen = outq_[j].to.len;
+      // One message: datagram j plus following ones of the same size to the
+      // same address (the run's last datagram may be shorter).
+      size_t seg = outq_[j].data.size();
+      int first = niov;
+      size_t total = 0;
+      size_t k = j;
+      while (k < outq_.size() && niov < kIov) {
+        const Out& o = outq_[k];
+        if (k > j) {
+          if (!gso_ok_ || o.local != outq_[j].local || o.to != outq_[j].to || o.data.size() > seg) break;
+          if (niov - first >= kGsoMaxSegs || total + o.data.size() > kGsoMaxBytes) break;
+        }
+        iovs[niov].iov_base = const_cast<uint8_t*>(o.data.data());
+        iovs[niov].iov_len = o.data.size();
+        niov++;
+        total += o.data.size();
+        k++;
+        if (o.data.size() < seg) break;  // a short datagram ends the run
+      }
+      mmsghdr& m = msgs[cnt];
+      memset(&m, 0, sizeof m);
+      m.msg_hdr.msg_iov = &iovs[first];
+      m.msg_hdr.msg_iovlen = size_t(niov - first);
+      m.msg_hdr.msg_name = const_cast<sockaddr*>(outq_[j].to.sa());
+      m.msg_hdr.msg_namelen = outq_[j].to.len;
+      if (niov - first > 1) {
+        m.msg_hdr.msg_control = ctrl[cnt];
+        m.msg_hdr.msg_controllen = sizeof ctrl[cnt];
+        cmsghdr* c = CMSG_FIRSTHDR(&m.msg_hdr);
+        c->cmsg_level = SOL_UDP;
+        c->cmsg_type = UDP_SEGMENT;
+        c->cmsg_len = CMSG_LEN(sizeof(uint16_t));
+        uint16_t gs = uint16_t(seg);
+        memcpy(CMSG_DATA(c), &gs, sizeof gs);
+        gso_sends_++;
+      }
       cnt++;
-      j++;
+      j = k;
     }
     int sent = 0;
     while (sent < cnt) {
       int rc = sendmmsg(fd, msgs + sent, unsigned(cnt - sent), 0);
       if (rc < 0) {
         if (errno == EINTR) continue;
+        if ((errno == EIO || errno == EINVAL || errno == ENOPROTOOPT) && gso_ok_ &&
+            msgs[sent].msg_hdr.msg_controllen) {
+          // No UDP GSO here (old kernel, device without it): send this
+          // message's datagrams one by one and stop using GSO.
+          LOG_DEBUG(kT, "UDP GSO unavailable (%s); sending datagrams individually", strerror(errno));
+          gso_ok_ = false;
+          mmsghdr& m = msgs[sent];
+          for (size_t q = 0; q < m.msg_hdr.msg_iovlen; q++)
+            sendto(fd, m.msg_hdr.msg_iov[q].iov_base, m.msg_hdr.msg_iov[q].iov_len, 0,
+                   static_cast<const sockaddr*>(m.msg_hdr.msg_name), m.msg_hdr.msg_namelen);
+          sent++;
+          continue;
+        }
         // EAGAIN (socket buffer full) or unreachable: drop; SCTP retransmits.
         if (errno != EAGAIN) LOG_TRACE(kT, "sendmmsg: %s", strerror(errno));
         break;
@@ -615,6 +682,7 @@ void IceAgent::on_readable(int si) {
   mmsghdr msgs[kBatch];
   iovec iovs[kBatch];
   sockaddr_storage from[kBatch];
+  alignas(cmsghdr) char ctrl[kBatch][CMSG_SPACE(sizeof(int))];
   for (int round = 0; round < 8 && !closed_; round++) {
     for (int i = 0; i < kBatch; i++) rxpool_[i].reset();
     for (int i = 0; i < kBatch; i++) {
@@ -629,6 +697,8 @@ void IceAgent::on_readable(int si) {
       msgs[i].msg_hdr.msg_iovlen = 1;
       msgs[i].msg_hdr.msg_name = &from[i];
       msgs[i].msg_hdr.msg_namelen = sizeof from[i];
+      msgs[i].msg_hdr.msg_control = ctrl[i];
+      msgs[i].msg_hdr.msg_controllen = sizeof ctrl[i];
     }
     int n = recvmmsg(socks_[si].fd, msgs, kBatch, MSG_DONTWAIT, nullptr);
     if (n <= 0) return;
@@ -640,19 +710,31 @@ void IceAgent::on_readable(int si) {
       SockAddr a;
       memcpy(&a.ss, &from[i], msgs[i].msg_hdr.msg_namelen);
       a.len = msgs[i].msg_hdr.msg_namelen;
-      dispatch_rx(si, a, rxpool_[i], msgs[i].msg_len);
+      dispatch_segments(si, a, rxpool_[i], msgs[i].msg_len, gro_segment(&msgs[i].msg_hdr));
     }
     if (n < kBatch) return;
   }
 }
 
-void IceAgent::dispatch_rx(int si, const SockAddr& a, const RawBufPtr& owner, size_t len) {
-  const uint8_t* p = owner->data.get();
+void IceAgent::dispatch_rx(int si, const SockAddr& a, const RawBufPtr& owner, size_t len, size_t off) {
+  const uint8_t* p = owner->data.get() + off;
   if (turn_ && turn_->is_server(si, a)) {
     turn_->on_packet(p, len);
     return;
   }
   handle_datagram(-1, si, a, p, len, false, owner);
+}
+
+// A GRO-coalesced receive holds several datagrams of `seg` bytes back to back
+// (the last may be shorter); each is its own DTLS datagram. Zero-copy: every
+// segment is handed up as a view of the same pooled buffer.
+void IceAgent::dispatch_segments(int si, const SockAddr& a, const RawBufPtr& owner, size_t len, size_t seg) {
+  if (!seg || seg >= len) {
+    dispatch_rx(si, a, owner, len, 0);
+    return;
+  }
+  gro_batches_++;
+  for (size_t off = 0; off < len && !closed_; off += seg) dispatch_rx(si, a, owner, std::min(seg, len - off), off);
 }
 
 int IceAgent::nat_fd_for(int si, const SockAddr& to) {
@@ -670,7 +752,7 @@ int IceAgent::nat_fd_for(int si, const SockAddr& to) {
     a.set_port(0);
     int buf = 4 << 20;
     setsockopt(np.fd, SOL_SOCKET, SO_RCVBUF, &buf, sizeof buf);
-    setsockopt(np.fd, SOL_SOCKET, SO_SNDBUF, &buf, sizeof buf);
+    setsockopt(np.fd, SOL_SOCKET, SO_SNDBUF, &buf, sizeof buf);  // no GRO: read with plain recvfrom
     if (np.fd < 0 || ::bind(np.fd, a.sa(), a.len) < 0) return socks_[si].fd;
     np.ext.len = sizeof np.ext.ss;
     getsockname(np.fd, np.ext.sa(), &np.ext.len);
@@ -724,8 +806,8 @@ void IceAgent::handle_datagram(int, int si, const SockAddr& from, const uint8_t*
     }
   }
   if (!on_data) return;
-  if (owner && p == owner->data.get()) {
-    on_data(owner, owner->data.get(), n);
+  if (owner && p >= owner->data.get() && p + n <= owner->data.get() + owner->cap) {
+    on_data(owner, owner->data.get() + (p - owner->data.get()), n);
   } else {  // relayed (inside a TURN message): private copy
     auto b = std::make_shared<RawBuf>(n ? n : 1);
     memcpy(b->data.get(), p, n);

@@ -160,7 +160,10 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   IceAgent(Reactor& r, IceConfig cfg, bool controlling);
   void open_sockets();
   void on_readable(int si);
-  void dispatch_rx(int si, const SockAddr& from, const RawBufPtr& owner, size_t len);
+  void dispatch_rx(int si, const SockAddr& from, const RawBufPtr& owner, size_t len, size_t off = 0);
+  void dispatch_segments(int si, const SockAddr& from, const RawBufPtr& owner, size_t len, size_t seg);
+  void enable_gro(int fd);
+  static size_t gro_segment(const struct msghdr* mh);
   // Test-only NAT emulation (TUNNEL_NAT=port-restricted|symmetric; SURVEY
   // §4.2, BASELINE config #4 without two real NATs). Every datagram leaves
   // through an emulated external socket: one per host socket (endpoint-
@@ -255,6 +258,15 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   size_t append_at_ = 0;
   std::vector<RawBufPtr> rxpool_;   // recvmmsg slots, filled from rxbufs_ each round
   BufPool rxbufs_{65536};
+  // UDP GSO/GRO (Linux): runs of equal-size datagrams leave as one message and
+  // arrive coalesced. Falls back to one datagram per send if the kernel refuses.
+  static constexpr int kGsoMaxSegs = 64;
+  static constexpr size_t kGsoMaxBytes = 60000;
+  bool gso_ok_ = getenv("TUNNEL_NO_GSO") == nullptr;
+  bool gro_enabled_ = false;
+ public:
+  uint64_t gso_sends_ = 0, gro_batches_ = 0;  // counters (metrics, tests)
+ private:
   DgVec drop_;                      // reserve_append target with no path
   friend class TurnClient;
 };

@@ -371,6 +371,18 @@ void PeerConnection::start_sctp() {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().retransmits) : 0.0;
   });
+  metrics::gauge_fn("tunnel_sctp_packets_sent", [w] {
+    auto s = w.lock();
+    return s && s->sctp_ ? double(s->sctp_->stats().packets_sent) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_udp_gso_sends", [w] {
+    auto s = w.lock();
+    return s && s->ice_ ? double(s->ice_->gso_sends_) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_udp_gro_batches", [w] {
+    auto s = w.lock();
+    return s && s->ice_ ? double(s->ice_->gro_batches_) : 0.0;
+  });
   set_state(PcState::Connected);
   sctp_->connect();
 }

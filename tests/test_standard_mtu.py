@@ -1,0 +1,46 @@
+"""The standard 1200-byte SCTP path (what every cross-host WebRTC peer uses,
+reference rtc.rs:31-72 via webrtc-rs defaults), forced on loopback with
+--no-jumbo-loopback: bulk bodies and SSE stay correct with UDP GSO/GRO on
+(runs of equal-size DTLS datagrams leave as one message and arrive
+coalesced) and with both switched off (TUNNEL_NO_GSO / TUNNEL_NO_GRO)."""
+import http.client
+import json
+import urllib.request
+
+import pytest
+
+from p2p_llm_tunnel_amd.utils.procs import Tunnel, free_port
+
+STD = ["--no-jumbo-loopback"]
+
+
+def _metrics(port):
+    txt = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5).read().decode()
+    return {l.split()[0]: float(l.split()[1]) for l in txt.splitlines() if l and not l.startswith("#")}
+
+
+@pytest.mark.parametrize("offload", [True, False])
+def test_standard_mtu_bulk_and_sse(mock_upstream, offload):
+    ms, mp = free_port(), free_port()
+    env = None if offload else {"TUNNEL_NO_GSO": "1", "TUNNEL_NO_GRO": "1"}
+    with Tunnel(mock_upstream, transport="webrtc", env=env,
+                serve_extra=STD + ["--metrics-listen", f"127.0.0.1:{ms}"],
+                proxy_extra=STD + ["--metrics-listen", f"127.0.0.1:{mp}"]) as t:
+        assert "mtu=1200" in t.serve.wait_for("connection established", 5)
+        c = http.client.HTTPConnection("127.0.0.1", t.proxy_port, timeout=60)
+        body = bytes((i * 7 + 3) & 0xFF for i in range(3 * 1024 * 1024 + 17))
+        for _ in range(2):
+            c.request("POST", "/echo", body=body)
+            r = c.getresponse()
+            assert r.status == 200 and r.read() == body
+        c.request("POST", "/v1/chat/completions", body=json.dumps({"stream": True}))
+        r = c.getresponse()
+        assert r.status == 200 and r.read().count(b"data: ") == 7
+        sm, pm = _metrics(ms), _metrics(mp)
+        if offload:
+            # the echoed bodies left as GSO runs and arrived GRO-coalesced
+            assert sm["tunnel_udp_gso_sends"] > 0 and pm["tunnel_udp_gso_sends"] > 0
+            assert sm["tunnel_udp_gro_batches"] > 0 and pm["tunnel_udp_gro_batches"] > 0
+        else:
+            assert sm["tunnel_udp_gso_sends"] == 0 and sm["tunnel_udp_gro_batches"] == 0
+        assert sm["tunnel_sctp_packets_sent"] > 2 * len(body) / 1200
