@@ -126,15 +126,57 @@ struct Server {
     auto buf = std::make_shared<std::string>();
     auto done = std::make_shared<bool>(false);
     std::weak_ptr<TcpConn> w = c;
-    c->on_data([this, w, buf, done](const uint8_t* p, size_t n) {
+    // POST /sink: the body is consumed as it arrives (counted and checksummed,
+    // never held), then {"bytes": N, "wsum": S} with S = sum of (i+1)*byte[i]
+    // mod 2^64 (order-sensitive) — for bounded-memory upload tests of
+    // gigabyte bodies.
+    struct Sink {
+      bool on = false;
+      http::BodyDecoder body;
+      uint64_t bytes = 0, wsum = 0;
+      void eat(const uint8_t* d, size_t k) {
+        for (size_t i = 0; i < k; i++) wsum += (bytes + i + 1) * d[i];
+        bytes += k;
+      }
+      std::string json() const {
+        return "{\"bytes\": " + std::to_string(bytes) + ", \"wsum\": " + std::to_string(wsum) + "}";
+      }
+    };
+    auto sink = std::make_shared<Sink>();
+    c->on_data([this, w, buf, done, sink](const uint8_t* p, size_t n) {
       if (*done) return;
+      if (sink->on) {
+        size_t used = sink->body.feed(p, n, [&](const uint8_t* d, size_t k) { sink->eat(d, k); });
+        if (used == SIZE_MAX || sink->body.done()) {
+          *done = true;
+          if (auto s = w.lock()) respond(s, used == SIZE_MAX ? 400 : 200, "application/json", sink->json());
+        }
+        return;
+      }
       buf->append(reinterpret_cast<const char*>(p), n);
       http::Head h;
       size_t used = 0;
       if (http::parse_request_head(*buf, h, used, nullptr) != http::ParseResult::Done) return;
       uint64_t len = 0;
       std::string err;
-      http::request_body_mode(h, len, &err);
+      auto mode = http::request_body_mode(h, len, &err);
+      if (h.method == "POST" && h.target == "/sink") {
+        sink->on = true;
+        sink->body.reset(mode, len);
+        std::string rest = buf->substr(used);
+        buf->clear();
+        if (auto s = w.lock()) {
+          if (rest.empty() && !sink->body.done()) return;
+          // Feed what arrived with the head through the same path.
+          size_t u = sink->body.feed(reinterpret_cast<const uint8_t*>(rest.data()), rest.size(),
+                                     [&](const uint8_t* d, size_t k) { sink->eat(d, k); });
+          if (u == SIZE_MAX || sink->body.done()) {
+            *done = true;
+            respond(s, u == SIZE_MAX ? 400 : 200, "application/json", sink->json());
+          }
+        }
+        return;
+      }
       if (buf->size() - used < len) return;
       *done = true;
       if (trace) fprintf(stderr, "mock_req %llu\n", static_cast<unsigned long long>(Reactor::now_us()));

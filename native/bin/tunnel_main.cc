@@ -88,6 +88,10 @@ const std::vector<Opt>& ext_opts() {
        "HTTP worker threads beside the association thread (auto: one per 4 CPUs, 1..4; 0: single thread)"},
       {"inline-streams", "TUNNEL_INLINE_STREAMS", "16",
        "Concurrent streams handled on the association thread before new ones go to workers"},
+      {"max-request-body", "TUNNEL_MAX_REQUEST_BODY", "0",
+       "serve: answer 413 to request bodies larger than this many bytes (0 = unlimited)"},
+      {"stream-body-threshold", "TUNNEL_STREAM_BODY_THRESHOLD", "8388608",
+       "serve: request bodies this big stream to the upstream as they arrive instead of being buffered"},
       {"upstream-prewarm", "TUNNEL_UPSTREAM_PREWARM", "4",
        "serve: spare pre-connected upstream sockets (follows peak concurrency; 0=off)"},
       {"upstream-prewarm-ttl-ms", "TUNNEL_UPSTREAM_PREWARM_TTL_MS", "1000",
@@ -321,6 +325,8 @@ int main(int argc, char** argv) {
   cfg.busy_poll_us = num(m, "busy-poll-us");
   cfg.workers = m["workers"] == "auto" ? -1 : int(num(m, "workers"));
   cfg.inline_streams = num(m, "inline-streams");
+  cfg.max_request_body = num(m, "max-request-body");
+  cfg.stream_body_threshold = num(m, "stream-body-threshold");
   cfg.secret = m["secret"];
   if (!m["cpu-affinity"].empty()) {
     std::string err;

@@ -367,6 +367,25 @@ void ClientCall::start() {
   pool_key_ = url_.scheme + "://" + url_.host + ":" + std::to_string(url_.port);
   pool_->call_started(pool_key_);
   counted_ = true;
+  chunked_body_ = req_.stream_body && req_.content_length < 0;
+  if (req_.stream_body) {
+    for (auto& b : req_.body) queued_body_ += b.size();
+    std::weak_ptr<ClientCall> w = shared_from_this();
+    TcpConn::connect(*r_, url_.host, url_.port, url_.tls(), [w](std::shared_ptr<TcpConn> c, std::string e) {
+      auto self = w.lock();
+      if (!self || self->finished_) {
+        if (c) c->close();
+        return;
+      }
+      if (!c) {
+        if (self->cb_.on_connect_failed) self->cb_.on_connect_failed();
+        self->finish("error sending request for url (" + self->req_.url + "): " + e);
+        return;
+      }
+      self->attach(c, false);
+    });
+    return;
+  }
   if (auto c = pool_->take(pool_key_)) {
     attach(c, true);
     return;
@@ -422,6 +441,28 @@ void ClientCall::attach(std::shared_ptr<TcpConn> c, bool reused) {
     head += "\r\n";
   }
   if (!has_accept) head += "accept: */*\r\n";
+  if (req_.stream_body) {
+    if (chunked_body_) head += "transfer-encoding: chunked\r\n";
+    else head += "content-length: " + std::to_string(req_.content_length) + "\r\n";
+    head += "\r\n";
+    conn_->write(std::move(head));
+    std::weak_ptr<ClientCall> wd = shared_from_this();
+    conn_->on_drain(
+        [wd] {
+          auto s = wd.lock();
+          if (s && !s->finished_ && s->cb_.on_body_drain) s->cb_.on_body_drain();
+        },
+        cb_.body_low_water);
+    auto pieces = std::move(req_.body);
+    req_.body.clear();
+    queued_body_ = 0;
+    for (auto& b : pieces) write_piece(b);
+    if (body_ended_ && chunked_body_) conn_->write(std::string("0\r\n\r\n"));
+    if (paused_) conn_->pause_reading();
+    if (cb_.on_sent) cb_.on_sent(reused);
+    if (cb_.on_body_drain && conn_->pending_out() <= cb_.body_low_water) cb_.on_body_drain();
+    return;
+  }
   if (req_.body_len > 0 || req_.force_content_length) head += "content-length: " + std::to_string(req_.body_len) + "\r\n";
   head += "\r\n";
   // Small bodies ride in the same segment as the head.
@@ -575,6 +616,37 @@ void ClientCall::finish(const std::string& err) {
   if (cb) cb(err, before_head);
   live_calls().erase(this);
 }
+
+void ClientCall::write_piece(const Bytes& b) {
+  if (b.empty() || !conn_) return;
+  if (chunked_body_) {
+    char h[24];
+    int n = snprintf(h, sizeof h, "%zx\r\n", b.size());
+    conn_->write(slab_copy(h, size_t(n)));
+    conn_->write(b);
+    conn_->write(slab_copy("\r\n", 2));
+  } else {
+    conn_->write(b);
+  }
+}
+
+void ClientCall::write_body(Bytes b) {
+  if (finished_ || body_ended_ || b.empty()) return;
+  if (!conn_) {  // still connecting: queued, written right after the head
+    queued_body_ += b.size();
+    req_.body.push_back(std::move(b));
+    return;
+  }
+  write_piece(b);
+}
+
+void ClientCall::end_body() {
+  if (finished_ || body_ended_) return;
+  body_ended_ = true;
+  if (conn_ && chunked_body_) conn_->write(std::string("0\r\n\r\n"));
+}
+
+size_t ClientCall::body_backlog() const { return conn_ ? conn_->pending_out() : size_t(queued_body_); }
 
 void ClientCall::pause() {
   if (paused_ || finished_) return;

@@ -27,6 +27,12 @@ struct ClientRequest {
   std::vector<Bytes> body;      // gathered, not concatenated
   uint64_t body_len = 0;
   bool force_content_length = false;  // send content-length even when 0
+  // Streamed request body: `body` holds what is known at start, the rest comes
+  // through ClientCall::write_body()/end_body(). Sent with content-length when
+  // `content_length` >= 0, chunked otherwise; always on a fresh connection
+  // (a stale pooled socket could not replay a body that is already gone).
+  bool stream_body = false;
+  int64_t content_length = -1;
 };
 
 struct ClientCallbacks {
@@ -42,6 +48,10 @@ struct ClientCallbacks {
   // request never reached it (fires right before on_done). Safe to retry on
   // another origin.
   std::function<void()> on_connect_failed;
+  // Streamed body: the socket's backlog drained below body_low_water after
+  // having been above it (the producer may send more).
+  std::function<void()> on_body_drain;
+  size_t body_low_water = 64 * 1024;
 };
 
 class ClientConnPool;
@@ -52,6 +62,11 @@ class ClientCall : public std::enable_shared_from_this<ClientCall> {
   void resume();
   void cancel();
   bool finished() const { return finished_; }
+  // Streamed request body (ClientRequest::stream_body).
+  void write_body(Bytes b);
+  void end_body();
+  // Request-body bytes accepted but not yet handed to the kernel.
+  size_t body_backlog() const;
   ~ClientCall();
 
  private:
@@ -77,6 +92,10 @@ class ClientCall : public std::enable_shared_from_this<ClientCall> {
   bool paused_ = false;
   bool keep_alive_ = false;
   bool counted_ = false;
+  bool chunked_body_ = false;
+  bool body_ended_ = false;
+  uint64_t queued_body_ = 0;  // streamed pieces waiting for the connection
+  void write_piece(const Bytes& b);
   Head head_;
   BodyDecoder body_;
   std::string buf_;

@@ -10,7 +10,7 @@ namespace p2pt::proto {
 std::optional<MsgType> msg_type_from_u8(uint8_t v) {
   switch (v) {
     case 1: case 2: case 3: case 4:
-    case 10: case 11: case 12: case 13:
+    case 10: case 11: case 12: case 13: case 14:
     case 20: case 21: case 22:
     case 99:
       return MsgType(v);
@@ -29,6 +29,7 @@ const char* msg_type_name(MsgType t) {
     case MsgType::ReqBody: return "ReqBody";
     case MsgType::ReqEnd: return "ReqEnd";
     case MsgType::Cancel: return "Cancel";
+    case MsgType::Credit: return "Credit";
     case MsgType::ResHeaders: return "ResHeaders";
     case MsgType::ResBody: return "ResBody";
     case MsgType::ResEnd: return "ResEnd";
@@ -197,8 +198,23 @@ std::string psk_mac(const std::string& secret, const char* role, const std::stri
   return hex_encode(mac.data(), mac.size());
 }
 
+// TUNNEL_FEATURES=<comma list> replaces the list (e.g. "sse" to behave
+// exactly like a reference peer in interop and A/B tests).
 const std::vector<std::string>& our_features() {
-  static const std::vector<std::string> f{"sse", "cancel"};
+  static const std::vector<std::string> f = [] {
+    std::vector<std::string> v{"sse", "cancel", "flow"};
+    if (const char* e = getenv("TUNNEL_FEATURES")) {
+      v.clear();
+      std::string s = e;
+      for (size_t a = 0; a <= s.size();) {
+        size_t c = s.find(',', a);
+        if (c == std::string::npos) c = s.size();
+        if (c > a) v.push_back(s.substr(a, c - a));
+        a = c + 1;
+      }
+    }
+    return v;
+  }();
   return f;
 }
 
@@ -288,6 +304,12 @@ Frame make_res_headers(const ResponseHeaders& h) { return json_frame(MsgType::Re
 Frame make_body(MsgType t, uint32_t sid, Bytes data) { return Frame{t, sid, std::move(data)}; }
 Frame make_empty(MsgType t, uint32_t sid) { return Frame{t, sid, Bytes()}; }
 Frame make_error(uint32_t sid, const std::string& msg) { return Frame{MsgType::Error, sid, Bytes::copy(msg)}; }
+Frame make_credit(uint32_t sid, uint32_t bytes) {
+  uint8_t b[4];
+  wr32(b, bytes);
+  return Frame{MsgType::Credit, sid, slab_copy(b, 4)};
+}
+uint32_t credit_bytes(const Frame& f) { return f.payload.size() == 4 ? rd32(f.payload.data()) : 0; }
 
 static std::string trim_trailing_slashes(const std::string& s) {
   size_t n = s.size();

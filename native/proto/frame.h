@@ -43,6 +43,12 @@ enum class MsgType : uint8_t {
   // Extension (only sent when both HELLOs list "cancel"): the proxy's client
   // went away; serve aborts the upstream request. Not in the reference.
   Cancel = 13,
+  // Extension "flow" (only when both HELLOs list it): per-stream credit. The
+  // payload is a u32 (big-endian) number of body bytes the receiver grants the
+  // sender on this stream: RES_BODY when sent by the proxy, REQ_BODY when
+  // sent by serve. Each side starts with kFlowWindow bytes per stream and
+  // direction. Not in the reference (which has no flow control, Q11).
+  Credit = 14,
   ResHeaders = 20,
   ResBody = 21,
   ResEnd = 22,
@@ -99,8 +105,9 @@ std::string psk_mac(const std::string& secret, const char* role, const std::stri
                     const std::string& binding);
 
 // Features this build understands. "sse" is the reference's only feature;
-// "cancel" (client-disconnect propagation) is only *acted on* when
-// both peers list it, so reference peers are unaffected.
+// "cancel" (client-disconnect propagation) and "flow" (per-stream
+// credit, Q11) are only *acted on* when both peers list them, so reference
+// peers are unaffected.
 const std::vector<std::string>& our_features();
 // Negotiate from a peer HELLO (reference Agree::from_hello, protocol.rs:44-80).
 bool agree_from_hello(const Hello& h, Agree& out, std::string* err,
@@ -138,6 +145,14 @@ Frame make_res_headers(const ResponseHeaders& h);
 Frame make_body(MsgType t, uint32_t stream_id, Bytes data);
 Frame make_empty(MsgType t, uint32_t stream_id);
 Frame make_error(uint32_t stream_id, const std::string& msg);
+Frame make_credit(uint32_t stream_id, uint32_t bytes);
+// Bytes granted by a Credit frame (0 if malformed).
+uint32_t credit_bytes(const Frame& f);
+
+// "flow" extension: initial per-stream, per-direction body credit, and the
+// backlog below which a receiver hands consumed bytes back as credit.
+constexpr int64_t kFlowWindow = 256 * 1024;
+constexpr size_t kFlowGrantMin = 16 * 1024;
 
 // Upstream URL rewrite (reference serve.rs:167-185, incl. quirk Q1: the prefix
 // is stripped without a path-segment boundary check).

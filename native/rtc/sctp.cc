@@ -554,6 +554,9 @@ void SctpAssociation::handle_data(uint8_t flags, const uint8_t* c, size_t len, c
     Partial& pa = U ? partial_u_[st] : partial_[st];
     if (B) {
       pa.data.clear();
+      // Reserve once for a whole tunnel frame (<= 64 KiB): fragments append
+      // without reallocation (a 64 KiB frame is ~55 fragments at 1200 B).
+      if (pa.data.capacity() < 65536 + 1024) pa.data.reserve(65536 + 1024);
       pa.ppid = pp;
       pa.active = true;
     }

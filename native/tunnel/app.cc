@@ -246,6 +246,8 @@ int run_app(const AppConfig& cfg) {
         sc.upstream_prewarm_ttl_ms = cfg.upstream_prewarm_ttl_ms;
         sc.secret = cfg.secret;
         sc.inline_streams = cfg.inline_streams;
+        sc.max_request_body = cfg.max_request_body;
+        sc.stream_body_threshold = cfg.stream_body_threshold ? cfg.stream_body_threshold : UINT64_MAX;
         st.serve = ServeSession::start(r, ch, sc, [&](const std::string& e) { on_fail(e); }, &pool);
       } else {
         LOG_INFO(kT, "WebRTC connected, starting proxy...");

@@ -64,6 +64,10 @@ struct AppConfig {
   int workers = -1;
   // Streams kept on the association thread before new ones go to workers.
   size_t inline_streams = 16;
+  // serve: request bodies at least this big stream to the upstream as they
+  // arrive; 413 above max_request_body (0 = unlimited).
+  uint64_t stream_body_threshold = 8 << 20;
+  uint64_t max_request_body = 0;
   std::string secret;  // "psk" extension; empty = reference behaviour
 };
 

@@ -51,6 +51,7 @@ class ProxyWorker : public std::enable_shared_from_this<ProxyWorker> {
   bool ready() const { return shared_->ready.load(std::memory_order_relaxed); }
   size_t body_chunk() const { return shared_->body_chunk; }
   bool cancel_feature() const { return shared_->cancel_feature.load(std::memory_order_relaxed); }
+  bool flow() const { return shared_->flow.load(std::memory_order_relaxed); }
   const ProxyConfig& config() const { return shared_->cfg; }
   Reactor& reactor() { return r_; }
   void conn_closed(ProxyConn* c);
@@ -82,6 +83,11 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     conn_->on_close([w](const std::string& err) {
       if (auto s = w.lock()) s->on_client_closed(err);
     });
+    conn_->on_drain(
+        [w] {
+          if (auto s = w.lock()) s->maybe_grant();
+        },
+        kGrantLow);
   }
 
   void on_res_headers(const proto::ResponseHeaders& rh) {
@@ -125,6 +131,28 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     } else {
       conn_->write(payload);
     }
+    if (stream_registered_ && sess_flow()) {
+      owed_ += payload.size();
+      maybe_grant();
+    }
+  }
+
+  // "flow": RES_BODY bytes the client has taken (our output backlog for it is
+  // small again) are credit for serve to send more of this stream.
+  void maybe_grant() {
+    if (owed_ < proto::kFlowGrantMin || !conn_ || conn_->closed() || conn_->pending_out() > kGrantLow) return;
+    if (auto sess = sess_.lock()) sess->send(proto::make_credit(sid_, uint32_t(std::min<uint64_t>(owed_, UINT32_MAX))));
+    owed_ = 0;
+  }
+
+  // "flow": serve granted more REQ_BODY bytes for this upload.
+  void on_credit(uint32_t n) {
+    send_credit_ += n;
+    if (credit_paused_ && send_credit_ > 0) {
+      credit_paused_ = false;
+      update_reading();
+      if (conn_ && !inbuf_.empty()) process();
+    }
   }
 
   void on_res_end() {
@@ -159,12 +187,20 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
   // Per-stream back-pressure from the session: this upload's frames pile up.
   void flow_pause() {
     flow_paused_ = true;
-    if (conn_ && !conn_->closed()) conn_->pause_reading();
+    update_reading();
   }
   void flow_resume() {
     flow_paused_ = false;
-    if (conn_ && !conn_->closed() && !pipelined_hold_) conn_->resume_reading();
+    update_reading();
     if (conn_ && !inbuf_.empty()) process();
+  }
+
+  // The client socket is read unless a pipelined request waits, the session
+  // holds this upload back, or serve's credit for it ran out.
+  void update_reading() {
+    if (!conn_ || conn_->closed()) return;
+    if (pipelined_hold_ || flow_paused_ || credit_paused_) conn_->pause_reading();
+    else conn_->resume_reading();
   }
 
  private:
@@ -266,6 +302,9 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
       simple_and_close(431, "text/plain", "Request header fields too large for the tunnel");
       return false;
     }
+    send_credit_ = proto::kFlowWindow;
+    credit_paused_ = false;
+    owed_ = 0;
     sess->register_stream(sid_, weak_from_this());
     stream_registered_ = true;
     sess->send(std::move(hf));
@@ -288,11 +327,13 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     bool reject = reject_not_ready_;
     size_t cs = sess->body_chunk();
     auto conn = conn_;
+    bool flow = sess->flow();
     size_t used = body_.feed(data, len, [&](const uint8_t* d, size_t n) {
       if (reject) return;
       Bytes b = conn ? conn->rx_view(d, n) : Bytes::copy(d, n);
       for (size_t off = 0; off < n; off += cs)
         sess->send(proto::make_body(proto::MsgType::ReqBody, sid, b.slice(off, cs)));
+      if (flow) send_credit_ -= int64_t(n);
     });
     *used_out = used;
     if (used == SIZE_MAX) {
@@ -302,6 +343,10 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     if (body_.done()) {
       finish_request_body();
       return true;
+    }
+    if (flow && send_credit_ <= 0 && !credit_paused_) {  // wait for serve's credit
+      credit_paused_ = true;
+      update_reading();
     }
     return false;
   }
@@ -431,11 +476,12 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     }
     state_ = State::Head;
     req_ = http::Head{};
-    // A flow pause belonged to the stream that just ended (its Resume may
-    // never come: the session drops a finished stream's pause state).
-    if (pipelined_hold_ || flow_paused_) {
+    // Pauses belonged to the stream that just ended (its Resume may never
+    // come: the session drops a finished stream's pause state).
+    if (pipelined_hold_ || flow_paused_ || credit_paused_) {
       pipelined_hold_ = false;
       flow_paused_ = false;
+      credit_paused_ = false;
       conn_->resume_reading();
     }
     if (!inbuf_.empty()) {
@@ -497,6 +543,14 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
   bool pipelined_hold_ = false;
   bool reject_not_ready_ = false;
   bool flow_paused_ = false;
+  bool credit_paused_ = false;   // "flow": upload out of serve's credit
+  int64_t send_credit_ = proto::kFlowWindow;
+  uint64_t owed_ = 0;            // "flow": RES_BODY bytes delivered, not yet granted back
+  static constexpr size_t kGrantLow = 64 * 1024;
+  bool sess_flow() const {
+    auto s = sess_.lock();
+    return s && s->flow();
+  }
   uint64_t body_sent_ = 0;
   uint64_t timer_ = 0;
   friend class ProxyWorker;
@@ -560,6 +614,9 @@ void ProxyWorker::handle(ProxySession::Cmd& c) {
       break;
     case Cmd::Resume:
       if (conn) conn->flow_resume();
+      break;
+    case Cmd::Credit:
+      if (conn) conn->on_credit(c.bytes);
       break;
     case Cmd::Adopt:
       break;
@@ -766,6 +823,7 @@ void ProxySession::on_agree(const proto::Frame& f) {
   }
   shared_->cancel_feature =
       std::find(agree.features.begin(), agree.features.end(), "cancel") != agree.features.end();
+  shared_->flow = std::find(agree.features.begin(), agree.features.end(), "flow") != agree.features.end();
   ready_ = true;
   shared_->ready = true;
   last_pong_ms_ = Reactor::now_ms();
@@ -924,6 +982,15 @@ void ProxySession::route(const proto::Frame& f) {
         Cmd c{Cmd::Error, f.stream_id};
         c.data = f.payload;
         command(k, std::move(c));
+      }
+      break;
+    }
+    case MsgType::Credit: {
+      auto it = routes_.find(f.stream_id);
+      if (it != routes_.end() && shared_->flow) {
+        Cmd c{Cmd::Credit, f.stream_id};
+        c.bytes = proto::credit_bytes(f);
+        command(it->second.thread, std::move(c));
       }
       break;
     }

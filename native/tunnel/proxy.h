@@ -83,16 +83,18 @@ class ProxySession : public std::enable_shared_from_this<ProxySession> {
     std::atomic<uint32_t> next_sid{1};
     std::atomic<bool> ready{false};
     std::atomic<bool> cancel_feature{false};
+    std::atomic<bool> flow{false};  // "flow" negotiated: per-stream credit both ways
     size_t body_chunk = proto::kMaxBodyChunk;
   };
   // Association thread -> a connection thread.
   struct Cmd {
-    enum Kind : uint8_t { Adopt, Headers, Body, End, Error, Pause, Resume } kind;
+    enum Kind : uint8_t { Adopt, Headers, Body, End, Error, Pause, Resume, Credit } kind;
     explicit Cmd(Kind k, uint32_t s = 0) : kind(k), sid(s) {}
     uint32_t sid = 0;
     int fd = -1;                                  // Adopt
     Bytes data;                                   // Body / Error message
     std::shared_ptr<proto::ResponseHeaders> rh;   // Headers
+    uint32_t bytes = 0;                           // Credit: REQ_BODY bytes granted by serve
   };
   // A connection thread -> association thread.
   struct Ev {

@@ -39,7 +39,7 @@ void FrameScheduler::send(proto::Frame f) {
   }
   size_t sz = f.wire_size();
   queued_ += sz;
-  if (f.stream_id == 0) {
+  if (f.stream_id == 0 || f.type == proto::MsgType::Credit) {  // credit is cumulative: no ordering with data
     control_.push_back(std::move(f));
   } else {
     uint32_t sid = f.stream_id;

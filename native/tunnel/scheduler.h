@@ -6,7 +6,7 @@
 // body. Here frames wait in per-stream FIFOs and are released into the channel
 // only while its buffered amount is below a window, in this order:
 //
-//   1. control frames (stream 0: HELLO/AGREE/PING/PONG/credit);
+//   1. control frames (stream 0: HELLO/AGREE/PING/PONG; CREDIT of any stream);
 //   2. the "interactive" lane: streams with little queued (<= kInteractive
 //      bytes, e.g. an SSE stream with its next token), one frame per turn;
 //   3. the bulk lane: backlogged streams, round-robin one frame per turn.

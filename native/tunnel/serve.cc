@@ -23,7 +23,7 @@ class ServeWorker : public std::enable_shared_from_this<ServeWorker> {
   ~ServeWorker() {
     auto calls = std::move(calls_);
     for (auto& kv : calls)
-      if (kv.second) kv.second->cancel();
+      if (kv.second.call) kv.second.call->cancel();
     client_.reset();
     out_.reset();
   }
@@ -39,11 +39,11 @@ class ServeWorker : public std::enable_shared_from_this<ServeWorker> {
   void handle(ServeSession::Cmd& c) {
     using Cmd = ServeSession::Cmd;
     switch (c.kind) {
-      case Cmd::Start: start(c.sid, std::move(c.req), c.body_chunk, c.retryable); break;
+      case Cmd::Start: start(c.sid, std::move(c.req), c.body_chunk, c.retryable, c.grant); break;
       case Cmd::Cancel: {
         auto it = calls_.find(c.sid);
         if (it == calls_.end()) break;
-        auto call = it->second;
+        auto call = it->second.call;
         calls_.erase(it);
         if (call) call->cancel();
         break;
@@ -51,13 +51,26 @@ class ServeWorker : public std::enable_shared_from_this<ServeWorker> {
       case Cmd::Pause:
       case Cmd::Resume: {
         auto it = calls_.find(c.sid);
-        if (it != calls_.end() && it->second) {
-          if (c.kind == Cmd::Pause) it->second->pause();
-          else it->second->resume();
+        if (it != calls_.end() && it->second.call) {
+          if (c.kind == Cmd::Pause) it->second.call->pause();
+          else it->second.call->resume();
         }
         break;
       }
       case Cmd::Prewarm: prewarm(); break;
+      case Cmd::Body:
+      case Cmd::BodyEnd: {
+        auto it = calls_.find(c.sid);
+        if (it == calls_.end() || !it->second.call) break;
+        if (c.kind == Cmd::BodyEnd) {
+          it->second.call->end_body();
+          break;
+        }
+        it->second.owed += c.data.size();
+        it->second.call->write_body(std::move(c.data));
+        maybe_grant(c.sid, it->second);
+        break;
+      }
     }
   }
 
@@ -70,6 +83,22 @@ class ServeWorker : public std::enable_shared_from_this<ServeWorker> {
       if (!client_->prewarm(u, cfg_.upstream_prewarm, cfg_.upstream_prewarm_ttl_ms, &perr))
         LOG_DEBUG(kT, "upstream prewarm disabled for %s: %s", u.c_str(), perr.c_str());
     }
+  }
+
+  struct CallState {
+    std::shared_ptr<http::ClientCall> call;
+    bool grant = false;  // "flow": hand consumed streamed-body bytes back as credit
+    uint64_t owed = 0;
+  };
+
+  // Streamed request body: the bytes the upstream socket took off our hands
+  // are credit the session can give back to the proxy ("flow").
+  void maybe_grant(uint32_t sid, CallState& cs) {
+    if (!cs.grant || !cs.owed || !cs.call || cs.call->body_backlog() > 64 * 1024) return;
+    ServeSession::Ev ev(ServeSession::Ev::Credit, sid);
+    ev.bytes = uint32_t(std::min<uint64_t>(cs.owed, UINT32_MAX));
+    cs.owed -= ev.bytes;
+    out_->push(std::move(ev));
   }
 
   void emit(uint32_t sid, proto::Frame f) {
@@ -88,10 +117,18 @@ class ServeWorker : public std::enable_shared_from_this<ServeWorker> {
     emit(sid, proto::make_empty(proto::MsgType::ResEnd, sid));
   }
 
-  void start(uint32_t sid, http::ClientRequest req, size_t body_chunk, bool retryable) {
+  void start(uint32_t sid, http::ClientRequest req, size_t body_chunk, bool retryable, bool grant) {
     if (!inline_) prewarm();  // workers warm their own pools on first use
     std::weak_ptr<ServeWorker> w = shared_from_this();
     http::ClientCallbacks cb;
+    if (req.stream_body) {
+      cb.on_body_drain = [w, sid] {
+        auto s = w.lock();
+        if (!s) return;
+        auto it = s->calls_.find(sid);
+        if (it != s->calls_.end()) s->maybe_grant(sid, it->second);
+      };
+    }
     // Unreachable upstream: with other upstreams to try, the request goes back
     // to the session untouched (it never left this host).
     std::shared_ptr<ServeSession::Unreachable> back;
@@ -161,10 +198,13 @@ class ServeWorker : public std::enable_shared_from_this<ServeWorker> {
       }
       s->out_->push(std::move(done));
     };
-    calls_[sid] = nullptr;  // present while the call runs (on_done may fire inside request())
+    CallState& st = calls_[sid];  // present while the call runs (on_done may fire inside request())
+    st.grant = grant;
     auto call = client_->request(std::move(req), std::move(cb));
     auto it = calls_.find(sid);
-    if (it != calls_.end()) it->second = call;
+    if (it != calls_.end()) {
+      it->second.call = call;
+    }
   }
 
   Reactor& r_;
@@ -176,7 +216,7 @@ class ServeWorker : public std::enable_shared_from_this<ServeWorker> {
   bool prewarmed_ = false;
   std::unique_ptr<http::HttpClient> client_;
   std::unique_ptr<Pipe<ServeSession::Ev>> out_;
-  std::unordered_map<uint32_t, std::shared_ptr<http::ClientCall>> calls_;
+  std::unordered_map<uint32_t, CallState> calls_;
 };
 
 std::shared_ptr<ServeSession> ServeSession::start(Reactor& r, std::shared_ptr<MessageChannel> ch, ServeConfig cfg,
@@ -376,6 +416,7 @@ void ServeSession::on_hello(const proto::Frame& f) {
   }
   if (!cfg_.secret.empty()) agree.psk_mac = proto::psk_mac(cfg_.secret, "agree", hello.psk_nonce, binding);
   cancel_feature_ = std::find(agree.features.begin(), agree.features.end(), "cancel") != agree.features.end();
+  flow_ = std::find(agree.features.begin(), agree.features.end(), "flow") != agree.features.end();
   sched_->send(proto::make_agree(agree));
   handshaken_ = true;
   LOG_INFO(kT, "sent AGREE, tunnel ready");
@@ -419,15 +460,56 @@ void ServeSession::handle_frame(const proto::Frame& f) {
       trace::event("serve", h.stream_id, "req_headers");
       uint32_t sid = h.stream_id;  // keyed by the JSON stream_id (serve.rs:118)
       Pending p;
+      if (const std::string* cl = proto::header_get(h.headers, "content-length")) {
+        char* end = nullptr;
+        unsigned long long v = strtoull(cl->c_str(), &end, 10);
+        if (end && *end == 0 && !cl->empty()) p.declared = int64_t(v);
+      }
       p.headers = std::move(h);
-      streams_[sid] = std::move(p);
+      Pending& slot = streams_[sid] = std::move(p);
+      if (cfg_.max_request_body && slot.declared > int64_t(cfg_.max_request_body)) reject_too_large(sid);
       break;
     }
     case MsgType::ReqBody: {
+      if (f.payload.empty()) break;
       auto it = streams_.find(f.stream_id);
-      if (it != streams_.end() && !f.payload.empty()) {
-        it->second.body_len += f.payload.size();
-        it->second.body.push_back(f.payload);  // zero-copy: keeps the message alive
+      if (it != streams_.end()) {
+        Pending& p = it->second;
+        if (flow_) grant(f.stream_id, p.owed, f.payload.size());  // buffered here: bounded by the threshold
+        if (p.rejected) break;
+        p.body_len += f.payload.size();
+        p.body.push_back(f.payload);  // zero-copy: keeps the message alive
+        if (cfg_.max_request_body && p.body_len > cfg_.max_request_body) {
+          reject_too_large(f.stream_id);
+          break;
+        }
+        // Large bodies go to the upstream as they arrive instead of piling up.
+        if (p.body_len >= cfg_.stream_body_threshold) {
+          Pending moved = std::move(p);
+          streams_.erase(it);
+          start_request(f.stream_id, std::move(moved), true);
+        }
+        break;
+      }
+      auto fl = inflight_.find(f.stream_id);
+      if (fl != inflight_.end() && fl->second.uploading) {
+        fl->second.uploaded += f.payload.size();
+        if (cfg_.max_request_body && fl->second.uploaded > cfg_.max_request_body) {
+          LOG_WARN(kT, "stream %u: request body over %llu bytes, aborting", f.stream_id,
+                   static_cast<unsigned long long>(cfg_.max_request_body));
+          Inflight gone = fl->second;
+          release_upstream(gone);
+          place_->release(gone.thread);
+          inflight_.erase(fl);
+          paused_.erase(f.stream_id);
+          command(gone.thread, Cmd{Cmd::Cancel, f.stream_id});
+          sched_->send(proto::make_error(f.stream_id, "request body exceeds the tunnel's limit"));
+          sched_->send(proto::make_empty(MsgType::ResEnd, f.stream_id));
+          break;
+        }
+        Cmd c{Cmd::Body, f.stream_id};
+        c.data = f.payload;
+        command(fl->second.thread, std::move(c));
       }
       break;
     }
@@ -436,8 +518,26 @@ void ServeSession::handle_frame(const proto::Frame& f) {
       if (it != streams_.end()) {
         Pending p = std::move(it->second);
         streams_.erase(it);
+        if (p.rejected) break;
         trace::event("serve", f.stream_id, "req_end");
-        start_request(f.stream_id, std::move(p));
+        start_request(f.stream_id, std::move(p), false);
+        break;
+      }
+      auto fl = inflight_.find(f.stream_id);
+      if (fl != inflight_.end() && fl->second.uploading) {
+        fl->second.uploading = false;
+        trace::event("serve", f.stream_id, "req_end");
+        command(fl->second.thread, Cmd{Cmd::BodyEnd, f.stream_id});
+      }
+      break;
+    }
+    case MsgType::Credit: {
+      auto it = inflight_.find(f.stream_id);
+      if (!flow_ || it == inflight_.end()) break;
+      it->second.credit += proto::credit_bytes(f);
+      if (it->second.fc && it->second.credit > 0) {
+        it->second.fc = false;
+        set_paused(f.stream_id, it->second);
       }
       break;
     }
@@ -517,12 +617,35 @@ void ServeSession::send_start(uint32_t sid, Inflight& fl, http::ClientRequest re
   Cmd c{Cmd::Start, sid};
   c.req = std::move(req);
   c.body_chunk = sched_->body_chunk();
-  c.retryable = ups_.size() > 1 && fl.tries + 1u < ups_.size();
+  c.retryable = ups_.size() > 1 && fl.tries + 1u < ups_.size() && !c.req.stream_body;
+  c.grant = flow_ && c.req.stream_body;
   ups_[fl.up].outstanding++;
   command(fl.thread, std::move(c));
 }
 
-void ServeSession::start_request(uint32_t sid, Pending p) {
+// "flow": give `n` consumed body bytes back to the sender of `sid`, batched
+// (kFlowGrantMin) so small uploads cost no extra frames.
+void ServeSession::grant(uint32_t sid, uint64_t& owed, uint64_t n, bool force) {
+  owed += n;
+  if (!owed || (!force && owed < proto::kFlowGrantMin)) return;
+  uint32_t g = uint32_t(std::min<uint64_t>(owed, UINT32_MAX));
+  owed -= g;
+  sched_->send(proto::make_credit(sid, g));
+}
+
+void ServeSession::reject_too_large(uint32_t sid) {
+  auto it = streams_.find(sid);
+  if (it == streams_.end() || it->second.rejected) return;
+  LOG_WARN(kT, "stream %u: request body over %llu bytes, answering 413", sid,
+           static_cast<unsigned long long>(cfg_.max_request_body));
+  metrics::counter_add("tunnel_requests_too_large_total");
+  it->second.rejected = true;
+  it->second.body.clear();
+  it->second.body_len = 0;
+  send_simple_response(sid, 413, "Payload Too Large");
+}
+
+void ServeSession::start_request(uint32_t sid, Pending p, bool streaming) {
   if (!valid_method(p.headers.method)) {
     LOG_ERROR(kT, "failed to handle request: invalid HTTP method");
     send_simple_response(sid, 400, "Bad Request: invalid HTTP method");
@@ -549,11 +672,18 @@ void ServeSession::start_request(uint32_t sid, Pending p) {
   req.body = std::move(p.body);
   req.body_len = p.body_len;
   req.force_content_length = had_cl;
+  if (streaming) {  // the rest of the body arrives after the call started
+    req.stream_body = true;
+    req.content_length = p.declared;
+  }
   metrics::counter_add("tunnel_upstream_requests_total");
   Inflight& fl = inflight_[sid];
   fl.up = pick_upstream();
   fl.thread = place_->pick();
   fl.path = std::move(p.headers.path);
+  fl.uploading = streaming;
+  fl.uploaded = p.body_len;
+  if (flow_ && p.owed) grant(sid, p.owed, 0, true);  // what was buffered is consumed
   send_start(sid, fl, std::move(req));
 }
 
@@ -595,20 +725,46 @@ void ServeSession::on_event(Ev& ev) {
     paused_.erase(ev.sid);
     return;
   }
+  if (ev.kind == Ev::Credit) {  // the upstream took streamed request-body bytes
+    if (flow_) sched_->send(proto::make_credit(ev.sid, ev.bytes));
+    return;
+  }
+  Inflight& fl = it->second;
   bool body = ev.frame.type == proto::MsgType::ResBody;
+  size_t n = ev.frame.payload.size();
   sched_->send(std::move(ev.frame));
-  if (!body || it->second.paused) return;
+  if (!body) return;
+  // "flow": the proxy hands credit back as its client drains; out of credit,
+  // this stream's upstream read pauses (a slow client cannot grow the proxy).
+  if (flow_) {
+    fl.credit -= int64_t(n);
+    if (fl.credit <= 0 && !fl.fc) {
+      fl.fc = true;
+      metrics::counter_add("tunnel_stream_credit_stalls_total");
+    }
+  }
   // Per-stream back-pressure: only the stream whose frames pile up stops
   // reading its upstream; a congested channel (over the global high water)
   // also pauses every stream that has a backlog, but never an interactive
   // (SSE-like) one with nothing queued.
-  size_t q = sched_->stream_queued(ev.sid);
-  if (q > cfg_.stream_budget || (q > FrameScheduler::kInteractive && sched_->over_high())) {
-    it->second.paused = true;
-    paused_.insert(ev.sid);
-    metrics::counter_add("tunnel_stream_pauses_total");
-    command(it->second.thread, Cmd{Cmd::Pause, ev.sid});
+  if (!fl.bp) {
+    size_t q = sched_->stream_queued(ev.sid);
+    if (q > cfg_.stream_budget || (q > FrameScheduler::kInteractive && sched_->over_high())) {
+      fl.bp = true;
+      paused_.insert(ev.sid);
+      metrics::counter_add("tunnel_stream_pauses_total");
+    }
   }
+  set_paused(ev.sid, fl);
+}
+
+// Tells the call's reactor when the stream's wanted state (paused for
+// back-pressure or for lack of credit) differs from what it was last told.
+void ServeSession::set_paused(uint32_t sid, Inflight& fl) {
+  bool want = fl.bp || fl.fc;
+  if (want == fl.paused) return;
+  fl.paused = want;
+  command(fl.thread, Cmd{want ? Cmd::Pause : Cmd::Resume, sid});
 }
 
 void ServeSession::check_paused() {
@@ -621,9 +777,9 @@ void ServeSession::check_paused() {
       continue;
     }
     if (sched_->stream_queued(sid) <= cfg_.stream_budget / 4) {
-      it->second.paused = false;
+      it->second.bp = false;
       p = paused_.erase(p);
-      command(it->second.thread, Cmd{Cmd::Resume, sid});
+      set_paused(sid, it->second);
       continue;
     }
     ++p;

@@ -58,6 +58,12 @@ struct ServeConfig {
   // Concurrent upstream calls kept on the association thread before new ones
   // go to worker threads (see tunnel/workers.h).
   size_t inline_streams = 16;
+  // Request bodies are buffered to REQ_END like the reference (serve.rs:120-
+  // 139) while below this size (declared or received); larger ones stream to
+  // the upstream as they arrive, so serve memory stays bounded.
+  uint64_t stream_body_threshold = 8 << 20;
+  // 413 above this many request-body bytes (0 = unlimited, the reference).
+  uint64_t max_request_body = 0;
 };
 
 class ServeWorker;
@@ -76,12 +82,14 @@ class ServeSession : public std::enable_shared_from_this<ServeSession> {
 
   // Association thread -> the reactor running a call.
   struct Cmd {
-    enum Kind : uint8_t { Start, Cancel, Pause, Resume, Prewarm } kind;
+    enum Kind : uint8_t { Start, Cancel, Pause, Resume, Prewarm, Body, BodyEnd } kind;
     explicit Cmd(Kind k, uint32_t s = 0) : kind(k), sid(s) {}
     uint32_t sid = 0;
     http::ClientRequest req;  // Start
     size_t body_chunk = 0;    // Start: RES_BODY payload size for this channel
     bool retryable = false;   // Start: hand the request back if the upstream is unreachable
+    bool grant = false;       // Start: report consumed streamed-body bytes (Ev::Credit)
+    Bytes data;               // Body
   };
   // An upstream call that never connected, handed back for another upstream.
   struct Unreachable {
@@ -90,12 +98,13 @@ class ServeSession : public std::enable_shared_from_this<ServeSession> {
   };
   // A call's reactor -> association thread.
   struct Ev {
-    enum Kind : uint8_t { Frame, Done } kind;
+    enum Kind : uint8_t { Frame, Done, Credit } kind;
     explicit Ev(Kind k, uint32_t s = 0) : kind(k), sid(s) {}
     uint32_t sid = 0;
     proto::Frame frame{proto::MsgType::Ping, 0, Bytes()};
     bool responded = false;                    // Done: the upstream answered (any status)
     std::shared_ptr<Unreachable> unreachable;  // Done: no connection, nothing sent yet
+    uint32_t bytes = 0;                        // Credit: streamed-body bytes the upstream took
   };
 
  private:
@@ -103,13 +112,21 @@ class ServeSession : public std::enable_shared_from_this<ServeSession> {
     proto::RequestHeaders headers;
     std::vector<Bytes> body;
     uint64_t body_len = 0;
+    int64_t declared = -1;  // content-length of the request, if given
+    bool rejected = false;  // 413 sent: drop the rest of the body
+    uint64_t owed = 0;      // "flow": received body bytes not yet granted back
   };
   struct Inflight {
     size_t up = 0;      // index into ups_
     size_t thread = 0;  // index into links_
-    bool paused = false;
+    bool paused = false;  // what the call's reactor was last told
     uint8_t tries = 0;  // upstreams tried after connect failures
     std::string path;   // request path (the URL is rebuilt for another upstream)
+    bool bp = false;    // paused because its frames pile up here (back-pressure)
+    bool fc = false;    // paused because the peer's credit ran out ("flow")
+    bool uploading = false;   // request body still streaming to the upstream
+    uint64_t uploaded = 0;    // request-body bytes received
+    int64_t credit = proto::kFlowWindow;  // "flow": RES_BODY bytes we may still send
   };
   // One upstream origin (one inference endpoint, e.g. one per GPU) and its
   // passive health: an origin that refuses connections is ejected for an
@@ -139,11 +156,14 @@ class ServeSession : public std::enable_shared_from_this<ServeSession> {
   void on_message(Bytes raw);
   void on_hello(const proto::Frame& f);
   void handle_frame(const proto::Frame& f);
-  void start_request(uint32_t sid, Pending p);
+  void start_request(uint32_t sid, Pending p, bool streaming);
   void send_simple_response(uint32_t sid, uint16_t status, const std::string& body);
   void send_ping();
   void on_event(Ev& ev);
   void check_paused();
+  void set_paused(uint32_t sid, Inflight& fl);
+  void grant(uint32_t sid, uint64_t& owed, uint64_t n, bool force = false);
+  void reject_too_large(uint32_t sid);
   void command(size_t thread, Cmd c) { links_[thread].to->push(std::move(c)); }
 
   Reactor& r_;
@@ -154,6 +174,7 @@ class ServeSession : public std::enable_shared_from_this<ServeSession> {
   bool handshaken_ = false;
   bool stopped_ = false;
   bool cancel_feature_ = false;
+  bool flow_ = false;  // "flow" negotiated: per-stream credit both ways
   uint64_t hello_timer_ = 0;
   uint64_t ping_timer_ = 0;
   uint64_t last_pong_ms_ = 0;

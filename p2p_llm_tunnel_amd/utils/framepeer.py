@@ -11,7 +11,7 @@ import struct
 import time
 
 HELLO, AGREE, PING, PONG = 1, 2, 3, 4
-REQ_HEADERS, REQ_BODY, REQ_END, CANCEL = 10, 11, 12, 13
+REQ_HEADERS, REQ_BODY, REQ_END, CANCEL, CREDIT = 10, 11, 12, 13, 14
 RES_HEADERS, RES_BODY, RES_END, ERROR = 20, 21, 22, 99
 
 
