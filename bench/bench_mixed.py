@@ -1,0 +1,162 @@
+#!/usr/bin/env python3
+"""Head-of-line benchmark: SSE token streams sharing one tunnel with bulk
+downloads and a slow client.
+
+    8 SSE streams (a token every --interval-ms, --tokens per response)
+  + 8 concurrent 64 MB downloads (GET /bulk), repeated while the SSE runs
+  + 1 client reading a 64 MB download at 100 KB/s
+
+The reference sends every frame straight into its one ordered data channel
+with no scheduling or back-pressure (reference serve.rs:274, proxy.rs:391-419),
+so a token waits behind whatever body bytes were queued before it. Reported
+per transport (jumbo same-host packets and the standard 1200-byte path):
+inter-token latency (ITL) p50/p99/max of the SSE streams, tunneled vs direct
+(the same load straight to the upstream), the added ITL p99, bulk MB/s, and
+the proxy's peak RSS (the slow client must not make it grow).
+
+    python bench/bench_mixed.py [--transports jumbo,std] [--out FILE]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import socket
+import subprocess
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from p2p_llm_tunnel_amd import binary  # noqa: E402
+from p2p_llm_tunnel_amd.utils.build import ensure_native  # noqa: E402
+from p2p_llm_tunnel_amd.utils.procs import Tunnel, free_port, spawn  # noqa: E402
+
+
+def rss_kb(pid):
+    try:
+        for line in open(f"/proc/{pid}/status"):
+            if line.startswith("VmRSS:"):
+                return int(line.split()[1])
+    except OSError:
+        pass
+    return 0
+
+
+def lg(port, *args, timeout=600):
+    return subprocess.Popen([binary("tunnel-loadgen"), "--target", f"127.0.0.1:{port}", *map(str, args)],
+                            stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+
+
+def result(p, timeout=600):
+    out, _ = p.communicate(timeout=timeout)
+    return json.loads(out.strip().splitlines()[-1])
+
+
+def slow_reader(port, rate, stop, stats):
+    """Reads a 64 MB download at `rate` bytes/s until stopped."""
+    s = socket.create_connection(("127.0.0.1", port))
+    s.sendall(b"GET /bulk?bytes=67108864 HTTP/1.1\r\nHost: x\r\n\r\n")
+    s.settimeout(1)
+    t0, got = time.time(), 0
+    while not stop.is_set():
+        due = t0 + got / rate
+        if time.time() < due:
+            time.sleep(min(0.01, due - time.time()))
+            continue
+        try:
+            d = s.recv(8192)
+        except socket.timeout:
+            continue
+        if not d:
+            break
+        got += len(d)
+    stats["slow_bytes"] = got
+    s.close()
+
+
+def scenario(port, a, watch_pid=None):
+    """Bulk + slow reader + SSE against `port`; returns the SSE loadgen result etc."""
+    stop = threading.Event()
+    stats = {}
+    peak = [0]
+
+    def watch():
+        while not stop.is_set():
+            if watch_pid:
+                peak[0] = max(peak[0], rss_kb(watch_pid))
+            time.sleep(0.05)
+
+    w = threading.Thread(target=watch)
+    w.start()
+    sr = threading.Thread(target=slow_reader, args=(port, a.slow_rate, stop, stats))
+    sr.start()
+    bulk = lg(port, "--streams", a.bulk_streams, "--steps", a.bulk_steps, "--warmup", 0, "--method", "GET",
+              "--path", f"/bulk?bytes={a.bulk_mb << 20}", "--events", "none")
+    time.sleep(0.3)
+    sse = lg(port, "--streams", a.sse_streams, "--steps", a.sse_steps, "--warmup", 0, "--warm-conns", 1)
+    sse_r = result(sse)
+    bulk_r = result(bulk)
+    stop.set()
+    sr.join()
+    w.join()
+    return sse_r, bulk_r, stats, peak[0]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--transports", default="jumbo,std")
+    ap.add_argument("--interval-ms", type=int, default=10)
+    ap.add_argument("--tokens", type=int, default=100)
+    ap.add_argument("--sse-streams", type=int, default=8)
+    ap.add_argument("--sse-steps", type=int, default=3)
+    ap.add_argument("--bulk-streams", type=int, default=8)
+    ap.add_argument("--bulk-steps", type=int, default=2)
+    ap.add_argument("--bulk-mb", type=int, default=64)
+    ap.add_argument("--slow-rate", type=int, default=100 * 1024)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    ensure_native()
+    mport = free_port()
+    mock = spawn("mock", [binary("tunnel-mock"), "--port", str(mport), "--interval-ms", str(a.interval_ms),
+                          "--tokens", str(a.tokens), "--threads", "4"])
+    mock.wait_for("Mock LLM server running", 10)
+    res = {"host": os.uname().nodename, "time": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
+           "sse": f"{a.sse_streams} streams x {a.tokens} tokens @ {a.interval_ms} ms",
+           "bulk": f"{a.bulk_streams} x {a.bulk_mb} MB GET, {a.bulk_steps} rounds", "slow_client_Bps": a.slow_rate,
+           "rows": []}
+    try:
+        d_sse, d_bulk, _, _ = scenario(mport, a)
+        print(json.dumps({"direct_itl_p99_ms": d_sse["p99_itl_ms"], "direct_bulk_MBps": d_bulk["MBps"]}),
+              file=sys.stderr, flush=True)
+        for tr in [x for x in a.transports.split(",") if x]:
+            extra = ["--no-jumbo-loopback"] if tr == "std" else []
+            with Tunnel(f"http://127.0.0.1:{mport}", transport="webrtc", serve_extra=extra, proxy_extra=extra) as t:
+                path = t.serve.wait_for("connection established", 5).split(" via ", 1)[-1]
+                base = rss_kb(t.proxy.popen.pid)
+                sse_r, bulk_r, stats, peak = scenario(t.proxy_port, a, t.proxy.popen.pid)
+                row = {"transport": tr, "path": path,
+                       "tunneled_itl_p50_ms": sse_r["p50_itl_ms"], "tunneled_itl_p99_ms": sse_r["p99_itl_ms"],
+                       "tunneled_itl_max_ms": sse_r["max_itl_ms"], "direct_itl_p50_ms": d_sse["p50_itl_ms"],
+                       "direct_itl_p99_ms": d_sse["p99_itl_ms"], "direct_itl_max_ms": d_sse["max_itl_ms"],
+                       "added_itl_p99_ms": sse_r["p99_itl_ms"] - d_sse["p99_itl_ms"],
+                       "tunneled_ttft_p99_ms": sse_r["p99_ttft_ms"], "direct_ttft_p99_ms": d_sse["p99_ttft_ms"],
+                       "sse_events": sse_r["events"], "sse_errors": sse_r["errors"],
+                       "bulk_MBps": bulk_r["MBps"], "direct_bulk_MBps": d_bulk["MBps"], "bulk_errors": bulk_r["errors"],
+                       "slow_client_bytes": stats.get("slow_bytes"),
+                       "proxy_rss_base_mib": round(base / 1024, 1), "proxy_rss_peak_mib": round(peak / 1024, 1)}
+                res["rows"].append(row)
+                print(json.dumps(row), file=sys.stderr, flush=True)
+    finally:
+        mock.stop()
+    doc = json.dumps(res, indent=1)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(doc + "\n")
+    print(doc)
+
+
+if __name__ == "__main__":
+    main()

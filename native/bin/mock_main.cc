@@ -95,9 +95,20 @@ struct Server {
       size_t n = 1 << 20;
       size_t q = h.target.find("bytes=");
       if (q != std::string::npos) n = size_t(strtoull(h.target.c_str() + q + 6, nullptr, 10));
-      std::string b(n, '\0');
-      for (size_t i = 0; i < n; i++) b[i] = char(i & 0xFF);
-      respond(c, 200, "application/octet-stream", b);
+      // The body (bytes i & 0xFF) is built once per size and shared by every
+      // response as a zero-copy view: a 64 MB download costs the reactor no
+      // fill loop, so it never delays other connections' token timers.
+      static thread_local std::map<size_t, Bytes> cache;
+      auto it = cache.find(n);
+      if (it == cache.end()) {
+        std::vector<uint8_t> b(n);
+        for (size_t i = 0; i < n; i++) b[i] = uint8_t(i & 0xFF);
+        it = cache.emplace(n, Bytes::take(std::move(b))).first;
+      }
+      c->write("HTTP/1.0 200 OK\r\nServer: p2pt-mock\r\nDate: " + http::http_date_now() +
+               "\r\nContent-Type: application/octet-stream\r\nContent-Length: " + std::to_string(n) + "\r\n\r\n");
+      c->write(it->second);
+      c->close_after_flush();
     } else if (h.method == "POST" && (path == "/v1/chat/completions" || path == "/chat/completions")) {
       bool stream = body.find("\"stream\": true") != std::string::npos || body.find("\"stream\":true") != std::string::npos;
       if (stream) sse(c);

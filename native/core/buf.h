@@ -94,8 +94,11 @@ class BufPool {
  public:
   explicit BufPool(size_t buf_size, size_t max_keep = 512) : size_(buf_size), max_keep_(max_keep) {}
   RawBufPtr get() {
+    // Buffers come back roughly in the order they went out, so a short scan
+    // from the rotating cursor finds a free one; when it does not, the pool
+    // grows (up to max_keep) rather than scanning every pinned buffer.
     size_t n = bufs_.size();
-    for (size_t k = 0; k < n && k < 128; k++) {
+    for (size_t k = 0; k < n && k < kScan; k++) {
       size_t i = next_ + k < n ? next_ + k : next_ + k - n;
       if (bufs_[i].use_count() == 1) {
         reuse_fence();
@@ -104,12 +107,16 @@ class BufPool {
       }
     }
     auto b = std::make_shared<RawBuf>(size_);
-    if (n < max_keep_) bufs_.push_back(b);
+    if (n < max_keep_) {
+      bufs_.insert(bufs_.begin() + long(next_ < n ? next_ : n), b);  // scanned last next time round
+      next_ = next_ < n ? next_ + 1 : 0;
+    }
     return b;
   }
   size_t size() const { return bufs_.size(); }
 
  private:
+  static constexpr size_t kScan = 16;
   size_t size_, max_keep_;
   std::vector<RawBufPtr> bufs_;
   size_t next_ = 0;

@@ -280,8 +280,16 @@ void TcpConn::do_read() {
   constexpr size_t kRx = 65536;
   // Bounded number of reads per wakeup keeps the loop fair across sockets.
   for (int iter = 0; iter < 16 && fd_ >= 0 && !paused_; iter++) {
-    if (!rx_ || rx_.use_count() > 1) rx_ = std::make_shared<RawBuf>(kRx);
-    else reuse_fence();  // the last view may have been dropped on another thread
+    if (!rx_ || rx_.use_count() > 1) {
+      // Views of the previous buffer are still alive (body frames queued for
+      // the channel, possibly on another thread): take a recycled one from
+      // this thread's pool instead of allocating — and later freeing across
+      // threads — 64 KiB per read.
+      thread_local BufPool pool(kRx, 1024);
+      rx_ = pool.get();
+    } else {
+      reuse_fence();  // the last view may have been dropped on another thread
+    }
     uint8_t* buf = rx_->data.get();
     ssize_t n;
     if (ssl_) {

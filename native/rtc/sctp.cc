@@ -553,20 +553,30 @@ void SctpAssociation::handle_data(uint8_t flags, const uint8_t* c, size_t len, c
     }
     Partial& pa = U ? partial_u_[st] : partial_[st];
     if (B) {
-      pa.data.clear();
-      // Reserve once for a whole tunnel frame (<= 64 KiB): fragments append
-      // without reallocation (a 64 KiB frame is ~55 fragments at 1200 B).
-      if (pa.data.capacity() < 65536 + 1024) pa.data.reserve(65536 + 1024);
+      // Reassembled into a pooled buffer sized for a whole tunnel frame (one
+      // copy per fragment, no reallocation, recycled once the message's
+      // views are gone — possibly on a worker thread).
+      pa.buf = reasm_pool_.get();
+      pa.len = 0;
+      pa.big.clear();
       pa.ppid = pp;
       pa.active = true;
     }
     if (!pa.active) return;  // middle fragment without a beginning (after FORWARD-TSN)
-    pa.data.insert(pa.data.end(), dp, dp + dn);
+    if (pa.big.empty() && pa.len + dn <= pa.buf->cap) {
+      memcpy(pa.buf->data.get() + pa.len, dp, dn);
+      pa.len += dn;
+    } else {  // larger than any tunnel frame: fall back to a growing vector
+      if (pa.big.empty()) pa.big.assign(pa.buf->data.get(), pa.buf->data.get() + pa.len);
+      pa.big.insert(pa.big.end(), dp, dp + dn);
+    }
     if (E) {
       pa.active = false;
-      std::vector<uint8_t> msg;
-      msg.swap(pa.data);
-      if (on_message) on_message(st, pa.ppid, Bytes::take(std::move(msg)));
+      Bytes msg = pa.big.empty() ? Bytes::adopt(pa.buf, pa.buf->data.get(), pa.len) : Bytes::take(std::move(pa.big));
+      pa.buf.reset();
+      pa.big.clear();
+      pa.len = 0;
+      if (on_message) on_message(st, pa.ppid, std::move(msg));
     }
   };
   if (d == 1) {
@@ -598,7 +608,7 @@ void SctpAssociation::handle_data(uint8_t flags, const uint8_t* c, size_t len, c
 
 void SctpAssociation::build_sack(std::vector<uint8_t>& b) {
   size_t held = ooo_bytes_;
-  for (auto& kv : partial_) held += kv.second.data.size();
+  for (auto& kv : partial_) held += kv.second.size();
   uint32_t a_rwnd = held >= cfg_.rwnd ? 0 : uint32_t(cfg_.rwnd - held);
   // Gap blocks relative to the cumulative TSN (ooo_ keys sorted numerically;
   // sort by serial distance to survive TSN wrap).

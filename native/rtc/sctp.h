@@ -208,9 +208,14 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   uint64_t sack_timer_ = 0;
   struct Partial {
     uint32_t ppid = 0;
-    std::vector<uint8_t> data;
+    RawBufPtr buf;  // pooled (reasm_pool_): a whole tunnel frame fits
+    size_t len = 0;
+    std::vector<uint8_t> big;  // only for messages beyond the pooled size
     bool active = false;
+    size_t size() const { return big.empty() ? len : big.size(); }
   };
+  BufPool reasm_pool_{kReasmBuf, 256};
+  static constexpr size_t kReasmBuf = 65536 + 1024;
   std::map<uint16_t, Partial> partial_;  // per-stream reassembly (ordered)
   std::map<uint16_t, Partial> partial_u_;  // unordered
 
