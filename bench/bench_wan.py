@@ -1,0 +1,109 @@
+#!/usr/bin/env python3
+"""The tunnel over an emulated WAN path at the standard 1200-byte SCTP MTU.
+
+Both peers' datagrams go through the ICE agent's WAN shim (native/rtc/ice.cc):
+a bottleneck link of --rate-mbps with a drop-tail queue, a fixed round-trip
+time and Bernoulli loss (TUNNEL_FAULT_RTT_MS / _RATE_MBPS / _LOSS). For each
+(RTT, loss) it measures
+
+  * SSE alone: 8 streams, a token every 10 ms — inter-token latency (ITL);
+  * SSE + bulk: the same 8 SSE streams while 4 downloads (--bulk-mb) share the
+    path — a lost bulk packet holds back every later message on the single
+    ordered SCTP stream (the reference's layout, rtc.rs:133), so the SSE ITL
+    tail measures that cross-stream head-of-line stall;
+  * bulk alone: 8 concurrent 1 MB echoes (req/s, MB/s each way).
+
+    python bench/bench_wan.py [--rtts 20,50] [--losses 0,0.005,0.02]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from p2p_llm_tunnel_amd import binary  # noqa: E402
+from p2p_llm_tunnel_amd.utils.build import ensure_native  # noqa: E402
+from p2p_llm_tunnel_amd.utils.procs import Tunnel, free_port, spawn  # noqa: E402
+
+
+def lg(port, *args):
+    return subprocess.Popen([binary("tunnel-loadgen"), "--target", f"127.0.0.1:{port}", *map(str, args)],
+                            stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+
+
+def result(p, timeout=900):
+    out, _ = p.communicate(timeout=timeout)
+    return json.loads(out.strip().splitlines()[-1])
+
+
+def sse(port, steps):
+    return lg(port, "--streams", 8, "--steps", steps, "--warmup", 0, "--warm-conns", 1)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rtts", default="20,50")
+    ap.add_argument("--losses", default="0,0.005,0.02")
+    ap.add_argument("--rate-mbps", type=float, default=200)
+    ap.add_argument("--queue-kb", type=float, default=0, help="bottleneck queue (0: one BDP)")
+    ap.add_argument("--sse-steps", type=int, default=3)
+    ap.add_argument("--bulk-mb", type=int, default=4, help="size of each of the 4 background downloads")
+    ap.add_argument("--echo-steps", type=int, default=1)
+    ap.add_argument("--extra", default="", help="extra flags for both tunnel processes")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    ensure_native()
+    mport = free_port()
+    mock = spawn("mock", [binary("tunnel-mock"), "--port", str(mport), "--interval-ms", "10", "--tokens", "100",
+                          "--threads", "2"])
+    mock.wait_for("Mock LLM server running", 10)
+    res = {"host": os.uname().nodename, "time": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
+           "mtu": 1200, "rate_mbps": a.rate_mbps, "extra": a.extra, "rows": []}
+    extra = ["--no-jumbo-loopback"] + [x for x in a.extra.split() if x]
+    try:
+        for rtt in [float(x) for x in a.rtts.split(",") if x]:
+            for loss in [float(x) for x in a.losses.split(",") if x]:
+                qkb = a.queue_kb or max(64.0, a.rate_mbps * 1e6 / 8 * rtt / 1e3 / 1024)
+                env = {"TUNNEL_FAULT_RTT_MS": str(rtt), "TUNNEL_FAULT_RATE_MBPS": str(a.rate_mbps),
+                       "TUNNEL_FAULT_QUEUE_KB": str(qkb), "TUNNEL_FAULT_LOSS": str(loss),
+                       "RUST_LOG": "warn,tunnel::rtc=info,tunnel::serve=info,tunnel::proxy=info"}
+                with Tunnel(f"http://127.0.0.1:{mport}", transport="webrtc", serve_extra=extra, proxy_extra=extra,
+                            env=env) as t:
+                    result(sse(t.proxy_port, 1))  # warm: connections, cwnd
+                    alone = result(sse(t.proxy_port, a.sse_steps))
+                    bulk = lg(t.proxy_port, "--streams", 4, "--steps", 1, "--warmup", 0, "--method", "GET",
+                              "--path", f"/bulk?bytes={a.bulk_mb << 20}", "--events", "none")
+                    time.sleep(0.5)
+                    mixed = result(sse(t.proxy_port, a.sse_steps))
+                    bulk_r = result(bulk)
+                    t0 = time.time()
+                    echo = result(lg(t.proxy_port, "--streams", 8, "--steps", a.echo_steps, "--warmup", 0,
+                                     "--post-bytes", 1 << 20))
+                    row = {"rtt_ms": rtt, "loss": loss, "queue_kb": round(qkb),
+                           "sse_itl_p50_ms": alone["p50_itl_ms"], "sse_itl_p99_ms": alone["p99_itl_ms"],
+                           "sse_itl_max_ms": alone["max_itl_ms"], "sse_ttft_p50_ms": alone["p50_ttft_ms"],
+                           "mixed_itl_p50_ms": mixed["p50_itl_ms"], "mixed_itl_p99_ms": mixed["p99_itl_ms"],
+                           "mixed_itl_p999_ms": mixed["p999_itl_ms"], "mixed_itl_max_ms": mixed["max_itl_ms"],
+                           "bulk_bg_MBps": bulk_r["MBps"], "echo_req_s": echo["req_s"],
+                           "echo_MBps_each_way": echo["req_s"] * 1.048576,
+                           "errors": alone["errors"] + mixed["errors"] + bulk_r["errors"] + echo["errors"],
+                           "echo_wall_s": round(time.time() - t0, 2)}
+                    res["rows"].append(row)
+                    print(json.dumps(row), file=sys.stderr, flush=True)
+    finally:
+        mock.stop()
+    doc = json.dumps(res, indent=1)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(doc + "\n")
+    print(doc)
+
+
+if __name__ == "__main__":
+    main()

@@ -489,31 +489,46 @@ void IceAgent::send(const uint8_t* p, size_t n) {
 }
 
 // Test-only fault injection on the datagram path (SURVEY §4.2 "fault
-// injection"): TUNNEL_FAULT_DROP / TUNNEL_FAULT_DUP are probabilities,
-// TUNNEL_FAULT_DELAY_MS a uniform random extra delay (which also reorders);
-// STUN (connectivity checks) is exempt from those so the path still comes up.
-// TUNNEL_FAULT_BLACKHOLE=<start_ms>:<duration_ms> drops every outbound
-// datagram, STUN included, in that window after the first send (a path that
-// dies and later comes back).
+// injection"): TUNNEL_FAULT_DROP (alias TUNNEL_FAULT_LOSS) / TUNNEL_FAULT_DUP
+// are probabilities, TUNNEL_FAULT_DELAY_MS a uniform random extra delay (which
+// also reorders); STUN (connectivity checks) is exempt from those so the path
+// still comes up. TUNNEL_FAULT_BLACKHOLE=<start_ms>:<duration_ms> drops every
+// outbound datagram, STUN included, in that window after the first send (a
+// path that dies and later comes back).
+//
+// WAN emulation (order-preserving, every datagram): TUNNEL_FAULT_RTT_MS adds
+// half the given round-trip time to each outbound datagram (set it on both
+// peers for that RTT); TUNNEL_FAULT_RATE_MBPS makes the outbound path a
+// bottleneck link of that rate with a drop-tail queue of
+// TUNNEL_FAULT_QUEUE_KB (default 256) — serialization and queueing delay,
+// congestion losses — so SCTP's congestion control meets a realistic path.
 namespace {
 struct FaultCfg {
   double drop = 0, dup = 0;
   uint64_t delay_us = 0;
+  uint64_t fixed_us = 0;    // one-way propagation delay
+  double rate_bps = 0;      // bottleneck rate (0 = unlimited)
+  uint64_t queue_bytes = 256 * 1024;
   uint64_t bh_start_ms = 0, bh_len_ms = 0, t0_ms = 0;
   bool on = false;
   uint64_t rng = 0x9E3779B97F4A7C15ull;
   FaultCfg() {
     if (const char* e = getenv("TUNNEL_FAULT_DROP")) drop = atof(e);
+    if (const char* e = getenv("TUNNEL_FAULT_LOSS")) drop = atof(e);
     if (const char* e = getenv("TUNNEL_FAULT_DUP")) dup = atof(e);
     if (const char* e = getenv("TUNNEL_FAULT_DELAY_MS")) delay_us = uint64_t(atof(e) * 1000);
+    if (const char* e = getenv("TUNNEL_FAULT_RTT_MS")) fixed_us = uint64_t(atof(e) * 500);
+    if (const char* e = getenv("TUNNEL_FAULT_RATE_MBPS")) rate_bps = atof(e) * 1e6;
+    if (const char* e = getenv("TUNNEL_FAULT_QUEUE_KB")) queue_bytes = uint64_t(atof(e) * 1024);
     if (const char* e = getenv("TUNNEL_FAULT_BLACKHOLE")) {
       bh_start_ms = strtoull(e, nullptr, 10);
       if (const char* c = strchr(e, ':')) bh_len_ms = strtoull(c + 1, nullptr, 10);
     }
     t0_ms = Reactor::now_ms();
-    on = drop > 0 || dup > 0 || delay_us > 0 || bh_len_ms > 0;
+    on = drop > 0 || dup > 0 || delay_us > 0 || bh_len_ms > 0 || fixed_us > 0 || rate_bps > 0;
     rng ^= uint64_t(getpid()) << 20;
   }
+  bool wan() const { return fixed_us > 0 || rate_bps > 0; }
   bool blackholed() const {
     uint64_t t = Reactor::now_ms() - t0_ms;
     return bh_len_ms && t >= bh_start_ms && t < bh_start_ms + bh_len_ms;
@@ -531,6 +546,24 @@ FaultCfg& fault() {
 }
 }  // namespace
 
+// Releases the WAN-emulation queue's due datagrams into the send queue (the
+// flush hook that follows the timer sends them).
+void IceAgent::arm_delay_timer() {
+  std::weak_ptr<IceAgent> w = shared_from_this();
+  delay_timer_ = r_.call_at(delayq_.front().first, [w] {
+    auto s = w.lock();
+    if (!s) return;
+    s->delay_timer_ = 0;
+    if (s->closed_) return;
+    uint64_t now = Reactor::now_us();
+    while (!s->delayq_.empty() && s->delayq_.front().first <= now) {
+      s->outq_.push_back(std::move(s->delayq_.front().second));
+      s->delayq_.pop_front();
+    }
+    if (!s->delayq_.empty()) s->arm_delay_timer();
+  });
+}
+
 void IceAgent::flush() {
   struct Recycle {
     IceAgent* a;
@@ -547,13 +580,31 @@ void IceAgent::flush() {
   if (fault().on) {
     if (fault().blackholed()) return;
     std::vector<Out> keep;
+    FaultCfg& f = fault();
     for (auto& o : outq_) {
-      if (o.faulted || stun::looks_like_stun(o.data.data(), o.data.size()) || o.local < 0) {
+      if (o.faulted || o.local < 0) {
         keep.push_back(std::move(o));
         continue;
       }
-      FaultCfg& f = fault();
-      if (f.uni() < f.drop) continue;
+      bool stun = stun::looks_like_stun(o.data.data(), o.data.size());
+      if (!stun && f.uni() < f.drop) continue;
+      if (f.wan()) {  // bottleneck link + propagation delay, in order
+        uint64_t now = Reactor::now_us();
+        uint64_t start = std::max(now, link_free_us_);
+        if (f.rate_bps > 0 && double(start - now) * f.rate_bps / 8e6 > double(f.queue_bytes)) {
+          wan_queue_drops_++;  // drop-tail: the bottleneck queue is full
+          continue;
+        }
+        uint64_t tx = f.rate_bps > 0 ? uint64_t(double(o.data.size()) * 8e6 / f.rate_bps) : 0;
+        link_free_us_ = start + tx;
+        o.faulted = true;
+        delayq_.emplace_back(link_free_us_ + f.fixed_us, std::move(o));
+        continue;
+      }
+      if (stun) {
+        keep.push_back(std::move(o));
+        continue;
+      }
       int copies = f.uni() < f.dup ? 2 : 1;
       for (int c = 0; c < copies; c++) {
         if (f.delay_us) {
@@ -572,6 +623,7 @@ void IceAgent::flush() {
       }
     }
     outq_.swap(keep);
+    if (!delayq_.empty() && !delay_timer_) arm_delay_timer();
     if (outq_.empty()) return;
   }
   // Group consecutive datagrams by socket for sendmmsg; within a group, runs

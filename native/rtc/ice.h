@@ -243,6 +243,15 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
     bool coalesce = false; // more records may be appended
   };
   std::vector<Out> outq_;
+  // WAN emulation (TUNNEL_FAULT_RTT_MS / _RATE_MBPS): datagrams waiting for
+  // their release time, in order.
+  std::deque<std::pair<uint64_t, Out>> delayq_;
+  uint64_t link_free_us_ = 0;
+  uint64_t delay_timer_ = 0;
+  void arm_delay_timer();
+ public:
+  uint64_t wan_queue_drops_ = 0;
+ private:
   struct NatPort {
     int fd = -1;
     int si = -1;                   // host socket it translates for

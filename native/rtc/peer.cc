@@ -371,6 +371,22 @@ void PeerConnection::start_sctp() {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().retransmits) : 0.0;
   });
+  metrics::gauge_fn("tunnel_sctp_fast_retransmits", [w] {
+    auto s = w.lock();
+    return s && s->sctp_ ? double(s->sctp_->stats().fast_retransmits) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_sctp_t3_expirations", [w] {
+    auto s = w.lock();
+    return s && s->sctp_ ? double(s->sctp_->stats().t3_expirations) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_sctp_rto_us", [w] {
+    auto s = w.lock();
+    return s && s->sctp_ ? double(s->sctp_->rto_us()) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_wan_queue_drops", [w] {
+    auto s = w.lock();
+    return s && s->ice_ ? double(s->ice_->wan_queue_drops_) : 0.0;
+  });
   metrics::gauge_fn("tunnel_sctp_packets_sent", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().packets_sent) : 0.0;

@@ -109,6 +109,7 @@ SctpAssociation::SctpAssociation(Reactor& r, SctpConfig cfg, PacketOut out) : r_
 SctpAssociation::~SctpAssociation() {
   if (sack_timer_) r_.cancel(sack_timer_);
   if (t3_timer_) r_.cancel(t3_timer_);
+  if (tlp_timer_) r_.cancel(tlp_timer_);
   if (init_timer_) r_.cancel(init_timer_);
   for (auto* c : inflight_) delete c;
   for (auto* c : chunk_free_) delete c;
@@ -475,6 +476,8 @@ void SctpAssociation::closed(const std::string& why) {
   closed_fired_ = true;
   state_ = State::Closed;
   stop_t3();
+  if (tlp_timer_) r_.cancel(tlp_timer_);
+  tlp_timer_ = 0;
   if (init_timer_) r_.cancel(init_timer_);
   init_timer_ = 0;
   auto cb = std::move(on_closed);
@@ -661,13 +664,17 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
   size_t flight_before = flight_size_;
   bool cum_advanced = tsn_lt(cum_acked_, cum);
   uint64_t rtt_sample = 0;
+  uint64_t newest_cum_sent = 0;
   while (!inflight_.empty() && tsn_le(inflight_.front()->tsn, cum)) {
     Chunk* ch = inflight_.front();
     inflight_.pop_front();
     if (ch->in_flight) flight_size_ -= ch->len;
     if (!ch->acked) {
       newly_acked += ch->len;
-      if (ch->tx == 1) rtt_sample = now - ch->sent_us;
+      if (ch->tx == 1) {
+        rtt_sample = now - ch->sent_us;
+        newest_cum_sent = std::max(newest_cum_sent, ch->sent_us);
+      }
     }
     free_chunk(ch);
   }
@@ -691,31 +698,59 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
       if (tsn_lt(highest_gap, ch->tsn)) highest_gap = ch->tsn;
     }
   }
-  if (rtt_sample) update_rto(rtt_sample);
-  // Miss indications -> fast retransmit (RFC 9260 §7.2.4).
+  if (rtt_sample) {
+    update_rto(rtt_sample);
+    if (!min_rtt_us_ || rtt_sample < min_rtt_us_) min_rtt_us_ = rtt_sample;
+  }
+  // Loss detection. (1) Miss indications -> fast retransmit (RFC 9260
+  // §7.2.4). (2) Time-based, after RACK (RFC 8985): a chunk still missing
+  // although a chunk *sent* more than a quarter SRTT after it has been
+  // acknowledged is lost — this also catches lost retransmissions and losses
+  // in sparse traffic (credit frames, lone SSE tokens) where three miss
+  // reports never come, which would otherwise wait for T3 (RTO >= 100 ms,
+  // doubling, cwnd collapse to one MTU).
+  // Only chunks transmitted once count as evidence: the acknowledgement of a
+  // retransmitted chunk may be for its original copy (RFC 8985's ambiguity),
+  // which would declare everything sent before the retransmission lost.
+  uint64_t rack_sent = 0;  // latest send time among acknowledged once-sent chunks
+  for (Chunk* ch : inflight_)
+    if (ch->acked && ch->tx == 1 && ch->sent_us > rack_sent) rack_sent = ch->sent_us;
+  if (cum_advanced) rack_sent = std::max(rack_sent, newest_cum_sent);
+  uint64_t reo = std::max<uint64_t>(srtt_us_ / 4, 1000);
   bool new_fast = false;
-  if (highest_gap != cum) {
-    for (Chunk* ch : inflight_) {
-      if (!tsn_lt(ch->tsn, highest_gap)) break;
-      if (ch->acked || ch->retransmit) continue;
-      if (++ch->miss == 3) {
-        ch->miss = 0;
-        ch->retransmit = true;
-        ch->fast = true;
-        if (ch->in_flight) {
-          flight_size_ -= ch->len;
-          ch->in_flight = false;
-        }
-        new_fast = true;
-        stats_.fast_retransmits++;
-      }
+  auto mark = [&](Chunk* ch) {
+    ch->miss = 0;
+    ch->retransmit = true;
+    ch->fast = true;
+    if (ch->in_flight) {
+      flight_size_ -= ch->len;
+      ch->in_flight = false;
+    }
+    new_fast = true;
+    stats_.fast_retransmits++;
+  };
+  for (Chunk* ch : inflight_) {
+    if (ch->acked || ch->retransmit) continue;
+    // Fast retransmit at most once per chunk (RFC 9260 §7.2.4); a lost
+    // retransmission is found by the time-based rule, a probe or T3.
+    bool below_gap = highest_gap != cum && tsn_lt(ch->tsn, highest_gap) && ch->tx == 1;
+    if (below_gap && ++ch->miss == 3) {
+      mark(ch);
+      continue;
+    }
+    if (rack_sent && ch->sent_us + reo < rack_sent) {
+      stats_.rack_marks++;
+      mark(ch);
     }
   }
   if (cum_advanced) assoc_errors_ = 0;
   // Congestion control (RFC 9260 §7.2.1-7.2.2).
   if (newly_acked && cum_advanced && !fast_recovery_) {
     if (cwnd_ <= ssthresh_) {
-      if (flight_before + cfg_.mtu >= cwnd_) cwnd_ += std::min(newly_acked, cfg_.mtu);
+      // Byte counting with RFC 3465's limit L = 2 MTUs per SACK: the peer
+      // SACKs once per received batch, so one MTU per SACK would make slow
+      // start nearly linear; unbounded counting overshoots a bottleneck queue.
+      if (flight_before + cfg_.mtu >= cwnd_) cwnd_ += std::min(newly_acked, 2 * cfg_.mtu);
     } else {
       partial_acked_ += newly_acked;
       if (partial_acked_ >= cwnd_ && flight_before + cfg_.mtu >= cwnd_) {
@@ -725,7 +760,17 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
     }
   }
   if (new_fast && !fast_recovery_) {
-    ssthresh_ = std::max(cwnd_ / 2, 4 * cfg_.mtu);
+    cwnd_bypass_ = 1;
+    // Loss response after TCP Veno: the backlog this association keeps in the
+    // path's queues is cwnd * (SRTT - min RTT) / SRTT. A loss with (almost) no
+    // backlog is taken as random (wireless, lossy WAN) and cuts cwnd by 1/5;
+    // a loss with a standing queue is congestion and cuts by 0.3 (CUBIC's
+    // beta, RFC 9438) rather than Reno's half.
+    uint64_t rtt = std::max<uint64_t>(srtt_us_, 1);
+    size_t backlog = min_rtt_us_ && rtt > min_rtt_us_ ? size_t(double(cwnd_) * double(rtt - min_rtt_us_) / double(rtt)) : 0;
+    bool random_loss = backlog < 3 * cfg_.mtu + cwnd_ / 16;
+    if (random_loss) stats_.random_loss_events++;
+    ssthresh_ = std::max(random_loss ? cwnd_ * 4 / 5 : cwnd_ * 7 / 10, 4 * cfg_.mtu);
     cwnd_ = ssthresh_;
     partial_acked_ = 0;
     fast_recovery_ = true;
@@ -733,9 +778,51 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
   }
   if (fast_recovery_ && !tsn_lt(cum, fast_recovery_exit_)) fast_recovery_ = false;
   peer_rwnd_ = a_rwnd > flight_size_ ? a_rwnd - flight_size_ : 0;
-  if (inflight_.empty()) stop_t3();
-  else if (cum_advanced) start_t3();
+  if (cum_advanced) tlp_count_ = 0;
+  if (inflight_.empty()) {
+    stop_t3();
+    if (tlp_timer_) r_.cancel(tlp_timer_);
+    tlp_timer_ = 0;
+  } else if (cum_advanced) {
+    start_t3();
+    arm_tlp();
+  }
   maybe_finish_shutdown();
+}
+
+// Tail-loss probe (after RFC 8985 TLP): with data outstanding and no SACK for
+// ~2 SRTT, retransmit the oldest unacknowledged chunk. The probe's SACK
+// either acknowledges it or exposes the gaps for the time-based detection,
+// instead of waiting for T3. Up to two probes per episode; no cwnd change.
+void SctpAssociation::arm_tlp() {
+  if (tlp_timer_) r_.cancel(tlp_timer_);
+  tlp_timer_ = 0;
+  if (inflight_.empty() || tlp_count_ >= 2 || !srtt_us_) return;
+  uint64_t pto = std::max<uint64_t>(2 * srtt_us_ + cfg_.sack_delay_us, 10000);
+  if (pto >= rto_us_) return;  // T3 comes first anyway
+  std::weak_ptr<SctpAssociation> w = shared_from_this();
+  tlp_timer_ = r_.call_later_us(pto, [w] {
+    if (auto s = w.lock()) {
+      s->tlp_timer_ = 0;
+      s->on_tlp();
+    }
+  });
+}
+
+void SctpAssociation::on_tlp() {
+  for (Chunk* ch : inflight_) {
+    if (ch->acked || ch->retransmit) continue;
+    ch->retransmit = true;
+    ch->fast = true;  // may go out even when cwnd is full
+    if (ch->in_flight) {
+      flight_size_ -= ch->len;
+      ch->in_flight = false;
+    }
+    tlp_count_++;
+    stats_.tlp_probes++;
+    cwnd_bypass_ = 1;
+    break;  // flush() at the end of this iteration sends it
+  }
 }
 
 void SctpAssociation::handle_forward_tsn(const uint8_t* c, size_t len) {
@@ -1002,13 +1089,15 @@ void SctpAssociation::flush() {
     stats_.bytes_sent += ch->len;
   };
   // Retransmissions first. A fast-retransmit burst may exceed cwnd once.
-  bool fast_budget = true;
+  // A chunk may go out beyond cwnd only once per loss event: the first fast
+  // retransmission of a recovery episode (RFC 9260 §7.2.4) or a tail-loss
+  // probe — not once per flush, which would overdrive a congested path.
   bool sent_any = false;
   for (Chunk* ch : inflight_) {
     if (!ch->retransmit || ch->acked) continue;
-    bool allowed = flight_size_ + ch->len <= cwnd_ || flight_size_ == 0 || (ch->fast && fast_budget);
+    bool allowed = flight_size_ + ch->len <= cwnd_ || flight_size_ == 0 || (ch->fast && cwnd_bypass_ > 0);
     if (!allowed) break;
-    if (ch->fast) fast_budget = false;
+    if (ch->fast && flight_size_ + ch->len > cwnd_ && flight_size_ && cwnd_bypass_ > 0) cwnd_bypass_--;
     ch->retransmit = false;
     ch->fast = false;
     ch->miss = 0;
@@ -1063,6 +1152,7 @@ void SctpAssociation::flush() {
   }
   flush_pkt();
   if (sent_any && !t3_timer_) start_t3();
+  if (sent_any && !tlp_timer_) arm_tlp();
   if (sent_any && on_sent) on_sent();
 }
 

@@ -55,6 +55,7 @@ struct SctpStats {
   uint64_t packets_sent = 0, packets_received = 0;
   uint64_t data_chunks_sent = 0, data_chunks_received = 0;
   uint64_t retransmits = 0, fast_retransmits = 0, t3_expirations = 0;
+  uint64_t tlp_probes = 0, rack_marks = 0, random_loss_events = 0;
   uint64_t sacks_sent = 0, sacks_received = 0;
   uint64_t bytes_sent = 0, bytes_received = 0;
 };
@@ -106,6 +107,7 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   const SctpStats& stats() const { return stats_; }
   size_t cwnd() const { return cwnd_; }
   uint64_t srtt_us() const { return srtt_us_; }
+  uint64_t rto_us() const { return rto_us_; }
   void set_mtu(size_t mtu);
   void set_initial_cwnd(size_t c) { if (c > cwnd_) cwnd_ = c; }
   void request_stream_reset(uint16_t stream);
@@ -147,6 +149,8 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   void start_t3();
   void stop_t3();
   void on_t3();
+  void arm_tlp();
+  void on_tlp();
   void emit_packet(std::vector<uint8_t>& pkt);
   void begin_gather();
   void close_run();
@@ -190,8 +194,12 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   bool fast_recovery_ = false;
   uint32_t fast_recovery_exit_ = 0;
   uint64_t t3_timer_ = 0;
+  uint64_t tlp_timer_ = 0;  // tail-loss probe (fires before T3, no cwnd collapse)
+  int tlp_count_ = 0;       // probes since the cumulative ack last advanced
+  int cwnd_bypass_ = 0;     // chunks allowed out beyond cwnd (one per loss event)
   uint64_t rto_us_;
   uint64_t srtt_us_ = 0, rttvar_us_ = 0;
+  uint64_t min_rtt_us_ = 0;  // smallest RTT sample: the path's base RTT
   int assoc_errors_ = 0;
   bool retransmit_pending_ = false;
 
