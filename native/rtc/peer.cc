@@ -50,6 +50,11 @@ void DataChannel::close() {
   on_buffered_low = nullptr;
 }
 
+size_t DataChannel::send_window_hint() const {
+  auto pc = pc_.lock();
+  return pc && pc->sctp_ ? pc->sctp_->cwnd() : 0;
+}
+
 // On same-host jumbo paths (16 KiB SCTP packets) body frames are sized to one
 // DATA chunk: no fragmentation on send, no reassembly copy on receive, and
 // finer interleaving of streams. On network paths (~1200 B packets) the

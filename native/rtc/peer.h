@@ -55,6 +55,7 @@ class DataChannel : public MessageChannel, public std::enable_shared_from_this<D
   void close() override;
   std::string describe() const override;
   size_t body_chunk() const override;
+  size_t send_window_hint() const override;
   std::string channel_binding() const override;
   const std::string& label() const { return label_; }
   int stream() const { return stream_; }

@@ -39,6 +39,11 @@ class MessageChannel {
   // peers compute the same string. Empty when the transport has no such
   // identity (the TCP debug transport).
   virtual std::string channel_binding() const { return ""; }
+  // How many bytes the transport can move per round trip right now (SCTP's
+  // congestion window); 0 = unknown. The frame scheduler keeps only a
+  // fraction of it queued in the channel, so on a slow path a token does
+  // not wait behind a full 64 KiB of other streams' bodies.
+  virtual size_t send_window_hint() const { return 0; }
 
   // Message arrived (whole message, zero-copy view where possible).
   std::function<void(Bytes)> on_message;

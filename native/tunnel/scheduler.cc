@@ -31,8 +31,11 @@ void FrameScheduler::list(uint32_t sid, StreamQ& s) {
 
 void FrameScheduler::send(proto::Frame f) {
   if (!ch_ || !ch_->is_open()) return;
-  // Fast path: nothing queued and the channel has room.
-  if (queued_ == 0 && ch_->buffered_amount() < window_) {
+  // Fast path: nothing queued and the channel has room. The channel's
+  // low-water mark follows the (adaptive) window so the pump is woken again.
+  size_t win = window();
+  ch_->buffered_low_threshold = win / 2;
+  if (queued_ == 0 && ch_->buffered_amount() < win) {
     emit(f);
     if (pending_bytes() > high_) was_high_ = true;
     return;
@@ -82,7 +85,9 @@ void FrameScheduler::pump() {
   if (pumping_ || !ch_) return;
   pumping_ = true;
   bool progressed = false;
-  while (ch_->is_open() && queued_ && ch_->buffered_amount() < window_) {
+  size_t win = window();
+  ch_->buffered_low_threshold = win / 2;
+  while (ch_->is_open() && queued_ && ch_->buffered_amount() < win) {
     if (!control_.empty()) {
       proto::Frame f = std::move(control_.front());
       control_.pop_front();

@@ -53,7 +53,13 @@ class FrameScheduler {
   void pump();
   MessageChannel* channel() const { return ch_.get(); }
   size_t body_chunk() const { return ch_ ? ch_->body_chunk() : proto::kMaxBodyChunk; }
-  size_t window() const { return window_; }
+  // Bytes kept queued in the channel: the configured window, or a quarter of
+  // the transport's congestion window when that is smaller (at least 8 KiB),
+  // so queued bulk ahead of a token stays below ~1/4 round trip of sending.
+  size_t window() const {
+    size_t h = ch_ ? ch_->send_window_hint() : 0;
+    return h ? std::min(window_, std::max<size_t>(8192, h / 4)) : window_;
+  }
 
  private:
   struct StreamQ {

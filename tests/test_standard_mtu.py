@@ -44,3 +44,26 @@ def test_standard_mtu_bulk_and_sse(mock_upstream, offload):
         else:
             assert sm["tunnel_udp_gso_sends"] == 0 and sm["tunnel_udp_gro_batches"] == 0
         assert sm["tunnel_sctp_packets_sent"] > 2 * len(body) / 1200
+
+
+def test_emulated_wan_path_with_loss(mock_upstream):
+    """20 ms RTT, 100 Mbit/s bottleneck, 1% loss on both peers' datagrams
+    (the ICE agent's WAN shim): bodies and SSE still arrive intact, losses are
+    repaired without T3 collapse, and a slow path keeps the scheduler's
+    channel window small without stalling it (adaptive window + low-water)."""
+    ms = free_port()
+    env = {"TUNNEL_FAULT_RTT_MS": "20", "TUNNEL_FAULT_RATE_MBPS": "100", "TUNNEL_FAULT_LOSS": "0.01"}
+    with Tunnel(mock_upstream, transport="webrtc", env=env, serve_extra=STD + ["--metrics-listen", f"127.0.0.1:{ms}"],
+                proxy_extra=STD) as t:
+        c = http.client.HTTPConnection("127.0.0.1", t.proxy_port, timeout=60)
+        body = bytes((i * 13 + 1) & 0xFF for i in range(1024 * 1024 + 3))
+        c.request("POST", "/echo", body=body)
+        r = c.getresponse()
+        assert r.status == 200 and r.read() == body
+        for _ in range(3):
+            c.request("POST", "/v1/chat/completions", body=json.dumps({"stream": True}))
+            r = c.getresponse()
+            assert r.status == 200 and r.read().count(b"data: ") == 7
+        m = _metrics(ms)
+        assert m["tunnel_sctp_retransmits"] > 0  # losses happened and were repaired
+        assert 15000 <= m["tunnel_sctp_srtt_us"] <= 200000
