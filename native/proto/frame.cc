@@ -202,7 +202,7 @@ std::string psk_mac(const std::string& secret, const char* role, const std::stri
 // exactly like a reference peer in interop and A/B tests).
 const std::vector<std::string>& our_features() {
   static const std::vector<std::string> f = [] {
-    std::vector<std::string> v{"sse", "cancel", "flow"};
+    std::vector<std::string> v{"sse", "cancel", "flow", "multistream"};
     if (const char* e = getenv("TUNNEL_FEATURES")) {
       v.clear();
       std::string s = e;

@@ -105,9 +105,11 @@ std::string psk_mac(const std::string& secret, const char* role, const std::stri
                     const std::string& binding);
 
 // Features this build understands. "sse" is the reference's only feature;
-// "cancel" (client-disconnect propagation) and "flow" (per-stream
-// credit, Q11) are only *acted on* when both peers list them, so reference
-// peers are unaffected.
+// "cancel" (client-disconnect propagation), "flow" (per-stream
+// credit, Q11) and "multistream" (tunnel streams spread over independently
+// delivered SCTP streams, MessageChannel::set_lanes) are only *acted on* when
+// both peers list them, so reference peers are unaffected.
+constexpr int kLanes = 16;
 const std::vector<std::string>& our_features();
 // Negotiate from a peer HELLO (reference Agree::from_hello, protocol.rs:44-80).
 bool agree_from_hello(const Hello& h, Agree& out, std::string* err,

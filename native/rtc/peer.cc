@@ -29,7 +29,12 @@ const char* pc_state_name(PcState s) {
 bool DataChannel::send(const uint8_t* hdr, size_t hlen, const Bytes& payload) {
   auto pc = pc_.lock();
   if (!pc || !is_open() || !pc->sctp_) return false;
-  bool ok = pc->sctp_->send_framed(uint16_t(stream_), kPpidBinary, hdr, hlen, payload);
+  uint16_t st = uint16_t(stream_);
+  if (lanes_ && hlen >= 5) {
+    uint32_t sid = rd32(hdr + 1);
+    if (sid) st = uint16_t(stream_ + 2 * (1 + int(sid % uint32_t(lanes_))));
+  }
+  bool ok = pc->sctp_->send_framed(st, kPpidBinary, hdr, hlen, payload);
   if (ok && buffered_amount() > buffered_low_threshold) above_low_ = true;
   return ok;
 }
@@ -453,7 +458,15 @@ void PeerConnection::on_sctp_message(uint16_t st, uint32_t ppid, Bytes msg) {
     return;
   }
   auto it = channels_.find(st);
-  if (it == channels_.end()) return;
+  if (it == channels_.end()) {
+    // A lane of a channel ("multistream" extension)?
+    for (auto& kv : channels_)
+      if (kv.second->owns_lane(st)) {
+        it = channels_.find(kv.first);
+        break;
+      }
+    if (it == channels_.end()) return;
+  }
   auto dc = it->second;
   if (!dc->is_open()) {
     // Data may follow an OPEN we have not ACKed to ourselves yet: an opener

@@ -15,6 +15,8 @@
 // sends them with one sendmmsg.
 #pragma once
 
+#include <algorithm>
+
 #include <functional>
 #include <map>
 #include <memory>
@@ -56,7 +58,14 @@ class DataChannel : public MessageChannel, public std::enable_shared_from_this<D
   std::string describe() const override;
   size_t body_chunk() const override;
   size_t send_window_hint() const override;
+  void set_lanes(int lanes) override { lanes_ = std::clamp(lanes, 0, kMaxLanes); }
   std::string channel_binding() const override;
+  static constexpr int kMaxLanes = 64;
+  // The channel's lane streams: stream + 2, + 4, ... (same parity as the
+  // channel's own stream, as RFC 8832 allocates per DTLS role).
+  bool owns_lane(uint16_t st) const {
+    return stream_ >= 0 && st > stream_ && (st - stream_) % 2 == 0 && (st - stream_) / 2 <= kMaxLanes;
+  }
   const std::string& label() const { return label_; }
   int stream() const { return stream_; }
 
@@ -67,6 +76,7 @@ class DataChannel : public MessageChannel, public std::enable_shared_from_this<D
   std::weak_ptr<PeerConnection> pc_;
   std::string label_;
   int stream_ = -1;
+  int lanes_ = 0;
   bool open_ = false;
   bool closed_ = false;
   bool above_low_ = false;

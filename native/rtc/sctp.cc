@@ -79,6 +79,8 @@ struct SctpAssociation::InChunk {
   uint16_t stream;
   uint32_t ppid;
   Bytes data;
+  uint16_t ssn;
+  bool delivered;  // handed up early (stream-independent delivery); kept for TSN accounting
 };
 
 namespace {
@@ -524,10 +526,96 @@ void SctpAssociation::abort(const std::string& reason) {
   closed(reason);
 }
 
+// Reassembly of one (possibly fragmented) message on stream `st`, fed in TSN
+// order; delivers when the last fragment arrives.
+void SctpAssociation::deliver_chunk(uint8_t fl, uint16_t st, uint16_t ssn, uint32_t pp, const Bytes& d) {
+  bool B = fl & 2, E = fl & 1, U = fl & 4;
+  const uint8_t* dp = d.data();
+  size_t dn = d.size();
+  if (B && E) {
+    deliver_message(st, ssn, U, pp, d);
+    return;
+  }
+  Partial& pa = U ? partial_u_[st] : partial_[st];
+  if (B) {
+    // Reassembled into a pooled buffer sized for a whole tunnel frame (one
+    // copy per fragment, no reallocation, recycled once the message's views
+    // are gone — possibly on a worker thread).
+    pa.buf = reasm_pool_.get();
+    pa.len = 0;
+    pa.big.clear();
+    pa.ppid = pp;
+    pa.active = true;
+  }
+  if (!pa.active) return;  // middle fragment without a beginning (after FORWARD-TSN)
+  if (pa.big.empty() && pa.len + dn <= pa.buf->cap) {
+    memcpy(pa.buf->data.get() + pa.len, dp, dn);
+    pa.len += dn;
+  } else {  // larger than any tunnel frame: fall back to a growing vector
+    if (pa.big.empty()) pa.big.assign(pa.buf->data.get(), pa.buf->data.get() + pa.len);
+    pa.big.insert(pa.big.end(), dp, dp + dn);
+  }
+  if (E) {
+    pa.active = false;
+    Bytes msg = pa.big.empty() ? Bytes::adopt(pa.buf, pa.buf->data.get(), pa.len) : Bytes::take(std::move(pa.big));
+    pa.buf.reset();
+    pa.big.clear();
+    pa.len = 0;
+    deliver_message(st, ssn, U, pa.ppid, std::move(msg));
+  }
+}
+
+// Hands a complete message up and keeps the per-stream sequence (SSN) state;
+// then releases any later single-chunk messages of that stream that arrived
+// early (out of TSN order) and now are next in their stream's sequence.
+void SctpAssociation::deliver_message(uint16_t st, uint16_t ssn, bool unordered, uint32_t pp, Bytes msg) {
+  if (!unordered) {
+    next_ssn_in_[st] = uint16_t(ssn + 1);
+    early_ready_.erase(stream_ssn(st, ssn));
+  }
+  if (on_message) on_message(st, pp, std::move(msg));
+  if (!unordered) release_ready(st);
+}
+
+void SctpAssociation::release_ready(uint16_t st) {
+  while (!early_ready_.empty()) {
+    auto it = early_ready_.find(stream_ssn(st, next_ssn_in_[st]));
+    if (it == early_ready_.end()) return;
+    auto oc = ooo_.find(it->second);
+    early_ready_.erase(it);
+    if (oc == ooo_.end() || oc->second->delivered) continue;
+    InChunk* ic = oc->second;
+    ic->delivered = true;
+    ooo_bytes_ -= ic->data.size();
+    Bytes m = std::move(ic->data);
+    ic->data = Bytes();
+    stats_.early_deliveries++;
+    deliver_message(ic->stream, ic->ssn, false, ic->ppid, std::move(m));
+  }
+}
+
+// Delivers the out-of-order chunks that became contiguous with the cumulative
+// TSN (those already delivered early only advance it).
+void SctpAssociation::drain_in_order() {
+  while (!ooo_.empty()) {
+    auto it = ooo_.find(peer_cum_tsn_ + 1);
+    if (it == ooo_.end()) break;
+    InChunk* ic = it->second;
+    ooo_.erase(it);
+    peer_cum_tsn_ = ic->tsn;
+    if (!ic->delivered) {
+      ooo_bytes_ -= ic->data.size();
+      deliver_chunk(ic->flags, ic->stream, ic->ssn, ic->ppid, ic->data);
+    }
+    delete ic;
+  }
+}
+
 void SctpAssociation::handle_data(uint8_t flags, const uint8_t* c, size_t len, const Bytes& pkt) {
   if (len < 12 || !have_peer_tsn_) return;
   uint32_t tsn = rd32(c);
   uint16_t stream = rd16(c + 4);
+  uint16_t ssn = rd16(c + 6);
   uint32_t ppid = rd32(c + 8);
   const uint8_t* data = c + 12;
   size_t dlen = len - 12;
@@ -546,57 +634,11 @@ void SctpAssociation::handle_data(uint8_t flags, const uint8_t* c, size_t len, c
       return pkt.slice(size_t(dp - pkt.data()), dn);
     return slab_copy(dp, dn);  // packed with other small messages (core/buf.h)
   };
-  auto deliver_chunk = [this](uint8_t fl, uint16_t st, uint32_t pp, const Bytes& d) {
-    bool B = fl & 2, E = fl & 1, U = fl & 4;
-    const uint8_t* dp = d.data();
-    size_t dn = d.size();
-    if (B && E) {
-      if (on_message) on_message(st, pp, d);
-      return;
-    }
-    Partial& pa = U ? partial_u_[st] : partial_[st];
-    if (B) {
-      // Reassembled into a pooled buffer sized for a whole tunnel frame (one
-      // copy per fragment, no reallocation, recycled once the message's
-      // views are gone — possibly on a worker thread).
-      pa.buf = reasm_pool_.get();
-      pa.len = 0;
-      pa.big.clear();
-      pa.ppid = pp;
-      pa.active = true;
-    }
-    if (!pa.active) return;  // middle fragment without a beginning (after FORWARD-TSN)
-    if (pa.big.empty() && pa.len + dn <= pa.buf->cap) {
-      memcpy(pa.buf->data.get() + pa.len, dp, dn);
-      pa.len += dn;
-    } else {  // larger than any tunnel frame: fall back to a growing vector
-      if (pa.big.empty()) pa.big.assign(pa.buf->data.get(), pa.buf->data.get() + pa.len);
-      pa.big.insert(pa.big.end(), dp, dp + dn);
-    }
-    if (E) {
-      pa.active = false;
-      Bytes msg = pa.big.empty() ? Bytes::adopt(pa.buf, pa.buf->data.get(), pa.len) : Bytes::take(std::move(pa.big));
-      pa.buf.reset();
-      pa.big.clear();
-      pa.len = 0;
-      if (on_message) on_message(st, pa.ppid, std::move(msg));
-    }
-  };
   if (d == 1) {
     peer_cum_tsn_ = tsn;
     bool whole = (flags & 3) == 3;
-    deliver_chunk(flags, stream, ppid, whole ? hold(data, dlen) : Bytes::adopt(nullptr, data, dlen));
-    // Drain now-contiguous out-of-order chunks.
-    while (!ooo_.empty()) {
-      auto it = ooo_.find(peer_cum_tsn_ + 1);
-      if (it == ooo_.end()) break;
-      InChunk* ic = it->second;
-      ooo_.erase(it);
-      ooo_bytes_ -= ic->data.size();
-      peer_cum_tsn_ = ic->tsn;
-      deliver_chunk(ic->flags, ic->stream, ic->ppid, ic->data);
-      delete ic;
-    }
+    deliver_chunk(flags, stream, ssn, ppid, whole ? hold(data, dlen) : Bytes::adopt(nullptr, data, dlen));
+    drain_in_order();
     return;
   }
   if (ooo_.count(tsn)) {
@@ -604,9 +646,26 @@ void SctpAssociation::handle_data(uint8_t flags, const uint8_t* c, size_t len, c
     return;
   }
   if (ooo_bytes_ + dlen > cfg_.rwnd) return;  // window exceeded: drop, peer retransmits
-  auto* ic = new InChunk{tsn, flags, stream, ppid, hold(data, dlen)};
+  auto* ic = new InChunk{tsn, flags, stream, ppid, hold(data, dlen), ssn, false};
   ooo_[tsn] = ic;
   ooo_bytes_ += dlen;
+  // Stream-independent delivery (RFC 9260 §6.6: order is per stream): a
+  // complete single-chunk message that is next in its own stream goes up now
+  // instead of waiting behind a gap in another stream's TSNs — so a lost bulk
+  // packet on one stream no longer holds back the tokens of the others.
+  if ((flags & 3) == 3) {
+    bool unordered = flags & 4;
+    if (unordered || ssn == next_ssn_in_[stream]) {
+      ic->delivered = true;
+      ooo_bytes_ -= dlen;
+      Bytes m = std::move(ic->data);
+      ic->data = Bytes();
+      stats_.early_deliveries++;
+      deliver_message(stream, ssn, unordered, ppid, std::move(m));
+    } else {
+      early_ready_[stream_ssn(stream, ssn)] = tsn;
+    }
+  }
 }
 
 void SctpAssociation::build_sack(std::vector<uint8_t>& b) {
@@ -832,7 +891,7 @@ void SctpAssociation::handle_forward_tsn(const uint8_t* c, size_t len) {
   if (!tsn_lt(peer_cum_tsn_, nc)) return;
   for (auto it = ooo_.begin(); it != ooo_.end();) {
     if (tsn_le(it->first, nc)) {
-      ooo_bytes_ -= it->second->data.size();
+      if (!it->second->delivered) ooo_bytes_ -= it->second->data.size();
       delete it->second;
       it = ooo_.erase(it);
     } else {
@@ -841,27 +900,11 @@ void SctpAssociation::handle_forward_tsn(const uint8_t* c, size_t len) {
   }
   peer_cum_tsn_ = nc;
   for (auto& kv : partial_u_) kv.second.active = false;
-  // Continue delivery of anything now contiguous.
-  while (!ooo_.empty()) {
-    auto it = ooo_.find(peer_cum_tsn_ + 1);
-    if (it == ooo_.end()) break;
-    InChunk* ic = it->second;
-    ooo_.erase(it);
-    ooo_bytes_ -= ic->data.size();
-    Bytes tmp = std::move(ic->data);
-    uint8_t fl = ic->flags;
-    uint16_t st = ic->stream;
-    uint32_t pp = ic->ppid;
-    delete ic;
-    // Re-enter the in-order path.
-    std::vector<uint8_t> hdr(12);
-    wr32(hdr.data(), peer_cum_tsn_ + 1);
-    wr16(hdr.data() + 4, st);
-    wr32(hdr.data() + 8, pp);
-    hdr.insert(hdr.end(), tmp.begin(), tmp.end());
-    Bytes whole = Bytes::take(std::move(hdr));
-    handle_data(fl, whole.data(), whole.size(), whole);
+  for (auto it = early_ready_.begin(); it != early_ready_.end();) {
+    if (!ooo_.count(it->second)) it = early_ready_.erase(it);
+    else ++it;
   }
+  drain_in_order();  // continue delivery of anything now contiguous
 }
 
 void SctpAssociation::handle_reconfig(const uint8_t* c, size_t len) {

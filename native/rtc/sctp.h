@@ -56,6 +56,7 @@ struct SctpStats {
   uint64_t data_chunks_sent = 0, data_chunks_received = 0;
   uint64_t retransmits = 0, fast_retransmits = 0, t3_expirations = 0;
   uint64_t tlp_probes = 0, rack_marks = 0, random_loss_events = 0;
+  uint64_t early_deliveries = 0;  // messages handed up ahead of a TSN gap (another stream's loss)
   uint64_t sacks_sent = 0, sacks_received = 0;
   uint64_t bytes_sent = 0, bytes_received = 0;
 };
@@ -145,6 +146,11 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   void queue_control(uint8_t type, uint8_t flags, std::vector<uint8_t> body);
   void build_sack(std::vector<uint8_t>& body);
   void deliver_ready();
+  void deliver_chunk(uint8_t fl, uint16_t st, uint16_t ssn, uint32_t pp, const Bytes& d);
+  void deliver_message(uint16_t st, uint16_t ssn, bool unordered, uint32_t pp, Bytes msg);
+  void release_ready(uint16_t st);
+  void drain_in_order();
+  static uint32_t stream_ssn(uint16_t st, uint16_t ssn) { return uint32_t(st) << 16 | ssn; }
   void update_rto(uint64_t rtt_us);
   void start_t3();
   void stop_t3();
@@ -226,6 +232,8 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   static constexpr size_t kReasmBuf = 65536 + 1024;
   std::map<uint16_t, Partial> partial_;  // per-stream reassembly (ordered)
   std::map<uint16_t, Partial> partial_u_;  // unordered
+  std::map<uint16_t, uint16_t> next_ssn_in_;      // per inbound stream: next SSN to deliver
+  std::map<uint32_t, uint32_t> early_ready_;      // (stream, ssn) -> TSN of a complete message held out of order
 
   std::vector<std::vector<uint8_t>> ctrl_;  // control chunks to bundle at next flush
   bool shutdown_requested_ = false;

@@ -44,6 +44,13 @@ class MessageChannel {
   // fraction of it queued in the channel, so on a slow path a token does
   // not wait behind a full 64 KiB of other streams' bodies.
   virtual size_t send_window_hint() const { return 0; }
+  // "multistream" extension: spread the frames of tunnel stream ids over
+  // `lanes` extra transport streams (SCTP streams delivered independently),
+  // so a loss on one stream's packets does not hold back the others. Frames of
+  // one tunnel stream always share a lane (their order is kept); stream 0
+  // (control) stays on the channel's own stream. Transports without
+  // independent streams ignore it.
+  virtual void set_lanes(int lanes) { (void)lanes; }
 
   // Message arrived (whole message, zero-copy view where possible).
   std::function<void(Bytes)> on_message;

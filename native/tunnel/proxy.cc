@@ -824,6 +824,8 @@ void ProxySession::on_agree(const proto::Frame& f) {
   shared_->cancel_feature =
       std::find(agree.features.begin(), agree.features.end(), "cancel") != agree.features.end();
   shared_->flow = std::find(agree.features.begin(), agree.features.end(), "flow") != agree.features.end();
+  if (std::find(agree.features.begin(), agree.features.end(), "multistream") != agree.features.end())
+    ch_->set_lanes(proto::kLanes);
   ready_ = true;
   shared_->ready = true;
   last_pong_ms_ = Reactor::now_ms();

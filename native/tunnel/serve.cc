@@ -418,6 +418,8 @@ void ServeSession::on_hello(const proto::Frame& f) {
   cancel_feature_ = std::find(agree.features.begin(), agree.features.end(), "cancel") != agree.features.end();
   flow_ = std::find(agree.features.begin(), agree.features.end(), "flow") != agree.features.end();
   sched_->send(proto::make_agree(agree));
+  if (std::find(agree.features.begin(), agree.features.end(), "multistream") != agree.features.end())
+    ch_->set_lanes(proto::kLanes);
   handshaken_ = true;
   LOG_INFO(kT, "sent AGREE, tunnel ready");
   if (cfg_.upstream_prewarm) command(0, Cmd{Cmd::Prewarm});
