@@ -54,11 +54,11 @@ class FrameScheduler {
   MessageChannel* channel() const { return ch_.get(); }
   size_t body_chunk() const { return ch_ ? ch_->body_chunk() : proto::kMaxBodyChunk; }
   // Bytes kept queued in the channel: the configured window, or a quarter of
-  // the transport's congestion window when that is smaller (at least 8 KiB),
+  // the transport's congestion window when that is smaller (at least 2 KiB),
   // so queued bulk ahead of a token stays below ~1/4 round trip of sending.
   size_t window() const {
     size_t h = ch_ ? ch_->send_window_hint() : 0;
-    return h ? std::min(window_, std::max<size_t>(8192, h / 4)) : window_;
+    return h ? std::min(window_, std::max<size_t>(2048, h / 4)) : window_;
   }
 
  private:
