@@ -21,9 +21,15 @@ profiles/bench_gpu_upstream_r01.json.)
   POST /v1/completions       (same, "prompt" instead of "messages")
   POST /api/generate         (Ollama NDJSON stream)
 
-Tokenisation is byte-level (prompt bytes mod vocab); generated ids are
-rendered as `` t<id>`` pieces — the model is random-init, the point is the
-serving path, not the text.
+Two model sources:
+
+* random-init (``--config tiny|small|micro``, the benchmark default): byte-level
+  prompts (bytes mod vocab), generated ids rendered as `` t<id>`` pieces;
+* a Hugging Face Llama-architecture checkpoint (``--checkpoint DIR``: config.json,
+  safetensors, tokenizer.json; loaded weights-only by ``checkpoint.py``): prompts
+  go through the checkpoint's tokenizer and chat template, tokens are
+  detokenised incrementally, and generation stops at the EOS token
+  (finish_reason "stop").
 """
 from __future__ import annotations
 
@@ -101,8 +107,10 @@ class Engine:
         if model is None:
             from p2p_llm_tunnel_amd.models.tiny_llm import TinyLlama
             model = TinyLlama(config, device=device, max_batch=max_batch, seed=seed, fused=True)
-        else:
-            use_graph = False
+        # hipGraphs need the real fused model on a HIP device (a loaded
+        # checkpoint qualifies; CPU stand-ins in tests run eagerly).
+        use_graph = use_graph and model.device.type == "cuda" and hasattr(model, "_decode_impl")
+        max_batch = getattr(model, "max_batch", max_batch)
         if not (1 <= max_batch <= rows and 1 <= small_rows <= rows):
             raise ValueError("need 1 <= max_batch <= rows and small_rows <= rows")
         self.model = model
@@ -160,11 +168,12 @@ class Engine:
                     req = self.pending.get_nowait()
                 except queue.Empty:
                     return
-                # Keep at least the prompt's first token: max_new is clamped
-                # so prompt + generated rows fit max_seq.
+                # max_new is clamped so prompt + generated rows fit max_seq; a
+                # prompt too long for the rest keeps its end (for a chat, the
+                # latest turns and the generation prompt).
                 max_seq = self.model.cfg.max_seq
                 req.max_new = max(1, min(req.max_new, max_seq - 2))
-                ids = req.prompt[: max_seq - req.max_new - 1] or [0]
+                ids = req.prompt[-(max_seq - req.max_new - 1):] or [0]
                 self.slots[i] = {"req": req, "pos": 0, "ids": ids, "gen": 0}
 
     def _plan(self, batch: list):
@@ -325,12 +334,22 @@ class Engine:
             self.deliver(batch)
 
 
-def _prompt_ids(body: dict) -> list[int]:
+def _prompt_ids(body: dict, tok=None) -> list[int]:
+    msgs = body.get("messages")
+    if tok is not None:
+        if isinstance(msgs, list):
+            return tok.chat([m for m in msgs if isinstance(m, dict)]) or [0]
+        return tok.encode(str(body.get("prompt", ""))) or [0]
     if "messages" in body:
-        text = "\n".join(str(m.get("content", "")) for m in body.get("messages", []))
+        text = "\n".join(str(m.get("content", "")) for m in body.get("messages", []) if isinstance(m, dict))
     else:
         text = str(body.get("prompt", ""))
     return list(text.encode("utf-8"))[:512] or [1]
+
+
+def _piece(text: str) -> bytes:
+    """A text piece as the inside of a JSON string."""
+    return json.dumps(text, ensure_ascii=False)[1:-1].encode()
 
 
 def _chunk(data: bytes) -> bytes:
@@ -341,14 +360,16 @@ class _Stream:
     """Per-request output state on the I/O thread: the writer and the byte
     template around each token piece (token ids render as " t<id>": no JSON
     escaping needed)."""
-    __slots__ = ("writer", "stream", "kind", "rid", "pre", "post", "toks", "done")
+    __slots__ = ("writer", "stream", "kind", "rid", "pre", "post", "toks", "done", "detok", "reason")
 
-    def __init__(self, writer, stream, kind, rid, model):
+    def __init__(self, writer, stream, kind, rid, model, detok=None):
         self.writer = writer
         self.stream = stream
         self.kind = kind  # "chat" | "text" | "ollama"
         self.rid = rid
-        self.toks = []
+        self.toks = []  # non-streamed: rendered pieces (bytes, JSON-escaped when detokenised)
+        self.detok = detok  # checkpoint tokenizer: incremental text of this request
+        self.reason = "length"
         self.done = asyncio.get_running_loop().create_future()
         m = json.dumps(model)
         if kind == "chat":
@@ -367,9 +388,11 @@ class _Stream:
 class FrontEnd:
     """HTTP/1.1 server on one asyncio thread (see the module docstring)."""
 
-    def __init__(self, engine: Engine, host: str, port: int, model_name: str):
+    def __init__(self, engine: Engine, host: str, port: int, model_name: str, tokenizer=None):
         self.engine = engine
         self.model_name = model_name
+        self.tok = tokenizer
+        self.eos = tokenizer.eos_ids if tokenizer is not None else frozenset()
         self.loop = asyncio.new_event_loop()
         self._ready = threading.Event()
         self._err = None
@@ -413,10 +436,23 @@ class FrontEnd:
                 continue
             if tok is None:
                 self._finish(req, st)
-            elif st.stream:
-                st.writer.write(_chunk(b"%s t%d%s" % (st.pre, tok, st.post)))
+                continue
+            if tok in self.eos:  # stop: the engine frees the slot on its next step
+                req.cancelled = True
+                st.reason = "stop"
+                self._finish(req, st)
+                continue
+            if st.detok is not None:
+                piece = st.detok.push(tok)
+                if not piece:
+                    continue
+                body = _piece(piece)
             else:
-                st.toks.append(tok)
+                body = b" t%d" % tok
+            if st.stream:
+                st.writer.write(_chunk(st.pre + body + st.post))
+            else:
+                st.toks.append(body)
 
     def _finish(self, req, st):
         w = st.writer
@@ -424,25 +460,25 @@ class FrontEnd:
             if st.kind == "ollama":
                 tail = _chunk((json.dumps({"model": self.model_name, "response": "", "done": True}) + "\n").encode())
             else:
-                fin = {"index": 0, "delta": {}, "finish_reason": "length"} if st.kind == "chat" else \
-                    {"index": 0, "text": "", "finish_reason": "length"}
+                fin = {"index": 0, "delta": {}, "finish_reason": st.reason} if st.kind == "chat" else \
+                    {"index": 0, "text": "", "finish_reason": st.reason}
                 obj = {"id": st.rid, "object": "chat.completion.chunk" if st.kind == "chat" else "text_completion",
                        "choices": [fin]}
                 tail = _chunk(f"data: {json.dumps(obj)}\n\n".encode()) + _chunk(b"data: [DONE]\n\n")
             w.write(tail + b"0\r\n\r\n")
         else:
-            text = "".join(f" t{t}" for t in st.toks)
+            text = json.loads(b'"' + b"".join(st.toks) + b'"')
             if st.kind == "ollama":
                 obj = {"model": self.model_name, "response": text, "done": True}
             elif st.kind == "chat":
                 obj = {"id": st.rid, "object": "chat.completion", "model": self.model_name,
                        "choices": [{"index": 0, "message": {"role": "assistant", "content": text},
-                                    "finish_reason": "length"}],
-                       "usage": {"prompt_tokens": len(req.prompt), "completion_tokens": len(st.toks),
-                                 "total_tokens": len(req.prompt) + len(st.toks)}}
+                                    "finish_reason": st.reason}],
+                       "usage": {"prompt_tokens": len(req.prompt), "completion_tokens": req.generated,
+                                 "total_tokens": len(req.prompt) + req.generated}}
             else:
                 obj = {"id": st.rid, "object": "text_completion", "model": self.model_name,
-                       "choices": [{"index": 0, "text": text, "finish_reason": "length"}]}
+                       "choices": [{"index": 0, "text": text, "finish_reason": st.reason}]}
             w.write(self._json_response(obj))
         st.done.set_result(True)
 
@@ -550,8 +586,9 @@ class FrontEnd:
         kind = "ollama" if ollama else ("chat" if "chat" in path else "text")
         stream = bool(req_body.get("stream", ollama))
         rid = ("chatcmpl-" if kind == "chat" else "cmpl-") + uuid.uuid4().hex[:12]
-        req = Request(_prompt_ids(req_body), max(1, min(max_new, 1024)), batched=True)
-        st = _Stream(writer, stream, kind, rid, name)
+        prompt = _prompt_ids(req_body, self.tok)
+        req = Request(prompt, max(1, min(max_new, 1024)), batched=True)
+        st = _Stream(writer, stream, kind, rid, name, self.tok.detokenizer(prompt) if self.tok is not None else None)
         req.state = st
         if stream:
             writer.write(b"HTTP/1.1 200 OK\r\nContent-Type: %s\r\nCache-Control: no-cache\r\n"
@@ -562,12 +599,24 @@ class FrontEnd:
 
 
 def start_server(host="127.0.0.1", port=0, device="cuda:0", config="tiny", max_batch=8, model_name=None,
-                 engine: Engine | None = None):
+                 engine: Engine | None = None, checkpoint: str | None = None, max_seq: int | None = None,
+                 tokenizer=None):
     """Engine + HTTP front-end; returns (server, port, engine). ``server.shutdown()``
-    stops the HTTP side, ``engine.stop()`` the GPU side."""
+    stops the HTTP side, ``engine.stop()`` the GPU side. ``checkpoint``: serve a
+    Hugging Face Llama checkpoint directory (weights + tokenizer) instead of
+    the random-init ``config``. ``tokenizer`` (a ``checkpoint.Tokenizer``)
+    overrides the checkpoint's own or gives an injected engine a text side."""
     sys.setswitchinterval(0.0005)  # two busy threads: bound a GIL wait at 0.5 ms, not 5
+    tok = tokenizer
+    if checkpoint and engine is None:
+        import os
+        from p2p_llm_tunnel_amd.models.checkpoint import Tokenizer, load_llama
+        model = load_llama(checkpoint, device=device, max_batch=max_batch, max_seq=max_seq)
+        tok = tok or Tokenizer.for_checkpoint(checkpoint)
+        engine = Engine(device=device, max_batch=max_batch, model=model)
+        model_name = model_name or os.path.basename(os.path.normpath(checkpoint))
     engine = engine or Engine(device=device, config=config, max_batch=max_batch)
-    srv = FrontEnd(engine, host, port, model_name or f"p2pt-{config}")
+    srv = FrontEnd(engine, host, port, model_name or f"p2pt-{config}", tokenizer=tok)
     return srv, srv.server_address[1], engine
 
 
@@ -584,6 +633,8 @@ def _replicas(a) -> int:
     for i in range(a.gpus):
         cmd = [sys.executable, "-m", "p2p_llm_tunnel_amd.models.server", "--host", a.host, "--port", str(base + i),
                "--device", f"cuda:{i}", "--config", a.config, "--max-batch", str(a.max_batch)]
+        if a.checkpoint:
+            cmd += ["--checkpoint", a.checkpoint] + (["--max-seq", str(a.max_seq)] if a.max_seq else [])
         procs.append(subprocess.Popen(cmd))
     ups = ",".join(f"http://{a.host}:{base + i}" for i in range(a.gpus))
     print(f"{a.gpus} inference endpoints; use: tunnel serve --upstream {ups}", flush=True)
@@ -610,13 +661,18 @@ def main(argv=None):
     ap.add_argument("--device", default="cuda:0")
     ap.add_argument("--config", default="tiny")
     ap.add_argument("--max-batch", type=int, default=8)
+    ap.add_argument("--checkpoint", default=None,
+                    help="Hugging Face Llama checkpoint directory (config.json, *.safetensors, tokenizer.json)")
+    ap.add_argument("--max-seq", type=int, default=None, help="KV-cache length per slot (checkpoint default: "
+                    "min(max_position_embeddings, 8192))")
     ap.add_argument("--gpus", type=int, default=0,
                     help="spawn one endpoint per GPU (cuda:0..N-1) on consecutive ports instead of serving here")
     a = ap.parse_args(argv)
     if a.gpus > 0:
         raise SystemExit(_replicas(a))
-    srv, port, engine = start_server(a.host, a.port, a.device, a.config, a.max_batch)
-    print(f"inference endpoint on http://{a.host}:{port} ({a.config}, {a.device})", flush=True)
+    srv, port, engine = start_server(a.host, a.port, a.device, a.config, a.max_batch, checkpoint=a.checkpoint,
+                                     max_seq=a.max_seq)
+    print(f"inference endpoint on http://{a.host}:{port} ({a.checkpoint or a.config}, {a.device})", flush=True)
     try:
         threading.Event().wait()
     except KeyboardInterrupt:

@@ -53,13 +53,21 @@ CONFIGS = {
 
 class TinyLlama:
     def __init__(self, cfg: LlamaConfig | str = "tiny", device="cuda", max_batch: int = 8, seed: int = 0,
-                 fused: bool = True):
+                 fused: bool = True, weights: dict | None = None):
+        """Random-init weights from ``seed``, or ``weights`` (embed, final_norm,
+        lm_head, layers[{attn_norm, wqkv, wo, ffn_norm, w_gate_up, w_down}],
+        bf16 on ``device``) — see ``checkpoint.load_llama``."""
         self.cfg = CONFIGS[cfg] if isinstance(cfg, str) else cfg
         self.fused = fused
         self._fused = None
         c = self.cfg
         self.device = torch.device(device)
         self.max_batch = max_batch
+        if weights is not None:
+            self.embed, self.final_norm, self.lm_head = weights["embed"], weights["final_norm"], weights["lm_head"]
+            self.layers = weights["layers"]
+            self._alloc_caches()
+            return
         g = torch.Generator(device="cpu").manual_seed(seed)
 
         def w(*shape, scale):
@@ -82,9 +90,17 @@ class TinyLlama:
             })
         self.final_norm = norm_w(c.dim)
         self.lm_head = w(c.vocab, c.dim, scale=1 / math.sqrt(c.dim))
+        self._alloc_caches()
+
+    @classmethod
+    def from_weights(cls, cfg: LlamaConfig, weights: dict, device="cuda", max_batch: int = 8, fused: bool = True):
+        return cls(cfg, device=device, max_batch=max_batch, fused=fused, weights=weights)
+
+    def _alloc_caches(self):
+        c = self.cfg
         # One spare slot (index max_batch) absorbs the K/V writes of padding rows.
-        self.scratch_slot = max_batch
-        cache_shape = (c.n_layers, max_batch + 1, c.max_seq, c.n_kv_heads, c.head_dim)
+        self.scratch_slot = self.max_batch
+        cache_shape = (c.n_layers, self.max_batch + 1, c.max_seq, c.n_kv_heads, c.head_dim)
         self.k_cache = torch.zeros(cache_shape, dtype=torch.bfloat16, device=self.device)
         self.v_cache = torch.zeros(cache_shape, dtype=torch.bfloat16, device=self.device)
 
