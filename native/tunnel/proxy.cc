@@ -702,8 +702,9 @@ void ProxySession::release_links(const std::string& fail_why) {
   links_.clear();
   for (size_t k = 0; k < links.size(); k++) {
     links[k].to.reset();
-    std::shared_ptr<ProxyWorker> w = std::move(links[k].worker);
-    auto finish = [w, fail_why]() mutable {
+    // The task owns the only reference (moved in), so the worker is destroyed
+    // on its own thread, never by this loop's scope.
+    auto finish = [w = std::move(links[k].worker), fail_why]() mutable {
       if (!fail_why.empty()) w->fail_all(fail_why);
       Reactor& wr = w->reactor();
       wr.post([w]() mutable { w.reset(); });

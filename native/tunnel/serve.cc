@@ -308,8 +308,9 @@ void ServeSession::release_links() {
     if (k == 0) {
       links[k].worker.reset();
     } else {
-      std::shared_ptr<ServeWorker> w = std::move(links[k].worker);
-      links[k].r->post_threadsafe([w]() mutable { w.reset(); });
+      // Moved, not copied, into the task: the last reference must drop on the
+      // worker's own thread (its Pipe unhooks from that thread's reactor).
+      links[k].r->post_threadsafe([w = std::move(links[k].worker)]() mutable { w.reset(); });
     }
   }
 }
