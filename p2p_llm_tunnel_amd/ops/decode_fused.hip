@@ -86,6 +86,13 @@ struct GemmArgs {
   int ks;
   float* kpart;     // [tiles][ks][TN][4][64]
   unsigned* kctr;   // [tiles] arrival tickets (self-resetting)
+  // Column-tile width 2^cwl (16, 8 or 4 output columns per 16-lane MFMA
+  // subtile). Narrower tiles put a small-N projection on more workgroups, so
+  // its weight stream spreads over every CU (one CU streams ~10 B/cycle, a
+  // 2048-wide projection in 16-column tiles reached only 128 of the 256 CUs).
+  // Lanes c and c + 2^cwl load the same weight row in the same instruction
+  // (one fetch); their duplicate MFMA columns are dropped in the epilogue.
+  int cwl;
 };
 
 __device__ __forceinline__ frag8 as_frag(const uint4& v) { return __builtin_bit_cast(frag8, v); }
@@ -100,7 +107,6 @@ __device__ __forceinline__ float dot2_bf16(uint32_t a, uint32_t b, float c) {
 // same weights back to back, and models up to the 256 MB MALL keep them
 // resident between steps (non-temporal loads measured 1.75x slower on the
 // 4-layer config, and no faster on the 0.85 GB one).
-__device__ __forceinline__ uint4 ld_stream(const uint16_t* p) { return *reinterpret_cast<const uint4*>(p); }
 
 // Cross-workgroup hand-off without L2 write-back/invalidate fences: payload
 // stores are agent-scope relaxed atomics (write-through, `sc1`), drained with
@@ -121,43 +127,80 @@ __device__ __forceinline__ unsigned arrive(unsigned* ctr) {
   return __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Output column of lane column c (0..15) in subtile t of block bx.
+// Output column of lane column c (0..15) in subtile t of block bx, for
+// subtiles of 2^cwl distinct columns (lanes past 2^cwl repeat them).
 template <int TN>
-__device__ __forceinline__ int tile_col(int bx, int t, int c) {
-  return ((bx * TN + t) << 4) + c;
+__device__ __forceinline__ int tile_col(int bx, int t, int c, int cwl) {
+  return ((bx * TN + t) << cwl) + (c & ((1 << cwl) - 1));
 }
 
-// One batch of up to UM consecutive 32-wide k-steps [s, min(s + UM, s1)): every
-// load is issued before the first MFMA (one memory round trip per batch).
-// Steps past s1 re-load the last step (cache hits) with a zeroed A fragment,
-// so the code is branch-free and the waits are static.
+// Operand loads go through buffer descriptors (wave-uniform base and size
+// from the kernel arguments): a lane whose byte offset lies past the buffer
+// gets zeros from the range check without a memory access. Rows past M and
+// k-steps past a wave's share use that (kOob), so a batch is branch-free and a
+// decode step at batch 1 fetches its one activation row once per k-step
+// instead of for all 16 MFMA rows.
+constexpr uint32_t kOob = 0x80000000u;  // host keeps every operand below 2 GiB
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 buf_ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+// One batch of up to UM consecutive 32-wide k-steps [s, min(s + UM, s1)):
+// every load of the batch is issued before any of it is used.
 template <int UM, int TN>
-__device__ __forceinline__ void mma_batch(frag4 (&acc)[TN], const uint16_t* xrow, const uint16_t* const (&wrow)[TN],
-                                          bool a_ok, int s, int s1) {
-  uint4 bv[UM][TN], av[UM];
+struct Batch {
+  uint4 b[UM][TN];
+  uint4 a[UM];
+};
+
+template <int UM, int TN>
+__device__ __forceinline__ void load_batch(Batch<UM, TN>& bt, __amdgpu_buffer_rsrc_t ra, uint32_t xoff,
+                                           __amdgpu_buffer_rsrc_t rw, const uint32_t (&woff)[TN], int s, int s1) {
 #pragma unroll
   for (int u = 0; u < UM; u++) {
-    const int su = min(s + u, s1 - 1) * 32;
+    const bool in = s + u < s1;
+    const uint32_t su = uint32_t(s + u) * 64u;  // bytes per 32-wide k-step
 #pragma unroll
-    for (int t = 0; t < TN; t++) bv[u][t] = ld_stream(wrow[t] + su);
+    for (int t = 0; t < TN; t++) bt.b[u][t] = buf_ld16(rw, in ? woff[t] + su : kOob);
+    bt.a[u] = buf_ld16(ra, in ? xoff + su : kOob);
   }
-#pragma unroll
-  for (int u = 0; u < UM; u++) {
-    const int su = min(s + u, s1 - 1) * 32;
-    const uint4 x = *reinterpret_cast<const uint4*>(xrow + su);
-    av[u] = (a_ok && s + u < s1) ? x : make_uint4(0, 0, 0, 0);
-  }
+}
+
+template <int UM, int TN>
+__device__ __forceinline__ void mma_apply(frag4 (&acc)[TN], const Batch<UM, TN>& bt) {
 #pragma unroll
   for (int u = 0; u < UM; u++)
 #pragma unroll
     for (int t = 0; t < TN; t++)
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(av[u]), as_frag(bv[u][t]), acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(bt.a[u]), as_frag(bt.b[u][t]), acc[t], 0, 0, 0);
 }
 
-// Skinny GEMM + fused epilogue. NW waves split K; TN 16-column subtiles per
-// block; UM k-steps per load batch (host: >= each wave's share when possible).
-// ROPE and SILU take weights whose rows are interleaved in pairs (RoPE
-// partners d, d + D/2 of a head; gate_j, up_j), so a pair sits in lanes c, c^1.
+// The wave's k-steps [s0, s1), one batch at a time. (A two-deep batch
+// pipeline measured no faster on the down projection and 44 % slower on the LM
+// head, whose doubled registers halved the resident workgroups per CU: on
+// these kernels memory parallelism comes from resident waves.)
+template <int UM, int TN>
+__device__ __forceinline__ void mma_stream(frag4 (&acc)[TN], __amdgpu_buffer_rsrc_t ra, uint32_t xoff,
+                                           __amdgpu_buffer_rsrc_t rw, const uint32_t (&woff)[TN], int s0, int s1) {
+  for (int s = s0; s < s1; s += UM) {
+    Batch<UM, TN> p;
+    load_batch<UM, TN>(p, ra, xoff, rw, woff, s, s1);
+    // Keep every load of the batch ahead of the first MFMA: left alone, the
+    // scheduler interleaves them and the batch pays several memory latencies.
+    __builtin_amdgcn_sched_barrier(0);
+    mma_apply<UM, TN>(acc, p);
+  }
+}
+
+// Skinny GEMM + fused epilogue. NW waves split K; TN subtiles of 2^cwl
+// columns per block; UM k-steps per load batch (host: >= each wave's share
+// when possible). ROPE and SILU take weights whose rows are interleaved in
+// pairs (RoPE partners d, d + D/2 of a head; gate_j, up_j), so a pair sits in
+// lanes c, c^1.
 template <int NW, int TN, int EPI, int UM>
 __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
   __shared__ float red[NW][TN][4][kWave];
@@ -191,17 +234,41 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
   const int S = a.K >> 5;
   const int b0 = kslice * S / a.ks, bs = (kslice + 1) * S / a.ks - b0;  // this workgroup's k-steps
   const int s0 = b0 + wv * bs / NW, s1 = b0 + (wv + 1) * bs / NW;
-  // Rows past M are loaded from row M-1 (in bounds) and zeroed: the batch's
-  // loads are unconditional.
-  const uint16_t* xrow = a.x + size_t(min(m0 + m_a, a.M - 1)) * a.K + kq;
-  const uint16_t* wrow[TN];
+  // Byte offsets of this lane's A row and weight rows at k-step 0; rows past
+  // M read as zeros (kOob).
+  const __amdgpu_buffer_rsrc_t ra = rsrc(a.x, uint32_t(a.M) * uint32_t(a.K) * 2u);
+  const __amdgpu_buffer_rsrc_t rw = rsrc(a.w, uint32_t(a.N) * uint32_t(a.K) * 2u);
+  const uint32_t xoff = a_ok ? (uint32_t(m0 + m_a) * uint32_t(a.K) + uint32_t(kq)) * 2u : kOob;
+  uint32_t woff[TN];
 #pragma unroll
-  for (int t = 0; t < TN; t++) wrow[t] = a.w + size_t(tile_col<TN>(bx, t, lane & 15)) * a.K + kq;
+  for (int t = 0; t < TN; t++)
+    woff[t] = (uint32_t(tile_col<TN>(bx, t, lane & 15, a.cwl)) * uint32_t(a.K) + uint32_t(kq)) * 2u;
+
+  // C layout: row m = m0 + 4*(lane>>4) + r, column = tile_col(.., lane & 15).
+  const int lrow0 = (lane >> 4) << 2, mrow0 = m0 + lrow0;
+  const int c = lane & 15;
+  const bool col_ok = c < (1 << a.cwl);  // lanes past the tile width repeat its columns
+
+  // RESID: the residual values this lane's epilogue updates, loaded by wave 0
+  // ahead of the weight stream (they do not depend on it) instead of after
+  // the reduction, which would add a dependent memory round trip.
+  float rprev[EPI == EPI_RESID ? TN : 1][4];
+  if constexpr (EPI == EPI_RESID) {
+    if (wv == 0) {
+#pragma unroll
+      for (int t = 0; t < TN; t++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int m = min(mrow0 + r, a.M - 1);
+          rprev[t][r] = bf2f(a.out[size_t(m) * a.N + tile_col<TN>(bx, t, c, a.cwl)]);
+        }
+    }
+  }
 
   frag4 acc[TN];
 #pragma unroll
   for (int t = 0; t < TN; t++) acc[t] = frag4{0.f, 0.f, 0.f, 0.f};
-  for (int s = s0; s < s1; s += UM) mma_batch<UM, TN>(acc, xrow, wrow, a_ok, s, s1);
+  mma_stream<UM, TN>(acc, ra, xoff, rw, woff, s0, s1);
 
   if (norm) {
     float ssum = 0.f;
@@ -249,9 +316,6 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
     if (lane == 0) st_wt(&a.kctr[bx], 0u);
   }
 
-  // C layout: row m = m0 + 4*(lane>>4) + r, column = tile_col(.., lane & 15).
-  const int lrow0 = (lane >> 4) << 2, mrow0 = m0 + lrow0;
-  const int c = lane & 15;
   if (norm) {
     float ssum = 0.f;
 #pragma unroll
@@ -277,12 +341,12 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
     }
 #pragma unroll
     for (int t = 0; t < TN; t++) {
-      const int n = tile_col<TN>(bx, t, c);
+      const int n = tile_col<TN>(bx, t, c, a.cwl);
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         const int m = mrow0 + r;
         const float lv = bf_round(v[t][r]);
-        if (m < a.M) a.out[size_t(m) * a.N + n] = uint16_t(f2bf_bits(lv));
+        if (m < a.M && col_ok) a.out[size_t(m) * a.N + n] = uint16_t(f2bf_bits(lv));
         if (lv > best[r] || (lv == best[r] && n < bi[r])) {
           best[r] = lv;
           bi[r] = n;
@@ -301,18 +365,18 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
     }
   } else if constexpr (EPI == EPI_SILU) {
     // Interleaved rows: even lane = gate_j, odd lane = up_j, j = column / 2.
-    const int n = tile_col<TN>(bx, 0, c);
+    const int n = tile_col<TN>(bx, 0, c, a.cwl);
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const float mine = bf_round(v[0][r]);
       const float other = dpp<kDppXor1>(mine);
-      if ((c & 1) || mrow0 + r >= a.M) continue;
+      if ((c & 1) || !col_ok || mrow0 + r >= a.M) continue;
       a.out[size_t(mrow0 + r) * (a.N >> 1) + (n >> 1)] = uint16_t(f2bf_bits(mine / (1.f + __expf(-mine)) * other));
     }
   } else if constexpr (EPI == EPI_ROPE) {
     // Interleaved rows within each head: column 2i = dim i, 2i+1 = dim i + D/2.
     const int half = a.D >> 1;
-    const int col = tile_col<TN>(bx, 0, c);
+    const int col = tile_col<TN>(bx, 0, c, a.cwl);
     const int head = col / a.D, i = (col % a.D) >> 1;
     const bool second = c & 1;
     const float inv_freq = exp2f(-a.log2_theta * (2.f * i) / a.D);
@@ -321,7 +385,7 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
       const int m = mrow0 + r;
       const float mine = bf_round(v[0][r]);
       const float other = dpp<kDppXor1>(mine);
-      if (m >= a.M) continue;
+      if (m >= a.M || !col_ok) continue;
       // Host validates; clamped anyway so a bad index can never write outside the cache.
       const int p = min(max(a.pos[m], 0), a.Smax - 1);
       const int sl = a.slot ? min(max(a.slot[m], 0), a.nslots - 1) : m;
@@ -342,14 +406,13 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
     float sq[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < TN; t++) {
-      const int n = tile_col<TN>(bx, t, c);
+      const int n = tile_col<TN>(bx, t, c, a.cwl);
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         const int m = mrow0 + r;
-        if (m >= a.M) continue;
-        uint16_t* p = a.out + size_t(m) * a.N + n;
-        const float nv = bf_round(bf2f(*p) + bf_round(v[t][r]));
-        *p = uint16_t(f2bf_bits(nv));
+        if (m >= a.M || !col_ok) continue;
+        const float nv = bf_round(rprev[t][r] + bf_round(v[t][r]));
+        a.out[size_t(m) * a.N + n] = uint16_t(f2bf_bits(nv));
         sq[r] += nv * nv;
       }
     }
@@ -455,8 +518,8 @@ __global__ __launch_bounds__(512) void k_attn(const uint16_t* __restrict__ q, co
                                               const int* __restrict__ slot, int nslots, float* __restrict__ part_o,
                                               float* __restrict__ part_ml, unsigned* __restrict__ counters,
                                               uint16_t* __restrict__ out, int H, int Hkv, int Smax, int nsplit,
-                                              float scale) {
-  constexpr int TOK = 32, NWV = 8, MINSPAN = TOK * NWV;
+                                              float scale, int min_span) {
+  constexpr int TOK = 32, NWV = 8;
   constexpr int DPL = D / kWave;  // merges: dims per lane
   constexpr int MAXC = 16;        // partials merged per load batch
   constexpr int LPR = D / 8, RPI = kWave / LPR, NI = TOK / RPI;
@@ -467,7 +530,7 @@ __global__ __launch_bounds__(512) void k_attn(const uint16_t* __restrict__ q, co
   const int b = blockIdx.y / Hkv, kvh = blockIdx.y % Hkv;
   const int len = min(max(pos[b], 0), Smax - 1) + 1;
   int span = (len + gridDim.x - 1) / gridDim.x;
-  span = max(MINSPAN, (span + TOK - 1) / TOK * TOK);
+  span = max(min_span, (span + TOK - 1) / TOK * TOK);
   const int nact = (len + span - 1) / span;  // slots with tokens
   const int sl = blockIdx.x;
   if (sl >= nact) return;
@@ -658,11 +721,27 @@ __global__ __launch_bounds__(512) void k_attn(const uint16_t* __restrict__ q, co
   if (threadIdx.x == 0) st_wt(&counters[blockIdx.y], 0u);
 }
 
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return (e && *e) ? atoi(e) : dflt;
+}
+
 // Span slots per (row, KV head): about one round of workgroups on the chip,
 // at most the workspace's partial slots.
 int attn_slots(int B, int Hkv, int nsplit_ws) {
+  static const int cap = env_int("P2PT_ATTN_SLOTS", 16);
   int sl = 256 / std::max(1, B * Hkv);
-  return std::max(1, std::min({sl, 16, nsplit_ws}));
+  return std::max(1, std::min({sl, cap, nsplit_ws}));
+}
+
+// Smallest token span of one attention workgroup (a multiple of its 32-token
+// wave piece). 64 (two busy waves per workgroup) puts a short context on 4x
+// the workgroups of 256 (one piece per wave): at batch 1 and 1k tokens the
+// decode step went 396 -> 380 us on MI355X, unchanged at batch 16
+// (profiles/r02/decode/decode_sweep_s4.log). P2PT_ATTN_MINSPAN overrides.
+int attn_min_span() {
+  static const int v = std::max(32, env_int("P2PT_ATTN_MINSPAN", 64) / 32 * 32);
+  return v;
 }
 
 // ------------------------------------------------------------ host side
@@ -674,6 +753,10 @@ struct LlamaDims {
 constexpr int kChunk = 64;  // tokens per attention workgroup = workspace granularity of its partials
 constexpr int kTnResid = 1, kTnStore = 2;  // LM head: two 16-column subtiles per block
 constexpr int kMaxKs = 8;    // split-K ways over workgroups
+// O / down projections: 16-column tiles too. Narrowing them to one workgroup
+// per CU (256) measured 1-4 % slower end to end once operands went through
+// buffer loads (profiles/r02/decode/decode_sweep_*.log, "min256" vs "cw16").
+constexpr int kResidMinTiles = 0;
 
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -702,7 +785,7 @@ Workspace carve(const LlamaDims& d, uint8_t* base) {
   w.q = reinterpret_cast<uint16_t*>(take(size_t(kMaxM) * d.H * d.D * 2));
   w.attn = reinterpret_cast<uint16_t*>(take(size_t(kMaxM) * d.H * d.D * 2));
   w.h = reinterpret_cast<uint16_t*>(take(size_t(kMaxM) * d.ffn * 2));
-  w.ss = reinterpret_cast<float*>(take(size_t(ss_parts > 1 ? ss_parts : 1) * kMaxM * 4));
+  w.ss = reinterpret_cast<float*>(take(size_t(ss_parts > 1 ? ss_parts : 1) * kMaxM * 4 * 4));  // up to 4-column tiles
   w.part_o = reinterpret_cast<float*>(take(size_t(kMaxM) * d.H * nsplit * d.D * 4));
   w.part_ml = reinterpret_cast<float*>(take(size_t(kMaxM) * d.H * nsplit * 2 * 4));
   w.am_val = reinterpret_cast<float*>(take(size_t(am_parts) * kMaxM * 4));
@@ -747,7 +830,11 @@ template <int NW, int TN, int EPI>
 hipError_t launch_nw(const GemmArgs& a, int grid, hipStream_t s) {
   // Load batch: each wave's share of k-steps, rounded up to a power of two,
   // capped by the VGPR budget (8, or 4 for 1024-thread two-subtile blocks).
-  constexpr int kCap = (NW >= 16 && TN >= 2) ? 4 : 8;
+  // Batches of at most 4 k-steps: fewer registers, more resident waves (batch
+  // 1: 396 -> 389 us per step, batch 16 unchanged; P2PT_DECODE_UMCAP=8 restores
+  // 8-step batches).
+  static const int ucap = env_int("P2PT_DECODE_UMCAP", 4);
+  const int kCap = ((NW >= 16 && TN >= 2) || ucap <= 4) ? 4 : 8;
   const int per_wave = ((a.K >> 5) / a.ks + NW - 1) / NW;
   const dim3 g(grid * a.ks, (a.M + 15) >> 4), b(NW * 64);
   if (per_wave <= 1)
@@ -757,15 +844,32 @@ hipError_t launch_nw(const GemmArgs& a, int grid, hipStream_t s) {
   else if (per_wave <= 4 || kCap == 4)
     hipLaunchKernelGGL((k_skinny<NW, TN, EPI, 4>), g, b, 0, s, a);
   else
-    hipLaunchKernelGGL((k_skinny<NW, TN, EPI, (kCap > 4 ? 8 : 4)>), g, b, 0, s, a);
+    hipLaunchKernelGGL((k_skinny<NW, TN, EPI, 8>), g, b, 0, s, a);
   return hipGetLastError();
 }
 
-// grid = column tiles; the launch has grid * a.ks workgroups (a.ks == 0: pick).
+// Column-tile width (log2) for an N-column projection with TN subtiles per
+// workgroup: the widest tile (16) that still gives >= min_tiles workgroups,
+// down to 4 columns (P2PT_DECODE_MIN_TILES overrides the threshold; 0: always
+// 16). Measured on MI355X (profiles/r02/decode/): narrower tiles win a
+// little on the O projection alone (5.8 -> 5.5 us at batch 1) and lose on QKV
+// (6.1 -> 7.8 us), where the repeated activation loads cost more than the
+// extra CUs win; 16 everywhere is fastest end to end.
+int pick_cwl(int N, int TN, int dflt_min_tiles) {
+  static const int env = env_int("P2PT_DECODE_MIN_TILES", -1);
+  const int min_tiles = env >= 0 ? env : dflt_min_tiles;
+  int cwl = 4;
+  while (cwl > 2 && (N >> cwl) / TN < min_tiles) cwl--;
+  return cwl;
+}
+
+// grid = column tiles of the chosen width; the launch has grid * a.ks workgroups (a.ks == 0: pick).
 template <int EPI, int TN>
-hipError_t launch_gemm(GemmArgs a, int grid, hipStream_t s, int nw_override = 0) {
-  if (a.ks <= 0) a.ks = (a.kpart && a.kctr) ? pick_ks(grid, a.K) : 1;
-  if (a.M > 16) a.ks = 1;  // split-K slabs and tickets are per column tile: one row tile only
+hipError_t launch_gemm(GemmArgs a, hipStream_t s, int nw_override = 0) {
+  if (a.cwl <= 0) a.cwl = pick_cwl(a.N, TN, 0);
+  const int grid = a.N / (TN << a.cwl);
+  if (a.ks <= 0) a.ks = (a.kpart && a.kctr && a.cwl == 4) ? pick_ks(grid, a.K) : 1;
+  if (a.M > 16 || a.cwl != 4) a.ks = 1;  // split-K slabs and tickets: one row tile of 16-column tiles only
   const int nw = nw_override ? nw_override : pick_nw((a.K >> 5) / a.ks);
   if (nw == 16) return launch_nw<16, TN, EPI>(a, grid, s);
   if (nw == 8) return launch_nw<8, TN, EPI>(a, grid, s);
@@ -775,6 +879,9 @@ hipError_t launch_gemm(GemmArgs a, int grid, hipStream_t s, int nw_override = 0)
 
 bool dims_ok(const LlamaDims& d) {
   if (d.D != 64 && d.D != 128) return false;
+  // GEMM operands are addressed with 32-bit byte offsets below kOob (2 GiB)
+  const size_t widest = std::max({size_t(d.vocab), size_t(2) * d.ffn, size_t(d.H + 2 * d.Hkv) * d.D, size_t(d.dim)});
+  if (widest * size_t(std::max({d.dim, d.ffn, d.H * d.D})) * 2 >= kOob) return false;
   if (d.H % d.Hkv || (d.H / d.Hkv != 1 && d.H / d.Hkv != 2 && d.H / d.Hkv != 4 && d.H / d.Hkv != 8)) return false;
   if (d.dim % 32 || (d.H * d.D) % 32 || d.ffn % 32) return false;
   if (d.dim % (16 * kTnResid) || d.vocab % (16 * kTnStore) || d.ffn % 16) return false;
@@ -846,7 +953,7 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
     a.pos = pos; a.slot = slots; a.nslots = d.max_batch; a.q_out = W.q; a.kc = kc; a.vc = vc;
     a.H = d.H; a.Hkv = d.Hkv; a.D = d.D; a.Smax = d.max_seq; a.log2_theta = log2_theta;
     a.kpart = W.kpart; a.kctr = W.kctr;
-    if ((e = launch_gemm<EPI_ROPE, 1>(a, qkv_n / 16, s)) != hipSuccess) return int(e);
+    if ((e = launch_gemm<EPI_ROPE, 1>(a, s)) != hipSuccess) return int(e);
 
     // attention: (span slot, row, KV head) workgroups of 8 waves
     {
@@ -856,7 +963,7 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
       const int G = d.H / d.Hkv;
 #define P2PT_ATTN(DD, GG)                                                                                          \
   hipLaunchKernelGGL((k_attn<DD, GG>), grid, dim3(512), 0, s, W.q, kc, vc, pos, slots, d.max_batch, W.part_o,    \
-                     W.part_ml, W.counters, W.attn, d.H, d.Hkv, d.max_seq, nsplit_ws, scale)
+                     W.part_ml, W.counters, W.attn, d.H, d.Hkv, d.max_seq, nsplit_ws, scale, attn_min_span())
       if (d.D == 64) {
         if (G == 1) P2PT_ATTN(64, 1); else if (G == 2) P2PT_ATTN(64, 2); else if (G == 4) P2PT_ATTN(64, 4); else P2PT_ATTN(64, 8);
       } else {
@@ -870,20 +977,23 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
     GemmArgs o{};
     o.M = B; o.x = W.attn; o.w = wo; o.N = d.dim; o.K = d.H * d.D;
     o.out = W.resid; o.ss_out = W.ss; o.kpart = W.kpart; o.kctr = W.kctr;
-    if ((e = launch_gemm<EPI_RESID, kTnResid>(o, d.dim / (16 * kTnResid), s)) != hipSuccess) return int(e);
-    ss_parts = d.dim / (16 * kTnResid);
+    o.cwl = pick_cwl(d.dim, kTnResid, kResidMinTiles);
+    if ((e = launch_gemm<EPI_RESID, kTnResid>(o, s)) != hipSuccess) return int(e);
+    ss_parts = d.dim / (kTnResid << o.cwl);
 
     // gate/up + SwiGLU
     GemmArgs g{};
     g.M = B; g.eps = d.eps; g.x = W.resid; g.w = wgu; g.N = 2 * d.ffn; g.K = d.dim;
     g.ss_part = W.ss; g.ss_parts = ss_parts; g.out = W.h; g.kpart = W.kpart; g.kctr = W.kctr;
-    if ((e = launch_gemm<EPI_SILU, 1>(g, 2 * d.ffn / 16, s)) != hipSuccess) return int(e);
+    if ((e = launch_gemm<EPI_SILU, 1>(g, s)) != hipSuccess) return int(e);
 
     // down + residual
     GemmArgs dn{};
     dn.M = B; dn.x = W.h; dn.w = wdown; dn.N = d.dim; dn.K = d.ffn; dn.out = W.resid; dn.ss_out = W.ss;
     dn.kpart = W.kpart; dn.kctr = W.kctr;
-    if ((e = launch_gemm<EPI_RESID, kTnResid>(dn, d.dim / (16 * kTnResid), s)) != hipSuccess) return int(e);
+    dn.cwl = pick_cwl(d.dim, kTnResid, kResidMinTiles);
+    if ((e = launch_gemm<EPI_RESID, kTnResid>(dn, s)) != hipSuccess) return int(e);
+    ss_parts = d.dim / (kTnResid << dn.cwl);
   }
 
   // final norm + LM head + argmax
@@ -892,9 +1002,10 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
   h.ss_part = W.ss; h.ss_parts = ss_parts;
   h.out = static_cast<uint16_t*>(logits);
   h.am_val = W.am_val; h.am_idx = W.am_idx;
+  h.cwl = 4;  // the argmax partials are sized for 16-column tiles
   const int parts = d.vocab / (16 * kTnStore);
   // 4 waves x 2 subtiles: the fastest LM-head shape measured (vocab 32000, K 2048: 22.6 vs 29.6 us).
-  if ((e = launch_gemm<EPI_ARGMAX, kTnStore>(h, parts, s, 4)) != hipSuccess) return int(e);
+  if ((e = launch_gemm<EPI_ARGMAX, kTnStore>(h, s, 4)) != hipSuccess) return int(e);
   hipLaunchKernelGGL(k_argmax_merge, dim3(emit_rows), dim3(256), 0, s, W.am_val, W.am_idx, parts, ids);
   return int(hipGetLastError());
 }
@@ -906,8 +1017,8 @@ int p2pt_skinny_gemm(const void* x, const void* w, void* out, int M, int N, int 
   a.x = static_cast<const uint16_t*>(x);
   a.w = static_cast<const uint16_t*>(w);
   a.out = static_cast<uint16_t*>(out);
-  a.M = M; a.N = N; a.K = K; a.ks = 1;
-  return int(launch_gemm<EPI_STORE, 2>(a, N / 32, static_cast<hipStream_t>(stream)));
+  a.M = M; a.N = N; a.K = K; a.ks = 1; a.cwl = 4;
+  return int(launch_gemm<EPI_STORE, 2>(a, static_cast<hipStream_t>(stream)));
 }
 
 // Microbenchmark hook (scripts/bench_skinny.py --attn): `reps` back-to-back
@@ -930,10 +1041,10 @@ int p2pt_attn_bench(const void* q, const void* kc, const void* vc, const int* po
     auto oo = static_cast<uint16_t*>(out);
     if (D == 64)
       hipLaunchKernelGGL((k_attn<64, 4>), grid, dim3(512), 0, st, qq, kk, vv, pos, nullptr, B, part_o, part_ml,
-                         counters, oo, H, Hkv, Smax, nsplit_ws, scale);
+                         counters, oo, H, Hkv, Smax, nsplit_ws, scale, attn_min_span());
     else
       hipLaunchKernelGGL((k_attn<128, 4>), grid, dim3(512), 0, st, qq, kk, vv, pos, nullptr, B, part_o, part_ml,
-                         counters, oo, H, Hkv, Smax, nsplit_ws, scale);
+                         counters, oo, H, Hkv, Smax, nsplit_ws, scale, attn_min_span());
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return int(e);
   }
@@ -949,7 +1060,7 @@ int p2pt_skinny_bench(const void* x, const void* w, void* out, int M, int N, int
   a.x = static_cast<const uint16_t*>(x);
   a.w = static_cast<const uint16_t*>(w);
   a.out = static_cast<uint16_t*>(out);
-  a.M = M; a.N = N; a.K = K; a.ks = 1;
+  a.M = M; a.N = N; a.K = K; a.ks = 1; a.cwl = 4;
   auto st = static_cast<hipStream_t>(stream);
   for (int r = 0; r < reps; r++) {
     hipError_t e;

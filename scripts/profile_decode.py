@@ -32,10 +32,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--eager", action="store_true")
     ap.add_argument("--unfused", action="store_true", help="kernels.hip + hipBLASLt path instead of decode_fused.hip")
+    ap.add_argument("--loop", action="store_true",
+                    help="device-side autoregression: one graph = the fused step (ids feed the next step's "
+                         "tokens in place) + pos += 1, no host copies per step")
     a = ap.parse_args()
     m = TinyLlama(a.config, device="cuda", max_batch=a.batch, fused=not a.unfused)
     m.k_cache.normal_()
     m.v_cache.normal_()
+    if a.loop:
+        return loop(m, a)
     if not a.eager:
         m.capture_graph(rows=a.batch)
     B = a.batch
@@ -55,6 +60,43 @@ def main():
     dt = time.perf_counter() - t0
     print(json.dumps({"config": a.config, "batch": B, "ctx": a.ctx, "steps": a.steps, "graph": not a.eager, "fused": not a.unfused,
                       "ms_per_step": dt * 1e3 / a.steps, "tokens_per_s": B * a.steps / dt}))
+
+
+def loop(m, a):
+    """The decode step as the only work in the graph: the step's ids buffer is
+    the next step's token buffer and a pos += 1 kernel follows it, so a replay
+    is the fused kernels plus one tiny elementwise kernel."""
+    B, c = a.batch, m.cfg
+    dec = m.fused_decoder()
+    tok = torch.randint(0, c.vocab, (B,), device="cuda")
+    pos = torch.full((B,), a.ctx, dtype=torch.int32, device="cuda")
+    logits = torch.empty(B, c.vocab, dtype=torch.bfloat16, device="cuda")
+
+    def body():
+        dec.step(tok, pos, c.max_seq, logits, tok, None, 0)
+        pos.add_(1)
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        body()
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        body()
+    pos.fill_(a.ctx)
+    for _ in range(a.warmup):
+        g.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        g.replay()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    nbytes = sum(t.numel() * t.element_size() for t in dec.weights[2:]) + m.embed.shape[1] * 2 * B
+    print(json.dumps({"config": a.config, "batch": B, "ctx": a.ctx, "steps": a.steps, "graph": True, "loop": True,
+                      "ms_per_step": dt * 1e3 / a.steps, "tokens_per_s": B * a.steps / dt,
+                      "weight_TBps": nbytes / (dt / a.steps) / 1e12}))
 
 
 if __name__ == "__main__":
