@@ -9,7 +9,15 @@ Content-Length), the local signal server, ``tunnel serve`` and ``tunnel proxy``
 (native C++; WebRTC data channel over the host's interfaces by default).
 A *step* = one streamed completion on each of S concurrent keep-alive client
 connections (S = 8 for the headline). ``value`` = whole-job tunneled
-requests/s over all ranks (weak scaling: every rank runs its own tunnel).
+requests/s (weak scaling: S streams per GPU).
+
+Topology for N > 1 (``--topology node``, the default): the deployment shape
+of one MI355X node — every rank starts the upstream of its GPU, rank 0 runs
+ONE ``tunnel serve --upstream <all N upstreams>`` and ONE proxy, and a single
+load generator drives S x N streams through that tunnel; serve spreads them
+over the upstreams by fewest in flight (``--workers`` auto: one reactor per 4
+CPUs beside the association thread). ``--topology independent`` instead
+gives every rank its own tunnel (round 1's layout).
 
 The upstream and the client are native by default (``tunnel-mock``,
 ``tunnel-loadgen``) so the TTFT numbers measure the tunnel rather than
@@ -47,6 +55,8 @@ def parse():
     ap.add_argument("--mock", choices=["native", "python"], default="native")
     ap.add_argument("--interval-ms", type=float, default=100.0)
     ap.add_argument("--tokens", type=int, default=5)
+    ap.add_argument("--topology", choices=["node", "independent"], default="node",
+                    help="N > 1: one tunnel fronting every rank's upstream (node) or one tunnel per rank")
     ap.add_argument("--out", default=None, help="also write the JSON line here")
     return ap.parse_args()
 
@@ -97,6 +107,24 @@ def loadgen(port, streams, steps, warmup=0, path=None):
         raise RuntimeError(f"loadgen failed (rc={out.returncode}): {out.stdout[-500:]} {out.stderr[-500:]}")
 
 
+def direct(ups, streams, steps):
+    """The same load straight to the upstreams (no tunnel): streams split
+    evenly over them, one load generator each, run concurrently; merged
+    req/s and the p50/p99 TTFT of the most loaded one."""
+    from p2p_llm_tunnel_amd import binary
+    n = len(ups)
+    share = [streams // n + (1 if i < streams % n else 0) for i in range(n)]
+    procs = [subprocess.Popen([binary("tunnel-loadgen"), "--target", f"127.0.0.1:{p}", "--streams", str(k),
+                               "--steps", str(steps), "--warmup", "1"], stdout=subprocess.PIPE, text=True)
+             for p, k in zip(ups, share) if k]
+    res = []
+    for pr in procs:
+        out, _ = pr.communicate(timeout=600)
+        res.append(json.loads(out.strip().splitlines()[-1]))
+    return {"req_s": sum(r["req_s"] for r in res), "p50_ttft_ms": max(r["p50_ttft_ms"] for r in res),
+            "p99_ttft_ms": max(r["p99_ttft_ms"] for r in res), "errors": sum(r["errors"] for r in res)}
+
+
 def main():
     a = parse()
     dist, rank, world = dist_init()
@@ -111,32 +139,44 @@ def main():
         dist.barrier()
 
     mock, up_port = start_mock(a.mock, a.interval_ms, a.tokens)
-    tun = Tunnel(f"http://127.0.0.1:{up_port}", transport=a.transport,
-                 env={"RUST_LOG": "warn,tunnel::serve=info,tunnel::proxy=info,tunnel::transport=info,tunnel::rtc=info"})
-    tun.start(timeout=60)
+    node = dist is not None and a.topology == "node"
+    ups = [up_port]
+    if node:
+        ups = [None] * world
+        dist.all_gather_object(ups, up_port)
+    drive = rank == 0 or not node  # ranks that run a tunnel and a load generator
+    streams = a.streams * (world if node else 1)
+    tun = None
+    if drive:
+        tun = Tunnel(",".join(f"http://127.0.0.1:{p}" for p in ups), transport=a.transport,
+                     env={"RUST_LOG": "warn,tunnel::serve=info,tunnel::proxy=info,tunnel::transport=info,"
+                                      "tunnel::rtc=info"})
+        tun.start(timeout=60)
 
     def barrier():
         if dist:
             dist.barrier()
 
     # Warmup (untimed): connections, SCTP cwnd, upstream prewarm pool.
-    if a.warmup:
-        loadgen(tun.proxy_port, a.streams, a.warmup)
+    if a.warmup and drive:
+        loadgen(tun.proxy_port, streams, a.warmup)
 
-    # ---- headline: exactly K timed steps at S streams per rank
+    # ---- headline: exactly K timed steps at S streams per GPU
     barrier()
     sync_device()
     t0 = time.perf_counter()
-    head = loadgen(tun.proxy_port, a.streams, a.steps)
+    head = loadgen(tun.proxy_port, streams, a.steps) if drive else {"requests": 0, "errors": 0}
     barrier()
     sync_device()
     dt_wall = time.perf_counter() - t0
 
-    # ---- untimed: curve points + direct baseline (same upstream, no tunnel)
+    # ---- untimed: curve points + direct baseline (the same load straight to
+    # the upstream; node topology: S x N streams split evenly over the N upstreams)
     curve = {}
-    for s in sorted({int(x) for x in a.curve.split(",") if x} | {a.streams}):
-        tun_r = head if s == a.streams else loadgen(tun.proxy_port, s, a.curve_steps, warmup=1)
-        dir_r = loadgen(up_port, s, a.curve_steps, warmup=1)
+    for s in sorted({int(x) for x in a.curve.split(",") if x} | {a.streams}) if drive else []:
+        n = s * (world if node else 1)
+        tun_r = head if s == a.streams else loadgen(tun.proxy_port, n, a.curve_steps, warmup=1)
+        dir_r = direct(ups, n, a.curve_steps)
         curve[str(s)] = {
             "tunneled_req_s": tun_r["req_s"],
             "direct_req_s": dir_r["req_s"],
@@ -149,16 +189,18 @@ def main():
         }
 
     path = ""
-    for line in tun.serve.lines:
-        if "WebRTC connection established" in line:
-            path = line.split(" via ", 1)[-1]
-    tun.stop()
+    if drive:
+        for line in tun.serve.lines:
+            if "WebRTC connection established" in line:
+                path = line.split(" via ", 1)[-1]
+        tun.stop()
+    barrier()  # every upstream stays up until the driving rank is done
     mock.stop()
 
     requests = head["requests"]
     errors = head["errors"]
     dt = dt_wall
-    added = curve[str(a.streams)]["added_p50_ttft_ms"]
+    added = curve[str(a.streams)]["added_p50_ttft_ms"] if drive else 0.0
     if dist:
         import torch
         t = torch.tensor([dt, added], dtype=torch.float64)
@@ -187,7 +229,9 @@ def main():
                 "model": "mock-llm-sse (reference tmp/mock_llm.py workload)",
                 "global_batch": a.streams * world,
                 "seq_len": a.tokens,
-                "parallelism": f"{world} tunnel(s) x {a.streams} multiplexed streams",
+                "parallelism": (f"1 tunnel x {world} upstreams (one per GPU) x {a.streams} streams each"
+                                if node else f"{world} tunnel(s) x {a.streams} multiplexed streams"),
+                "topology": "node" if node else ("independent" if world > 1 else "single"),
                 "transport": a.transport,
                 "path_rank0": path,
             },

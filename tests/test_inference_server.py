@@ -149,7 +149,7 @@ def test_single_token_requests_with_multibyte_prompts():
                 n = 16 if mt is None else 1
                 assert text == "".join(f" t{t}" for t in expected(b"hello world", n)), (stream, mt, text)
         assert eng.thread.is_alive()
-        # max_tokens beyond the context: clamped, the prompt's head is kept
+        # max_tokens beyond the context: clamped, the prompt's tail is kept
         st, _, data, _ = _post(port, "/v1/completions", {"stream": False, "prompt": "abc", "max_tokens": 1000})
         assert st == 200 and json.loads(data)["choices"][0]["text"].count(" t") == 62
         for bad in ("lots", [3], {"x": 1}):
