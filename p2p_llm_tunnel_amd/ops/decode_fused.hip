@@ -179,10 +179,13 @@ __device__ __forceinline__ void mma_apply(frag4 (&acc)[TN], const Batch<UM, TN>&
       acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(bt.a[u]), as_frag(bt.b[u][t]), acc[t], 0, 0, 0);
 }
 
-// The wave's k-steps [s0, s1), one batch at a time. (A two-deep batch
-// pipeline measured no faster on the down projection and 44 % slower on the LM
-// head, whose doubled registers halved the resident workgroups per CU: on
-// these kernels memory parallelism comes from resident waves.)
+// The wave's k-steps [s0, s1), one batch at a time. Measured slower on
+// MI355X and dropped (profiles/r02/decode/decode_sweep_s6..s8.log): a
+// two-deep batch pipeline (every projection +0.5-1.8 us, LM head +0.5-2.4),
+// 16 waves on the K = 5632 down projection (9.4 -> 10.5 us), and one
+// workgroup per CU forced through padded LDS with 8-column tiles (down
+// unchanged at 9.4 us, QKV 5.9 -> 9.9): the down projection is not bound by
+// per-CU bandwidth or by its serial batches.
 template <int UM, int TN>
 __device__ __forceinline__ void mma_stream(frag4 (&acc)[TN], __amdgpu_buffer_rsrc_t ra, uint32_t xoff,
                                            __amdgpu_buffer_rsrc_t rw, const uint32_t (&woff)[TN], int s0, int s1) {
