@@ -106,7 +106,8 @@ __device__ __forceinline__ float dot2_bf16(uint32_t a, uint32_t b, float c) {
 // Weights use the default cache policy on purpose: a decode step replays the
 // same weights back to back, and models up to the 256 MB MALL keep them
 // resident between steps (non-temporal loads measured 1.75x slower on the
-// 4-layer config, and no faster on the 0.85 GB one).
+// 4-layer config in round 1; with buffer loads, nt (aux 2) on the weights was
+// 5 % slower on the 0.85 GB config too: profiles/r02/decode/decode_sweep_s9.log).
 
 // Cross-workgroup hand-off without L2 write-back/invalidate fences: payload
 // stores are agent-scope relaxed atomics (write-through, `sc1`), drained with
