@@ -23,6 +23,7 @@ import os
 import subprocess
 import sys
 import time
+import urllib.request
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -40,6 +41,25 @@ def lg(port, *args):
 def result(p, timeout=900):
     out, _ = p.communicate(timeout=timeout)
     return json.loads(out.strip().splitlines()[-1])
+
+
+SCTP_GAUGES = ("tunnel_sctp_fast_retransmits", "tunnel_sctp_t3_expirations", "tunnel_sctp_tlp_probes",
+               "tunnel_sctp_rack_marks", "tunnel_sctp_random_loss_events", "tunnel_sctp_cwnd_bytes",
+               "tunnel_sctp_rto_us", "tunnel_sctp_packets_sent")
+
+
+def scrape(port):
+    """The SCTP loss-recovery gauges of one tunnel process (--metrics-listen)."""
+    try:
+        text = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5).read().decode()
+    except OSError:
+        return {}
+    out = {}
+    for line in text.splitlines():
+        parts = line.split()
+        if len(parts) == 2 and parts[0] in SCTP_GAUGES:
+            out[parts[0].replace("tunnel_sctp_", "")] = float(parts[1])
+    return out
 
 
 def sse(port, steps):
@@ -73,8 +93,10 @@ def main():
                 env = {"TUNNEL_FAULT_RTT_MS": str(rtt), "TUNNEL_FAULT_RATE_MBPS": str(a.rate_mbps),
                        "TUNNEL_FAULT_QUEUE_KB": str(qkb), "TUNNEL_FAULT_LOSS": str(loss),
                        "RUST_LOG": "warn,tunnel::rtc=info,tunnel::serve=info,tunnel::proxy=info"}
-                with Tunnel(f"http://127.0.0.1:{mport}", transport="webrtc", serve_extra=extra, proxy_extra=extra,
-                            env=env) as t:
+                sm, pm = free_port(), free_port()
+                with Tunnel(f"http://127.0.0.1:{mport}", transport="webrtc",
+                            serve_extra=extra + ["--metrics-listen", f"127.0.0.1:{sm}"],
+                            proxy_extra=extra + ["--metrics-listen", f"127.0.0.1:{pm}"], env=env) as t:
                     result(sse(t.proxy_port, 1))  # warm: connections, cwnd
                     alone = result(sse(t.proxy_port, a.sse_steps))
                     bulk = lg(t.proxy_port, "--streams", 4, "--steps", 1, "--warmup", 0, "--method", "GET",
@@ -93,7 +115,8 @@ def main():
                            "bulk_bg_MBps": bulk_r["MBps"], "echo_req_s": echo["req_s"],
                            "echo_MBps_each_way": echo["req_s"] * 1.048576,
                            "errors": alone["errors"] + mixed["errors"] + bulk_r["errors"] + echo["errors"],
-                           "echo_wall_s": round(time.time() - t0, 2)}
+                           "echo_wall_s": round(time.time() - t0, 2),
+                           "serve_sctp": scrape(sm), "proxy_sctp": scrape(pm)}
                     res["rows"].append(row)
                     print(json.dumps(row), file=sys.stderr, flush=True)
     finally:

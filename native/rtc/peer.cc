@@ -401,6 +401,18 @@ void PeerConnection::start_sctp() {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().packets_sent) : 0.0;
   });
+  metrics::gauge_fn("tunnel_sctp_tlp_probes", [w] {
+    auto s = w.lock();
+    return s && s->sctp_ ? double(s->sctp_->stats().tlp_probes) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_sctp_rack_marks", [w] {
+    auto s = w.lock();
+    return s && s->sctp_ ? double(s->sctp_->stats().rack_marks) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_sctp_random_loss_events", [w] {
+    auto s = w.lock();
+    return s && s->sctp_ ? double(s->sctp_->stats().random_loss_events) : 0.0;
+  });
   metrics::gauge_fn("tunnel_udp_gso_sends", [w] {
     auto s = w.lock();
     return s && s->ice_ ? double(s->ice_->gso_sends_) : 0.0;

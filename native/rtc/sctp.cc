@@ -707,6 +707,11 @@ void SctpAssociation::update_rto(uint64_t r) {
     srtt_us_ = (7 * srtt_us_ + r) / 8;
   }
   uint64_t rto = srtt_us_ + std::max<uint64_t>(4 * rttvar_us_, 1000);
+  // Leave room for a tail-loss probe and its SACK before T3: RTO >= PTO +
+  // SRTT. With the 100 ms floor alone, a 50 ms path had RTO <= PTO, so every
+  // tail loss went to T3 (cwnd collapse to one MTU, RTO doubling): 219 T3
+  // expirations in one emulated 50 ms / 2 % loss run and a 2 s SSE stall tail.
+  rto = std::max<uint64_t>(rto, 3 * srtt_us_ + cfg_.sack_delay_us);
   rto_us_ = std::clamp<uint64_t>(rto, cfg_.rto_min_ms * 1000, cfg_.rto_max_ms * 1000);
 }
 
@@ -822,14 +827,14 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
     cwnd_bypass_ = 1;
     // Loss response after TCP Veno: the backlog this association keeps in the
     // path's queues is cwnd * (SRTT - min RTT) / SRTT. A loss with (almost) no
-    // backlog is taken as random (wireless, lossy WAN) and cuts cwnd by 1/5;
+    // backlog is taken as random (wireless, lossy WAN) and cuts cwnd by 1/10;
     // a loss with a standing queue is congestion and cuts by 0.3 (CUBIC's
     // beta, RFC 9438) rather than Reno's half.
     uint64_t rtt = std::max<uint64_t>(srtt_us_, 1);
     size_t backlog = min_rtt_us_ && rtt > min_rtt_us_ ? size_t(double(cwnd_) * double(rtt - min_rtt_us_) / double(rtt)) : 0;
     bool random_loss = backlog < 3 * cfg_.mtu + cwnd_ / 16;
     if (random_loss) stats_.random_loss_events++;
-    ssthresh_ = std::max(random_loss ? cwnd_ * 4 / 5 : cwnd_ * 7 / 10, 4 * cfg_.mtu);
+    ssthresh_ = std::max(random_loss ? cwnd_ * 9 / 10 : cwnd_ * 7 / 10, 4 * cfg_.mtu);
     cwnd_ = ssthresh_;
     partial_acked_ = 0;
     fast_recovery_ = true;

@@ -18,6 +18,7 @@ struct LossyLink {
   Reactor& r;
   double loss, dup;
   uint64_t max_delay_us;
+  uint64_t fixed_delay_us = 0;  // added to every packet (a path's one-way delay)
   std::mt19937 rng{12345};
   uint64_t dropped = 0;
   LossyLink(Reactor& rr, double l, double d, uint64_t delay) : r(rr), loss(l), dup(d), max_delay_us(delay) {}
@@ -30,7 +31,7 @@ struct LossyLink {
     int copies = u(rng) < dup ? 2 : 1;
     for (int i = 0; i < copies; i++) {
       auto pkt = std::make_shared<std::vector<uint8_t>>(p, p + n);
-      uint64_t d = max_delay_us ? std::uniform_int_distribution<uint64_t>(0, max_delay_us)(rng) : 0;
+      uint64_t d = fixed_delay_us + (max_delay_us ? std::uniform_int_distribution<uint64_t>(0, max_delay_us)(rng) : 0);
       r.call_later_us(d, [to, pkt] {
         if (auto s = to.lock()) s->on_packet(pkt->data(), pkt->size());
       });
@@ -44,12 +45,13 @@ struct SctpPair {
   LossyLink link;
   std::vector<std::pair<uint16_t, std::string>> got_a, got_b;
   size_t zero_sums_a = 0, zero_sums_b = 0;  // packets sent with checksum 0
-  SctpPair(double loss, double dup, uint64_t delay, size_t mtu = 1200, bool zc_a = false, bool zc_b = false)
+  SctpPair(double loss, double dup, uint64_t delay, size_t mtu = 1200, bool zc_a = false, bool zc_b = false,
+           uint64_t rto_min_ms = 20)
       : link(r, loss, dup, delay) {
     SctpConfig cfg;
     cfg.mtu = mtu;
     cfg.rto_initial_ms = 100;
-    cfg.rto_min_ms = 20;
+    cfg.rto_min_ms = rto_min_ms;
     auto zero = [](const std::vector<uint8_t>& f) { return f[8] == 0 && f[9] == 0 && f[10] == 0 && f[11] == 0; };
     cfg.zero_checksum = zc_a;
     a = SctpAssociation::create(r, cfg, [this, zero](const iovec* v, int c) {
@@ -138,6 +140,37 @@ TEST(sctp_loss_reorder_dup_recovery) {
   CHECK(p.link.dropped > 0);
   CHECK(p.a->stats().retransmits > 0);
   (void)total;
+}
+
+TEST(sctp_wan_tail_losses_recover_without_t3) {
+  // 50 ms RTT, 2 % loss, the production RTO floor (100 ms): the RTO must stay
+  // above the tail-loss probe's timeout plus a round trip, so lone losses are
+  // recovered by RACK / TLP instead of T3 (cwnd collapse, RTO doubling). With
+  // RTO <= PTO every tail loss expired T3.
+  SctpPair p(0.02, 0, 0, 1200, false, false, 100);
+  p.link.fixed_delay_us = 25000;
+  p.a->connect();
+  p.b->connect();
+  CHECK(p.r.run_until([&] { return p.a->established() && p.b->established(); }, 5000));
+  size_t sent = 0;
+  uint64_t next = Reactor::now_us();
+  // An SSE-like trickle: a 150-byte message every 5 ms for 6 s.
+  CHECK(p.r.run_until([&] {
+    if (Reactor::now_us() >= next && sent < 1200) {
+      p.a->send(uint16_t(1 + 2 * (sent % 4)), 53, {Bytes::copy(payload(150, uint32_t(sent)))});
+      sent++;
+      next += 5000;
+    }
+    return sent == 1200 && p.got_b.size() == sent && p.a->bytes_in_flight() == 0;
+  }, 20000));
+  CHECK_EQ(p.got_b.size(), size_t(1200));
+  CHECK(p.link.dropped > 10);
+  CHECK(p.a->srtt_us() >= 45000 && p.a->rto_us() >= 3 * p.a->srtt_us());
+  printf("  50 ms / 2 %%: %llu dropped, %llu fast rtx, %llu TLP, %llu T3, srtt %llu us, rto %llu us\n",
+         (unsigned long long)p.link.dropped, (unsigned long long)p.a->stats().fast_retransmits,
+         (unsigned long long)p.a->stats().tlp_probes, (unsigned long long)p.a->stats().t3_expirations,
+         (unsigned long long)p.a->srtt_us(), (unsigned long long)p.a->rto_us());
+  CHECK(p.a->stats().t3_expirations * 4 <= p.link.dropped);
 }
 
 TEST(sctp_jumbo_bulk_throughput) {
