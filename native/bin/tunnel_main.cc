@@ -69,6 +69,7 @@ const std::vector<Opt>& ext_opts() {
       {"stun", "TUNNEL_STUN", "stun:stun.l.google.com:19302", "STUN server(s), comma-separated; 'none' disables"},
       {"no-loopback-candidates", nullptr, nullptr, "Do not gather 127.0.0.1 host candidates", true},
       {"ipv6", nullptr, nullptr, "Gather IPv6 host candidates", true},
+      {"ipv6-only", nullptr, nullptr, "Gather host candidates on IPv6 interfaces only", true},
       {"ice-relay-only", nullptr, nullptr, "Only use TURN-relayed candidates (iceTransportPolicy=relay)", true},
       {"gather-timeout-ms", "TUNNEL_GATHER_TIMEOUT_MS", "5000", "Max wait for ICE gathering before sending SDP"},
       {"ice-timeout-ms", "TUNNEL_ICE_TIMEOUT_MS", "30000", "No traffic for this long => connection failed"},
@@ -306,7 +307,8 @@ int main(int argc, char** argv) {
     }
   }
   cfg.rtc.include_loopback = !m.count("no-loopback-candidates");
-  cfg.rtc.include_ipv6 = m.count("ipv6") > 0;
+  cfg.rtc.include_ipv6 = m.count("ipv6") > 0 || m.count("ipv6-only") > 0;
+  cfg.rtc.ipv6_only = m.count("ipv6-only") > 0;
   cfg.rtc.relay_only = m.count("ice-relay-only") > 0;
   cfg.rtc.gather_timeout_ms = num(m, "gather-timeout-ms");
   cfg.rtc.ice_failed_timeout_ms = num(m, "ice-timeout-ms");

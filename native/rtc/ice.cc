@@ -160,7 +160,10 @@ size_t IceAgent::gro_segment(const msghdr* mh) {
 }
 
 void IceAgent::open_sockets() {
-  auto addrs = local_addresses(cfg_.include_loopback, cfg_.include_ipv6);
+  auto addrs = local_addresses(cfg_.include_loopback, cfg_.include_ipv6 || cfg_.ipv6_only);
+  if (cfg_.ipv6_only)
+    addrs.erase(std::remove_if(addrs.begin(), addrs.end(), [](const IfaceAddr& a) { return a.addr.family() != AF_INET6; }),
+                addrs.end());
   // Non-loopback first so they get the higher local preference.
   std::stable_sort(addrs.begin(), addrs.end(),
                    [](const IfaceAddr& a, const IfaceAddr& b) { return !a.addr.is_loopback() && b.addr.is_loopback(); });

@@ -76,6 +76,7 @@ struct IceConfig {
   std::string turn_user, turn_pass;
   bool include_loopback = true;
   bool include_ipv6 = false;
+  bool ipv6_only = false;  // host candidates on IPv6 interfaces only (implies include_ipv6)
   // iceTransportPolicy "relay": only TURN-relayed local candidates are
   // advertised and checked (forces the TURN path, e.g. symmetric NATs).
   bool relay_only = false;

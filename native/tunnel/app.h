@@ -32,6 +32,7 @@ struct RtcOptions {
   TurnConfig turn;
   bool include_loopback = true;     // host candidates on lo (offline / same-host peers)
   bool include_ipv6 = false;
+  bool ipv6_only = false;
   bool relay_only = false;            // iceTransportPolicy=relay
   uint64_t gather_timeout_ms = 5000;  // reference waits <= 5 s (rtc.rs:181-182)
   uint64_t ice_failed_timeout_ms = 30000;

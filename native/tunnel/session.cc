@@ -66,6 +66,7 @@ class WebrtcSession : public std::enable_shared_from_this<WebrtcSession> {
     pc.ice.turn_pass = cfg_.rtc.turn.password;
     pc.ice.include_loopback = cfg_.rtc.include_loopback;
     pc.ice.include_ipv6 = cfg_.rtc.include_ipv6;
+    pc.ice.ipv6_only = cfg_.rtc.ipv6_only;
     pc.ice.relay_only = cfg_.rtc.relay_only;
     pc.ice.failed_ms = cfg_.rtc.ice_failed_timeout_ms;
     pc.sctp_mtu = cfg_.rtc.sctp_mtu;

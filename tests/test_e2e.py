@@ -302,3 +302,16 @@ def test_multiple_upstreams_least_loaded():
         for srv, _ in servers:
             srv.shutdown()
             srv.server_close()
+
+
+def test_webrtc_over_ipv6(mock_upstream):
+    """ICE, DTLS and SCTP over IPv6 host candidates only (--ipv6-only: the
+    ::1 loopback here): the session comes up on an IPv6 pair and streams SSE."""
+    with Tunnel(mock_upstream, transport="webrtc", serve_extra=["--ipv6-only"], proxy_extra=["--ipv6-only"]) as t:
+        line = t.serve.wait_for("connection established", 10)
+        assert "[" in line.split(" via ", 1)[-1], line  # IPv6 addresses print as [addr]:port
+        c = http.client.HTTPConnection("127.0.0.1", t.proxy_port, timeout=10)
+        c.request("POST", "/v1/chat/completions", body=json.dumps({"stream": True, "messages": []}))
+        r = c.getresponse()
+        data = r.read()
+        assert r.status == 200 and data.count(b"data: ") >= 6 and data.rstrip().endswith(b"data: [DONE]")
