@@ -7,7 +7,7 @@ the gfx950 fused decode path, continuous batching with chunked prefill, one
 hipGraph per step) and the native load generator streams chat completions
 through `tunnel proxy` and, for the baseline, straight to the server.
 
-    python bench/bench_gpu_upstream.py [--config tiny] [--streams 1,8,16] [--max-tokens 32]
+    python bench/bench_gpu_upstream.py [--config tiny | --checkpoint DIR] [--streams 1,8,16] [--max-tokens 32]
 
 Prints one JSON document: per stream count, direct and tunneled req/s,
 generated tokens/s, p50/p99 time to first token, and the added p50 TTFT.
@@ -46,6 +46,7 @@ def loadgen(port, streams, steps, body, warmup=1):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="tiny")
+    ap.add_argument("--checkpoint", default=None, help="serve this HF Llama checkpoint (models.server --checkpoint)")
     ap.add_argument("--max-batch", type=int, default=16)
     ap.add_argument("--streams", default="1,8,16")
     ap.add_argument("--steps", type=int, default=4)
@@ -55,8 +56,9 @@ def main():
     a = ap.parse_args()
     ensure_native()
     port = free_port()
+    model = ["--checkpoint", a.checkpoint] if a.checkpoint else ["--config", a.config]
     srv = spawn("gpu-server", [sys.executable, "-m", "p2p_llm_tunnel_amd.models.server", "--port", str(port),
-                               "--config", a.config, "--max-batch", str(a.max_batch)])
+                               *model, "--max-batch", str(a.max_batch)])
     try:
         srv.wait_for("inference endpoint on", 300)
         body = json.dumps({"model": "p2pt", "stream": True, "max_tokens": a.max_tokens,

@@ -202,7 +202,13 @@ __device__ __forceinline__ void mma_stream(frag4 (&acc)[TN], __amdgpu_buffer_rsr
 
 // Skinny GEMM + fused epilogue. NW waves split K; TN subtiles of 2^cwl
 // columns per block; UM k-steps per load batch (host: >= each wave's share
-// when possible). ROPE and SILU take weights whose rows are interleaved in
+// when possible). Steps of more than 16 rows put each 16-row tile on its own
+// workgroup (blockIdx.y). Sharing each weight fragment across the four tiles
+// of a 64-row step in one workgroup was measured slower (small config, 64
+// rows: 1.19 -> 1.26 ms; 1.1B-shaped checkpoint served at 16 streams 3.0 K ->
+// 2.7 K tok/s, profiles/r02/decode/decode_sweep_s10_rowtiles.log): the extra
+// tiles' weight reads hit the MALL, and a quarter of the workgroups each
+// issuing five times the loads leaves the load path, not HBM, as the limit. ROPE and SILU take weights whose rows are interleaved in
 // pairs (RoPE partners d, d + D/2 of a head; gate_j, up_j), so a pair sits in
 // lanes c, c^1.
 template <int NW, int TN, int EPI, int UM>

@@ -18,10 +18,8 @@ run() {  # label, env..., -- args
   out=$(env "${envs[@]}" timeout -k 10 120 python scripts/profile_decode.py --loop --steps 400 "$@" 2>/dev/null | tail -1) || return 1
   echo "$label $out" | tee -a gpurun_out/decode_sweep_$TAG.log
 }
-for cfg in "--config small --batch 1" "--config small --batch 16" "--config tiny --batch 1"; do
+for cfg in "--config small --batch 1" "--config small --batch 16" "--config small --batch 64" "--config tiny --batch 1" "--config tiny --batch 64"; do
   run "dflt" P2PT_X=0 -- $cfg || exit 1
-  run "cap8" P2PT_DECODE_UMCAP=8 -- $cfg || exit 1
-  run "span256" P2PT_ATTN_MINSPAN=256 -- $cfg || exit 1
 done
 cd /tmp
 for cfg in "small 1" "small 16"; do

@@ -32,11 +32,17 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--eager", action="store_true")
     ap.add_argument("--unfused", action="store_true", help="kernels.hip + hipBLASLt path instead of decode_fused.hip")
+    ap.add_argument("--checkpoint", default=None, help="load this HF Llama checkpoint instead of a random --config")
     ap.add_argument("--loop", action="store_true",
                     help="device-side autoregression: one graph = the fused step (ids feed the next step's "
                          "tokens in place) + pos += 1, no host copies per step")
     a = ap.parse_args()
-    m = TinyLlama(a.config, device="cuda", max_batch=a.batch, fused=not a.unfused)
+    if a.checkpoint:
+        from p2p_llm_tunnel_amd.models.checkpoint import load_llama
+        m = load_llama(a.checkpoint, device="cuda", max_batch=a.batch, fused=not a.unfused)
+        a.config = os.path.basename(os.path.normpath(a.checkpoint))
+    else:
+        m = TinyLlama(a.config, device="cuda", max_batch=a.batch, fused=not a.unfused)
     m.k_cache.normal_()
     m.v_cache.normal_()
     if a.loop:

@@ -224,3 +224,51 @@ def test_64_row_prefill_chunk_matches_16_row_chunks():
     m3.v_cache.zero_()
     g = m3.graph_step(toks[order], pos[order], slots[order])
     assert torch.equal(g[:3], ids2[order[:3]])
+
+
+@cuda
+@pytest.mark.parametrize("cfg,B", [("micro", 64), ("small", 40)])
+def test_fused_prefill_sized_steps_match_unfused(cfg, B):
+    # Steps of more than 16 rows run every GEMM with four 16-row tiles per
+    # workgroup sharing each weight fragment (decode_fused.hip RT = 4); they
+    # must agree with the unfused kernels + hipBLASLt on the same rows.
+    from p2p_llm_tunnel_amd.models.tiny_llm import TinyLlama
+    mf = TinyLlama(cfg, device="cuda", max_batch=B, seed=9, fused=True)
+    mu = TinyLlama(cfg, device="cuda", max_batch=B, seed=9, fused=False)
+    torch.manual_seed(3)
+    T = 6
+    seqs = torch.randint(0, mf.cfg.vocab, (B, T), device="cuda")
+    for p in range(T):
+        pos = torch.full((B,), p, dtype=torch.int32, device="cuda")
+        idf, lf = mf.decode_step(seqs[:, p], pos, (p, p), return_logits=True)
+        idu, lu = mu.decode_step(seqs[:, p], pos, (p, p), return_logits=True)
+    scale = lu.float().abs().max().item()
+    assert (lf.float() - lu.float()).abs().max().item() < 0.03 * scale
+    top2 = lu.float().topk(2, -1).values
+    confident = (top2[:, 0] - top2[:, 1]) > 0.03 * scale
+    assert torch.equal(idf[confident], idu[confident])
+    kdiff = (mf.k_cache[:, :B, :T].float() - mu.k_cache[:, :B, :T].float()).abs().max().item()
+    assert kdiff < 0.05 * mu.k_cache[:, :B, :T].float().abs().max().item()
+
+
+@cuda
+def test_64_row_prefill_chunk_matches_sequential():
+    # A 60-token prompt fed as ONE chunk (rows -> one slot, causal within the
+    # step) next to 4 other slots' decode rows: 64 rows, the four-tile path.
+    from p2p_llm_tunnel_amd.models.tiny_llm import TinyLlama
+    m1 = TinyLlama("micro", device="cuda", max_batch=5, seed=11)
+    m2 = TinyLlama("micro", device="cuda", max_batch=5, seed=11)
+    torch.manual_seed(5)
+    T = 60
+    prompt = torch.randint(0, m1.cfg.vocab, (T,), device="cuda")
+    four = torch.full((1,), 4, dtype=torch.int32, device="cuda")
+    for p in range(T):
+        _, l1 = m1.decode_step(prompt[p:p + 1], torch.full((1,), p, dtype=torch.int32, device="cuda"), (p, p),
+                               return_logits=True, slots=four)
+    toks = torch.cat([prompt, torch.tensor([5, 6, 7, 8], device="cuda")])
+    pos = torch.tensor(list(range(T)) + [0, 0, 0, 0], dtype=torch.int32, device="cuda")
+    slots = torch.tensor([4] * T + [0, 1, 2, 3], dtype=torch.int32, device="cuda")
+    _, l2 = m2.decode_step(toks, pos, (0, T - 1), return_logits=True, slots=slots)
+    last = l2[T - 1].float()
+    assert (last - l1[0].float()).abs().max().item() <= 1e-6 + 0.01 * l1.float().abs().max().item()
+    assert int(last.argmax()) == int(l1[0].float().argmax())
