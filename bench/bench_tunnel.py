@@ -13,6 +13,9 @@
      --idle-s; keepalive behaviour is identical for any idle length).
 
 Writes a JSON document (default: stdout) with every measured point.
+``--std-mtu`` runs every WebRTC row on the standard 1200-byte SCTP packet
+path (``--no-jumbo-loopback``) that cross-host deployments use; rows are then
+labelled ``webrtc-1200``.
 """
 from __future__ import annotations
 
@@ -31,10 +34,17 @@ from p2p_llm_tunnel_amd.utils.build import ensure_native  # noqa: E402
 from p2p_llm_tunnel_amd.utils.procs import Tunnel  # noqa: E402
 
 
+MTU_EXTRA: list[str] = []  # ["--no-jumbo-loopback"] with --std-mtu
+
+
+def label(transport):
+    return transport + ("-1200" if MTU_EXTRA and transport == "webrtc" else "")
+
+
 def sse_matrix(transport, mock_kind, streams_list, steps, threaded=True, busy_poll_us=0, path=None, nat=None):
     mock, port = start_mock(mock_kind, 100, 5) if (mock_kind == "native" or threaded) else _unthreaded()
     rows = []
-    extra = ["--busy-poll-us", str(busy_poll_us)] if busy_poll_us else []
+    extra = (["--busy-poll-us", str(busy_poll_us)] if busy_poll_us else []) + (MTU_EXTRA if transport == "webrtc" else [])
     env = None
     stun = None
     if nat:
@@ -51,7 +61,7 @@ def sse_matrix(transport, mock_kind, streams_list, steps, threaded=True, busy_po
                 if not threaded:
                     time.sleep(1.3)  # let serve's spare upstream sockets expire (single-threaded upstream)
                 dr = loadgen(port, s, steps, path=path)
-                rows.append({"transport": transport + (f"+nat:{nat}" if nat else ""),
+                rows.append({"transport": label(transport) + (f"+nat:{nat}" if nat else ""),
                              "mock": mock_kind if threaded else "python-unthreaded",
                              "busy_poll_us": busy_poll_us, "path": path or "/v1/chat/completions",
                              "streams": s, "tunneled_req_s": tr["req_s"], "direct_req_s": dr["req_s"],
@@ -77,7 +87,8 @@ def _unthreaded():
 def post_1mb(transport, streams=64, mb=1, steps=2):
     mock, port = start_mock("native", 100, 5)
     try:
-        with Tunnel(f"http://127.0.0.1:{port}", transport=transport) as t:
+        ex = MTU_EXTRA if transport == "webrtc" else []
+        with Tunnel(f"http://127.0.0.1:{port}", transport=transport, serve_extra=ex, proxy_extra=ex) as t:
             from p2p_llm_tunnel_amd import binary
             import subprocess
             def run(target):
@@ -87,7 +98,7 @@ def post_1mb(transport, streams=64, mb=1, steps=2):
                 return json.loads(out.stdout.strip().splitlines()[-1])
             tr, dr = run(t.proxy_port), run(port)
             # request + echoed response both cross the tunnel
-            row = {"transport": transport, "streams": streams, "body_mb": mb,
+            row = {"transport": label(transport), "streams": streams, "body_mb": mb,
                    "tunneled_req_s": tr["req_s"], "direct_req_s": dr["req_s"],
                    "tunneled_MBps_each_way": tr["req_s"] * mb * 1.048576,
                    "tunneled_p50_total_ms": tr["p50_total_ms"], "direct_p50_total_ms": dr["p50_total_ms"],
@@ -101,7 +112,8 @@ def post_1mb(transport, streams=64, mb=1, steps=2):
 def idle_burst(transport, idle_s=30, burst=16):
     mock, port = start_mock("native", 100, 5)
     try:
-        with Tunnel(f"http://127.0.0.1:{port}", transport=transport,
+        ex = MTU_EXTRA if transport == "webrtc" else []
+        with Tunnel(f"http://127.0.0.1:{port}", transport=transport, serve_extra=ex, proxy_extra=ex,
                     env={"RUST_LOG": "info,tunnel::serve=debug"}) as t:
             loadgen(t.proxy_port, 1, 1)
             pings0 = t.serve.count("sent keepalive ping")
@@ -109,7 +121,7 @@ def idle_burst(transport, idle_s=30, burst=16):
             pings = t.serve.count("sent keepalive ping") - pings0
             r = loadgen(t.proxy_port, burst, 1)
             d = loadgen(port, burst, 1)
-            row = {"transport": transport, "idle_s": idle_s, "burst_streams": burst, "pings_during_idle": pings,
+            row = {"transport": label(transport), "idle_s": idle_s, "burst_streams": burst, "pings_during_idle": pings,
                    "tunneled_req_s": r["req_s"], "tunneled_p50_ttft_ms": r["p50_ttft_ms"],
                    "direct_p50_ttft_ms": d["p50_ttft_ms"], "added_p50_ttft_ms": r["p50_ttft_ms"] - d["p50_ttft_ms"],
                    "errors": r["errors"]}
@@ -126,7 +138,10 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--quick", action="store_true", help="native mock + webrtc only")
     ap.add_argument("--busy-poll", default="", help="comma-separated busy-poll µs values to add as extra SSE rows")
+    ap.add_argument("--std-mtu", action="store_true", help="WebRTC rows on the 1200-byte SCTP packet path")
     a = ap.parse_args()
+    if a.std_mtu:
+        MTU_EXTRA.append("--no-jumbo-loopback")
     ensure_native()
     res = {"host": os.uname().nodename, "time": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()), "sse": []}
     streams = [1, 2, 4, 8]
