@@ -26,6 +26,8 @@ const char* pc_state_name(PcState s) {
 
 // ---------------------------------------------------------------- DataChannel
 
+constexpr size_t kPrioritySmallFrame = 1024;
+
 bool DataChannel::send(const uint8_t* hdr, size_t hlen, const Bytes& payload) {
   auto pc = pc_.lock();
   if (!pc || !is_open() || !pc->sctp_) return false;
@@ -34,7 +36,17 @@ bool DataChannel::send(const uint8_t* hdr, size_t hlen, const Bytes& payload) {
     uint32_t sid = rd32(hdr + 1);
     if (sid) st = uint16_t(stream_ + 2 * (1 + int(sid % uint32_t(lanes_))));
   }
-  bool ok = pc->sctp_->send_framed(st, kPpidBinary, hdr, hlen, payload);
+  // TUNNEL_SCTP_PRIORITY=1: small frames (SSE tokens, headers, control,
+  // credit) take the SCTP priority queue, ahead of queued bulk bodies. Off by
+  // default: on the emulated WAN it did not shorten the SSE-next-to-bulk tail
+  // (a token mostly waits behind a bulk message already being fragmented,
+  // which it may not interrupt), and 64 x 1 MB bulk ran ~20 % slower.
+  static const bool prio = [] {
+    const char* e = getenv("TUNNEL_SCTP_PRIORITY");
+    return e && *e == '1';
+  }();
+  const bool small = prio && hlen + payload.size() <= kPrioritySmallFrame;
+  bool ok = pc->sctp_->send_framed(st, kPpidBinary, hdr, hlen, payload, false, small);
   if (ok && buffered_amount() > buffered_low_threshold) above_low_ = true;
   return ok;
 }

@@ -500,7 +500,7 @@ void SctpAssociation::handle_shutdown(const uint8_t*, size_t) {
 }
 
 void SctpAssociation::maybe_finish_shutdown() {
-  if (!sendq_.empty() || !inflight_.empty()) return;
+  if (!sendq_.empty() || !sendq_pri_.empty() || !inflight_.empty()) return;
   if (state_ == State::ShutdownReceived) {
     state_ = State::ShutdownAckSent;
     send_control(kShutdownAck, 0, {}, peer_vtag_);
@@ -570,6 +570,13 @@ void SctpAssociation::deliver_chunk(uint8_t fl, uint16_t st, uint16_t ssn, uint3
 // early (out of TSN order) and now are next in their stream's sequence.
 void SctpAssociation::deliver_message(uint16_t st, uint16_t ssn, bool unordered, uint32_t pp, Bytes msg) {
   if (!unordered) {
+    int16_t ahead = int16_t(uint16_t(ssn - next_ssn_in_[st]));
+    if (ahead > 0) {  // an earlier message of this stream is still to come
+      held_bytes_ += msg.size();
+      held_[stream_ssn(st, ssn)] = {pp, std::move(msg)};
+      return;
+    }
+    if (ahead < 0) return;  // already delivered
     next_ssn_in_[st] = uint16_t(ssn + 1);
     early_ready_.erase(stream_ssn(st, ssn));
   }
@@ -577,9 +584,26 @@ void SctpAssociation::deliver_message(uint16_t st, uint16_t ssn, bool unordered,
   if (!unordered) release_ready(st);
 }
 
+// Delivers, in sequence, the messages of stream `st` that wait for their turn:
+// held complete messages and early single-chunk ones still in the gap map.
 void SctpAssociation::release_ready(uint16_t st) {
-  while (!early_ready_.empty()) {
-    auto it = early_ready_.find(stream_ssn(st, next_ssn_in_[st]));
+  for (;;) {
+    const uint32_t key = stream_ssn(st, next_ssn_in_[st]);
+    if (!held_.empty()) {
+      auto h = held_.find(key);
+      if (h != held_.end()) {
+        uint32_t pp = h->second.first;
+        Bytes m = std::move(h->second.second);
+        held_.erase(h);
+        held_bytes_ -= m.size();
+        early_ready_.erase(key);
+        next_ssn_in_[st] = uint16_t(next_ssn_in_[st] + 1);
+        if (on_message) on_message(st, pp, std::move(m));
+        continue;
+      }
+    }
+    if (early_ready_.empty()) return;
+    auto it = early_ready_.find(key);
     if (it == early_ready_.end()) return;
     auto oc = ooo_.find(it->second);
     early_ready_.erase(it);
@@ -590,7 +614,8 @@ void SctpAssociation::release_ready(uint16_t st) {
     Bytes m = std::move(ic->data);
     ic->data = Bytes();
     stats_.early_deliveries++;
-    deliver_message(ic->stream, ic->ssn, false, ic->ppid, std::move(m));
+    next_ssn_in_[st] = uint16_t(next_ssn_in_[st] + 1);
+    if (on_message) on_message(st, ic->ppid, std::move(m));
   }
 }
 
@@ -669,7 +694,7 @@ void SctpAssociation::handle_data(uint8_t flags, const uint8_t* c, size_t len, c
 }
 
 void SctpAssociation::build_sack(std::vector<uint8_t>& b) {
-  size_t held = ooo_bytes_;
+  size_t held = ooo_bytes_ + held_bytes_;
   for (auto& kv : partial_) held += kv.second.size();
   uint32_t a_rwnd = held >= cfg_.rwnd ? 0 : uint32_t(cfg_.rwnd - held);
   // Gap blocks relative to the cumulative TSN (ooo_ keys sorted numerically;
@@ -976,7 +1001,7 @@ bool SctpAssociation::send(uint16_t stream, uint32_t ppid, const std::vector<Byt
 }
 
 bool SctpAssociation::send_framed(uint16_t stream, uint32_t ppid, const uint8_t* hdr, size_t hlen, const Bytes& payload,
-                                  bool unordered) {
+                                  bool unordered, bool priority) {
   if (closed_fired_ || state_ == State::ShutdownPending || state_ == State::ShutdownSent) return false;
   if (hlen > kMsgHdrMax) return send(stream, ppid, {Bytes::copy(hdr, hlen), payload}, unordered);
   Msg m;
@@ -990,7 +1015,10 @@ bool SctpAssociation::send_framed(uint16_t stream, uint32_t ppid, const uint8_t*
   if (m.len == 0) return false;
   m.ssn = unordered ? 0 : next_ssn_[stream]++;
   unsent_bytes_ += m.len;
-  sendq_.push_back(std::move(m));
+  // Priority only for messages of one DATA chunk: a message's fragments must
+  // carry consecutive TSNs, so a message is never split around another.
+  if (priority && m.len <= cfg_.mtu - kCommonHdr - kDataHdr) sendq_pri_.push_back(std::move(m));
+  else sendq_.push_back(std::move(m));
   return true;
 }
 
@@ -1059,7 +1087,7 @@ void SctpAssociation::flush() {
   // delayed by sack_delay_us so a lone request frame is acknowledged by the
   // response that follows instead of by a pure SACK (one less wakeup per
   // request on each side). RFC 9260 §6.2 allows up to 500 ms.
-  bool data_ready = can_data && !sendq_.empty();
+  bool data_ready = can_data && (!sendq_.empty() || !sendq_pri_.empty());
   if (can_data && !data_ready)
     for (Chunk* ch : inflight_)
       if (ch->retransmit) {
@@ -1158,13 +1186,21 @@ void SctpAssociation::flush() {
   // within this flush while the windows allow, instead of idling until the
   // next SACK wakes the reactor (the producer keeps this queue shallow for
   // fairness, so without this loop a flush would send at most one window).
+  // Priority messages (one chunk each) go first whenever the bulk queue is
+  // between messages, and may exceed cwnd by a few packets: an SSE token
+  // queued behind a bulk transfer would otherwise wait for that transfer's
+  // SACKs, up to a round trip on a WAN path. The allowance bounds what this
+  // adds to a congested path (interactive traffic is a trickle).
+  const size_t pri_allow = 4 * mtu;
   for (int round = 0; round < 256; round++) {
   bool progressed = false;
-  while (!sendq_.empty()) {
-    Msg& m = sendq_.front();
+  while (!sendq_pri_.empty() || !sendq_.empty()) {
+    bool pri = !sendq_pri_.empty() && (sendq_.empty() || sendq_.front().off == 0);
+    Msg& m = pri ? sendq_pri_.front() : sendq_.front();
     size_t left = m.len - m.off;
     size_t take = std::min(left, max_payload);
-    if (flight_size_ > 0 && (flight_size_ + take > cwnd_ || take > peer_rwnd_)) break;
+    size_t window = pri ? cwnd_ + pri_allow : cwnd_;
+    if (flight_size_ > 0 && (flight_size_ + take > window || take > peer_rwnd_)) break;
     if (flight_size_ == 0 && peer_rwnd_ == 0 && !inflight_.empty()) break;  // wait for window / T3 probe
     progressed = true;
     Chunk* ch = new_chunk();
@@ -1191,9 +1227,12 @@ void SctpAssociation::flush() {
     add_data(ch);
     peer_rwnd_ = peer_rwnd_ > take ? peer_rwnd_ - take : 0;
     sent_any = true;
-    if (m.off == m.len) sendq_.pop_front();
+    if (m.off == m.len) {
+      if (pri) sendq_pri_.pop_front();
+      else sendq_.pop_front();
+    }
   }
-  if (!progressed || !sendq_.empty() || !on_sent) break;
+  if (!progressed || !sendq_.empty() || !sendq_pri_.empty() || !on_sent) break;
   size_t before = unsent_bytes_;
   on_sent();  // producer may refill the (now empty) queue
   if (closed_fired_ || unsent_bytes_ == before) break;

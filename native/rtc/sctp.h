@@ -93,8 +93,12 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   // Queue a message = a short header (copied, <= kMsgHdrMax bytes) followed by
   // a payload view (never copied): the tunnel's frame header + body.
   static constexpr size_t kMsgHdrMax = 16;
+  // priority: a latency-sensitive message that fits one DATA chunk (an SSE
+  // token frame, a control or credit frame) — sent ahead of queued bulk
+  // messages that have not started, and up to kPriorityAllowance bytes past
+  // cwnd, so it does not wait for a bulk transfer's window to drain.
   bool send_framed(uint16_t stream, uint32_t ppid, const uint8_t* hdr, size_t hlen, const Bytes& payload,
-                   bool unordered = false);
+                   bool unordered = false, bool priority = false);
   // Build and emit packets (bundled). Called once per reactor batch.
   void flush();
   void shutdown();
@@ -190,6 +194,7 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   void free_chunk(Chunk* c);
   std::vector<Chunk*> chunk_free_;
   std::deque<Msg> sendq_;
+  std::deque<Msg> sendq_pri_;  // single-chunk priority messages (send_framed(..., priority))
   std::map<uint16_t, uint16_t> next_ssn_;
   std::deque<Chunk*> inflight_;  // ordered by TSN
   size_t unsent_bytes_ = 0;
@@ -234,6 +239,11 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   std::map<uint16_t, Partial> partial_u_;  // unordered
   std::map<uint16_t, uint16_t> next_ssn_in_;      // per inbound stream: next SSN to deliver
   std::map<uint32_t, uint32_t> early_ready_;      // (stream, ssn) -> TSN of a complete message held out of order
+  // Complete ordered messages that arrived in TSN order but ahead of their
+  // stream's sequence (a peer may send a later small message of a stream
+  // before an earlier large one: RFC 9260 orders by SSN, not TSN).
+  std::map<uint32_t, std::pair<uint32_t, Bytes>> held_;  // (stream, ssn) -> (ppid, message)
+  size_t held_bytes_ = 0;
 
   std::vector<std::vector<uint8_t>> ctrl_;  // control chunks to bundle at next flush
   bool shutdown_requested_ = false;

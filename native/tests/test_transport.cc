@@ -173,6 +173,34 @@ TEST(sctp_wan_tail_losses_recover_without_t3) {
   CHECK(p.a->stats().t3_expirations * 4 <= p.link.dropped);
 }
 
+TEST(sctp_priority_messages_keep_stream_order) {
+  // Small priority messages overtake queued bulk messages on the wire, but a
+  // stream's messages are still delivered in the order they were sent.
+  SctpPair p(0, 0, 0);
+  p.a->connect();
+  p.b->connect();
+  CHECK(p.r.run_until([&] { return p.a->established() && p.b->established(); }, 2000));
+  std::vector<std::pair<uint16_t, std::string>> sent;
+  for (int i = 0; i < 60; i++) {
+    uint16_t st = uint16_t(1 + 2 * (i % 3));
+    bool small = i % 2 == 1;
+    std::string m = payload(small ? size_t(100 + i) : size_t(30000 + 97 * i), uint32_t(i));
+    uint8_t hdr[5] = {uint8_t(i), 0, 0, 0, 0};
+    p.a->send_framed(st, 53, hdr, 5, Bytes::copy(m), false, small);
+    sent.emplace_back(st, std::string(reinterpret_cast<char*>(hdr), 5) + m);
+  }
+  CHECK(p.r.run_until([&] { return p.got_b.size() == sent.size(); }, 10000));
+  CHECK_EQ(p.got_b.size(), sent.size());
+  for (uint16_t st : {uint16_t(1), uint16_t(3), uint16_t(5)}) {
+    std::vector<std::string> want, got;
+    for (auto& x : sent)
+      if (x.first == st) want.push_back(x.second);
+    for (auto& x : p.got_b)
+      if (x.first == st) got.push_back(x.second);
+    CHECK(want == got);
+  }
+}
+
 TEST(sctp_jumbo_bulk_throughput) {
   SctpPair p(0, 0, 0, 16000);
   p.a->set_initial_cwnd(1 << 20);
