@@ -330,4 +330,22 @@ std::string build_upstream_url(const std::string& upstream_base, const std::stri
   return base + request_path;
 }
 
+uint64_t FlowWindow::on_grant(uint64_t n, uint64_t now_us, uint64_t srtt_us) {
+  if (!epoch_t0) {  // the first grant opens the first measuring epoch
+    epoch_t0 = now_us ? now_us : 1;
+    return 0;
+  }
+  epoch_bytes += n;
+  if (epoch_bytes < uint64_t(win)) return 0;
+  uint64_t extra = 0;
+  const uint64_t grow_us = srtt_us ? 2 * srtt_us + kFlowGrowSlackUs : kFlowGrowUs;
+  if (win < kFlowMaxWindow && now_us - epoch_t0 < grow_us) {
+    extra = uint64_t(std::min(win, kFlowMaxWindow - win));
+    win += int64_t(extra);
+  }
+  epoch_bytes = 0;
+  epoch_t0 = now_us ? now_us : 1;
+  return extra;
+}
+
 }  // namespace p2pt::proto

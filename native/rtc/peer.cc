@@ -72,6 +72,11 @@ size_t DataChannel::send_window_hint() const {
   return pc && pc->sctp_ ? pc->sctp_->cwnd() : 0;
 }
 
+uint64_t DataChannel::rtt_hint_us() const {
+  auto pc = pc_.lock();
+  return pc && pc->sctp_ ? pc->sctp_->srtt_us() : 0;
+}
+
 // On same-host jumbo paths (16 KiB SCTP packets) body frames are sized to one
 // DATA chunk: no fragmentation on send, no reassembly copy on receive, and
 // finer interleaving of streams. On network paths (~1200 B packets) the

@@ -335,3 +335,39 @@ TEST(aesgcm_matches_evp_and_rejects_tampering) {
     }
   }
 }
+
+// "flow" window autotuning: a reader that takes a whole window within
+// kFlowGrowUs doubles it (up to kFlowMaxWindow); a slow reader never grows it.
+TEST(flow_window_autotune) {
+  using namespace p2pt::proto;
+  FlowWindow fast;
+  uint64_t t = 1000, extra = 0;
+  CHECK_EQ(fast.on_grant(64 * 1024, t, 0), uint64_t(0));  // opens the epoch
+  for (int i = 0; i < 400; i++) {
+    t += 2000;  // 64 KiB per 2 ms: 32 MB/s
+    extra += fast.on_grant(64 * 1024, t, 0);
+  }
+  CHECK_EQ(fast.win, int64_t(4 << 20));  // stops where a window takes > 100 ms (RTT unknown)
+  CHECK_EQ(extra, uint64_t((4 << 20) - kFlowWindow));
+
+  // Credit-bound at 50 ms RTT: each window is taken in one round trip.
+  FlowWindow wan;
+  t = 1000;
+  wan.on_grant(16 * 1024, t, 50000);
+  for (int i = 0; i < 64; i++) {
+    t += 50000;
+    wan.on_grant(uint64_t(wan.win), t, 50000);
+  }
+  CHECK_EQ(wan.win, kFlowMaxWindow);
+
+  FlowWindow slow;
+  t = 1000;
+  extra = 0;
+  slow.on_grant(16 * 1024, t, 0);
+  for (int i = 0; i < 400; i++) {
+    t += 200 * 1000;  // 16 KiB per 200 ms: 80 KB/s
+    extra += slow.on_grant(16 * 1024, t, 0);
+  }
+  CHECK_EQ(slow.win, kFlowWindow);
+  CHECK_EQ(extra, uint64_t(0));
+}

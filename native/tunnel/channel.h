@@ -44,6 +44,9 @@ class MessageChannel {
   // fraction of it queued in the channel, so on a slow path a token does
   // not wait behind a full 64 KiB of other streams' bodies.
   virtual size_t send_window_hint() const { return 0; }
+  // Smoothed round-trip time of the transport in microseconds; 0 = unknown.
+  // "flow" receivers size their per-stream windows from it.
+  virtual uint64_t rtt_hint_us() const { return 0; }
   // "multistream" extension: spread the frames of tunnel stream ids over
   // `lanes` extra transport streams (SCTP streams delivered independently),
   // so a loss on one stream's packets does not hold back the others. Frames of

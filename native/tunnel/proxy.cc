@@ -52,6 +52,7 @@ class ProxyWorker : public std::enable_shared_from_this<ProxyWorker> {
   size_t body_chunk() const { return shared_->body_chunk; }
   bool cancel_feature() const { return shared_->cancel_feature.load(std::memory_order_relaxed); }
   bool flow() const { return shared_->flow.load(std::memory_order_relaxed); }
+  uint64_t rtt_us() const { return shared_->rtt_us.load(std::memory_order_relaxed); }
   const ProxyConfig& config() const { return shared_->cfg; }
   Reactor& reactor() { return r_; }
   void conn_closed(ProxyConn* c);
@@ -141,7 +142,12 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
   // small again) are credit for serve to send more of this stream.
   void maybe_grant() {
     if (owed_ < proto::kFlowGrantMin || !conn_ || conn_->closed() || conn_->pending_out() > kGrantLow) return;
-    if (auto sess = sess_.lock()) sess->send(proto::make_credit(sid_, uint32_t(std::min<uint64_t>(owed_, UINT32_MAX))));
+    auto sess = sess_.lock();
+    if (!sess) return;
+    const uint64_t grow = rwin_.on_grant(owed_, Reactor::now_us(), sess->rtt_us());
+    if (grow) metrics::counter_add("tunnel_flow_window_growths_total");
+    const uint64_t g = owed_ + grow;
+    sess->send(proto::make_credit(sid_, uint32_t(std::min<uint64_t>(g, UINT32_MAX))));
     owed_ = 0;
   }
 
@@ -305,6 +311,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     send_credit_ = proto::kFlowWindow;
     credit_paused_ = false;
     owed_ = 0;
+    rwin_ = proto::FlowWindow{};
     sess->register_stream(sid_, weak_from_this());
     stream_registered_ = true;
     sess->send(std::move(hf));
@@ -546,6 +553,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
   bool credit_paused_ = false;   // "flow": upload out of serve's credit
   int64_t send_credit_ = proto::kFlowWindow;
   uint64_t owed_ = 0;            // "flow": RES_BODY bytes delivered, not yet granted back
+  proto::FlowWindow rwin_;       // "flow": RES_BODY window autotuning
   static constexpr size_t kGrantLow = 64 * 1024;
   bool sess_flow() const {
     auto s = sess_.lock();
@@ -957,6 +965,8 @@ void ProxySession::route(const proto::Frame& f) {
     }
     case MsgType::ResBody: {
       auto it = routes_.find(f.stream_id);
+      if (shared_->flow.load(std::memory_order_relaxed))
+        shared_->rtt_us.store(ch_ ? ch_->rtt_hint_us() : 0, std::memory_order_relaxed);
       if (it != routes_.end()) {
         Cmd c{Cmd::Body, f.stream_id};
         c.data = f.payload;

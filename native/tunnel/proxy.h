@@ -84,6 +84,7 @@ class ProxySession : public std::enable_shared_from_this<ProxySession> {
     std::atomic<bool> ready{false};
     std::atomic<bool> cancel_feature{false};
     std::atomic<bool> flow{false};  // "flow" negotiated: per-stream credit both ways
+    std::atomic<uint64_t> rtt_us{0};  // transport SRTT, refreshed as body frames arrive ("flow" windows)
     size_t body_chunk = proto::kMaxBodyChunk;
   };
   // Association thread -> a connection thread.

@@ -729,7 +729,12 @@ void ServeSession::on_event(Ev& ev) {
     return;
   }
   if (ev.kind == Ev::Credit) {  // the upstream took streamed request-body bytes
-    if (flow_) sched_->send(proto::make_credit(ev.sid, ev.bytes));
+    if (flow_) {
+      const uint64_t grow = it->second.upwin.on_grant(ev.bytes, Reactor::now_us(), ch_ ? ch_->rtt_hint_us() : 0);
+      if (grow) metrics::counter_add("tunnel_flow_window_growths_total");
+      const uint64_t g = ev.bytes + grow;
+      sched_->send(proto::make_credit(ev.sid, uint32_t(std::min<uint64_t>(g, UINT32_MAX))));
+    }
     return;
   }
   Inflight& fl = it->second;

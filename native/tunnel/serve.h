@@ -127,6 +127,7 @@ class ServeSession : public std::enable_shared_from_this<ServeSession> {
     bool uploading = false;   // request body still streaming to the upstream
     uint64_t uploaded = 0;    // request-body bytes received
     int64_t credit = proto::kFlowWindow;  // "flow": RES_BODY bytes we may still send
+    proto::FlowWindow upwin;              // "flow": streamed REQ_BODY window autotuning
   };
   // One upstream origin (one inference endpoint, e.g. one per GPU) and its
   // passive health: an origin that refuses connections is ejected for an

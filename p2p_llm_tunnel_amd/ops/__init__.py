@@ -27,7 +27,8 @@ class LlamaDims(ctypes.Structure):
 def lib() -> ctypes.CDLL:
     global _LIB
     if _LIB is None:
-        path = os.path.join(HERE, "_hip_ops.so")
+        # P2PT_HIP_OPS_LIB: another in-tree build of the same kernels (A/B runs on one box).
+        path = os.path.join(HERE, os.environ.get("P2PT_HIP_OPS_LIB", "_hip_ops.so"))
         if not os.path.exists(path):
             from . import build as _b
             _b.build()

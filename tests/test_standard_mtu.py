@@ -5,6 +5,7 @@ reference rtc.rs:31-72 via webrtc-rs defaults), forced on loopback with
 coalesced) and with both switched off (TUNNEL_NO_GSO / TUNNEL_NO_GRO)."""
 import http.client
 import json
+import time
 import urllib.request
 
 import pytest
@@ -67,3 +68,31 @@ def test_emulated_wan_path_with_loss(mock_upstream):
         m = _metrics(ms)
         assert m["tunnel_sctp_retransmits"] > 0  # losses happened and were repaired
         assert 15000 <= m["tunnel_sctp_srtt_us"] <= 200000
+
+
+def test_flow_window_grows_on_a_long_rtt_path(mock_upstream):
+    """50 ms RTT, 400 Mbit/s bottleneck with a one-BDP queue, no loss: 12 MiB
+    downloads on one keep-alive connection. A fixed 256 KiB "flow" window
+    caps a stream at 256 KiB per round trip (measured 4.8 MB/s before the
+    autotuning); the proxy's receive-window autotuning doubles it while
+    windows are taken within two round trips (measured 16 MB/s)."""
+    mp = free_port()
+    env = {"TUNNEL_FAULT_RTT_MS": "50", "TUNNEL_FAULT_RATE_MBPS": "400", "TUNNEL_FAULT_LOSS": "0",
+           "TUNNEL_FAULT_QUEUE_KB": "2441"}
+    n = 12 << 20
+    with Tunnel(mock_upstream, transport="webrtc", env=env, serve_extra=STD,
+                proxy_extra=STD + ["--metrics-listen", f"127.0.0.1:{mp}"]) as t:
+        c = http.client.HTTPConnection("127.0.0.1", t.proxy_port, timeout=60)
+        c.request("GET", "/bulk?bytes=65536")  # warm the association
+        assert len(c.getresponse().read()) == 65536
+        rates = []
+        for _ in range(2):  # the first also ramps SCTP's congestion window
+            t0 = time.time()
+            c.request("GET", f"/bulk?bytes={n}")
+            r = c.getresponse()
+            got = len(r.read())
+            rates.append(n / (time.time() - t0) / 1e6)
+            assert r.status == 200 and got == n
+        m = _metrics(mp)
+        assert m.get("tunnel_flow_window_growths_total", 0) >= 3  # 256 KiB -> >= 2 MiB
+        assert max(rates) > 8.0, rates
