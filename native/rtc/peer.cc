@@ -72,6 +72,14 @@ size_t DataChannel::send_window_hint() const {
   return pc && pc->sctp_ ? pc->sctp_->cwnd() : 0;
 }
 
+std::string DataChannel::debug_state() const {
+  auto pc = pc_.lock();
+  std::string s = "dc{buffered=" + std::to_string(buffered_amount()) + " low=" + std::to_string(buffered_low_threshold) +
+                  " above_low=" + std::to_string(int(above_low_)) + "} ";
+  if (pc && pc->sctp_) s += pc->sctp_->debug_state();
+  return s;
+}
+
 uint64_t DataChannel::rtt_hint_us() const {
   auto pc = pc_.lock();
   return pc && pc->sctp_ ? pc->sctp_->srtt_us() : 0;

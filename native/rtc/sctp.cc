@@ -752,8 +752,22 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
   size_t newly_acked = 0;
   size_t flight_before = flight_size_;
   bool cum_advanced = tsn_lt(cum_acked_, cum);
-  uint64_t rtt_sample = 0;
+  // RTT: one sample per SACK, from the most recently sent chunk it newly
+  // acknowledges that was transmitted once (Karn). A cumulative ack that
+  // also covers a retransmitted chunk gives no sample: it moved because a
+  // hole was filled, and the once-sent chunks behind the hole waited at the
+  // peer for that (counted as RTT, a tail loss repaired by probes inflated
+  // SRTT to seconds, and the RTO and probe timers with it).
+  uint64_t cum_sent = 0, gap_sent = 0;
+  bool cum_rtx = false;
   uint64_t newest_cum_sent = 0;
+  // RACK evidence from retransmitted chunks (RFC 8985 §6.2): an ack that
+  // arrives at least one minimum RTT after the latest transmission cannot be
+  // for an earlier copy, so that transmission was delivered.
+  uint64_t rtx_delivered = 0;
+  auto rtx_evidence = [&](const Chunk* ch) {
+    if (ch->tx > 1 && min_rtt_us_ && now - ch->sent_us >= min_rtt_us_) rtx_delivered = std::max(rtx_delivered, ch->sent_us);
+  };
   while (!inflight_.empty() && tsn_le(inflight_.front()->tsn, cum)) {
     Chunk* ch = inflight_.front();
     inflight_.pop_front();
@@ -761,8 +775,11 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
     if (!ch->acked) {
       newly_acked += ch->len;
       if (ch->tx == 1) {
-        rtt_sample = now - ch->sent_us;
+        cum_sent = std::max(cum_sent, ch->sent_us);
         newest_cum_sent = std::max(newest_cum_sent, ch->sent_us);
+      } else {
+        cum_rtx = true;
+        rtx_evidence(ch);
       }
     }
     free_chunk(ch);
@@ -782,11 +799,14 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
           ch->in_flight = false;
         }
         newly_acked += ch->len;
-        if (ch->tx == 1 && rtt_sample == 0) rtt_sample = now - ch->sent_us;
+        if (ch->tx == 1) gap_sent = std::max(gap_sent, ch->sent_us);
+        else rtx_evidence(ch);
       }
       if (tsn_lt(highest_gap, ch->tsn)) highest_gap = ch->tsn;
     }
   }
+  const uint64_t sample_sent = std::max(cum_rtx ? 0 : cum_sent, gap_sent);
+  const uint64_t rtt_sample = sample_sent ? std::max<uint64_t>(now - sample_sent, 1) : 0;
   if (rtt_sample) {
     update_rto(rtt_sample);
     if (!min_rtt_us_ || rtt_sample < min_rtt_us_) min_rtt_us_ = rtt_sample;
@@ -805,6 +825,7 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
   for (Chunk* ch : inflight_)
     if (ch->acked && ch->tx == 1 && ch->sent_us > rack_sent) rack_sent = ch->sent_us;
   if (cum_advanced) rack_sent = std::max(rack_sent, newest_cum_sent);
+  rack_sent = std::max(rack_sent, rtx_delivered);
   uint64_t reo = std::max<uint64_t>(srtt_us_ / 4, 1000);
   bool new_fast = false;
   auto mark = [&](Chunk* ch) {
@@ -1241,6 +1262,25 @@ void SctpAssociation::flush() {
   if (sent_any && !t3_timer_) start_t3();
   if (sent_any && !tlp_timer_) arm_tlp();
   if (sent_any && on_sent) on_sent();
+}
+
+std::string SctpAssociation::debug_state() const {
+  size_t rtx = 0, acked = 0, infl = 0;
+  for (const Chunk* ch : inflight_) {
+    rtx += ch->retransmit && !ch->acked;
+    acked += ch->acked;
+    infl += ch->in_flight;
+  }
+  char b[512];
+  snprintf(b, sizeof b,
+           "sctp{state=%d unsent=%zu sendq=%zu/%zu inflight=%zu(in_flight %zu, rtx %zu, gap-acked %zu) flight=%zu "
+           "cwnd=%zu ssthresh=%zu peer_rwnd=%zu t3=%d tlp=%d rto_ms=%llu srtt_us=%llu | rx ooo=%zu/%zuB held=%zuB "
+           "partial=%zu sack_needed=%d}",
+           int(state_), unsent_bytes_, sendq_.size(), sendq_pri_.size(), inflight_.size(), infl, rtx, acked,
+           flight_size_, cwnd_, ssthresh_, peer_rwnd_, t3_timer_ != 0, tlp_timer_ != 0,
+           static_cast<unsigned long long>(rto_us_ / 1000), static_cast<unsigned long long>(srtt_us_), ooo_.size(),
+           ooo_bytes_, held_bytes_, partial_.size(), int(sack_needed_));
+  return b;
 }
 
 }  // namespace p2pt::rtc

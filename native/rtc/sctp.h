@@ -112,6 +112,8 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   const SctpStats& stats() const { return stats_; }
   size_t cwnd() const { return cwnd_; }
   uint64_t srtt_us() const { return srtt_us_; }
+  // One-line sender/receiver state for the send-path stall watchdog.
+  std::string debug_state() const;
   uint64_t rto_us() const { return rto_us_; }
   void set_mtu(size_t mtu);
   void set_initial_cwnd(size_t c) { if (c > cwnd_) cwnd_ = c; }

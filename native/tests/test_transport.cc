@@ -1,6 +1,7 @@
 // Transport components in-process: SCTP association pair over a lossy,
 // reordering, duplicating link; DTLS pair; full PeerConnection pair over
 // loopback UDP (ICE + DTLS + SCTP + DCEP).
+#include <functional>
 #include <random>
 
 #include "core/reactor.h"
@@ -22,8 +23,13 @@ struct LossyLink {
   std::mt19937 rng{12345};
   uint64_t dropped = 0;
   LossyLink(Reactor& rr, double l, double d, uint64_t delay) : r(rr), loss(l), dup(d), max_delay_us(delay) {}
+  std::function<bool(const std::weak_ptr<SctpAssociation>&)> blackout;  // true: drop this packet
   void carry(std::weak_ptr<SctpAssociation> to, const uint8_t* p, size_t n) {
     std::uniform_real_distribution<double> u(0, 1);
+    if (blackout && blackout(to)) {
+      dropped++;
+      return;
+    }
     if (u(rng) < loss) {
       dropped++;
       return;
@@ -171,6 +177,46 @@ TEST(sctp_wan_tail_losses_recover_without_t3) {
          (unsigned long long)p.a->stats().tlp_probes, (unsigned long long)p.a->stats().t3_expirations,
          (unsigned long long)p.a->srtt_us(), (unsigned long long)p.a->rto_us());
   CHECK(p.a->stats().t3_expirations * 4 <= p.link.dropped);
+}
+
+TEST(sctp_tail_blackout_recovers_without_rtt_inflation) {
+  // 20 ms RTT, a bulk transfer with a full window in flight, then 40 ms in
+  // which every a -> b packet is lost: the whole tail of the window is gone
+  // and nothing after it is acknowledged, so RACK has no evidence and only a
+  // probe or T3 can repair it. The probe's acknowledgement must count as
+  // evidence (it arrived a minimum RTT after the retransmission, so it is for
+  // the retransmission) and mark the rest lost at once. Before: probes
+  // repaired one chunk per probe timeout, each repair moved the cumulative
+  // ack over chunks that had waited at the peer and were sampled as RTT
+  // (SRTT grew to seconds, the probe and T3 timers with it: a 40-55 s stall
+  // in the emulated-WAN benchmark).
+  SctpPair p(0, 0, 0, 1200, false, false, 100);
+  p.link.fixed_delay_us = 10000;
+  p.a->connect();
+  p.b->connect();
+  CHECK(p.r.run_until([&] { return p.a->established() && p.b->established(); }, 5000));
+  std::string blk = payload(10000, 3);
+  const int n = 600;  // 6 MB
+  for (int i = 0; i < n; i++) p.a->send(1, 53, {Bytes::copy(blk)});
+  const uint64_t t0 = Reactor::now_us();
+  std::weak_ptr<SctpAssociation> to_b = p.b;
+  uint64_t bo = 0;  // blackout start: when the last 100 KB are about to go out the first time
+  p.link.blackout = [&](const std::weak_ptr<SctpAssociation>& to) {
+    if (to.owner_before(to_b) || to_b.owner_before(to)) return false;  // b -> a: SACKs pass
+    const uint64_t now = Reactor::now_us();
+    if (!bo && p.a->buffered_amount() < 100000) bo = now;
+    return bo && now - bo < 40000;
+  };
+  CHECK(p.r.run_until([&] { return p.got_b.size() == size_t(n); }, 20000));
+  const double secs = double(Reactor::now_us() - t0) / 1e6;
+  CHECK_EQ(p.got_b.size(), size_t(n));
+  printf("  tail blackout: %llu dropped, %.2f s, %llu fast rtx, %llu TLP, %llu T3, srtt %llu us\n",
+         (unsigned long long)p.link.dropped, secs, (unsigned long long)p.a->stats().fast_retransmits,
+         (unsigned long long)p.a->stats().tlp_probes, (unsigned long long)p.a->stats().t3_expirations,
+         (unsigned long long)p.a->srtt_us());
+  CHECK(p.link.dropped > 20);
+  CHECK(secs < 3.0);
+  CHECK(p.a->srtt_us() < 100000);
 }
 
 TEST(sctp_priority_messages_keep_stream_order) {

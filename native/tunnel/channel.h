@@ -47,6 +47,8 @@ class MessageChannel {
   // Smoothed round-trip time of the transport in microseconds; 0 = unknown.
   // "flow" receivers size their per-stream windows from it.
   virtual uint64_t rtt_hint_us() const { return 0; }
+  // Transport state for the send-path stall watchdog (empty: nothing to add).
+  virtual std::string debug_state() const { return ""; }
   // "multistream" extension: spread the frames of tunnel stream ids over
   // `lanes` extra transport streams (SCTP streams delivered independently),
   // so a loss on one stream's packets does not hold back the others. Frames of

@@ -726,6 +726,8 @@ void ProxySession::release_links(const std::string& fail_why) {
 ProxySession::~ProxySession() {
   if (agree_timer_) r_.cancel(agree_timer_);
   if (ping_timer_) r_.cancel(ping_timer_);
+  if (wd_timer_) r_.cancel(wd_timer_);
+  wd_timer_ = 0;
   if (ch_) {
     ch_->on_message = nullptr;
     ch_->on_closed = nullptr;
@@ -742,6 +744,8 @@ void ProxySession::stop(const std::string& why) {
   shared_->ready = false;
   if (agree_timer_) r_.cancel(agree_timer_);
   if (ping_timer_) r_.cancel(ping_timer_);
+  if (wd_timer_) r_.cancel(wd_timer_);
+  wd_timer_ = 0;
   agree_timer_ = ping_timer_ = 0;
   listener_.reset();  // like the reference, the listener dies with the session
   routes_.clear();
@@ -839,6 +843,7 @@ void ProxySession::on_agree(const proto::Frame& f) {
   shared_->ready = true;
   last_pong_ms_ = Reactor::now_ms();
   send_ping();
+  watchdog();
   if (!listener_ && !cfg_.listen_early) {
     if (!bind_listener()) return;
   }
@@ -873,6 +878,28 @@ void ProxySession::accept(int fd) {
   Cmd c{Cmd::Adopt};
   c.fd = fd;
   command(k, std::move(c));
+}
+
+// Send-path stall watchdog: once a second, frames or channel bytes that are
+// waiting without any having moved since the last tick are logged with the
+// scheduler / data channel / SCTP state (and counted), so a stalled tunnel
+// says why.
+void ProxySession::watchdog() {
+  if (stopped_) return;
+  if (sched_ && sched_->stalled_tick()) {
+    if (++wd_stalled_s_ == 1) metrics::counter_add("tunnel_send_stalls_total");
+    if (wd_stalled_s_ <= 3 || wd_stalled_s_ % 10 == 0)
+      LOG_WARN(kT, "send path stalled for %d s: %s", wd_stalled_s_, sched_->debug_state().c_str());
+  } else {
+    wd_stalled_s_ = 0;
+  }
+  std::weak_ptr<ProxySession> w = shared_from_this();
+  wd_timer_ = r_.call_later_ms(1000, [w] {
+    if (auto s = w.lock()) {
+      s->wd_timer_ = 0;
+      s->watchdog();
+    }
+  });
 }
 
 void ProxySession::send_ping() {

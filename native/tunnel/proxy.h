@@ -123,6 +123,7 @@ class ProxySession : public std::enable_shared_from_this<ProxySession> {
   void on_agree(const proto::Frame& f);
   void route(const proto::Frame& f);
   void send_ping();
+  void watchdog();  // send-path stall watchdog (1 s)
   bool bind_listener();
   void on_event(size_t thread, Ev& ev);
   void check_paused();
@@ -145,6 +146,8 @@ class ProxySession : public std::enable_shared_from_this<ProxySession> {
   std::string psk_nonce_;  // psk extension: the nonce our HELLO carried
   uint64_t agree_timer_ = 0;
   uint64_t ping_timer_ = 0;
+  uint64_t wd_timer_ = 0;
+  int wd_stalled_s_ = 0;
   uint64_t last_pong_ms_ = 0;
   friend class ProxyWorker;
 };

@@ -21,7 +21,25 @@ bool FrameScheduler::emit(const proto::Frame& f) {
   uint8_t hdr[proto::kHeaderLen];
   f.header(hdr);
   metrics::frame_sent(uint8_t(f.type), f.wire_size());
+  emitted_++;
   return ch_->send(hdr, sizeof hdr, f.payload);
+}
+
+bool FrameScheduler::stalled_tick() {
+  const size_t buffered = ch_ ? ch_->buffered_amount() : 0;
+  const bool waiting = queued_ > 0 || buffered > 0;
+  const bool stalled = waiting && emitted_ == wd_emitted_ && buffered == wd_buffered_;
+  wd_emitted_ = emitted_;
+  wd_buffered_ = buffered;
+  return stalled;
+}
+
+std::string FrameScheduler::debug_state() const {
+  std::string s = "sched{queued=" + std::to_string(queued_) + " control=" + std::to_string(control_.size()) +
+                  " interactive=" + std::to_string(interactive_.size()) + " bulk=" + std::to_string(bulk_.size()) +
+                  " streams=" + std::to_string(streams_.size()) + " window=" + std::to_string(window()) +
+                  " emitted=" + std::to_string(emitted_) + " pumping=" + std::to_string(int(pumping_)) + "} ";
+  return s + (ch_ ? ch_->debug_state() : "");
 }
 
 void FrameScheduler::list(uint32_t sid, StreamQ& s) {

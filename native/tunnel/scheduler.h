@@ -39,6 +39,10 @@ class FrameScheduler {
   // Bytes held here plus bytes buffered in the channel.
   size_t pending_bytes() const { return queued_ + (ch_ ? ch_->buffered_amount() : 0); }
   size_t queued_bytes() const { return queued_; }
+  // Send-path stall watchdog, called about once a second: true when frames
+  // or channel bytes are waiting and neither moved since the previous call.
+  bool stalled_tick();
+  std::string debug_state() const;
   // Bytes of `sid` held in the scheduler (not yet handed to the channel).
   size_t stream_queued(uint32_t sid) const {
     auto it = streams_.find(sid);
@@ -77,6 +81,9 @@ class FrameScheduler {
   std::unordered_map<uint32_t, StreamQ> streams_;
   std::deque<uint32_t> interactive_, bulk_;
   size_t queued_ = 0;
+  uint64_t emitted_ = 0;  // frames handed to the channel
+  uint64_t wd_emitted_ = 0;
+  size_t wd_buffered_ = 0;
   size_t high_ = SIZE_MAX, low_ = 0;
   bool was_high_ = false;
   std::function<void()> low_cb_;

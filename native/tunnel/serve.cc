@@ -318,6 +318,8 @@ void ServeSession::release_links() {
 ServeSession::~ServeSession() {
   if (hello_timer_) r_.cancel(hello_timer_);
   if (ping_timer_) r_.cancel(ping_timer_);
+  if (wd_timer_) r_.cancel(wd_timer_);
+  wd_timer_ = 0;
   release_links();
   if (ch_) {
     ch_->on_message = nullptr;
@@ -332,6 +334,8 @@ void ServeSession::stop(const std::string& why) {
   stopped_ = true;
   if (hello_timer_) r_.cancel(hello_timer_);
   if (ping_timer_) r_.cancel(ping_timer_);
+  if (wd_timer_) r_.cancel(wd_timer_);
+  wd_timer_ = 0;
   hello_timer_ = ping_timer_ = 0;
   inflight_.clear();
   paused_.clear();
@@ -426,6 +430,29 @@ void ServeSession::on_hello(const proto::Frame& f) {
   if (cfg_.upstream_prewarm) command(0, Cmd{Cmd::Prewarm});
   last_pong_ms_ = Reactor::now_ms();
   send_ping();  // tokio::time::interval's first tick is immediate
+  watchdog();
+}
+
+// Send-path stall watchdog: once a second, frames or channel bytes that are
+// waiting without any having moved since the last tick are logged with the
+// scheduler / data channel / SCTP state (and counted), so a stalled tunnel
+// says why.
+void ServeSession::watchdog() {
+  if (stopped_) return;
+  if (sched_ && sched_->stalled_tick()) {
+    if (++wd_stalled_s_ == 1) metrics::counter_add("tunnel_send_stalls_total");
+    if (wd_stalled_s_ <= 3 || wd_stalled_s_ % 10 == 0)
+      LOG_WARN(kT, "send path stalled for %d s: %s", wd_stalled_s_, sched_->debug_state().c_str());
+  } else {
+    wd_stalled_s_ = 0;
+  }
+  std::weak_ptr<ServeSession> w = shared_from_this();
+  wd_timer_ = r_.call_later_ms(1000, [w] {
+    if (auto s = w.lock()) {
+      s->wd_timer_ = 0;
+      s->watchdog();
+    }
+  });
 }
 
 void ServeSession::send_ping() {

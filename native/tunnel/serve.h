@@ -160,6 +160,7 @@ class ServeSession : public std::enable_shared_from_this<ServeSession> {
   void start_request(uint32_t sid, Pending p, bool streaming);
   void send_simple_response(uint32_t sid, uint16_t status, const std::string& body);
   void send_ping();
+  void watchdog();  // send-path stall watchdog (1 s)
   void on_event(Ev& ev);
   void check_paused();
   void set_paused(uint32_t sid, Inflight& fl);
@@ -178,6 +179,8 @@ class ServeSession : public std::enable_shared_from_this<ServeSession> {
   bool flow_ = false;  // "flow" negotiated: per-stream credit both ways
   uint64_t hello_timer_ = 0;
   uint64_t ping_timer_ = 0;
+  uint64_t wd_timer_ = 0;
+  int wd_stalled_s_ = 0;
   uint64_t last_pong_ms_ = 0;
   std::unordered_map<uint32_t, Pending> streams_;
   std::unordered_map<uint32_t, Inflight> inflight_;

@@ -416,6 +416,13 @@ class FrontEnd:
             return
         self._ready.set()
         self.loop.run_forever()
+        # Stopped: cancel the keep-alive connection tasks still parked in a
+        # read and let them unwind, so none is destroyed while pending.
+        pending = [t for t in asyncio.all_tasks(self.loop) if not t.done()]
+        for t in pending:
+            t.cancel()
+        if pending:
+            self.loop.run_until_complete(asyncio.gather(*pending, return_exceptions=True))
 
     def shutdown(self):
         def stop():
