@@ -71,6 +71,7 @@ struct SctpAssociation::Chunk {
   bool in_flight = false;   // counted in flight_size_
   bool retransmit = false;  // marked for retransmission
   bool fast = false;        // marked by fast retransmit (may bypass cwnd once)
+  bool probe = false;       // latest transmission was a tail-loss probe
 };
 
 struct SctpAssociation::InChunk {
@@ -752,21 +753,27 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
   size_t newly_acked = 0;
   size_t flight_before = flight_size_;
   bool cum_advanced = tsn_lt(cum_acked_, cum);
-  // RTT: one sample per SACK, from the most recently sent chunk it newly
-  // acknowledges that was transmitted once (Karn). A cumulative ack that
-  // also covers a retransmitted chunk gives no sample: it moved because a
-  // hole was filled, and the once-sent chunks behind the hole waited at the
-  // peer for that (counted as RTT, a tail loss repaired by probes inflated
-  // SRTT to seconds, and the RTO and probe timers with it).
-  uint64_t cum_sent = 0, gap_sent = 0;
-  bool cum_rtx = false;
+  // RTT: one sample per SACK from a chunk transmitted once (Karn): the
+  // highest one the cumulative ack newly covers, else the first newly
+  // gap-acked one. A cumulative ack that moved because a tail-loss probe
+  // filled a hole gives no sample: the chunks behind the hole waited at the
+  // peer for the probe (a tail repaired probe by probe inflated SRTT to
+  // seconds, and the RTO and probe timers with it). Taking the newest chunk
+  // of every SACK instead, and dropping every cumulative sample that covers
+  // any retransmission, kept SRTT lower but tripled the SSE tail next to
+  // bulk at 50 ms / 2 % loss (fewer losses read as congestion).
+  uint64_t cum_sample = 0, gap_sample = 0;
+  bool cum_probe = false;
   uint64_t newest_cum_sent = 0;
-  // RACK evidence from retransmitted chunks (RFC 8985 §6.2): an ack that
-  // arrives at least one minimum RTT after the latest transmission cannot be
-  // for an earlier copy, so that transmission was delivered.
+  // RACK evidence from a tail-loss probe (RFC 8985 §6.2, §7): an ack that
+  // arrives at least one minimum RTT after the probe cannot be for an earlier
+  // copy, so the probe was delivered and every chunk sent well before it that
+  // is still unacknowledged is lost. (Ordinary retransmissions are not used:
+  // behind a standing queue their acks are often the original's, and on a
+  // 50 ms / 2 % path treating them as evidence tripled the SSE tail.)
   uint64_t rtx_delivered = 0;
   auto rtx_evidence = [&](const Chunk* ch) {
-    if (ch->tx > 1 && min_rtt_us_ && now - ch->sent_us >= min_rtt_us_) rtx_delivered = std::max(rtx_delivered, ch->sent_us);
+    if (ch->probe && min_rtt_us_ && now - ch->sent_us >= min_rtt_us_) rtx_delivered = std::max(rtx_delivered, ch->sent_us);
   };
   while (!inflight_.empty() && tsn_le(inflight_.front()->tsn, cum)) {
     Chunk* ch = inflight_.front();
@@ -775,10 +782,10 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
     if (!ch->acked) {
       newly_acked += ch->len;
       if (ch->tx == 1) {
-        cum_sent = std::max(cum_sent, ch->sent_us);
+        cum_sample = now - ch->sent_us;
         newest_cum_sent = std::max(newest_cum_sent, ch->sent_us);
       } else {
-        cum_rtx = true;
+        cum_probe |= ch->probe;
         rtx_evidence(ch);
       }
     }
@@ -799,14 +806,13 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
           ch->in_flight = false;
         }
         newly_acked += ch->len;
-        if (ch->tx == 1) gap_sent = std::max(gap_sent, ch->sent_us);
-        else rtx_evidence(ch);
+        if (ch->tx == 1 && !gap_sample) gap_sample = std::max<uint64_t>(now - ch->sent_us, 1);
+        else if (ch->tx > 1) rtx_evidence(ch);
       }
       if (tsn_lt(highest_gap, ch->tsn)) highest_gap = ch->tsn;
     }
   }
-  const uint64_t sample_sent = std::max(cum_rtx ? 0 : cum_sent, gap_sent);
-  const uint64_t rtt_sample = sample_sent ? std::max<uint64_t>(now - sample_sent, 1) : 0;
+  const uint64_t rtt_sample = cum_sample && !cum_probe ? cum_sample : (cum_sample ? 0 : gap_sample);
   if (rtt_sample) {
     update_rto(rtt_sample);
     if (!min_rtt_us_ || rtt_sample < min_rtt_us_) min_rtt_us_ = rtt_sample;
@@ -832,6 +838,7 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
     ch->miss = 0;
     ch->retransmit = true;
     ch->fast = true;
+    ch->probe = false;
     if (ch->in_flight) {
       flight_size_ -= ch->len;
       ch->in_flight = false;
@@ -924,6 +931,7 @@ void SctpAssociation::on_tlp() {
     if (ch->acked || ch->retransmit) continue;
     ch->retransmit = true;
     ch->fast = true;  // may go out even when cwnd is full
+    ch->probe = true;
     if (ch->in_flight) {
       flight_size_ -= ch->len;
       ch->in_flight = false;
@@ -1075,6 +1083,7 @@ void SctpAssociation::on_t3() {
     if (ch->acked) continue;
     ch->retransmit = true;
     ch->fast = false;
+    ch->probe = false;
     if (ch->in_flight) {
       flight_size_ -= ch->len;
       ch->in_flight = false;
