@@ -330,7 +330,7 @@ std::string build_upstream_url(const std::string& upstream_base, const std::stri
   return base + request_path;
 }
 
-uint64_t FlowWindow::on_grant(uint64_t n, uint64_t now_us, uint64_t srtt_us) {
+uint64_t FlowWindow::on_grant(uint64_t n, uint64_t now_us, uint64_t rtt_us) {
   if (!epoch_t0) {  // the first grant opens the first measuring epoch
     epoch_t0 = now_us ? now_us : 1;
     return 0;
@@ -338,8 +338,18 @@ uint64_t FlowWindow::on_grant(uint64_t n, uint64_t now_us, uint64_t srtt_us) {
   epoch_bytes += n;
   if (epoch_bytes < uint64_t(win)) return 0;
   uint64_t extra = 0;
-  const uint64_t grow_us = srtt_us ? 2 * srtt_us + kFlowGrowSlackUs : kFlowGrowUs;
-  if (win < kFlowMaxWindow && now_us - epoch_t0 < grow_us) {
+  const uint64_t elapsed = std::max<uint64_t>(now_us - epoch_t0, 1);
+  bool grow;
+  if (rtt_us) {
+    // Credit-bound: taken within two round trips, and two bandwidth-delay
+    // products at the rate it was taken exceed the window (on a LAN a
+    // window lasts many round trips: growing there only adds buffering).
+    const double bdp2 = 2.0 * double(epoch_bytes) / double(elapsed) * double(rtt_us);
+    grow = elapsed < 2 * rtt_us + kFlowGrowSlackUs && bdp2 > double(win);
+  } else {
+    grow = elapsed < kFlowGrowUs;
+  }
+  if (win < kFlowMaxWindow && grow) {
     extra = uint64_t(std::min(win, kFlowMaxWindow - win));
     win += int64_t(extra);
   }

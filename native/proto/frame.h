@@ -161,11 +161,12 @@ constexpr size_t kFlowGrantMin = 16 * 1024;
 // sender's window). A fixed 256 KiB window caps one stream at 256 KiB per
 // round trip (5 MB/s at 50 ms RTT) however fast the path and the reader. A
 // credit-bound stream's reader takes a whole window in about one round trip,
-// so a window taken within 2 SRTT + 20 ms (kFlowGrowUs while the RTT is
-// unknown) doubles, up to kFlowMaxWindow: a path-bound stream stops near two
-// bandwidth-delay products, and a slow reader (a window per several round
-// trips) never grows it, which keeps the per-stream memory bound that the
-// extension exists for.
+// so a window taken within 2 RTT + 20 ms whose two bandwidth-delay products
+// (at the rate it was taken) exceed it doubles (within kFlowGrowUs while the
+// RTT is unknown), up to kFlowMaxWindow: a path-bound stream stops near two
+// BDPs, a LAN stream (a window lasts many sub-ms round trips) stays put, and
+// a slow reader (a window per several round trips) never grows it, which
+// keeps the per-stream memory bound that the extension exists for.
 constexpr int64_t kFlowMaxWindow = 8 * 1024 * 1024;
 constexpr uint64_t kFlowGrowUs = 100 * 1000;
 constexpr uint64_t kFlowGrowSlackUs = 20 * 1000;
@@ -175,9 +176,9 @@ struct FlowWindow {
   uint64_t epoch_bytes = 0;  // granted since epoch_t0
   uint64_t epoch_t0 = 0;     // 0: no grant yet
   // `n` consumed bytes are about to be granted back at `now_us` on a path of
-  // smoothed RTT `srtt_us` (0: unknown): returns the extra credit to add to
+  // base RTT `rtt_us` (0: unknown): returns the extra credit to add to
   // that grant (the window's growth, usually 0).
-  uint64_t on_grant(uint64_t n, uint64_t now_us, uint64_t srtt_us);
+  uint64_t on_grant(uint64_t n, uint64_t now_us, uint64_t rtt_us);
 };
 
 // Upstream URL rewrite (reference serve.rs:167-185, incl. quirk Q1: the prefix

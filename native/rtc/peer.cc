@@ -82,7 +82,7 @@ std::string DataChannel::debug_state() const {
 
 uint64_t DataChannel::rtt_hint_us() const {
   auto pc = pc_.lock();
-  return pc && pc->sctp_ ? pc->sctp_->srtt_us() : 0;
+  return pc && pc->sctp_ ? pc->sctp_->min_rtt_us() : 0;
 }
 
 // On same-host jumbo paths (16 KiB SCTP packets) body frames are sized to one

@@ -112,6 +112,7 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   const SctpStats& stats() const { return stats_; }
   size_t cwnd() const { return cwnd_; }
   uint64_t srtt_us() const { return srtt_us_; }
+  uint64_t min_rtt_us() const { return min_rtt_us_; }  // smallest RTT sample: the path's base RTT
   // One-line sender/receiver state for the send-path stall watchdog.
   std::string debug_state() const;
   uint64_t rto_us() const { return rto_us_; }

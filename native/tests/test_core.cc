@@ -360,6 +360,17 @@ TEST(flow_window_autotune) {
   }
   CHECK_EQ(wan.win, kFlowMaxWindow);
 
+  // LAN: 0.3 ms RTT, a fast reader (64 KiB per 200 us, 330 MB/s): 256 KiB
+  // already covers two BDPs, so the window stays.
+  FlowWindow lan;
+  t = 1000;
+  lan.on_grant(64 * 1024, t, 300);
+  for (int i = 0; i < 400; i++) {
+    t += 200;
+    lan.on_grant(64 * 1024, t, 300);
+  }
+  CHECK_EQ(lan.win, kFlowWindow);
+
   FlowWindow slow;
   t = 1000;
   extra = 0;

@@ -44,8 +44,9 @@ class MessageChannel {
   // fraction of it queued in the channel, so on a slow path a token does
   // not wait behind a full 64 KiB of other streams' bodies.
   virtual size_t send_window_hint() const { return 0; }
-  // Smoothed round-trip time of the transport in microseconds; 0 = unknown.
-  // "flow" receivers size their per-stream windows from it.
+  // The transport's base round-trip time (smallest sample) in microseconds;
+  // 0 = unknown. "flow" receivers size their per-stream windows from it: the
+  // path's bandwidth-delay product, not the queueing a bulk load adds.
   virtual uint64_t rtt_hint_us() const { return 0; }
   // Transport state for the send-path stall watchdog (empty: nothing to add).
   virtual std::string debug_state() const { return ""; }
