@@ -45,7 +45,7 @@ def result(p, timeout=900):
 
 SCTP_GAUGES = ("tunnel_sctp_fast_retransmits", "tunnel_sctp_t3_expirations", "tunnel_sctp_tlp_probes",
                "tunnel_sctp_rack_marks", "tunnel_sctp_random_loss_events", "tunnel_sctp_cwnd_bytes",
-               "tunnel_sctp_rto_us", "tunnel_sctp_packets_sent")
+               "tunnel_sctp_rto_us", "tunnel_sctp_packets_sent", "tunnel_sctp_dup_copies")
 
 
 def scrape(port):

@@ -426,6 +426,10 @@ void PeerConnection::start_sctp() {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().packets_sent) : 0.0;
   });
+  metrics::gauge_fn("tunnel_sctp_dup_copies", [w] {
+    auto s = w.lock();
+    return s && s->sctp_ ? double(s->sctp_->stats().dup_copies_sent) : 0.0;
+  });
   metrics::gauge_fn("tunnel_sctp_tlp_probes", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().tlp_probes) : 0.0;

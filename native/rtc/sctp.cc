@@ -3,6 +3,7 @@
 #include <openssl/hmac.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "core/crypto.h"
@@ -1158,7 +1159,7 @@ void SctpAssociation::flush() {
     return;
   }
   uint64_t now = Reactor::now_us();
-  auto add_data = [&](Chunk* ch) {
+  auto add_data = [&](Chunk* ch, bool copy) {
     size_t padded = (ch->len + 3) & ~size_t(3);
     size_t need = kDataHdr + padded;
     if (pkt_len_ + need > mtu) flush_pkt();
@@ -1185,6 +1186,10 @@ void SctpAssociation::flush() {
     }
     pkt.insert(pkt.end(), padded - ch->len, 0);
     pkt_len_ += need;
+    if (copy) {  // redundant copy: bytes on the wire only, no sender state
+      stats_.dup_copies_sent++;
+      return;
+    }
     ch->sent_us = now;
     ch->tx++;
     if (!ch->in_flight) {
@@ -1207,7 +1212,7 @@ void SctpAssociation::flush() {
     ch->retransmit = false;
     ch->fast = false;
     ch->miss = 0;
-    add_data(ch);
+    add_data(ch, false);
     stats_.retransmits++;
     sent_any = true;
   }
@@ -1222,6 +1227,7 @@ void SctpAssociation::flush() {
   // SACKs, up to a round trip on a WAN path. The allowance bounds what this
   // adds to a congested path (interactive traffic is a trickle).
   const size_t pri_allow = 4 * mtu;
+  const bool dup = dup_small_enabled();
   for (int round = 0; round < 256; round++) {
   bool progressed = false;
   while (!sendq_pri_.empty() || !sendq_.empty()) {
@@ -1254,7 +1260,8 @@ void SctpAssociation::flush() {
     m.off += take;
     unsent_bytes_ -= take;
     inflight_.push_back(ch);
-    add_data(ch);
+    add_data(ch, false);
+    if (dup && ch->flags == (ch->flags | 3) && ch->len <= kDupMaxChunk) dup_.push_back(ch);
     peer_rwnd_ = peer_rwnd_ > take ? peer_rwnd_ - take : 0;
     sent_any = true;
     if (m.off == m.len) {
@@ -1268,6 +1275,16 @@ void SctpAssociation::flush() {
   if (closed_fired_ || unsent_bytes_ == before) break;
   }
   flush_pkt();
+  // Redundant copies of this flush's small whole messages (SSE tokens,
+  // credit, pings), in packets of their own after the originals: on a path
+  // that loses packets at random a token then arrives unless both copies are
+  // lost, instead of waiting a loss-recovery round trip (the receiver drops
+  // the second copy and reports it as a duplicate).
+  if (!dup_.empty()) {
+    for (Chunk* ch : dup_) add_data(ch, true);
+    dup_.clear();
+    flush_pkt();
+  }
   if (sent_any && !t3_timer_) start_t3();
   if (sent_any && !tlp_timer_) arm_tlp();
   if (sent_any && on_sent) on_sent();
@@ -1290,6 +1307,20 @@ std::string SctpAssociation::debug_state() const {
            static_cast<unsigned long long>(rto_us_ / 1000), static_cast<unsigned long long>(srtt_us_), ooo_.size(),
            ooo_bytes_, held_bytes_, partial_.size(), int(sack_needed_));
   return b;
+}
+
+// Redundant copies of small messages: TUNNEL_SCTP_DUP=1 always, =0 never;
+// by default on once the path has shown random loss (at least 8 loss
+// events, more than 1 in 400 data chunks sent). A lossless LAN path never
+// pays for it; tokens are ~100-300 bytes, so doubling them costs little.
+bool SctpAssociation::dup_small_enabled() const {
+  static const int mode = [] {
+    const char* e = getenv("TUNNEL_SCTP_DUP");
+    return e && *e ? atoi(e) : -1;
+  }();
+  if (mode >= 0) return mode != 0;
+  const uint64_t losses = stats_.fast_retransmits + stats_.tlp_probes + stats_.t3_expirations;
+  return losses >= 8 && losses * 400 > stats_.data_chunks_sent;
 }
 
 }  // namespace p2pt::rtc

@@ -56,6 +56,7 @@ struct SctpStats {
   uint64_t data_chunks_sent = 0, data_chunks_received = 0;
   uint64_t retransmits = 0, fast_retransmits = 0, t3_expirations = 0;
   uint64_t tlp_probes = 0, rack_marks = 0, random_loss_events = 0;
+  uint64_t dup_copies_sent = 0;  // redundant copies of small messages (lossy paths)
   uint64_t early_deliveries = 0;  // messages handed up ahead of a TSN gap (another stream's loss)
   uint64_t sacks_sent = 0, sacks_received = 0;
   uint64_t bytes_sent = 0, bytes_received = 0;
@@ -200,6 +201,9 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   std::deque<Msg> sendq_pri_;  // single-chunk priority messages (send_framed(..., priority))
   std::map<uint16_t, uint16_t> next_ssn_;
   std::deque<Chunk*> inflight_;  // ordered by TSN
+  std::vector<Chunk*> dup_;      // this flush's small whole messages to send twice
+  static constexpr size_t kDupMaxChunk = 512;
+  bool dup_small_enabled() const;
   size_t unsent_bytes_ = 0;
   size_t flight_size_ = 0;
   size_t cwnd_ = 0, ssthresh_ = 0, partial_acked_ = 0;

@@ -177,6 +177,10 @@ TEST(sctp_wan_tail_losses_recover_without_t3) {
          (unsigned long long)p.a->stats().tlp_probes, (unsigned long long)p.a->stats().t3_expirations,
          (unsigned long long)p.a->srtt_us(), (unsigned long long)p.a->rto_us());
   CHECK(p.a->stats().t3_expirations * 4 <= p.link.dropped);
+  // Random loss turned on redundant copies of the small messages; the peer
+  // still delivered each message exactly once (got_b holds 1200, above).
+  CHECK(p.a->stats().dup_copies_sent > 100);
+  printf("  redundant copies: %llu\n", (unsigned long long)p.a->stats().dup_copies_sent);
 }
 
 TEST(sctp_tail_blackout_recovers_without_rtt_inflation) {
