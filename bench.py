@@ -72,10 +72,18 @@ def dist_init():
     return dist, dist.get_rank(), dist.get_world_size()
 
 
+_DEVICE_SET = False
+
+
 def sync_device():
+    """Synchronise this rank's GPU (one rank per GPU: LOCAL_RANK's device)."""
+    global _DEVICE_SET
     try:
         import torch
         if torch.cuda.is_available():
+            if not _DEVICE_SET:
+                torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
+                _DEVICE_SET = True
             torch.cuda.synchronize()
     except Exception:
         pass

@@ -883,13 +883,14 @@ void ProxySession::accept(int fd) {
 // Send-path stall watchdog: once a second, frames or channel bytes that are
 // waiting without any having moved since the last tick are logged with the
 // scheduler / data channel / SCTP state (and counted), so a stalled tunnel
-// says why.
+// says why, and the scheduler is pumped once more.
 void ProxySession::watchdog() {
   if (stopped_) return;
   if (sched_ && sched_->stalled_tick()) {
     if (++wd_stalled_s_ == 1) metrics::counter_add("tunnel_send_stalls_total");
     if (wd_stalled_s_ <= 3 || wd_stalled_s_ % 10 == 0)
       LOG_WARN(kT, "send path stalled for %d s: %s", wd_stalled_s_, sched_->debug_state().c_str());
+    sched_->pump();  // heals a missed channel wake-up; a no-op when the transport is the one waiting
   } else {
     wd_stalled_s_ = 0;
   }
