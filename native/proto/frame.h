@@ -109,7 +109,13 @@ std::string psk_mac(const std::string& secret, const char* role, const std::stri
 // credit, Q11) and "multistream" (tunnel streams spread over independently
 // delivered SCTP streams, MessageChannel::set_lanes) are only *acted on* when
 // both peers list them, so reference peers are unaffected.
-constexpr int kLanes = 16;
+// Lanes: 64 (the most a peer accepts, DataChannel::kMaxLanes). A tunnel stream
+// rides lane sid % kLanes, so two streams share a lane (and a loss on one
+// holds the other) only when their ids differ by a multiple of it; with 16,
+// an SSE stream opened 16 streams after a bulk download shared its lane, and
+// on the emulated 50 ms / 2 % path that put bulk loss recovery in the token
+// tail.
+constexpr int kLanes = 64;
 const std::vector<std::string>& our_features();
 // Negotiate from a peer HELLO (reference Agree::from_hello, protocol.rs:44-80).
 bool agree_from_hello(const Hello& h, Agree& out, std::string* err,

@@ -88,12 +88,22 @@ uint64_t DataChannel::rtt_hint_us() const {
 // On same-host jumbo paths (16 KiB SCTP packets) body frames are sized to one
 // DATA chunk: no fragmentation on send, no reassembly copy on receive, and
 // finer interleaving of streams. On network paths (~1200 B packets) the
-// reference's 65408 B frames are kept.
+// reference's 65408 B frames are kept while the congestion window is large;
+// once it is small (a lossy WAN), a frame is cut to about an eighth of it
+// (whole DATA chunks, at least one): an SCTP message's fragments go out
+// back to back, so an SSE token queued behind a 64 KB body frame waited for
+// the whole frame, several round trips at a 20-40 KB window (the 150 ms
+// SSE-next-to-bulk tail at 50 ms RTT / 2 % loss). Sized when a response
+// starts, for that response.
 size_t DataChannel::body_chunk() const {
   auto pc = pc_.lock();
   size_t mtu = pc ? pc->mtu_ : 0;
-  if (mtu < 8192) return proto::kMaxBodyChunk;
-  return mtu - 12 - 16 - proto::kHeaderLen;  // SCTP common + DATA chunk headers, frame header
+  const size_t per_chunk = mtu > 12 + 16 ? mtu - 12 - 16 : 0;  // SCTP common + DATA chunk headers
+  if (mtu >= 8192) return per_chunk - proto::kHeaderLen;       // one chunk, less the frame header
+  const size_t cw = pc && pc->sctp_ ? pc->sctp_->cwnd() : 0;
+  if (!per_chunk || cw == 0 || cw >= kSmallCwnd) return proto::kMaxBodyChunk;
+  const size_t chunks = std::max<size_t>(1, cw / 8 / per_chunk);
+  return std::min(proto::kMaxBodyChunk, chunks * per_chunk - proto::kHeaderLen);
 }
 
 // Both DTLS certificate fingerprints (ours and the one the remote SDP pinned

@@ -940,6 +940,13 @@ void SctpAssociation::on_tlp() {
     tlp_count_++;
     stats_.tlp_probes++;
     cwnd_bypass_ = 1;
+    // Re-arm T3 from the probe (RFC 8985 §7.3): its acknowledgement, one
+    // round trip away, either repairs the tail or exposes the rest of it to
+    // RACK. Left running from the last cumulative ack, T3 expired before that
+    // ack could arrive whenever cwnd had shrunk to a few packets (2 % loss,
+    // bursts behind a token trickle): cwnd to one MTU and RTO doubled for a
+    // loss the probe was already repairing.
+    start_t3();
     break;  // flush() at the end of this iteration sends it
   }
 }

@@ -432,3 +432,38 @@ TEST(peerconnection_pair_loopback) {
   off->close();
   ans->close();
 }
+
+TEST(sctp_probe_rearms_t3_at_small_cwnd) {
+  // 50 ms RTT, 2 % loss, a token trickle with 240 KB bursts: after a few loss
+  // events cwnd is ~3 packets, so a lost burst tail is found only by a
+  // tail-loss probe. T3 must be re-armed from the probe (RFC 8985 §7.3);
+  // left running from the last cumulative ack it expired before the probe's
+  // ack could return (2 T3s in this run before, each cwnd to one MTU).
+  SctpPair p(0.02, 0, 0, 1200, false, false, 100);
+  p.link.fixed_delay_us = 25000;
+  p.a->connect();
+  p.b->connect();
+  CHECK(p.r.run_until([&] { return p.a->established() && p.b->established(); }, 5000));
+  std::string blk = payload(60000, 5);
+  size_t sent = 0, bulk = 0;
+  uint64_t next = Reactor::now_us();
+  uint64_t t3 = 0;
+  CHECK(p.r.run_until([&] {
+    if (Reactor::now_us() >= next && sent < 1000) {
+      p.a->send(uint16_t(1 + 2 * (sent % 4)), 53, {Bytes::copy(payload(150, uint32_t(sent)))});
+      sent++;
+      next += 10000;
+      if (sent % 25 == 0 && bulk < 40) { for (int k = 0; k < 4; k++) p.a->send(9, 53, {Bytes::copy(blk)}); bulk += 4; }
+    }
+    if (p.a->stats().t3_expirations != t3) {
+      t3 = p.a->stats().t3_expirations;
+      printf("  T3 #%llu at %zu msgs: %s\n", (unsigned long long)t3, sent, p.a->debug_state().c_str());
+    }
+    return sent == 1000 && p.got_b.size() == sent + bulk && p.a->bytes_in_flight() == 0;
+  }, 60000));
+  printf("  small cwnd: t3 %llu tlp %llu fast %llu dropped %llu\n", (unsigned long long)p.a->stats().t3_expirations,
+         (unsigned long long)p.a->stats().tlp_probes, (unsigned long long)p.a->stats().fast_retransmits,
+         (unsigned long long)p.link.dropped);
+  CHECK(p.link.dropped > 20);
+  CHECK(p.a->stats().t3_expirations <= 1);
+}
