@@ -101,7 +101,11 @@ size_t DataChannel::body_chunk() const {
   const size_t per_chunk = mtu > 12 + 16 ? mtu - 12 - 16 : 0;  // SCTP common + DATA chunk headers
   if (mtu >= 8192) return per_chunk - proto::kHeaderLen;       // one chunk, less the frame header
   const size_t cw = pc && pc->sctp_ ? pc->sctp_->cwnd() : 0;
-  if (!per_chunk || cw == 0 || cw >= kSmallCwnd) return proto::kMaxBodyChunk;
+  // Only on a long path: on a LAN a 64 KB frame leaves in microseconds, and a
+  // response that started in slow start kept small frames for its whole body
+  // (MI355X host, 1200-MTU mixed row: bulk 2125 -> 1543 MB/s, token p99 +2 ms).
+  const uint64_t base_rtt = pc && pc->sctp_ ? pc->sctp_->min_rtt_us() : 0;
+  if (!per_chunk || cw == 0 || cw >= kSmallCwnd || base_rtt < kLongPathUs) return proto::kMaxBodyChunk;
   const size_t chunks = std::max<size_t>(1, cw / 8 / per_chunk);
   return std::min(proto::kMaxBodyChunk, chunks * per_chunk - proto::kHeaderLen);
 }

@@ -63,7 +63,8 @@ class DataChannel : public MessageChannel, public std::enable_shared_from_this<D
   void set_lanes(int lanes) override { lanes_ = std::clamp(lanes, 0, kMaxLanes); }
   std::string channel_binding() const override;
   static constexpr int kMaxLanes = 64;
-  static constexpr size_t kSmallCwnd = 256 * 1024;  // below: body frames follow cwnd (body_chunk)
+  static constexpr size_t kSmallCwnd = 256 * 1024;  // below: body frames follow cwnd (body_chunk) ...
+  static constexpr uint64_t kLongPathUs = 5000;      // ... on paths with a base RTT of at least this
   // The channel's lane streams: stream + 2, + 4, ... (same parity as the
   // channel's own stream, as RFC 8832 allocates per DTLS role).
   bool owns_lane(uint16_t st) const {
