@@ -331,10 +331,10 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     auto sess = sess_.lock();
     if (!sess) return false;
     uint32_t sid = sid_;
-    bool reject = reject_not_ready_;
+    bool reject = reject_not_ready_ || discard_body_;
     size_t cs = sess->body_chunk();
     auto conn = conn_;
-    bool flow = sess->flow();
+    bool flow = sess->flow() && !discard_body_;
     size_t used = body_.feed(data, len, [&](const uint8_t* d, size_t n) {
       if (reject) return;
       Bytes b = conn ? conn->rx_view(d, n) : Bytes::copy(d, n);
@@ -368,8 +368,10 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
       response_done();
       return;
     }
-    sess->send(proto::make_empty(proto::MsgType::ReqEnd, sid_));
-    trace::event("proxy", sid_, "req_end");
+    if (!discard_body_) {
+      sess->send(proto::make_empty(proto::MsgType::ReqEnd, sid_));
+      trace::event("proxy", sid_, "req_end");
+    }
     if (state_ == State::ReadingBody) state_ = head_written_ ? State::Responding : State::Awaiting;
     if (!head_written_) {
       std::weak_ptr<ProxyConn> w = shared_from_this();
@@ -473,8 +475,25 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
       stream_registered_ = false;
     }
     if (state_ == State::ReadingBody) {
-      // Response finished before the request body: complete it first.
+      // Response finished before the request body (a 413, an upstream that
+      // answered a streamed upload early): read and discard the rest of the
+      // body so a client that sends everything before reading still gets to
+      // the response. The stream is unregistered, so no Credit or Resume for
+      // it will come: its pauses end here, and nothing more is forwarded.
       response_complete_ = true;
+      discard_body_ = true;
+      if (flow_paused_ || credit_paused_) {
+        flow_paused_ = false;
+        credit_paused_ = false;
+        update_reading();
+      }
+      if (conn_ && !inbuf_.empty()) {
+        std::weak_ptr<ProxyConn> w = shared_from_this();
+        if (auto sess = sess_.lock())
+          sess->reactor().post([w] {
+            if (auto s = w.lock()) s->process();
+          });
+      }
       return;
     }
     if (!keep_alive_) {
@@ -506,6 +525,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     no_body_ = false;
     first_body_ = false;
     response_complete_ = false;
+    discard_body_ = false;
     body_sent_ = 0;
   }
 
@@ -547,6 +567,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
   bool no_body_ = false;
   bool first_body_ = false;
   bool response_complete_ = false;
+  bool discard_body_ = false;    // response done mid-upload: drain the body, forward nothing
   bool pipelined_hold_ = false;
   bool reject_not_ready_ = false;
   bool flow_paused_ = false;

@@ -323,3 +323,30 @@ def test_one_gib_upload_keeps_serve_and_proxy_small():
             s.close()
     finally:
         mock.stop()
+
+
+@pytest.mark.parametrize("chunked", [False, True])
+def test_upload_answered_early_with_413_completes(chunked):
+    """A client that sends its whole 1 MB body before reading gets the 413
+    serve answered early: the proxy drains the rest of the upload once the
+    response is done, although serve's credit for the stream never comes
+    (the window is 256 KiB), and the connection stays usable."""
+    mock, mport = _native_mock()
+    try:
+        with Tunnel(f"http://127.0.0.1:{mport}", transport="tcp",
+                    serve_extra=["--max-request-body", "100000"]) as t:
+            body = b"q" * (1 << 20)
+            c = http.client.HTTPConnection("127.0.0.1", t.proxy_port, timeout=20)
+            if chunked:
+                c.request("POST", "/sink", body=iter([body[o:o + 65536] for o in range(0, len(body), 65536)]),
+                          encode_chunked=True)
+            else:
+                c.request("POST", "/sink", body=body)
+            r = c.getresponse()
+            assert r.status == 413
+            r.read()
+            c.request("GET", "/health")  # same connection: the upload was drained
+            r = c.getresponse()
+            assert r.status == 200 and r.read()
+    finally:
+        mock.stop()
