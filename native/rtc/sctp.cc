@@ -835,7 +835,9 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
   rack_sent = std::max(rack_sent, rtx_delivered);
   uint64_t reo = std::max<uint64_t>(srtt_us_ / 4, 1000);
   bool new_fast = false;
+  size_t marked_now = 0;  // chunks this SACK declared lost
   auto mark = [&](Chunk* ch) {
+    marked_now++;
     ch->miss = 0;
     ch->retransmit = true;
     ch->fast = true;
@@ -886,19 +888,38 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
     // beta, RFC 9438) rather than Reno's half.
     uint64_t rtt = std::max<uint64_t>(srtt_us_, 1);
     size_t backlog = min_rtt_us_ && rtt > min_rtt_us_ ? size_t(double(cwnd_) * double(rtt - min_rtt_us_) / double(rtt)) : 0;
-    bool random_loss = backlog < 3 * cfg_.mtu + cwnd_ / 16;
+    // Random loss also means isolated loss: a policer or a shallow drop-tail
+    // queue overrun by cwnd drops a run of packets with no standing queue in
+    // front of it, which is congestion all the same.
+    bool random_loss = backlog < 3 * cfg_.mtu + cwnd_ / 16 && marked_now <= 2;
     if (random_loss) stats_.random_loss_events++;
     // A random loss keeps cwnd (TUNNEL_SCTP_RANDOM_BETA_PCT, default 100):
     // with no standing queue it says nothing about congestion, and a cut per
     // random loss capped bulk at the loss rate's AIMD equilibrium (emulated
     // 50 ms / 2 %: 0.54 MB/s at 0.9, 1.67 MB/s kept; the SSE tails and the
     // clean rows, whose queue-overflow losses read as congestion, unchanged).
-    // Losses with a backlog still cut by 0.3.
+    // Losses with a backlog still cut by 0.3. Sustained loss still backs off
+    // multiplicatively (RFC 5033): every kRandomStreakCut-th random-loss
+    // episode in a row (episodes less than 8 SRTT apart) cuts by 0.15, so a
+    // path whose losses only look random converges instead of being overdriven.
     static const int random_beta_pct = [] {
       const char* e = getenv("TUNNEL_SCTP_RANDOM_BETA_PCT");
       return e && *e ? std::clamp(atoi(e), 50, 100) : 100;
     }();
-    ssthresh_ = std::max(random_loss ? cwnd_ * size_t(random_beta_pct) / 100 : cwnd_ * 7 / 10, 4 * cfg_.mtu);
+    if (last_loss_us_ && now - last_loss_us_ > 8 * rtt) random_streak_ = 0;
+    last_loss_us_ = now;
+    size_t keep = cwnd_ * 7 / 10;
+    if (random_loss) {
+      keep = cwnd_ * size_t(random_beta_pct) / 100;
+      if (++random_streak_ >= kRandomStreakCut) {
+        random_streak_ = 0;
+        keep = std::min(keep, cwnd_ * 85 / 100);
+        stats_.random_loss_cuts++;
+      }
+    } else {
+      random_streak_ = 0;
+    }
+    ssthresh_ = std::max(keep, 4 * cfg_.mtu);
     cwnd_ = ssthresh_;
     partial_acked_ = 0;
     fast_recovery_ = true;
@@ -1000,12 +1021,29 @@ void SctpAssociation::handle_reconfig(const uint8_t* c, size_t len) {
       put32(b, 1);  // Success - Performed
       queue_control(kReconfig, 0, b);
       for (uint16_t s : streams) {
-        partial_.erase(s);
+        reset_inbound_stream(s);
         if (on_stream_reset) on_stream_reset(s);
       }
     }
     off += (pl + 3u) & ~3u;
   }
+}
+
+// The peer reset its outgoing stream `st` (RFC 6525 §5.2.2): it restarts at
+// SSN 0, so every piece of per-stream receive state goes — a partial message
+// (ordered or not), the expected SSN, and complete messages held or marked
+// early for their turn — or the restarted stream's messages would be dropped
+// as already delivered or held forever.
+void SctpAssociation::reset_inbound_stream(uint16_t st) {
+  partial_.erase(st);
+  partial_u_.erase(st);
+  next_ssn_in_.erase(st);
+  const uint32_t lo = stream_ssn(st, 0), hi = stream_ssn(st, 0xFFFF);
+  for (auto it = held_.lower_bound(lo); it != held_.end() && it->first <= hi;) {
+    held_bytes_ -= it->second.second.size();
+    it = held_.erase(it);
+  }
+  early_ready_.erase(early_ready_.lower_bound(lo), early_ready_.upper_bound(hi));
 }
 
 void SctpAssociation::request_stream_reset(uint16_t stream) {
@@ -1019,6 +1057,7 @@ void SctpAssociation::request_stream_reset(uint16_t stream) {
   put16(b, stream);
   pad4(b);
   queue_control(kReconfig, 0, b);
+  next_ssn_.erase(stream);  // the stream restarts at SSN 0 (RFC 6525 §5.1.2)
 }
 
 // ------------------------------------------------------------------ sender

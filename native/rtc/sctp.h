@@ -56,6 +56,7 @@ struct SctpStats {
   uint64_t data_chunks_sent = 0, data_chunks_received = 0;
   uint64_t retransmits = 0, fast_retransmits = 0, t3_expirations = 0;
   uint64_t tlp_probes = 0, rack_marks = 0, random_loss_events = 0;
+  uint64_t random_loss_cuts = 0;  // sustained random loss: the periodic 0.85 cut
   uint64_t dup_copies_sent = 0;  // redundant copies of small messages (lossy paths)
   uint64_t early_deliveries = 0;  // messages handed up ahead of a TSN gap (another stream's loss)
   uint64_t sacks_sent = 0, sacks_received = 0;
@@ -158,6 +159,7 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   void deliver_message(uint16_t st, uint16_t ssn, bool unordered, uint32_t pp, Bytes msg);
   void release_ready(uint16_t st);
   void drain_in_order();
+  void reset_inbound_stream(uint16_t st);
   static uint32_t stream_ssn(uint16_t st, uint16_t ssn) { return uint32_t(st) << 16 | ssn; }
   void update_rto(uint64_t rtt_us);
   void start_t3();
@@ -215,6 +217,9 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   uint64_t tlp_timer_ = 0;  // tail-loss probe (fires before T3, no cwnd collapse)
   int tlp_count_ = 0;       // probes since the cumulative ack last advanced
   int cwnd_bypass_ = 0;     // chunks allowed out beyond cwnd (one per loss event)
+  int random_streak_ = 0;   // random-loss episodes in a row (see handle_sack)
+  uint64_t last_loss_us_ = 0;
+  static constexpr int kRandomStreakCut = 8;
   uint64_t rto_us_;
   uint64_t srtt_us_ = 0, rttvar_us_ = 0;
   uint64_t min_rtt_us_ = 0;  // smallest RTT sample: the path's base RTT

@@ -24,10 +24,29 @@ struct LossyLink {
   uint64_t dropped = 0;
   LossyLink(Reactor& rr, double l, double d, uint64_t delay) : r(rr), loss(l), dup(d), max_delay_us(delay) {}
   std::function<bool(const std::weak_ptr<SctpAssociation>&)> blackout;  // true: drop this packet
+  // Optional bottleneck on the path towards `bottleneck_to` (bits/s, drop-tail
+  // queue of queue_bytes): serialisation + queueing delay, overflow drops.
+  double rate_bps = 0;
+  uint64_t queue_bytes = 0, link_free_us = 0, queue_drops = 0, carried = 0;
+  std::weak_ptr<SctpAssociation> bottleneck_to;
   void carry(std::weak_ptr<SctpAssociation> to, const uint8_t* p, size_t n) {
     std::uniform_real_distribution<double> u(0, 1);
     if (blackout && blackout(to)) {
       dropped++;
+      return;
+    }
+    if (rate_bps > 0 && !to.owner_before(bottleneck_to) && !bottleneck_to.owner_before(to)) {
+      const uint64_t now = Reactor::now_us(), start = std::max(now, link_free_us);
+      if (double(start - now) * rate_bps / 8e6 > double(queue_bytes)) {
+        queue_drops++;
+        return;
+      }
+      link_free_us = start + uint64_t(double(n) * 8e6 / rate_bps);
+      carried++;
+      auto pkt = std::make_shared<std::vector<uint8_t>>(p, p + n);
+      r.call_at(link_free_us + fixed_delay_us, [to, pkt] {
+        if (auto s = to.lock()) s->on_packet(pkt->data(), pkt->size());
+      });
       return;
     }
     if (u(rng) < loss) {
@@ -249,6 +268,54 @@ TEST(sctp_priority_messages_keep_stream_order) {
       if (x.first == st) got.push_back(x.second);
     CHECK(want == got);
   }
+}
+
+TEST(sctp_shallow_queue_bottleneck_backs_off) {
+  // 20 ms RTT, 40 Mbit/s bottleneck with a 6 KiB drop-tail queue (a policer
+  // or shallow buffer: losses with no standing queue in front of them). The
+  // sender must still back off: overflow drops stay a small share of what it
+  // sends (about 2 %; 5 % when random-looking losses never cut cwnd), and the
+  // transfer still uses half the rate (an unpaced window bursts past 6 KiB).
+  SctpPair p(0, 0, 0, 1200, false, false, 100);
+  p.link.fixed_delay_us = 10000;
+  p.link.rate_bps = 40e6;
+  p.link.queue_bytes = 6 * 1024;
+  p.link.bottleneck_to = p.b;
+  p.a->connect();
+  p.b->connect();
+  CHECK(p.r.run_until([&] { return p.a->established() && p.b->established(); }, 5000));
+  std::string blk = payload(10000, 5);
+  const int n = 1200;  // 12 MB: 2.4 s at the bottleneck rate
+  const uint64_t t0 = Reactor::now_us();
+  for (int i = 0; i < n; i++) p.a->send(1, 53, {Bytes::copy(blk)});
+  CHECK(p.r.run_until([&] { return p.got_b.size() == size_t(n); }, 30000));
+  const double secs = double(Reactor::now_us() - t0) / 1e6;
+  const double mbps = n * 10000.0 * 8 / secs / 1e6;
+  const double drop_share = double(p.link.queue_drops) / double(p.link.queue_drops + p.link.carried);
+  printf("  shallow queue: %.1f Mbit/s of 40, %llu drops (%.2f %%), %llu T3, %llu random-loss events, %llu cuts\n",
+         mbps, (unsigned long long)p.link.queue_drops, 100 * drop_share,
+         (unsigned long long)p.a->stats().t3_expirations, (unsigned long long)p.a->stats().random_loss_events,
+         (unsigned long long)p.a->stats().random_loss_cuts);
+  CHECK_EQ(p.got_b.size(), size_t(n));
+  CHECK(drop_share < 0.035);  // 5 % with random losses never cut (before)
+  CHECK(mbps > 0.3 * 40);
+}
+
+TEST(sctp_stream_reset_restarts_inbound_sequence) {
+  // After an outgoing-stream reset the peer's stream restarts at SSN 0: the
+  // receiver must forget the stream's expected SSN (and anything held for
+  // it), or the restarted messages read as already delivered and vanish.
+  SctpPair p(0, 0, 0);
+  p.a->connect();
+  p.b->connect();
+  CHECK(p.r.run_until([&] { return p.a->established() && p.b->established(); }, 2000));
+  for (int i = 0; i < 3; i++) p.a->send(1, 53, {Bytes::copy(payload(100, uint32_t(i)))});
+  CHECK(p.r.run_until([&] { return p.got_b.size() == 3; }, 2000));
+  p.a->request_stream_reset(1);
+  for (int i = 3; i < 6; i++) p.a->send(1, 53, {Bytes::copy(payload(100, uint32_t(i)))});
+  CHECK(p.r.run_until([&] { return p.got_b.size() == 6; }, 2000));
+  CHECK_EQ(p.got_b.size(), size_t(6));
+  for (size_t i = 0; i < p.got_b.size(); i++) CHECK(p.got_b[i].second == payload(100, uint32_t(i)));
 }
 
 TEST(sctp_jumbo_bulk_throughput) {

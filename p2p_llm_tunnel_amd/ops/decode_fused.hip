@@ -889,9 +889,14 @@ hipError_t launch_gemm(GemmArgs a, hipStream_t s, int nw_override = 0) {
 
 bool dims_ok(const LlamaDims& d) {
   if (d.D != 64 && d.D != 128) return false;
-  // GEMM operands are addressed with 32-bit byte offsets below kOob (2 GiB)
-  const size_t widest = std::max({size_t(d.vocab), size_t(2) * d.ffn, size_t(d.H + 2 * d.Hkv) * d.D, size_t(d.dim)});
-  if (widest * size_t(std::max({d.dim, d.ffn, d.H * d.D})) * 2 >= kOob) return false;
+  // GEMM operands are addressed with 32-bit byte offsets below kOob (2 GiB):
+  // each weight's own N x K bf16 extent (LM head vocab x dim, QKV, gate/up,
+  // O, down), not the widest N times the largest K of different GEMMs.
+  const size_t dim = size_t(d.dim), ffn = size_t(d.ffn), hd = size_t(d.H) * d.D;
+  const size_t gemm_bytes[] = {size_t(d.vocab) * dim * 2, size_t(d.H + 2 * d.Hkv) * d.D * dim * 2,
+                               2 * ffn * dim * 2, dim * hd * 2, dim * ffn * 2};
+  for (size_t b : gemm_bytes)
+    if (b >= kOob) return false;
   if (d.H % d.Hkv || (d.H / d.Hkv != 1 && d.H / d.Hkv != 2 && d.H / d.Hkv != 4 && d.H / d.Hkv != 8)) return false;
   if (d.dim % 32 || (d.H * d.D) % 32 || d.ffn % 32) return false;
   if (d.dim % (16 * kTnResid) || d.vocab % (16 * kTnStore) || d.ffn % 16) return false;
