@@ -75,7 +75,7 @@ def main():
             for name, p in (("serve", ms), ("proxy", mp)):
                 txt = urllib.request.urlopen(f"http://127.0.0.1:{p}/metrics", timeout=5).read().decode()
                 out[f"{name}_sctp"] = {l.split()[0]: float(l.split()[1]) for l in txt.splitlines()
-                                       if l.startswith("tunnel_sctp")}
+                                       if l.startswith(("tunnel_sctp", "tunnel_dtls", "tunnel_udp"))}
     finally:
         mock.stop()
     print(json.dumps(out))

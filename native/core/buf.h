@@ -57,6 +57,8 @@ class Bytes {
     return b;
   }
   std::string_view view() const { return {reinterpret_cast<const char*>(ptr_), len_}; }
+  // What keeps the bytes alive (null for views of unowned memory).
+  const std::shared_ptr<const void>& owner() const { return owner_; }
   std::string str() const { return std::string(view()); }
   bool operator==(const Bytes& o) const {
     return len_ == o.len_ && (len_ == 0 || std::memcmp(ptr_, o.ptr_, len_) == 0);

@@ -469,6 +469,18 @@ void TcpConn::close(const std::string& why) {
   if (cb) cb(why);
 }
 
+int TcpConn::release_fd() {
+  if (fd_ < 0 || ssl_ || out_bytes_ || in_write_) return -1;
+  r_.remove(fd_);
+  int fd = fd_;
+  fd_ = -1;
+  out_.clear();
+  on_close_ = nullptr;
+  on_data_ = nullptr;
+  on_drain_ = nullptr;
+  return fd;
+}
+
 void TcpConn::tls_handshake_step() {
   ERR_clear_error();
   int rc = SSL_connect(ssl_);

@@ -98,6 +98,10 @@ class TcpConn : public std::enable_shared_from_this<TcpConn> {
   // Immediate close (RST semantics not forced). Fires on_close("") if not yet closed.
   void close(const std::string& why = "");
   bool closed() const { return fd_ < 0; }
+  // Hands the socket over (another reactor adopts it): deregistered, not
+  // closed, no callbacks fire. Only for a plain-TCP connection with nothing
+  // left to write; -1 otherwise (the connection is unchanged).
+  int release_fd();
   int fd() const { return fd_; }
   SockAddr peer() const { return peer_; }
   void set_nodelay(bool on);

@@ -1,0 +1,292 @@
+#include "rtc/datapath.h"
+
+#include <netinet/in.h>
+#include <netinet/udp.h>
+#include <pthread.h>
+#include <signal.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstdlib>
+#include <cstring>
+
+#include "core/log.h"
+#include "core/profiler.h"
+
+#ifndef UDP_SEGMENT
+#define UDP_SEGMENT 103
+#endif
+
+namespace p2pt::rtc {
+
+static const char* kT = "tunnel::datapath";
+
+// ------------------------------------------------------------------ Lane
+
+Lane::Lane(const char* name) {
+  th_ = std::thread([this, n = std::string(name)] {
+    // Signals belong to the main reactor's signalfd (as on the HTTP workers).
+    sigset_t mask;
+    sigemptyset(&mask);
+    for (int sig : {SIGINT, SIGTERM, SIGHUP, SIGQUIT, SIGUSR1, SIGUSR2, SIGPIPE}) sigaddset(&mask, sig);
+    pthread_sigmask(SIG_BLOCK, &mask, nullptr);
+    pthread_setname_np(pthread_self(), n.c_str());
+    profiler::register_thread(n[n.size() - 1] == 'x' ? 90 : 91);  // tx / rx lanes in profiles
+    run();
+  });
+}
+
+Lane::~Lane() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
+  }
+  cv_.notify_one();
+  th_.join();
+}
+
+void Lane::submit(std::function<void()> job) {
+  pending_.fetch_add(1, std::memory_order_relaxed);
+  bool wake;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    wake = q_.empty();
+    q_.push_back(std::move(job));
+  }
+  if (wake) cv_.notify_one();
+}
+
+void Lane::run() {
+  std::vector<std::function<void()>> jobs;
+  for (;;) {
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
+      if (q_.empty()) return;  // stop_ and drained
+      jobs.swap(q_);
+    }
+    for (auto& j : jobs) {
+      j();
+      j = nullptr;  // release what the job held before counting it done
+      pending_.fetch_sub(1, std::memory_order_release);
+    }
+    jobs.clear();
+  }
+}
+
+LaneFd::LaneFd(int source) : fd(::dup(source)), src(source) {}
+LaneFd::~LaneFd() {
+  if (fd >= 0) ::close(fd);
+}
+
+// ------------------------------------------------------------------ batches
+
+void TxBatch::clear() {
+  arena.clear();
+  pieces.clear();
+  recs.clear();
+  keep.clear();
+  bytes = 0;
+  last_owner = nullptr;
+}
+
+void TxBatch::add(uint64_t seq, uint8_t type, const iovec* iov, const Bytes* const* owners, int cnt) {
+  Rec r{seq, type, uint32_t(pieces.size()), 0, 0};
+  for (int i = 0; i < cnt; i++) {
+    const size_t n = iov[i].iov_len;
+    if (!n) continue;
+    const Bytes* o = owners ? owners[i] : nullptr;
+    if (o && o->owner()) {
+      // One reference per run of pieces from the same buffer (a body frame
+      // spans many packets): the count is touched once per frame, not per
+      // packet, on both threads.
+      if (o->owner().get() != last_owner) {
+        keep.push_back(o->owner());
+        last_owner = o->owner().get();
+      }
+      pieces.push_back(Piece{static_cast<const uint8_t*>(iov[i].iov_base), 0, uint32_t(n)});
+    } else {
+      pieces.push_back(Piece{nullptr, uint32_t(arena.size()), uint32_t(n)});
+      arena.insert(arena.end(), static_cast<const uint8_t*>(iov[i].iov_base),
+                   static_cast<const uint8_t*>(iov[i].iov_base) + n);
+    }
+    r.count++;
+    r.total += uint32_t(n);
+  }
+  bytes += r.total;
+  recs.push_back(r);
+}
+
+int TxBatch::gather(const Rec& r, iovec* out, int max) const {
+  int k = 0;
+  for (uint32_t i = 0; i < r.count && k < max; i++) {
+    const Piece& p = pieces[r.first + i];
+    out[k].iov_base = const_cast<uint8_t*>(p.p ? p.p : arena.data() + p.off);
+    out[k].iov_len = p.n;
+    k++;
+  }
+  return k;
+}
+
+// ------------------------------------------------------------------ records
+
+namespace {
+void wr48(uint8_t* p, uint64_t v) {
+  for (int i = 5; i >= 0; i--) {
+    p[i] = uint8_t(v);
+    v >>= 8;
+  }
+}
+}  // namespace
+
+void seal_record(const AesGcm& g, const uint8_t iv[4], uint8_t* out, uint8_t type, uint64_t seq, const iovec* iov,
+                 int cnt, size_t total) {
+  out[0] = type;
+  out[1] = 0xFE;  // DTLS 1.2
+  out[2] = 0xFD;
+  wr16(out + 3, 1);  // epoch
+  wr48(out + 5, seq);
+  wr16(out + 11, uint16_t(kExplicit + total + kTag));
+  memcpy(out + kRecHdr, out + 3, 8);  // explicit nonce = epoch || seq (as OpenSSL does)
+  uint8_t nonce[12], aad[13];
+  memcpy(nonce, iv, 4);
+  memcpy(nonce + 4, out + 3, 8);
+  memcpy(aad, out + 3, 8);
+  aad[8] = type;
+  aad[9] = 0xFE;
+  aad[10] = 0xFD;
+  wr16(aad + 11, uint16_t(total));
+  uint8_t* o = out + kRecHdr + kExplicit;
+  g.seal_gather(nonce, aad, 13, iov, cnt, o, total, o + total);
+}
+
+bool open_record(const AesGcm& g, const uint8_t iv[4], uint8_t* rec, size_t len, uint8_t** pt, size_t* ptl) {
+  if (len < kRecHdr + kExplicit + kTag) return false;
+  const size_t ctlen = len - kRecHdr - kExplicit - kTag;
+  uint8_t* ct = rec + kRecHdr + kExplicit;
+  uint8_t nonce[12], aad[13];
+  memcpy(nonce, iv, 4);
+  memcpy(nonce + 4, rec + kRecHdr, 8);
+  memcpy(aad, rec + 3, 8);
+  aad[8] = rec[0];
+  aad[9] = rec[1];
+  aad[10] = rec[2];
+  wr16(aad + 11, uint16_t(ctlen));
+  if (!g.open(nonce, aad, 13, ct, ct, ctlen, ct + ctlen)) return false;
+  *pt = ct;
+  *ptl = ctlen;
+  return true;
+}
+
+// ------------------------------------------------------------------ TX lane
+
+void TxLaneState::run(const TxBatch& b, const RecordKeys& k, int fd, const SockAddr& to, size_t coalesce) {
+  // 1. Seal every record into one contiguous buffer; datagram boundaries are
+  // kept aside (several records per datagram on same-host jumbo paths).
+  size_t need = 0;
+  for (auto& r : b.recs) need += record_size(r.total);
+  if (out_.size() < need) out_.resize(need);
+  dgs_.clear();
+  size_t off = 0;
+  iovec iov[64];
+  for (auto& r : b.recs) {
+    const size_t sz = record_size(r.total);
+    if (coalesce && !dgs_.empty() && dgs_.back().second + sz <= coalesce) dgs_.back().second += sz;
+    else dgs_.emplace_back(off, sz);
+    int cnt = b.gather(r, iov, 64);
+    seal_record(*k.w, k.wiv, out_.data() + off, r.type, r.seq, iov, cnt, r.total);
+    off += sz;
+  }
+  records.fetch_add(b.recs.size(), std::memory_order_relaxed);
+  batches.fetch_add(1, std::memory_order_relaxed);
+  datagrams.fetch_add(dgs_.size(), std::memory_order_relaxed);
+  // 2. sendmmsg: runs of equal-size datagrams leave as one UDP GSO message
+  // (contiguous in out_, so one iovec each); a shorter datagram ends a run.
+  constexpr int kBatch = 64;
+  constexpr size_t kGsoMaxSegs = 64, kGsoMaxBytes = 60000;
+  mmsghdr msgs[kBatch];
+  iovec iovs[kBatch];
+  alignas(cmsghdr) char ctrl[kBatch][CMSG_SPACE(sizeof(uint16_t))];
+  size_t i = 0;
+  while (i < dgs_.size()) {
+    int cnt = 0;
+    while (i < dgs_.size() && cnt < kBatch) {
+      const size_t seg = dgs_[i].second;
+      size_t j = i + 1, total = seg;
+      if (gso_ok_)
+        while (j < dgs_.size() && j - i < kGsoMaxSegs && dgs_[j].second <= seg && total + dgs_[j].second <= kGsoMaxBytes) {
+          total += dgs_[j].second;
+          if (dgs_[j++].second < seg) break;
+        }
+      mmsghdr& m = msgs[cnt];
+      memset(&m, 0, sizeof m);
+      iovs[cnt].iov_base = out_.data() + dgs_[i].first;
+      iovs[cnt].iov_len = total;
+      m.msg_hdr.msg_iov = &iovs[cnt];
+      m.msg_hdr.msg_iovlen = 1;
+      m.msg_hdr.msg_name = const_cast<sockaddr*>(to.sa());
+      m.msg_hdr.msg_namelen = to.len;
+      if (j - i > 1) {
+        m.msg_hdr.msg_control = ctrl[cnt];
+        m.msg_hdr.msg_controllen = sizeof ctrl[cnt];
+        cmsghdr* c = CMSG_FIRSTHDR(&m.msg_hdr);
+        c->cmsg_level = SOL_UDP;
+        c->cmsg_type = UDP_SEGMENT;
+        c->cmsg_len = CMSG_LEN(sizeof(uint16_t));
+        uint16_t gs = uint16_t(seg);
+        memcpy(CMSG_DATA(c), &gs, sizeof gs);
+        gso_msgs.fetch_add(1, std::memory_order_relaxed);
+      }
+      cnt++;
+      i = j;
+    }
+    int sent = 0;
+    while (sent < cnt) {
+      int rc = sendmmsg(fd, msgs + sent, unsigned(cnt - sent), 0);
+      if (rc < 0) {
+        if (errno == EINTR) continue;
+        if ((errno == EIO || errno == EINVAL || errno == ENOPROTOOPT) && gso_ok_ && msgs[sent].msg_hdr.msg_controllen) {
+          // No UDP GSO on this path: datagram by datagram from here on.
+          LOG_DEBUG(kT, "UDP GSO unavailable (%s); sending datagrams individually", strerror(errno));
+          gso_ok_ = false;
+          const uint8_t* p = static_cast<const uint8_t*>(msgs[sent].msg_hdr.msg_iov->iov_base);
+          const size_t len = msgs[sent].msg_hdr.msg_iov->iov_len;
+          for (size_t o = 0; o < len;) {
+            size_t seg = 0;
+            for (auto& d : dgs_)
+              if (out_.data() + d.first == p + o) seg = d.second;
+            if (!seg) break;
+            sendto(fd, p + o, seg, 0, to.sa(), to.len);
+            o += seg;
+          }
+          sent++;
+          continue;
+        }
+        // EAGAIN (socket buffer full) or unreachable: drop; SCTP retransmits.
+        send_drops.fetch_add(uint64_t(cnt - sent), std::memory_order_relaxed);
+        break;
+      }
+      sent += rc;
+    }
+  }
+}
+
+size_t datapath_inline_bytes() {
+  static const size_t v = [] {
+    const char* e = getenv("TUNNEL_DATAPATH_INLINE_BYTES");
+    return e && *e ? size_t(strtoull(e, nullptr, 10)) : size_t(32 * 1024);
+  }();
+  return v;
+}
+
+bool datapath_enabled() {
+  static const bool v = [] {
+    const char* e = getenv("TUNNEL_DATAPATH");
+    return !(e && *e == '0');
+  }();
+  return v;
+}
+
+}  // namespace p2pt::rtc

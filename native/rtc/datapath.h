@@ -1,0 +1,163 @@
+// Crypto/IO lanes for the DTLS record layer: AES-GCM sealing + UDP sends and
+// AES-GCM opening run beside the association thread instead of on it.
+//
+// The reference runs webrtc-rs on tokio's multi-threaded runtime
+// (tunnel/src/main.rs:18, Cargo.toml:11), so its record encryption and socket
+// I/O for a bulk body (serve.rs:263-286, proxy.rs:318-330) spread over cores.
+// Here one association thread owns everything that must stay ordered — the
+// SCTP state machine, DTLS epoch/sequence numbers, the replay window — and in
+// a 64 x 1 MB echo it spent three quarters of its time on the bytes instead:
+// sealing 21-25 %, sendmmsg 12-27 %, opening 12-16 % (profiles/r02/bulk_prof).
+//
+//   TX: SCTP packets (gather lists of headers + zero-copy body slices) become
+//       records with their sequence numbers assigned on the association
+//       thread; a flush's records go to the TX lane as one batch holding
+//       references to the body buffers. The lane seals them into one
+//       contiguous buffer and sends it with sendmmsg + UDP GSO on its own
+//       dup of the socket.
+//   RX: the association thread still reads the socket (recvmmsg); a burst's
+//       application records go to the RX lane, which authenticates and
+//       decrypts them in place; the replay check and hand-off to SCTP run back
+//       on the association thread, in order.
+//
+// Small batches never cross threads: a flush (or receive burst) below
+// kInlineBytes whose lane has nothing outstanding is processed inline, so an
+// SSE token keeps the single-thread latency and only bulk pays a hand-off.
+// Lanes are used only with the vector AES-GCM (its contexts are immutable
+// after key setup, so both threads may use them) and on a direct UDP path
+// (no TURN relay, NAT or WAN emulation, which live in the ICE agent's send
+// path).
+#pragma once
+
+#include <sys/uio.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "core/aesgcm.h"
+#include "core/buf.h"
+#include "core/net.h"
+
+namespace p2pt::rtc {
+
+// One thread that runs submitted jobs in submission order.
+class Lane {
+ public:
+  explicit Lane(const char* name);
+  ~Lane();  // runs what is queued, then joins
+  Lane(const Lane&) = delete;
+  Lane& operator=(const Lane&) = delete;
+  void submit(std::function<void()> job);
+  // Nothing queued or running (the last job's effects are visible).
+  bool idle() const { return pending_.load(std::memory_order_acquire) == 0; }
+
+ private:
+  void run();
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<std::function<void()>> q_;
+  bool stop_ = false;
+  std::atomic<int> pending_{0};
+  std::thread th_;
+};
+
+// A dup() of the ICE agent's socket for the TX lane: the lane sends on its
+// own descriptor, so the agent closing (or the kernel reusing) its fd number
+// never points a queued batch at another socket.
+struct LaneFd {
+  int fd = -1;
+  int src = -1;  // the agent's descriptor it duplicates
+  explicit LaneFd(int source);
+  ~LaneFd();
+};
+
+// Where the TX lane sends: the selected pair's socket and remote address, and
+// how many bytes of records may share one datagram (same-host jumbo paths).
+struct TxTarget {
+  int fd = -1;
+  SockAddr to;
+  size_t coalesce = 0;
+};
+
+// One flush's records: inline bytes (SCTP headers, small chunks) copied into
+// `arena`, large body slices referenced in place and kept alive by `keep`.
+struct TxBatch {
+  struct Piece {
+    const uint8_t* p;   // nullptr: arena[off, off + n)
+    uint32_t off;
+    uint32_t n;
+  };
+  struct Rec {
+    uint64_t seq;
+    uint8_t type;
+    uint32_t first, count;  // pieces
+    uint32_t total;         // plaintext bytes
+  };
+  std::vector<uint8_t> arena;
+  std::vector<Piece> pieces;
+  std::vector<Rec> recs;
+  std::vector<std::shared_ptr<const void>> keep;
+  size_t bytes = 0;  // plaintext bytes of all records
+  const void* last_owner = nullptr;
+  void clear();
+  // Appends one record; `owners[i]` (may be null) keeps iov[i] alive, or the
+  // piece is copied into the arena.
+  void add(uint64_t seq, uint8_t type, const iovec* iov, const Bytes* const* owners, int cnt);
+  // The gather list of record r (arena pieces resolved; arena must be final).
+  int gather(const Rec& r, iovec* out, int max) const;
+};
+
+// Application records of one receive burst, decrypted in place by the lane.
+struct RxBatch {
+  struct Rec {
+    uint8_t* rec;
+    uint32_t len;
+    uint8_t type;
+    bool ok = false;
+    uint64_t seq;
+    uint8_t* pt = nullptr;
+    uint32_t ptl = 0;
+    std::shared_ptr<const void> owner;
+  };
+  std::vector<Rec> recs;
+  size_t bytes = 0;
+};
+
+// Record crypto shared by the association thread and the lanes (the keys are
+// immutable once derived).
+struct RecordKeys {
+  std::shared_ptr<const AesGcm> w, r;
+  uint8_t wiv[4] = {}, riv[4] = {};
+};
+constexpr size_t kRecHdr = 13;    // type, version(2), epoch(2), seq(6), length(2)
+constexpr size_t kExplicit = 8;   // GCM explicit nonce
+constexpr size_t kTag = 16;
+inline size_t record_size(size_t plaintext) { return kRecHdr + kExplicit + plaintext + kTag; }
+// DTLS 1.2 epoch-1 AEAD record of `type`/`seq` from the gather list, into out.
+void seal_record(const AesGcm& g, const uint8_t iv[4], uint8_t* out, uint8_t type, uint64_t seq, const iovec* iov,
+                 int cnt, size_t total);
+// Authenticates and decrypts one record in place; false if it fails.
+bool open_record(const AesGcm& g, const uint8_t iv[4], uint8_t* rec, size_t len, uint8_t** pt, size_t* ptl);
+
+// TX lane state (lane thread only): the output buffer and GSO availability.
+class TxLaneState {
+ public:
+  // Seals the batch and sends it to target (runs on the lane).
+  void run(const TxBatch& b, const RecordKeys& k, int fd, const SockAddr& to, size_t coalesce);
+  std::atomic<uint64_t> batches{0}, records{0}, datagrams{0}, gso_msgs{0}, send_drops{0};
+
+ private:
+  std::vector<uint8_t> out_;
+  std::vector<std::pair<size_t, size_t>> dgs_;  // (offset, length) in out_
+  bool gso_ok_ = true;
+};
+
+size_t datapath_inline_bytes();  // TUNNEL_DATAPATH_INLINE_BYTES (default 32 KiB)
+bool datapath_enabled();         // TUNNEL_DATAPATH (default on; 0 = everything on the association thread)
+
+}  // namespace p2pt::rtc

@@ -304,9 +304,6 @@ bool DtlsTransport::verify_peer() {
 }
 
 namespace {
-constexpr size_t kRecHdr = 13;     // type, version(2), epoch(2), seq(6), length(2)
-constexpr size_t kExplicit = 8;    // GCM explicit nonce
-constexpr size_t kTag = 16;
 constexpr uint8_t kAppData = 23, kAlert = 21;
 
 uint64_t rd48(const uint8_t* p) {
@@ -423,14 +420,17 @@ void DtlsTransport::setup_fast_path() {
                EVP_DecryptFinal_ex(t, out + l, &l2) == 1 && memcmp(out, kProbe, ctlen) == 0;
     EVP_CIPHER_CTX_free(t);
     // The vector AES-GCM must open OpenSSL's probe too, or it stays unused.
+    keys_ = std::make_shared<RecordKeys>();
+    memcpy(keys_->wiv, wiv_, 4);
+    memcpy(keys_->riv, riv_, 4);
     if (probe_ok && AesGcm::supported() && !getenv("TUNNEL_DTLS_EVP")) {
-      auto w = std::make_unique<AesGcm>(), r = std::make_unique<AesGcm>();
+      auto w = std::make_shared<AesGcm>(), r = std::make_shared<AesGcm>();
       uint8_t ct[sizeof kProbe];
       if (w->init(wkey, klen) && r->init(rkey, klen) &&
           w->open(nonce, aad, 13, rec + kRecHdr + kExplicit, ct, ctlen, rec + kRecHdr + kExplicit + ctlen) &&
           memcmp(ct, kProbe, ctlen) == 0) {
-        wgcm_ = std::move(w);
-        rgcm_ = std::move(r);
+        keys_->w = std::move(w);
+        keys_->r = std::move(r);
       } else {
         LOG_WARN(kT, "vector AES-GCM self-check failed; using OpenSSL's EVP for records");
       }
@@ -442,14 +442,33 @@ void DtlsTransport::setup_fast_path() {
     return;
   }
   fast_rx_ = true;
-  LOG_DEBUG(kT, "DTLS own record layer armed (%s, %s)", cipher().c_str(), wgcm_ ? "VAES AES-GCM" : "EVP AES-GCM");
+  LOG_DEBUG(kT, "DTLS own record layer armed (%s, %s)", cipher().c_str(), lanes_possible() ? "VAES AES-GCM" : "EVP AES-GCM");
+}
+
+bool DtlsTransport::replay_seen(uint64_t seq) const {
+  if (!rx_any_ || seq > rx_max_) return false;
+  uint64_t d = rx_max_ - seq;
+  return d >= 64 || (rx_bitmap_ >> d) & 1;  // replayed or too old
+}
+
+void DtlsTransport::replay_mark(uint64_t seq) {
+  if (!rx_any_ || seq > rx_max_) {
+    uint64_t sh = rx_any_ ? seq - rx_max_ : 64;
+    rx_bitmap_ = sh >= 64 ? 1 : (rx_bitmap_ << sh) | 1;
+    rx_max_ = seq;
+    rx_any_ = true;
+  } else {
+    rx_bitmap_ |= uint64_t(1) << (rx_max_ - seq);
+  }
 }
 
 bool DtlsTransport::fast_decrypt(uint8_t* rec, size_t len, uint8_t type, uint64_t seq, uint8_t** pt, size_t* pt_len) {
   if (len < kRecHdr + kExplicit + kTag) return false;
-  if (rx_any_ && seq <= rx_max_) {
-    uint64_t d = rx_max_ - seq;
-    if (d >= 64 || (rx_bitmap_ >> d) & 1) return false;  // replayed or too old
+  if (replay_seen(seq)) return false;
+  if (keys_ && keys_->r) {
+    if (!open_record(*keys_->r, riv_, rec, len, pt, pt_len)) return false;
+    replay_mark(seq);
+    return true;
   }
   size_t ctlen = len - kRecHdr - kExplicit - kTag;
   uint8_t* ct = rec + kRecHdr + kExplicit;
@@ -461,24 +480,13 @@ bool DtlsTransport::fast_decrypt(uint8_t* rec, size_t len, uint8_t type, uint64_
   aad[9] = rec[1];
   aad[10] = rec[2];
   wr16(aad + 11, uint16_t(ctlen));
-  if (rgcm_) {
-    if (!rgcm_->open(nonce, aad, 13, ct, ct, ctlen, ct + ctlen)) return false;
-  } else {
-    int l = 0, l2 = 0;
-    if (EVP_DecryptInit_ex(rctx_, nullptr, nullptr, nullptr, nonce) != 1 ||
-        EVP_DecryptUpdate(rctx_, nullptr, &l, aad, 13) != 1 || EVP_DecryptUpdate(rctx_, ct, &l, ct, int(ctlen)) != 1 ||
-        EVP_CIPHER_CTX_ctrl(rctx_, EVP_CTRL_GCM_SET_TAG, 16, ct + ctlen) != 1 ||
-        EVP_DecryptFinal_ex(rctx_, ct + l, &l2) != 1)
-      return false;
-  }
-  if (!rx_any_ || seq > rx_max_) {
-    uint64_t sh = rx_any_ ? seq - rx_max_ : 64;
-    rx_bitmap_ = sh >= 64 ? 1 : (rx_bitmap_ << sh) | 1;
-    rx_max_ = seq;
-    rx_any_ = true;
-  } else {
-    rx_bitmap_ |= uint64_t(1) << (rx_max_ - seq);
-  }
+  int l = 0, l2 = 0;
+  if (EVP_DecryptInit_ex(rctx_, nullptr, nullptr, nullptr, nonce) != 1 ||
+      EVP_DecryptUpdate(rctx_, nullptr, &l, aad, 13) != 1 || EVP_DecryptUpdate(rctx_, ct, &l, ct, int(ctlen)) != 1 ||
+      EVP_CIPHER_CTX_ctrl(rctx_, EVP_CTRL_GCM_SET_TAG, 16, ct + ctlen) != 1 ||
+      EVP_DecryptFinal_ex(rctx_, ct + l, &l2) != 1)
+    return false;
+  replay_mark(seq);
   *pt = ct;
   *pt_len = ctlen;
   return true;
@@ -500,9 +508,9 @@ bool DtlsTransport::fast_encrypt_into(uint8_t* out, uint8_t type, const iovec* i
   aad[9] = 0xFE;
   aad[10] = 0xFD;
   wr16(aad + 11, uint16_t(total));
-  if (wgcm_) {  // straight from the gather list into the datagram
+  if (keys_ && keys_->w) {  // straight from the gather list into the datagram
     uint8_t* o = out + kRecHdr + kExplicit;
-    wgcm_->seal_gather(nonce, aad, 13, iov, cnt, o, total, o + total);
+    keys_->w->seal_gather(nonce, aad, 13, iov, cnt, o, total, o + total);
     return true;
   }
   int l = 0;
@@ -622,27 +630,24 @@ void DtlsTransport::on_datagram(std::shared_ptr<const void> owner, uint8_t* p, s
     if (off + len > n) break;  // truncated record: drop the rest
     off += len;
     if (fast_rx_ && epoch == 1 && (type == kAppData || type == kAlert)) {
+      if (rx_lane_ && fast_tx_) {  // opened at the end of the receive burst (commit_rx)
+        RxBatch::Rec r;
+        r.rec = rec;
+        r.len = uint32_t(len);
+        r.type = type;
+        r.seq = rd48(rec + 5);
+        r.owner = owner;
+        rx_pend_.recs.push_back(std::move(r));
+        rx_pend_.bytes += len;
+        continue;
+      }
       uint8_t* pt;
       size_t ptl;
       if (!fast_decrypt(rec, len, type, rd48(rec + 5), &pt, &ptl)) {
         LOG_TRACE(kT, "dropping DTLS record that fails authentication or replay check");
         continue;
       }
-      if (type == kAlert) {
-        if (ptl >= 2 && (pt[0] == 2 || pt[1] == 0)) {
-          fail(pt[1] == 0 ? "DTLS close_notify received" : "DTLS fatal alert received");
-          return;
-        }
-        continue;
-      }
-      if (!fast_tx_) {
-        // The peer finished its handshake: OpenSSL has nothing left to send.
-        fast_tx_ = true;
-        wseq_ = ossl_max_wseq_ + 1;
-        if (timer_) r_.cancel(timer_);
-        timer_ = 0;
-      }
-      if (on_data) on_data(Bytes::adopt(owner, pt, ptl));
+      if (!deliver_plain(owner, type, pt, ptl)) return;
       continue;
     }
     if (fast_tx_) continue;  // stale handshake retransmissions: OpenSSL is retired
@@ -650,13 +655,144 @@ void DtlsTransport::on_datagram(std::shared_ptr<const void> owner, uint8_t* p, s
   }
 }
 
-bool DtlsTransport::send(const uint8_t* p, size_t n) {
-  iovec v{const_cast<uint8_t*>(p), n};
-  return send(&v, 1);
+bool DtlsTransport::deliver_plain(const std::shared_ptr<const void>& owner, uint8_t type, uint8_t* pt, size_t ptl) {
+  if (type == kAlert) {
+    if (ptl >= 2 && (pt[0] == 2 || pt[1] == 0)) {
+      fail(pt[1] == 0 ? "DTLS close_notify received" : "DTLS fatal alert received");
+      return false;
+    }
+    return true;
+  }
+  if (!fast_tx_) {
+    // The peer finished its handshake: OpenSSL has nothing left to send.
+    fast_tx_ = true;
+    wseq_ = ossl_max_wseq_ + 1;
+    if (timer_) r_.cancel(timer_);
+    timer_ = 0;
+  }
+  if (on_data) on_data(Bytes::adopt(owner, pt, ptl));
+  return !closed_;
 }
 
-bool DtlsTransport::send(const iovec* iov, int cnt) {
+void DtlsTransport::enable_lanes(std::function<bool(TxTarget&)> target) {
+  if (tx_lane_ || !lanes_possible() || !datapath_enabled()) return;
+  tx_target_ = std::move(target);
+  tx_state_ = std::make_shared<TxLaneState>();
+  tx_pend_ = std::make_shared<TxBatch>();
+  tx_lane_ = std::make_unique<Lane>("p2pt-dtls-tx");
+  rx_lane_ = std::make_unique<Lane>("p2pt-dtls-rx");
+  LOG_DEBUG(kT, "DTLS crypto lanes on (inline below %zu bytes)", datapath_inline_bytes());
+}
+
+void DtlsTransport::seal_inline(const TxBatch& b) {
+  iovec iov[64];
+  for (auto& r : b.recs) {
+    const int cnt = b.gather(r, iov, 64);
+    const size_t rec = record_size(r.total);
+    if (reserve_) {
+      uint8_t* o = reserve_(rec);
+      seal_record(*keys_->w, wiv_, o, r.type, r.seq, iov, cnt, r.total);
+      commit_(rec);
+    } else {
+      if (scratch_.size() < rec) scratch_.resize(rec);
+      seal_record(*keys_->w, wiv_, scratch_.data(), r.type, r.seq, iov, cnt, r.total);
+      if (write_) write_(scratch_.data(), rec);
+    }
+  }
+}
+
+void DtlsTransport::commit_tx() {
+  if (!tx_pend_ || tx_pend_->recs.empty()) return;
+  if (closed_) {
+    tx_pend_->clear();
+    return;
+  }
+  TxTarget t;
+  const bool direct = tx_target_ && tx_target_(t) && t.fd >= 0;
+  if (!direct || (tx_pend_->bytes < datapath_inline_bytes() && tx_lane_->idle())) {
+    // A small flush with nothing ahead of it on the lane (or no direct path):
+    // sealed here, sent by the ICE agent's flush — no thread hop on the
+    // latency path of a token.
+    seal_inline(*tx_pend_);
+    tx_pend_->clear();
+    inline_tx_batches_++;
+    return;
+  }
+  if (!lane_fd_ || lane_fd_->src != t.fd) lane_fd_ = std::make_shared<LaneFd>(t.fd);
+  auto b = std::move(tx_pend_);
+  tx_pend_ = std::make_shared<TxBatch>();
+  tx_pend_->arena.reserve(b->arena.capacity());
+  tx_pend_->pieces.reserve(b->pieces.capacity());
+  tx_pend_->recs.reserve(b->recs.capacity());
+  lane_tx_batches_++;
+  tx_lane_->submit([b, st = tx_state_, k = keys_, fd = lane_fd_, to = t.to, co = t.coalesce] {
+    st->run(*b, *k, fd->fd, to, co);
+  });
+}
+
+void DtlsTransport::commit_rx() {
+  if (rx_pend_.recs.empty()) return;
+  if (closed_) {
+    rx_pend_ = RxBatch();
+    return;
+  }
+  auto self = shared_from_this();
+  if (rx_outstanding_ == 0 && rx_pend_.bytes < datapath_inline_bytes()) {
+    RxBatch b = std::move(rx_pend_);
+    rx_pend_ = RxBatch();
+    for (auto& r : b.recs) {
+      uint8_t* pt;
+      size_t ptl;
+      if (!fast_decrypt(r.rec, r.len, r.type, r.seq, &pt, &ptl)) continue;
+      if (!deliver_plain(r.owner, r.type, pt, ptl)) return;
+    }
+    return;
+  }
+  auto b = std::make_shared<RxBatch>(std::move(rx_pend_));
+  rx_pend_ = RxBatch();
+  rx_outstanding_++;
+  lane_rx_batches_++;
+  std::weak_ptr<DtlsTransport> w = self;
+  Reactor* r = &r_;
+  rx_lane_->submit([b, k = keys_, w, r] {
+    for (auto& x : b->recs) {
+      size_t ptl = 0;
+      x.ok = open_record(*k->r, k->riv, x.rec, x.len, &x.pt, &ptl);
+      x.ptl = uint32_t(ptl);
+    }
+    r->post_threadsafe([b, w] {
+      if (auto s = w.lock()) s->rx_done(*b);
+    });
+  });
+}
+
+// Opened records back on the association thread, in receive order: the
+// replay window (only authenticated records move it), then up the stack.
+void DtlsTransport::rx_done(RxBatch& b) {
+  rx_outstanding_--;
+  if (closed_) return;
+  auto self = shared_from_this();
+  for (auto& x : b.recs) {
+    if (!x.ok || replay_seen(x.seq)) {
+      LOG_TRACE(kT, "dropping DTLS record that fails authentication or replay check");
+      continue;
+    }
+    replay_mark(x.seq);
+    if (!deliver_plain(x.owner, x.type, x.pt, x.ptl)) return;
+  }
+}
+
+bool DtlsTransport::send(const uint8_t* p, size_t n) {
+  iovec v{const_cast<uint8_t*>(p), n};
+  return send(&v, nullptr, 1);
+}
+
+bool DtlsTransport::send(const iovec* iov, const Bytes* const* owners, int cnt) {
   if (!connected_ || closed_) return false;
+  if (fast_tx_ && tx_pend_) {  // lanes: sealed at commit_tx (end of this flush)
+    tx_pend_->add(wseq_++, kAppData, iov, owners, cnt);
+    return true;
+  }
   size_t total = 0;
   for (int i = 0; i < cnt; i++) total += iov[i].iov_len;
   if (fast_tx_) {
@@ -706,6 +842,7 @@ std::string DtlsTransport::cipher() const {
 
 void DtlsTransport::close() {
   if (closed_) return;
+  commit_tx();  // records of this flush go before the close_notify
   if (fast_tx_ && connected_) {
     static const uint8_t kCloseNotify[2] = {1, 0};
     iovec v{const_cast<uint8_t*>(kCloseNotify), 2};

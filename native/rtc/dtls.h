@@ -37,6 +37,7 @@
 #include "core/aesgcm.h"
 #include "core/buf.h"
 #include "core/reactor.h"
+#include "rtc/datapath.h"
 
 typedef struct ssl_st SSL;
 typedef struct bio_st BIO;
@@ -84,9 +85,27 @@ class DtlsTransport : public std::enable_shared_from_this<DtlsTransport> {
   void on_datagram(std::shared_ptr<const void> owner, uint8_t* p, size_t n);
   void on_datagram(const uint8_t* p, size_t n);  // copies first
   // Encrypt and send one application record (one SCTP packet) given as a
-  // gather list.
-  bool send(const iovec* iov, int cnt);
+  // gather list. owners[i] (optional, may be null) keeps iov[i] alive: with
+  // the crypto lanes on, such pieces are sealed later on the TX lane without
+  // a copy; pieces without an owner are copied.
+  bool send(const iovec* iov, const Bytes* const* owners, int cnt);
+  bool send(const iovec* iov, int cnt) { return send(iov, nullptr, cnt); }
   bool send(const uint8_t* p, size_t n);
+
+  // Crypto/IO lanes (rtc/datapath.h). Possible once the own record layer runs
+  // on the vector AES-GCM; `target` says where the TX lane may send directly
+  // (false: through the ICE agent, sealed inline).
+  bool lanes_possible() const { return keys_ && keys_->w && keys_->r; }
+  void enable_lanes(std::function<bool(TxTarget&)> target);
+  bool lanes_enabled() const { return tx_lane_ != nullptr; }
+  // End of a flush: seal this flush's records inline or hand them to the TX
+  // lane. End of a receive burst: open its records inline or on the RX lane.
+  void commit_tx();
+  void commit_rx();
+  const TxLaneState* tx_lane_state() const { return tx_state_.get(); }
+  uint64_t lane_tx_batches() const { return lane_tx_batches_; }
+  uint64_t lane_rx_batches() const { return lane_rx_batches_; }
+  uint64_t inline_tx_batches() const { return inline_tx_batches_; }
   void close();
   bool connected() const { return connected_; }
   bool fast_path() const { return fast_tx_; }  // own record layer carries sends
@@ -107,6 +126,13 @@ class DtlsTransport : public std::enable_shared_from_this<DtlsTransport> {
   void setup_fast_path();
   bool fast_decrypt(uint8_t* rec, size_t len, uint8_t type, uint64_t seq48, uint8_t** pt, size_t* pt_len);
   bool fast_encrypt_into(uint8_t* out, uint8_t type, const iovec* iov, int cnt, size_t total);
+  bool replay_seen(uint64_t seq) const;
+  void replay_mark(uint64_t seq);
+  // An authenticated application/alert record: alerts may end the transport
+  // (false), data goes up.
+  bool deliver_plain(const std::shared_ptr<const void>& owner, uint8_t type, uint8_t* pt, size_t ptl);
+  void seal_inline(const TxBatch& b);
+  void rx_done(RxBatch& b);
   void feed_openssl(const uint8_t* p, size_t n);
   void bio_wrote(const uint8_t* p, size_t n);
 
@@ -133,9 +159,19 @@ class DtlsTransport : public std::enable_shared_from_this<DtlsTransport> {
   std::string captured_;
   EVP_CIPHER_CTX* wctx_ = nullptr;
   EVP_CIPHER_CTX* rctx_ = nullptr;
-  // VAES/VPCLMULQDQ AES-GCM (core/aesgcm.h) when the CPU has it; EVP otherwise.
-  std::unique_ptr<AesGcm> wgcm_, rgcm_;
+  // VAES/VPCLMULQDQ AES-GCM (core/aesgcm.h) when the CPU has it (keys_->w,
+  // keys_->r, shared with the lanes); EVP otherwise.
+  std::shared_ptr<RecordKeys> keys_;
   uint8_t wiv_[4] = {}, riv_[4] = {};
+  // --- crypto/IO lanes
+  std::unique_ptr<Lane> tx_lane_, rx_lane_;
+  std::shared_ptr<TxLaneState> tx_state_;
+  std::shared_ptr<LaneFd> lane_fd_;
+  std::function<bool(TxTarget&)> tx_target_;
+  std::shared_ptr<TxBatch> tx_pend_;
+  RxBatch rx_pend_;
+  int rx_outstanding_ = 0;
+  uint64_t lane_tx_batches_ = 0, lane_rx_batches_ = 0, inline_tx_batches_ = 0;
   uint64_t wseq_ = 0;              // next epoch-1 sequence number we send
   uint64_t ossl_max_wseq_ = 0;     // highest epoch-1 sequence OpenSSL wrote
   uint64_t rx_max_ = 0;            // anti-replay: highest authenticated seq

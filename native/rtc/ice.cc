@@ -549,6 +549,14 @@ FaultCfg& fault() {
 }
 }  // namespace
 
+bool IceAgent::direct_target(int* fd, SockAddr* to, size_t* coalesce) const {
+  if (sel_local_ < 0 || closed_ || nat_mode_ || fault().on || locals_[sel_local_].relay) return false;
+  *fd = socks_[locals_[sel_local_].sock].fd;
+  *to = sel_remote_;
+  *coalesce = coalesce_limit_;
+  return true;
+}
+
 // Releases the WAN-emulation queue's due datagrams into the send queue (the
 // flush hook that follows the timer sends them).
 void IceAgent::arm_delay_timer() {
@@ -756,7 +764,7 @@ void IceAgent::on_readable(int si) {
       msgs[i].msg_hdr.msg_controllen = sizeof ctrl[i];
     }
     int n = recvmmsg(socks_[si].fd, msgs, kBatch, MSG_DONTWAIT, nullptr);
-    if (n <= 0) return;
+    if (n <= 0) break;
     for (int i = 0; i < n && !closed_; i++) {
       if (nat_mode_) {  // private address: unreachable from outside the emulated NAT
         nat_dropped_++;
@@ -767,8 +775,9 @@ void IceAgent::on_readable(int si) {
       a.len = msgs[i].msg_hdr.msg_namelen;
       dispatch_segments(si, a, rxpool_[i], msgs[i].msg_len, gro_segment(&msgs[i].msg_hdr));
     }
-    if (n < kBatch) return;
+    if (n < kBatch) break;
   }
+  if (on_rx_burst_end && !closed_) on_rx_burst_end();
 }
 
 void IceAgent::dispatch_rx(int si, const SockAddr& a, const RawBufPtr& owner, size_t len, size_t off) {

@@ -121,6 +121,10 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   // datagram). Only for same-host jumbo paths, where IP never fragments.
   void set_coalesce_limit(size_t n) { coalesce_limit_ = n; }
   bool has_path() const { return sel_local_ >= 0; }
+  // The selected pair as a plain UDP path another thread may send on (the
+  // DTLS TX lane): false with no pair, a TURN relay, or NAT / WAN / fault
+  // emulation, all of which live in this agent's own send path.
+  bool direct_target(int* fd, SockAddr* to, size_t* coalesce) const;
   // True when both ends of the selected pair are on this host.
   bool selected_same_host() const;
   std::string selected_desc() const;
@@ -134,6 +138,8 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   // Non-STUN datagrams (DTLS), in a pooled buffer the receiver may modify in
   // place and keep views into (via `owner`).
   std::function<void(std::shared_ptr<const void> owner, uint8_t*, size_t)> on_data;
+  // After a readable socket's datagrams were all handed to on_data.
+  std::function<void()> on_rx_burst_end;
 
  private:
   struct Sock {

@@ -173,6 +173,10 @@ std::shared_ptr<PeerConnection> PeerConnection::create(Reactor& r, PcConfig cfg,
     auto s = w.lock();
     if (s && s->dtls_) s->dtls_->on_datagram(std::move(owner), p, n);
   };
+  pc->ice_->on_rx_burst_end = [w] {
+    auto s = w.lock();
+    if (s && s->dtls_) s->dtls_->commit_rx();
+  };
   // One flush per reactor batch, in dependency order: SCTP packets ->
   // DTLS records -> ICE datagrams (sendmmsg).
   pc->flush_hook_ = r.add_flush_hook([w] {
@@ -188,7 +192,9 @@ PeerConnection::~PeerConnection() { close(); }
 
 void PeerConnection::flush() {
   if (closed_) return;
+  if (dtls_) dtls_->commit_rx();
   if (sctp_) sctp_->flush();
+  if (dtls_) dtls_->commit_tx();
   if (ice_) ice_->flush();
 }
 
@@ -372,9 +378,14 @@ void PeerConnection::start_sctp() {
   sc.zero_checksum = true;  // SCTP runs over DTLS (RFC 8261), EDMID 1
   if (jumbo) sc.initial_cwnd = cfg_.jumbo_initial_cwnd;
   std::weak_ptr<PeerConnection> w = shared_from_this();
-  sctp_ = SctpAssociation::create(r_, sc, [w](const iovec* iov, int cnt) {
+  // Record crypto and UDP sends of bulk flushes off this thread (rtc/datapath.h).
+  dtls_->enable_lanes([w](TxTarget& t) {
     auto s = w.lock();
-    if (s && s->dtls_) s->dtls_->send(iov, cnt);
+    return s && s->ice_ && s->ice_->direct_target(&t.fd, &t.to, &t.coalesce);
+  });
+  sctp_ = SctpAssociation::create(r_, sc, [w](const iovec* iov, const Bytes* const* owners, int cnt) {
+    auto s = w.lock();
+    if (s && s->dtls_) s->dtls_->send(iov, owners, cnt);
   });
   sctp_->on_established = [w] {
     auto s = w.lock();
@@ -455,6 +466,23 @@ void PeerConnection::start_sctp() {
   metrics::gauge_fn("tunnel_sctp_random_loss_events", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().random_loss_events) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_dtls_lane_tx_batches", [w] {
+    auto s = w.lock();
+    return s && s->dtls_ ? double(s->dtls_->lane_tx_batches()) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_dtls_inline_tx_batches", [w] {
+    auto s = w.lock();
+    return s && s->dtls_ ? double(s->dtls_->inline_tx_batches()) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_dtls_lane_rx_batches", [w] {
+    auto s = w.lock();
+    return s && s->dtls_ ? double(s->dtls_->lane_rx_batches()) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_dtls_lane_send_drops", [w] {
+    auto s = w.lock();
+    auto* st = s && s->dtls_ ? s->dtls_->tx_lane_state() : nullptr;
+    return st ? double(st->send_drops.load()) : 0.0;
   });
   metrics::gauge_fn("tunnel_udp_gso_sends", [w] {
     auto s = w.lock();

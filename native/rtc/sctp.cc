@@ -156,7 +156,7 @@ void SctpAssociation::emit_packet(std::vector<uint8_t>& pkt) {
   pkt[11] = uint8_t(crc >> 24);
   stats_.packets_sent++;
   iovec v{pkt.data(), pkt.size()};
-  if (out_) out_(&v, 1);
+  if (out_) out_(&v, nullptr, 1);
 }
 
 void SctpAssociation::begin_gather() {
@@ -167,12 +167,16 @@ void SctpAssociation::begin_gather() {
   put32(pkt_, peer_vtag_);
   put32(pkt_, 0);
   iov_.clear();
+  iov_own_.clear();
   run_start_ = 0;
   pkt_len_ = kCommonHdr;
 }
 
 void SctpAssociation::close_run() {
-  if (pkt_.size() > run_start_) iov_.push_back(iovec{pkt_.data() + run_start_, pkt_.size() - run_start_});
+  if (pkt_.size() > run_start_) {
+    iov_.push_back(iovec{pkt_.data() + run_start_, pkt_.size() - run_start_});
+    iov_own_.push_back(nullptr);
+  }
   run_start_ = pkt_.size();
 }
 
@@ -191,7 +195,7 @@ void SctpAssociation::emit_gather() {
   pkt_[10] = uint8_t(crc >> 16);
   pkt_[11] = uint8_t(crc >> 24);
   stats_.packets_sent++;
-  if (out_) out_(iov_.data(), int(iov_.size()));
+  if (out_) out_(iov_.data(), iov_own_.data(), int(iov_.size()));
 }
 
 static void begin_packet(std::vector<uint8_t>& pkt, uint16_t sport, uint16_t dport, uint32_t vtag) {
@@ -1238,6 +1242,7 @@ void SctpAssociation::flush() {
       } else {
         close_run();
         iov_.push_back(iovec{const_cast<uint8_t*>(b.data()), b.size()});
+        iov_own_.push_back(&b);
       }
     }
     pkt.insert(pkt.end(), padded - ch->len, 0);

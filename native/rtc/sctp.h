@@ -70,7 +70,9 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   // One outbound SCTP packet as a gather list: common/chunk headers and small
   // payloads live in an internal assembly buffer, large payload slices are
   // referenced in place (the DTLS layer encrypts straight from them).
-  using PacketOut = std::function<void(const iovec*, int)>;
+  // owners[i] is the Bytes that iov[i] is a view of (null for the assembly
+  // buffer, which is reused after the call; `owners` itself may be null).
+  using PacketOut = std::function<void(const iovec*, const Bytes* const* owners, int)>;
 
   static std::shared_ptr<SctpAssociation> create(Reactor& r, SctpConfig cfg, PacketOut out);
   // Contiguous view of a gathered packet (tests, fallbacks).
@@ -265,6 +267,7 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   // gather assembly of the packet being built by flush()
   std::vector<uint8_t> pkt_;  // inline bytes; reserved so it never reallocates mid-packet
   std::vector<iovec> iov_;
+  std::vector<const Bytes*> iov_own_;  // parallel to iov_
   size_t run_start_ = 0;      // start of the inline run not yet in iov_
   size_t pkt_len_ = 0;        // total packet bytes (inline + referenced)
 };

@@ -295,7 +295,7 @@ TEST(fuzz_sctp_packets) {
   std::shared_ptr<SctpAssociation> a, b;
   SctpConfig cfg;
   cfg.sack_delay_us = 0;
-  a = SctpAssociation::create(r, cfg, [&](const iovec* iov, int cnt) {
+  a = SctpAssociation::create(r, cfg, [&](const iovec* iov, const Bytes* const*, int cnt) {
     auto flat = SctpAssociation::flatten(iov, cnt);
     const uint8_t* p = flat.data();
     size_t n = flat.size();
@@ -303,7 +303,7 @@ TEST(fuzz_sctp_packets) {
     auto pkt = std::make_shared<Buf>(p, p + n);
     r.post([&b, pkt] { if (b) b->on_packet(pkt->data(), pkt->size()); });
   });
-  b = SctpAssociation::create(r, cfg, [&](const iovec* iov, int cnt) {
+  b = SctpAssociation::create(r, cfg, [&](const iovec* iov, const Bytes* const*, int cnt) {
     auto flat = SctpAssociation::flatten(iov, cnt);
     const uint8_t* p = flat.data();
     size_t n = flat.size();

@@ -79,13 +79,13 @@ struct SctpPair {
     cfg.rto_min_ms = rto_min_ms;
     auto zero = [](const std::vector<uint8_t>& f) { return f[8] == 0 && f[9] == 0 && f[10] == 0 && f[11] == 0; };
     cfg.zero_checksum = zc_a;
-    a = SctpAssociation::create(r, cfg, [this, zero](const iovec* v, int c) {
+    a = SctpAssociation::create(r, cfg, [this, zero](const iovec* v, const Bytes* const*, int c) {
       auto f = SctpAssociation::flatten(v, c);
       zero_sums_a += zero(f);
       link.carry(b, f.data(), f.size());
     });
     cfg.zero_checksum = zc_b;
-    b = SctpAssociation::create(r, cfg, [this, zero](const iovec* v, int c) {
+    b = SctpAssociation::create(r, cfg, [this, zero](const iovec* v, const Bytes* const*, int c) {
       auto f = SctpAssociation::flatten(v, c);
       zero_sums_b += zero(f);
       link.carry(a, f.data(), f.size());

@@ -56,9 +56,13 @@ class ProxyWorker : public std::enable_shared_from_this<ProxyWorker> {
   const ProxyConfig& config() const { return shared_->cfg; }
   Reactor& reactor() { return r_; }
   void conn_closed(ProxyConn* c);
+  // The association thread's inline connection with a bulk request hands its
+  // socket to a worker (Placement: bulk I/O off the association thread).
+  bool may_migrate() const { return index_ == 0 && shared_->workers > 0; }
+  void migrate(ProxyConn* c, int fd, Bytes unparsed);
 
  private:
-  void adopt(int fd);
+  void adopt(int fd, Bytes unparsed = Bytes());
   Reactor& r_;
   Reactor& assoc_;
   std::weak_ptr<ProxySession> sess_;
@@ -265,6 +269,24 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     if (res == http::ParseResult::Error) {
       simple_and_close(400, "text/plain", "Bad Request");
       return false;
+    }
+    if (sess->may_migrate() && sess->ready()) {
+      // A large upload on the association thread: move the connection, head
+      // and all, to a worker before any stream exists for it.
+      uint64_t blen = 0;
+      std::string e2;
+      if (http::request_body_mode(h, blen, &e2) == http::BodyDecoder::Mode::Length && blen >= Placement::kBulkBytes &&
+          !pipelined_hold_) {
+        int fd = conn_->release_fd();
+        if (fd >= 0) {
+          Bytes rest = Bytes::copy(inbuf_);
+          inbuf_.clear();
+          auto keep = shared_from_this();
+          conn_.reset();
+          sess->migrate(this, fd, std::move(rest));
+          return false;
+        }
+      }
     }
     inbuf_.erase(0, used);
     req_ = std::move(h);
@@ -595,12 +617,24 @@ ProxyWorker::~ProxyWorker() {
   out_.reset();
 }
 
-void ProxyWorker::adopt(int fd) {
+void ProxyWorker::adopt(int fd, Bytes unparsed) {
   trace::event("proxy", uint32_t(fd), "tcp_accept");
   auto tc = TcpConn::adopt(r_, fd);
   auto pc = std::make_shared<ProxyConn>(weak_from_this(), tc);
   conns_[pc.get()] = pc;
   pc->start();
+  if (!unparsed.empty()) pc->on_data(unparsed.data(), unparsed.size());
+}
+
+void ProxyWorker::migrate(ProxyConn* c, int fd, Bytes unparsed) {
+  if (!conns_.erase(c)) {
+    ::close(fd);
+    return;
+  }
+  ProxySession::Ev ev(ProxySession::Ev::Migrate);
+  ev.fd = fd;
+  ev.frame.payload = std::move(unparsed);
+  out_->push(std::move(ev));
 }
 
 void ProxyWorker::conn_closed(ProxyConn* c) {
@@ -617,7 +651,7 @@ void ProxyWorker::fail_all(const std::string& why) {
 void ProxyWorker::handle(ProxySession::Cmd& c) {
   using Cmd = ProxySession::Cmd;
   if (c.kind == Cmd::Adopt) {
-    adopt(c.fd);
+    adopt(c.fd, std::move(c.data));
     return;
   }
   auto it = streams_.find(c.sid);
@@ -706,6 +740,7 @@ ProxySession::ProxySession(Reactor& r, std::shared_ptr<MessageChannel> ch, Proxy
 void ProxySession::init_links(WorkerPool* pool) {
   size_t n = 1 + (pool ? pool->size() : 0);
   place_ = std::make_unique<Placement>(n, cfg_.inline_streams);
+  shared_->workers = n - 1;
   std::weak_ptr<ProxySession> self = shared_from_this();
   for (size_t k = 0; k < n; k++) {
     Reactor& wr = k == 0 ? r_ : pool->reactor(k - 1);
@@ -954,6 +989,15 @@ void ProxySession::on_event(size_t thread, Ev& ev) {
     case Ev::ConnClosed:
       place_->release(thread);
       return;
+    case Ev::Migrate: {
+      place_->release(thread);
+      metrics::counter_add("tunnel_conns_migrated_total");
+      Cmd c{Cmd::Adopt};
+      c.fd = ev.fd;
+      c.data = std::move(ev.frame.payload);
+      command(place_->pick(true), std::move(c));
+      return;
+    }
     case Ev::Frame:
       break;
   }

@@ -86,6 +86,7 @@ class ProxySession : public std::enable_shared_from_this<ProxySession> {
     std::atomic<bool> flow{false};  // "flow" negotiated: per-stream credit both ways
     std::atomic<uint64_t> rtt_us{0};  // transport SRTT, refreshed as body frames arrive ("flow" windows)
     size_t body_chunk = proto::kMaxBodyChunk;
+    size_t workers = 0;  // worker threads beside the association thread
   };
   // Association thread -> a connection thread.
   struct Cmd {
@@ -93,15 +94,18 @@ class ProxySession : public std::enable_shared_from_this<ProxySession> {
     explicit Cmd(Kind k, uint32_t s = 0) : kind(k), sid(s) {}
     uint32_t sid = 0;
     int fd = -1;                                  // Adopt
-    Bytes data;                                   // Body / Error message
+    Bytes data;                                   // Body / Error message; Adopt: bytes already read
     std::shared_ptr<proto::ResponseHeaders> rh;   // Headers
     uint32_t bytes = 0;                           // Credit: REQ_BODY bytes granted by serve
   };
   // A connection thread -> association thread.
   struct Ev {
-    enum Kind : uint8_t { Route, Unroute, Frame, ConnClosed } kind;
+    // Migrate: an inline connection whose request turned out bulk hands its
+    // socket (fd) and unparsed bytes (frame.payload) to a worker.
+    enum Kind : uint8_t { Route, Unroute, Frame, ConnClosed, Migrate } kind;
     explicit Ev(Kind k, uint32_t s = 0) : kind(k), sid(s) {}
     uint32_t sid = 0;
+    int fd = -1;
     proto::Frame frame{proto::MsgType::Ping, 0, Bytes()};
   };
 

@@ -710,7 +710,7 @@ void ServeSession::start_request(uint32_t sid, Pending p, bool streaming) {
   metrics::counter_add("tunnel_upstream_requests_total");
   Inflight& fl = inflight_[sid];
   fl.up = pick_upstream();
-  fl.thread = place_->pick();
+  fl.thread = place_->pick(p.body_len >= Placement::kBulkBytes || p.declared >= int64_t(Placement::kBulkBytes));
   fl.path = std::move(p.headers.path);
   fl.uploading = streaming;
   fl.uploaded = p.body_len;

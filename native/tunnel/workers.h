@@ -124,13 +124,16 @@ class Pipe {
 
 // Picks the thread for a new stream/connection: the association thread
 // (index 0) while fewer than `inline_max` are active there, otherwise the
-// least-loaded worker (ties round-robin).
+// least-loaded worker (ties round-robin). A stream known to be bulk (a large
+// request body) always goes to a worker when there is one: its socket I/O
+// would otherwise take the association thread's time from every other stream.
 class Placement {
  public:
+  static constexpr uint64_t kBulkBytes = 256 * 1024;
   Placement(size_t threads, size_t inline_max) : active_(threads, 0), inline_max_(inline_max) {}
-  size_t pick() {
+  size_t pick(bool bulk = false) {
     size_t n = active_.size(), best = 0;
-    if (n > 1 && active_[0] >= inline_max_) {
+    if (n > 1 && (bulk || active_[0] >= inline_max_)) {
       best = 1 + rr_ % (n - 1);
       for (size_t k = 0; k + 1 < n; k++) {
         size_t i = 1 + (rr_ + k) % (n - 1);

@@ -154,3 +154,48 @@ def test_upstream_death_fails_its_share_fast_then_is_avoided():
     finally:
         for m in ms:
             m.stop()
+
+
+def test_bulk_uploads_leave_the_association_thread():
+    """Requests with a large declared body are bulk: serve starts them on a
+    worker, and the proxy hands an inline client connection (head and body
+    bytes already read included) to a worker before the stream exists. The
+    echoed bodies come back intact, keep-alive included, and small requests
+    on the same connections keep working."""
+    ms, ports = _mocks(1)
+    try:
+        with Tunnel(f"http://127.0.0.1:{ports[0]}", transport="webrtc",
+                    serve_extra=["--workers", "2", "--metrics-listen", f"127.0.0.1:{(mp := free_port())}"],
+                    proxy_extra=["--workers", "2", "--metrics-listen", f"127.0.0.1:{(pp := free_port())}"]) as t:
+            import hashlib
+            import urllib.request
+            body = bytes(range(256)) * 4096  # 1 MiB
+            errs = []
+
+            def run(i):
+                try:
+                    c = http.client.HTTPConnection("127.0.0.1", t.proxy_port, timeout=60)
+                    for k in range(3):
+                        c.request("POST", "/echo", body=body[i + k:] + body[:i + k])
+                        r = c.getresponse()
+                        got = r.read()
+                        assert r.status == 200 and hashlib.sha256(got).digest() == hashlib.sha256(
+                            body[i + k:] + body[:i + k]).digest(), (r.status, len(got))
+                        c.request("GET", "/health")
+                        h = c.getresponse()
+                        assert h.status == 200 and h.read()
+                except Exception as e:  # noqa: BLE001
+                    errs.append(repr(e))
+
+            ths = [threading.Thread(target=run, args=(i,)) for i in range(8)]
+            for th in ths:
+                th.start()
+            for th in ths:
+                th.join(120)
+            assert not errs, errs[:3]
+            m = urllib.request.urlopen(f"http://127.0.0.1:{pp}/metrics", timeout=5).read().decode()
+            migrated = [float(l.split()[1]) for l in m.splitlines() if l.startswith("tunnel_conns_migrated_total")]
+            assert migrated and migrated[0] >= 8, migrated
+    finally:
+        for m in ms:
+            m.stop()
