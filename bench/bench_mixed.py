@@ -12,9 +12,14 @@ so a token waits behind whatever body bytes were queued before it. Reported
 per transport (jumbo same-host packets and the standard 1200-byte path):
 inter-token latency (ITL) p50/p99/max of the SSE streams, tunneled vs direct
 (the same load straight to the upstream), the added ITL p99, bulk MB/s, and
-the proxy's peak RSS (the slow client must not make it grow).
+the proxy's peak RSS (the slow client must not make it grow), and the SSE
+time to first token (TTFT) p99 next to the bulk, tunneled vs direct.
 
-    python bench/bench_mixed.py [--transports jumbo,std] [--out FILE]
+Each run lasts --seconds (10 by default) with the downloads repeating for its
+whole length; --reps alternating direct / tunneled repetitions (5) are
+summarised as median and min-max per transport ("rows"), raw runs in "runs".
+
+    python bench/bench_mixed.py [--transports jumbo,std] [--seconds 10] [--reps 5] [--out FILE]
 """
 from __future__ import annotations
 
@@ -22,6 +27,7 @@ import argparse
 import json
 import os
 import socket
+import statistics
 import subprocess
 import sys
 import threading
@@ -78,7 +84,9 @@ def slow_reader(port, rate, stop, stats):
 
 
 def scenario(port, a, watch_pid=None):
-    """Bulk + slow reader + SSE against `port`; returns the SSE loadgen result etc."""
+    """Bulk + slow reader + SSE against `port` for a.seconds; returns the SSE
+    loadgen result etc. The bulk downloads start first and run until after
+    the SSE load ends, so every token competes with them."""
     stop = threading.Event()
     stats = {}
     peak = [0]
@@ -93,10 +101,11 @@ def scenario(port, a, watch_pid=None):
     w.start()
     sr = threading.Thread(target=slow_reader, args=(port, a.slow_rate, stop, stats))
     sr.start()
-    bulk = lg(port, "--streams", a.bulk_streams, "--steps", a.bulk_steps, "--warmup", 0, "--method", "GET",
-              "--path", f"/bulk?bytes={a.bulk_mb << 20}", "--events", "none")
+    bulk = lg(port, "--streams", a.bulk_streams, "--steps", 1 << 20, "--warmup", 0, "--method", "GET",
+              "--path", f"/bulk?bytes={a.bulk_mb << 20}", "--events", "none", "--duration-s", a.seconds + 0.5)
     time.sleep(0.3)
-    sse = lg(port, "--streams", a.sse_streams, "--steps", a.sse_steps, "--warmup", 0, "--warm-conns", 1)
+    sse = lg(port, "--streams", a.sse_streams, "--steps", 1 << 20, "--warmup", 1, "--warm-conns", 1,
+             "--duration-s", a.seconds)
     sse_r = result(sse)
     bulk_r = result(bulk)
     stop.set()
@@ -105,17 +114,25 @@ def scenario(port, a, watch_pid=None):
     return sse_r, bulk_r, stats, peak[0]
 
 
+def summary(vals):
+    v = sorted(x for x in vals if x is not None)
+    if not v:
+        return None
+    return {"median": round(statistics.median(v), 3), "min": round(v[0], 3), "max": round(v[-1], 3)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--transports", default="jumbo,std")
     ap.add_argument("--interval-ms", type=int, default=10)
     ap.add_argument("--tokens", type=int, default=100)
     ap.add_argument("--sse-streams", type=int, default=8)
-    ap.add_argument("--sse-steps", type=int, default=3)
+    ap.add_argument("--seconds", type=float, default=10.0, help="length of each run (SSE load; bulk overlaps it)")
+    ap.add_argument("--reps", type=int, default=5, help="alternating direct / tunneled repetitions")
     ap.add_argument("--bulk-streams", type=int, default=8)
-    ap.add_argument("--bulk-steps", type=int, default=2)
     ap.add_argument("--bulk-mb", type=int, default=64)
     ap.add_argument("--slow-rate", type=int, default=100 * 1024)
+    ap.add_argument("--extra", default="", help="extra flags for both tunnel processes")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     ensure_native()
@@ -123,33 +140,57 @@ def main():
     mock = spawn("mock", [binary("tunnel-mock"), "--port", str(mport), "--interval-ms", str(a.interval_ms),
                           "--tokens", str(a.tokens), "--threads", "4"])
     mock.wait_for("Mock LLM server running", 10)
+    trs = [x for x in a.transports.split(",") if x]
     res = {"host": os.uname().nodename, "time": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
            "sse": f"{a.sse_streams} streams x {a.tokens} tokens @ {a.interval_ms} ms",
-           "bulk": f"{a.bulk_streams} x {a.bulk_mb} MB GET, {a.bulk_steps} rounds", "slow_client_Bps": a.slow_rate,
-           "rows": []}
+           "bulk": f"{a.bulk_streams} x {a.bulk_mb} MB GET, repeated for the whole run",
+           "slow_client_Bps": a.slow_rate, "seconds_per_run": a.seconds, "reps": a.reps, "extra": a.extra,
+           "runs": [], "rows": []}
+    tunnels = {}
     try:
-        d_sse, d_bulk, _, _ = scenario(mport, a)
-        print(json.dumps({"direct_itl_p99_ms": d_sse["p99_itl_ms"], "direct_bulk_MBps": d_bulk["MBps"]}),
-              file=sys.stderr, flush=True)
-        for tr in [x for x in a.transports.split(",") if x]:
-            extra = ["--no-jumbo-loopback"] if tr == "std" else []
-            with Tunnel(f"http://127.0.0.1:{mport}", transport="webrtc", serve_extra=extra, proxy_extra=extra) as t:
+        for tr in trs:
+            extra = [x for x in a.extra.split() if x] + (["--no-jumbo-loopback"] if tr == "std" else [])
+            t = Tunnel(f"http://127.0.0.1:{mport}", transport="webrtc", serve_extra=extra, proxy_extra=extra)
+            t.__enter__()
+            tunnels[tr] = t
+        for rep in range(a.reps):
+            d_sse, d_bulk, _, _ = scenario(mport, a)
+            print(json.dumps({"rep": rep, "direct_itl_p99_ms": d_sse["p99_itl_ms"],
+                              "direct_ttft_p99_ms": d_sse["p99_ttft_ms"], "direct_bulk_MBps": d_bulk["MBps"]}),
+                  file=sys.stderr, flush=True)
+            for tr in trs:
+                t = tunnels[tr]
                 path = t.serve.wait_for("connection established", 5).split(" via ", 1)[-1]
                 base = rss_kb(t.proxy.popen.pid)
                 sse_r, bulk_r, stats, peak = scenario(t.proxy_port, a, t.proxy.popen.pid)
-                row = {"transport": tr, "path": path,
+                run = {"rep": rep, "transport": tr, "path": path,
                        "tunneled_itl_p50_ms": sse_r["p50_itl_ms"], "tunneled_itl_p99_ms": sse_r["p99_itl_ms"],
                        "tunneled_itl_max_ms": sse_r["max_itl_ms"], "direct_itl_p50_ms": d_sse["p50_itl_ms"],
                        "direct_itl_p99_ms": d_sse["p99_itl_ms"], "direct_itl_max_ms": d_sse["max_itl_ms"],
                        "added_itl_p99_ms": sse_r["p99_itl_ms"] - d_sse["p99_itl_ms"],
+                       "tunneled_ttft_p50_ms": sse_r["p50_ttft_ms"], "direct_ttft_p50_ms": d_sse["p50_ttft_ms"],
                        "tunneled_ttft_p99_ms": sse_r["p99_ttft_ms"], "direct_ttft_p99_ms": d_sse["p99_ttft_ms"],
-                       "sse_events": sse_r["events"], "sse_errors": sse_r["errors"],
-                       "bulk_MBps": bulk_r["MBps"], "direct_bulk_MBps": d_bulk["MBps"], "bulk_errors": bulk_r["errors"],
-                       "slow_client_bytes": stats.get("slow_bytes"),
+                       "added_ttft_p99_ms": sse_r["p99_ttft_ms"] - d_sse["p99_ttft_ms"],
+                       "sse_requests": sse_r["requests"], "sse_events": sse_r["events"], "sse_errors": sse_r["errors"],
+                       "bulk_MBps": bulk_r["MBps"], "direct_bulk_MBps": d_bulk["MBps"],
+                       "bulk_ratio": bulk_r["MBps"] / d_bulk["MBps"] if d_bulk["MBps"] else None,
+                       "bulk_errors": bulk_r["errors"], "slow_client_bytes": stats.get("slow_bytes"),
                        "proxy_rss_base_mib": round(base / 1024, 1), "proxy_rss_peak_mib": round(peak / 1024, 1)}
-                res["rows"].append(row)
-                print(json.dumps(row), file=sys.stderr, flush=True)
+                res["runs"].append(run)
+                print(json.dumps(run), file=sys.stderr, flush=True)
+        keys = ["added_itl_p99_ms", "tunneled_itl_p99_ms", "direct_itl_p99_ms", "added_ttft_p99_ms",
+                "tunneled_ttft_p99_ms", "direct_ttft_p99_ms", "tunneled_ttft_p50_ms", "bulk_MBps", "direct_bulk_MBps",
+                "bulk_ratio", "proxy_rss_peak_mib"]
+        for tr in trs:
+            runs = [r for r in res["runs"] if r["transport"] == tr]
+            row = {"transport": tr, "path": runs[0]["path"] if runs else "", "reps": len(runs),
+                   "sse_errors": sum(r["sse_errors"] for r in runs), "bulk_errors": sum(r["bulk_errors"] for r in runs)}
+            for k in keys:
+                row[k] = summary([r[k] for r in runs])
+            res["rows"].append(row)
     finally:
+        for t in tunnels.values():
+            t.__exit__(None, None, None)
         mock.stop()
     doc = json.dumps(res, indent=1)
     if a.out:

@@ -53,6 +53,7 @@ struct Opts {
   size_t post_bytes = 0;  // >0: POST /echo with this many bytes instead
   char event_sep = 0;     // 0: auto from content-type (SSE "\n\n", NDJSON "\n"); 'n' none
   uint64_t read_rate = 0; // >0: read at most this many body bytes/s per stream (slow client)
+  uint64_t duration_us = 0;  // >0: repeat timed steps for this long (--duration-s)
 };
 
 struct Result {
@@ -273,7 +274,11 @@ void run_thread(const Opts& o, int first, int count, Result& res, Result& warm_r
         if (--pending == 0) {
           if (step >= o.warmup) res.step_end.push_back(Reactor::now_us());
           step++;
-          if (step >= total_steps) {
+          // --duration-s: timed steps repeat until the duration has passed
+          // (the step in progress finishes), whatever --steps says.
+          const bool done = o.duration_us ? step > o.warmup && Reactor::now_us() - res.t_start >= o.duration_us
+                                          : step >= total_steps;
+          if (done) {
             res.t_end = Reactor::now_us();
             r.stop();
             return;
@@ -328,6 +333,7 @@ int main(int argc, char** argv) {
     else if (a == "--warm-conns") o.warm_conns = v == "1";
     else if (a == "--events") o.event_sep = v == "sse" ? 's' : v == "ndjson" ? 'l' : v == "none" ? 'n' : 0;
     else if (a == "--read-rate") o.read_rate = strtoull(v.c_str(), nullptr, 10);
+    else if (a == "--duration-s") o.duration_us = uint64_t(atof(v.c_str()) * 1e6);
   }
   signal(SIGPIPE, SIG_IGN);
   int T = std::min(o.threads, std::max(1, o.streams));
