@@ -14,6 +14,10 @@ time and Bernoulli loss (TUNNEL_FAULT_RTT_MS / _RATE_MBPS / _LOSS). For each
   * bulk alone: 8 concurrent 1 MB echoes (req/s, MB/s each way).
 
     python bench/bench_wan.py [--rtts 20,50] [--losses 0,0.005,0.02]
+
+--steady-mb N adds steady-state rows (run alone with --rtts ''): 4 downloads of
+N MB each at every (rate, RTT, loss, queue) of --steady-*, reporting goodput
+as a share of the bottleneck and the sending process's per-thread CPU.
 """
 from __future__ import annotations
 
@@ -45,7 +49,8 @@ def result(p, timeout=900):
 
 SCTP_GAUGES = ("tunnel_sctp_fast_retransmits", "tunnel_sctp_t3_expirations", "tunnel_sctp_tlp_probes",
                "tunnel_sctp_rack_marks", "tunnel_sctp_random_loss_events", "tunnel_sctp_cwnd_bytes",
-               "tunnel_sctp_rto_us", "tunnel_sctp_packets_sent", "tunnel_sctp_dup_copies")
+               "tunnel_sctp_rto_us", "tunnel_sctp_packets_sent", "tunnel_sctp_dup_copies",
+               "tunnel_sctp_hystart_exits", "tunnel_sctp_random_loss_cuts")
 
 
 def scrape(port):
@@ -62,6 +67,53 @@ def scrape(port):
     return out
 
 
+def thread_cpu(pid):
+    """CPU seconds per thread of a process, keyed "name/tid"."""
+    out = {}
+    tck = os.sysconf("SC_CLK_TCK")
+    try:
+        for tid in os.listdir(f"/proc/{pid}/task"):
+            try:
+                st = open(f"/proc/{pid}/task/{tid}/stat").read()
+            except OSError:
+                continue
+            name = st[st.index("(") + 1:st.rindex(")")]
+            f = st.rsplit(")", 1)[1].split()
+            out[f"{name}/{tid}"] = (int(f[11]) + int(f[12])) / tck
+    except OSError:
+        pass
+    return out
+
+
+def steady_row(mport, rtt, loss, rate, qkb, mb, streams, extra):
+    """Steady-state goodput: `streams` downloads of `mb` MB each over the
+    emulated path, alone; MB/s against the bottleneck rate, and the CPU share
+    of every thread of the sending side (serve) over the transfer."""
+    env = {"TUNNEL_FAULT_RTT_MS": str(rtt), "TUNNEL_FAULT_RATE_MBPS": str(rate), "TUNNEL_FAULT_QUEUE_KB": str(qkb),
+           "TUNNEL_FAULT_LOSS": str(loss), "RUST_LOG": "warn,tunnel::rtc=info,tunnel::serve=info,tunnel::proxy=info"}
+    sm, pm = free_port(), free_port()
+    with Tunnel(f"http://127.0.0.1:{mport}", transport="webrtc",
+                serve_extra=extra + ["--metrics-listen", f"127.0.0.1:{sm}"],
+                proxy_extra=extra + ["--metrics-listen", f"127.0.0.1:{pm}"], env=env) as t:
+        result(sse(t.proxy_port, 1))  # warm: connections
+        pid, ppid = t.serve.popen.pid, t.proxy.popen.pid
+        c0, p0, t0 = thread_cpu(pid), thread_cpu(ppid), time.time()
+        r = result(lg(t.proxy_port, "--streams", streams, "--steps", 1, "--warmup", 0, "--method", "GET",
+                      "--path", f"/bulk?bytes={mb << 20}", "--events", "none"))
+        wall = time.time() - t0
+        c1, p1 = thread_cpu(pid), thread_cpu(ppid)
+        cpu = {k: round(100 * (c1[k] - c0.get(k, 0.0)) / wall, 1) for k in c1 if c1[k] - c0.get(k, 0.0) > 0}
+        pcpu = {k: round(100 * (p1[k] - p0.get(k, 0.0)) / wall, 1) for k in p1 if p1[k] - p0.get(k, 0.0) > 0}
+        mbps = r["MBps"]
+        row = {"rtt_ms": rtt, "loss": loss, "rate_mbps": rate, "queue_kb": round(qkb), "downloads": streams,
+               "mb_each": mb, "MBps": mbps, "pct_of_bottleneck": round(100 * mbps * 1e6 * 8 / (rate * 1e6), 1),
+               "seconds": round(wall, 2), "errors": r["errors"],
+               "serve_thread_cpu_pct": dict(sorted(cpu.items(), key=lambda kv: -kv[1])),
+               "proxy_thread_cpu_pct": dict(sorted(pcpu.items(), key=lambda kv: -kv[1])),
+               "serve_sctp": scrape(sm), "proxy_sctp": scrape(pm)}
+        return row
+
+
 def sse(port, steps):
     return lg(port, "--streams", 8, "--steps", steps, "--warmup", 0, "--warm-conns", 1)
 
@@ -76,6 +128,13 @@ def main():
     ap.add_argument("--bulk-mb", type=int, default=4, help="size of each of the 4 background downloads")
     ap.add_argument("--echo-steps", type=int, default=1)
     ap.add_argument("--extra", default="", help="extra flags for both tunnel processes")
+    ap.add_argument("--steady-mb", type=int, default=0,
+                    help="steady-state goodput rows: downloads of this many MB each (0: off)")
+    ap.add_argument("--steady-streams", type=int, default=4)
+    ap.add_argument("--steady-rates", default="200,1000", help="bottleneck Mbit/s of the steady rows")
+    ap.add_argument("--steady-rtts", default="20,50")
+    ap.add_argument("--steady-losses", default="0,0.005")
+    ap.add_argument("--steady-queues", default="0", help="queue KB per steady row (0: one BDP), e.g. 0,16")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     ensure_native()
@@ -84,9 +143,18 @@ def main():
                           "--threads", "2"])
     mock.wait_for("Mock LLM server running", 10)
     res = {"host": os.uname().nodename, "time": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
-           "mtu": 1200, "rate_mbps": a.rate_mbps, "extra": a.extra, "rows": []}
+           "mtu": 1200, "rate_mbps": a.rate_mbps, "extra": a.extra, "rows": [], "steady": []}
     extra = ["--no-jumbo-loopback"] + [x for x in a.extra.split() if x]
     try:
+        if a.steady_mb:
+            for rate in [float(x) for x in a.steady_rates.split(",") if x]:
+                for rtt in [float(x) for x in a.steady_rtts.split(",") if x]:
+                    for loss in [float(x) for x in a.steady_losses.split(",") if x]:
+                        for q in [float(x) for x in a.steady_queues.split(",") if x != ""]:
+                            qkb = q or max(64.0, rate * 1e6 / 8 * rtt / 1e3 / 1024)
+                            row = steady_row(mport, rtt, loss, rate, qkb, a.steady_mb, a.steady_streams, extra)
+                            res["steady"].append(row)
+                            print(json.dumps(row), file=sys.stderr, flush=True)
         for rtt in [float(x) for x in a.rtts.split(",") if x]:
             for loss in [float(x) for x in a.losses.split(",") if x]:
                 qkb = a.queue_kb or max(64.0, a.rate_mbps * 1e6 / 8 * rtt / 1e3 / 1024)

@@ -463,6 +463,14 @@ void PeerConnection::start_sctp() {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().rack_marks) : 0.0;
   });
+  metrics::gauge_fn("tunnel_sctp_hystart_exits", [w] {
+    auto s = w.lock();
+    return s && s->sctp_ ? double(s->sctp_->stats().hystart_exits) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_sctp_random_loss_cuts", [w] {
+    auto s = w.lock();
+    return s && s->sctp_ ? double(s->sctp_->stats().random_loss_cuts) : 0.0;
+  });
   metrics::gauge_fn("tunnel_sctp_random_loss_events", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().random_loss_events) : 0.0;

@@ -784,6 +784,7 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
     Chunk* ch = inflight_.front();
     inflight_.pop_front();
     if (ch->in_flight) flight_size_ -= ch->len;
+    if (ch->retransmit) rtx_.erase(ch->tsn);
     if (!ch->acked) {
       newly_acked += ch->len;
       if (ch->tx == 1) {
@@ -797,26 +798,71 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
     free_chunk(ch);
   }
   cum_acked_ = cum;
-  uint32_t highest_gap = cum;
+  // Gap blocks, processed in O(news): the peer repeats its blocks in every
+  // SACK, so only the parts not already known to be acknowledged (gap_known_,
+  // the previous SACK's blocks) are walked, by direct index into inflight_
+  // (consecutive TSNs from the cumulative ack up). A 1 Gbit/s x 50 ms path
+  // has ~5,000 chunks in flight; rescanning them per block was O(window x
+  // blocks) per SACK.
+  const uint32_t head = inflight_.empty() ? cum + 1 : inflight_.front()->tsn;
+  auto at = [&](uint32_t tsn) -> Chunk* {
+    uint32_t k = tsn - head;
+    return k < inflight_.size() ? inflight_[k] : nullptr;
+  };
+  const uint32_t top = next_tsn_ - 1;  // highest TSN ever sent
+  blocks_.clear();
   for (uint16_t i = 0; i < ngap; i++) {
-    uint32_t s = cum + rd16(c + 12 + 4 * i), e = cum + rd16(c + 14 + 4 * i);
-    for (Chunk* ch : inflight_) {
-      if (tsn_lt(ch->tsn, s)) continue;
-      if (tsn_lt(e, ch->tsn)) break;
-      if (!ch->acked) {
+    uint32_t s0 = cum + rd16(c + 12 + 4 * i), e0 = cum + rd16(c + 14 + 4 * i);
+    if (rd16(c + 12 + 4 * i) == 0 || tsn_lt(e0, s0) || tsn_lt(top, s0)) continue;  // malformed / beyond what was sent
+    if (tsn_lt(top, e0)) e0 = top;
+    blocks_.emplace_back(s0, e0);
+  }
+  std::sort(blocks_.begin(), blocks_.end(), [cum](const auto& a, const auto& b) { return a.first - cum < b.first - cum; });
+  uint32_t highest_gap = cum;
+  size_t k = 0;  // cursor into gap_known_ (sorted, absolute TSNs)
+  auto ack_range = [&](uint32_t a, uint32_t b) {
+    for (uint32_t t = a;; t++) {
+      if (Chunk* ch = at(t); ch && !ch->acked) {
         ch->acked = true;
-        ch->retransmit = false;
+        if (ch->retransmit) {
+          ch->retransmit = false;
+          rtx_.erase(ch->tsn);
+        }
         if (ch->in_flight) {
           flight_size_ -= ch->len;
           ch->in_flight = false;
         }
         newly_acked += ch->len;
-        if (ch->tx == 1 && !gap_sample) gap_sample = std::max<uint64_t>(now - ch->sent_us, 1);
-        else if (ch->tx > 1) rtx_evidence(ch);
+        if (ch->tx == 1) {
+          if (!gap_sample) gap_sample = std::max<uint64_t>(now - ch->sent_us, 1);
+          rack_xmit_us_ = std::max(rack_xmit_us_, ch->sent_us);
+        } else {
+          rtx_evidence(ch);
+        }
       }
-      if (tsn_lt(highest_gap, ch->tsn)) highest_gap = ch->tsn;
+      if (t == b) break;
+    }
+  };
+  for (auto& blk : blocks_) {
+    if (tsn_lt(highest_gap, blk.second)) highest_gap = blk.second;
+    uint32_t pos = blk.first;
+    while (k < gap_known_.size() && tsn_lt(gap_known_[k].second, pos)) k++;
+    while (tsn_le(pos, blk.second)) {
+      if (k < gap_known_.size() && tsn_le(gap_known_[k].first, pos)) {  // known part: skip it
+        if (tsn_le(blk.second, gap_known_[k].second)) break;
+        pos = gap_known_[k].second + 1;
+        k++;
+        continue;
+      }
+      uint32_t end = blk.second;
+      if (k < gap_known_.size() && tsn_le(gap_known_[k].first, blk.second)) end = gap_known_[k].first - 1;
+      ack_range(pos, end);
+      if (end == blk.second) break;
+      pos = end + 1;
     }
   }
+  gap_known_.swap(blocks_);
+  if (cum_advanced && newest_cum_sent) rack_xmit_us_ = std::max(rack_xmit_us_, newest_cum_sent);
   const uint64_t rtt_sample = cum_sample && !cum_probe ? cum_sample : (cum_sample ? 0 : gap_sample);
   if (rtt_sample) {
     update_rto(rtt_sample);
@@ -832,11 +878,9 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
   // Only chunks transmitted once count as evidence: the acknowledgement of a
   // retransmitted chunk may be for its original copy (RFC 8985's ambiguity),
   // which would declare everything sent before the retransmission lost.
-  uint64_t rack_sent = 0;  // latest send time among acknowledged once-sent chunks
-  for (Chunk* ch : inflight_)
-    if (ch->acked && ch->tx == 1 && ch->sent_us > rack_sent) rack_sent = ch->sent_us;
-  if (cum_advanced) rack_sent = std::max(rack_sent, newest_cum_sent);
-  rack_sent = std::max(rack_sent, rtx_delivered);
+  // rack_xmit_us_ is the latest send time of an acknowledged once-sent chunk
+  // (RACK.xmit_ts, monotonic), kept as acks arrive instead of rescanned.
+  const uint64_t rack_sent = std::max(rack_xmit_us_, rtx_delivered);
   uint64_t reo = std::max<uint64_t>(srtt_us_ / 4, 1000);
   bool new_fast = false;
   size_t marked_now = 0;  // chunks this SACK declared lost
@@ -844,6 +888,7 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
     marked_now++;
     ch->miss = 0;
     ch->retransmit = true;
+    rtx_.insert(ch->tsn);
     ch->fast = true;
     ch->probe = false;
     if (ch->in_flight) {
@@ -853,28 +898,53 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
     new_fast = true;
     stats_.fast_retransmits++;
   };
-  for (Chunk* ch : inflight_) {
-    if (ch->acked || ch->retransmit) continue;
-    // Fast retransmit at most once per chunk (RFC 9260 §7.2.4); a lost
-    // retransmission is found by the time-based rule, a probe or T3.
-    bool below_gap = highest_gap != cum && tsn_lt(ch->tsn, highest_gap) && ch->tx == 1;
-    if (below_gap && ++ch->miss == 3) {
-      mark(ch);
-      continue;
+  // (1) Only the holes below the highest gap-acked TSN can collect miss
+  // indications: walk them (lost chunks), not the window.
+  if (highest_gap != cum) {
+    uint32_t pos = cum + 1;
+    for (size_t b = 0; b <= gap_known_.size(); b++) {
+      const uint32_t end = b < gap_known_.size() ? gap_known_[b].first - 1 : highest_gap - 1;
+      for (uint32_t t = pos; tsn_le(t, end); t++) {
+        Chunk* ch = at(t);
+        if (!ch || ch->acked || ch->retransmit || ch->tx != 1) continue;
+        // Fast retransmit at most once per chunk (RFC 9260 §7.2.4); a lost
+        // retransmission is found by the time-based rule, a probe or T3.
+        if (++ch->miss == 3) mark(ch);
+      }
+      if (b < gap_known_.size()) pos = gap_known_[b].second + 1;
     }
-    if (rack_sent && ch->sent_us + reo < rack_sent) {
+  }
+  // (2) Transmissions in send order: everything sent more than `reo` before
+  // rack_sent and still outstanding is lost; entries for chunks since
+  // acknowledged or sent again are dropped on the way.
+  while (!sendlog_.empty()) {
+    const SendRec& f = sendlog_.front();
+    Chunk* ch = tsn_lt(f.tsn, head) ? nullptr : at(f.tsn);
+    const bool live = ch && ch->tx == f.tx && !ch->acked && !ch->retransmit;
+    if (live) {
+      if (!rack_sent || f.sent_us + reo >= rack_sent) break;
       stats_.rack_marks++;
       mark(ch);
     }
+    sendlog_.pop_front();
   }
   if (cum_advanced) assoc_errors_ = 0;
   // Congestion control (RFC 9260 §7.2.1-7.2.2).
+  const bool long_path = min_rtt_us_ >= kLongPathUs;
+  if (cwnd_ <= ssthresh_ && !hs_done_ && long_path && !fast_recovery_) hystart(cum, rtt_sample);
   if (newly_acked && cum_advanced && !fast_recovery_) {
     if (cwnd_ <= ssthresh_) {
-      // Byte counting with RFC 3465's limit L = 2 MTUs per SACK: the peer
-      // SACKs once per received batch, so one MTU per SACK would make slow
-      // start nearly linear; unbounded counting overshoots a bottleneck queue.
-      if (flight_before + cfg_.mtu >= cwnd_) cwnd_ += std::min(newly_acked, 2 * cfg_.mtu);
+      // Byte counting with RFC 3465's limit L = 2 MTUs per SACK on short
+      // paths: the peer SACKs once per received batch, so one MTU per SACK
+      // would make slow start nearly linear, while unbounded counting
+      // overshoots a LAN bottleneck. On a long path a SACK covers a whole
+      // burst (a hundred packets at 1 Gbit/s), and L = 2 MTUs took seconds to
+      // open a 2.5 MB window (1 Gbit/s x 20 ms at 21 % of the rate over 64 MB):
+      // there the whole acknowledged amount counts, and HyStart++ (RFC 9406,
+      // hystart()) ends slow start on rising delay before the queue overflows.
+      size_t grow = long_path ? newly_acked : std::min(newly_acked, 2 * cfg_.mtu);
+      if (hs_css_) grow /= kCssDivisor;
+      if (flight_before + cfg_.mtu >= cwnd_) cwnd_ += std::max<size_t>(grow, 1);
     } else {
       partial_acked_ += newly_acked;
       if (partial_acked_ >= cwnd_ && flight_before + cfg_.mtu >= cwnd_) {
@@ -885,6 +955,7 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
   }
   if (new_fast && !fast_recovery_) {
     cwnd_bypass_ = 1;
+    hs_done_ = true;  // HyStart++ covers only the initial slow start
     // Loss response after TCP Veno: the backlog this association keeps in the
     // path's queues is cwnd * (SRTT - min RTT) / SRTT. A loss with (almost) no
     // backlog is taken as random (wireless, lossy WAN) and keeps cwnd (below);
@@ -966,6 +1037,7 @@ void SctpAssociation::on_tlp() {
   for (Chunk* ch : inflight_) {
     if (ch->acked || ch->retransmit) continue;
     ch->retransmit = true;
+    rtx_.insert(ch->tsn);
     ch->fast = true;  // may go out even when cwnd is full
     ch->probe = true;
     if (ch->in_flight) {
@@ -1112,6 +1184,45 @@ bool SctpAssociation::send_framed(uint16_t stream, uint32_t ppid, const uint8_t*
   return true;
 }
 
+// HyStart++ (RFC 9406) for the initial slow start on long paths: per round
+// (one window's worth of TSNs), the minimum RTT of at least kHsSamples
+// samples; once it exceeds the previous round's by clamp(prev / 8, 4 ms,
+// 16 ms) the queue is building: growth drops to a quarter (conservative slow
+// start) for kCssRounds rounds, then congestion avoidance takes over with
+// ssthresh = cwnd. A round whose minimum falls back below the CSS baseline
+// was a false alarm and resumes slow start.
+void SctpAssociation::hystart(uint32_t cum, uint64_t rtt_sample) {
+  if (!hs_round_ || !tsn_lt(cum, hs_window_end_)) {  // a round ended
+    hs_last_min_ = hs_cur_min_;
+    hs_cur_min_ = UINT64_MAX;
+    hs_samples_ = 0;
+    hs_window_end_ = next_tsn_ - 1;
+    hs_round_ = true;
+    if (hs_css_ && ++hs_css_rounds_ >= kCssRounds) {
+      hs_css_ = false;
+      hs_done_ = true;
+      ssthresh_ = cwnd_;
+      stats_.hystart_exits++;
+      return;
+    }
+  }
+  if (rtt_sample) {
+    hs_cur_min_ = std::min(hs_cur_min_, rtt_sample);
+    hs_samples_++;
+  }
+  if (hs_samples_ < kHsSamples || hs_cur_min_ == UINT64_MAX || hs_last_min_ == UINT64_MAX) return;
+  if (!hs_css_) {
+    const uint64_t thresh = std::clamp<uint64_t>(hs_last_min_ / 8, 4000, 16000);
+    if (hs_cur_min_ >= hs_last_min_ + thresh) {
+      hs_css_ = true;
+      hs_css_base_ = hs_cur_min_;
+      hs_css_rounds_ = 0;
+    }
+  } else if (hs_cur_min_ < hs_css_base_) {
+    hs_css_ = false;  // spurious: back to slow start
+  }
+}
+
 void SctpAssociation::start_t3() {
   stop_t3();
   std::weak_ptr<SctpAssociation> w = shared_from_this();
@@ -1139,10 +1250,13 @@ void SctpAssociation::on_t3() {
   cwnd_ = cfg_.mtu;
   partial_acked_ = 0;
   fast_recovery_ = false;
+  hs_done_ = true;
+  hs_css_ = false;
   rto_us_ = std::min<uint64_t>(rto_us_ * 2, cfg_.rto_max_ms * 1000);
   for (Chunk* ch : inflight_) {
     if (ch->acked) continue;
     ch->retransmit = true;
+    rtx_.insert(ch->tsn);
     ch->fast = false;
     ch->probe = false;
     if (ch->in_flight) {
@@ -1178,13 +1292,7 @@ void SctpAssociation::flush() {
   // delayed by sack_delay_us so a lone request frame is acknowledged by the
   // response that follows instead of by a pure SACK (one less wakeup per
   // request on each side). RFC 9260 §6.2 allows up to 500 ms.
-  bool data_ready = can_data && (!sendq_.empty() || !sendq_pri_.empty());
-  if (can_data && !data_ready)
-    for (Chunk* ch : inflight_)
-      if (ch->retransmit) {
-        data_ready = true;
-        break;
-      }
+  bool data_ready = can_data && (!sendq_.empty() || !sendq_pri_.empty() || !rtx_.empty());
   bool sack_now = sack_needed_ && (sack_urgent_ || data_pkts_unacked_ >= 2 || data_ready || cfg_.sack_delay_us == 0 ||
                                    !ooo_.empty() || !dups_.empty());
   if (sack_needed_ && !sack_now && !sack_timer_) {
@@ -1253,6 +1361,7 @@ void SctpAssociation::flush() {
     }
     ch->sent_us = now;
     ch->tx++;
+    sendlog_.push_back(SendRec{ch->tsn, ch->tx, now});
     if (!ch->in_flight) {
       ch->in_flight = true;
       flight_size_ += ch->len;
@@ -1265,11 +1374,17 @@ void SctpAssociation::flush() {
   // retransmission of a recovery episode (RFC 9260 §7.2.4) or a tail-loss
   // probe — not once per flush, which would overdrive a congested path.
   bool sent_any = false;
-  for (Chunk* ch : inflight_) {
-    if (!ch->retransmit || ch->acked) continue;
+  for (auto it = rtx_.begin(); it != rtx_.end();) {
+    const uint32_t k = *it - (inflight_.empty() ? 0 : inflight_.front()->tsn);
+    Chunk* ch = k < inflight_.size() ? inflight_[k] : nullptr;
+    if (!ch || !ch->retransmit || ch->acked) {
+      it = rtx_.erase(it);
+      continue;
+    }
     bool allowed = flight_size_ + ch->len <= cwnd_ || flight_size_ == 0 || (ch->fast && cwnd_bypass_ > 0);
     if (!allowed) break;
     if (ch->fast && flight_size_ + ch->len > cwnd_ && flight_size_ && cwnd_bypass_ > 0) cwnd_bypass_--;
+    it = rtx_.erase(it);
     ch->retransmit = false;
     ch->fast = false;
     ch->miss = 0;

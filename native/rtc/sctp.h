@@ -24,6 +24,7 @@
 #include <functional>
 #include <map>
 #include <memory>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -57,6 +58,7 @@ struct SctpStats {
   uint64_t retransmits = 0, fast_retransmits = 0, t3_expirations = 0;
   uint64_t tlp_probes = 0, rack_marks = 0, random_loss_events = 0;
   uint64_t random_loss_cuts = 0;  // sustained random loss: the periodic 0.85 cut
+  uint64_t hystart_exits = 0;     // initial slow starts ended by HyStart++ (rising delay)
   uint64_t dup_copies_sent = 0;  // redundant copies of small messages (lossy paths)
   uint64_t early_deliveries = 0;  // messages handed up ahead of a TSN gap (another stream's loss)
   uint64_t sacks_sent = 0, sacks_received = 0;
@@ -204,7 +206,20 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   std::deque<Msg> sendq_;
   std::deque<Msg> sendq_pri_;  // single-chunk priority messages (send_framed(..., priority))
   std::map<uint16_t, uint16_t> next_ssn_;
-  std::deque<Chunk*> inflight_;  // ordered by TSN
+  std::deque<Chunk*> inflight_;  // consecutive TSNs from cum_acked_ + 1
+  // Loss bookkeeping kept incrementally (handle_sack is O(news), not O(window)):
+  struct TsnLess {
+    bool operator()(uint32_t a, uint32_t b) const { return int32_t(a - b) < 0; }
+  };
+  std::set<uint32_t, TsnLess> rtx_;  // TSNs marked for retransmission, in TSN order
+  std::vector<std::pair<uint32_t, uint32_t>> gap_known_, blocks_;  // last SACK's gap blocks (absolute TSNs)
+  struct SendRec {
+    uint32_t tsn;
+    int tx;            // transmission count this entry is for (stale once the chunk is sent again)
+    uint64_t sent_us;
+  };
+  std::deque<SendRec> sendlog_;  // transmissions in send order (RACK)
+  uint64_t rack_xmit_us_ = 0;    // latest send time of an acknowledged once-sent chunk (RACK.xmit_ts)
   std::vector<Chunk*> dup_;      // this flush's small whole messages to send twice
   static constexpr size_t kDupMaxChunk = 512;
   bool dup_small_enabled() const;
@@ -219,6 +234,15 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   uint64_t tlp_timer_ = 0;  // tail-loss probe (fires before T3, no cwnd collapse)
   int tlp_count_ = 0;       // probes since the cumulative ack last advanced
   int cwnd_bypass_ = 0;     // chunks allowed out beyond cwnd (one per loss event)
+  // HyStart++ state (hystart()).
+  void hystart(uint32_t cum, uint64_t rtt_sample);
+  static constexpr uint64_t kLongPathUs = 5000;  // base RTT from which a path counts as long (WAN)
+  static constexpr int kHsSamples = 8, kCssRounds = 5;
+  static constexpr size_t kCssDivisor = 4;
+  bool hs_done_ = false, hs_css_ = false, hs_round_ = false;
+  int hs_samples_ = 0, hs_css_rounds_ = 0;
+  uint32_t hs_window_end_ = 0;
+  uint64_t hs_last_min_ = UINT64_MAX, hs_cur_min_ = UINT64_MAX, hs_css_base_ = 0;
   int random_streak_ = 0;   // random-loss episodes in a row (see handle_sack)
   uint64_t last_loss_us_ = 0;
   static constexpr int kRandomStreakCut = 8;
