@@ -21,6 +21,7 @@
 #include "core/log.h"
 #include "core/profiler.h"
 #include "rtc/dtls.h"
+#include "rtc/turn.h"
 #include "tunnel/app.h"
 
 using namespace p2pt;
@@ -43,7 +44,7 @@ const std::vector<Opt>& serve_opts() {
       {"room", "TUNNEL_ROOM", nullptr, "Room name to join"},
       {"upstream", "TUNNEL_UPSTREAM", nullptr, "Upstream HTTP URL to forward requests to (comma-separated: least-loaded across several)"},
       {"advertise", nullptr, "/", "Path prefix to advertise (e.g. /v1)"},
-      {"turn", "TUNNEL_TURN", "", "TURN server URL (e.g. turn:turn.example.com:3478)"},
+      {"turn", "TUNNEL_TURN", "", "TURN server URL (turn:host[:3478][?transport=udp|tcp], turns:host[:5349])"},
       {"turn-user", "TUNNEL_TURN_USER", "", "TURN server username"},
       {"turn-pass", "TUNNEL_TURN_PASS", "", "TURN server password"},
   };
@@ -55,7 +56,7 @@ const std::vector<Opt>& proxy_opts() {
       {"signal", "TUNNEL_SIGNAL", "wss://signal-server.fly.dev", "WebSocket URL of the signaling server"},
       {"room", "TUNNEL_ROOM", nullptr, "Room name to join"},
       {"listen", "TUNNEL_LISTEN", "127.0.0.1:8000", "Local address to listen on"},
-      {"turn", "TUNNEL_TURN", "", "TURN server URL (e.g. turn:turn.example.com:3478)"},
+      {"turn", "TUNNEL_TURN", "", "TURN server URL (turn:host[:3478][?transport=udp|tcp], turns:host[:5349])"},
       {"turn-user", "TUNNEL_TURN_USER", "", "TURN server username"},
       {"turn-pass", "TUNNEL_TURN_PASS", "", "TURN server password"},
   };
@@ -292,6 +293,14 @@ int main(int argc, char** argv) {
     cfg.listen = m["listen"];
   }
   cfg.rtc.turn.url = m["turn"];
+  if (!cfg.rtc.turn.url.empty()) {
+    rtc::TurnUrl tu;
+    std::string err;
+    if (!rtc::TurnClient::parse_url(cfg.rtc.turn.url, tu, &err)) {
+      fprintf(stderr, "error: --turn: %s\n", err.c_str());
+      return 2;
+    }
+  }
   cfg.rtc.turn.username = m["turn-user"];
   cfg.rtc.turn.password = m["turn-pass"];
   cfg.transport = m["transport"];

@@ -317,16 +317,17 @@ void IceAgent::srflx_window_done(const std::shared_ptr<SrflxWindow>& win) {
 
 void IceAgent::start_relay() {
   if (cfg_.turn_url.empty()) return;
-  std::string host;
-  uint16_t port;
-  if (!parse_server_url(cfg_.turn_url, host, port, 3478)) {
-    LOG_WARN(kT, "invalid TURN URL %s", cfg_.turn_url.c_str());
+  TurnUrl url;
+  std::string err;
+  if (!TurnClient::parse_url(cfg_.turn_url, url, &err)) {
+    LOG_ERROR(kT, "%s", err.c_str());  // the CLI refuses such URLs before any session
     return;
   }
   // A loopback TURN server (tests, same-host relays) is reached from the
   // loopback socket; anything else from the first routable IPv4 socket.
+  // (Over TCP/TLS the socket is only the relayed candidate's base.)
   SockAddr probe;
-  bool server_loopback = SockAddr::parse(host, port, probe) && probe.is_loopback();
+  bool server_loopback = SockAddr::parse(url.host, url.port, probe) && probe.is_loopback();
   int si = -1;
   for (int i = 0; i < int(socks_.size()); i++)
     if (socks_[i].loopback == server_loopback && socks_[i].addr.family() == AF_INET) {
@@ -339,7 +340,7 @@ void IceAgent::start_relay() {
   }
   pending_gather_++;
   std::weak_ptr<IceAgent> w = shared_from_this();
-  turn_ = TurnClient::create(r_, this, si, host, port, cfg_.turn_user, cfg_.turn_pass,
+  turn_ = TurnClient::create(r_, this, si, url, cfg_.turn_user, cfg_.turn_pass,
                              [w, si](bool ok, const SockAddr& relayed, const SockAddr& mapped) {
                                auto s = w.lock();
                                if (!s) return;

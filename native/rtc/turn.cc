@@ -10,13 +10,78 @@ namespace p2pt::rtc {
 
 static const char* kT = "tunnel::turn";
 
-std::shared_ptr<TurnClient> TurnClient::create(Reactor& r, IceAgent* agent, int sock, const std::string& host,
-                                               uint16_t port, const std::string& user, const std::string& pass,
-                                               AllocCb cb) {
+bool TurnClient::parse_url(const std::string& url, TurnUrl& out, std::string* err) {
+  auto fail = [&](const std::string& why) {
+    if (err) *err = why;
+    return false;
+  };
+  size_t colon = url.find(':');
+  if (colon == std::string::npos) return fail("TURN URL '" + url + "' has no scheme (turn: or turns:)");
+  const std::string scheme = url.substr(0, colon);
+  if (scheme == "turn") {
+    out.transport = TurnUrl::Transport::Udp;
+    out.port = 3478;
+  } else if (scheme == "turns") {
+    out.transport = TurnUrl::Transport::Tls;
+    out.port = 5349;
+  } else {
+    return fail("unsupported TURN URL scheme '" + scheme + ":' in '" + url + "' (use turn: or turns:)");
+  }
+  std::string s = url.substr(colon + 1);
+  if (s.rfind("//", 0) == 0) s = s.substr(2);
+  std::string query;
+  if (size_t q = s.find('?'); q != std::string::npos) {
+    query = s.substr(q + 1);
+    s = s.substr(0, q);
+  }
+  for (size_t a = 0; a < query.size();) {
+    size_t amp = query.find('&', a);
+    if (amp == std::string::npos) amp = query.size();
+    std::string kv = query.substr(a, amp - a);
+    a = amp + 1;
+    if (kv.rfind("transport=", 0) != 0) continue;  // other parameters carry no meaning here
+    std::string tr = kv.substr(10);
+    for (auto& c : tr) c = char(tolower(static_cast<unsigned char>(c)));
+    if (tr == "tcp") {
+      if (out.transport == TurnUrl::Transport::Udp) out.transport = TurnUrl::Transport::Tcp;
+    } else if (tr == "udp") {
+      if (out.transport == TurnUrl::Transport::Tls)
+        return fail("unsupported TURN transport in '" + url + "': turns: over udp (DTLS) is not supported");
+    } else {
+      return fail("unsupported TURN transport '" + tr + "' in '" + url + "' (udp or tcp)");
+    }
+  }
+  if (!s.empty() && s[0] == '[') {
+    size_t rb = s.find(']');
+    if (rb == std::string::npos) return fail("malformed IPv6 host in TURN URL '" + url + "'");
+    out.host = s.substr(1, rb - 1);
+    if (rb + 1 < s.size()) {
+      if (s[rb + 1] != ':') return fail("malformed TURN URL '" + url + "'");
+      out.port = uint16_t(atoi(s.c_str() + rb + 2));
+    }
+  } else if (size_t pc = s.rfind(':'); pc != std::string::npos) {
+    out.host = s.substr(0, pc);
+    out.port = uint16_t(atoi(s.c_str() + pc + 1));
+  } else {
+    out.host = s;
+  }
+  if (out.host.empty() || out.port == 0) return fail("malformed TURN URL '" + url + "'");
+  return true;
+}
+
+std::shared_ptr<TurnClient> TurnClient::create(Reactor& r, IceAgent* agent, int sock, const TurnUrl& url,
+                                               const std::string& user, const std::string& pass, AllocCb cb) {
   auto t = std::shared_ptr<TurnClient>(new TurnClient(r, agent, sock));
   t->user_ = user;
   t->pass_ = pass;
   t->alloc_cb_ = std::move(cb);
+  if (url.transport != TurnUrl::Transport::Udp) {
+    t->stream_ = true;
+    t->connect_stream(url);
+    return t;
+  }
+  const std::string host = url.host;
+  const uint16_t port = url.port;
   std::weak_ptr<TurnClient> w = t;
   resolve_async(r, host, port, [w, host](std::vector<SockAddr> addrs, std::string err) {
     auto s = w.lock();
@@ -38,6 +103,74 @@ std::shared_ptr<TurnClient> TurnClient::create(Reactor& r, IceAgent* agent, int 
   return t;
 }
 
+// TCP / TLS control connection (TLS verified against the system trust store,
+// SNI and host/IP checks, as for wss:// and https://).
+void TurnClient::connect_stream(const TurnUrl& url) {
+  std::weak_ptr<TurnClient> w = shared_from_this();
+  const bool tls = url.transport == TurnUrl::Transport::Tls;
+  const std::string desc = url.host + ":" + std::to_string(url.port) + " (" + url.transport_name() + ")";
+  TcpConn::connect(
+      r_, url.host, url.port, tls,
+      [w, desc](std::shared_ptr<TcpConn> c, std::string err) {
+        auto s = w.lock();
+        if (!s || s->closed_) {
+          if (c) c->close();
+          return;
+        }
+        if (!c) {
+          LOG_WARN(kT, "TURN server %s unreachable: %s", desc.c_str(), err.c_str());
+          s->fail_alloc();
+          return;
+        }
+        s->conn_ = c;
+        s->server_ = c->peer();
+        s->resolved_ = true;
+        c->on_data([w](const uint8_t* p, size_t n) {
+          if (auto x = w.lock()) x->on_stream_data(p, n);
+        });
+        c->on_close([w, desc](const std::string& why) {
+          auto x = w.lock();
+          if (!x || x->closed_) return;
+          LOG_WARN(kT, "TURN connection to %s closed%s%s", desc.c_str(), why.empty() ? "" : ": ", why.c_str());
+          x->conn_.reset();
+          if (!x->allocated_) x->fail_alloc();
+        });
+        LOG_DEBUG(kT, "TURN control connection to %s up", desc.c_str());
+        s->allocate();
+      },
+      10000);
+}
+
+// Stream framing (RFC 8656 §12.5 / RFC 5389 §7.2.2): ChannelData (first byte
+// 0x40-0x7F) is 4 + length bytes padded to 4; a STUN message is 20 + length.
+void TurnClient::on_stream_data(const uint8_t* p, size_t n) {
+  inbuf_.append(reinterpret_cast<const char*>(p), n);
+  size_t off = 0;
+  auto self = shared_from_this();
+  while (inbuf_.size() - off >= 4 && !closed_) {
+    const uint8_t* m = reinterpret_cast<const uint8_t*>(inbuf_.data()) + off;
+    size_t len;
+    if (m[0] >= 0x40 && m[0] <= 0x7F) len = (4 + size_t(rd16(m + 2)) + 3) & ~size_t(3);
+    else if (m[0] < 4) len = 20 + size_t(rd16(m + 2));
+    else {  // not STUN or ChannelData: the stream is out of sync
+      LOG_WARN(kT, "TURN stream framing lost; closing the connection");
+      inbuf_.clear();
+      if (conn_) conn_->close("framing");
+      return;
+    }
+    if (inbuf_.size() - off < len) break;
+    on_packet(m, len);
+    off += len;
+  }
+  inbuf_.erase(0, off);
+}
+
+void TurnClient::fail_alloc() {
+  auto cb = std::move(alloc_cb_);
+  alloc_cb_ = nullptr;
+  if (cb) cb(false, {}, {});
+}
+
 TurnClient::~TurnClient() { close(); }
 
 void TurnClient::close() {
@@ -55,12 +188,22 @@ void TurnClient::close() {
     sign(m);
     auto b = m.serialize(key_.empty() ? nullptr : &key_, true);
     raw_send(b.data(), b.size());
-    agent_->flush();
+    if (!stream_) agent_->flush();
+  }
+  if (conn_) {
+    conn_->on_data(nullptr);
+    conn_->on_close(nullptr);
+    conn_->close_after_flush();
+    conn_.reset();
   }
   agent_ = nullptr;
 }
 
 void TurnClient::raw_send(const uint8_t* p, size_t n) {
+  if (stream_) {
+    if (conn_ && !conn_->closed()) conn_->write(Bytes::copy(p, n));
+    return;
+  }
   if (agent_) agent_->send_raw(-1 - sock_, server_, p, n);
 }
 
@@ -80,7 +223,10 @@ void TurnClient::send_request(stun::Message m, std::function<void(const stun::Me
   pd.bytes = b;
   pd.tries = 1;
   raw_send(b.data(), b.size());
-  arm_retransmit(tid, 500);
+  // A reliable stream delivers the request or fails: no retransmissions, one
+  // overall timeout (7 tries' worth) instead.
+  if (stream_) pd.tries = 6;
+  arm_retransmit(tid, stream_ ? 9500 : 500);
 }
 
 // STUN request retransmission: RTO doubling from 500 ms (capped at 3.2 s), 6 tries.

@@ -1,4 +1,4 @@
-// TURN client (RFC 8656, UDP allocations, long-term credentials).
+// TURN client (RFC 8656, UDP relays, long-term credentials).
 //
 // The reference wires --turn/--turn-user/--turn-pass into webrtc-rs's ICE
 // servers (tunnel/src/cli.rs:30-40, rtc.rs:54-63) while its README claims TURN
@@ -6,6 +6,14 @@
 // client: Allocate (401 -> REALM/NONCE -> authenticated retry), Refresh before
 // expiry, CreatePermission per remote candidate, ChannelBind for compact
 // ChannelData framing, Send/Data indications until the channel is bound.
+//
+// The client reaches its server over UDP (turn:host[:3478]), TCP
+// (turn:host?transport=tcp) or TLS (turns:host[:5349], RFC 8656 §3.1): the
+// transports firewalled networks leave open. Over a stream, STUN messages and
+// ChannelData (padded to 4 bytes, §12.5) are framed back to back and requests
+// are not retransmitted; the relayed transport to the peer stays UDP
+// (REQUESTED-TRANSPORT 17). A URL with another scheme or transport is refused
+// with an error naming it (parse_url), never silently used as UDP.
 #pragma once
 
 #include <functional>
@@ -21,15 +29,32 @@ namespace p2pt::rtc {
 
 class IceAgent;
 
+
+struct TurnUrl {
+  enum class Transport { Udp, Tcp, Tls };
+  std::string host;
+  uint16_t port = 3478;
+  Transport transport = Transport::Udp;
+  const char* transport_name() const {
+    return transport == Transport::Udp ? "udp" : transport == Transport::Tcp ? "tcp" : "tls";
+  }
+};
+
 class TurnClient : public std::enable_shared_from_this<TurnClient> {
  public:
   using AllocCb = std::function<void(bool ok, const SockAddr& relayed, const SockAddr& mapped)>;
-  static std::shared_ptr<TurnClient> create(Reactor& r, IceAgent* agent, int sock, const std::string& host,
-                                            uint16_t port, const std::string& user, const std::string& pass,
-                                            AllocCb cb);
+  // "turn:host[:port][?transport=udp|tcp]" or "turns:host[:port][?transport=tcp]"
+  // (an IPv6 host in brackets); false with *err naming what is not supported.
+  static bool parse_url(const std::string& url, TurnUrl& out, std::string* err);
+  // `sock`: the ICE socket the relayed candidate is based on (and, over UDP,
+  // the one the server is reached from).
+  static std::shared_ptr<TurnClient> create(Reactor& r, IceAgent* agent, int sock, const TurnUrl& url,
+                                            const std::string& user, const std::string& pass, AllocCb cb);
   ~TurnClient();
   void close();
-  bool is_server(int sock, const SockAddr& from) const { return sock == sock_ && resolved_ && from == server_; }
+  bool is_server(int sock, const SockAddr& from) const {
+    return !stream_ && sock == sock_ && resolved_ && from == server_;
+  }
   void on_packet(const uint8_t* p, size_t n);
   void permit(const SockAddr& peer);
   void send_to(const SockAddr& peer, const uint8_t* p, size_t n);
@@ -45,10 +70,16 @@ class TurnClient : public std::enable_shared_from_this<TurnClient> {
   void channel_bind(const SockAddr& peer);
   void sign(stun::Message& m);
   void raw_send(const uint8_t* p, size_t n);
+  void fail_alloc();
+  void connect_stream(const TurnUrl& url);
+  void on_stream_data(const uint8_t* p, size_t n);
 
   Reactor& r_;
   IceAgent* agent_;
   int sock_;
+  bool stream_ = false;                 // TCP or TLS to the server
+  std::shared_ptr<TcpConn> conn_;       // the stream, once connected
+  std::string inbuf_;                   // stream bytes not yet framed
   SockAddr server_;
   bool resolved_ = false;
   std::string user_, pass_, realm_, nonce_, key_;

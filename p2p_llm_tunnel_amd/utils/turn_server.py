@@ -5,6 +5,12 @@ the native TURN client (native/rtc/turn.cc) is checked against a separate
 implementation. Supports Allocate (401 challenge -> authenticated), Refresh
 (incl. LIFETIME 0), CreatePermission, ChannelBind, Send/Data indications and
 ChannelData in both directions.
+
+Clients reach it over UDP (default), TCP (transport="tcp": turn:...?transport=tcp)
+or TLS (transport="tls" with an ssl.SSLContext: turns:...); over a stream,
+STUN messages and ChannelData (padded to 4 bytes) are framed back to back
+(RFC 8656 §12.5) and each connection is its own allocation. Relays to peers
+are UDP in every case.
 """
 from __future__ import annotations
 
@@ -64,24 +70,115 @@ def unxor_addr(v: bytes):
     return socket.inet_ntoa(struct.pack(">I", xi ^ MAGIC)), xp ^ (MAGIC >> 16)
 
 
+def frames(buf: bytearray):
+    """Complete STUN / ChannelData messages at the front of a stream buffer
+    (consumed from it)."""
+    out = []
+    while len(buf) >= 4:
+        if 0x40 <= buf[0] <= 0x7F:
+            n = (4 + struct.unpack(">H", buf[2:4])[0] + 3) & ~3
+        elif buf[0] < 4:
+            n = 20 + struct.unpack(">H", buf[2:4])[0]
+        else:
+            raise ValueError("stream out of sync")
+        if len(buf) < n:
+            break
+        out.append(bytes(buf[:n]))
+        del buf[:n]
+    return out
+
+
 class TurnServer:
-    def __init__(self, user="user", password="pass", realm="p2pt.test", host="127.0.0.1"):
+    def __init__(self, user="user", password="pass", realm="p2pt.test", host="127.0.0.1", transport="udp",
+                 ssl_ctx=None):
         self.user, self.password, self.realm = user, password, realm
         self.key = hashlib.md5(f"{user}:{realm}:{password}".encode()).digest()
         self.nonce = os.urandom(8).hex().encode()
-        self.sock = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
-        self.sock.bind((host, 0))
+        self.transport, self.ssl_ctx = transport, ssl_ctx
         self.host = host
-        self.port = self.sock.getsockname()[1]
-        self.allocs = {}     # client addr -> dict(relay=sock, perms=set(ip), chans={num: peer}, peers={peer: num})
-        self.by_relay = {}   # relay sock -> client addr
-        self.stats = {"bindings": 0, "allocations": 0, "relayed_to_peer": 0, "relayed_to_client": 0, "channel_binds": 0}
+        self.sock = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)  # UDP clients (transport "udp")
+        self.lsock = None
+        if transport == "udp":
+            self.sock.bind((host, 0))
+            self.port = self.sock.getsockname()[1]
+        else:
+            self.lsock = socket.create_server((host, 0))
+            self.port = self.lsock.getsockname()[1]
+        self.conns = {}      # stream connection -> (key, rx buffer)
+        self.conn_of = {}    # key -> stream connection
+        self.peer_of = {}    # key -> the client's (ip, port) as seen by the server
+        self.allocs = {}     # client key -> dict(relay=sock, perms=set(ip), chans={num: peer}, peers={peer: num})
+        self.by_relay = {}   # relay sock -> client key
+        self.stats = {"bindings": 0, "allocations": 0, "relayed_to_peer": 0, "relayed_to_client": 0, "channel_binds": 0,
+                      "stream_connections": 0}
         self._stop = False
         self.thread = threading.Thread(target=self._run, daemon=True)
 
     @property
     def url(self):
+        if self.transport == "tcp":
+            return f"turn:{self.host}:{self.port}?transport=tcp"
+        if self.transport == "tls":
+            return f"turns:{self.host}:{self.port}"
         return f"turn:{self.host}:{self.port}"
+
+    def _send(self, data, addr):
+        c = self.conn_of.get(addr)
+        if c is not None:
+            try:
+                c.sendall(data)
+            except OSError:
+                pass
+        else:
+            self.sock.sendto(data, addr)
+
+    def _accept(self):
+        try:
+            c, peer = self.lsock.accept()
+        except OSError:
+            return
+        try:
+            if self.ssl_ctx is not None:
+                c.settimeout(5)
+                c = self.ssl_ctx.wrap_socket(c, server_side=True)
+            c.settimeout(5)
+        except OSError:
+            c.close()
+            return
+        key = ("stream", self.stats["stream_connections"])
+        self.stats["stream_connections"] += 1
+        self.conns[c] = (key, bytearray())
+        self.conn_of[key] = c
+        self.peer_of[key] = peer
+
+    def _drop_conn(self, c):
+        key, _ = self.conns.pop(c)
+        self.conn_of.pop(key, None)
+        a = self.allocs.pop(key, None)
+        if a:
+            self.by_relay.pop(a["relay"], None)
+            a["relay"].close()
+        c.close()
+
+    def _read_conn(self, c):
+        key, buf = self.conns[c]
+        try:
+            d = c.recv(65536)
+            while d and getattr(c, "pending", lambda: 0)():
+                d += c.recv(65536)
+        except (OSError, ValueError):
+            d = b""
+        if not d:
+            self._drop_conn(c)
+            return
+        buf += d
+        try:
+            msgs = frames(buf)
+        except ValueError:
+            self._drop_conn(c)
+            return
+        for m in msgs:
+            self._handle_client(m, key)
 
     def start(self):
         self.thread.start()
@@ -92,6 +189,10 @@ class TurnServer:
         self.thread.join(timeout=2)
         for a in self.allocs.values():
             a["relay"].close()
+        for c in list(self.conns):
+            c.close()
+        if self.lsock is not None:
+            self.lsock.close()
         self.sock.close()
 
     # ------------------------------------------------------------------
@@ -107,7 +208,7 @@ class TurnServer:
     def _err(self, t, tid, code, reason, addr):
         v = struct.pack(">HBB", 0, code // 100, code % 100) + reason.encode()
         attrs = [(0x0009, v), (0x0014, self.realm.encode()), (0x0015, self.nonce)]
-        self.sock.sendto(build(t | 0x0110, tid, attrs), addr)
+        self._send(build(t | 0x0110, tid, attrs), addr)
 
     def _handle_client(self, data, addr):
         if 0x40 <= data[0] <= 0x7F:  # ChannelData
@@ -135,7 +236,7 @@ class TurnServer:
             return
         if method == 0x0001:  # Binding
             self.stats["bindings"] += 1
-            self.sock.sendto(build(0x0101, tid, [(0x0020, xor_addr(*addr))]), addr)
+            self._send(build(0x0101, tid, [(0x0020, xor_addr(*self.peer_of.get(addr, addr)))]), addr)
             return
         if not self._auth_ok(data, attrs, mi_off):
             self._err(method, tid, 401, "Unauthorized", addr)
@@ -150,20 +251,20 @@ class TurnServer:
             self.by_relay[r] = addr
             self.stats["allocations"] += 1
             rh, rp = r.getsockname()
-            self.sock.sendto(build(0x0103, tid, [(0x0016, xor_addr(rh, rp)), (0x0020, xor_addr(*addr)),
-                                                  (0x000D, struct.pack(">I", 600))], self.key), addr)
+            self._send(build(0x0103, tid, [(0x0016, xor_addr(rh, rp)), (0x0020, xor_addr(*self.peer_of.get(addr, addr))),
+                                            (0x000D, struct.pack(">I", 600))], self.key), addr)
         elif method == 0x0004:  # Refresh
             lt = struct.unpack(">I", d.get(0x000D, b"\0\0\x02\x58"))[0]
             if lt == 0 and addr in self.allocs:
                 a = self.allocs.pop(addr)
                 self.by_relay.pop(a["relay"], None)
                 a["relay"].close()
-            self.sock.sendto(build(0x0104, tid, [(0x000D, struct.pack(">I", lt))], self.key), addr)
+            self._send(build(0x0104, tid, [(0x000D, struct.pack(">I", lt))], self.key), addr)
         elif method == 0x0008:  # CreatePermission
             a = self.allocs.get(addr)
             if a and 0x0012 in d:
                 a["perms"].add(unxor_addr(d[0x0012])[0])
-            self.sock.sendto(build(0x0108, tid, [], self.key), addr)
+            self._send(build(0x0108, tid, [], self.key), addr)
         elif method == 0x0009:  # ChannelBind
             a = self.allocs.get(addr)
             ch = struct.unpack(">H", d[0x000C][:2])[0]
@@ -172,7 +273,7 @@ class TurnServer:
             a["peers"][peer] = ch
             a["perms"].add(peer[0])
             self.stats["channel_binds"] += 1
-            self.sock.sendto(build(0x0109, tid, [], self.key), addr)
+            self._send(build(0x0109, tid, [], self.key), addr)
 
     def _handle_relay(self, r):
         try:
@@ -188,18 +289,22 @@ class TurnServer:
             msg = struct.pack(">HH", ch, len(data)) + data + b"\0" * _pad(len(data))
         else:
             msg = build(0x0017, os.urandom(12), [(0x0012, xor_addr(*peer)), (0x0013, data)], fingerprint=False)
-        self.sock.sendto(msg, client)
+        self._send(msg, client)
         self.stats["relayed_to_client"] += 1
 
     def _run(self):
         while not self._stop:
-            socks = [self.sock] + list(self.by_relay)
+            socks = [self.sock] + list(self.by_relay) + list(self.conns) + ([self.lsock] if self.lsock else [])
             try:
                 ready, _, _ = select.select(socks, [], [], 0.1)
             except (OSError, ValueError):
                 continue
             for s in ready:
-                if s is self.sock:
+                if s is self.lsock:
+                    self._accept()
+                elif s in self.conns:
+                    self._read_conn(s)
+                elif s is self.sock:
                     try:
                         data, addr = s.recvfrom(65536)
                     except OSError:

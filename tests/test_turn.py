@@ -1,20 +1,59 @@
 """TURN relay path (--turn/--turn-user/--turn-pass; reference cli.rs:30-40,
 rtc.rs:54-63). Both peers are forced onto relayed candidates
-(--ice-relay-only) so every datagram crosses the test TURN server."""
+(--ice-relay-only) so every datagram crosses the test TURN server, reached
+over UDP, TCP (turn:...?transport=tcp) or TLS (turns:...), the transports a
+firewalled network leaves open. URLs the client cannot honour are refused."""
 import http.client
 import json
+import shutil
+import ssl
+import subprocess
 import urllib.request
 
+import pytest
+
+from p2p_llm_tunnel_amd import binary
 from p2p_llm_tunnel_amd.utils.procs import Tunnel
 from p2p_llm_tunnel_amd.utils.turn_server import TurnServer
 
 
-def test_tunnel_through_turn_relay(mock_upstream):
-    turn = TurnServer(user="alice", password="s3cret").start()
+@pytest.fixture(scope="module")
+def pki(tmp_path_factory):
+    if shutil.which("openssl") is None:
+        pytest.skip("openssl CLI not available")
+    d = tmp_path_factory.mktemp("turnpki")
+
+    def run(*args):
+        subprocess.run(list(args), cwd=d, check=True, capture_output=True)
+
+    run("openssl", "req", "-x509", "-newkey", "ec", "-pkeyopt", "ec_paramgen_curve:P-256", "-nodes",
+        "-keyout", "ca.key", "-out", "ca.pem", "-days", "2", "-subj", "/CN=p2pt turn test CA")
+    (d / "ext.cnf").write_text("subjectAltName=DNS:localhost,IP:127.0.0.1\nbasicConstraints=CA:FALSE\n")
+    run("openssl", "req", "-newkey", "ec", "-pkeyopt", "ec_paramgen_curve:P-256", "-nodes",
+        "-keyout", "srv.key", "-out", "srv.csr", "-subj", "/CN=localhost")
+    run("openssl", "x509", "-req", "-in", "srv.csr", "-CA", "ca.pem", "-CAkey", "ca.key", "-CAcreateserial",
+        "-out", "srv.pem", "-days", "2", "-extfile", "ext.cnf")
+    return d
+
+
+def _server(transport, pki=None):
+    ctx = None
+    if transport == "tls":
+        ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+        ctx.load_cert_chain(pki / "srv.pem", pki / "srv.key")
+    return TurnServer(user="alice", password="s3cret", transport=transport, ssl_ctx=ctx).start()
+
+
+@pytest.mark.parametrize("transport", ["udp", "tcp", "tls"])
+def test_tunnel_through_turn_relay(mock_upstream, transport, request):
+    pki = request.getfixturevalue("pki") if transport == "tls" else None
+    turn = _server(transport, pki)
+    env = {"RUST_LOG": "info,tunnel::rtc=debug,tunnel::turn=info"}
+    if pki:
+        env["SSL_CERT_FILE"] = str(pki / "ca.pem")  # the relay's certificate is verified, not trusted blindly
     try:
         extra = ["--turn", turn.url, "--turn-user", "alice", "--turn-pass", "s3cret", "--ice-relay-only"]
-        with Tunnel(mock_upstream, transport="webrtc", serve_extra=extra, proxy_extra=extra,
-                    env={"RUST_LOG": "info,tunnel::rtc=debug,tunnel::turn=info"}) as t:
+        with Tunnel(mock_upstream, transport="webrtc", serve_extra=extra, proxy_extra=extra, env=env) as t:
             assert urllib.request.urlopen(t.url + "/health", timeout=10).read() == b"ok"
             c = http.client.HTTPConnection("127.0.0.1", t.proxy_port, timeout=30)
             body = b"z" * 300000
@@ -29,6 +68,8 @@ def test_tunnel_through_turn_relay(mock_upstream):
         assert turn.stats["allocations"] >= 2
         assert turn.stats["relayed_to_peer"] > 50 and turn.stats["relayed_to_client"] > 50
         assert turn.stats["channel_binds"] >= 2
+        if transport != "udp":
+            assert turn.stats["stream_connections"] >= 2
     finally:
         turn.stop()
 
@@ -43,3 +84,30 @@ def test_turn_bad_credentials_fail_gathering_gracefully(mock_upstream):
         assert turn.stats["allocations"] == 0
     finally:
         turn.stop()
+
+
+def test_turns_with_untrusted_certificate_fails_gathering_gracefully(mock_upstream, pki):
+    """A TLS relay whose certificate does not verify gives no relayed
+    candidate (the host path still connects) instead of an unauthenticated
+    relay."""
+    turn = _server("tls", pki)
+    try:
+        extra = ["--turn", turn.url, "--turn-user", "alice", "--turn-pass", "s3cret"]
+        with Tunnel(mock_upstream, transport="webrtc", serve_extra=extra, proxy_extra=extra) as t:
+            assert urllib.request.urlopen(t.url + "/health", timeout=10).read() == b"ok"
+            assert "TURN allocation: relayed" not in t.serve.text()
+        assert turn.stats["allocations"] == 0
+    finally:
+        turn.stop()
+
+
+@pytest.mark.parametrize("url,msg", [
+    ("stun:relay.example.com", "unsupported TURN URL scheme 'stun:'"),
+    ("turns:relay.example.com?transport=udp", "turns: over udp (DTLS) is not supported"),
+    ("turn:relay.example.com?transport=sctp", "unsupported TURN transport 'sctp'"),
+    ("relay.example.com:3478", "unsupported TURN URL scheme"),
+])
+def test_unsupported_turn_url_is_refused(url, msg):
+    r = subprocess.run([binary("tunnel"), "proxy", "--room", "x", "--turn", url, "--signal", "ws://127.0.0.1:1",
+                        "--max-retries", "0"], capture_output=True, text=True, timeout=10)
+    assert r.returncode == 2 and msg in r.stderr, (r.returncode, r.stderr)
