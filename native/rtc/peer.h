@@ -107,6 +107,7 @@ class PeerConnection : public std::enable_shared_from_this<PeerConnection> {
   std::string describe_path() const;
   const SctpStats* sctp_stats() const { return sctp_ ? &sctp_->stats() : nullptr; }
   size_t sctp_mtu() const { return mtu_; }
+  const DtlsTransport* dtls() const { return dtls_.get(); }
 
   std::function<void(const std::string& candidate_json)> on_ice_candidate;
   std::function<void()> on_gathering_complete;

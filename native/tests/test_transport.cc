@@ -297,8 +297,10 @@ TEST(sctp_shallow_queue_bottleneck_backs_off) {
          (unsigned long long)p.a->stats().t3_expirations, (unsigned long long)p.a->stats().random_loss_events,
          (unsigned long long)p.a->stats().random_loss_cuts);
   CHECK_EQ(p.got_b.size(), size_t(n));
-  CHECK(drop_share < 0.035);  // 5 % with random losses never cut (before)
-  CHECK(mbps > 0.3 * 40);
+  if (kTimingChecks) {
+    CHECK(drop_share < 0.035);  // 5 % with random losses never cut (before)
+    CHECK(mbps > 0.3 * 40);
+  }
 }
 
 TEST(sctp_stream_reset_restarts_inbound_sequence) {
@@ -498,6 +500,78 @@ TEST(peerconnection_pair_loopback) {
   printf("  path: %s\n", off->describe_path().c_str());
   off->close();
   ans->close();
+}
+
+// Bulk both ways through a PeerConnection pair: flushes above the inline
+// threshold are sealed and sent on the DTLS TX lane and opened on the RX lane
+// (rtc/datapath.h) while the association thread runs SCTP; every byte must
+// arrive intact and in order, on the 1200-byte and the jumbo path.
+TEST(peerconnection_bulk_through_crypto_lanes) {
+  for (int jumbo = 0; jumbo < 2; jumbo++) {
+    Reactor r;
+    PcConfig cfg;
+    cfg.ice.include_loopback = true;
+    cfg.allow_jumbo = jumbo == 1;
+    auto off = PeerConnection::create(r, cfg, true);
+    auto ans = PeerConnection::create(r, cfg, false);
+    off->on_ice_candidate = [&](const std::string& c) { ans->add_ice_candidate(c, nullptr); };
+    ans->on_ice_candidate = [&](const std::string& c) { off->add_ice_candidate(c, nullptr); };
+    auto dc = off->create_data_channel("tunnel");
+    std::shared_ptr<DataChannel> rdc;
+    size_t got_ans = 0, got_off = 0, bytes_ans = 0, bytes_off = 0;
+    bool order_ok = true;
+    const int n = 300;
+    const std::string blk = payload(65000, 77);
+    ans->on_data_channel = [&](std::shared_ptr<DataChannel> d) {
+      rdc = d;
+      d->on_message = [&](Bytes m) {
+        order_ok &= m.size() == blk.size() + 5 && rd32(m.data() + 1) == got_ans + 1 &&
+                    memcmp(m.data() + 5, blk.data(), blk.size()) == 0;
+        got_ans++;
+        bytes_ans += m.size();
+      };
+    };
+    dc->on_message = [&](Bytes m) {
+      order_ok &= m.size() == blk.size() + 5 && memcmp(m.data() + 5, blk.data(), blk.size()) == 0;
+      got_off++;
+      bytes_off += m.size();
+    };
+    off->start_gathering();
+    ans->start_gathering();
+    CHECK(r.run_until([&] { return off->gathering_complete(); }, 3000));
+    std::string err;
+    CHECK(ans->set_remote_description(off->local_description(), &err));
+    CHECK(off->set_remote_description(ans->local_description(), &err));
+    CHECK(r.run_until([&] { return dc->is_open() && rdc && rdc->is_open(); }, 5000));
+    Bytes body = Bytes::copy(blk);
+    int sent_off = 0, sent_ans = 0;
+    // Keep a few MB queued each way (the tunnel's scheduler does the same).
+    CHECK(r.run_until([&] {
+      while (sent_off < n && dc->buffered_amount() < (4u << 20)) {
+        uint8_t hdr[5] = {21, 0, 0, 0, 0};
+        wr32(hdr + 1, uint32_t(++sent_off));
+        dc->send(hdr, 5, body);
+      }
+      while (sent_ans < n && rdc->buffered_amount() < (4u << 20)) {
+        uint8_t hdr[5] = {21, 0, 0, 0, 2};
+        rdc->send(hdr, 5, body);
+        sent_ans++;
+      }
+      return got_ans == size_t(n) && got_off == size_t(n);
+    }, 30000));
+    CHECK_EQ(got_ans, size_t(n));
+    CHECK_EQ(got_off, size_t(n));
+    CHECK(order_ok);
+    const auto* d = off->dtls();
+    CHECK(d && d->lanes_enabled());
+    if (d && d->lanes_possible()) CHECK(d->lane_tx_batches() > 0 && ans->dtls()->lane_rx_batches() > 0);
+    printf("  %s: %zu + %zu MB, lane tx batches %llu, inline %llu, rx batches %llu\n", off->describe_path().c_str(),
+           bytes_ans >> 20, bytes_off >> 20, (unsigned long long)(d ? d->lane_tx_batches() : 0),
+           (unsigned long long)(d ? d->inline_tx_batches() : 0),
+           (unsigned long long)(ans->dtls() ? ans->dtls()->lane_rx_batches() : 0));
+    off->close();
+    ans->close();
+  }
 }
 
 TEST(sctp_probe_rearms_t3_at_small_cwnd) {

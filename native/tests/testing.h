@@ -21,6 +21,21 @@ void fail(const char* file, int line, const std::string& msg);
 
 }  // namespace p2pt::testing
 
+// Sanitizer builds run several times slower: checks on wall-clock-sensitive
+// outcomes (drop shares under a rate-limited link, throughputs) only hold in
+// plain builds. kTimingChecks gates them; the behaviour checks always run.
+#if defined(__SANITIZE_THREAD__) || defined(__SANITIZE_ADDRESS__)
+constexpr bool kTimingChecks = false;
+#elif defined(__has_feature)
+#if __has_feature(thread_sanitizer) || __has_feature(address_sanitizer)
+constexpr bool kTimingChecks = false;
+#else
+constexpr bool kTimingChecks = true;
+#endif
+#else
+constexpr bool kTimingChecks = true;
+#endif
+
 #define TEST(name)                                                         \
   static void test_##name();                                               \
   static ::p2pt::testing::Reg reg_##name(#name, test_##name);              \

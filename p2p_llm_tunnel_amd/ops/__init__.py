@@ -40,12 +40,13 @@ def lib() -> ctypes.CDLL:
         _LIB.p2pt_decode_attention.argtypes = [vp, vp, vp, vp, vp, vp, i, i, i, i, i, i, i, f, vp]
         _LIB.p2pt_argmax.argtypes = [vp, vp, i, i, vp]
         _LIB.p2pt_skinny_gemm.argtypes = [vp, vp, vp, i, i, i, vp]
+        _LIB.p2pt_sample.argtypes = [vp, vp, vp, i, i, vp]
         _LIB.p2pt_llama_ws_bytes.argtypes = [ctypes.POINTER(LlamaDims)]
         _LIB.p2pt_llama_ws_bytes.restype = ctypes.c_size_t
         _LIB.p2pt_llama_decode.argtypes = [ctypes.POINTER(LlamaDims), ctypes.POINTER(vp), vp, vp, vp, vp, vp, i, i,
                                            i, vp, ctypes.c_size_t, vp, vp, vp]
         for fn in ("p2pt_rmsnorm", "p2pt_silu_mul", "p2pt_rope_qkv_cache", "p2pt_decode_attention", "p2pt_argmax",
-                   "p2pt_skinny_gemm", "p2pt_llama_decode"):
+                   "p2pt_skinny_gemm", "p2pt_llama_decode", "p2pt_sample"):
             getattr(_LIB, fn).restype = ctypes.c_int
     return _LIB
 
@@ -198,6 +199,37 @@ def argmax(logits: torch.Tensor) -> torch.Tensor:
     out = torch.empty(B, dtype=torch.int64, device=logits.device)
     _ok(lib().p2pt_argmax(_p(logits), _p(out), B, V, _stream(logits)), "argmax")
     return out
+
+
+def sample_(logits: torch.Tensor, ids: torch.Tensor, params: torch.Tensor) -> torch.Tensor:
+    """In-place stochastic sampling (sample.hip): rows of bf16 ``logits`` [B, V]
+    whose temperature is > 0 get ``ids[b]`` replaced by a draw from
+    softmax(logits / T) after top-k and top-p filtering; greedy rows (T <= 0)
+    keep the id already there. ``params``: int64 [5, >= B] — float32 bits of
+    T, top_k (<= 0 off), float32 bits of top_p (>= 1 off), seed, counter
+    (see ``pack_sampling``)."""
+    _check(logits, torch.bfloat16, "logits")
+    _check(ids, torch.int64, "ids", logits.device)
+    _check(params, torch.int64, "params", logits.device)
+    if logits.dim() != 2 or ids.shape != (logits.shape[0],) or params.dim() != 2 or params.shape[0] != 5:
+        raise ValueError("need logits [B, V], ids [B], params [5, B]")
+    B, V = logits.shape
+    if params.shape[1] != B:
+        raise ValueError("params must have one column per row")
+    _ok(lib().p2pt_sample(_p(logits), _p(ids), _p(params), B, V, _stream(logits)), "sample")
+    return ids
+
+
+def f32_bits(x: float) -> int:
+    """The float32 bit pattern of x as a non-negative int (the sampler's params encoding)."""
+    import struct
+    return struct.unpack("<I", struct.pack("<f", float(x)))[0]
+
+
+def pack_sampling(temperature: float, top_k: int, top_p: float, seed: int, counter: int) -> list[int]:
+    """One params column for ``sample_``."""
+    return [f32_bits(temperature), int(top_k), f32_bits(top_p), int(seed) & 0x7FFFFFFFFFFFFFFF,
+            int(counter) & 0x7FFFFFFFFFFFFFFF]
 
 
 def skinny_gemm(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:

@@ -1,6 +1,6 @@
 """Compile the HIP kernels in-tree for gfx950 (CDNA4 / MI355X).
 
-    hipcc -O3 --offload-arch=gfx950 -shared -fPIC kernels.hip decode_fused.hip -o _hip_ops.so
+    hipcc -O3 --offload-arch=gfx950 -shared -fPIC kernels.hip decode_fused.hip sample.hip -o _hip_ops.so
 
 Cross-compiles on a CPU-only host; the .so travels with the repo snapshot to
 the GPU box.
@@ -12,7 +12,7 @@ import shutil
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRCS = [os.path.join(HERE, f) for f in ("kernels.hip", "decode_fused.hip")]
+SRCS = [os.path.join(HERE, f) for f in ("kernels.hip", "decode_fused.hip", "sample.hip")]
 DEPS = SRCS + [os.path.join(HERE, "bf16_common.h")]
 OUT = os.path.join(HERE, "_hip_ops.so")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]

@@ -177,3 +177,88 @@ def test_native_library_is_loaded(ops):
     assert os.path.exists(path)
     with open("/proc/self/maps") as f:
         assert "_hip_ops.so" in f.read()
+
+
+def _ref_probs(logits_row: torch.Tensor, T: float, k: int, p: float) -> torch.Tensor:
+    """fp32 reference of the sampler's distribution: softmax(z / T) after
+    top-k (ties at the k-th value kept) and top-p (the largest tokens until
+    their mass reaches p, the crossing token included)."""
+    z = logits_row.float() / T
+    keep = torch.ones_like(z, dtype=torch.bool)
+    if 0 < k < z.numel():
+        keep &= z >= torch.topk(z, k).values[-1]
+    if p < 1:
+        zk = torch.where(keep, z, torch.tensor(-float("inf"), device=z.device))
+        pr = torch.softmax(zk, -1)
+        order = torch.argsort(pr, descending=True)
+        before = torch.cumsum(pr[order], 0) - pr[order]
+        kp = torch.zeros_like(keep)
+        kp[order] = before < p
+        keep &= kp
+    zf = torch.where(keep, z, torch.tensor(-float("inf"), device=z.device))
+    return torch.softmax(zf, -1)
+
+
+def _draws(ops, row, T, k, p, n_launch=200, B=64, seed=1234):
+    logits = row.expand(B, -1).contiguous()
+    out = []
+    for j in range(n_launch):
+        ids = torch.zeros(B, dtype=torch.int64, device="cuda")
+        params = torch.tensor([ops.pack_sampling(T, k, p, seed, j * B + b) for b in range(B)],
+                              dtype=torch.int64, device="cuda").T.contiguous()
+        ops.sample_(logits, ids, params)
+        out.append(ids)
+    return torch.cat(out)
+
+
+@cuda
+@pytest.mark.parametrize("T,k,p", [(0.8, 0, 1.0), (1.0, 20, 1.0), (0.7, 0, 0.9), (1.2, 50, 0.8), (1.0, 0, 0.5)])
+def test_sample_matches_reference_distribution(ops, T, k, p):
+    """12,800 draws from one logits row vs the fp32 reference distribution:
+    a chi-square test (bins of expected count >= 5, the rest pooled) at the
+    0.1 % level, and no draw outside the kept set."""
+    from scipy.stats import chi2
+    torch.manual_seed(11)
+    V = 1000
+    row = bf(torch.randn(V, device="cuda") * 2.0)
+    probs = _ref_probs(row, T, k, p).double().cpu()
+    got = _draws(ops, row, T, k, p).cpu()
+    n = got.numel()
+    assert (probs[got] > 0).all(), "a draw outside the top-k / top-p set"
+    counts = torch.bincount(got, minlength=V).double()
+    exp = probs * n
+    big = exp >= 5
+    obs_b, exp_b = counts[big], exp[big]
+    rest_o, rest_e = counts[~big].sum(), exp[~big].sum()
+    stat = ((obs_b - exp_b) ** 2 / exp_b).sum().item()
+    dof = int(big.sum().item()) - 1
+    if rest_e >= 5:
+        stat += ((rest_o - rest_e) ** 2 / rest_e).item()
+        dof += 1
+    assert dof >= 1
+    assert stat < chi2.ppf(0.999, dof), (stat, dof)
+
+
+@cuda
+def test_sample_greedy_rows_untouched_and_seeded_draws_reproduce(ops):
+    torch.manual_seed(3)
+    B, V = 8, 32000
+    logits = bf(torch.randn(B, V, device="cuda"))
+    greedy = ops.argmax(logits)
+    cols = [ops.pack_sampling(0.0, 0, 1.0, 7, b) for b in range(4)] + \
+           [ops.pack_sampling(0.9, 40, 0.95, 7, b) for b in range(4)]
+    params = torch.tensor(cols, dtype=torch.int64, device="cuda").T.contiguous()
+    a = greedy.clone()
+    ops.sample_(logits, a, params)
+    assert torch.equal(a[:4], greedy[:4])  # T = 0: the fused argmax stands, bit-exact
+    b = greedy.clone()
+    ops.sample_(logits, b, params)
+    assert torch.equal(a, b)  # same seed and counters: the same draws
+    # top_k = 1 is greedy whatever the temperature (a unique maximum per row)
+    logits[torch.arange(B), torch.arange(B) * 1000 + 17] = 12.0
+    greedy = ops.argmax(logits)
+    one = torch.tensor([ops.pack_sampling(1.5, 1, 1.0, 9, b) for b in range(B)], dtype=torch.int64,
+                       device="cuda").T.contiguous()
+    c = torch.zeros(B, dtype=torch.int64, device="cuda")
+    ops.sample_(logits, c, one)
+    assert torch.equal(c, greedy)
