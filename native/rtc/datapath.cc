@@ -33,7 +33,7 @@ Lane::Lane(const char* name) {
     for (int sig : {SIGINT, SIGTERM, SIGHUP, SIGQUIT, SIGUSR1, SIGUSR2, SIGPIPE}) sigaddset(&mask, sig);
     pthread_sigmask(SIG_BLOCK, &mask, nullptr);
     pthread_setname_np(pthread_self(), n.c_str());
-    profiler::register_thread(n[n.size() - 1] == 'x' ? 90 : 91);  // tx / rx lanes in profiles
+    profiler::register_thread(n.find("-tx") != std::string::npos ? 90 : 91);  // T90 / T91 in profiles
     run();
   });
 }

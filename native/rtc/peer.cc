@@ -487,6 +487,16 @@ void PeerConnection::start_sctp() {
     auto s = w.lock();
     return s && s->dtls_ ? double(s->dtls_->lane_rx_batches()) : 0.0;
   });
+  metrics::gauge_fn("tunnel_dtls_lane_datagrams", [w] {
+    auto s = w.lock();
+    auto* st = s && s->dtls_ ? s->dtls_->tx_lane_state() : nullptr;
+    return st ? double(st->datagrams.load()) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_dtls_lane_gso_msgs", [w] {
+    auto s = w.lock();
+    auto* st = s && s->dtls_ ? s->dtls_->tx_lane_state() : nullptr;
+    return st ? double(st->gso_msgs.load()) : 0.0;
+  });
   metrics::gauge_fn("tunnel_dtls_lane_send_drops", [w] {
     auto s = w.lock();
     auto* st = s && s->dtls_ ? s->dtls_->tx_lane_state() : nullptr;

