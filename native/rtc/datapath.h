@@ -112,6 +112,27 @@ struct TxBatch {
   int gather(const Rec& r, iovec* out, int max) const;
 };
 
+// Finished TX batches travel back to the association thread for reuse, so
+// their buffers are allocated once and never freed across threads.
+class TxBatchPool {
+ public:
+  std::shared_ptr<TxBatch> get() {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (free_.empty()) return std::make_shared<TxBatch>();
+    auto b = std::move(free_.back());
+    free_.pop_back();
+    return b;
+  }
+  void put(std::shared_ptr<TxBatch> b) {  // any thread; b already cleared
+    std::lock_guard<std::mutex> lk(mu_);
+    if (free_.size() < 64) free_.push_back(std::move(b));
+  }
+
+ private:
+  std::mutex mu_;
+  std::vector<std::shared_ptr<TxBatch>> free_;
+};
+
 // Application records of one receive burst, decrypted in place by the lane.
 struct RxBatch {
   struct Rec {

@@ -678,7 +678,8 @@ void DtlsTransport::enable_lanes(std::function<bool(TxTarget&)> target) {
   if (tx_lane_ || !lanes_possible() || !datapath_enabled()) return;
   tx_target_ = std::move(target);
   tx_state_ = std::make_shared<TxLaneState>();
-  tx_pend_ = std::make_shared<TxBatch>();
+  tx_pool_ = std::make_shared<TxBatchPool>();
+  tx_pend_ = tx_pool_->get();
   tx_lane_ = std::make_unique<Lane>("p2pt-dtls-tx");
   rx_lane_ = std::make_unique<Lane>("p2pt-dtls-rx");
   LOG_DEBUG(kT, "DTLS crypto lanes on (inline below %zu bytes)", datapath_inline_bytes());
@@ -720,13 +721,13 @@ void DtlsTransport::commit_tx() {
   }
   if (!lane_fd_ || lane_fd_->src != t.fd) lane_fd_ = std::make_shared<LaneFd>(t.fd);
   auto b = std::move(tx_pend_);
-  tx_pend_ = std::make_shared<TxBatch>();
-  tx_pend_->arena.reserve(b->arena.capacity());
-  tx_pend_->pieces.reserve(b->pieces.capacity());
-  tx_pend_->recs.reserve(b->recs.capacity());
+  tx_pend_ = tx_pool_->get();
   lane_tx_batches_++;
-  tx_lane_->submit([b, st = tx_state_, k = keys_, fd = lane_fd_, to = t.to, co = t.coalesce] {
+  tx_lane_->submit([b = std::move(b), st = tx_state_, k = keys_, fd = lane_fd_, to = t.to, co = t.coalesce,
+                    pool = tx_pool_]() mutable {
     st->run(*b, *k, fd->fd, to, co);
+    b->clear();  // the body references go here, once the records are sent
+    pool->put(std::move(b));
   });
 }
 

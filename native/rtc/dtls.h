@@ -169,6 +169,7 @@ class DtlsTransport : public std::enable_shared_from_this<DtlsTransport> {
   std::shared_ptr<LaneFd> lane_fd_;
   std::function<bool(TxTarget&)> tx_target_;
   std::shared_ptr<TxBatch> tx_pend_;
+  std::shared_ptr<TxBatchPool> tx_pool_;
   RxBatch rx_pend_;
   int rx_outstanding_ = 0;
   uint64_t lane_tx_batches_ = 0, lane_rx_batches_ = 0, inline_tx_batches_ = 0;

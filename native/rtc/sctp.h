@@ -134,6 +134,7 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
 
  private:
   struct Chunk;     // outbound DATA fragment
+  struct BodyRef;   // a message body shared by its fragments
   struct InChunk;   // inbound DATA fragment awaiting cum-ack
   SctpAssociation(Reactor& r, SctpConfig cfg, PacketOut out);
 
@@ -196,13 +197,17 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
     uint16_t ssn;
     uint8_t hlen = 0;
     uint8_t hdr[kMsgHdrMax];
-    Bytes body;      // message = hdr[0, hlen) ++ body
+    Bytes body;      // message = hdr[0, hlen) ++ body (moved into `ref` at the first fragment)
     size_t len;
     size_t off = 0;  // bytes already fragmented
+    BodyRef* ref = nullptr;
   };
   Chunk* new_chunk();
   void free_chunk(Chunk* c);
+  BodyRef* new_ref(Bytes body);
+  void unref(BodyRef* b);
   std::vector<Chunk*> chunk_free_;
+  std::vector<BodyRef*> ref_free_;
   std::deque<Msg> sendq_;
   std::deque<Msg> sendq_pri_;  // single-chunk priority messages (send_framed(..., priority))
   std::map<uint16_t, uint16_t> next_ssn_;
