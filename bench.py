@@ -6,7 +6,10 @@ Per rank (one rank per GPU of the node; torch.distributed.run launches N > 1):
 a mock OpenAI upstream serving the reference workload (tmp/mock_llm.py: 5 SSE
 tokens 100 ms apart, then a stop event and [DONE]; HTTP/1.0, no
 Content-Length), the local signal server, ``tunnel serve`` and ``tunnel proxy``
-(native C++; WebRTC data channel over the host's interfaces by default).
+(native C++; WebRTC data channel over the host's interfaces by default, on the
+1200-byte SCTP path a reference webrtc-rs peer negotiates — ``--mtu jumbo``
+takes this repo's same-host 16 KiB extension instead, and an untimed jumbo
+point is reported beside the headline as ``jumbo_rank0``).
 A *step* = one streamed completion on each of S concurrent keep-alive client
 connections (S = 8 for the headline). ``value`` = whole-job tunneled
 requests/s (weak scaling: S streams per GPU).
@@ -57,6 +60,11 @@ def parse():
     ap.add_argument("--tokens", type=int, default=5)
     ap.add_argument("--topology", choices=["node", "independent"], default="node",
                     help="N > 1: one tunnel fronting every rank's upstream (node) or one tunnel per rank")
+    ap.add_argument("--mtu", choices=["std", "jumbo"], default="std",
+                    help="std: the 1200-byte SCTP path a reference (webrtc-rs) peer negotiates (headline); jumbo: "
+                         "this repo's same-host 16 KiB extension (a=x-p2pt-jumbo)")
+    ap.add_argument("--no-jumbo-extra", action="store_true",
+                    help="skip the untimed jumbo-path point reported beside a std headline")
     ap.add_argument("--out", default=None, help="also write the JSON line here")
     return ap.parse_args()
 
@@ -155,10 +163,11 @@ def main():
     drive = rank == 0 or not node  # ranks that run a tunnel and a load generator
     streams = a.streams * (world if node else 1)
     tun = None
+    log_env = {"RUST_LOG": "warn,tunnel::serve=info,tunnel::proxy=info,tunnel::transport=info,tunnel::rtc=info"}
+    mtu_flags = ["--no-jumbo-loopback"] if a.mtu == "std" and a.transport == "webrtc" else []
+    upstreams = ",".join(f"http://127.0.0.1:{p}" for p in ups)
     if drive:
-        tun = Tunnel(",".join(f"http://127.0.0.1:{p}" for p in ups), transport=a.transport,
-                     env={"RUST_LOG": "warn,tunnel::serve=info,tunnel::proxy=info,tunnel::transport=info,"
-                                      "tunnel::rtc=info"})
+        tun = Tunnel(upstreams, transport=a.transport, env=log_env, serve_extra=mtu_flags, proxy_extra=mtu_flags)
         tun.start(timeout=60)
 
     def barrier():
@@ -202,6 +211,20 @@ def main():
             if "WebRTC connection established" in line:
                 path = line.split(" via ", 1)[-1]
         tun.stop()
+    # Untimed extra: the same headline load on the same-host jumbo path.
+    jumbo = None
+    if drive and a.mtu == "std" and a.transport == "webrtc" and not a.no_jumbo_extra:
+        with Tunnel(upstreams, transport=a.transport, env=log_env) as tj:
+            loadgen(tj.proxy_port, streams, max(1, a.warmup))
+            r = loadgen(tj.proxy_port, streams, a.steps)
+            jp = ""
+            for line in tj.serve.lines:
+                if "WebRTC connection established" in line:
+                    jp = line.split(" via ", 1)[-1]
+        d = curve[str(a.streams)]
+        jumbo = {"path": jp, "tunneled_req_s": r["req_s"], "p50_ttft_ms": r["p50_ttft_ms"],
+                 "p99_ttft_ms": r["p99_ttft_ms"], "added_p50_ttft_ms": r["p50_ttft_ms"] - d["direct_p50_ttft_ms"],
+                 "errors": r["errors"]}
     barrier()  # every upstream stays up until the driving rank is done
     mock.stop()
 
@@ -209,11 +232,13 @@ def main():
     errors = head["errors"]
     dt = dt_wall
     added = curve[str(a.streams)]["added_p50_ttft_ms"] if drive else 0.0
+    added_p99 = (curve[str(a.streams)]["tunneled_p99_ttft_ms"] - curve[str(a.streams)]["direct_p99_ttft_ms"]
+                 if drive else 0.0)
     if dist:
         import torch
-        t = torch.tensor([dt, added], dtype=torch.float64)
+        t = torch.tensor([dt, added, added_p99], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt, added = float(t[0].item()), float(t[1].item())
+        dt, added, added_p99 = float(t[0].item()), float(t[1].item()), float(t[2].item())
         r = torch.tensor([requests, errors], dtype=torch.float64)
         dist.all_reduce(r, op=dist.ReduceOp.SUM)
         requests, errors = int(r[0].item()), int(r[1].item())
@@ -241,13 +266,16 @@ def main():
                                 if node else f"{world} tunnel(s) x {a.streams} multiplexed streams"),
                 "topology": "node" if node else ("independent" if world > 1 else "single"),
                 "transport": a.transport,
+                "mtu": a.mtu if a.transport == "webrtc" else "n/a",
                 "path_rank0": path,
             },
             "added_p50_ttft_ms": added,
+            "added_p99_ttft_ms": added_p99,
             "p50_ttft_ms": head["p50_ttft_ms"],
             "p99_ttft_ms": head["p99_ttft_ms"],
             "errors": errors,
             "curve_rank0": curve,
+            "jumbo_rank0": jumbo,
         }
         line = json.dumps(out)
         print(line, flush=True)
