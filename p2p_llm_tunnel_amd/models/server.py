@@ -21,6 +21,14 @@ profiles/bench_gpu_upstream_r01.json.)
   POST /v1/completions       (same, "prompt" instead of "messages")
   POST /api/generate         (Ollama NDJSON stream)
 
+Sampling: temperature / top_p / seed (and the common top_k extension) from an
+OpenAI request, or "options" of an Ollama one, drawn on device after the LM
+head (ops.sample_, sample.hip: top-k and top-p by radix select, Gumbel-max
+draw); temperature 0 — the default unless --default-temperature — keeps the
+fused LM head's greedy argmax. Parameters that would change the output and are
+not implemented (n > 1, penalties, logit_bias, stop sequences, logprobs,
+Ollama's repeat_penalty, mirostat, ...) are answered with 400.
+
 Two model sources:
 
 * random-init (``--config tiny|small|micro``, the benchmark default): byte-level
@@ -36,6 +44,7 @@ from __future__ import annotations
 import argparse
 import asyncio
 import json
+import os
 import queue
 import socket
 import sys
@@ -46,18 +55,87 @@ import uuid
 import torch
 
 
+class Sampling:
+    """How a request picks its tokens: temperature (0 = greedy argmax, the
+    fused LM head's own result), then top-k (0 = off) and top-p (1 = off),
+    drawn on device by ``ops.sample_`` (sample.hip) from a per-request seed
+    and the token's index, so a fixed seed replays the same completion."""
+    __slots__ = ("temperature", "top_k", "top_p", "seed")
+
+    def __init__(self, temperature: float = 0.0, top_k: int = 0, top_p: float = 1.0, seed: int | None = None):
+        self.temperature = float(temperature)
+        self.top_k = int(top_k)
+        self.top_p = float(top_p)
+        self.seed = int.from_bytes(os.urandom(8), "little") >> 1 if seed is None else int(seed) & ((1 << 63) - 1)
+
+    @property
+    def greedy(self) -> bool:
+        return not self.temperature >= 1e-4 or self.top_k == 1  # the kernel's own greedy rule (+ top-1)
+
+    def column(self, counter: int) -> list[int]:
+        from p2p_llm_tunnel_amd.ops import pack_sampling
+        return pack_sampling(0.0 if self.greedy else self.temperature, self.top_k, self.top_p, self.seed, counter)
+
+
+class SamplingError(ValueError):
+    """A request asks for sampling this server does not implement (answered with 400)."""
+
+
+def _number(src: dict, key: str, lo: float, hi: float, default, integer=False, lo_open=False):
+    v = src.get(key)
+    if v is None:
+        return default
+    if isinstance(v, bool) or not isinstance(v, (int, float)) or (integer and isinstance(v, float) and not v.is_integer()):
+        raise SamplingError(f"{key} must be {'an integer' if integer else 'a number'}, got {v!r}")
+    if not (lo < v if lo_open else lo <= v) or v > hi:
+        raise SamplingError(f"{key} must be in {'(' if lo_open else '['}{lo}, {hi}], got {v!r}")
+    return int(v) if integer else float(v)
+
+
+# Parameters that would change which tokens come out and that this server
+# does not implement: neutral values pass, anything else is refused instead of
+# being silently ignored.
+_OPENAI_NEUTRAL = {"n": (1,), "best_of": (1,), "presence_penalty": (0, 0.0), "frequency_penalty": (0, 0.0),
+                   "logprobs": (False, 0), "top_logprobs": (0,), "logit_bias": ({},), "stop": ([], "")}
+_OLLAMA_NEUTRAL = {"repeat_penalty": (1, 1.0), "presence_penalty": (0, 0.0), "frequency_penalty": (0, 0.0),
+                   "mirostat": (0,), "tfs_z": (1, 1.0), "typical_p": (1, 1.0), "min_p": (0, 0.0), "stop": ([], "")}
+
+
+def sampling_params(body: dict, ollama: bool, default_temperature: float = 0.0) -> Sampling:
+    """Sampling of an OpenAI request (top-level temperature / top_p / seed, and
+    the common top_k extension) or an Ollama one ("options"). Raises
+    SamplingError for values out of range or parameters not implemented."""
+    src = body.get("options", {}) if ollama else body
+    if src is None:
+        src = {}
+    if not isinstance(src, dict):
+        raise SamplingError("options must be an object")
+    for key, neutral in (_OLLAMA_NEUTRAL if ollama else _OPENAI_NEUTRAL).items():
+        if key in src and src[key] is not None and not any(src[key] == x and type(src[key]) is type(x)
+                                                            for x in neutral):
+            raise SamplingError(f"{key}={src[key]!r} is not supported by this server")
+    if not ollama and "stop" in src and src["stop"] not in (None, [], ""):
+        raise SamplingError("stop sequences are not supported by this server")
+    t = _number(src, "temperature", 0.0, 100.0, default_temperature)
+    top_p = _number(src, "top_p", 0.0, 1.0, 1.0, lo_open=True)
+    top_k = _number(src, "top_k", 0, 1 << 30, 0, integer=True)
+    seed = _number(src, "seed", -(1 << 63), (1 << 64) - 1, None, integer=True)
+    return Sampling(t, top_k, top_p, seed)
+
+
 class Request:
     """A generation request. Tokens go to ``out`` (a queue ending with None)
     unless ``batched`` is set: then the engine's ``deliver`` hook receives them
     together with every other batched request's tokens of the same step."""
 
-    def __init__(self, prompt_ids: list[int], max_new: int, batched: bool = False):
+    def __init__(self, prompt_ids: list[int], max_new: int, batched: bool = False, sampling: Sampling | None = None):
         self.prompt = prompt_ids
         self.max_new = max_new
         self.out: queue.Queue = queue.Queue()
         self.generated = 0
         self.cancelled = False
         self.batched = batched
+        self.sampling = sampling or Sampling()
         self.state = None  # front-end bookkeeping for batched requests
 
 
@@ -65,15 +143,16 @@ class _StepBuf:
     """Host staging of one in-flight step (two alternate: step k+1 is planned
     and launched while step k runs). Rows: token (prompt rows), position,
     slot, decode flag, slot to record the sampled id under (scratch for rows
-    that emit nothing)."""
+    that emit nothing), then the sampler's column per row (rows 5-9:
+    temperature bits, top_k, top_p bits, seed, counter; temperature 0 = greedy)."""
 
     def __init__(self, rows: int, cuda: bool):
-        self.h_in = torch.zeros((5, rows), dtype=torch.int64, pin_memory=cuda)
+        self.h_in = torch.zeros((10, rows), dtype=torch.int64, pin_memory=cuda)
         self.np = self.h_in.numpy()
         self.h_out = torch.zeros(rows, dtype=torch.int64, pin_memory=cuda)
         self.ev = torch.cuda.Event() if cuda else None
         self.n = 0
-        self.emits = []  # (row, req, finished)
+        self.emits = []  # (row, req, finished, token index)
 
 
 class Engine:
@@ -133,10 +212,14 @@ class Engine:
             # one per staging buffer of the pair, so a step is one replay.
             sizes = [small_rows] + ([rows] if rows > small_rows else [])
             self._bufs = {R: [_StepBuf(R, cuda), _StepBuf(R, cuda)] for R in sizes}
-            self._d_in = {R: torch.zeros((5, R), dtype=torch.int64, device=self.device) for R in sizes}
+            self._d_in = {R: torch.zeros((10, R), dtype=torch.int64, device=self.device) for R in sizes}
+            # Steps where some row samples replay a graph with the sampler
+            # kernel after the fused step; all-greedy steps one without it.
             for R in sizes:
                 for par in (0, 1):
-                    self._graphs[(R, par)] = self._capture(self._bufs[R][par], R, 0 if R == small_rows else max_batch)
+                    for smp in (False, True):
+                        self._graphs[(R, par, smp)] = self._capture(self._bufs[R][par], R,
+                                                                    0 if R == small_rows else max_batch, smp)
         else:
             self._bufs = {rows: [_StepBuf(rows, cuda), _StepBuf(rows, cuda)]}
         self.max_batch = max_batch
@@ -216,25 +299,31 @@ class Engine:
             s = self.slots[i]
             s["gen"] += 1
             fin = s["gen"] >= s["req"].max_new or s["pos"] >= max_seq - 1
-            emits.append((r, s["req"], fin))
+            emits.append((r, s["req"], fin, s["gen"] - 1))  # the token's index: the sampler's counter
             if fin:
                 done.append(i)
         for i in done:
             self.slots[i] = None
         return rows, emits
 
-    def _step_body(self, b: _StepBuf, R: int, emit_rows: int):
+    def _step_body(self, b: _StepBuf, R: int, emit_rows: int, sample: bool = False):
         """The captured step: staging -> device, token gather, fused step,
-        last-token scatter, ids -> pinned staging."""
+        (the sampler over the emitting rows' logits,) last-token scatter, ids
+        -> pinned staging."""
         d = self._d_in[R]
         d.copy_(b.h_in, non_blocking=True)
         tok = torch.where(d[3] != 0, self._d_last[d[2]], d[0])
         S = self.model.cfg.max_seq
-        ids, _ = self.model._decode_impl(tok, d[1].to(torch.int32), (0, S - 1), S, d[2].to(torch.int32), emit_rows)
+        ids, logits = self.model._decode_impl(tok, d[1].to(torch.int32), (0, S - 1), S, d[2].to(torch.int32),
+                                              emit_rows)
+        if sample:
+            from p2p_llm_tunnel_amd import ops
+            n = emit_rows or R
+            ops.sample_(logits[:n], ids[:n], d[5:10])
         self._d_last.index_copy_(0, d[4], ids)
         b.h_out.copy_(ids, non_blocking=True)
 
-    def _capture(self, b: _StepBuf, R: int, emit_rows: int):
+    def _capture(self, b: _StepBuf, R: int, emit_rows: int, sample: bool = False):
         scratch = self.model.scratch_slot
         b.np[:] = 0
         b.np[2, :] = scratch  # warm-up and capture touch the scratch slot only
@@ -243,11 +332,11 @@ class Engine:
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.no_grad(), torch.cuda.stream(side):
             for _ in range(2):  # allocator + kernel warm-up outside capture
-                self._step_body(b, R, emit_rows)
+                self._step_body(b, R, emit_rows, sample)
         torch.cuda.current_stream(self.device).wait_stream(side)
         graph = torch.cuda.CUDAGraph()
         with torch.no_grad(), torch.cuda.graph(graph):
-            self._step_body(b, R, emit_rows)
+            self._step_body(b, R, emit_rows, sample)
         torch.cuda.synchronize(self.device)
         return graph
 
@@ -266,6 +355,12 @@ class Engine:
         h[2, :n] = [r[0] for r in rows]
         h[3, :n] = [r[3] for r in rows]
         h[4, :n] = [r[0] if r[4] else scratch for r in rows]
+        h[5:10, :] = 0  # greedy unless an emitting row samples
+        sample = False
+        for r, req, _, ctr in emits:
+            if not req.sampling.greedy:
+                h[5:10, r] = req.sampling.column(ctr)
+                sample = True
         if n < R:  # padding rows: scratch slot, nothing recorded
             h[0:2, n:R] = 0
             h[2, n:R] = scratch
@@ -273,7 +368,7 @@ class Engine:
             h[4, n:R] = scratch
         b.n, b.emits = n, emits
         if self.use_graph:
-            self._graphs[(R, par)].replay()
+            self._graphs[(R, par, sample)].replay()
         else:  # injected model (tests): the same step, eagerly, on its n rows
             d = b.h_in.to(self.device)
             tok = torch.where(d[3, :n] != 0, self._d_last[d[2, :n]], d[0, :n])
@@ -290,7 +385,7 @@ class Engine:
         if b.ev is not None:
             b.ev.synchronize()  # GIL released: the HTTP thread writes meanwhile
         out = b.h_out[: b.n].tolist() if b.emits else []
-        for r, req, fin in b.emits:
+        for r, req, fin, _ in b.emits:
             if req.cancelled:
                 continue
             self._emit(req, out[r], batch)
@@ -388,9 +483,14 @@ class _Stream:
 class FrontEnd:
     """HTTP/1.1 server on one asyncio thread (see the module docstring)."""
 
-    def __init__(self, engine: Engine, host: str, port: int, model_name: str, tokenizer=None):
+    def __init__(self, engine: Engine, host: str, port: int, model_name: str, tokenizer=None,
+                 default_temperature: float = 0.0):
         self.engine = engine
         self.model_name = model_name
+        # Temperature of requests that give none. 0 (greedy) by default — the
+        # OpenAI API's nominal default is 1 — so unparameterised completions
+        # stay deterministic; --default-temperature sets it.
+        self.default_temperature = default_temperature
         self.tok = tokenizer
         self.eos = tokenizer.eos_ids if tokenizer is not None else frozenset()
         self.loop = asyncio.new_event_loop()
@@ -496,8 +596,8 @@ class FrontEnd:
                 % (status, reason.encode(), ctype.encode(), len(body))) + body
 
     def _json_response(self, obj, status=200) -> bytes:
-        return self._response(status, "application/json", json.dumps(obj).encode(),
-                              "OK" if status == 200 else "Not Found")
+        reason = {200: "OK", 400: "Bad Request", 404: "Not Found"}.get(status, "Error")
+        return self._response(status, "application/json", json.dumps(obj).encode(), reason)
 
     async def _conn(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter):
         sock = writer.get_extra_info("socket")
@@ -591,10 +691,15 @@ class FrontEnd:
             return True
         ollama = path == "/api/generate"
         kind = "ollama" if ollama else ("chat" if "chat" in path else "text")
+        try:
+            sampling = sampling_params(req_body, ollama, self.default_temperature)
+        except SamplingError as e:
+            writer.write(self._json_response({"error": {"message": str(e), "type": "invalid_request_error"}}, 400))
+            return True
         stream = bool(req_body.get("stream", ollama))
         rid = ("chatcmpl-" if kind == "chat" else "cmpl-") + uuid.uuid4().hex[:12]
         prompt = _prompt_ids(req_body, self.tok)
-        req = Request(prompt, max(1, min(max_new, 1024)), batched=True)
+        req = Request(prompt, max(1, min(max_new, 1024)), batched=True, sampling=sampling)
         st = _Stream(writer, stream, kind, rid, name, self.tok.detokenizer(prompt) if self.tok is not None else None)
         req.state = st
         if stream:
@@ -607,7 +712,7 @@ class FrontEnd:
 
 def start_server(host="127.0.0.1", port=0, device="cuda:0", config="tiny", max_batch=8, model_name=None,
                  engine: Engine | None = None, checkpoint: str | None = None, max_seq: int | None = None,
-                 tokenizer=None):
+                 tokenizer=None, default_temperature: float = 0.0):
     """Engine + HTTP front-end; returns (server, port, engine). ``server.shutdown()``
     stops the HTTP side, ``engine.stop()`` the GPU side. ``checkpoint``: serve a
     Hugging Face Llama checkpoint directory (weights + tokenizer) instead of
@@ -623,7 +728,8 @@ def start_server(host="127.0.0.1", port=0, device="cuda:0", config="tiny", max_b
         engine = Engine(device=device, max_batch=max_batch, model=model)
         model_name = model_name or os.path.basename(os.path.normpath(checkpoint))
     engine = engine or Engine(device=device, config=config, max_batch=max_batch)
-    srv = FrontEnd(engine, host, port, model_name or f"p2pt-{config}", tokenizer=tok)
+    srv = FrontEnd(engine, host, port, model_name or f"p2pt-{config}", tokenizer=tok,
+                   default_temperature=default_temperature)
     return srv, srv.server_address[1], engine
 
 
@@ -642,6 +748,7 @@ def _replicas(a) -> int:
                "--device", f"cuda:{i}", "--config", a.config, "--max-batch", str(a.max_batch)]
         if a.checkpoint:
             cmd += ["--checkpoint", a.checkpoint] + (["--max-seq", str(a.max_seq)] if a.max_seq else [])
+        cmd += ["--default-temperature", str(a.default_temperature)]
         procs.append(subprocess.Popen(cmd))
     ups = ",".join(f"http://{a.host}:{base + i}" for i in range(a.gpus))
     print(f"{a.gpus} inference endpoints; use: tunnel serve --upstream {ups}", flush=True)
@@ -674,11 +781,14 @@ def main(argv=None):
                     "min(max_position_embeddings, 8192))")
     ap.add_argument("--gpus", type=int, default=0,
                     help="spawn one endpoint per GPU (cuda:0..N-1) on consecutive ports instead of serving here")
+    ap.add_argument("--default-temperature", type=float, default=0.0,
+                    help="temperature of requests that set none (0: greedy; requests may set temperature, top_p, "
+                         "top_k, seed)")
     a = ap.parse_args(argv)
     if a.gpus > 0:
         raise SystemExit(_replicas(a))
     srv, port, engine = start_server(a.host, a.port, a.device, a.config, a.max_batch, checkpoint=a.checkpoint,
-                                     max_seq=a.max_seq)
+                                     max_seq=a.max_seq, default_temperature=a.default_temperature)
     print(f"inference endpoint on http://{a.host}:{port} ({a.checkpoint or a.config}, {a.device})", flush=True)
     try:
         threading.Event().wait()

@@ -40,7 +40,7 @@ def lib() -> ctypes.CDLL:
         _LIB.p2pt_decode_attention.argtypes = [vp, vp, vp, vp, vp, vp, i, i, i, i, i, i, i, f, vp]
         _LIB.p2pt_argmax.argtypes = [vp, vp, i, i, vp]
         _LIB.p2pt_skinny_gemm.argtypes = [vp, vp, vp, i, i, i, vp]
-        _LIB.p2pt_sample.argtypes = [vp, vp, vp, i, i, vp]
+        _LIB.p2pt_sample.argtypes = [vp, vp, vp, i, i, i, vp]
         _LIB.p2pt_llama_ws_bytes.argtypes = [ctypes.POINTER(LlamaDims)]
         _LIB.p2pt_llama_ws_bytes.restype = ctypes.c_size_t
         _LIB.p2pt_llama_decode.argtypes = [ctypes.POINTER(LlamaDims), ctypes.POINTER(vp), vp, vp, vp, vp, vp, i, i,
@@ -205,18 +205,18 @@ def sample_(logits: torch.Tensor, ids: torch.Tensor, params: torch.Tensor) -> to
     """In-place stochastic sampling (sample.hip): rows of bf16 ``logits`` [B, V]
     whose temperature is > 0 get ``ids[b]`` replaced by a draw from
     softmax(logits / T) after top-k and top-p filtering; greedy rows (T <= 0)
-    keep the id already there. ``params``: int64 [5, >= B] — float32 bits of
-    T, top_k (<= 0 off), float32 bits of top_p (>= 1 off), seed, counter
-    (see ``pack_sampling``)."""
+    keep the id already there. ``params``: int64 [5, >= B] (contiguous; column
+    b for row b) — float32 bits of T, top_k (<= 0 off), float32 bits of top_p
+    (>= 1 off), seed, counter (see ``pack_sampling``)."""
     _check(logits, torch.bfloat16, "logits")
     _check(ids, torch.int64, "ids", logits.device)
     _check(params, torch.int64, "params", logits.device)
     if logits.dim() != 2 or ids.shape != (logits.shape[0],) or params.dim() != 2 or params.shape[0] != 5:
-        raise ValueError("need logits [B, V], ids [B], params [5, B]")
+        raise ValueError("need logits [B, V], ids [B], params [5, >= B]")
     B, V = logits.shape
-    if params.shape[1] != B:
-        raise ValueError("params must have one column per row")
-    _ok(lib().p2pt_sample(_p(logits), _p(ids), _p(params), B, V, _stream(logits)), "sample")
+    if params.shape[1] < B:
+        raise ValueError("params need a column per row")
+    _ok(lib().p2pt_sample(_p(logits), _p(ids), _p(params), B, params.shape[1], V, _stream(logits)), "sample")
     return ids
 
 

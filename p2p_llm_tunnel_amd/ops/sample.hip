@@ -17,7 +17,7 @@
 //   Rows with T <= 0 keep the greedy id already in `ids` (the fused LM head's
 //   argmax): greedy decoding stays bit-exact and costs one early-exit wave.
 //
-// params: int64 [5, B] — float32 bits of T, top_k (<= 0: off), float32 bits
+// params: int64 [5, ld] — float32 bits of T, top_k (<= 0: off), float32 bits
 // of top_p (>= 1: off), seed, counter (the request's token index, so each
 // draw of a request uses fresh noise and a fixed seed replays the same text).
 #include "bf16_common.h"
@@ -112,8 +112,9 @@ __device__ __forceinline__ void find_bucket(const T* hist, T need, int* digit_ou
 }
 
 __global__ __launch_bounds__(kThreads) void k_sample(const uint16_t* __restrict__ logits, int64_t* __restrict__ ids,
-                                                     const int64_t* __restrict__ params, int B, int V) {
+                                                     const int64_t* __restrict__ params, int ld, int V) {
   const int row = blockIdx.x;
+  const int B = ld;  // params rows are `ld` long (a view of the engine's staging block)
   const float T = __uint_as_float(uint32_t(params[row]));
   if (!(T >= 1e-4f)) return;  // greedy row (or T -> 0, whose limit is greedy): the fused argmax stands
   int64_t k = params[B + row];
@@ -214,11 +215,12 @@ __global__ __launch_bounds__(kThreads) void k_sample(const uint16_t* __restrict_
 extern "C" {
 
 // ids: int64 [B] (in: greedy ids; out: samples for rows with T > 0);
-// params: int64 [5, B]; logits: bf16 [B, V] rows contiguous.
-int p2pt_sample(const void* logits, int64_t* ids, const int64_t* params, int B, int V, void* stream) {
-  if (B <= 0 || V <= 0) return int(hipErrorInvalidValue);
+// params: int64 [5, ld] (ld >= B, row k of parameter p at params[p * ld + k]);
+// logits: bf16 [B, V] rows contiguous.
+int p2pt_sample(const void* logits, int64_t* ids, const int64_t* params, int B, int ld, int V, void* stream) {
+  if (B <= 0 || V <= 0 || ld < B) return int(hipErrorInvalidValue);
   hipLaunchKernelGGL(k_sample, dim3(B), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
-                     static_cast<const uint16_t*>(logits), ids, params, B, V);
+                     static_cast<const uint16_t*>(logits), ids, params, ld, V);
   return int(hipGetLastError());
 }
 

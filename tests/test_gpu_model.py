@@ -272,3 +272,67 @@ def test_64_row_prefill_chunk_matches_sequential():
     last = l2[T - 1].float()
     assert (last - l1[0].float()).abs().max().item() <= 1e-6 + 0.01 * l1.float().abs().max().item()
     assert int(last.argmax()) == int(l1[0].float().argmax())
+
+
+@cuda
+def test_engine_sampling_on_device():
+    """Requests with sampling parameters draw on device inside the captured
+    step (ops.sample_): a fixed seed replays the same completion, different
+    seeds give different ones, temperature 0 and top_k 1 are the greedy
+    tokens bit for bit, and greedy neighbours in the same step are unaffected."""
+    from p2p_llm_tunnel_amd.models.server import Engine, Request, Sampling
+    eng = Engine(device="cuda:0", config="micro", max_batch=4)
+    try:
+        pr = list(b"sampling prompt")
+
+        def run(sampling, n=24):
+            r = eng.submit(Request(pr, n, sampling=sampling))
+            return list(iter(r.out.get, None))
+
+        greedy = run(Sampling())
+        assert run(Sampling(temperature=0.0, seed=1)) == greedy
+        assert run(Sampling(temperature=1.3, top_k=1, seed=2)) == greedy
+        a = run(Sampling(temperature=1.0, top_p=0.95, seed=42))
+        assert run(Sampling(temperature=1.0, top_p=0.95, seed=42)) == a  # replayable
+        b = run(Sampling(temperature=1.0, top_p=0.95, seed=43))
+        assert a != b and a != greedy
+        # batched together: a sampled request beside a greedy one
+        rs = [eng.submit(Request(pr, 24, sampling=Sampling(temperature=1.0, top_p=0.95, seed=42))),
+              eng.submit(Request(pr, 24))]
+        both = [list(iter(r.out.get, None)) for r in rs]
+        assert both == [a, greedy]
+    finally:
+        eng.stop()
+
+
+@cuda
+def test_endpoint_honours_and_validates_sampling_parameters():
+    from p2p_llm_tunnel_amd.models.server import start_server
+    srv, port, engine = start_server(device="cuda:0", config="micro", max_batch=4)
+    try:
+        def post(path, body):
+            c = http.client.HTTPConnection("127.0.0.1", port, timeout=60)
+            c.request("POST", path, body=json.dumps(body), headers={"content-type": "application/json"})
+            r = c.getresponse()
+            return r.status, r.read()
+
+        chat = {"max_tokens": 12, "messages": [{"role": "user", "content": "hi"}]}
+        st, greedy = post("/v1/chat/completions", chat)
+        assert st == 200
+        st, s1 = post("/v1/chat/completions", dict(chat, temperature=0.9, top_p=0.9, top_k=40, seed=7))
+        st2, s2 = post("/v1/chat/completions", dict(chat, temperature=0.9, top_p=0.9, top_k=40, seed=7))
+        assert st == st2 == 200 and s1 == s2
+        txt = lambda b: json.loads(b)["choices"][0]["message"]["content"]  # noqa: E731
+        assert txt(s1) != txt(greedy)
+        st, o1 = post("/api/generate", {"prompt": "hi", "stream": False, "num_predict": 12,
+                                        "options": {"temperature": 0.9, "seed": 7}})
+        assert st == 200 and json.loads(o1)["done"]
+        for bad in ({"temperature": -1}, {"top_p": 0}, {"top_k": 2.5}, {"n": 2}, {"presence_penalty": 0.3},
+                    {"logit_bias": {"5": 1}}, {"stop": ["\n"]}):
+            st, body = post("/v1/chat/completions", dict(chat, **bad))
+            assert st == 400, (bad, body)
+        st, _ = post("/api/generate", {"prompt": "hi", "options": {"repeat_penalty": 1.1}})
+        assert st == 400
+    finally:
+        engine.stop()
+        srv.shutdown()
