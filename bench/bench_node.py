@@ -15,13 +15,17 @@ would run on tokio's multi-threaded runtime (reference tunnel/src/main.rs:18,
 serve.rs:131-137); here it measures the tunnel's worker threads
 (``--workers``, native/tunnel/workers.h).
 
-    python bench/bench_node.py --streams 64,256,512 --workers 0,4
+Each point alternates direct and tunneled runs of --seconds (10) each,
+--reps (5) times, and reports median and min-max ("rows"; raw runs in "runs").
+
+    python bench/bench_node.py --streams 256,512,1024 --workers auto [--seconds 10 --reps 5]
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import statistics
 import subprocess
 import sys
 import time
@@ -69,13 +73,21 @@ def row(kind, r):
                                            "p99_itl_ms", "p999_itl_ms", "max_itl_ms", "errors")}
 
 
+def summary(vals):
+    v = sorted(x for x in vals if x is not None)
+    if not v:
+        return None
+    return {"median": round(statistics.median(v), 4), "min": round(v[0], 4), "max": round(v[-1], 4)}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--streams", default="64,256,512")
+    ap.add_argument("--streams", default="256,512,1024")
     ap.add_argument("--upstreams", type=int, default=8)
     ap.add_argument("--interval-us", type=int, default=1000)
     ap.add_argument("--tokens", type=int, default=64)
-    ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--seconds", type=float, default=10.0, help="length of each run (repeated steps)")
+    ap.add_argument("--reps", type=int, default=5, help="alternating direct / tunneled repetitions per point")
     ap.add_argument("--workers", default="auto", help="comma list of tunnel --workers values to compare")
     ap.add_argument("--lg-threads", type=int, default=4)
     ap.add_argument("--transport", default="webrtc")
@@ -87,13 +99,10 @@ def main():
     counts = [int(x) for x in a.streams.split(",") if x]
     mocks, ports = start_mocks(a.upstreams, a.interval_us, a.tokens)
     res = {"host": os.uname().nodename, "time": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
-           "upstreams": a.upstreams, "interval_us": a.interval_us, "tokens": a.tokens, "steps": a.steps,
-           "transport": a.transport, "cpus": os.cpu_count(), "rows": []}
+           "upstreams": a.upstreams, "interval_us": a.interval_us, "tokens": a.tokens, "seconds_per_run": a.seconds,
+           "reps": a.reps, "transport": a.transport, "cpus": os.cpu_count(), "runs": [], "rows": []}
+    dur = ["--duration-s", str(a.seconds)]
     try:
-        direct = {}
-        for s in counts:
-            direct[s] = loadgen(ports, s, a.steps, a.lg_threads)
-            print(json.dumps({"direct": s, **row("direct", direct[s])}), file=sys.stderr, flush=True)
         for w in [x for x in a.workers.split(",") if x]:
             extra = ["--workers", w] + [x for x in a.extra.split() if x]
             env = {"RUST_LOG": "warn,tunnel::serve=info,tunnel::proxy=info"}
@@ -105,19 +114,33 @@ def main():
             with Tunnel(up, transport=a.transport, serve_extra=extra, proxy_extra=extra, env=env) as t:
                 for s in counts:
                     loadgen([t.proxy_port], s, 1, a.lg_threads, warmup=0)
-                    c0 = (cpu_s(t.serve.popen.pid), cpu_s(t.proxy.popen.pid))
-                    tr = loadgen([t.proxy_port], s, a.steps, a.lg_threads)
-                    c1 = (cpu_s(t.serve.popen.pid), cpu_s(t.proxy.popen.pid))
-                    d = direct[s]
-                    r = {"workers": w, "streams": s, **row("tunneled", tr), **row("direct", d),
-                         "events_ratio": tr["events_s"] / d["events_s"] if d["events_s"] else None,
-                         "added_p50_ttft_ms": tr["p50_ttft_ms"] - d["p50_ttft_ms"],
-                         "added_p99_ttft_ms": tr["p99_ttft_ms"] - d["p99_ttft_ms"],
-                         "added_p99_itl_ms": tr["p99_itl_ms"] - d["p99_itl_ms"],
-                         "serve_cpu_s": round(c1[0] - c0[0], 3), "proxy_cpu_s": round(c1[1] - c0[1], 3),
-                         "seconds": tr["seconds"]}
-                    res["rows"].append(r)
-                    print(json.dumps(r), file=sys.stderr, flush=True)
+                    for rep in range(a.reps):
+                        d = loadgen(ports, s, 1 << 20, a.lg_threads, extra=dur)
+                        c0 = (cpu_s(t.serve.popen.pid), cpu_s(t.proxy.popen.pid))
+                        tr = loadgen([t.proxy_port], s, 1 << 20, a.lg_threads, extra=dur)
+                        c1 = (cpu_s(t.serve.popen.pid), cpu_s(t.proxy.popen.pid))
+                        r = {"workers": w, "streams": s, "rep": rep, **row("tunneled", tr), **row("direct", d),
+                             "events_ratio": tr["events_s"] / d["events_s"] if d["events_s"] else None,
+                             "added_p50_ttft_ms": tr["p50_ttft_ms"] - d["p50_ttft_ms"],
+                             "added_p99_ttft_ms": tr["p99_ttft_ms"] - d["p99_ttft_ms"],
+                             "added_p99_itl_ms": tr["p99_itl_ms"] - d["p99_itl_ms"],
+                             "serve_cpu_s": round(c1[0] - c0[0], 3), "proxy_cpu_s": round(c1[1] - c0[1], 3),
+                             "seconds": tr["seconds"], "direct_seconds": d["seconds"]}
+                        res["runs"].append(r)
+                        print(json.dumps(r), file=sys.stderr, flush=True)
+        keys = ["events_ratio", "tunneled_events_s", "direct_events_s", "added_p50_ttft_ms", "added_p99_ttft_ms",
+                "tunneled_p99_ttft_ms", "direct_p99_ttft_ms", "tunneled_p99_itl_ms", "direct_p99_itl_ms",
+                "added_p99_itl_ms", "serve_cpu_s", "proxy_cpu_s"]
+        for w in [x for x in a.workers.split(",") if x]:
+            for s in counts:
+                runs = [r for r in res["runs"] if r["workers"] == w and r["streams"] == s]
+                row_ = {"workers": w, "streams": s, "reps": len(runs),
+                        "errors": sum(r["tunneled_errors"] + r["direct_errors"] for r in runs),
+                        "seconds_per_run": summary([r["seconds"] for r in runs])}
+                for k in keys:
+                    row_[k] = summary([r[k] for r in runs])
+                res["rows"].append(row_)
+                print(json.dumps({"summary": row_}), file=sys.stderr, flush=True)
     finally:
         for m in mocks:
             m.stop()
