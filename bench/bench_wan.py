@@ -50,7 +50,8 @@ def result(p, timeout=900):
 SCTP_GAUGES = ("tunnel_sctp_fast_retransmits", "tunnel_sctp_t3_expirations", "tunnel_sctp_tlp_probes",
                "tunnel_sctp_rack_marks", "tunnel_sctp_random_loss_events", "tunnel_sctp_cwnd_bytes",
                "tunnel_sctp_rto_us", "tunnel_sctp_packets_sent", "tunnel_sctp_dup_copies",
-               "tunnel_sctp_hystart_exits", "tunnel_sctp_random_loss_cuts")
+               "tunnel_sctp_hystart_exits", "tunnel_sctp_random_loss_cuts", "tunnel_sctp_congestion_cuts",
+               "tunnel_sctp_over_bdp_losses")
 
 
 def scrape(port):

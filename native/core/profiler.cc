@@ -3,7 +3,9 @@
 #include <dlfcn.h>
 #include <pthread.h>
 #include <signal.h>
+#include <sys/syscall.h>
 #include <sys/time.h>
+#include <time.h>
 #include <ucontext.h>
 #include <unistd.h>
 
@@ -36,6 +38,33 @@ std::string g_path;
 thread_local uintptr_t t_stack_lo = 0, t_stack_hi = 0;
 thread_local uint64_t t_tag = 0;  // 0 = main reactor thread, k = worker k
 std::atomic<bool> g_dumped{false};
+int g_hz = 0;  // sampling rate once started
+
+// One CPU-time timer per registered thread (CLOCK_THREAD_CPUTIME_ID, signal
+// aimed at that thread): a process-wide ITIMER_PROF is capped by the kernel
+// tick and lands on whichever thread happens to run, which left a busy
+// association thread with a few hundred samples for a multi-second run.
+struct ThreadTimer {
+  timer_t id{};
+  bool armed = false;
+  void arm() {
+    if (armed || !g_hz) return;
+    sigevent ev = {};
+    ev.sigev_notify = SIGEV_THREAD_ID;
+    ev.sigev_signo = SIGPROF;
+    ev._sigev_un._tid = pid_t(syscall(SYS_gettid));
+    if (timer_create(CLOCK_THREAD_CPUTIME_ID, &ev, &id) != 0) return;
+    itimerspec it = {};
+    it.it_interval.tv_nsec = 1000000000L / g_hz;
+    it.it_value = it.it_interval;
+    timer_settime(id, 0, &it, nullptr);
+    armed = true;
+  }
+  ~ThreadTimer() {
+    if (armed) timer_delete(id);
+  }
+};
+thread_local ThreadTimer t_timer;
 
 inline bool on_stack(uintptr_t p) { return p >= t_stack_lo && p + 16 <= t_stack_hi && (p & 7) == 0; }
 
@@ -114,6 +143,7 @@ void register_thread(int tag) {
     t_stack_hi = t_stack_lo + sz;
     pthread_attr_destroy(&attr);
   }
+  t_timer.arm();
 }
 
 bool start_from_env() {
@@ -122,9 +152,8 @@ bool start_from_env() {
   g_path = p;
   if (size_t at = g_path.find("%p"); at != std::string::npos) g_path.replace(at, 2, std::to_string(getpid()));
   int hz = 2000;
-  if (const char* h = getenv("TUNNEL_PROFILE_HZ")) hz = std::max(10, atoi(h));
+  if (const char* h = getenv("TUNNEL_PROFILE_HZ")) hz = std::min(20000, std::max(10, atoi(h)));
   g_slots = new Slot[kSlots];
-  register_thread(0);
   // Resolve dladdr's lazy state before the first signal.
   Dl_info di;
   dladdr(reinterpret_cast<void*>(&start_from_env), &di);
@@ -133,18 +162,15 @@ bool start_from_env() {
   sa.sa_flags = SA_SIGINFO | SA_RESTART;
   sigemptyset(&sa.sa_mask);
   sigaction(SIGPROF, &sa, nullptr);
-  struct itimerval it = {};
-  it.it_interval.tv_usec = 1000000 / hz;
-  it.it_value = it.it_interval;
-  setitimer(ITIMER_PROF, &it, nullptr);
+  g_hz = hz;
+  register_thread(0);  // the main reactor; other threads arm theirs in register_thread()
   atexit(dump);
   return true;
 }
 
 void dump() {
   if (!g_slots || g_dumped.exchange(true)) return;
-  struct itimerval off = {};
-  setitimer(ITIMER_PROF, &off, nullptr);
+  g_hz = 0;  // late samples still land in the table; the dump below reads it once
   FILE* f = fopen(g_path.c_str(), "w");
   if (!f) return;
   fprintf(f, "# samples %llu dropped %llu\n", static_cast<unsigned long long>(g_samples.load()),

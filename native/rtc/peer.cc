@@ -471,6 +471,14 @@ void PeerConnection::start_sctp() {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().random_loss_cuts) : 0.0;
   });
+  metrics::gauge_fn("tunnel_sctp_congestion_cuts", [w] {
+    auto s = w.lock();
+    return s && s->sctp_ ? double(s->sctp_->stats().congestion_cuts) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_sctp_over_bdp_losses", [w] {
+    auto s = w.lock();
+    return s && s->sctp_ ? double(s->sctp_->stats().over_bdp_losses) : 0.0;
+  });
   metrics::gauge_fn("tunnel_sctp_random_loss_events", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().random_loss_events) : 0.0;

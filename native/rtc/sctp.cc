@@ -967,6 +967,7 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
     sendlog_.pop_front();
   }
   if (cum_advanced) assoc_errors_ = 0;
+  dr_on_sack(cum, newly_acked, flight_before + cfg_.mtu >= cwnd_, now);
   // Congestion control (RFC 9260 §7.2.1-7.2.2).
   const bool long_path = min_rtt_us_ >= kLongPathUs;
   if (cwnd_ <= ssthresh_ && !hs_done_ && long_path && !fast_recovery_) hystart(cum, rtt_sample);
@@ -987,12 +988,18 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
       partial_acked_ += newly_acked;
       if (partial_acked_ >= cwnd_ && flight_before + cfg_.mtu >= cwnd_) {
         partial_acked_ -= cwnd_;
-        cwnd_ += cfg_.mtu;
+        // One MTU per round trip (RFC 9260 §7.2.2) while the path shows a
+        // queue; with none, cwnd / 64 per round trip (Scalable TCP's rate):
+        // after a random loss on a 1 Gbit/s x 20 ms path (2,000 packets of
+        // BDP) one MTU per round trip would take 30 s to reopen the window.
+        const uint64_t rtt = std::max<uint64_t>(srtt_us_, 1);
+        const bool queue = min_rtt_us_ && rtt > min_rtt_us_ + rtt / 8;
+        cwnd_ += queue ? cfg_.mtu : std::max(cfg_.mtu, cwnd_ / 64);
       }
     }
   }
+  if (new_fast && !fast_recovery_) cwnd_bypass_ = 1;
   if (new_fast && !fast_recovery_) {
-    cwnd_bypass_ = 1;
     hs_done_ = true;  // HyStart++ covers only the initial slow start
     // Loss response after TCP Veno: the backlog this association keeps in the
     // path's queues is cwnd * (SRTT - min RTT) / SRTT. A loss with (almost) no
@@ -1004,41 +1011,23 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
     // Random loss also means isolated loss: a policer or a shallow drop-tail
     // queue overrun by cwnd drops a run of packets with no standing queue in
     // front of it, which is congestion all the same.
-    bool random_loss = backlog < 3 * cfg_.mtu + cwnd_ / 16 && marked_now <= 2;
-    if (random_loss) stats_.random_loss_events++;
-    // A random loss keeps cwnd (TUNNEL_SCTP_RANDOM_BETA_PCT, default 100):
-    // with no standing queue it says nothing about congestion, and a cut per
-    // random loss capped bulk at the loss rate's AIMD equilibrium (emulated
-    // 50 ms / 2 %: 0.54 MB/s at 0.9, 1.67 MB/s kept; the SSE tails and the
-    // clean rows, whose queue-overflow losses read as congestion, unchanged).
-    // Losses with a backlog still cut by 0.3. Sustained loss still backs off
-    // multiplicatively (RFC 5033): every kRandomStreakCut-th random-loss
-    // episode in a row (episodes less than 8 SRTT apart) cuts by 0.15, so a
-    // path whose losses only look random converges instead of being overdriven.
-    static const int random_beta_pct = [] {
-      const char* e = getenv("TUNNEL_SCTP_RANDOM_BETA_PCT");
-      return e && *e ? std::clamp(atoi(e), 50, 100) : 100;
-    }();
-    if (last_loss_us_ && now - last_loss_us_ > 8 * rtt) random_streak_ = 0;
-    last_loss_us_ = now;
-    size_t keep = cwnd_ * 7 / 10;
-    if (random_loss) {
-      keep = cwnd_ * size_t(random_beta_pct) / 100;
-      if (++random_streak_ >= kRandomStreakCut) {
-        random_streak_ = 0;
-        keep = std::min(keep, cwnd_ * 85 / 100);
-        stats_.random_loss_cuts++;
-      }
-    } else {
-      random_streak_ = 0;
-    }
-    ssthresh_ = std::max(keep, 4 * cfg_.mtu);
-    cwnd_ = ssthresh_;
-    partial_acked_ = 0;
-    fast_recovery_ = true;
-    fast_recovery_exit_ = next_tsn_ - 1;
+    // And a window already past what the path has delivered in recent rounds
+    // (1.125 x max delivery rate x min RTT) is overrunning a bottleneck whose
+    // queue is too shallow to show as delay: congestion too. A random loss
+    // leaves delivery rising with cwnd (emulated 20 ms, 40 Mbit/s behind a
+    // 6 KiB queue: 3-6 % of packets dropped while such losses kept cwnd).
+    const size_t bdp = dr_bdp();
+    const bool over_bdp = bdp && cwnd_ > bdp + bdp / 8 + 2 * cfg_.mtu;
+    // "Isolated": at most 2 chunks, or 1 % of the window, newly found lost
+    // by this SACK (at 0.5 % random loss a 1 Gbit/s x 20 ms window loses
+    // several chunks per round trip, and reading that as congestion held bulk
+    // near 10 % of the link).
+    const size_t isolated = std::max<size_t>(2, flight_before / (100 * cfg_.mtu));
+    bool random_loss = backlog < 3 * cfg_.mtu + cwnd_ / 8 && marked_now <= isolated && !over_bdp;
+    if (!(random_loss && random_episode_)) loss_response(random_loss, over_bdp, now);
   }
   if (fast_recovery_ && !tsn_lt(cum, fast_recovery_exit_)) fast_recovery_ = false;
+  if (random_episode_ && !tsn_lt(cum, random_exit_)) random_episode_ = false;
   peer_rwnd_ = a_rwnd > flight_size_ ? a_rwnd - flight_size_ : 0;
   if (cum_advanced) tlp_count_ = 0;
   if (inflight_.empty()) {
@@ -1050,6 +1039,55 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
     arm_tlp();
   }
   maybe_finish_shutdown();
+}
+
+// A new loss episode: cwnd and ssthresh after it (handle_sack classified it).
+void SctpAssociation::loss_response(bool random_loss, bool over_bdp, uint64_t now) {
+  const uint64_t rtt = std::max<uint64_t>(srtt_us_, 1);
+  if (random_loss) stats_.random_loss_events++;
+  // A random loss keeps cwnd (TUNNEL_SCTP_RANDOM_BETA_PCT, default 100):
+  // with no standing queue it says nothing about congestion, and a cut per
+  // random loss capped bulk at the loss rate's AIMD equilibrium (emulated
+  // 50 ms / 2 %: 0.54 MB/s at 0.9, 1.67 MB/s kept; the SSE tails and the
+  // clean rows, whose queue-overflow losses read as congestion, unchanged).
+  // Losses with a backlog still cut by 0.3. Sustained loss still backs off
+  // multiplicatively (RFC 5033): every kRandomStreakCut-th random-loss
+  // episode in a row (episodes less than 8 SRTT apart) cuts by 0.15, so a
+  // path whose losses only look random converges instead of being overdriven.
+  static const int random_beta_pct = [] {
+    const char* e = getenv("TUNNEL_SCTP_RANDOM_BETA_PCT");
+    return e && *e ? std::clamp(atoi(e), 50, 100) : 100;
+  }();
+  if (last_loss_us_ && now - last_loss_us_ > 8 * rtt) random_streak_ = 0;
+  last_loss_us_ = now;
+  size_t keep = cwnd_ * 7 / 10;
+  if (random_loss) {
+    keep = cwnd_ * size_t(random_beta_pct) / 100;
+    if (++random_streak_ >= kRandomStreakCut) {
+      random_streak_ = 0;
+      keep = std::min(keep, cwnd_ * 85 / 100);
+      stats_.random_loss_cuts++;
+    }
+  } else {
+    random_streak_ = 0;
+    stats_.congestion_cuts++;
+    if (over_bdp) stats_.over_bdp_losses++;
+  }
+  ssthresh_ = std::max(keep, 4 * cfg_.mtu);
+  cwnd_ = ssthresh_;
+  partial_acked_ = 0;
+  if (random_loss) {
+    // No recovery period: cwnd keeps growing while the losses are repaired
+    // (at 0.5 % loss and 1 Gbit/s a new loss comes every few ms, so a
+    // recovery period per loss froze cwnd for good). Further losses within
+    // this window's round trip are the same episode.
+    random_episode_ = true;
+    random_exit_ = next_tsn_ - 1;
+  } else {
+    fast_recovery_ = true;
+    fast_recovery_exit_ = next_tsn_ - 1;
+    random_episode_ = false;
+  }
 }
 
 // Tail-loss probe (after RFC 8985 TLP): with data outstanding and no SACK for
@@ -1229,6 +1267,38 @@ bool SctpAssociation::send_framed(uint16_t stream, uint32_t ppid, const uint8_t*
 // start) for kCssRounds rounds, then congestion avoidance takes over with
 // ssthresh = cwnd. A round whose minimum falls back below the CSS baseline
 // was a false alarm and resumes slow start.
+void SctpAssociation::dr_on_sack(uint32_t cum, size_t newly_acked, bool cwnd_limited, uint64_t now) {
+  if (!dr_active_) {
+    if (!newly_acked) return;
+    dr_active_ = true;
+    dr_end_ = next_tsn_ - 1;
+    dr_start_us_ = now;
+    dr_bytes_ = 0;
+    dr_limited_ = cwnd_limited;
+    return;
+  }
+  dr_bytes_ += newly_acked;
+  dr_limited_ = dr_limited_ || cwnd_limited;
+  if (tsn_lt(cum, dr_end_)) return;
+  // Round over: app-limited rounds (the sender never filled cwnd) say nothing
+  // about the path and are not recorded.
+  if (dr_limited_ && now > dr_start_us_) {
+    dr_rates_[dr_next_] = dr_bytes_ * 1000000 / (now - dr_start_us_);
+    dr_next_ = (dr_next_ + 1) % kDrRounds;
+  }
+  dr_end_ = next_tsn_ - 1;
+  dr_start_us_ = now;
+  dr_bytes_ = 0;
+  dr_limited_ = cwnd_limited;
+}
+
+size_t SctpAssociation::dr_bdp() const {
+  uint64_t mx = 0;
+  for (uint64_t r : dr_rates_) mx = std::max(mx, r);
+  if (!mx || !min_rtt_us_) return 0;
+  return size_t(mx * min_rtt_us_ / 1000000);
+}
+
 void SctpAssociation::hystart(uint32_t cum, uint64_t rtt_sample) {
   if (!hs_round_ || !tsn_lt(cum, hs_window_end_)) {  // a round ended
     hs_last_min_ = hs_cur_min_;
@@ -1288,6 +1358,7 @@ void SctpAssociation::on_t3() {
   cwnd_ = cfg_.mtu;
   partial_acked_ = 0;
   fast_recovery_ = false;
+  random_episode_ = false;
   hs_done_ = true;
   hs_css_ = false;
   rto_us_ = std::min<uint64_t>(rto_us_ * 2, cfg_.rto_max_ms * 1000);

@@ -58,6 +58,8 @@ struct SctpStats {
   uint64_t retransmits = 0, fast_retransmits = 0, t3_expirations = 0;
   uint64_t tlp_probes = 0, rack_marks = 0, random_loss_events = 0;
   uint64_t random_loss_cuts = 0;  // sustained random loss: the periodic 0.85 cut
+  uint64_t congestion_cuts = 0;   // loss episodes read as congestion (0.7 cut)
+  uint64_t over_bdp_losses = 0;   // ... of them because cwnd was past the delivery-rate BDP
   uint64_t hystart_exits = 0;     // initial slow starts ended by HyStart++ (rising delay)
   uint64_t dup_copies_sent = 0;  // redundant copies of small messages (lossy paths)
   uint64_t early_deliveries = 0;  // messages handed up ahead of a TSN gap (another stream's loss)
@@ -244,6 +246,21 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   static constexpr uint64_t kLongPathUs = 5000;  // base RTT from which a path counts as long (WAN)
   static constexpr int kHsSamples = 8, kCssRounds = 5;
   static constexpr size_t kCssDivisor = 4;
+  // Delivery rate per round trip (bytes acknowledged between a round's first
+  // SACK and the SACK covering the last TSN sent when it began), windowed max
+  // over the last kDrRounds rounds in which the sender was cwnd-limited:
+  // max rate x min RTT estimates the path's BDP (dr_bdp()).
+  static constexpr int kDrRounds = 10;
+  bool random_episode_ = false;  // a random-loss episode (no recovery period) is open until random_exit_
+  uint32_t random_exit_ = 0;
+  bool dr_active_ = false, dr_limited_ = false;
+  uint32_t dr_end_ = 0;
+  uint64_t dr_start_us_ = 0, dr_bytes_ = 0;
+  uint64_t dr_rates_[kDrRounds] = {};  // bytes per second
+  int dr_next_ = 0;
+  void dr_on_sack(uint32_t cum, size_t newly_acked, bool cwnd_limited, uint64_t now);
+  void loss_response(bool random_loss, bool over_bdp, uint64_t now);
+  size_t dr_bdp() const;
   bool hs_done_ = false, hs_css_ = false, hs_round_ = false;
   int hs_samples_ = 0, hs_css_rounds_ = 0;
   uint32_t hs_window_end_ = 0;

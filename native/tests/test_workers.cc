@@ -112,13 +112,66 @@ TEST(scheduler_interactive_lane_goes_first) {
   CHECK_EQ(ch->sent.size(), size_t(3));
   CHECK_EQ(ch->sent[0].first, 0u);  // control first
   CHECK_EQ(ch->sent[1].first, 3u);  // then the token, ahead of both bulk streams
-  CHECK(ch->sent[2].first == 1u || ch->sent[2].first == 2u);
+  CHECK_EQ(ch->sent[2].first, 1u);  // then the oldest bulk stream
   CHECK_EQ(s.stream_queued(3), size_t(0));
   for (int i = 0; i < 7; i++) {
     ch->buffered = 0;
     s.pump();
   }
   CHECK_EQ(ch->sent.size(), size_t(10));
-  for (size_t i = 3; i < 10; i++) CHECK(ch->sent[i].first != ch->sent[i - 1].first);  // bulk streams alternate
+  // Within their first kFifoBytes bulk streams go oldest first: stream 1
+  // finishes before stream 2 starts.
+  for (size_t i = 3; i < 10; i++) CHECK_EQ(ch->sent[i].first, i < 6 ? 1u : 2u);
+  CHECK_EQ(s.queued_bytes(), size_t(0));
+}
+
+// Past kFifoBytes a stream drops to round-robin: a newer stream's first
+// kFifoBytes go ahead of it, then the two alternate.
+TEST(scheduler_bulk_fifo_then_round_robin) {
+  auto ch = std::make_shared<FakeChannel>();
+  FrameScheduler s(ch, 1000);
+  ch->buffered = 5000;
+  Bytes big = Bytes::copy(std::string(60000, 'b'));
+  const int n = 45;  // 2.7 MB per stream
+  for (int i = 0; i < n; i++) s.send(proto::make_body(proto::MsgType::ResBody, 7, big));
+  for (int i = 0; i < n; i++) s.send(proto::make_body(proto::MsgType::ResBody, 9, big));
+  for (int i = 0; i < 2 * n; i++) {
+    ch->buffered = 0;
+    s.pump();
+  }
+  CHECK_EQ(ch->sent.size(), size_t(2 * n));
+  const size_t fifo_frames = (FrameScheduler::kFifoBytes + 60004) / 60005;
+  size_t i = 0;
+  for (; i < fifo_frames; i++) CHECK_EQ(ch->sent[i].first, 7u);
+  for (; i < 2 * fifo_frames; i++) CHECK_EQ(ch->sent[i].first, 9u);
+  for (; i + 1 < size_t(2 * (n - fifo_frames)) + 2 * fifo_frames; i++)
+    CHECK(ch->sent[i].first != ch->sent[i + 1].first);  // round-robin
+  CHECK_EQ(s.queued_bytes(), size_t(0));
+}
+
+// A stream whose queue ran dry keeps its attained service: past kFifoBytes it
+// stays behind a younger stream's first bytes after producing again; a
+// finished stream is forgotten.
+TEST(scheduler_fifo_survives_idle_gaps) {
+  auto ch = std::make_shared<FakeChannel>();
+  FrameScheduler s(ch, 1000);
+  Bytes big = Bytes::copy(std::string(60000, 'b'));
+  const int n = int(FrameScheduler::kFifoBytes / 60005) + 2;
+  for (int i = 0; i < n; i++) {
+    s.send(proto::make_body(proto::MsgType::ResBody, 4, big));
+    ch->buffered = 0;
+  }
+  CHECK_EQ(ch->sent.size(), size_t(n));
+  CHECK_EQ(s.queued_bytes(), size_t(0));
+  ch->buffered = 5000;
+  for (int i = 0; i < 3; i++) s.send(proto::make_body(proto::MsgType::ResBody, 4, big));
+  for (int i = 0; i < 3; i++) s.send(proto::make_body(proto::MsgType::ResBody, 6, big));
+  for (int i = 0; i < 6; i++) {
+    ch->buffered = 0;
+    s.pump();
+  }
+  CHECK_EQ(ch->sent.size(), size_t(n + 6));
+  for (size_t i = 0; i < 3; i++) CHECK_EQ(ch->sent[n + i].first, 6u);  // the younger stream's first bytes
+  for (size_t i = 3; i < 6; i++) CHECK_EQ(ch->sent[n + i].first, 4u);
   CHECK_EQ(s.queued_bytes(), size_t(0));
 }

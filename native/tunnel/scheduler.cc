@@ -36,7 +36,8 @@ bool FrameScheduler::stalled_tick() {
 
 std::string FrameScheduler::debug_state() const {
   std::string s = "sched{queued=" + std::to_string(queued_) + " control=" + std::to_string(control_.size()) +
-                  " interactive=" + std::to_string(interactive_.size()) + " bulk=" + std::to_string(bulk_.size()) +
+                  " interactive=" + std::to_string(interactive_.size()) + " fifo=" + std::to_string(fifo_.size()) +
+                  " bulk=" + std::to_string(bulk_.size()) +
                   " streams=" + std::to_string(streams_.size()) + " window=" + std::to_string(window()) +
                   " emitted=" + std::to_string(emitted_) + " pumping=" + std::to_string(int(pumping_)) + "} ";
   return s + (ch_ ? ch_->debug_state() : "");
@@ -44,7 +45,9 @@ std::string FrameScheduler::debug_state() const {
 
 void FrameScheduler::list(uint32_t sid, StreamQ& s) {
   s.listed = true;
-  (s.bytes <= kInteractive ? interactive_ : bulk_).push_back(sid);
+  if (s.bytes <= kInteractive) interactive_.push_back(sid);
+  else if (s.sent < kFifoBytes) fifo_.insert(sid);
+  else bulk_.push_back(sid);
 }
 
 void FrameScheduler::send(proto::Frame f) {
@@ -54,6 +57,7 @@ void FrameScheduler::send(proto::Frame f) {
   size_t win = window();
   ch_->buffered_low_threshold = win / 2;
   if (queued_ == 0 && ch_->buffered_amount() < win) {
+    if (f.stream_id && f.type != proto::MsgType::Credit) remember(f);
     emit(f);
     if (pending_bytes() > high_) was_high_ = true;
     return;
@@ -64,13 +68,64 @@ void FrameScheduler::send(proto::Frame f) {
     control_.push_back(std::move(f));
   } else {
     uint32_t sid = f.stream_id;
-    auto& s = streams_[sid];
+    auto [it, fresh] = streams_.try_emplace(sid);
+    auto& s = it->second;
+    if (fresh) {  // a stream that emptied its queue before keeps its attained service
+      auto sv = sent_.find(sid);
+      if (sv != sent_.end()) {
+        s.sent = sv->second;
+        sent_.erase(sv);
+      }
+    }
     s.q.push_back(std::move(f));
     s.bytes += sz;
     if (!s.listed) list(sid, s);
   }
   if (pending_bytes() > high_) was_high_ = true;
   pump();
+}
+
+bool FrameScheduler::last_frame(const proto::Frame& f) {
+  return f.type == proto::MsgType::ReqEnd || f.type == proto::MsgType::ResEnd || f.type == proto::MsgType::Error ||
+         f.type == proto::MsgType::Cancel;
+}
+
+// A frame sent on the fast path (nothing queued) counts toward its stream's
+// attained service too; small frames are left out (they decide nothing and
+// an SSE token should not pay a map update).
+void FrameScheduler::remember(const proto::Frame& f) {
+  if (last_frame(f)) {
+    if (!sent_.empty()) sent_.erase(f.stream_id);
+  } else if (f.wire_size() > kInteractive) {
+    sent_[f.stream_id] += f.wire_size();
+    if (sent_.size() > kRemember) sent_.erase(sent_.begin());
+  }
+}
+
+// Releases the head frame of a listed stream; false if its queue was empty.
+bool FrameScheduler::release(uint32_t sid, StreamQ& s, std::unordered_map<uint32_t, StreamQ>::iterator it) {
+  s.listed = false;
+  if (s.q.empty()) {
+    streams_.erase(it);
+    return false;
+  }
+  proto::Frame f = std::move(s.q.front());
+  s.q.pop_front();
+  size_t sz = f.wire_size();
+  s.bytes -= sz;
+  s.sent += sz;
+  queued_ -= sz;
+  if (s.q.empty()) {
+    if (!last_frame(f)) {  // attained service outlives an empty queue while the stream may still produce
+      sent_[sid] = s.sent;
+      if (sent_.size() > kRemember) sent_.erase(sent_.begin());
+    }
+    streams_.erase(it);
+  } else {
+    list(sid, s);  // re-queued behind the others, in the lane its backlog now calls for
+  }
+  emit(f);
+  return true;
 }
 
 // Releases the head frame of the first stream in `lane`; false if the lane is empty.
@@ -80,21 +135,19 @@ bool FrameScheduler::pop_from(std::deque<uint32_t>& lane) {
     lane.pop_front();
     auto it = streams_.find(sid);
     if (it == streams_.end()) continue;
-    StreamQ& s = it->second;
-    s.listed = false;
-    if (s.q.empty()) {
-      streams_.erase(it);
-      continue;
-    }
-    proto::Frame f = std::move(s.q.front());
-    s.q.pop_front();
-    size_t sz = f.wire_size();
-    s.bytes -= sz;
-    queued_ -= sz;
-    if (s.q.empty()) streams_.erase(it);
-    else list(sid, s);  // re-queued behind the others, in the lane its backlog now calls for
-    emit(f);
-    return true;
+    if (release(sid, it->second, it)) return true;
+  }
+  return false;
+}
+
+// The oldest bulk stream still within its first kFifoBytes.
+bool FrameScheduler::pop_fifo() {
+  while (!fifo_.empty()) {
+    uint32_t sid = *fifo_.begin();
+    fifo_.erase(fifo_.begin());
+    auto it = streams_.find(sid);
+    if (it == streams_.end()) continue;
+    if (release(sid, it->second, it)) return true;
   }
   return false;
 }
@@ -114,7 +167,7 @@ void FrameScheduler::pump() {
       progressed = true;
       continue;
     }
-    if (pop_from(interactive_) || pop_from(bulk_)) {
+    if (pop_from(interactive_) || pop_fifo() || pop_from(bulk_)) {
       progressed = true;
       continue;
     }

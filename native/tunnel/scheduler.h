@@ -9,7 +9,14 @@
 //   1. control frames (stream 0: HELLO/AGREE/PING/PONG; CREDIT of any stream);
 //   2. the "interactive" lane: streams with little queued (<= kInteractive
 //      bytes, e.g. an SSE stream with its next token), one frame per turn;
-//   3. the bulk lane: backlogged streams, round-robin one frame per turn.
+//   3. the bulk lane: backlogged streams. A stream's first kFifoBytes go out
+//      oldest stream first (lowest id; ids are handed out in arrival order):
+//      with round-robin, 64 concurrent 1 MB uploads all finished together at
+//      the very end, so the upstream of a store-and-forward hop idled until
+//      then; served in order, each completes in turn and the next hop starts
+//      on it while the rest are still in transit. Past kFifoBytes a stream
+//      goes round-robin, one frame per turn, so a long transfer never holds
+//      the others back for longer than that.
 //
 // So a token waits for at most the channel window plus one frame, never for
 // other streams' queued bodies. Per-stream FIFO order is preserved (the wire
@@ -20,7 +27,9 @@
 
 #include <deque>
 #include <functional>
+#include <map>
 #include <memory>
+#include <set>
 #include <unordered_map>
 
 #include "proto/frame.h"
@@ -31,6 +40,7 @@ namespace p2pt {
 class FrameScheduler {
  public:
   static constexpr size_t kInteractive = 4096;
+  static constexpr uint64_t kFifoBytes = 2u << 20;
 
   explicit FrameScheduler(std::shared_ptr<MessageChannel> ch, size_t window = 64 * 1024);
   ~FrameScheduler();
@@ -69,17 +79,25 @@ class FrameScheduler {
   struct StreamQ {
     std::deque<proto::Frame> q;
     size_t bytes = 0;
+    uint64_t sent = 0;  // bytes released so far (attained service)
     bool listed = false;
   };
   bool emit(const proto::Frame& f);
   void list(uint32_t sid, StreamQ& s);
   bool pop_from(std::deque<uint32_t>& lane);
+  bool pop_fifo();
+  static bool last_frame(const proto::Frame& f);
+  void remember(const proto::Frame& f);
+  static constexpr size_t kRemember = 4096;  // streams whose attained service is kept while their queue is empty
+  bool release(uint32_t sid, StreamQ& s, std::unordered_map<uint32_t, StreamQ>::iterator it);
 
   std::shared_ptr<MessageChannel> ch_;
   size_t window_;
   std::deque<proto::Frame> control_;
   std::unordered_map<uint32_t, StreamQ> streams_;
   std::deque<uint32_t> interactive_, bulk_;
+  std::set<uint32_t> fifo_;  // bulk streams within their first kFifoBytes, oldest (lowest id) first
+  std::map<uint32_t, uint64_t> sent_;  // attained service of open streams whose queue ran dry
   size_t queued_ = 0;
   uint64_t emitted_ = 0;  // frames handed to the channel
   uint64_t wd_emitted_ = 0;

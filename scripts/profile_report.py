@@ -58,6 +58,8 @@ def main():
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--thread", default=None,
                     help="only samples of this thread tag (0 = main reactor, k = worker k; 'workers' = all k > 0)")
+    ap.add_argument("--leaf", default=None,
+                    help="also list the fp-chain callers (frames 2..4) of samples whose leaf contains this text")
     a = ap.parse_args()
     per_thread = collections.Counter()
     stacks = []
@@ -116,6 +118,15 @@ def main():
     print(f"\n{'%':>7}  leaf <- caller")
     for (l, cl), c in leaf_caller.most_common(a.top):
         print(f"{100 * c / total:7.2f}  {l}  <-  {cl}")
+    if a.leaf:
+        chains = collections.Counter()
+        for cnt, fr in stacks:
+            if a.leaf in names[fr[0]]:
+                chain = [names[f][:70] for f in fr[2:5] if not names[f].startswith("?")]
+                chains[" <- ".join(chain) or "?"] += cnt
+        print(f"\n{'%':>7}  callers of leaves matching {a.leaf!r} (fp chain)")
+        for ch, c in chains.most_common(a.top):
+            print(f"{100 * c / total:7.2f}  {ch}")
 
 
 if __name__ == "__main__":
