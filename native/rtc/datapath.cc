@@ -2,7 +2,9 @@
 
 #include <netinet/in.h>
 #include <netinet/udp.h>
+#include <poll.h>
 #include <pthread.h>
+#include <sys/eventfd.h>
 #include <signal.h>
 #include <sys/socket.h>
 #include <unistd.h>
@@ -17,6 +19,9 @@
 
 #ifndef UDP_SEGMENT
 #define UDP_SEGMENT 103
+#endif
+#ifndef UDP_GRO
+#define UDP_GRO 104
 #endif
 
 namespace p2pt::rtc {
@@ -273,6 +278,157 @@ void TxLaneState::run(const TxBatch& b, const RecordKeys& k, int fd, const SockA
   }
 }
 
+// ------------------------------------------------------------------ RX reader
+
+RxReader::RxReader(int fd, const SockAddr& remote, std::shared_ptr<const RecordKeys> keys, Deliver deliver)
+    : fd_(fd), stop_fd_(eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC)), remote_(remote), keys_(std::move(keys)),
+      deliver_(std::move(deliver)) {
+  th_ = std::thread([this] {
+    sigset_t mask;
+    sigemptyset(&mask);
+    for (int sig : {SIGINT, SIGTERM, SIGHUP, SIGQUIT, SIGUSR1, SIGUSR2, SIGPIPE}) sigaddset(&mask, sig);
+    pthread_sigmask(SIG_BLOCK, &mask, nullptr);
+    pthread_setname_np(pthread_self(), "p2pt-udp-rx");
+    profiler::register_thread(92);  // T92 in profiles
+    run();
+  });
+}
+
+RxReader::~RxReader() {
+  stop_.store(true, std::memory_order_release);
+  uint64_t one = 1;
+  if (stop_fd_ >= 0 && ::write(stop_fd_, &one, sizeof one) < 0) {
+  }
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+  }
+  cv_.notify_all();
+  th_.join();
+  if (stop_fd_ >= 0) ::close(stop_fd_);
+}
+
+void RxReader::done() {
+  if (outstanding_.fetch_sub(1, std::memory_order_acq_rel) == kMaxOutstanding) {
+    std::lock_guard<std::mutex> lk(mu_);
+    cv_.notify_one();
+  }
+}
+
+namespace {
+size_t gro_seg(const msghdr* mh) {
+  for (cmsghdr* c = CMSG_FIRSTHDR(const_cast<msghdr*>(mh)); c; c = CMSG_NXTHDR(const_cast<msghdr*>(mh), c))
+    if (c->cmsg_level == SOL_UDP && c->cmsg_type == UDP_GRO) {
+      int v = 0;
+      memcpy(&v, CMSG_DATA(c), sizeof v);
+      return size_t(v);
+    }
+  return 0;
+}
+}  // namespace
+
+// One datagram: all-application-data from the selected remote is opened here;
+// anything else goes to the association thread as it came.
+void RxReader::segment(const RawBufPtr& buf, uint32_t off, uint32_t len, const SockAddr& from, Burst& b) {
+  datagrams.fetch_add(1, std::memory_order_relaxed);
+  uint8_t* p = buf->data.get() + off;
+  bool fast = from == remote_ && len >= kRecHdr;
+  if (fast) {  // every record epoch-1 application data and whole
+    for (size_t o = 0; o < len;) {
+      if (o + kRecHdr > len || p[o] != 23 || rd16(p + o + 3) != 1) {
+        fast = false;
+        break;
+      }
+      const size_t rl = kRecHdr + rd16(p + o + 11);
+      if (o + rl > len) {
+        fast = false;
+        break;
+      }
+      o += rl;
+    }
+  }
+  if (!fast) {
+    raw_datagrams.fetch_add(1, std::memory_order_relaxed);
+    b.raw.push_back(Raw{buf, off, len, from});
+    return;
+  }
+  for (size_t o = 0; o < len;) {
+    uint8_t* rec = p + o;
+    const size_t rl = kRecHdr + rd16(rec + 11);
+    o += rl;
+    RxBatch::Rec r;
+    r.rec = rec;
+    r.len = uint32_t(rl);
+    r.type = rec[0];
+    uint64_t seq = 0;
+    for (int i = 0; i < 6; i++) seq = (seq << 8) | rec[5 + i];
+    r.seq = seq;
+    size_t ptl = 0;
+    r.ok = open_record(*keys_->r, keys_->riv, rec, rl, &r.pt, &ptl);
+    r.ptl = uint32_t(ptl);
+    r.owner = buf;
+    b.opened.bytes += rl;
+    b.opened.recs.push_back(std::move(r));
+    records.fetch_add(1, std::memory_order_relaxed);
+  }
+}
+
+void RxReader::run() {
+  constexpr int kBatch = 32;
+  mmsghdr msgs[kBatch];
+  iovec iovs[kBatch];
+  sockaddr_storage from[kBatch];
+  alignas(cmsghdr) char ctrl[kBatch][CMSG_SPACE(sizeof(int))];
+  RawBufPtr slots[kBatch];
+  pollfd pf[2] = {{fd_.fd, POLLIN, 0}, {stop_fd_, POLLIN, 0}};
+  while (!stop_.load(std::memory_order_acquire)) {
+    if (outstanding_.load(std::memory_order_acquire) >= kMaxOutstanding) {
+      waits.fetch_add(1, std::memory_order_relaxed);
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait_for(lk, std::chrono::milliseconds(5), [this] {
+        return stop_.load(std::memory_order_acquire) || outstanding_.load(std::memory_order_acquire) < kMaxOutstanding;
+      });
+      continue;
+    }
+    if (poll(pf, 2, 100) <= 0 || (pf[1].revents & POLLIN)) continue;  // the loop head sees stop_
+    auto burst = std::make_unique<Burst>();
+    for (int round = 0; round < 8; round++) {
+      for (int i = 0; i < kBatch; i++) {
+        slots[i] = pool_.get();
+        memset(&msgs[i], 0, sizeof msgs[i]);
+        iovs[i].iov_base = slots[i]->data.get();
+        iovs[i].iov_len = 65536;
+        msgs[i].msg_hdr.msg_iov = &iovs[i];
+        msgs[i].msg_hdr.msg_iovlen = 1;
+        msgs[i].msg_hdr.msg_name = &from[i];
+        msgs[i].msg_hdr.msg_namelen = sizeof from[i];
+        msgs[i].msg_hdr.msg_control = ctrl[i];
+        msgs[i].msg_hdr.msg_controllen = sizeof ctrl[i];
+      }
+      const int n = recvmmsg(fd_.fd, msgs, kBatch, MSG_DONTWAIT, nullptr);
+      if (n <= 0) break;
+      for (int i = 0; i < n; i++) {
+        SockAddr a;
+        memcpy(&a.ss, &from[i], msgs[i].msg_hdr.msg_namelen);
+        a.len = msgs[i].msg_hdr.msg_namelen;
+        const uint32_t total = msgs[i].msg_len;
+        const uint32_t seg = uint32_t(gro_seg(&msgs[i].msg_hdr));
+        if (!seg || seg >= total) {
+          segment(slots[i], 0, total, a, *burst);
+        } else {
+          gro_batches.fetch_add(1, std::memory_order_relaxed);
+          for (uint32_t o = 0; o < total; o += seg) segment(slots[i], o, std::min(seg, total - o), a, *burst);
+        }
+      }
+      for (auto& sl : slots) sl.reset();  // the burst holds what it uses
+      if (n < kBatch) break;
+    }
+    if (burst->opened.recs.empty() && burst->raw.empty()) continue;
+    bursts.fetch_add(1, std::memory_order_relaxed);
+    outstanding_.fetch_add(1, std::memory_order_acq_rel);
+    deliver_(std::move(burst));
+  }
+}
+
 size_t datapath_inline_bytes() {
   static const size_t v = [] {
     const char* e = getenv("TUNNEL_DATAPATH_INLINE_BYTES");
@@ -280,6 +436,22 @@ size_t datapath_inline_bytes() {
   }();
   return v;
 }
+
+namespace {
+std::atomic<int> g_rx_reader{-1};  // -1: from the environment
+}
+
+bool rx_reader_enabled() {
+  int v = g_rx_reader.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = getenv("TUNNEL_RX_READER");
+    v = (e && *e == '0') ? 0 : 1;
+    g_rx_reader.store(v, std::memory_order_relaxed);
+  }
+  return v != 0;
+}
+
+void set_rx_reader_enabled(bool on) { g_rx_reader.store(on ? 1 : 0, std::memory_order_relaxed); }
 
 bool datapath_enabled() {
   static const bool v = [] {

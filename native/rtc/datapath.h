@@ -15,10 +15,12 @@
 //       references to the body buffers. The lane seals them into one
 //       contiguous buffer and sends it with sendmmsg + UDP GSO on its own
 //       dup of the socket.
-//   RX: the association thread still reads the socket (recvmmsg); a burst's
-//       application records go to the RX lane, which authenticates and
-//       decrypts them in place; the replay check and hand-off to SCTP run back
-//       on the association thread, in order.
+//   RX: a reader thread owns the selected pair's socket (RxReader): recvmmsg
+//       with GRO, application records authenticated and decrypted in place
+//       there; the replay check and hand-off to SCTP run on the association
+//       thread, in order. Without a reader (relay, emulation, before the pair
+//       is direct) the association thread reads the socket and a burst's
+//       records go to the RX lane instead.
 //
 // Small batches never cross threads: a flush (or receive burst) below
 // kInlineBytes whose lane has nothing outstanding is processed inline, so an
@@ -178,7 +180,55 @@ class TxLaneState {
   bool gso_ok_ = true;
 };
 
+// Socket reader: the selected pair's UDP socket read on a thread of its own
+// (recvmmsg + GRO), application records from the selected remote opened
+// there, everything else (STUN, handshake or alert records, other senders)
+// passed on untouched. A burst goes to the association thread through
+// `deliver`, which must post it (it runs on the reader); the association
+// thread calls done() once it has processed one, and the reader stops
+// reading (the socket buffer holds, then drops) while kMaxOutstanding bursts
+// wait, so a slow association thread never piles up pinned buffers.
+class RxReader {
+ public:
+  struct Raw {
+    RawBufPtr buf;
+    uint32_t off, len;
+    SockAddr from;
+  };
+  struct Burst {
+    RxBatch opened;         // application records, authenticated (ok) or not
+    std::vector<Raw> raw;   // datagrams for the ICE agent / DTLS state machine
+  };
+  using Deliver = std::function<void(std::unique_ptr<Burst>)>;
+  static constexpr int kMaxOutstanding = 4;
+
+  RxReader(int fd, const SockAddr& remote, std::shared_ptr<const RecordKeys> keys, Deliver deliver);
+  ~RxReader();  // stops and joins; bursts already delivered stay valid
+  RxReader(const RxReader&) = delete;
+  RxReader& operator=(const RxReader&) = delete;
+  void done();  // association thread: one delivered burst processed
+
+  std::atomic<uint64_t> bursts{0}, datagrams{0}, records{0}, raw_datagrams{0}, waits{0}, gro_batches{0};
+
+ private:
+  void run();
+  void segment(const RawBufPtr& buf, uint32_t off, uint32_t len, const SockAddr& from, Burst& b);
+  LaneFd fd_;
+  int stop_fd_ = -1;
+  SockAddr remote_;
+  std::shared_ptr<const RecordKeys> keys_;
+  Deliver deliver_;
+  BufPool pool_{65536};
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::atomic<int> outstanding_{0};
+  std::atomic<bool> stop_{false};
+  std::thread th_;
+};
+
 size_t datapath_inline_bytes();  // TUNNEL_DATAPATH_INLINE_BYTES (default 32 KiB)
+bool rx_reader_enabled();        // TUNNEL_RX_READER (default on; 0 = the association thread reads the socket)
+void set_rx_reader_enabled(bool on);  // tests: both receive paths in one process
 bool datapath_enabled();         // TUNNEL_DATAPATH (default on; 0 = everything on the association thread)
 
 }  // namespace p2pt::rtc

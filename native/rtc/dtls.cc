@@ -771,6 +771,10 @@ void DtlsTransport::commit_rx() {
 // replay window (only authenticated records move it), then up the stack.
 void DtlsTransport::rx_done(RxBatch& b) {
   rx_outstanding_--;
+  deliver_opened(b);
+}
+
+void DtlsTransport::deliver_opened(RxBatch& b) {
   if (closed_) return;
   auto self = shared_from_this();
   for (auto& x : b.recs) {

@@ -102,6 +102,10 @@ class DtlsTransport : public std::enable_shared_from_this<DtlsTransport> {
   // lane. End of a receive burst: open its records inline or on the RX lane.
   void commit_tx();
   void commit_rx();
+  // Records opened by the socket reader (RxReader), on this thread, in
+  // receive order: replay check, then up the stack as received records are.
+  void deliver_opened(RxBatch& b);
+  std::shared_ptr<const RecordKeys> record_keys() const { return keys_; }
   const TxLaneState* tx_lane_state() const { return tx_state_.get(); }
   uint64_t lane_tx_batches() const { return lane_tx_batches_; }
   uint64_t lane_rx_batches() const { return lane_rx_batches_; }

@@ -558,6 +558,34 @@ bool IceAgent::direct_target(int* fd, SockAddr* to, size_t* coalesce) const {
   return true;
 }
 
+bool IceAgent::detach_reader(int* fd, int* si, SockAddr* remote) {
+  size_t co;
+  if (detached_ >= 0 || !direct_target(fd, remote, &co)) return false;
+  *si = locals_[sel_local_].sock;
+  detached_ = *si;
+  r_.modify(*fd, 0);
+  return true;
+}
+
+void IceAgent::reattach_reader(int si) {
+  if (detached_ != si) return;
+  detached_ = -1;
+  if (!closed_ && si >= 0 && si < int(socks_.size()) && socks_[si].fd >= 0) {
+    r_.modify(socks_[si].fd, EPOLLIN);
+    on_readable(si);  // whatever arrived in between
+  }
+}
+
+void IceAgent::inject(int si, const SockAddr& from, const RawBufPtr& owner, size_t off, size_t len) {
+  if (closed_ || nat_mode_) return;
+  dispatch_rx(si, from, owner, len, off);
+}
+
+void IceAgent::note_rx() {
+  last_rx_ = Reactor::now_ms();
+  if (state_ == IceState::Disconnected && sel_local_ >= 0) set_state(IceState::Connected);
+}
+
 // Releases the WAN-emulation queue's due datagrams into the send queue (the
 // flush hook that follows the timer sends them).
 void IceAgent::arm_delay_timer() {

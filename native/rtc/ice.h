@@ -125,6 +125,16 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   // DTLS TX lane): false with no pair, a TURN relay, or NAT / WAN / fault
   // emulation, all of which live in this agent's own send path.
   bool direct_target(int* fd, SockAddr* to, size_t* coalesce) const;
+  // An outside reader (the DTLS RX reader, rtc/datapath.h) takes over the
+  // selected direct pair's socket: its reactor reads stop until reattach().
+  // False when direct_target() does not hold.
+  bool detach_reader(int* fd, int* si, SockAddr* remote);
+  void reattach_reader(int si);
+  // From that reader, on this agent's thread: a datagram it did not handle
+  // (STUN, non-application records, other senders), and proof of life for
+  // the ones it did (consent freshness).
+  void inject(int si, const SockAddr& from, const RawBufPtr& owner, size_t off, size_t len);
+  void note_rx();
   // True when both ends of the selected pair are on this host.
   bool selected_same_host() const;
   std::string selected_desc() const;
@@ -241,6 +251,7 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   uint64_t last_keepalive_ = 0;
   uint64_t flush_hook_ = 0;
   bool closed_ = false;
+  int detached_ = -1;  // socket index read by an outside reader
   // Outgoing datagrams for the current batch.
   struct Out {
     int local;

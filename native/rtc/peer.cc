@@ -198,6 +198,39 @@ void PeerConnection::flush() {
   if (ice_) ice_->flush();
 }
 
+void PeerConnection::start_rx_reader() {
+  if (rx_reader_ || closed_ || !dtls_ || !ice_ || !dtls_->lanes_enabled() || !rx_reader_enabled()) return;
+  int fd = -1, si = -1;
+  SockAddr remote;
+  if (!ice_->detach_reader(&fd, &si, &remote)) return;
+  rx_reader_si_ = si;
+  std::weak_ptr<PeerConnection> w = shared_from_this();
+  Reactor* r = &r_;
+  rx_reader_ = std::make_unique<RxReader>(fd, remote, dtls_->record_keys(), [w, r](std::unique_ptr<RxReader::Burst> b) {
+    std::shared_ptr<RxReader::Burst> sb(std::move(b));
+    r->post_threadsafe([w, sb] {
+      if (auto s = w.lock()) s->on_rx_burst(*sb);
+    });
+  });
+  LOG_DEBUG(kT, "UDP socket reader on for %s", remote.str().c_str());
+}
+
+// A burst from the socket reader: opened records up the stack (replay check
+// in DTLS), the rest through the ICE agent as if it had read them.
+void PeerConnection::on_rx_burst(RxReader::Burst& b) {
+  if (rx_reader_) rx_reader_->done();
+  if (closed_) return;
+  auto self = shared_from_this();
+  if (!b.opened.recs.empty()) {
+    if (ice_) ice_->note_rx();
+    if (dtls_) dtls_->deliver_opened(b.opened);
+  }
+  for (auto& raw : b.raw) {
+    if (closed_ || !ice_) break;
+    ice_->inject(rx_reader_si_, raw.from, raw.buf, raw.off, raw.len);
+  }
+}
+
 void PeerConnection::close() {
   if (closed_) return;
   if (sctp_ && sctp_->established()) {
@@ -209,6 +242,7 @@ void PeerConnection::close() {
     if (ice_) ice_->flush();
   }
   closed_ = true;
+  rx_reader_.reset();  // joins the reader; bursts already posted find closed_ set
   if (flush_hook_) r_.remove_flush_hook(flush_hook_);
   flush_hook_ = 0;
   for (auto& kv : channels_) kv.second->set_closed("peer connection closed");
@@ -383,6 +417,7 @@ void PeerConnection::start_sctp() {
     auto s = w.lock();
     return s && s->ice_ && s->ice_->direct_target(&t.fd, &t.to, &t.coalesce);
   });
+  start_rx_reader();
   sctp_ = SctpAssociation::create(r_, sc, [w](const iovec* iov, const Bytes* const* owners, int cnt) {
     auto s = w.lock();
     if (s && s->dtls_) s->dtls_->send(iov, owners, cnt);
@@ -500,6 +535,22 @@ void PeerConnection::start_sctp() {
     auto* st = s && s->dtls_ ? s->dtls_->tx_lane_state() : nullptr;
     return st ? double(st->datagrams.load()) : 0.0;
   });
+  metrics::gauge_fn("tunnel_udp_reader_datagrams", [w] {
+    auto s = w.lock();
+    return s && s->rx_reader_ ? double(s->rx_reader_->datagrams.load()) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_udp_reader_bursts", [w] {
+    auto s = w.lock();
+    return s && s->rx_reader_ ? double(s->rx_reader_->bursts.load()) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_udp_reader_raw", [w] {
+    auto s = w.lock();
+    return s && s->rx_reader_ ? double(s->rx_reader_->raw_datagrams.load()) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_udp_reader_waits", [w] {
+    auto s = w.lock();
+    return s && s->rx_reader_ ? double(s->rx_reader_->waits.load()) : 0.0;
+  });
   metrics::gauge_fn("tunnel_dtls_lane_gso_msgs", [w] {
     auto s = w.lock();
     auto* st = s && s->dtls_ ? s->dtls_->tx_lane_state() : nullptr;
@@ -516,7 +567,8 @@ void PeerConnection::start_sctp() {
   });
   metrics::gauge_fn("tunnel_udp_gro_batches", [w] {
     auto s = w.lock();
-    return s && s->ice_ ? double(s->ice_->gro_batches_) : 0.0;
+    if (!s || !s->ice_) return 0.0;
+    return double(s->ice_->gro_batches_ + (s->rx_reader_ ? s->rx_reader_->gro_batches.load() : 0));
   });
   set_state(PcState::Connected);
   sctp_->connect();

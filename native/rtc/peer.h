@@ -125,6 +125,8 @@ class PeerConnection : public std::enable_shared_from_this<PeerConnection> {
   void set_state(PcState s);
   void fail(const std::string& why);
   void flush();
+  void start_rx_reader();
+  void on_rx_burst(RxReader::Burst& b);
 
   Reactor& r_;
   PcConfig cfg_;
@@ -142,6 +144,11 @@ class PeerConnection : public std::enable_shared_from_this<PeerConnection> {
   uint64_t flush_hook_ = 0;
   size_t mtu_ = 1200;
   bool closed_ = false;
+  // The selected direct pair's socket read off this thread (rtc/datapath.h).
+  std::unique_ptr<RxReader> rx_reader_;
+  int rx_reader_si_ = -1;
+ public:
+  const RxReader* rx_reader() const { return rx_reader_.get(); }
 };
 
 }  // namespace p2pt::rtc
