@@ -1,7 +1,12 @@
 // Transport components in-process: SCTP association pair over a lossy,
 // reordering, duplicating link; DTLS pair; full PeerConnection pair over
 // loopback UDP (ICE + DTLS + SCTP + DCEP).
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <condition_variable>
 #include <functional>
+#include <mutex>
 #include <random>
 
 #include "core/reactor.h"
@@ -517,6 +522,95 @@ TEST(peerconnection_pair_loopback) {
 // threshold are sealed and sent on the DTLS TX lane and opened on the RX lane
 // (rtc/datapath.h) while the association thread runs SCTP; every byte must
 // arrive intact and in order, on the 1200-byte and the jumbo path.
+// The socket reader opens application records from the selected remote on
+// its own thread and passes everything else on untouched: a STUN-looking
+// datagram, a datagram from another sender, a record that fails
+// authentication (handed over with ok = false for the association thread to
+// drop), and a datagram mixing an alert with data.
+TEST(rx_reader_opens_app_records_and_passes_the_rest) {
+  if (!AesGcm::supported()) return;
+  auto keys = std::make_shared<RecordKeys>();
+  auto g = std::make_shared<AesGcm>();
+  uint8_t key[16];
+  for (int i = 0; i < 16; i++) key[i] = uint8_t(i * 11 + 3);
+  CHECK(g->init(key, 16));
+  keys->w = g;
+  keys->r = g;
+  for (int i = 0; i < 4; i++) keys->wiv[i] = keys->riv[i] = uint8_t(0xA0 + i);
+  auto udp = [](SockAddr* bound) {
+    int fd = ::socket(AF_INET, SOCK_DGRAM | SOCK_CLOEXEC, 0);
+    SockAddr a;
+    CHECK(SockAddr::parse("127.0.0.1", 0, a));
+    CHECK(::bind(fd, a.sa(), a.len) == 0);
+    bound->len = sizeof bound->ss;
+    getsockname(fd, bound->sa(), &bound->len);
+    return fd;
+  };
+  SockAddr ra, pa, oa;
+  int rfd = udp(&ra), pfd = udp(&pa), ofd = udp(&oa);
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<std::unique_ptr<RxReader::Burst>> got;
+  size_t opened = 0, raw = 0;
+  {
+    RxReader reader(rfd, pa, keys, [&](std::unique_ptr<RxReader::Burst> b) {
+      std::lock_guard<std::mutex> lk(mu);
+      opened += b->opened.recs.size();
+      raw += b->raw.size();
+      got.push_back(std::move(b));
+      cv.notify_all();
+    });
+    auto record = [&](uint8_t type, uint64_t seq, const std::string& pt) {
+      std::vector<uint8_t> out(record_size(pt.size()));
+      iovec v{const_cast<char*>(pt.data()), pt.size()};
+      seal_record(*g, keys->wiv, out.data(), type, seq, &v, 1, pt.size());
+      return out;
+    };
+    auto send = [&](int fd, const std::vector<uint8_t>& d) {
+      CHECK(::sendto(fd, d.data(), d.size(), 0, ra.sa(), ra.len) == ssize_t(d.size()));
+    };
+    auto r1 = record(23, 7, "hello"), r2 = record(23, 8, "world!");
+    std::vector<uint8_t> two = r1;
+    two.insert(two.end(), r2.begin(), r2.end());
+    send(pfd, two);                                   // 2 records, one datagram: opened
+    std::vector<uint8_t> stun(20, 0);
+    stun[0] = 0x00; stun[1] = 0x01; stun[4] = 0x21; stun[5] = 0x12; stun[6] = 0xA4; stun[7] = 0x42;
+    send(pfd, stun);                                  // STUN: raw
+    send(ofd, record(23, 9, "other sender"));         // another address: raw
+    auto bad = record(23, 10, "tampered");
+    bad.back() ^= 1;
+    send(pfd, bad);                                   // fails authentication: opened, ok = false
+    auto mixed = record(21, 11, "\x01\x00");
+    auto r3 = record(23, 12, "data");
+    mixed.insert(mixed.end(), r3.begin(), r3.end());
+    send(pfd, mixed);                                 // alert + data: raw, whole
+    std::unique_lock<std::mutex> lk(mu);
+    CHECK(cv.wait_for(lk, std::chrono::seconds(5), [&] { return opened + raw >= 6; }));
+    for (size_t i = 0; i < got.size(); i++) reader.done();
+  }
+  CHECK_EQ(opened, size_t(3));
+  CHECK_EQ(raw, size_t(3));
+  std::vector<std::string> texts;
+  int ok = 0, bad_recs = 0;
+  for (auto& b : got)
+    for (auto& r : b->opened.recs) {
+      if (r.ok) {
+        ok++;
+        texts.emplace_back(reinterpret_cast<const char*>(r.pt), r.ptl);
+      } else {
+        bad_recs++;
+      }
+    }
+  CHECK_EQ(ok, 2);
+  CHECK_EQ(bad_recs, 1);
+  CHECK(texts.size() == 2 && texts[0] == "hello" && texts[1] == "world!");
+  for (auto& b : got)
+    for (auto& r : b->raw) CHECK(r.buf && r.len > 0);
+  ::close(rfd);
+  ::close(pfd);
+  ::close(ofd);
+}
+
 TEST(peerconnection_bulk_through_crypto_lanes) {
   // Standard and jumbo paths, each with the socket reader (default) and with
   // the association thread reading the socket (records opened on the RX lane).
