@@ -656,8 +656,17 @@ void DtlsTransport::on_datagram(std::shared_ptr<const void> owner, uint8_t* p, s
 }
 
 bool DtlsTransport::deliver_plain(const std::shared_ptr<const void>& owner, uint8_t type, uint8_t* pt, size_t ptl) {
+  std::shared_ptr<const void> o = owner;
+  return deliver_plain_take(o, type, pt, ptl);
+}
+
+// `owner` is moved into the record's view (no reference count traffic), and
+// with a batch open (deliver_opened) the view is collected for on_data_batch.
+bool DtlsTransport::deliver_plain_take(std::shared_ptr<const void>& owner, uint8_t type, uint8_t* pt, size_t ptl) {
   if (type == kAlert) {
     if (ptl >= 2 && (pt[0] == 2 || pt[1] == 0)) {
+      flush_batch();  // what came before the alert goes up first
+      if (closed_) return false;
       fail(pt[1] == 0 ? "DTLS close_notify received" : "DTLS fatal alert received");
       return false;
     }
@@ -670,8 +679,21 @@ bool DtlsTransport::deliver_plain(const std::shared_ptr<const void>& owner, uint
     if (timer_) r_.cancel(timer_);
     timer_ = 0;
   }
-  if (on_data) on_data(Bytes::adopt(owner, pt, ptl));
+  if (batching_ && on_data_batch) {
+    batch_.push_back(Bytes::adopt(std::move(owner), pt, ptl));
+    return true;
+  }
+  if (on_data) on_data(Bytes::adopt(std::move(owner), pt, ptl));
   return !closed_;
+}
+
+void DtlsTransport::flush_batch() {
+  if (batch_.empty()) return;
+  std::vector<Bytes> b;
+  b.swap(batch_);
+  if (on_data_batch && !closed_) on_data_batch(b.data(), b.size());
+  b.clear();
+  if (batch_.empty()) batch_.swap(b);  // keep the capacity
 }
 
 void DtlsTransport::enable_lanes(std::function<bool(TxTarget&)> target) {
@@ -741,12 +763,15 @@ void DtlsTransport::commit_rx() {
   if (rx_outstanding_ == 0 && rx_pend_.bytes < datapath_inline_bytes()) {
     RxBatch b = std::move(rx_pend_);
     rx_pend_ = RxBatch();
+    batching_ = true;
     for (auto& r : b.recs) {
       uint8_t* pt;
       size_t ptl;
       if (!fast_decrypt(r.rec, r.len, r.type, r.seq, &pt, &ptl)) continue;
-      if (!deliver_plain(r.owner, r.type, pt, ptl)) return;
+      if (!deliver_plain_take(r.owner, r.type, pt, ptl)) break;
     }
+    batching_ = false;
+    flush_batch();
     return;
   }
   auto b = std::make_shared<RxBatch>(std::move(rx_pend_));
@@ -774,17 +799,22 @@ void DtlsTransport::rx_done(RxBatch& b) {
   deliver_opened(b);
 }
 
+// A burst's records go up as one batch (on_data_batch): the receiver takes
+// its references once per burst instead of once per record.
 void DtlsTransport::deliver_opened(RxBatch& b) {
   if (closed_) return;
   auto self = shared_from_this();
+  batching_ = true;
   for (auto& x : b.recs) {
     if (!x.ok || replay_seen(x.seq)) {
       LOG_TRACE(kT, "dropping DTLS record that fails authentication or replay check");
       continue;
     }
     replay_mark(x.seq);
-    if (!deliver_plain(x.owner, x.type, x.pt, x.ptl)) return;
+    if (!deliver_plain_take(x.owner, x.type, x.pt, x.ptl)) break;
   }
+  batching_ = false;
+  flush_batch();
 }
 
 bool DtlsTransport::send(const uint8_t* p, size_t n) {

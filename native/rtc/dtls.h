@@ -119,6 +119,9 @@ class DtlsTransport : public std::enable_shared_from_this<DtlsTransport> {
 
   std::function<void()> on_connected;
   std::function<void(Bytes)> on_data;
+  // Records of one receive burst together (set: used for bursts; on_data for
+  // single datagrams). The views may be moved from.
+  std::function<void(Bytes*, size_t)> on_data_batch;
   std::function<void(const std::string&)> on_closed;
 
  private:
@@ -135,6 +138,10 @@ class DtlsTransport : public std::enable_shared_from_this<DtlsTransport> {
   // An authenticated application/alert record: alerts may end the transport
   // (false), data goes up.
   bool deliver_plain(const std::shared_ptr<const void>& owner, uint8_t type, uint8_t* pt, size_t ptl);
+  bool deliver_plain_take(std::shared_ptr<const void>& owner, uint8_t type, uint8_t* pt, size_t ptl);
+  void flush_batch();
+  bool batching_ = false;
+  std::vector<Bytes> batch_;
   void seal_inline(const TxBatch& b);
   void rx_done(RxBatch& b);
   void feed_openssl(const uint8_t* p, size_t n);

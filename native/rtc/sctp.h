@@ -96,6 +96,7 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   // never pins a whole receive buffer.
   void on_packet(const Bytes& pkt);
   void on_packet(const uint8_t* p, size_t n) { on_packet(Bytes::copy(p, n)); }
+  void on_packets(const Bytes* pkts, size_t n);  // a receive burst
   // Queue a message made of gathered pieces (a single piece is never copied).
   bool send(uint16_t stream, uint32_t ppid, const std::vector<Bytes>& pieces, bool unordered = false);
   // Queue a message = a short header (copied, <= kMsgHdrMax bytes) followed by
@@ -140,6 +141,7 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   struct InChunk;   // inbound DATA fragment awaiting cum-ack
   SctpAssociation(Reactor& r, SctpConfig cfg, PacketOut out);
 
+  void packet_in(const Bytes& pkt);
   void handle_init(const uint8_t* c, size_t len, uint32_t vtag);
   void handle_init_ack(const uint8_t* c, size_t len);
   void handle_cookie_echo(const uint8_t* c, size_t len);
