@@ -93,6 +93,14 @@ struct GemmArgs {
   // Lanes c and c + 2^cwl load the same weight row in the same instruction
   // (one fetch); their duplicate MFMA columns are dropped in the epilogue.
   int cwl;
+  // K parts (kpl = log2 P, 0: off; P = 16 >> cwl, TN = 1, M * P <= 16): lanes
+  // past the tile width take the other K parts of the same columns instead of
+  // repeating them, and MFMA rows m * P + p carry activation row m's K part p,
+  // so every lane streams unique weight bytes. The diagonal blocks of the
+  // 16 x 16 accumulator are summed in the epilogue. With spare MFMA rows (a
+  // decode step of <= 16 / P tokens) a 2048-wide projection then spreads
+  // over every CU without the duplicate fetches of narrow tiles.
+  int kpl;
 };
 
 __device__ __forceinline__ frag8 as_frag(const uint4& v) { return __builtin_bit_cast(frag8, v); }
@@ -238,21 +246,24 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
 
   // A fragment: row lane & 15, k = 32*s + 8*(lane>>4) + j; B fragment: W row n, same k.
   // The K steps are split evenly over the NW waves.
-  const int m_a = lane & 15;
+  const int kparts = 1 << a.kpl, Kp = a.K >> a.kpl;  // Kp: K elements per part
+  const int m_a = (lane & 15) >> a.kpl;              // activation row of this lane's MFMA row
+  const int p_a = (lane & 15) & (kparts - 1);        // ... and the K part it carries
   const bool a_ok = m0 + m_a < a.M;
   const int kq = (lane >> 4) << 3;
-  const int S = a.K >> 5;
+  const int S = Kp >> 5;
   const int b0 = kslice * S / a.ks, bs = (kslice + 1) * S / a.ks - b0;  // this workgroup's k-steps
   const int s0 = b0 + wv * bs / NW, s1 = b0 + (wv + 1) * bs / NW;
   // Byte offsets of this lane's A row and weight rows at k-step 0; rows past
   // M read as zeros (kOob).
   const __amdgpu_buffer_rsrc_t ra = rsrc(a.x, uint32_t(a.M) * uint32_t(a.K) * 2u);
   const __amdgpu_buffer_rsrc_t rw = rsrc(a.w, uint32_t(a.N) * uint32_t(a.K) * 2u);
-  const uint32_t xoff = a_ok ? (uint32_t(m0 + m_a) * uint32_t(a.K) + uint32_t(kq)) * 2u : kOob;
+  const uint32_t xoff = a_ok ? (uint32_t(m0 + m_a) * uint32_t(a.K) + uint32_t(p_a * Kp + kq)) * 2u : kOob;
+  const int p_b = a.kpl ? (lane & 15) >> a.cwl : 0;  // K part of this lane's weight column
   uint32_t woff[TN];
 #pragma unroll
   for (int t = 0; t < TN; t++)
-    woff[t] = (uint32_t(tile_col<TN>(bx, t, lane & 15, a.cwl)) * uint32_t(a.K) + uint32_t(kq)) * 2u;
+    woff[t] = (uint32_t(tile_col<TN>(bx, t, lane & 15, a.cwl)) * uint32_t(a.K) + uint32_t(p_b * Kp + kq)) * 2u;
 
   // C layout: row m = m0 + 4*(lane>>4) + r, column = tile_col(.., lane & 15).
   const int lrow0 = (lane >> 4) << 2, mrow0 = m0 + lrow0;
@@ -324,6 +335,26 @@ __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
         v[t][r] = sum;
       }
     if (lane == 0) st_wt(&a.kctr[bx], 0u);
+  }
+
+  if (a.kpl) {
+    // Sum the diagonal blocks: output (row m, column c < 2^cwl) is
+    // sum_p C[m * P + p][c + p * 2^cwl]. Wave 0 alone from here on: the
+    // reduction buffer (its own reads are done) holds C [16][17].
+    float* cbuf = &red[0][0][0][0];
+#pragma unroll
+    for (int r = 0; r < 4; r++) cbuf[(lrow0 + r) * 17 + c] = v[0][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int row = lrow0 + r;
+      float sum = 0.f;
+      if (row < (16 >> a.kpl) && col_ok)
+        for (int p = 0; p < kparts; p++) sum += cbuf[(row * kparts + p) * 17 + c + (p << a.cwl)];
+      v[0][r] = sum;
+    }
   }
 
   if (norm) {
@@ -694,14 +725,15 @@ __global__ __launch_bounds__(512) void k_attn(const uint16_t* __restrict__ q, co
   __syncthreads();
   if (s_ticket != unsigned(nact - 1)) return;
 
-  // Last slot: merge the slot partials, heads spread over the waves; each
-  // batch of up to MAXC partials is loaded before any of it is used.
+  // Last slot: merge the slot partials, heads spread over the waves. Each
+  // batch of up to MAXC partials (maxima, sums and vectors together) is loaded
+  // before any of it is used and folded in with a running maximum, so a merge
+  // of <= MAXC slots is one memory round trip (a separate pass for the global
+  // maximum first cost a second one).
   for (int g = wv; g < G; g += NWV) {
     const size_t hb = hb0 + g;
     const float* ml = part_ml + hb * nsplit * 2;
     float M = -INFINITY;
-    for (int c = lane; c < nact; c += kWave) M = fmaxf(M, ld_wt(ml + 2 * c));
-    M = wave_max(M);
     float L = 0.f, o[DPL];
 #pragma unroll
     for (int k = 0; k < DPL; k++) o[k] = 0.f;
@@ -716,6 +748,15 @@ __global__ __launch_bounds__(512) void k_attn(const uint16_t* __restrict__ q, co
 #pragma unroll
         for (int k = 0; k < DPL; k++) pv[j][k] = ld_wt(part_o + (hb * nsplit + c) * D + lane + k * kWave);
       }
+      float Mb = M;
+#pragma unroll
+      for (int j = 0; j < MAXC; j++)
+        if (ll[j] > 0.f) Mb = fmaxf(Mb, wl[j]);
+      const float rs = M == -INFINITY ? 0.f : __expf(M - Mb);  // rescale what is folded in so far
+      L *= rs;
+#pragma unroll
+      for (int k = 0; k < DPL; k++) o[k] *= rs;
+      M = Mb;
 #pragma unroll
       for (int j = 0; j < MAXC; j++) {
         const float ww = ll[j] > 0.f ? __expf(wl[j] - M) : 0.f;
@@ -767,6 +808,7 @@ constexpr int kMaxKs = 8;    // split-K ways over workgroups
 // per CU (256) measured 1-4 % slower end to end once operands went through
 // buffer loads (profiles/r02/decode/decode_sweep_*.log, "min256" vs "cw16").
 constexpr int kResidMinTiles = 0;
+constexpr int kCUs = 256;  // MI355X compute units: K-parts tiling aims at one workgroup per CU
 
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -845,7 +887,7 @@ hipError_t launch_nw(const GemmArgs& a, int grid, hipStream_t s) {
   // 8-step batches).
   static const int ucap = env_int("P2PT_DECODE_UMCAP", 4);
   const int kCap = ((NW >= 16 && TN >= 2) || ucap <= 4) ? 4 : 8;
-  const int per_wave = ((a.K >> 5) / a.ks + NW - 1) / NW;
+  const int per_wave = (((a.K >> a.kpl) >> 5) / a.ks + NW - 1) / NW;
   const dim3 g(grid * a.ks, (a.M + 15) >> 4), b(NW * 64);
   if (per_wave <= 1)
     hipLaunchKernelGGL((k_skinny<NW, TN, EPI, 1>), g, b, 0, s, a);
@@ -873,14 +915,53 @@ int pick_cwl(int N, int TN, int dflt_min_tiles) {
   return cwl;
 }
 
+// K-parts tiling (GemmArgs::kpl) for an N-column, TN = 1 projection of M rows:
+// the tile width 2^cwl whose N >> cwl column tiles first reach `min_tiles`
+// workgroups (one per CU), if the spare MFMA rows allow it (M * P <= 16,
+// P = 16 >> cwl) and K splits into P parts of whole k-steps; false otherwise.
+bool pick_kparts(int N, int M, int K, int min_tiles, int* cwl, int* kpl) {
+  for (int c = 4; c >= 2; c--) {
+    if ((N >> c) < min_tiles && c > 2) continue;
+    const int P = 16 >> c;
+    if (P == 1 || M * P > 16 || K % (P * 32)) return false;
+    *cwl = c;
+    *kpl = 4 - c;
+    return true;
+  }
+  return false;
+}
+
+// K parts for the 2048-wide O and down projections (one workgroup per CU):
+// small config, batch 1, 0.372 -> 0.359 ms per step (profiles/r03/decode/
+// decode_ab_kparts.log). On QKV (3072 columns: 384 workgroups of 8) it cost
+// 3-4 us per step, so that stays opt-in (P2PT_DECODE_QKV_KPARTS=1).
+// P2PT_DECODE_KPARTS=0 turns it off.
+// K parts at a given tile width (2^cwl columns, P = 16 >> cwl parts); false
+// where the rows or K do not allow it.
+bool kparts_at(int M, int K, int cwl, int* out_cwl, int* kpl) {
+  if (cwl < 2 || cwl > 3) return false;
+  const int P = 16 >> cwl;
+  if (M * P > 16 || K % (P * 32)) return false;
+  *out_cwl = cwl;
+  *kpl = 4 - cwl;
+  return true;
+}
+
+bool kparts_on() {
+  static const bool v = env_int("P2PT_DECODE_KPARTS", 1) != 0;
+  return v;
+}
+
 // grid = column tiles of the chosen width; the launch has grid * a.ks workgroups (a.ks == 0: pick).
 template <int EPI, int TN>
 hipError_t launch_gemm(GemmArgs a, hipStream_t s, int nw_override = 0) {
   if (a.cwl <= 0) a.cwl = pick_cwl(a.N, TN, 0);
+  if (a.kpl && (TN != 1 || a.M * (16 >> a.cwl) > 16 || (16 >> a.cwl) != (1 << a.kpl) || a.K % (32 << a.kpl)))
+    return hipErrorInvalidValue;
   const int grid = a.N / (TN << a.cwl);
   if (a.ks <= 0) a.ks = (a.kpart && a.kctr && a.cwl == 4) ? pick_ks(grid, a.K) : 1;
-  if (a.M > 16 || a.cwl != 4) a.ks = 1;  // split-K slabs and tickets: one row tile of 16-column tiles only
-  const int nw = nw_override ? nw_override : pick_nw((a.K >> 5) / a.ks);
+  if (a.M > 16 || a.cwl != 4 || a.kpl) a.ks = 1;  // split-K slabs and tickets: one row tile of 16-column tiles only
+  const int nw = nw_override ? nw_override : pick_nw(((a.K >> a.kpl) >> 5) / a.ks);
   if (nw == 16) return launch_nw<16, TN, EPI>(a, grid, s);
   if (nw == 8) return launch_nw<8, TN, EPI>(a, grid, s);
   if (nw == 4) return launch_nw<4, TN, EPI>(a, grid, s);
@@ -968,6 +1049,12 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
     a.pos = pos; a.slot = slots; a.nslots = d.max_batch; a.q_out = W.q; a.kc = kc; a.vc = vc;
     a.H = d.H; a.Hkv = d.Hkv; a.D = d.D; a.Smax = d.max_seq; a.log2_theta = log2_theta;
     a.kpart = W.kpart; a.kctr = W.kctr;
+    static const bool qkv_kparts = env_int("P2PT_DECODE_QKV_KPARTS", 0) != 0;
+    static const int qkv_cwl = env_int("P2PT_DECODE_QKV_CWL", 0);  // experiments: K parts at this width
+    if (!(kparts_on() && ((qkv_cwl && kparts_at(B, d.dim, qkv_cwl, &a.cwl, &a.kpl)) ||
+                          (qkv_kparts && pick_kparts(qkv_n, B, d.dim, kCUs, &a.cwl, &a.kpl)))))
+      a.kpl = 0;
+    if (a.kpl == 0) a.cwl = 0;
     if ((e = launch_gemm<EPI_ROPE, 1>(a, s)) != hipSuccess) return int(e);
 
     // attention: (span slot, row, KV head) workgroups of 8 waves
@@ -992,7 +1079,10 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
     GemmArgs o{};
     o.M = B; o.x = W.attn; o.w = wo; o.N = d.dim; o.K = d.H * d.D;
     o.out = W.resid; o.ss_out = W.ss; o.kpart = W.kpart; o.kctr = W.kctr;
-    o.cwl = pick_cwl(d.dim, kTnResid, kResidMinTiles);
+    if (!(kparts_on() && pick_kparts(d.dim, B, d.H * d.D, kCUs, &o.cwl, &o.kpl))) {
+      o.kpl = 0;
+      o.cwl = pick_cwl(d.dim, kTnResid, kResidMinTiles);
+    }
     if ((e = launch_gemm<EPI_RESID, kTnResid>(o, s)) != hipSuccess) return int(e);
     ss_parts = d.dim / (kTnResid << o.cwl);
 
@@ -1000,13 +1090,21 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
     GemmArgs g{};
     g.M = B; g.eps = d.eps; g.x = W.resid; g.w = wgu; g.N = 2 * d.ffn; g.K = d.dim;
     g.ss_part = W.ss; g.ss_parts = ss_parts; g.out = W.h; g.kpart = W.kpart; g.kctr = W.kctr;
+    static const int gu_cwl = env_int("P2PT_DECODE_GU_CWL", 0);  // experiments: K parts at this width
+    if (!(kparts_on() && gu_cwl && kparts_at(B, d.dim, gu_cwl, &g.cwl, &g.kpl))) {
+      g.kpl = 0;
+      g.cwl = 0;
+    }
     if ((e = launch_gemm<EPI_SILU, 1>(g, s)) != hipSuccess) return int(e);
 
     // down + residual
     GemmArgs dn{};
     dn.M = B; dn.x = W.h; dn.w = wdown; dn.N = d.dim; dn.K = d.ffn; dn.out = W.resid; dn.ss_out = W.ss;
     dn.kpart = W.kpart; dn.kctr = W.kctr;
-    dn.cwl = pick_cwl(d.dim, kTnResid, kResidMinTiles);
+    if (!(kparts_on() && pick_kparts(d.dim, B, d.ffn, kCUs, &dn.cwl, &dn.kpl))) {
+      dn.kpl = 0;
+      dn.cwl = pick_cwl(d.dim, kTnResid, kResidMinTiles);
+    }
     if ((e = launch_gemm<EPI_RESID, kTnResid>(dn, s)) != hipSuccess) return int(e);
     ss_parts = d.dim / (kTnResid << dn.cwl);
   }
@@ -1020,6 +1118,10 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
   h.cwl = 4;  // the argmax partials are sized for 16-column tiles
   const int parts = d.vocab / (16 * kTnStore);
   // 4 waves x 2 subtiles: the fastest LM-head shape measured (vocab 32000, K 2048: 22.6 vs 29.6 us).
+  // The merge stays a launch of its own: folded into the LM head's last block
+  // (write-through partials + arrival ticket) the step took 0.359 -> 0.366 ms
+  // at batch 1 and 0.522 -> 0.554 ms at 16, the 1,000 blocks' arrivals on one
+  // counter costing more than the launch (profiles/r03/decode/decode_ab_kparts.log).
   if ((e = launch_gemm<EPI_ARGMAX, kTnStore>(h, s, 4)) != hipSuccess) return int(e);
   hipLaunchKernelGGL(k_argmax_merge, dim3(emit_rows), dim3(256), 0, s, W.am_val, W.am_idx, parts, ids);
   return int(hipGetLastError());
