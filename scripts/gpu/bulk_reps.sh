@@ -11,19 +11,26 @@ STEPS=${STEPS:-150}
 PATHS=${PATHS:-jumbo std}
 mkdir -p gpurun_out/$TAG
 export TMPDIR=/tmp
-# BUILDS="build build-r2": interleave builds of the tunnel (bin dirs) for an
-# A/B on one box; file names then carry the build: <build>.<path>_<rep>.json.
+# A/B on one box, interleaved: BUILDS="build build-ab" (bin dirs of two builds
+# of the tunnel) or VARIANTS="label:bindir:VAR=v,VAR2=w ..." (same or other
+# builds under different environments). File names then carry the label:
+# <label>.<path>_<rep>.json.
 BUILDS=${BUILDS:-build}
+if [ -z "$VARIANTS" ]; then
+  for b in $BUILDS; do VARIANTS="$VARIANTS $b:$b:"; done
+fi
+nvar=$(echo $VARIANTS | wc -w)
 for i in $(seq 1 $REPS); do
-  for b in $BUILDS; do
+  for v in $VARIANTS; do
+    IFS=: read -r label bindir envs <<< "$v"
     for p in $PATHS; do
       x="${EXTRA}"
       t=webrtc
       [ $p = std ] && x="$x --no-jumbo-loopback"
       [ $p = tcp ] && t=tcp
       n=$p
-      [ "$BUILDS" != build ] && n=$b.$p
-      P2PT_BIN_DIR=$PWD/$b/bin timeout -k 10 300 python bench/profile_bulk.py --transport $t --steps $STEPS --extra="$x" > gpurun_out/$TAG/${n}_$i.json 2>> gpurun_out/$TAG/err.log || { tail -5 gpurun_out/$TAG/err.log; exit 1; }
+      [ $nvar -gt 1 ] && n=$label.$p
+      env ${envs//,/ } P2PT_BIN_DIR=$PWD/$bindir/bin timeout -k 10 300 python bench/profile_bulk.py --transport $t --steps $STEPS --extra="$x" > gpurun_out/$TAG/${n}_$i.json 2>> gpurun_out/$TAG/err.log || { tail -5 gpurun_out/$TAG/err.log; exit 1; }
       python -c "import json; d=json.load(open('gpurun_out/$TAG/${n}_$i.json')); print('$n $i', round(d['tunneled_req_s'],1), round(d['direct_req_s'],1), round(d['tunneled_req_s']/d['direct_req_s'],3), d['cpu_s_incl_warmup'], d['wall_s_incl_warmup'], flush=True)"
     done
   done
