@@ -1050,7 +1050,12 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
     a.H = d.H; a.Hkv = d.Hkv; a.D = d.D; a.Smax = d.max_seq; a.log2_theta = log2_theta;
     a.kpart = W.kpart; a.kctr = W.kctr;
     static const bool qkv_kparts = env_int("P2PT_DECODE_QKV_KPARTS", 0) != 0;
-    static const int qkv_cwl = env_int("P2PT_DECODE_QKV_CWL", 0);  // experiments: K parts at this width
+    // Experiments: K parts at a given width. Slower than 16-column tiles on
+    // QKV (batch 1: 4 columns 0.360 -> 0.373 ms per step) and gate/up (8
+    // columns 0.368, 4 columns 0.391 ms): more, smaller workgroups do not
+    // stream faster once the grid already covers the chip
+    // (profiles/r03/decode/decode_ab_cwl.log).
+    static const int qkv_cwl = env_int("P2PT_DECODE_QKV_CWL", 0);
     if (!(kparts_on() && ((qkv_cwl && kparts_at(B, d.dim, qkv_cwl, &a.cwl, &a.kpl)) ||
                           (qkv_kparts && pick_kparts(qkv_n, B, d.dim, kCUs, &a.cwl, &a.kpl)))))
       a.kpl = 0;
@@ -1090,7 +1095,7 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
     GemmArgs g{};
     g.M = B; g.eps = d.eps; g.x = W.resid; g.w = wgu; g.N = 2 * d.ffn; g.K = d.dim;
     g.ss_part = W.ss; g.ss_parts = ss_parts; g.out = W.h; g.kpart = W.kpart; g.kctr = W.kctr;
-    static const int gu_cwl = env_int("P2PT_DECODE_GU_CWL", 0);  // experiments: K parts at this width
+    static const int gu_cwl = env_int("P2PT_DECODE_GU_CWL", 0);  // experiments (see QKV above)
     if (!(kparts_on() && gu_cwl && kparts_at(B, d.dim, gu_cwl, &g.cwl, &g.kpl))) {
       g.kpl = 0;
       g.cwl = 0;
