@@ -190,7 +190,7 @@ struct Server {
       }
       if (buf->size() - used < len) return;
       *done = true;
-      if (trace) fprintf(stderr, "mock_req %llu\n", static_cast<unsigned long long>(Reactor::now_us()));
+      if (trace) fprintf(stderr, "mock_req %llu %s\n", static_cast<unsigned long long>(Reactor::now_us()), h.method.c_str());
       if (auto s = w.lock()) handle(s, h, buf->substr(used, size_t(len)));
     });
     TcpConn* key = c.get();

@@ -470,6 +470,18 @@ void PeerConnection::start_sctp() {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->srtt_us()) : 0.0;
   });
+  metrics::gauge_fn("tunnel_sctp_min_rtt_us", [w] {
+    auto s = w.lock();
+    return s && s->sctp_ ? double(s->sctp_->min_rtt_us()) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_sctp_round_min_rtt_us", [w] {
+    auto s = w.lock();
+    return s && s->sctp_ ? double(s->sctp_->last_round_min_rtt_us()) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_sctp_queue_cuts", [w] {
+    auto s = w.lock();
+    return s && s->sctp_ ? double(s->sctp_->stats().queue_cuts) : 0.0;
+  });
   metrics::gauge_fn("tunnel_sctp_retransmits", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().retransmits) : 0.0;

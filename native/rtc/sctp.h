@@ -59,6 +59,7 @@ struct SctpStats {
   uint64_t tlp_probes = 0, rack_marks = 0, random_loss_events = 0;
   uint64_t random_loss_cuts = 0;  // sustained random loss: the periodic 0.85 cut
   uint64_t congestion_cuts = 0;   // loss episodes read as congestion (0.7 cut)
+  uint64_t queue_cuts = 0;        // short-path queue bound: cwnd cuts for a standing queue
   uint64_t over_bdp_losses = 0;   // ... of them because cwnd was past the delivery-rate BDP
   uint64_t hystart_exits = 0;     // initial slow starts ended by HyStart++ (rising delay)
   uint64_t dup_copies_sent = 0;  // redundant copies of small messages (lossy paths)
@@ -122,6 +123,7 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   size_t cwnd() const { return cwnd_; }
   uint64_t srtt_us() const { return srtt_us_; }
   uint64_t min_rtt_us() const { return min_rtt_us_; }  // smallest RTT sample: the path's base RTT
+  uint64_t last_round_min_rtt_us() const { return qb_last_; }  // smallest RTT of the last full round
   // One-line sender/receiver state for the send-path stall watchdog.
   std::string debug_state() const;
   uint64_t rto_us() const { return rto_us_; }
@@ -263,6 +265,13 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   void dr_on_sack(uint32_t cum, size_t newly_acked, bool cwnd_limited, uint64_t now);
   void loss_response(bool random_loss, bool over_bdp, uint64_t now);
   size_t dr_bdp() const;
+  // Short-path queue bound (queue_bound()): per round trip, the smallest RTT
+  // sample minus the base RTT is the queue this association keeps standing
+  // in front of itself (socket buffers, crypto lanes, the peer's reader).
+  void queue_bound(uint32_t cum, uint64_t rtt_sample);
+  uint32_t qb_end_ = 0;
+  bool qb_active_ = false;
+  uint64_t qb_min_ = UINT64_MAX, qb_last_ = 0;
   bool hs_done_ = false, hs_css_ = false, hs_round_ = false;
   int hs_samples_ = 0, hs_css_rounds_ = 0;
   uint32_t hs_window_end_ = 0;

@@ -310,6 +310,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     sid_ = sess->next_stream_id();
     metrics::counter_add("tunnel_streams_opened_total");
     trace::event("proxy", sid_, "accept");
+    if (req_.method == "GET") trace::event("proxy", sid_, "get");  // tells bulk downloads apart in the traces
     std::string path = req_.target;
     if (path.rfind("http://", 0) == 0 || path.rfind("https://", 0) == 0) {
       size_t s = path.find('/', path.find("://") + 3);

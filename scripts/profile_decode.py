@@ -11,6 +11,7 @@ hipGraph by default, or launched eagerly with --eager; the fused step
 from __future__ import annotations
 
 import argparse
+import dataclasses
 import json
 import os
 import sys
@@ -20,7 +21,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch  # noqa: E402
 
-from p2p_llm_tunnel_amd.models.tiny_llm import TinyLlama  # noqa: E402
+from p2p_llm_tunnel_amd.models.tiny_llm import CONFIGS, TinyLlama  # noqa: E402
 
 
 def main():
@@ -32,6 +33,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--eager", action="store_true")
     ap.add_argument("--unfused", action="store_true", help="kernels.hip + hipBLASLt path instead of decode_fused.hip")
+    ap.add_argument("--set", action="append", default=[], metavar="FIELD=INT",
+                    help="override a field of --config (e.g. --set n_layers=2 --set vocab=8000)")
     ap.add_argument("--checkpoint", default=None, help="load this HF Llama checkpoint instead of a random --config")
     ap.add_argument("--loop", action="store_true",
                     help="device-side autoregression: one graph = the fused step (ids feed the next step's "
@@ -42,7 +45,11 @@ def main():
         m = load_llama(a.checkpoint, device="cuda", max_batch=a.batch, fused=not a.unfused)
         a.config = os.path.basename(os.path.normpath(a.checkpoint))
     else:
-        m = TinyLlama(a.config, device="cuda", max_batch=a.batch, fused=not a.unfused)
+        cfg = CONFIGS[a.config]
+        if a.set:
+            cfg = dataclasses.replace(cfg, **{k: int(v) for k, v in (x.split("=", 1) for x in a.set)})
+            a.config += "[" + ",".join(a.set) + "]"
+        m = TinyLlama(cfg, device="cuda", max_batch=a.batch, fused=not a.unfused)
     m.k_cache.normal_()
     m.v_cache.normal_()
     if a.loop:

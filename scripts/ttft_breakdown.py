@@ -24,6 +24,7 @@ import statistics
 import subprocess
 import sys
 import tempfile
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -37,6 +38,9 @@ def main():
     ap.add_argument("--requests", type=int, default=40)
     ap.add_argument("--transport", default="webrtc")
     ap.add_argument("--streams", type=int, default=1)
+    ap.add_argument("--bulk", type=int, default=0, help="concurrent 64 MB GET /bulk downloads running through the "
+                    "same tunnel for the whole measurement (the mixed row's head-of-line load)")
+    ap.add_argument("--extra", default="", help="extra flags for both tunnel processes, e.g. --no-jumbo-loopback")
     a = ap.parse_args()
     ensure_native()
     with tempfile.NamedTemporaryFile(suffix=".jsonl", prefix="p2pt-trace-", delete=False) as tf:
@@ -45,16 +49,29 @@ def main():
     mock = spawn("mock", [binary("tunnel-mock"), "--port", str(port), "--interval-ms", "20"], env={"MOCK_TRACE": "1"})
     mock.wait_for("Mock LLM server running", 10)
     try:
-        with Tunnel(f"http://127.0.0.1:{port}", transport=a.transport, env={"TUNNEL_TRACE": trace}) as t:
+        extra = [x for x in a.extra.split() if x]
+        with Tunnel(f"http://127.0.0.1:{port}", transport=a.transport, env={"TUNNEL_TRACE": trace},
+                    serve_extra=extra, proxy_extra=extra) as t:
+            bulk = None
+            if a.bulk:
+                bulk = subprocess.Popen([binary("tunnel-loadgen"), "--target", f"127.0.0.1:{t.proxy_port}", "--streams",
+                                         str(a.bulk), "--steps", str(1 << 20), "--warmup", "0", "--method", "GET",
+                                         "--path", f"/bulk?bytes={64 << 20}", "--events", "none", "--duration-s", "600"],
+                                        stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+                time.sleep(0.5)
             subprocess.run([binary("tunnel-loadgen"), "--target", f"127.0.0.1:{t.proxy_port}", "--streams",
                             str(a.streams), "--steps", str(a.requests // a.streams), "--warmup", "1"],
                            check=True, capture_output=True)
+            if bulk:
+                bulk.kill()
+                bulk.wait()
         ev = {}
         with open(trace) as f:
             for line in f:
                 e = json.loads(line)
                 ev.setdefault(e["sid"], {})[(e["role"], e["ev"])] = e["t_us"]
-        mock_t = sorted(int(l.split()[1]) for l in mock.lines if l.startswith("mock_req "))
+        # SSE requests are POSTs; the --bulk downloads are GETs (left out on both sides).
+        mock_t = sorted(int(l.split()[1]) for l in mock.lines if l.startswith("mock_req ") and "GET" not in l.split()[2:])
     finally:
         mock.stop()
         if os.path.exists(trace):
@@ -72,7 +89,7 @@ def main():
         hops = [h for h in hops if "mock" not in (h[0], h[2])]
         rows = {f"{a_}.{b_} -> {c_}.{d_}": [] for a_, b_, c_, d_ in hops}
     for sid, e in sorted(ev.items()):
-        if ("serve", "upstream_sent") not in e or ("proxy", "first_body") not in e:
+        if ("serve", "upstream_sent") not in e or ("proxy", "first_body") not in e or ("proxy", "get") in e:
             continue
         if join_mock:
             up = e[("serve", "upstream_sent")]
@@ -88,7 +105,7 @@ def main():
         if v:
             v.sort()
             out[k] = {"n": len(v), "p50_us": statistics.median(v), "p90_us": v[int(0.9 * (len(v) - 1))]}
-    res = {"transport": a.transport, "streams": a.streams, "hops": out}
+    res = {"transport": a.transport, "streams": a.streams, "bulk": a.bulk, "extra": a.extra, "hops": out}
     if not join_mock:
         res["note"] = "mock hops omitted: mock trace lines cannot be joined to streams when streams > 1"
     print(json.dumps(res, indent=1))
