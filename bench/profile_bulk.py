@@ -71,7 +71,7 @@ def main():
                    "tunneled_req_s": tr["req_s"], "direct_req_s": dr["req_s"],
                    "tunneled_MBps_each_way": tr["req_s"] * a.mb * 1.048576, "errors": tr["errors"] + dr["errors"],
                    "wall_s_incl_warmup": round(wall, 3),
-                   "cpu_s_incl_warmup": {k: round(c1[k] - c0[k], 3) for k in pids}}
+                   "cpu_s_incl_warmup": {k: round(c1[k] - c0[k], 3) for k in pids}, "pids": pids}
             for name, p in (("serve", ms), ("proxy", mp)):
                 txt = urllib.request.urlopen(f"http://127.0.0.1:{p}/metrics", timeout=5).read().decode()
                 out[f"{name}_sctp"] = {l.split()[0]: float(l.split()[1]) for l in txt.splitlines()

@@ -1573,7 +1573,7 @@ void SctpAssociation::flush() {
   // non-blocking turn (its I/O first) and the next flush continues.
   static const size_t quantum = [] {
     const char* e = getenv("TUNNEL_SCTP_FLUSH_KB");
-    return size_t(e && *e ? std::max(0, atoi(e)) : 0) * 1024;
+    return size_t(e && *e ? std::max(0, atoi(e)) : 128) * 1024;
   }();
   size_t new_bytes = 0;
   bool yielded = false;

@@ -76,6 +76,29 @@ TEST(placement_inline_then_least_loaded) {
   CHECK_EQ(single.pick(), size_t(0));
 }
 
+TEST(bulk_routes_learn_downloads_not_streams) {
+  BulkRoutes r;
+  const std::string dl = BulkRoutes::key("GET", "/bulk?bytes=67108864");
+  CHECK(dl == BulkRoutes::key("GET", "/bulk?bytes=1"));  // the query does not split a route
+  CHECK(!r.bulk(dl));
+  r.note(dl, 64u << 20, false);
+  CHECK(r.bulk(dl));
+  CHECK(!r.bulk(BulkRoutes::key("POST", "/bulk")));  // the method is part of the route
+  // A long SSE / NDJSON response is interactive however many bytes it carried.
+  const std::string chat = BulkRoutes::key("POST", "/v1/chat/completions");
+  CHECK(BulkRoutes::streaming_type("text/event-stream; charset=utf-8"));
+  CHECK(BulkRoutes::streaming_type("application/x-ndjson"));
+  r.note(chat, 8u << 20, true);
+  CHECK(!r.bulk(chat));
+  // A small answer on a learnt route unlearns it.
+  r.note(dl, 1000, false);
+  CHECK(!r.bulk(dl));
+  // Bounded: past 256 routes the table starts over.
+  for (int i = 0; i < 300; i++) r.note(BulkRoutes::key("GET", "/f" + std::to_string(i)), 1u << 20, false);
+  CHECK(r.bulk(BulkRoutes::key("GET", "/f299")));
+  CHECK(!r.bulk(BulkRoutes::key("GET", "/f0")));
+}
+
 namespace {
 // A channel that accepts at most `room` bytes until drained by the test.
 struct FakeChannel : MessageChannel {

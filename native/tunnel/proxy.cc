@@ -60,6 +60,7 @@ class ProxyWorker : public std::enable_shared_from_this<ProxyWorker> {
   // socket to a worker (Placement: bulk I/O off the association thread).
   bool may_migrate() const { return index_ == 0 && shared_->workers > 0; }
   void migrate(ProxyConn* c, int fd, Bytes unparsed);
+  BulkRoutes& bulk_routes() { return bulk_routes_; }
 
  private:
   void adopt(int fd, Bytes unparsed = Bytes());
@@ -71,6 +72,7 @@ class ProxyWorker : public std::enable_shared_from_this<ProxyWorker> {
   std::unique_ptr<Pipe<ProxySession::Ev>> out_;
   std::unordered_map<uint32_t, std::weak_ptr<ProxyConn>> streams_;
   std::unordered_map<ProxyConn*, std::shared_ptr<ProxyConn>> conns_;
+  BulkRoutes bulk_routes_;  // learnt on this thread's connections (the inline one's decide migrations)
 };
 
 // One accepted client connection. Requests on a connection are handled one
@@ -275,8 +277,9 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
       // and all, to a worker before any stream exists for it.
       uint64_t blen = 0;
       std::string e2;
-      if (http::request_body_mode(h, blen, &e2) == http::BodyDecoder::Mode::Length && blen >= Placement::kBulkBytes &&
-          !pipelined_hold_) {
+      const bool big_upload =
+          http::request_body_mode(h, blen, &e2) == http::BodyDecoder::Mode::Length && blen >= Placement::kBulkBytes;
+      if ((big_upload || sess->bulk_routes().bulk(BulkRoutes::key(h.method, h.target))) && !pipelined_hold_) {
         int fd = conn_->release_fd();
         if (fd >= 0) {
           Bytes rest = Bytes::copy(inbuf_);
@@ -443,8 +446,10 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     snprintf(line, sizeof line, "HTTP/1.1 %d %s\r\n", status, http::reason_phrase(status));
     out += line;
     bool has_cl = false, has_date = false;
+    res_streaming_ = false;
     for (auto& kv : rh.headers) {
       if (http::iequals(kv.first, "transfer-encoding") || http::iequals(kv.first, "connection")) continue;
+      if (http::iequals(kv.first, "content-type")) res_streaming_ = BulkRoutes::streaming_type(kv.second);
       if (http::iequals(kv.first, "content-length")) has_cl = true;
       if (http::iequals(kv.first, "date")) has_date = true;
       out += kv.first;
@@ -493,6 +498,8 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
 
   void response_done() {
     cancel_timer();
+    if (head_written_ && !req_.method.empty())
+      if (auto sess = sess_.lock()) sess->bulk_routes().note(BulkRoutes::key(req_.method, req_.target), body_sent_, res_streaming_);
     if (stream_registered_) {
       if (auto sess = sess_.lock()) sess->unregister_stream(sid_);
       stream_registered_ = false;
@@ -604,6 +611,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     return s && s->flow();
   }
   uint64_t body_sent_ = 0;
+  bool res_streaming_ = false;  // SSE / NDJSON response (never a bulk route)
   uint64_t timer_ = 0;
   friend class ProxyWorker;
 };

@@ -710,7 +710,9 @@ void ServeSession::start_request(uint32_t sid, Pending p, bool streaming) {
   metrics::counter_add("tunnel_upstream_requests_total");
   Inflight& fl = inflight_[sid];
   fl.up = pick_upstream();
-  fl.thread = place_->pick(p.body_len >= Placement::kBulkBytes || p.declared >= int64_t(Placement::kBulkBytes));
+  fl.route = BulkRoutes::key(req.method, p.headers.path);
+  fl.thread = place_->pick(p.body_len >= Placement::kBulkBytes || p.declared >= int64_t(Placement::kBulkBytes) ||
+                           bulk_routes_.bulk(fl.route));
   fl.path = std::move(p.headers.path);
   fl.uploading = streaming;
   fl.uploaded = p.body_len;
@@ -750,6 +752,7 @@ void ServeSession::on_event(Ev& ev) {
     } else if (ev.responded) {
       u.fails = 0;
       u.down_until_ms = 0;
+      bulk_routes_.note(fl.route, fl.res_bytes, fl.res_streaming);
     }
     place_->release(fl.thread);
     inflight_.erase(it);
@@ -768,8 +771,10 @@ void ServeSession::on_event(Ev& ev) {
   Inflight& fl = it->second;
   bool body = ev.frame.type == proto::MsgType::ResBody;
   size_t n = ev.frame.payload.size();
+  if (ev.frame.type == proto::MsgType::ResHeaders) fl.res_streaming = BulkRoutes::streaming_type(ev.frame.payload.view());
   sched_->send(std::move(ev.frame));
   if (!body) return;
+  fl.res_bytes += n;
   // "flow": the proxy hands credit back as its client drains; out of credit,
   // this stream's upstream read pauses (a slow client cannot grow the proxy).
   if (flow_) {

@@ -128,6 +128,9 @@ class ServeSession : public std::enable_shared_from_this<ServeSession> {
     uint64_t uploaded = 0;    // request-body bytes received
     int64_t credit = proto::kFlowWindow;  // "flow": RES_BODY bytes we may still send
     proto::FlowWindow upwin;              // "flow": streamed REQ_BODY window autotuning
+    std::string route;                    // BulkRoutes key
+    uint64_t res_bytes = 0;               // response body bytes so far
+    bool res_streaming = false;           // SSE / NDJSON response
   };
   // One upstream origin (one inference endpoint, e.g. one per GPU) and its
   // passive health: an origin that refuses connections is ejected for an
@@ -189,6 +192,7 @@ class ServeSession : public std::enable_shared_from_this<ServeSession> {
   size_t rr_ = 0;
   std::vector<Link> links_;
   std::unique_ptr<Placement> place_;
+  BulkRoutes bulk_routes_;
   friend class ServeWorker;
 };
 

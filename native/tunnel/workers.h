@@ -24,9 +24,13 @@
 #pragma once
 
 #include <atomic>
+#include <cstdlib>
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <string>
+#include <string_view>
+#include <unordered_set>
 #include <thread>
 #include <vector>
 
@@ -154,6 +158,47 @@ class Placement {
   std::vector<size_t> active_;
   size_t inline_max_;
   size_t rr_ = 0;
+};
+
+// Routes (method + path, query dropped) whose last response was bulk. A
+// download's size is unknown when its request arrives, so Placement cannot
+// send it to a worker up front the way it does a large upload; the first
+// response of a route teaches it instead, and later requests to that route go
+// to a worker (serve) or move their client connection to one (proxy). Streamed
+// responses (SSE, NDJSON) never count as bulk, however long: they are the
+// interactive traffic the association thread keeps close. One per thread.
+class BulkRoutes {
+ public:
+  static std::string key(std::string_view method, std::string_view path) {
+    const size_t q = path.find('?');
+    std::string k(method);
+    k += ' ';
+    k.append(path.substr(0, q));
+    return k;
+  }
+  static bool streaming_type(std::string_view ctype) {
+    return ctype.find("event-stream") != std::string_view::npos || ctype.find("ndjson") != std::string_view::npos;
+  }
+  bool bulk(const std::string& k) const { return !m_.empty() && enabled() && m_.count(k) != 0; }
+  static bool enabled() {  // TUNNEL_BULK_ROUTES=0 turns the learning off (A/B)
+    static const bool on = [] {
+      const char* e = getenv("TUNNEL_BULK_ROUTES");
+      return !(e && *e == '0');
+    }();
+    return on;
+  }
+  void note(const std::string& k, uint64_t bytes, bool streaming) {
+    if (bytes >= Placement::kBulkBytes && !streaming) {
+      if (m_.size() >= kMax) m_.clear();
+      m_.insert(k);
+    } else if (!m_.empty()) {
+      m_.erase(k);
+    }
+  }
+
+ private:
+  static constexpr size_t kMax = 256;
+  std::unordered_set<std::string> m_;
 };
 
 }  // namespace p2pt

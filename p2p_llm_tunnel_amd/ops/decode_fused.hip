@@ -172,6 +172,13 @@ __device__ __forceinline__ uint4 buf_ld16(__amdgpu_buffer_rsrc_t r, uint32_t off
 // memory-side cache, which every XCD shares) and discard it; the projection
 // then streams from the cache instead of HBM. Block `blk` of `nblk` takes one
 // contiguous 4 KiB-aligned share; each thread keeps 8 x 16 B loads in flight.
+// Measured on MI355X and left off (P2PT_DECODE_PF, profiles/r03/decode_mall/):
+// the projections are not bound by where their weights come from. With every
+// weight resident in the Infinity Cache (2 layers, 8000-row head) gate/up
+// takes 10.8 us against 11.8-12.1 from HBM, QKV 5.9 against 6.6, down 7.4
+// against 8.1; and the prefetch itself slows the kernel it rides on (small,
+// batch 1: 0.372 ms per step; QKV -> O 0.372, attention -> gate/up 0.378,
+// O -> down 0.413, all four 0.438).
 __device__ __forceinline__ void prefetch_range(const void* base, uint32_t bytes, int blk, int nblk) {
   if (!base || !bytes || nblk <= 0) return;
   const uint32_t per = ((bytes + uint32_t(nblk) - 1) / uint32_t(nblk) + 4095u) & ~4095u;
