@@ -101,12 +101,6 @@ struct GemmArgs {
   // decode step of <= 16 / P tokens) a 2048-wide projection then spreads
   // over every CU without the duplicate fetches of narrow tiles.
   int kpl;
-  // Weight prefetch (pf_blocks > 0): the last pf_blocks workgroups of row
-  // tile 0 compute nothing; they read [pf, pf + pf_bytes) once so that the
-  // next projection finds its weights in the Infinity Cache (prefetch_range).
-  const void* pf;
-  uint32_t pf_bytes;
-  int pf_blocks;
 };
 
 __device__ __forceinline__ frag8 as_frag(const uint4& v) { return __builtin_bit_cast(frag8, v); }
@@ -162,40 +156,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t b
 }
 __device__ __forceinline__ uint4 buf_ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
-}
-
-// Weight prefetch into the Infinity Cache. A decode step's narrow phases
-// (QKV: 192 workgroups, attention: 64 at batch 1) leave CUs and most of the
-// HBM bandwidth idle while the weights of the next projection wait to be
-// streamed. Workgroups appended to such a kernel read a later projection's
-// weight range once (default cache policy: the lines allocate in the 256 MB
-// memory-side cache, which every XCD shares) and discard it; the projection
-// then streams from the cache instead of HBM. Block `blk` of `nblk` takes one
-// contiguous 4 KiB-aligned share; each thread keeps 8 x 16 B loads in flight.
-// Measured on MI355X and left off (P2PT_DECODE_PF, profiles/r03/decode_mall/):
-// the projections are not bound by where their weights come from. With every
-// weight resident in the Infinity Cache (2 layers, 8000-row head) gate/up
-// takes 10.8 us against 11.8-12.1 from HBM, QKV 5.9 against 6.6, down 7.4
-// against 8.1; and the prefetch itself slows the kernel it rides on (small,
-// batch 1: 0.372 ms per step; QKV -> O 0.372, attention -> gate/up 0.378,
-// O -> down 0.413, all four 0.438).
-__device__ __forceinline__ void prefetch_range(const void* base, uint32_t bytes, int blk, int nblk) {
-  if (!base || !bytes || nblk <= 0) return;
-  const uint32_t per = ((bytes + uint32_t(nblk) - 1) / uint32_t(nblk) + 4095u) & ~4095u;
-  const uint32_t lo = uint32_t(blk) * per;
-  if (lo >= bytes) return;
-  const uint32_t hi = min(bytes, lo + per);
-  const __amdgpu_buffer_rsrc_t r = rsrc(base, bytes);
-  const uint32_t step = blockDim.x * 16u;
-  constexpr int U = 8;
-  for (uint32_t off = lo + threadIdx.x * 16u; off < hi; off += U * step) {
-    uint4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) v[u] = buf_ld16(r, off + u * step < hi ? off + u * step : kOob);
-    // Consume the loads (and wait for them) without using the data.
-#pragma unroll
-    for (int u = 0; u < U; u++) asm volatile("" ::"v"(v[u].x));
-  }
 }
 
 // One batch of up to UM consecutive 32-wide k-steps [s, min(s + UM, s1)):
@@ -263,10 +223,6 @@ template <int NW, int TN, int EPI, int UM>
 __global__ __launch_bounds__(NW * 64) void k_skinny(GemmArgs a) {
   __shared__ float red[NW][TN][4][kWave];
   __shared__ float red_ss[NW][kWave];
-  if (a.pf_blocks && int(blockIdx.x) >= int(gridDim.x) - a.pf_blocks) {  // prefetch workgroups
-    if (blockIdx.y == 0) prefetch_range(a.pf, a.pf_bytes, int(blockIdx.x) - (int(gridDim.x) - a.pf_blocks), a.pf_blocks);
-    return;
-  }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int m0 = blockIdx.y << 4;    // first row of this workgroup's 16-row tile
   const int bx = blockIdx.x / a.ks;  // column tile
@@ -603,8 +559,7 @@ __global__ __launch_bounds__(512) void k_attn(const uint16_t* __restrict__ q, co
                                               const int* __restrict__ slot, int nslots, float* __restrict__ part_o,
                                               float* __restrict__ part_ml, unsigned* __restrict__ counters,
                                               uint16_t* __restrict__ out, int H, int Hkv, int Smax, int nsplit,
-                                              float scale, int min_span, int attn_rows, const void* pf,
-                                              uint32_t pf_bytes) {
+                                              float scale, int min_span) {
   constexpr int TOK = 32, NWV = 8;
   constexpr int DPL = D / kWave;  // merges: dims per lane
   constexpr int MAXC = 16;        // partials merged per load batch
@@ -613,11 +568,6 @@ __global__ __launch_bounds__(512) void k_attn(const uint16_t* __restrict__ q, co
   __shared__ float pml[NWV][G][2];
   __shared__ unsigned s_ticket;
 
-  if (int(blockIdx.y) >= attn_rows) {  // prefetch rows appended to the grid (prefetch_range)
-    prefetch_range(pf, pf_bytes, (int(blockIdx.y) - attn_rows) * int(gridDim.x) + int(blockIdx.x),
-                   (int(gridDim.y) - attn_rows) * int(gridDim.x));
-    return;
-  }
   const int b = blockIdx.y / Hkv, kvh = blockIdx.y % Hkv;
   const int len = min(max(pos[b], 0), Smax - 1) + 1;
   int span = (len + gridDim.x - 1) / gridDim.x;
@@ -938,7 +888,7 @@ hipError_t launch_nw(const GemmArgs& a, int grid, hipStream_t s) {
   static const int ucap = env_int("P2PT_DECODE_UMCAP", 4);
   const int kCap = ((NW >= 16 && TN >= 2) || ucap <= 4) ? 4 : 8;
   const int per_wave = (((a.K >> a.kpl) >> 5) / a.ks + NW - 1) / NW;
-  const dim3 g(grid * a.ks + (a.pf_blocks > 0 ? a.pf_blocks : 0), (a.M + 15) >> 4), b(NW * 64);
+  const dim3 g(grid * a.ks, (a.M + 15) >> 4), b(NW * 64);
   if (per_wave <= 1)
     hipLaunchKernelGGL((k_skinny<NW, TN, EPI, 1>), g, b, 0, s, a);
   else if (per_wave <= 2)
@@ -1018,28 +968,6 @@ hipError_t launch_gemm(GemmArgs a, hipStream_t s, int nw_override = 0) {
   return hipErrorInvalidValue;
 }
 
-// Which kernels carry prefetch workgroups (prefetch_range), from the bit mask
-// P2PT_DECODE_PF: 1 QKV -> O weights, 2 attention -> gate/up weights,
-// 4 O -> down weights, 8 down -> the next layer's QKV weights. Workgroups per
-// skinny GEMM: P2PT_DECODE_PF_BLOCKS; the attention fills up to
-// P2PT_DECODE_PF_WG workgroups in all.
-struct PfPlan {
-  bool qkv_o, attn_gu, o_down, down_qkv;
-  int blocks;
-};
-PfPlan pf_plan() {
-  static const PfPlan p = [] {
-    const int m = env_int("P2PT_DECODE_PF", 0);
-    return PfPlan{(m & 1) != 0, (m & 2) != 0, (m & 4) != 0, (m & 8) != 0,
-                  std::max(1, env_int("P2PT_DECODE_PF_BLOCKS", 64))};
-  }();
-  return p;
-}
-int pf_wg() {
-  static const int v = std::max(0, env_int("P2PT_DECODE_PF_WG", 256));
-  return v;
-}
-
 bool dims_ok(const LlamaDims& d) {
   if (d.D != 64 && d.D != 128) return false;
   // GEMM operands are addressed with 32-bit byte offsets below kOob (2 GiB):
@@ -1098,7 +1026,6 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
   const size_t layer_cache = size_t(d.max_batch) * d.max_seq * d.Hkv * d.D;
   const int nsplit_ws = (d.max_seq + kChunk - 1) / kChunk;
   const float log2_theta = log2f(d.theta);
-  const PfPlan pf = pf_plan();
 
   hipLaunchKernelGGL(k_embed, dim3(B), dim3(256), 0, s, bf(0), tokens, W.resid, W.ss, d.dim, d.vocab);
   int ss_parts = 1;
@@ -1133,27 +1060,17 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
                           (qkv_kparts && pick_kparts(qkv_n, B, d.dim, kCUs, &a.cwl, &a.kpl)))))
       a.kpl = 0;
     if (a.kpl == 0) a.cwl = 0;
-    if (pf.qkv_o) {
-      a.pf = wo;
-      a.pf_bytes = uint32_t(size_t(d.dim) * d.H * d.D * 2);
-      a.pf_blocks = pf.blocks;
-    }
     if ((e = launch_gemm<EPI_ROPE, 1>(a, s)) != hipSuccess) return int(e);
 
     // attention: (span slot, row, KV head) workgroups of 8 waves
     {
       (void)max_len;  // the grid no longer depends on the context length
-      const int arows = B * d.Hkv, aslots = attn_slots(B, d.Hkv, nsplit_ws);
-      // Prefetch rows: enough workgroups to fill the CUs the attention leaves idle.
-      const int pf_rows = pf.attn_gu ? std::max(0, (pf_wg() - aslots * arows) / aslots) : 0;
-      dim3 grid(aslots, arows + pf_rows);
+      dim3 grid(attn_slots(B, d.Hkv, nsplit_ws), B * d.Hkv);
       const float scale = 1.f / sqrtf(float(d.D));
       const int G = d.H / d.Hkv;
-      const uint32_t gu_bytes = uint32_t(2 * size_t(d.ffn) * d.dim * 2);
 #define P2PT_ATTN(DD, GG)                                                                                          \
   hipLaunchKernelGGL((k_attn<DD, GG>), grid, dim3(512), 0, s, W.q, kc, vc, pos, slots, d.max_batch, W.part_o,    \
-                     W.part_ml, W.counters, W.attn, d.H, d.Hkv, d.max_seq, nsplit_ws, scale, attn_min_span(), arows, \
-                     pf_rows ? static_cast<const void*>(wgu) : nullptr, pf_rows ? gu_bytes : 0u)
+                     W.part_ml, W.counters, W.attn, d.H, d.Hkv, d.max_seq, nsplit_ws, scale, attn_min_span())
       if (d.D == 64) {
         if (G == 1) P2PT_ATTN(64, 1); else if (G == 2) P2PT_ATTN(64, 2); else if (G == 4) P2PT_ATTN(64, 4); else P2PT_ATTN(64, 8);
       } else {
@@ -1170,11 +1087,6 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
     if (!(kparts_on() && pick_kparts(d.dim, B, d.H * d.D, kCUs, &o.cwl, &o.kpl))) {
       o.kpl = 0;
       o.cwl = pick_cwl(d.dim, kTnResid, kResidMinTiles);
-    }
-    if (pf.o_down) {
-      o.pf = wdown;
-      o.pf_bytes = uint32_t(size_t(d.dim) * d.ffn * 2);
-      o.pf_blocks = pf.blocks;
     }
     if ((e = launch_gemm<EPI_RESID, kTnResid>(o, s)) != hipSuccess) return int(e);
     ss_parts = d.dim / (kTnResid << o.cwl);
@@ -1197,11 +1109,6 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
     if (!(kparts_on() && pick_kparts(d.dim, B, d.ffn, kCUs, &dn.cwl, &dn.kpl))) {
       dn.kpl = 0;
       dn.cwl = pick_cwl(d.dim, kTnResid, kResidMinTiles);
-    }
-    if (pf.down_qkv && L + 1 < d.n_layers) {
-      dn.pf = bf(4 + 6 * (L + 1));
-      dn.pf_bytes = uint32_t(size_t(qkv_n) * d.dim * 2);
-      dn.pf_blocks = pf.blocks;
     }
     if ((e = launch_gemm<EPI_RESID, kTnResid>(dn, s)) != hipSuccess) return int(e);
     ss_parts = d.dim / (kTnResid << dn.cwl);
@@ -1256,10 +1163,10 @@ int p2pt_attn_bench(const void* q, const void* kc, const void* vc, const int* po
     auto oo = static_cast<uint16_t*>(out);
     if (D == 64)
       hipLaunchKernelGGL((k_attn<64, 4>), grid, dim3(512), 0, st, qq, kk, vv, pos, nullptr, B, part_o, part_ml,
-                         counters, oo, H, Hkv, Smax, nsplit_ws, scale, attn_min_span(), B * Hkv, nullptr, 0u);
+                         counters, oo, H, Hkv, Smax, nsplit_ws, scale, attn_min_span());
     else
       hipLaunchKernelGGL((k_attn<128, 4>), grid, dim3(512), 0, st, qq, kk, vv, pos, nullptr, B, part_o, part_ml,
-                         counters, oo, H, Hkv, Smax, nsplit_ws, scale, attn_min_span(), B * Hkv, nullptr, 0u);
+                         counters, oo, H, Hkv, Smax, nsplit_ws, scale, attn_min_span());
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return int(e);
   }
