@@ -7,6 +7,7 @@
 #include <condition_variable>
 #include <functional>
 #include <mutex>
+#include <thread>
 #include <random>
 
 #include "core/reactor.h"
@@ -598,7 +599,6 @@ TEST(rx_reader_opens_app_records_and_passes_the_rest) {
   SockAddr ra, pa, oa;
   int rfd = udp(&ra), pfd = udp(&pa), ofd = udp(&oa);
   std::mutex mu;
-  std::condition_variable cv;
   std::vector<std::unique_ptr<RxReader::Burst>> got;
   size_t opened = 0, raw = 0;
   {
@@ -607,7 +607,6 @@ TEST(rx_reader_opens_app_records_and_passes_the_rest) {
       opened += b->opened.recs.size();
       raw += b->raw.size();
       got.push_back(std::move(b));
-      cv.notify_all();
     });
     auto record = [&](uint8_t type, uint64_t seq, const std::string& pt) {
       std::vector<uint8_t> out(record_size(pt.size()));
@@ -633,8 +632,19 @@ TEST(rx_reader_opens_app_records_and_passes_the_rest) {
     auto r3 = record(23, 12, "data");
     mixed.insert(mixed.end(), r3.begin(), r3.end());
     send(pfd, mixed);                                 // alert + data: raw, whole
-    std::unique_lock<std::mutex> lk(mu);
-    CHECK(cv.wait_for(lk, std::chrono::seconds(5), [&] { return opened + raw >= 6; }));
+    // Polled rather than cv.wait_for: libstdc++ 11 waits through
+    // pthread_cond_clockwait, which GCC 11's ThreadSanitizer does not
+    // intercept (it then reports a double lock and races under one mutex).
+    bool all = false;
+    for (int i = 0; i < 5000 && !all; i++) {
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        all = opened + raw >= 6;
+      }
+      if (!all) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+    CHECK(all);
+    std::lock_guard<std::mutex> lk(mu);
     for (size_t i = 0; i < got.size(); i++) reader.done();
   }
   CHECK_EQ(opened, size_t(3));
