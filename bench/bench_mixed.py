@@ -133,18 +133,21 @@ def main():
     ap.add_argument("--bulk-mb", type=int, default=64)
     ap.add_argument("--slow-rate", type=int, default=100 * 1024)
     ap.add_argument("--extra", default="", help="extra flags for both tunnel processes")
+    ap.add_argument("--mock-threads", type=int, default=4,
+                    help="reactor threads of the native mock (it serves the SSE and the downloads, tunneled and direct)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     ensure_native()
     mport = free_port()
     mock = spawn("mock", [binary("tunnel-mock"), "--port", str(mport), "--interval-ms", str(a.interval_ms),
-                          "--tokens", str(a.tokens), "--threads", "4"])
+                          "--tokens", str(a.tokens), "--threads", str(a.mock_threads)])
     mock.wait_for("Mock LLM server running", 10)
     trs = [x for x in a.transports.split(",") if x]
     res = {"host": os.uname().nodename, "time": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
            "sse": f"{a.sse_streams} streams x {a.tokens} tokens @ {a.interval_ms} ms",
            "bulk": f"{a.bulk_streams} x {a.bulk_mb} MB GET, repeated for the whole run",
            "slow_client_Bps": a.slow_rate, "seconds_per_run": a.seconds, "reps": a.reps, "extra": a.extra,
+           "mock_threads": a.mock_threads,
            "runs": [], "rows": []}
     tunnels = {}
     try:
