@@ -13,7 +13,7 @@ done
 timeout -k 10 600 python -u -m pytest tests/test_gpu_model.py -k block_kernel -x -v -s --timeout 300 --timeout-method thread \
   -p no:cacheprovider > gpurun_out/block/pytest.log 2>&1; rc=$?; tail -n 8 gpurun_out/block/pytest.log; [ $rc -eq 0 ] || exit $rc
 for b in 1 16; do
-  for v in ${BLKS:-0 256 0 256}; do
+  for v in ${BLKS:-0 256 512 768 0}; do
     echo -n "block=$v " >> gpurun_out/block/wall.log
     P2PT_DECODE_BLOCK=$v timeout -k 10 180 python scripts/profile_decode.py --config small --batch $b --loop --steps 400 >> gpurun_out/block/wall.log 2>&1 || exit 1
     tail -1 gpurun_out/block/wall.log

@@ -1,6 +1,7 @@
 # Environment A/B of the tunnel on the MI355X host (CPU-only work): 64 x 1 MB
 # echo (bulk_reps.sh VARIANTS), the mixed row and the TTFT hop breakdown next
 # to 8 bulk downloads, per variant. VARS="label:ENV=v,ENV2=w label2:..."
+# SKIP_BULK=1 leaves out the 64 x 1 MB part; MIXED_EXTRA passes flags to bench_mixed.py.
 # Results under gpurun_out/$TAG/ (default env_ab).
 set -o pipefail
 TAG=${TAG:-env_ab}
@@ -9,11 +10,13 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 V=""
 for x in $VARS; do V="$V ${x%%:*}:build:${x#*:}"; done
-TAG=$TAG/bulk REPS=${REPS:-3} STEPS=${STEPS:-150} VARIANTS="$V" bash scripts/gpu/bulk_reps.sh || exit 1
+if [ -z "$SKIP_BULK" ]; then
+  TAG=$TAG/bulk REPS=${REPS:-3} STEPS=${STEPS:-150} VARIANTS="$V" bash scripts/gpu/bulk_reps.sh || exit 1
+fi
 for x in $VARS; do
   l=${x%%:*}; e=${x#*:}
   env ${e//,/ } timeout -k 10 300 python bench/bench_mixed.py --seconds ${MIXED_S:-8} --reps ${MIXED_REPS:-3} \
-    --out $OUT/mixed_$l.json > /dev/null 2> $OUT/mixed_$l.err || { tail -5 $OUT/mixed_$l.err; exit 1; }
+    ${MIXED_EXTRA} --out $OUT/mixed_$l.json > /dev/null 2> $OUT/mixed_$l.err || { tail -5 $OUT/mixed_$l.err; exit 1; }
   for p in jumbo std; do
     xx=""; [ $p = std ] && xx="--no-jumbo-loopback"
     env ${e//,/ } timeout -k 10 200 python scripts/ttft_breakdown.py --requests 80 --bulk 8 --extra="$xx" \
