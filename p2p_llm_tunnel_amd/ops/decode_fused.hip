@@ -795,15 +795,18 @@ __global__ __launch_bounds__(512) void k_attn(const uint16_t* __restrict__ q, co
 // with NW = 8, TN = 1, UM = 4, one 16-row tile, no split-K.
 // Measured on MI355X and left off (profiles/r03/decode_block/): correct
 // (tests/test_gpu_model.py::test_block_kernel_matches_launches) but slower,
-// small 0.358 -> 0.620 ms per step at batch 1, 0.521 -> 0.815 ms at 16. The
-// body needs 223 VGPRs, so one workgroup per CU runs its ~5 tiles of a layer
-// one after another, each paying a dequeue, two barriers and an arrival, where
-// the three launches keep several workgroups per CU in flight. What would
-// make a persistent layer pay (MI355X_MICROARCH price list: 0.87-0.89x of the
-// launches at best): a register diet to two or more workgroups per CU, tiles
-// claimed in chunks, and the next tile's weights streamed while the current
-// one reduces.
+// small 0.358 -> 0.61-0.62 ms per step at batch 1, 0.521 -> 0.81 ms at 16,
+// against every variant tried: three inlined bodies (223 VGPRs, one
+// workgroup per CU) or one body (70 VGPRs) at 256 workgroups; 512 or 768
+// workgroups 0.97-1.09 ms; waiters polling one completion word instead of 8
+// shards 0.68; 4 items per dequeue 1.00. Each tile is a serial chain in its
+// workgroup (dependent loads, reduction, write-through drain, barriers,
+// arrival) and the launched GEMMs overlap many such chains per CU; a
+// persistent layer would need each workgroup to stream the next tile's
+// weights while the current one reduces (MI355X_MICROARCH's LDS-DMA loader
+// engine: 0.87-0.89x of the launches at best).
 constexpr int kBlkNW = 8, kBlkUM = 4;
+constexpr int kBlkChunk = 1;  // work-queue items claimed per dequeue (4 measured slower: 0.61 -> 1.00 ms)
 constexpr int kAuxSc1 = 16;  // buffer-load cache policy bit sc1 (CPol::SC1)
 constexpr int kBlkCtr = 8 + 3 * 8;  // queue head, exits, 6 spare, 3 phases x 8 shards
 
@@ -819,9 +822,11 @@ __device__ __forceinline__ uint4 buf_ld16_sc1(__amdgpu_buffer_rsrc_t r, uint32_t
   return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kAuxSc1));
 }
 
-// Lane 0 only: until the 8 shards of `done` sum to `need` (bounded: ~1 s).
-// Polled with atomic adds of 0, which read the counter where the arrivals'
-// atomics land; sc1 loads of it (flat, then buffer) never saw the arrivals.
+// Lane 0 only: until the 8 arrival shards of a phase sum to `need` (bounded).
+// Polled with atomic adds of 0, which read the counters where the arrivals'
+// atomics land: `sc1` loads of them (flat, then buffer) never saw the
+// arrivals. (A two-level scheme, shards plus one completion word bumped by
+// each shard's last arriver so that waiters poll one word, measured slower.)
 __device__ __forceinline__ void blk_wait(unsigned* done, unsigned need, int* err, int iters) {
   for (int it = 0; it < iters; it++) {
     unsigned s = 0;
@@ -833,8 +838,7 @@ __device__ __forceinline__ void blk_wait(unsigned* done, unsigned need, int* err
   __hip_atomic_fetch_add(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int EPI>
-__device__ __forceinline__ void blk_tile(const GemmArgs& a, int bx, unsigned* wait_done, unsigned wait_need,
+__device__ __forceinline__ void blk_tile(const GemmArgs& a, const int EPI, int bx, unsigned* wait_done, unsigned wait_need,
                                          int* err, int iters, float (&red)[kBlkNW][4][kWave],
                                          float (&red_ss)[kBlkNW][kWave]) {
   constexpr int NW = kBlkNW, UM = kBlkUM;
@@ -880,7 +884,7 @@ __device__ __forceinline__ void blk_tile(const GemmArgs& a, int bx, unsigned* wa
     }
   }
   float rprev[4];
-  if constexpr (EPI == EPI_RESID) {
+  if (EPI == EPI_RESID) {
     if (wv == 0) {
       const int col = tile_col<1>(bx, 0, c, a.cwl);
 #pragma unroll
@@ -950,7 +954,7 @@ __device__ __forceinline__ void blk_tile(const GemmArgs& a, int bx, unsigned* wa
     for (int r = 0; r < 4; r++) v[r] *= __shfl(rs_row, lrow0 + r, kWave);
   }
   const int n = tile_col<1>(bx, 0, c, a.cwl);
-  if constexpr (EPI == EPI_SILU) {
+  if (EPI == EPI_SILU) {
     // Even lane = gate_j, odd = up_j; lanes c and c + 2 hold h_j, h_{j+1}: one 4-byte store per pair.
 #pragma unroll
     for (int r = 0; r < 4; r++) {
@@ -992,25 +996,33 @@ __global__ __launch_bounds__(kBlkNW * 64) void k_block(BlockArgs ba) {
   // no barrier sits in lane-divergent control flow. (A `for (;;)` with the
   // fetch at its top and a `break` was restructured by the compiler into
   // nested loops whose waves passed different barriers: it hung.)
-  if (threadIdx.x == 0) s_item = int(arrive(ba.ctr));
+  // Items are claimed kBlkChunk at a time (a chunk is worked in order, so the
+  // in-order argument holds). One queue word serves about 88 dequeues per
+  // microsecond (MI355X_MICROARCH) against ~1,200 tiles per layer, but
+  // claiming 4 at once made a workgroup's tiles, already serial, longer still.
+  if (threadIdx.x == 0) s_item = int(__hip_atomic_fetch_add(ba.ctr, unsigned(kBlkChunk), __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT));
   __syncthreads();
-  int item = __builtin_amdgcn_readfirstlane(s_item);
-  while (item < total) {
-    const int phase = item < t0 ? 0 : item < t1 ? 1 : 2;
-    if (phase == 0)
-      blk_tile<EPI_RESID>(ba.g[0], item, nullptr, 0u, ba.err, ba.wait_iters, red, red_ss);
-    else if (phase == 1)
-      blk_tile<EPI_SILU>(ba.g[1], item - t0, done, unsigned(t0), ba.err, ba.wait_iters, red, red_ss);
-    else
-      blk_tile<EPI_RESID>(ba.g[2], item - t1, done + 8, unsigned(ba.tiles[1]), ba.err, ba.wait_iters, red, red_ss);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores have landed
-    __syncthreads();                                  // ... and every wave's
-    if (threadIdx.x == 0) {
-      arrive(done + 8 * phase + (item & 7));
-      s_item = int(arrive(ba.ctr));
+  int base = __builtin_amdgcn_readfirstlane(s_item);
+  while (base < total) {
+    const int end = min(base + kBlkChunk, total);
+    for (int item = base; item < end; item++) {
+      const int phase = item < t0 ? 0 : item < t1 ? 1 : 2;
+      // One body for the three GEMMs (the phase's arguments read from the
+      // kernel-argument segment with a uniform index): three inlined bodies
+      // held every argument live at once, 223 VGPRs, one workgroup per CU.
+      const GemmArgs& ga = ba.g[phase];
+      const int tile = item - (phase == 0 ? 0 : phase == 1 ? t0 : t1);
+      blk_tile(ga, phase == 1 ? EPI_SILU : EPI_RESID, tile, phase == 0 ? nullptr : done + 8 * (phase - 1),
+               unsigned(phase == 0 ? 0 : ba.tiles[phase - 1]), ba.err, ba.wait_iters, red, red_ss);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores have landed
+      __syncthreads();                                  // ... and every wave's
+      if (threadIdx.x == 0) arrive(done + 8 * phase + (tile & 7));
     }
+    if (threadIdx.x == 0) s_item = int(__hip_atomic_fetch_add(ba.ctr, unsigned(kBlkChunk), __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT));
     __syncthreads();
-    item = __builtin_amdgcn_readfirstlane(s_item);
+    base = __builtin_amdgcn_readfirstlane(s_item);
   }
   if (threadIdx.x == 0 && arrive(ba.ctr + 1) == gridDim.x - 1) {  // the last to leave resets the counters
     for (int i = 0; i < kBlkCtr; i++) __hip_atomic_exchange(ba.ctr + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
