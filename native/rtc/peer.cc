@@ -28,7 +28,17 @@ const char* pc_state_name(PcState s) {
 
 constexpr size_t kPrioritySmallFrame = 1024;
 
+bool DataChannel::send_urgent(const uint8_t* hdr, size_t hlen, const Bytes& payload) {
+  return send_impl(hdr, hlen, payload, hlen + payload.size() <= kPrioritySmallFrame);
+}
+
 bool DataChannel::send(const uint8_t* hdr, size_t hlen, const Bytes& payload) {
+  return send_impl(hdr, hlen, payload, false);
+}
+
+// `urgent`: the SCTP priority queue (one-chunk messages only), ahead of bulk
+// messages not yet started; the receiver keeps each stream's order (SSN).
+bool DataChannel::send_impl(const uint8_t* hdr, size_t hlen, const Bytes& payload, bool urgent) {
   auto pc = pc_.lock();
   if (!pc || !is_open() || !pc->sctp_) return false;
   uint16_t st = uint16_t(stream_);
@@ -45,7 +55,7 @@ bool DataChannel::send(const uint8_t* hdr, size_t hlen, const Bytes& payload) {
     const char* e = getenv("TUNNEL_SCTP_PRIORITY");
     return e && *e == '1';
   }();
-  const bool small = prio && hlen + payload.size() <= kPrioritySmallFrame;
+  const bool small = urgent || (prio && hlen + payload.size() <= kPrioritySmallFrame);
   bool ok = pc->sctp_->send_framed(st, kPpidBinary, hdr, hlen, payload, false, small);
   if (ok && buffered_amount() > buffered_low_threshold) above_low_ = true;
   return ok;

@@ -52,6 +52,7 @@ class DataChannel : public MessageChannel, public std::enable_shared_from_this<D
  public:
   DataChannel(std::weak_ptr<PeerConnection> pc, std::string label) : pc_(std::move(pc)), label_(std::move(label)) {}
   bool send(const uint8_t* hdr, size_t hlen, const Bytes& payload) override;
+  bool send_urgent(const uint8_t* hdr, size_t hlen, const Bytes& payload) override;
   size_t buffered_amount() const override;
   bool is_open() const override { return open_ && !closed_; }
   void close() override;
@@ -74,6 +75,7 @@ class DataChannel : public MessageChannel, public std::enable_shared_from_this<D
   int stream() const { return stream_; }
 
  private:
+  bool send_impl(const uint8_t* hdr, size_t hlen, const Bytes& payload, bool urgent);
   friend class PeerConnection;
   void set_open();
   void set_closed(const std::string& why);

@@ -26,6 +26,11 @@ class MessageChannel {
   // Queue one message made of a small header and a payload view (gathered,
   // never concatenated by the caller). Returns false when the channel is closed.
   virtual bool send(const uint8_t* hdr, size_t hlen, const Bytes& payload) = 0;
+  // The same for a latency-sensitive message (the frame scheduler's
+  // interactive bypass: a token-sized frame of a stream with nothing queued):
+  // a transport with a priority path may send it ahead of bulk messages it
+  // holds unsent. Per-stream order is the transport's to keep.
+  virtual bool send_urgent(const uint8_t* hdr, size_t hlen, const Bytes& payload) { return send(hdr, hlen, payload); }
   // Bytes accepted by send() but not yet handed to the network.
   virtual size_t buffered_amount() const = 0;
   virtual bool is_open() const = 0;

@@ -1070,6 +1070,10 @@ void ProxySession::route(const proto::Frame& f) {
       if (shared_->flow.load(std::memory_order_relaxed))
         shared_->rtt_us.store(ch_ ? ch_->rtt_hint_us() : 0, std::memory_order_relaxed);
       if (it != routes_.end()) {
+        if (!it->second.body_seen) {
+          it->second.body_seen = true;
+          trace::event("proxy", f.stream_id, "chan_rx");
+        }
         Cmd c{Cmd::Body, f.stream_id};
         c.data = f.payload;
         command(it->second.thread, std::move(c));

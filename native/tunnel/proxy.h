@@ -118,6 +118,7 @@ class ProxySession : public std::enable_shared_from_this<ProxySession> {
   struct Route {
     size_t thread = 0;
     bool paused = false;
+    bool body_seen = false;  // trace: first RES_BODY frame out of the channel
   };
   ProxySession(Reactor& r, std::shared_ptr<MessageChannel> ch, ProxyConfig cfg);
   void init_links(WorkerPool* pool);

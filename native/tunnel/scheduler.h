@@ -25,12 +25,14 @@
 // their budget instead of everyone.
 #pragma once
 
+#include <cstdlib>
 #include <deque>
 #include <functional>
 #include <map>
 #include <memory>
 #include <set>
 #include <unordered_map>
+#include <unordered_set>
 
 #include "proto/frame.h"
 #include "tunnel/channel.h"
@@ -48,6 +50,12 @@ class FrameScheduler {
   void send(proto::Frame f);
   // Bytes held here plus bytes buffered in the channel.
   size_t pending_bytes() const { return queued_ + (ch_ ? ch_->buffered_amount() : 0); }
+  bool bypass_ = [] {  // TUNNEL_SCHED_BYPASS=0 turns the interactive bypass off (A/B)
+    const char* e = getenv("TUNNEL_SCHED_BYPASS");
+    return !(e && *e == '0');
+  }();
+  uint64_t bypassed_ = 0;  // frames sent through the interactive bypass
+  std::unordered_set<uint32_t> traced_;  // TUNNEL_TRACE: streams whose first body frame was stamped
   size_t queued_bytes() const { return queued_; }
   // Send-path stall watchdog, called about once a second: true when frames
   // or channel bytes are waiting and neither moved since the previous call.
@@ -82,7 +90,7 @@ class FrameScheduler {
     uint64_t sent = 0;  // bytes released so far (attained service)
     bool listed = false;
   };
-  bool emit(const proto::Frame& f);
+  bool emit(const proto::Frame& f, bool urgent = false);
   void list(uint32_t sid, StreamQ& s);
   bool pop_from(std::deque<uint32_t>& lane);
   bool pop_fifo();

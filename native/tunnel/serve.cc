@@ -772,6 +772,7 @@ void ServeSession::on_event(Ev& ev) {
   bool body = ev.frame.type == proto::MsgType::ResBody;
   size_t n = ev.frame.payload.size();
   if (ev.frame.type == proto::MsgType::ResHeaders) fl.res_streaming = BulkRoutes::streaming_type(ev.frame.payload.view());
+  if (body && fl.res_bytes == 0) trace::event("serve", ev.sid, "sched_in");  // first body frame reaches the scheduler
   sched_->send(std::move(ev.frame));
   if (!body) return;
   fl.res_bytes += n;

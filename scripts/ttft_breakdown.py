@@ -13,7 +13,11 @@ generator, joins the per-stream events (all processes stamp CLOCK_MONOTONIC
   serve req_end -> upstream_sent          serve picks an upstream socket and writes
   upstream_sent -> mock_req               upstream wakes up and parses
   mock_req -> serve first_body            first event back at serve
-  serve first_body -> proxy first_body    response crosses the tunnel
+  serve first_body -> proxy first_body    response crosses the tunnel, split into
+    serve first_body -> serve sched_in      upstream reader -> serve association thread
+    serve sched_in -> serve chan_tx         frame scheduler (queued behind the channel window?)
+    serve chan_tx -> proxy chan_rx          SCTP, DTLS, UDP, socket reader, proxy association thread
+    proxy chan_rx -> proxy first_body       hand-off to the client connection, its write
 """
 from __future__ import annotations
 
@@ -79,7 +83,13 @@ def main():
     hops = [("proxy", "accept", "proxy", "req_end"), ("proxy", "req_end", "serve", "req_headers"),
             ("serve", "req_headers", "serve", "req_end"), ("serve", "req_end", "serve", "upstream_sent"),
             ("serve", "upstream_sent", "mock", "req"), ("mock", "req", "serve", "first_body"),
-            ("serve", "first_body", "proxy", "first_body")]
+            ("serve", "first_body", "proxy", "first_body"),
+            # the token crossing split: upstream reader -> serve association thread,
+            # scheduler + SCTP + DTLS + UDP + socket reader -> proxy association
+            # thread, then the hand-off to the client connection and its write
+            ("serve", "first_body", "serve", "sched_in"), ("serve", "sched_in", "serve", "chan_tx"),
+            ("serve", "chan_tx", "proxy", "chan_rx"),
+            ("proxy", "chan_rx", "proxy", "first_body")]
     rows = {f"{a_}.{b_} -> {c_}.{d_}": [] for a_, b_, c_, d_ in hops}
     # The mock's trace line carries no stream id, so a mock request can only be
     # paired with the upstream send that preceded it when one stream runs at a
