@@ -104,10 +104,15 @@ namespace {
 struct FakeChannel : MessageChannel {
   size_t buffered = 0, room = 0;
   std::vector<std::pair<uint32_t, size_t>> sent;  // (stream, payload bytes)
+  size_t urgent = 0;  // messages that came through send_urgent
   bool send(const uint8_t* hdr, size_t, const Bytes& payload) override {
     sent.emplace_back(rd32(hdr + 1), payload.size());
     buffered += 5 + payload.size();
     return true;
+  }
+  bool send_urgent(const uint8_t* hdr, size_t hlen, const Bytes& payload) override {
+    urgent++;
+    return send(hdr, hlen, payload);
   }
   size_t buffered_amount() const override { return buffered; }
   bool is_open() const override { return true; }
@@ -146,6 +151,40 @@ TEST(scheduler_interactive_lane_goes_first) {
   // finishes before stream 2 starts.
   for (size_t i = 3; i < 10; i++) CHECK_EQ(ch->sent[i].first, i < 6 ? 1u : 2u);
   CHECK_EQ(s.queued_bytes(), size_t(0));
+}
+
+// Interactive bypass: over its window (but under 4 windows) the channel still
+// takes a token-sized frame of a stream with nothing queued, through the
+// transport's urgent path; frames of streams with a backlog, big frames and
+// everything past 4 windows queue as before.
+TEST(scheduler_interactive_bypass) {
+  auto ch = std::make_shared<FakeChannel>();
+  FrameScheduler s(ch, 1000);
+  ch->buffered = 2000;  // over the 1000-byte window
+  Bytes big = Bytes::copy(std::string(60000, 'b'));
+  Bytes tok = Bytes::copy(std::string(150, 't'));
+  s.send(proto::make_body(proto::MsgType::ResBody, 1, big));  // queues
+  s.send(proto::make_body(proto::MsgType::ResBody, 1, tok));  // behind stream 1's backlog: queues
+  s.send(proto::make_body(proto::MsgType::ResBody, 3, tok));  // nothing queued for stream 3: bypass
+  CHECK_EQ(ch->sent.size(), size_t(1));
+  CHECK_EQ(ch->sent[0].first, 3u);
+  CHECK_EQ(ch->urgent, size_t(1));
+  CHECK_EQ(s.stream_queued(1), size_t(60005 + 155));
+  ch->buffered = 5000;  // past 4 windows: a token queues too
+  s.send(proto::make_body(proto::MsgType::ResBody, 4, tok));
+  CHECK_EQ(ch->sent.size(), size_t(1));
+  CHECK_EQ(s.stream_queued(4), size_t(155));
+  ch->buffered = 0;
+  for (int i = 0; i < 4; i++) {
+    s.pump();
+    ch->buffered = 0;
+  }
+  CHECK_EQ(ch->sent.size(), size_t(4));
+  CHECK_EQ(s.queued_bytes(), size_t(0));
+  // Stream 1's frames stayed in order.
+  size_t i1 = 0;
+  for (auto& f : ch->sent)
+    if (f.first == 1u) CHECK_EQ(f.second, i1++ == 0 ? size_t(60000) : size_t(150));
 }
 
 // Past kFifoBytes a stream drops to round-robin: a newer stream's first
