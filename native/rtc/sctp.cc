@@ -1310,8 +1310,8 @@ void SctpAssociation::dr_on_sack(uint32_t cum, size_t newly_acked, bool cwnd_lim
 // buffers and crypto lanes, and an SSE token sent behind it waits for all of
 // them: on the MI355X host the mixed row's SSE TTFT p50 was 1.0-1.4 ms next to
 // bulk (direct 0.13-0.27 ms), the SCTP SRTT 1-2.5 ms over a 50 us path. Per
-// round trip the smallest RTT sample, less the base RTT, is the standing
-// queue; above TUNNEL_SCTP_QUEUE_US it takes cwnd down by a quarter (and ends
+// round trip the smallest RTT sample, less the base RTT (the smallest sample
+// of the last 5-10 s), is the standing queue; above TUNNEL_SCTP_QUEUE_US it takes cwnd down by a quarter (and ends
 // slow start), never below TUNNEL_SCTP_QUEUE_FLOOR_KB. WAN paths (base RTT >=
 // kLongPathUs) keep the loss-based response alone, as do paths whose queue
 // stays under the target.
@@ -1324,7 +1324,16 @@ void SctpAssociation::queue_bound(uint32_t cum, uint64_t rtt_sample) {
     const char* e = getenv("TUNNEL_SCTP_QUEUE_FLOOR_KB");
     return size_t(e && *e ? std::max(64, atoi(e)) : 1024) * 1024;
   }();
-  if (rtt_sample) qb_min_ = std::min(qb_min_, rtt_sample);
+  if (rtt_sample) {
+    qb_min_ = std::min(qb_min_, rtt_sample);
+    const uint64_t now = Reactor::now_us();
+    if (!qb_base_t0_ || now - qb_base_t0_ > 5000000) {
+      qb_base_prev_ = qb_base_cur_;
+      qb_base_cur_ = UINT64_MAX;
+      qb_base_t0_ = now;
+    }
+    qb_base_cur_ = std::min(qb_base_cur_, rtt_sample);
+  }
   if (!qb_active_) {
     qb_active_ = true;
     qb_end_ = next_tsn_ - 1;
@@ -1337,8 +1346,9 @@ void SctpAssociation::queue_bound(uint32_t cum, uint64_t rtt_sample) {
   qb_min_ = UINT64_MAX;
   if (round_min == UINT64_MAX) return;
   qb_last_ = round_min;
-  if (!target_us || !min_rtt_us_ || min_rtt_us_ >= kLongPathUs) return;
-  if (round_min <= min_rtt_us_ + target_us || cwnd_ <= floor_bytes) return;
+  const uint64_t base = std::min(qb_base_cur_, qb_base_prev_);
+  if (!target_us || base == UINT64_MAX || base >= kLongPathUs) return;
+  if (round_min <= base + target_us || cwnd_ <= floor_bytes) return;
   cwnd_ = std::max(floor_bytes, cwnd_ - cwnd_ / 4);
   ssthresh_ = std::min(ssthresh_, cwnd_);
   partial_acked_ = 0;

@@ -272,6 +272,10 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   uint32_t qb_end_ = 0;
   bool qb_active_ = false;
   uint64_t qb_min_ = UINT64_MAX, qb_last_ = 0;
+  // The bound's base RTT: the smallest sample of the last 5-10 s (two 5 s
+  // buckets), so a path whose base RTT rises (a route change, a peer that
+  // moved) is not read as a standing queue forever.
+  uint64_t qb_base_cur_ = UINT64_MAX, qb_base_prev_ = UINT64_MAX, qb_base_t0_ = 0;
   bool hs_done_ = false, hs_css_ = false, hs_round_ = false;
   int hs_samples_ = 0, hs_css_rounds_ = 0;
   uint32_t hs_window_end_ = 0;
