@@ -36,6 +36,11 @@ bool DataChannel::send(const uint8_t* hdr, size_t hlen, const Bytes& payload) {
   return send_impl(hdr, hlen, payload, false);
 }
 
+void DataChannel::note_interactive() {
+  auto pc = pc_.lock();
+  if (pc && pc->sctp_) pc->sctp_->note_interactive();
+}
+
 // `urgent`: the SCTP priority queue (one-chunk messages only), ahead of bulk
 // messages not yet started; the receiver keeps each stream's order (SSN).
 bool DataChannel::send_impl(const uint8_t* hdr, size_t hlen, const Bytes& payload, bool urgent) {

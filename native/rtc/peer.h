@@ -53,6 +53,7 @@ class DataChannel : public MessageChannel, public std::enable_shared_from_this<D
   DataChannel(std::weak_ptr<PeerConnection> pc, std::string label) : pc_(std::move(pc)), label_(std::move(label)) {}
   bool send(const uint8_t* hdr, size_t hlen, const Bytes& payload) override;
   bool send_urgent(const uint8_t* hdr, size_t hlen, const Bytes& payload) override;
+  void note_interactive() override;
   size_t buffered_amount() const override;
   bool is_open() const override { return open_ && !closed_; }
   void close() override;

@@ -129,6 +129,9 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   uint64_t rto_us() const { return rto_us_; }
   void set_mtu(size_t mtu);
   void set_initial_cwnd(size_t c) { if (c > cwnd_) cwnd_ = c; }
+  // Interactive traffic is flowing (see queue_bound()): the tighter queue
+  // bound applies for the next 200 ms.
+  void note_interactive();
   void request_stream_reset(uint16_t stream);
 
   std::function<void()> on_established;
@@ -276,6 +279,7 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   // buckets), so a path whose base RTT rises (a route change, a peer that
   // moved) is not read as a standing queue forever.
   uint64_t qb_base_cur_ = UINT64_MAX, qb_base_prev_ = UINT64_MAX, qb_base_t0_ = 0;
+  uint64_t interactive_until_us_ = 0;
   bool hs_done_ = false, hs_css_ = false, hs_round_ = false;
   int hs_samples_ = 0, hs_css_rounds_ = 0;
   uint32_t hs_window_end_ = 0;

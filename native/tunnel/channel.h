@@ -31,6 +31,9 @@ class MessageChannel {
   // a transport with a priority path may send it ahead of bulk messages it
   // holds unsent. Per-stream order is the transport's to keep.
   virtual bool send_urgent(const uint8_t* hdr, size_t hlen, const Bytes& payload) { return send(hdr, hlen, payload); }
+  // Interactive traffic (a token-sized body frame) is flowing right now: a
+  // transport may trade some bulk throughput for a shorter queue while it does.
+  virtual void note_interactive() {}
   // Bytes accepted by send() but not yet handed to the network.
   virtual size_t buffered_amount() const = 0;
   virtual bool is_open() const = 0;

@@ -77,6 +77,13 @@ void FrameScheduler::send(proto::Frame f) {
       bypass_) {
     auto it = streams_.find(f.stream_id);
     if (it == streams_.end() || it->second.q.empty()) {
+      // A small body frame of a stream that has not moved bulk is a token
+      // (headers and end frames, and the short last body frame of a 1 MB
+      // upload, take this path too but say nothing about interactivity).
+      if (f.type == proto::MsgType::ResBody || f.type == proto::MsgType::ReqBody) {
+        auto sv = sent_.find(f.stream_id);
+        if (sv == sent_.end() || sv->second < kBulkSent) ch_->note_interactive();
+      }
       emit(f, true);
       bypassed_++;
       return;

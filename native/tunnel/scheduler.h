@@ -42,6 +42,7 @@ namespace p2pt {
 class FrameScheduler {
  public:
   static constexpr size_t kInteractive = 4096;
+  static constexpr uint64_t kBulkSent = 256 * 1024;  // a stream past this is bulk, not interactive
   static constexpr uint64_t kFifoBytes = 2u << 20;
 
   explicit FrameScheduler(std::shared_ptr<MessageChannel> ch, size_t window = 64 * 1024);
