@@ -80,9 +80,15 @@ void FrameScheduler::send(proto::Frame f) {
       // A small body frame of a stream that has not moved bulk is a token
       // (headers and end frames, and the short last body frame of a 1 MB
       // upload, take this path too but say nothing about interactivity).
+      // Evidence is a stream's second small body frame: a bulk response's
+      // first read from its upstream is often small too, and counting it kept
+      // the tighter bound on through a 64 x 1 MB echo.
       if (f.type == proto::MsgType::ResBody || f.type == proto::MsgType::ReqBody) {
         auto sv = sent_.find(f.stream_id);
-        if (sv == sent_.end() || sv->second < kBulkSent) ch_->note_interactive();
+        if ((sv == sent_.end() || sv->second < kBulkSent) && ++small_[f.stream_id] >= 2) ch_->note_interactive();
+        if (small_.size() > kRemember) small_.erase(small_.begin());
+      } else if (last_frame(f) && !small_.empty()) {
+        small_.erase(f.stream_id);
       }
       emit(f, true);
       bypassed_++;
@@ -123,6 +129,7 @@ bool FrameScheduler::last_frame(const proto::Frame& f) {
 void FrameScheduler::remember(const proto::Frame& f) {
   if (last_frame(f)) {
     if (!sent_.empty()) sent_.erase(f.stream_id);
+    if (!small_.empty()) small_.erase(f.stream_id);
   } else if (f.wire_size() > kInteractive) {
     sent_[f.stream_id] += f.wire_size();
     if (sent_.size() > kRemember) sent_.erase(sent_.begin());
