@@ -131,6 +131,10 @@ def main():
     ap.add_argument("--extra", default="", help="extra flags for both tunnel processes")
     ap.add_argument("--steady-mb", type=int, default=0,
                     help="steady-state goodput rows: downloads of this many MB each (0: off)")
+    ap.add_argument("--steady-seconds", type=float, default=0,
+                    help="size each steady row to at least this many seconds at its bottleneck rate "
+                         "(MB per download = max(--steady-mb, rate x seconds / downloads)), so slow start "
+                         "is a small part of the row at high rates")
     ap.add_argument("--steady-streams", type=int, default=4)
     ap.add_argument("--steady-rates", default="200,1000", help="bottleneck Mbit/s of the steady rows")
     ap.add_argument("--steady-rtts", default="20,50")
@@ -153,7 +157,8 @@ def main():
                     for loss in [float(x) for x in a.steady_losses.split(",") if x]:
                         for q in [float(x) for x in a.steady_queues.split(",") if x != ""]:
                             qkb = q or max(64.0, rate * 1e6 / 8 * rtt / 1e3 / 1024)
-                            row = steady_row(mport, rtt, loss, rate, qkb, a.steady_mb, a.steady_streams, extra)
+                            mb = max(a.steady_mb, int(rate / 8 * a.steady_seconds / a.steady_streams))
+                            row = steady_row(mport, rtt, loss, rate, qkb, mb, a.steady_streams, extra)
                             res["steady"].append(row)
                             print(json.dumps(row), file=sys.stderr, flush=True)
         for rtt in [float(x) for x in a.rtts.split(",") if x]:
