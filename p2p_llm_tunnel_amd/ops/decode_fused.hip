@@ -553,14 +553,14 @@ __global__ __launch_bounds__(256) void k_embed(const uint16_t* __restrict__ embe
 // to finish merges, its waves taking different heads.
 // Row b reads cache slot slot[b] (rows may share a slot: chunked prefill) and
 // attends to positions 0..pos[b]; the output is bf16 [B][H*D].
-template <int D, int G>
-__global__ __launch_bounds__(512) void k_attn(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+template <int D, int G, int TOK = 32>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(TOK == 16 ? 4 : 1))) void k_attn(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
                                               const uint16_t* __restrict__ vc, const int* __restrict__ pos,
                                               const int* __restrict__ slot, int nslots, float* __restrict__ part_o,
                                               float* __restrict__ part_ml, unsigned* __restrict__ counters,
                                               uint16_t* __restrict__ out, int H, int Hkv, int Smax, int nsplit,
                                               float scale, int min_span) {
-  constexpr int TOK = 32, NWV = 8;
+  constexpr int NWV = 8;
   constexpr int DPL = D / kWave;  // merges: dims per lane
   constexpr int MAXC = 16;        // partials merged per load batch
   constexpr int LPR = D / 8, RPI = kWave / LPR, NI = TOK / RPI;
@@ -1038,7 +1038,11 @@ int env_int(const char* name, int dflt) {
 // at most the workspace's partial slots.
 int attn_slots(int B, int Hkv, int nsplit_ws) {
   static const int cap = env_int("P2PT_ATTN_SLOTS", 16);
-  int sl = 256 / std::max(1, B * Hkv);
+  // Target workgroups of the launch: 256 (one 512-thread, 234-VGPR workgroup
+  // per CU). More slots per row are slower: b16 0.522 / 0.567 / 0.597 /
+  // 0.645 ms at 256 / 512 / 768 / 1024 (profiles/r03/decode/attn_grid_sweep_head.log).
+  static const int wgs = std::max(1, env_int("P2PT_ATTN_WGS", 256));
+  int sl = wgs / std::max(1, B * Hkv);
   return std::max(1, std::min({sl, cap, nsplit_ws}));
 }
 
@@ -1047,6 +1051,16 @@ int attn_slots(int B, int Hkv, int nsplit_ws) {
 // the workgroups of 256 (one piece per wave): at batch 1 and 1k tokens the
 // decode step went 396 -> 380 us on MI355X, unchanged at batch 16
 // (profiles/r02/decode/decode_sweep_s4.log). P2PT_ATTN_MINSPAN overrides.
+// Tokens per wave piece: 32, or 16 (half the K/V registers: 128 instead of
+// 234 VGPRs, so two 8-wave workgroups fit a CU). Occupancy is not what bounds
+// the kernel: 16 measured slower at every batch on MI355X (small, ctx 1024:
+// b1 0.358 -> 0.365 ms, b16 0.522 -> 0.531, b64 1.125 -> 1.134;
+// profiles/r03/decode/attn_tok_ab_head.log). P2PT_ATTN_TOK=16 opts in.
+int attn_tok() {
+  static const int v = env_int("P2PT_ATTN_TOK", 32) == 16 ? 16 : 32;
+  return v;
+}
+
 int attn_min_span() {
   static const int v = std::max(32, env_int("P2PT_ATTN_MINSPAN", 64) / 32 * 32);
   return v;
@@ -1351,8 +1365,15 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
       const float scale = 1.f / sqrtf(float(d.D));
       const int G = d.H / d.Hkv;
 #define P2PT_ATTN(DD, GG)                                                                                          \
-  hipLaunchKernelGGL((k_attn<DD, GG>), grid, dim3(512), 0, s, W.q, kc, vc, pos, slots, d.max_batch, W.part_o,    \
-                     W.part_ml, W.counters, W.attn, d.H, d.Hkv, d.max_seq, nsplit_ws, scale, attn_min_span())
+  do {                                                                                                             \
+    if (attn_tok() == 16)                                                                                          \
+      hipLaunchKernelGGL((k_attn<DD, GG, 16>), grid, dim3(512), 0, s, W.q, kc, vc, pos, slots, d.max_batch,      \
+                         W.part_o, W.part_ml, W.counters, W.attn, d.H, d.Hkv, d.max_seq, nsplit_ws, scale,        \
+                         attn_min_span());                                                                         \
+    else                                                                                                           \
+      hipLaunchKernelGGL((k_attn<DD, GG>), grid, dim3(512), 0, s, W.q, kc, vc, pos, slots, d.max_batch, W.part_o, \
+                         W.part_ml, W.counters, W.attn, d.H, d.Hkv, d.max_seq, nsplit_ws, scale, attn_min_span());\
+  } while (0)
       if (d.D == 64) {
         if (G == 1) P2PT_ATTN(64, 1); else if (G == 2) P2PT_ATTN(64, 2); else if (G == 4) P2PT_ATTN(64, 4); else P2PT_ATTN(64, 8);
       } else {
