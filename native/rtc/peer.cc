@@ -433,6 +433,8 @@ void PeerConnection::start_sctp() {
   sc.remote_port = remote_.sctp_port;
   sc.zero_checksum = true;  // SCTP runs over DTLS (RFC 8261), EDMID 1
   if (jumbo) sc.initial_cwnd = cfg_.jumbo_initial_cwnd;
+  if (const char* e = getenv("TUNNEL_SCTP_RWND_KB"); e && *e)  // advertised receive window (default 8 MiB)
+    sc.rwnd = uint32_t(std::clamp(atoi(e), 256, 1 << 20)) * 1024u;
   std::weak_ptr<PeerConnection> w = shared_from_this();
   // Record crypto and UDP sends of bulk flushes off this thread (rtc/datapath.h).
   dtls_->enable_lanes([w](TxTarget& t) {
