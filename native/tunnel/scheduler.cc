@@ -21,8 +21,10 @@ bool FrameScheduler::emit(const proto::Frame& f, bool urgent) {
   uint8_t hdr[proto::kHeaderLen];
   f.header(hdr);
   // Trace: a stream's first response body frame leaves the scheduler for the channel.
-  if (f.type == proto::MsgType::ResBody && trace::enabled() && traced_.insert(f.stream_id).second)
-    trace::event("serve", f.stream_id, "chan_tx");
+  if (f.type == proto::MsgType::ResBody && trace::enabled()) {
+    if (traced_.size() >= (1u << 16)) traced_.clear();  // bounded on long traced runs
+    if (traced_.insert(f.stream_id).second) trace::event("serve", f.stream_id, "chan_tx");
+  }
   metrics::frame_sent(uint8_t(f.type), f.wire_size());
   emitted_++;
   return urgent ? ch_->send_urgent(hdr, sizeof hdr, f.payload) : ch_->send(hdr, sizeof hdr, f.payload);
