@@ -11,6 +11,7 @@
 #include <sched.h>
 
 #include <cerrno>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -30,12 +31,22 @@ static const char* kVersion = "0.2.0";
 
 namespace {
 
+// Value kinds checked after parsing (clap's value parsers, cli.rs:13-68, reject
+// what does not parse; a bare strtoull would turn "x" into 0).
+enum class Kind { Str, Flag, U64, U64OrAuto };
+
+// Which subcommand accepts an extension (clap rejects a flag the subcommand
+// does not define, so `tunnel proxy --max-request-body 1` is an error).
+enum class Role { Both, Serve, Proxy };
+
 struct Opt {
   const char* name;
   const char* env;
   const char* dflt;
   const char* help;
-  bool flag = false;  // boolean switch
+  Kind kind = Kind::Str;
+  Role role = Role::Both;
+  uint64_t lo = 0, hi = UINT64_MAX;  // accepted range of a numeric value
 };
 
 const std::vector<Opt>& serve_opts() {
@@ -68,36 +79,37 @@ const std::vector<Opt>& ext_opts() {
   static const std::vector<Opt> o = {
       {"transport", "TUNNEL_TRANSPORT", "webrtc", "webrtc | tcp-listen:HOST:PORT | tcp-connect:HOST:PORT"},
       {"stun", "TUNNEL_STUN", "stun:stun.l.google.com:19302", "STUN server(s), comma-separated; 'none' disables"},
-      {"no-loopback-candidates", nullptr, nullptr, "Do not gather 127.0.0.1 host candidates", true},
-      {"ipv6", nullptr, nullptr, "Gather IPv6 host candidates", true},
-      {"ipv6-only", nullptr, nullptr, "Gather host candidates on IPv6 interfaces only", true},
-      {"ice-relay-only", nullptr, nullptr, "Only use TURN-relayed candidates (iceTransportPolicy=relay)", true},
-      {"gather-timeout-ms", "TUNNEL_GATHER_TIMEOUT_MS", "5000", "Max wait for ICE gathering before sending SDP"},
-      {"ice-timeout-ms", "TUNNEL_ICE_TIMEOUT_MS", "30000", "No traffic for this long => connection failed"},
-      {"sctp-mtu", "TUNNEL_SCTP_MTU", "1200", "SCTP packet size budget (bytes)"},
-      {"no-jumbo-loopback", nullptr, nullptr, "Disable large SCTP packets on loopback paths", true},
-      {"max-retries", "TUNNEL_MAX_RETRIES", "4294967295", "Give up after this many failed attempts"},
-      {"reset-backoff-after", "TUNNEL_RESET_BACKOFF_AFTER", "0", "Reset backoff after a session lasted N s (0=never)"},
-      {"ping-interval-ms", "TUNNEL_PING_INTERVAL_MS", "10000", "Keepalive PING interval"},
-      {"pong-timeout-ms", "TUNNEL_PONG_TIMEOUT_MS", "0", "Fail the session if no PONG for this long (0=off)"},
-      {"header-timeout-ms", "TUNNEL_HEADER_TIMEOUT_MS", "60000", "Proxy wait for response headers (504 after)"},
-      {"handshake-timeout-ms", "TUNNEL_HANDSHAKE_TIMEOUT_MS", "300000", "HELLO/AGREE timeout"},
-      {"listen-early", nullptr, nullptr, "proxy: bind before the tunnel is up and answer 503 until ready", true},
+      {"no-loopback-candidates", nullptr, nullptr, "Do not gather 127.0.0.1 host candidates", Kind::Flag},
+      {"ipv6", nullptr, nullptr, "Gather IPv6 host candidates", Kind::Flag},
+      {"ipv6-only", nullptr, nullptr, "Gather host candidates on IPv6 interfaces only", Kind::Flag},
+      {"ice-relay-only", nullptr, nullptr, "Only use TURN-relayed candidates (iceTransportPolicy=relay)", Kind::Flag},
+      {"gather-timeout-ms", "TUNNEL_GATHER_TIMEOUT_MS", "5000", "Max wait for ICE gathering before sending SDP", Kind::U64},
+      {"ice-timeout-ms", "TUNNEL_ICE_TIMEOUT_MS", "30000", "No traffic for this long => connection failed", Kind::U64},
+      {"sctp-mtu", "TUNNEL_SCTP_MTU", "1200", "SCTP packet size budget (bytes)", Kind::U64, Role::Both, 576, 65535},
+      {"no-jumbo-loopback", nullptr, nullptr, "Disable large SCTP packets on loopback paths", Kind::Flag},
+      {"max-retries", "TUNNEL_MAX_RETRIES", "4294967295", "Give up after this many failed attempts", Kind::U64},
+      {"reset-backoff-after", "TUNNEL_RESET_BACKOFF_AFTER", "0", "Reset backoff after a session lasted N s (0=never)", Kind::U64},
+      {"ping-interval-ms", "TUNNEL_PING_INTERVAL_MS", "10000", "Keepalive PING interval", Kind::U64},
+      {"pong-timeout-ms", "TUNNEL_PONG_TIMEOUT_MS", "0", "Fail the session if no PONG for this long (0=off)", Kind::U64},
+      {"header-timeout-ms", "TUNNEL_HEADER_TIMEOUT_MS", "60000", "Proxy wait for response headers (504 after)", Kind::U64},
+      {"handshake-timeout-ms", "TUNNEL_HANDSHAKE_TIMEOUT_MS", "300000", "HELLO/AGREE timeout", Kind::U64},
+      {"listen-early", nullptr, nullptr, "proxy: bind before the tunnel is up and answer 503 until ready", Kind::Flag,
+       Role::Proxy},
       {"metrics-listen", "TUNNEL_METRICS_LISTEN", "", "Serve Prometheus metrics on HOST:PORT"},
       {"busy-poll-us", "TUNNEL_BUSY_POLL_US", "0",
-       "Keep polling for N us after I/O instead of sleeping (lower per-hop latency, more CPU)"},
+       "Keep polling for N us after I/O instead of sleeping (lower per-hop latency, more CPU)", Kind::U64},
       {"workers", "TUNNEL_WORKERS", "auto",
-       "HTTP worker threads beside the association thread (auto: one per 4 CPUs, 1..4; 0: single thread)"},
+       "HTTP worker threads beside the association thread (auto: one per 4 CPUs, 1..4; 0: single thread)", Kind::U64OrAuto, Role::Both, 0, 256},
       {"inline-streams", "TUNNEL_INLINE_STREAMS", "16",
-       "Concurrent streams handled on the association thread before new ones go to workers"},
+       "Concurrent streams handled on the association thread before new ones go to workers", Kind::U64},
       {"max-request-body", "TUNNEL_MAX_REQUEST_BODY", "0",
-       "serve: answer 413 to request bodies larger than this many bytes (0 = unlimited)"},
+       "serve: answer 413 to request bodies larger than this many bytes (0 = unlimited)", Kind::U64, Role::Serve},
       {"stream-body-threshold", "TUNNEL_STREAM_BODY_THRESHOLD", "8388608",
-       "serve: request bodies this big stream to the upstream as they arrive instead of being buffered"},
+       "serve: request bodies this big stream to the upstream as they arrive instead of being buffered", Kind::U64, Role::Serve},
       {"upstream-prewarm", "TUNNEL_UPSTREAM_PREWARM", "4",
-       "serve: spare pre-connected upstream sockets (follows peak concurrency; 0=off)"},
+       "serve: spare pre-connected upstream sockets (follows peak concurrency; 0=off)", Kind::U64, Role::Serve},
       {"upstream-prewarm-ttl-ms", "TUNNEL_UPSTREAM_PREWARM_TTL_MS", "1000",
-       "serve: close a spare upstream socket unused for this long"},
+       "serve: close a spare upstream socket unused for this long", Kind::U64, Role::Serve},
       {"secret", "TUNNEL_SECRET", "",
        "Pre-shared secret both peers must prove (HMAC bound to the DTLS fingerprints); prefer the env var"},
       {"cpu-affinity", "TUNNEL_CPU_AFFINITY", "",
@@ -119,12 +131,17 @@ void usage_main() {
          "Options:\n  -h, --help     Print help\n  -V, --version  Print version\n");
 }
 
+bool for_role(const Opt& o, const char* cmd) {
+  return o.role == Role::Both || (o.role == Role::Serve) == (strcmp(cmd, "serve") == 0);
+}
+
 void usage_sub(const char* cmd, const std::vector<Opt>& opts) {
   printf("Usage: tunnel %s [OPTIONS]\n\nOptions:\n", cmd);
   for (auto* list : {&opts, &ext_opts()}) {
     if (list == &ext_opts()) printf("\nExtensions (defaults keep reference behaviour):\n");
     for (auto& o : *list) {
-      std::string left = std::string("      --") + o.name + (o.flag ? "" : " <VALUE>");
+      if (!for_role(o, cmd)) continue;
+      std::string left = std::string("      --") + o.name + (o.kind == Kind::Flag ? "" : " <VALUE>");
       printf("%-36s %s", left.c_str(), o.help);
       if (o.env) printf(" [env: %s=]", o.env);
       if (o.dflt && *o.dflt) printf(" [default: %s]", o.dflt);
@@ -134,10 +151,38 @@ void usage_sub(const char* cmd, const std::vector<Opt>& opts) {
   printf("  -h, --help                           Print help\n");
 }
 
+// A whole unsigned decimal within [lo, hi] (clap's u64 parser: no sign, no
+// trailing text, no overflow).
+bool parse_u64(const std::string& v, uint64_t lo, uint64_t hi, uint64_t* out, std::string* why) {
+  if (v.empty()) {
+    *why = "cannot parse integer from empty string";
+    return false;
+  }
+  uint64_t x = 0;
+  for (char c : v) {
+    if (c < '0' || c > '9') {
+      *why = "invalid digit found in string";
+      return false;
+    }
+    if (x > (UINT64_MAX - uint64_t(c - '0')) / 10) {
+      *why = "number too large to fit in target type";
+      return false;
+    }
+    x = x * 10 + uint64_t(c - '0');
+  }
+  if (x < lo || x > hi) {
+    *why = std::to_string(x) + " is not in " + std::to_string(lo) + ".." + std::to_string(hi);
+    return false;
+  }
+  *out = x;
+  return true;
+}
+
 bool parse_sub(int argc, char** argv, const char* cmd, const std::vector<Opt>& opts,
                std::map<std::string, std::string>& out) {
   std::vector<Opt> all = opts;
-  for (auto& o : ext_opts()) all.push_back(o);
+  for (auto& o : ext_opts())
+    if (for_role(o, cmd)) all.push_back(o);
   for (int i = 2; i < argc; i++) {
     std::string a = argv[i];
     if (a == "-h" || a == "--help") {
@@ -163,7 +208,12 @@ bool parse_sub(int argc, char** argv, const char* cmd, const std::vector<Opt>& o
       fprintf(stderr, "error: unexpected argument '--%s' found\n\nUsage: tunnel %s [OPTIONS]\n", name.c_str(), cmd);
       return false;
     }
-    if (found->flag) {
+    if (found->kind == Kind::Flag) {
+      if (has_eq) {
+        fprintf(stderr, "error: unexpected value '%s' for '--%s' found; no more were expected\n", val.c_str(),
+                name.c_str());
+        return false;
+      }
       out[name] = "1";
       continue;
     }
@@ -179,13 +229,26 @@ bool parse_sub(int argc, char** argv, const char* cmd, const std::vector<Opt>& o
   for (auto& o : all) {
     if (out.count(o.name)) continue;
     const char* e = o.env ? getenv(o.env) : nullptr;
-    if (e && !o.flag) out[o.name] = e;
+    if (e && o.kind != Kind::Flag) out[o.name] = e;
     else if (o.dflt) out[o.name] = o.dflt;
   }
   for (auto& o : opts) {
-    if (!o.dflt && !o.flag && !out.count(o.name)) {
+    if (!o.dflt && o.kind != Kind::Flag && !out.count(o.name)) {
       fprintf(stderr, "error: the following required arguments were not provided:\n  --%s <%s>\n\nUsage: tunnel %s --%s <VALUE>\n",
               o.name, o.name, cmd, o.name);
+      return false;
+    }
+  }
+  // Numeric values, from the command line or the environment alike.
+  for (auto& o : all) {
+    if (o.kind != Kind::U64 && o.kind != Kind::U64OrAuto) continue;
+    auto it = out.find(o.name);
+    if (it == out.end() || (o.kind == Kind::U64OrAuto && it->second == "auto")) continue;
+    uint64_t v;
+    std::string why;
+    if (!parse_u64(it->second, o.lo, o.hi, &v, &why)) {
+      fprintf(stderr, "error: invalid value '%s' for '--%s <VALUE>': %s\n\nFor more information, try '--help'.\n",
+              it->second.c_str(), o.name, why.c_str());
       return false;
     }
   }
@@ -230,6 +293,7 @@ bool pin_cpus(const std::string& list, std::string* err) {
   return true;
 }
 
+// Validated by parse_sub; absent (an option of the other subcommand) reads 0.
 uint64_t num(const std::map<std::string, std::string>& m, const char* k) {
   auto it = m.find(k);
   return it == m.end() ? 0 : strtoull(it->second.c_str(), nullptr, 10);
@@ -331,13 +395,15 @@ int main(int argc, char** argv) {
   cfg.handshake_timeout_ms = num(m, "handshake-timeout-ms");
   cfg.listen_early = m.count("listen-early") > 0;
   cfg.metrics_listen = m["metrics-listen"];
-  cfg.upstream_prewarm = num(m, "upstream-prewarm");
-  cfg.upstream_prewarm_ttl_ms = num(m, "upstream-prewarm-ttl-ms");
   cfg.busy_poll_us = num(m, "busy-poll-us");
   cfg.workers = m["workers"] == "auto" ? -1 : int(num(m, "workers"));
   cfg.inline_streams = num(m, "inline-streams");
-  cfg.max_request_body = num(m, "max-request-body");
-  cfg.stream_body_threshold = num(m, "stream-body-threshold");
+  if (cmd == "serve") {
+    cfg.upstream_prewarm = num(m, "upstream-prewarm");
+    cfg.upstream_prewarm_ttl_ms = num(m, "upstream-prewarm-ttl-ms");
+    cfg.max_request_body = num(m, "max-request-body");
+    cfg.stream_body_threshold = num(m, "stream-body-threshold");
+  }
   cfg.secret = m["secret"];
   if (!m["cpu-affinity"].empty()) {
     std::string err;

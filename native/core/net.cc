@@ -1,5 +1,7 @@
 #include "core/net.h"
 
+#include <linux/sock_diag.h>
+
 #include <arpa/inet.h>
 #include <fcntl.h>
 #include <ifaddrs.h>
@@ -20,6 +22,39 @@
 #include "core/log.h"
 
 namespace p2pt {
+
+uint64_t udp_socket_drops(int fd) {
+#ifdef SO_MEMINFO
+  uint32_t mi[SK_MEMINFO_VARS] = {};
+  socklen_t l = sizeof mi;
+  if (fd >= 0 && getsockopt(fd, SOL_SOCKET, SO_MEMINFO, mi, &l) == 0 && l > SK_MEMINFO_DROPS * sizeof(uint32_t))
+    return mi[SK_MEMINFO_DROPS];
+#endif
+  return 0;
+}
+
+size_t udp_socket_rcvbuf(int fd) {
+  int v = 0;
+  socklen_t l = sizeof v;
+  if (fd < 0 || getsockopt(fd, SOL_SOCKET, SO_RCVBUF, &v, &l) != 0) return 0;
+  return size_t(v);
+}
+
+size_t udp_socket_buffers(int fd, int bytes) {
+  setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &bytes, sizeof bytes);
+  setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &bytes, sizeof bytes);
+  // The kernel doubles the request (bookkeeping overhead) and clamps it to
+  // net.core.rmem_max / wmem_max first; a clamped buffer holds only a few
+  // GSO-coalesced bursts, so try the privileged variants.
+  if (udp_socket_rcvbuf(fd) < size_t(bytes)) setsockopt(fd, SOL_SOCKET, SO_RCVBUFFORCE, &bytes, sizeof bytes);
+  int sb = 0;
+  socklen_t l = sizeof sb;
+  if (getsockopt(fd, SOL_SOCKET, SO_SNDBUF, &sb, &l) == 0 && sb < bytes)
+    setsockopt(fd, SOL_SOCKET, SO_SNDBUFFORCE, &bytes, sizeof bytes);
+  int one = 1;
+  setsockopt(fd, SOL_SOCKET, SO_RXQ_OVFL, &one, sizeof one);
+  return udp_socket_rcvbuf(fd);
+}
 
 // ---------------------------------------------------------------- SockAddr
 

@@ -44,6 +44,16 @@ struct SockAddr {
   bool operator!=(const SockAddr& o) const { return !(*this == o); }
 };
 
+// UDP socket receive-side accounting (Linux SO_MEMINFO): datagrams dropped
+// because the receive buffer was full (sk_drops, what SO_RXQ_OVFL reports per
+// datagram) and the effective receive buffer size. 0 when unavailable.
+uint64_t udp_socket_drops(int fd);
+size_t udp_socket_rcvbuf(int fd);
+// Sets SO_RCVBUF / SO_SNDBUF to `bytes`, retrying with the *FORCE variants
+// (CAP_NET_ADMIN) when net.core.[rw]mem_max clamps the request, and enables
+// SO_RXQ_OVFL. Returns the effective receive buffer.
+size_t udp_socket_buffers(int fd, int bytes);
+
 struct IfaceAddr {
   std::string name;
   SockAddr addr;

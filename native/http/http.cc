@@ -218,12 +218,48 @@ static bool parse_content_length(const Head& h, uint64_t& len, bool& present, st
   return true;
 }
 
+// The transfer codings of every Transfer-Encoding field line, in order
+// (RFC 9112 §6.1: the list is the concatenation of the field lines).
+static std::vector<std::string_view> te_codings(const Head& h) {
+  std::vector<std::string_view> out;
+  for (auto& hd : h.headers) {
+    if (!iequals(hd.name, "transfer-encoding")) continue;
+    std::string_view v = hd.value;
+    for (;;) {
+      size_t c = v.find(',');
+      std::string_view t = v.substr(0, c);
+      while (!t.empty() && (t.front() == ' ' || t.front() == '\t')) t.remove_prefix(1);
+      while (!t.empty() && (t.back() == ' ' || t.back() == '\t')) t.remove_suffix(1);
+      if (!t.empty()) out.push_back(t);
+      if (c == std::string_view::npos) break;
+      v.remove_prefix(c + 1);
+    }
+  }
+  return out;
+}
+
 BodyDecoder::Mode request_body_mode(const Head& h, uint64_t& length, std::string* err) {
   length = 0;
   if (h.get("transfer-encoding")) {
-    if (h.has_token("transfer-encoding", "chunked")) return BodyDecoder::Mode::Chunked;
-    if (err) *err = "unsupported transfer-encoding";
-    return BodyDecoder::Mode::UntilClose;  // caller treats err as fatal
+    // RFC 9112 §6.1 / §6.3: a request whose final coding is not chunked cannot
+    // be framed (400, then close); Transfer-Encoding next to Content-Length is
+    // a smuggling vector, rejected rather than read as chunked. Chunked is the
+    // only coding relayed (serve re-frames the body for the upstream), so any
+    // other coding before it is refused too.
+    auto te = te_codings(h);
+    if (te.empty() || !iequals(te.back(), "chunked")) {
+      if (err) *err = "transfer-encoding without chunked as the final coding";
+      return BodyDecoder::Mode::UntilClose;  // caller treats err as fatal
+    }
+    if (h.get("content-length")) {
+      if (err) *err = "both transfer-encoding and content-length";
+      return BodyDecoder::Mode::UntilClose;
+    }
+    if (te.size() != 1) {
+      if (err) *err = "unsupported transfer-encoding";
+      return BodyDecoder::Mode::UntilClose;
+    }
+    return BodyDecoder::Mode::Chunked;
   }
   bool present;
   if (!parse_content_length(h, length, present, err)) return BodyDecoder::Mode::UntilClose;
@@ -235,7 +271,12 @@ BodyDecoder::Mode response_body_mode(const Head& h, const std::string& method, u
   length = 0;
   if (method == "HEAD" || h.status == 204 || h.status == 304 || (h.status >= 100 && h.status < 200))
     return BodyDecoder::Mode::None;
-  if (h.has_token("transfer-encoding", "chunked")) return BodyDecoder::Mode::Chunked;
+  if (h.get("transfer-encoding")) {
+    // RFC 9112 §6.3 (3): chunked last => chunked; otherwise read until close.
+    // Transfer-Encoding overrides Content-Length.
+    auto te = te_codings(h);
+    return !te.empty() && iequals(te.back(), "chunked") ? BodyDecoder::Mode::Chunked : BodyDecoder::Mode::UntilClose;
+  }
   bool present;
   if (parse_content_length(h, length, present, nullptr) && present)
     return length ? BodyDecoder::Mode::Length : BodyDecoder::Mode::None;

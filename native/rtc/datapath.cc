@@ -81,7 +81,7 @@ void Lane::run() {
   }
 }
 
-LaneFd::LaneFd(int source) : fd(::dup(source)), src(source) {}
+LaneFd::LaneFd(int source, uint64_t generation) : fd(::dup(source)), src(source), gen(generation) {}
 LaneFd::~LaneFd() {
   if (fd >= 0) ::close(fd);
 }
@@ -213,6 +213,7 @@ void TxLaneState::run(const TxBatch& b, const RecordKeys& k, int fd, const SockA
   constexpr size_t kGsoMaxSegs = 64, kGsoMaxBytes = 60000;
   mmsghdr msgs[kBatch];
   iovec iovs[kBatch];
+  size_t first_dg[kBatch];  // index in dgs_ of each message's first datagram
   alignas(cmsghdr) char ctrl[kBatch][CMSG_SPACE(sizeof(uint16_t))];
   size_t i = 0;
   while (i < dgs_.size()) {
@@ -227,6 +228,7 @@ void TxLaneState::run(const TxBatch& b, const RecordKeys& k, int fd, const SockA
         }
       mmsghdr& m = msgs[cnt];
       memset(&m, 0, sizeof m);
+      first_dg[cnt] = i;
       iovs[cnt].iov_base = out_.data() + dgs_[i].first;
       iovs[cnt].iov_len = total;
       m.msg_hdr.msg_iov = &iovs[cnt];
@@ -242,37 +244,44 @@ void TxLaneState::run(const TxBatch& b, const RecordKeys& k, int fd, const SockA
         c->cmsg_len = CMSG_LEN(sizeof(uint16_t));
         uint16_t gs = uint16_t(seg);
         memcpy(CMSG_DATA(c), &gs, sizeof gs);
-        gso_msgs.fetch_add(1, std::memory_order_relaxed);
       }
       cnt++;
       i = j;
     }
     int sent = 0;
+    int waited_ms = 0;
     while (sent < cnt) {
       int rc = sendmmsg(fd, msgs + sent, unsigned(cnt - sent), 0);
       if (rc < 0) {
         if (errno == EINTR) continue;
         if ((errno == EIO || errno == EINVAL || errno == ENOPROTOOPT) && gso_ok_ && msgs[sent].msg_hdr.msg_controllen) {
-          // No UDP GSO on this path: datagram by datagram from here on.
+          // No UDP GSO on this path: rebuild the rest of the batch datagram by
+          // datagram (its later messages were built with UDP_SEGMENT too and
+          // would fail the same way).
           LOG_DEBUG(kT, "UDP GSO unavailable (%s); sending datagrams individually", strerror(errno));
           gso_ok_ = false;
-          const uint8_t* p = static_cast<const uint8_t*>(msgs[sent].msg_hdr.msg_iov->iov_base);
-          const size_t len = msgs[sent].msg_hdr.msg_iov->iov_len;
-          for (size_t o = 0; o < len;) {
-            size_t seg = 0;
-            for (auto& d : dgs_)
-              if (out_.data() + d.first == p + o) seg = d.second;
-            if (!seg) break;
-            sendto(fd, p + o, seg, 0, to.sa(), to.len);
-            o += seg;
-          }
-          sent++;
+          i = first_dg[sent];
+          break;
+        }
+        if ((errno == EAGAIN || errno == EWOULDBLOCK || errno == ENOBUFS) && waited_ms < kSendWaitMs) {
+          // Socket buffer full: wait (bounded) for room instead of dropping
+          // packets SCTP would have to recover by retransmission.
+          pollfd pf{fd, POLLOUT, 0};
+          send_waits.fetch_add(1, std::memory_order_relaxed);
+          const int rcp = poll(&pf, 1, 1);
+          waited_ms += 1;
+          (void)rcp;
           continue;
         }
-        // EAGAIN (socket buffer full) or unreachable: drop; SCTP retransmits.
-        send_drops.fetch_add(uint64_t(cnt - sent), std::memory_order_relaxed);
+        // Still full after the bound, or unreachable: drop; SCTP retransmits.
+        for (int k = sent; k < cnt; k++) {
+          const size_t end = k + 1 < cnt ? first_dg[k + 1] : i;
+          send_drops.fetch_add(uint64_t(end - first_dg[k]), std::memory_order_relaxed);
+        }
         break;
       }
+      for (int k = sent; k < sent + rc; k++)
+        if (msgs[k].msg_hdr.msg_controllen) gso_msgs.fetch_add(1, std::memory_order_relaxed);
       sent += rc;
     }
   }
@@ -280,9 +289,9 @@ void TxLaneState::run(const TxBatch& b, const RecordKeys& k, int fd, const SockA
 
 // ------------------------------------------------------------------ RX reader
 
-RxReader::RxReader(int fd, const SockAddr& remote, std::shared_ptr<const RecordKeys> keys, Deliver deliver)
+RxReader::RxReader(int fd, const SockAddr& remote, std::shared_ptr<const RecordKeys> keys, Deliver deliver, uint64_t id)
     : fd_(fd), stop_fd_(eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC)), remote_(remote), keys_(std::move(keys)),
-      deliver_(std::move(deliver)) {
+      deliver_(std::move(deliver)), id_(id) {
   th_ = std::thread([this] {
     sigset_t mask;
     sigemptyset(&mask);
@@ -315,14 +324,20 @@ void RxReader::done() {
 }
 
 namespace {
-size_t gro_seg(const msghdr* mh) {
-  for (cmsghdr* c = CMSG_FIRSTHDR(const_cast<msghdr*>(mh)); c; c = CMSG_NXTHDR(const_cast<msghdr*>(mh), c))
+// The GRO segment size, and the socket's drop count when SO_RXQ_OVFL reports
+// one (the kernel attaches it once drops have happened).
+size_t gro_seg(const msghdr* mh, uint32_t* ovfl) {
+  size_t seg = 0;
+  for (cmsghdr* c = CMSG_FIRSTHDR(const_cast<msghdr*>(mh)); c; c = CMSG_NXTHDR(const_cast<msghdr*>(mh), c)) {
     if (c->cmsg_level == SOL_UDP && c->cmsg_type == UDP_GRO) {
       int v = 0;
       memcpy(&v, CMSG_DATA(c), sizeof v);
-      return size_t(v);
+      seg = size_t(v);
+    } else if (c->cmsg_level == SOL_SOCKET && c->cmsg_type == SO_RXQ_OVFL) {
+      memcpy(ovfl, CMSG_DATA(c), sizeof *ovfl);
     }
-  return 0;
+  }
+  return seg;
 }
 }  // namespace
 
@@ -377,7 +392,7 @@ void RxReader::run() {
   mmsghdr msgs[kBatch];
   iovec iovs[kBatch];
   sockaddr_storage from[kBatch];
-  alignas(cmsghdr) char ctrl[kBatch][CMSG_SPACE(sizeof(int))];
+  alignas(cmsghdr) char ctrl[kBatch][CMSG_SPACE(sizeof(int)) + CMSG_SPACE(sizeof(uint32_t))];
   RawBufPtr slots[kBatch];
   pollfd pf[2] = {{fd_.fd, POLLIN, 0}, {stop_fd_, POLLIN, 0}};
   while (!stop_.load(std::memory_order_acquire)) {
@@ -391,6 +406,7 @@ void RxReader::run() {
     }
     if (poll(pf, 2, 100) <= 0 || (pf[1].revents & POLLIN)) continue;  // the loop head sees stop_
     auto burst = std::make_unique<Burst>();
+    burst->reader = id_;
     for (int round = 0; round < 8; round++) {
       for (int i = 0; i < kBatch; i++) {
         slots[i] = pool_.get();
@@ -411,7 +427,9 @@ void RxReader::run() {
         memcpy(&a.ss, &from[i], msgs[i].msg_hdr.msg_namelen);
         a.len = msgs[i].msg_hdr.msg_namelen;
         const uint32_t total = msgs[i].msg_len;
-        const uint32_t seg = uint32_t(gro_seg(&msgs[i].msg_hdr));
+        uint32_t ovfl = 0;
+        const uint32_t seg = uint32_t(gro_seg(&msgs[i].msg_hdr, &ovfl));
+        if (ovfl > rxq_ovfl.load(std::memory_order_relaxed)) rxq_ovfl.store(ovfl, std::memory_order_relaxed);
         if (!seg || seg >= total) {
           segment(slots[i], 0, total, a, *burst);
         } else {

@@ -73,8 +73,9 @@ class Lane {
 // never points a queued batch at another socket.
 struct LaneFd {
   int fd = -1;
-  int src = -1;  // the agent's descriptor it duplicates
-  explicit LaneFd(int source);
+  int src = -1;      // the agent's descriptor it duplicates
+  uint64_t gen = 0;  // the ICE path generation it was taken for (an fd number can be reused)
+  explicit LaneFd(int source, uint64_t generation = 0);
   ~LaneFd();
 };
 
@@ -84,6 +85,7 @@ struct TxTarget {
   int fd = -1;
   SockAddr to;
   size_t coalesce = 0;
+  uint64_t gen = 0;  // IceAgent::path_generation() of this target
 };
 
 // One flush's records: inline bytes (SCTP headers, small chunks) copied into
@@ -172,7 +174,10 @@ class TxLaneState {
  public:
   // Seals the batch and sends it to target (runs on the lane).
   void run(const TxBatch& b, const RecordKeys& k, int fd, const SockAddr& to, size_t coalesce);
-  std::atomic<uint64_t> batches{0}, records{0}, datagrams{0}, gso_msgs{0}, send_drops{0};
+  // send_drops: datagrams dropped (socket buffer still full after kSendWaitMs
+  // of POLLOUT waits, or unreachable); send_waits: POLLOUT waits taken.
+  std::atomic<uint64_t> batches{0}, records{0}, datagrams{0}, gso_msgs{0}, send_drops{0}, send_waits{0};
+  static constexpr int kSendWaitMs = 20;
 
  private:
   std::vector<uint8_t> out_;
@@ -198,17 +203,22 @@ class RxReader {
   struct Burst {
     RxBatch opened;         // application records, authenticated (ok) or not
     std::vector<Raw> raw;   // datagrams for the ICE agent / DTLS state machine
+    uint64_t reader = 0;    // id of the RxReader that read it (done() goes to that one only)
+    int si = -1;            // the ICE socket index it was read from (set by the deliver hook)
   };
   using Deliver = std::function<void(std::unique_ptr<Burst>)>;
   static constexpr int kMaxOutstanding = 4;
 
-  RxReader(int fd, const SockAddr& remote, std::shared_ptr<const RecordKeys> keys, Deliver deliver);
+  RxReader(int fd, const SockAddr& remote, std::shared_ptr<const RecordKeys> keys, Deliver deliver, uint64_t id = 0);
+  uint64_t id() const { return id_; }
   ~RxReader();  // stops and joins; bursts already delivered stay valid
   RxReader(const RxReader&) = delete;
   RxReader& operator=(const RxReader&) = delete;
   void done();  // association thread: one delivered burst processed
 
   std::atomic<uint64_t> bursts{0}, datagrams{0}, records{0}, raw_datagrams{0}, waits{0}, gro_batches{0};
+  // The socket's drop count as last reported by SO_RXQ_OVFL (cumulative).
+  std::atomic<uint32_t> rxq_ovfl{0};
 
  private:
   void run();
@@ -218,6 +228,7 @@ class RxReader {
   SockAddr remote_;
   std::shared_ptr<const RecordKeys> keys_;
   Deliver deliver_;
+  uint64_t id_ = 0;
   BufPool pool_{65536};
   std::mutex mu_;
   std::condition_variable cv_;

@@ -741,7 +741,7 @@ void DtlsTransport::commit_tx() {
     inline_tx_batches_++;
     return;
   }
-  if (!lane_fd_ || lane_fd_->src != t.fd) lane_fd_ = std::make_shared<LaneFd>(t.fd);
+  if (!lane_fd_ || lane_fd_->src != t.fd || lane_fd_->gen != t.gen) lane_fd_ = std::make_shared<LaneFd>(t.fd, t.gen);
   auto b = std::move(tx_pend_);
   tx_pend_ = tx_pool_->get();
   lane_tx_batches_++;

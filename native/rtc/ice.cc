@@ -159,6 +159,19 @@ size_t IceAgent::gro_segment(const msghdr* mh) {
   return 0;
 }
 
+uint64_t IceAgent::rx_overflow() const {
+  uint64_t n = 0;
+  for (auto& s : socks_) n += udp_socket_drops(s.fd);
+  for (auto& np : nat_ports_) n += udp_socket_drops(np.fd);
+  return n;
+}
+
+size_t IceAgent::rcvbuf_bytes() const {
+  if (sel_local_ < 0 || sel_local_ >= int(locals_.size())) return 0;
+  const int si = locals_[size_t(sel_local_)].sock;
+  return si >= 0 && si < int(socks_.size()) ? udp_socket_rcvbuf(socks_[size_t(si)].fd) : 0;
+}
+
 void IceAgent::open_sockets() {
   auto addrs = local_addresses(cfg_.include_loopback, cfg_.include_ipv6 || cfg_.ipv6_only);
   if (cfg_.ipv6_only)
@@ -175,9 +188,8 @@ void IceAgent::open_sockets() {
       int one = 1;
       setsockopt(fd, IPPROTO_IPV6, IPV6_V6ONLY, &one, sizeof one);
     }
-    int buf = 4 << 20;
-    setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &buf, sizeof buf);
-    setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &buf, sizeof buf);
+    const size_t rb = udp_socket_buffers(fd, 4 << 20);
+    LOG_DEBUG(kT, "UDP socket %s: receive buffer %zu bytes", ia.addr.str().c_str(), rb);
     enable_gro(fd);
     SockAddr a = ia.addr;
     a.set_port(0);
@@ -774,7 +786,9 @@ void IceAgent::on_readable(int si) {
   mmsghdr msgs[kBatch];
   iovec iovs[kBatch];
   sockaddr_storage from[kBatch];
-  alignas(cmsghdr) char ctrl[kBatch][CMSG_SPACE(sizeof(int))];
+  // Room for UDP_GRO and SO_RXQ_OVFL (a truncated GRO cmsg would read a
+  // coalesced burst as one datagram).
+  alignas(cmsghdr) char ctrl[kBatch][CMSG_SPACE(sizeof(int)) + CMSG_SPACE(sizeof(uint32_t))];
   for (int round = 0; round < 8 && !closed_; round++) {
     for (int i = 0; i < kBatch; i++) rxpool_[i].reset();
     for (int i = 0; i < kBatch; i++) {
@@ -843,9 +857,7 @@ int IceAgent::nat_fd_for(int si, const SockAddr& to) {
     np.fd = ::socket(socks_[si].addr.family(), SOCK_DGRAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
     SockAddr a = socks_[si].addr;
     a.set_port(0);
-    int buf = 4 << 20;
-    setsockopt(np.fd, SOL_SOCKET, SO_RCVBUF, &buf, sizeof buf);
-    setsockopt(np.fd, SOL_SOCKET, SO_SNDBUF, &buf, sizeof buf);  // no GRO: read with plain recvfrom
+    udp_socket_buffers(np.fd, 4 << 20);  // no GRO: read with plain recvfrom
     if (np.fd < 0 || ::bind(np.fd, a.sa(), a.len) < 0) return socks_[si].fd;
     np.ext.len = sizeof np.ext.ss;
     getsockname(np.fd, np.ext.sa(), &np.ext.len);
@@ -896,6 +908,7 @@ void IceAgent::handle_datagram(int, int si, const SockAddr& from, const uint8_t*
     if (li >= 0 && find_remote(from) >= 0) {
       sel_local_ = li;
       sel_remote_ = from;
+      path_gen_++;
     }
   }
   if (!on_data) return;
@@ -1068,6 +1081,7 @@ void IceAgent::handle_response(const SockAddr& from, const stun::Message& m, con
 void IceAgent::select_pair(int pi) {
   Pair& pr = pairs_[pi];
   sel_pair_ = pi;
+  if (sel_local_ != pr.local || sel_remote_ != remotes_[pr.remote].addr) path_gen_++;
   sel_local_ = pr.local;
   sel_remote_ = remotes_[pr.remote].addr;
   LOG_DEBUG(kT, "ICE selected pair %s", selected_desc().c_str());

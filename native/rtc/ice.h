@@ -125,6 +125,10 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   // DTLS TX lane): false with no pair, a TURN relay, or NAT / WAN / fault
   // emulation, all of which live in this agent's own send path.
   bool direct_target(int* fd, SockAddr* to, size_t* coalesce) const;
+  // Bumped whenever the selected pair (local socket or remote address)
+  // changes: readers and lanes bound to the old path restart on it.
+  uint64_t path_generation() const { return path_gen_; }
+  void test_bump_path_generation() { path_gen_++; }  // tests: as if the pair had switched
   // An outside reader (the DTLS RX reader, rtc/datapath.h) takes over the
   // selected direct pair's socket: its reactor reads stop until reattach().
   // False when direct_target() does not hold.
@@ -139,6 +143,11 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   bool selected_same_host() const;
   std::string selected_desc() const;
   IceState state() const { return state_; }
+  // Datagrams the kernel dropped on this agent's sockets because their
+  // receive buffer was full (sk_drops, the count SO_RXQ_OVFL reports; read
+  // with SO_MEMINFO), and the selected socket's effective receive buffer.
+  uint64_t rx_overflow() const;
+  size_t rcvbuf_bytes() const;
   // Send every queued datagram (sendmmsg, grouped by socket).
   void flush();
 
@@ -252,6 +261,7 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   uint64_t flush_hook_ = 0;
   bool closed_ = false;
   int detached_ = -1;  // socket index read by an outside reader
+  uint64_t path_gen_ = 0;
   // Outgoing datagrams for the current batch.
   struct Out {
     int local;

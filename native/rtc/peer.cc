@@ -28,8 +28,12 @@ const char* pc_state_name(PcState s) {
 
 constexpr size_t kPrioritySmallFrame = 1024;
 
+// The SCTP priority queue only shortens delivery when the frame rides an SCTP
+// stream of its own (negotiated `multistream` lanes): on the one ordered
+// stream the receiver holds it until every earlier SSN has arrived, so
+// sending it ahead of queued bulk would only push traffic beyond cwnd.
 bool DataChannel::send_urgent(const uint8_t* hdr, size_t hlen, const Bytes& payload) {
-  return send_impl(hdr, hlen, payload, hlen + payload.size() <= kPrioritySmallFrame);
+  return send_impl(hdr, hlen, payload, lanes_ && hlen + payload.size() <= kPrioritySmallFrame);
 }
 
 bool DataChannel::send(const uint8_t* hdr, size_t hlen, const Bytes& payload) {
@@ -207,6 +211,10 @@ PeerConnection::~PeerConnection() { close(); }
 
 void PeerConnection::flush() {
   if (closed_) return;
+  // The selected pair changed under the socket reader (a pair switch or the
+  // peer rebinding): give the old socket back to the ICE agent and read the
+  // new pair's instead of forwarding everything through the slow path.
+  if (rx_reader_ && ice_ && ice_->path_generation() != rx_reader_gen_) restart_rx_reader();
   if (dtls_) dtls_->commit_rx();
   if (sctp_) sctp_->flush();
   if (dtls_) dtls_->commit_tx();
@@ -219,21 +227,33 @@ void PeerConnection::start_rx_reader() {
   SockAddr remote;
   if (!ice_->detach_reader(&fd, &si, &remote)) return;
   rx_reader_si_ = si;
+  rx_reader_gen_ = ice_->path_generation();
   std::weak_ptr<PeerConnection> w = shared_from_this();
   Reactor* r = &r_;
-  rx_reader_ = std::make_unique<RxReader>(fd, remote, dtls_->record_keys(), [w, r](std::unique_ptr<RxReader::Burst> b) {
+  rx_reader_ = std::make_unique<RxReader>(fd, remote, dtls_->record_keys(), [w, r, si](std::unique_ptr<RxReader::Burst> b) {
+    b->si = si;
     std::shared_ptr<RxReader::Burst> sb(std::move(b));
     r->post_threadsafe([w, sb] {
       if (auto s = w.lock()) s->on_rx_burst(*sb);
     });
-  });
+  }, ++rx_reader_ids_);
   LOG_DEBUG(kT, "UDP socket reader on for %s", remote.str().c_str());
+}
+
+void PeerConnection::restart_rx_reader() {
+  LOG_DEBUG(kT, "selected pair changed (generation %llu -> %llu): restarting the UDP socket reader",
+            static_cast<unsigned long long>(rx_reader_gen_), static_cast<unsigned long long>(ice_->path_generation()));
+  rx_reader_.reset();  // joins; bursts it already posted still arrive (their done() is ignored)
+  ice_->reattach_reader(rx_reader_si_);
+  rx_reader_si_ = -1;
+  rx_reader_restarts_++;
+  start_rx_reader();
 }
 
 // A burst from the socket reader: opened records up the stack (replay check
 // in DTLS), the rest through the ICE agent as if it had read them.
 void PeerConnection::on_rx_burst(RxReader::Burst& b) {
-  if (rx_reader_) rx_reader_->done();
+  if (rx_reader_ && rx_reader_->id() == b.reader) rx_reader_->done();
   if (closed_) return;
   auto self = shared_from_this();
   if (!b.opened.recs.empty()) {
@@ -242,7 +262,7 @@ void PeerConnection::on_rx_burst(RxReader::Burst& b) {
   }
   for (auto& raw : b.raw) {
     if (closed_ || !ice_) break;
-    ice_->inject(rx_reader_si_, raw.from, raw.buf, raw.off, raw.len);
+    ice_->inject(b.si, raw.from, raw.buf, raw.off, raw.len);
   }
 }
 
@@ -439,7 +459,9 @@ void PeerConnection::start_sctp() {
   // Record crypto and UDP sends of bulk flushes off this thread (rtc/datapath.h).
   dtls_->enable_lanes([w](TxTarget& t) {
     auto s = w.lock();
-    return s && s->ice_ && s->ice_->direct_target(&t.fd, &t.to, &t.coalesce);
+    if (!s || !s->ice_ || !s->ice_->direct_target(&t.fd, &t.to, &t.coalesce)) return false;
+    t.gen = s->ice_->path_generation();
+    return true;
   });
   start_rx_reader();
   // Packets straight to the DTLS transport, held strongly (it never refers
@@ -601,6 +623,24 @@ void PeerConnection::start_sctp() {
   metrics::gauge_fn("tunnel_udp_gso_sends", [w] {
     auto s = w.lock();
     return s && s->ice_ ? double(s->ice_->gso_sends_) : 0.0;
+  });
+  // Loss the stack cannot see otherwise: datagrams the kernel dropped on a
+  // full receive buffer (every ICE socket, the reader's included).
+  metrics::gauge_fn("tunnel_udp_rx_overflow_total", [w] {
+    auto s = w.lock();
+    if (!s || !s->ice_) return 0.0;
+    const uint64_t meminfo = s->ice_->rx_overflow();
+    const uint64_t cmsg = s->rx_reader_ ? s->rx_reader_->rxq_ovfl.load() : 0;
+    return double(std::max(meminfo, cmsg));
+  });
+  metrics::gauge_fn("tunnel_udp_rcvbuf_bytes", [w] {
+    auto s = w.lock();
+    return s && s->ice_ ? double(s->ice_->rcvbuf_bytes()) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_dtls_lane_send_waits", [w] {
+    auto s = w.lock();
+    auto* st = s && s->dtls_ ? s->dtls_->tx_lane_state() : nullptr;
+    return st ? double(st->send_waits.load()) : 0.0;
   });
   metrics::gauge_fn("tunnel_udp_gro_batches", [w] {
     auto s = w.lock();

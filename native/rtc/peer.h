@@ -111,6 +111,7 @@ class PeerConnection : public std::enable_shared_from_this<PeerConnection> {
   const SctpStats* sctp_stats() const { return sctp_ ? &sctp_->stats() : nullptr; }
   size_t sctp_mtu() const { return mtu_; }
   const DtlsTransport* dtls() const { return dtls_.get(); }
+  IceAgent* ice() const { return ice_.get(); }
 
   std::function<void(const std::string& candidate_json)> on_ice_candidate;
   std::function<void()> on_gathering_complete;
@@ -150,6 +151,12 @@ class PeerConnection : public std::enable_shared_from_this<PeerConnection> {
   // The selected direct pair's socket read off this thread (rtc/datapath.h).
   std::unique_ptr<RxReader> rx_reader_;
   int rx_reader_si_ = -1;
+  uint64_t rx_reader_gen_ = 0;   // ICE path generation the reader was started for
+  uint64_t rx_reader_ids_ = 0;
+  void restart_rx_reader();
+ public:
+  uint64_t rx_reader_restarts_ = 0;
+ private:
  public:
   const RxReader* rx_reader() const { return rx_reader_.get(); }
 };

@@ -168,18 +168,24 @@ TEST(scheduler_interactive_bypass) {
   s.send(proto::make_body(proto::MsgType::ResBody, 3, tok));  // nothing queued for stream 3: bypass
   CHECK_EQ(ch->sent.size(), size_t(1));
   CHECK_EQ(ch->sent[0].first, 3u);
+  CHECK_EQ(ch->urgent, size_t(0));  // one small frame says nothing yet
+  s.send(proto::make_body(proto::MsgType::ResBody, 3, tok));  // the stream's second token: the urgent path
+  CHECK_EQ(ch->sent.size(), size_t(2));
+  CHECK_EQ(ch->urgent, size_t(1));
+  s.send(proto::make_empty(proto::MsgType::ResEnd, 3));  // an end frame bypasses, not urgent
+  CHECK_EQ(ch->sent.size(), size_t(3));
   CHECK_EQ(ch->urgent, size_t(1));
   CHECK_EQ(s.stream_queued(1), size_t(60005 + 155));
   ch->buffered = 5000;  // past 4 windows: a token queues too
   s.send(proto::make_body(proto::MsgType::ResBody, 4, tok));
-  CHECK_EQ(ch->sent.size(), size_t(1));
+  CHECK_EQ(ch->sent.size(), size_t(3));
   CHECK_EQ(s.stream_queued(4), size_t(155));
   ch->buffered = 0;
   for (int i = 0; i < 4; i++) {
     s.pump();
     ch->buffered = 0;
   }
-  CHECK_EQ(ch->sent.size(), size_t(4));
+  CHECK_EQ(ch->sent.size(), size_t(6));
   CHECK_EQ(s.queued_bytes(), size_t(0));
   // Stream 1's frames stayed in order.
   size_t i1 = 0;
@@ -203,12 +209,75 @@ TEST(scheduler_bulk_fifo_then_round_robin) {
   }
   CHECK_EQ(ch->sent.size(), size_t(2 * n));
   const size_t fifo_frames = (FrameScheduler::kFifoBytes + 60004) / 60005;
+  const size_t share = (FrameScheduler::kBulkShareBytes + 60004) / 60005;  // oldest-first frames per bulk turn
   size_t i = 0;
   for (; i < fifo_frames; i++) CHECK_EQ(ch->sent[i].first, 7u);
-  for (; i < 2 * fifo_frames; i++) CHECK_EQ(ch->sent[i].first, 9u);
-  for (; i + 1 < size_t(2 * (n - fifo_frames)) + 2 * fifo_frames; i++)
-    CHECK(ch->sent[i].first != ch->sent[i + 1].first);  // round-robin
+  // Stream 9's first 2 MB go oldest-first, with stream 7 (now past its
+  // kFifoBytes) given one frame after every `share` of them.
+  size_t nine = 0, seven = 0, run = 0;
+  for (; nine < fifo_frames; i++) {
+    if (ch->sent[i].first == 9u) {
+      nine++;
+      run++;
+    } else {
+      CHECK_EQ(ch->sent[i].first, 7u);
+      CHECK_EQ(run, share);
+      run = 0;
+      seven++;
+    }
+  }
+  CHECK_EQ(seven, (fifo_frames - 1) / share);
+  // Then round-robin: stream 7's remaining frames never go back to back.
+  size_t rest7 = 0;
+  for (size_t k = i; k < ch->sent.size(); k++) {
+    if (ch->sent[k].first != 7u) continue;
+    rest7++;
+    CHECK(k + 1 >= ch->sent.size() || ch->sent[k + 1].first == 9u);
+  }
+  CHECK_EQ(rest7, size_t(n) - fifo_frames - seven);
   CHECK_EQ(s.queued_bytes(), size_t(0));
+}
+
+// A transfer past kFifoBytes keeps making progress while new streams keep the
+// oldest-first lane busy (advice r3: a 32 MB download under a steady load of
+// 1 MB requests got no turns).
+TEST(scheduler_long_stream_not_starved_by_new_fifo_streams) {
+  auto ch = std::make_shared<FakeChannel>();
+  FrameScheduler s(ch, 1000);
+  Bytes big = Bytes::copy(std::string(60000, 'b'));
+  ch->buffered = 5000;
+  const int long_frames = 32 * 1048576 / 60000;
+  for (int i = 0; i < long_frames; i++) s.send(proto::make_body(proto::MsgType::ResBody, 1, big));
+  // Let stream 1 move past its first 2 MB.
+  for (int i = 0; i < 40; i++) {
+    ch->buffered = 0;
+    s.pump();
+  }
+  size_t long_sent = 0;
+  for (auto& e : ch->sent) long_sent += e.first == 1u;
+  CHECK_EQ(long_sent, size_t(40));
+  // A steady load: a new 1 MB stream arrives every turn, always with queued
+  // frames ahead in the oldest-first lane.
+  uint32_t next = 2;
+  const size_t before = ch->sent.size();
+  for (int turn = 0; turn < 400; turn++) {
+    if (turn % 2 == 0) {
+      for (int k = 0; k < 18; k++) s.send(proto::make_body(proto::MsgType::ReqBody, next, big));
+      s.send(proto::make_empty(proto::MsgType::ReqEnd, next));
+      next++;
+    }
+    ch->buffered = 0;
+    s.pump();
+  }
+  size_t long_now = 0, total = 0;
+  for (size_t k = before; k < ch->sent.size(); k++) {
+    total++;
+    long_now += ch->sent[k].first == 1u;
+  }
+  // The round-robin lane gets about one frame per kBulkShareBytes of
+  // oldest-first bytes: well above zero, and the new streams still lead.
+  CHECK(long_now * 8 >= total);
+  CHECK(long_now * 2 <= total);
 }
 
 // A stream whose queue ran dry keeps its attained service: past kFifoBytes it

@@ -85,14 +85,20 @@ void FrameScheduler::send(proto::Frame f) {
       // Evidence is a stream's second small body frame: a bulk response's
       // first read from its upstream is often small too, and counting it kept
       // the tighter bound on through a 64 x 1 MB echo.
+      // Only a token takes the transport's priority path: headers and end
+      // frames of bulk streams gain nothing from it (advice r3).
+      bool token = false;
       if (f.type == proto::MsgType::ResBody || f.type == proto::MsgType::ReqBody) {
         auto sv = sent_.find(f.stream_id);
-        if ((sv == sent_.end() || sv->second < kBulkSent) && ++small_[f.stream_id] >= 2) ch_->note_interactive();
+        if ((sv == sent_.end() || sv->second < kBulkSent) && ++small_[f.stream_id] >= 2) {
+          ch_->note_interactive();
+          token = true;
+        }
         if (small_.size() > kRemember) small_.erase(small_.begin());
       } else if (last_frame(f) && !small_.empty()) {
         small_.erase(f.stream_id);
       }
-      emit(f, true);
+      emit(f, token);
       bypassed_++;
       return;
     }
@@ -151,6 +157,7 @@ bool FrameScheduler::release(uint32_t sid, StreamQ& s, std::unordered_map<uint32
   s.bytes -= sz;
   s.sent += sz;
   queued_ -= sz;
+  released_ = sz;
   if (s.q.empty()) {
     if (!last_frame(f)) {  // attained service outlives an empty queue while the stream may still produce
       sent_[sid] = s.sent;
@@ -203,7 +210,26 @@ void FrameScheduler::pump() {
       progressed = true;
       continue;
     }
-    if (pop_from(interactive_) || pop_fifo() || pop_from(bulk_)) {
+    if (pop_from(interactive_)) {
+      progressed = true;
+      continue;
+    }
+    // The round-robin lane's guaranteed share: without it a transfer past
+    // kFifoBytes got no turn while newer streams kept the oldest-first lane
+    // busy (a steady load of 1 MB requests starved a large download).
+    if (fifo_run_ >= kBulkShareBytes && pop_from(bulk_)) {
+      fifo_run_ = 0;
+      progressed = true;
+      continue;
+    }
+    const bool rr_waiting = !bulk_.empty();
+    if (pop_fifo()) {
+      fifo_run_ = rr_waiting ? fifo_run_ + released_ : 0;  // the share accrues while round-robin waits
+      progressed = true;
+      continue;
+    }
+    if (pop_from(bulk_)) {
+      fifo_run_ = 0;
       progressed = true;
       continue;
     }

@@ -16,7 +16,10 @@
 //      then; served in order, each completes in turn and the next hop starts
 //      on it while the rest are still in transit. Past kFifoBytes a stream
 //      goes round-robin, one frame per turn, so a long transfer never holds
-//      the others back for longer than that.
+//      the others back for longer than that. The round-robin lane is never
+//      starved by a steady arrival of new streams: after kBulkShareBytes of
+//      oldest-first frames it gets one frame (about a fifth of the bytes while
+//      both lanes are backlogged).
 //
 // So a token waits for at most the channel window plus one frame, never for
 // other streams' queued bodies. Per-stream FIFO order is preserved (the wire
@@ -44,6 +47,7 @@ class FrameScheduler {
   static constexpr size_t kInteractive = 4096;
   static constexpr uint64_t kBulkSent = 256 * 1024;  // a stream past this is bulk, not interactive
   static constexpr uint64_t kFifoBytes = 2u << 20;
+  static constexpr uint64_t kBulkShareBytes = 256 * 1024;  // oldest-first bytes per guaranteed round-robin frame
 
   explicit FrameScheduler(std::shared_ptr<MessageChannel> ch, size_t window = 64 * 1024);
   ~FrameScheduler();
@@ -109,6 +113,8 @@ class FrameScheduler {
   std::set<uint32_t> fifo_;  // bulk streams within their first kFifoBytes, oldest (lowest id) first
   std::map<uint32_t, uint64_t> sent_;  // attained service of open streams whose queue ran dry
   size_t queued_ = 0;
+  size_t released_ = 0;   // wire bytes of the last frame release() handed to the channel
+  uint64_t fifo_run_ = 0;  // oldest-first bytes released since the round-robin lane last had a turn
   uint64_t emitted_ = 0;  // frames handed to the channel
   uint64_t wd_emitted_ = 0;
   size_t wd_buffered_ = 0;

@@ -117,6 +117,97 @@ def test_cli_help_version_and_missing_args():
     assert "connecting to signaling server: ws://127.0.0.1:1" in out.stdout  # env fallbacks honoured
 
 
+@pytest.mark.parametrize("args,env,flag,why", [
+    (["serve", "--room", "r", "--upstream", "http://x", "--workers", "x"], {}, "--workers", "invalid digit"),
+    (["proxy", "--room", "r", "--ping-interval-ms", "x"], {}, "--ping-interval-ms", "invalid digit"),
+    (["proxy", "--room", "r", "--ping-interval-ms="], {}, "--ping-interval-ms", "empty string"),
+    (["proxy", "--room", "r", "--pong-timeout-ms", "-5"], {}, "--pong-timeout-ms", "invalid digit"),
+    (["proxy", "--room", "r", "--header-timeout-ms", "99999999999999999999999"], {}, "--header-timeout-ms",
+     "too large"),
+    (["serve", "--room", "r", "--upstream", "http://x", "--sctp-mtu", "100"], {}, "--sctp-mtu", "not in 576..65535"),
+    (["serve", "--room", "r", "--upstream", "http://x", "--max-request-body", "1k"], {}, "--max-request-body",
+     "invalid digit"),
+    (["proxy", "--room", "r"], {"TUNNEL_WORKERS": "four"}, "--workers", "invalid digit"),  # env values are checked too
+    (["proxy", "--room", "r"], {"TUNNEL_GATHER_TIMEOUT_MS": "5s"}, "--gather-timeout-ms", "invalid digit"),
+])
+def test_cli_rejects_bad_numbers(args, env, flag, why):
+    """Every numeric flag is parsed whole (clap's u64 parser, cli.rs:13-68): exit 2 naming the flag."""
+    import os
+    import subprocess
+    out = subprocess.run([binary("tunnel")] + args, capture_output=True, text=True, timeout=10,
+                         env={"PATH": os.environ.get("PATH", "/usr/bin"), **env})
+    assert out.returncode == 2, out
+    assert f"for '{flag} <VALUE>'" in out.stderr and why in out.stderr, out.stderr
+
+
+@pytest.mark.parametrize("cmd,flag", [
+    ("proxy", ["--max-request-body", "5"]),
+    ("proxy", ["--stream-body-threshold", "5"]),
+    ("proxy", ["--upstream-prewarm", "0"]),
+    ("proxy", ["--upstream-prewarm-ttl-ms=10"]),
+    ("proxy", ["--upstream", "http://x"]),
+    ("proxy", ["--advertise", "/v1"]),
+    ("serve", ["--listen-early"]),
+    ("serve", ["--listen", "127.0.0.1:1"]),
+])
+def test_cli_rejects_flags_of_the_other_subcommand(cmd, flag):
+    """clap rejects an argument its subcommand does not define (cli.rs:13-68); so do the extensions."""
+    import subprocess
+    base = ["--room", "r"] + (["--upstream", "http://x"] if cmd == "serve" else [])
+    out = subprocess.run([binary("tunnel"), cmd] + base + flag, capture_output=True, text=True, timeout=10)
+    name = flag[0].split("=")[0]
+    assert out.returncode == 2 and f"unexpected argument '{name}'" in out.stderr, out
+    help_text = subprocess.run([binary("tunnel"), cmd, "--help"], capture_output=True, text=True).stdout
+    assert name + " " not in help_text and name + "\n" not in help_text
+
+
+def test_cli_flag_switch_takes_no_value():
+    import subprocess
+    out = subprocess.run([binary("tunnel"), "proxy", "--room", "r", "--ipv6=1"], capture_output=True, text=True)
+    assert out.returncode == 2 and "'--ipv6'" in out.stderr
+
+
+def _raw_exchange(port, request: bytes) -> bytes:
+    s = socket.create_connection(("127.0.0.1", port), timeout=10)
+    s.sendall(request)
+    data = b""
+    while True:
+        d = s.recv(65536)
+        if not d:
+            break
+        data += d
+    s.close()
+    return data
+
+
+@pytest.mark.parametrize("framing", [
+    b"Transfer-Encoding: chunked\r\nContent-Length: 5\r\n",          # TE + CL (RFC 9112 §6.3 smuggling vector)
+    b"Content-Length: 5\r\nTransfer-Encoding: chunked\r\n",
+    b"Transfer-Encoding: chunked, gzip\r\n",                        # chunked not the final coding
+    b"Transfer-Encoding: chunked\r\nTransfer-Encoding: gzip\r\n",  # same, over two field lines
+    b"Transfer-Encoding: gzip\r\n",
+    b"Transfer-Encoding: gzip, chunked\r\n",                        # a coding serve could not relay
+])
+def test_request_framing_rejected_with_400_and_close(mock_upstream, framing):
+    """Ambiguous or unsupported request framing: 400 and the connection closes
+    (RFC 9112 §6.1), so nothing after the head is read as a next request."""
+    with Tunnel(mock_upstream, transport="tcp") as t:
+        smuggled = b"GET /health HTTP/1.1\r\nHost: x\r\n\r\n"
+        data = _raw_exchange(t.proxy_port, b"POST /echo HTTP/1.1\r\nHost: x\r\n" + framing + b"\r\n"
+                             b"5\r\nhello\r\n0\r\n\r\n" + smuggled)
+        assert data.startswith(b"HTTP/1.1 400"), data[:200]
+        assert data.count(b"HTTP/1.1 ") == 1  # closed: the trailing request was never served
+        # The proxy itself is fine afterwards.
+        assert urllib.request.urlopen(t.url + "/health", timeout=10).read() == b"ok"
+
+
+def test_request_chunked_alone_still_accepted(mock_upstream):
+    with Tunnel(mock_upstream, transport="tcp") as t:
+        data = _raw_exchange(t.proxy_port, b"POST /echo HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: Chunked\r\n"
+                             b"Connection: close\r\n\r\n5\r\nhello\r\n0\r\n\r\n")
+        assert data.startswith(b"HTTP/1.1 200") and b"hello" in data
+
+
 def test_cpu_affinity(mock_upstream):
     """--cpu-affinity pins the reactor thread (NUMA placement next to the NIC)."""
     import os
