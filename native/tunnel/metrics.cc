@@ -1,5 +1,11 @@
 #include "tunnel/metrics.h"
 
+#include <algorithm>
+
+#include <unistd.h>
+
+#include <fcntl.h>
+
 #include <cstdio>
 #include <cstdlib>
 #include <atomic>
@@ -159,23 +165,66 @@ std::shared_ptr<void> serve(Reactor& r, const std::string& addr, std::string* er
 
 namespace p2pt::trace {
 namespace {
-FILE* sink() {
-  static FILE* f = [] () -> FILE* {
+// TUNNEL_TRACE_BUFFERED=1: events collect in memory and go out in whole-line
+// write()s of up to 512 KiB (and at exit): bulk waterfalls stamp ~10 events
+// per request, and a flush per event would cost a syscall each on the
+// measured path. Several processes append to one file (O_APPEND), so a write
+// never ends inside a line. Default: one write per event.
+struct Sink {
+  int fd = -1;
+  bool buffered = false;
+  std::mutex mu;
+  std::string buf;
+  void drain() {  // mu held
+    size_t off = 0;
+    while (off < buf.size()) {
+      ssize_t n = ::write(fd, buf.data() + off, buf.size() - off);
+      if (n <= 0) break;
+      off += size_t(n);
+    }
+    buf.clear();
+  }
+};
+
+Sink* sink() {
+  static Sink* s = [] () -> Sink* {
     const char* p = getenv("TUNNEL_TRACE");
     if (!p || !*p) return nullptr;
-    return fopen(p, "a");
+    int fd = ::open(p, O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
+    if (fd < 0) return nullptr;
+    auto* k = new Sink;
+    k->fd = fd;
+    const char* b = getenv("TUNNEL_TRACE_BUFFERED");
+    k->buffered = b && *b == '1';
+    if (k->buffered) {
+      k->buf.reserve(1 << 20);
+      std::atexit([] { flush(); });
+    }
+    return k;
   }();
-  return f;
+  return s;
 }
 }  // namespace
 
 bool enabled() { return sink() != nullptr; }
 
 void event(const char* role, uint32_t sid, const char* ev) {
-  FILE* f = sink();
-  if (!f) return;
-  fprintf(f, "{\"t_us\":%llu,\"role\":\"%s\",\"sid\":%u,\"ev\":\"%s\"}\n",
-          static_cast<unsigned long long>(Reactor::now_us()), role, sid, ev);
-  fflush(f);
+  Sink* k = sink();
+  if (!k) return;
+  char line[160];
+  int n = snprintf(line, sizeof line, "{\"t_us\":%llu,\"role\":\"%s\",\"sid\":%u,\"ev\":\"%s\"}\n",
+                   static_cast<unsigned long long>(Reactor::now_us()), role, sid, ev);
+  if (n <= 0) return;
+  n = std::min(n, int(sizeof line) - 1);
+  std::lock_guard<std::mutex> lk(k->mu);
+  k->buf.append(line, size_t(n));
+  if (!k->buffered || k->buf.size() >= (512u << 10)) k->drain();
+}
+
+void flush() {
+  Sink* k = sink();
+  if (!k) return;
+  std::lock_guard<std::mutex> lk(k->mu);
+  k->drain();
 }
 }  // namespace p2pt::trace

@@ -35,4 +35,5 @@ namespace p2pt::trace {
 bool enabled();
 // Append {"t_us":..,"role":..,"sid":..,"ev":..} to $TUNNEL_TRACE.
 void event(const char* role, uint32_t stream_id, const char* ev);
+void flush();  // buffered mode (TUNNEL_TRACE_BUFFERED=1): write out what is held
 }  // namespace p2pt::trace

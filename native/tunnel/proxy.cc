@@ -363,6 +363,10 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     bool flow = sess->flow() && !discard_body_;
     size_t used = body_.feed(data, len, [&](const uint8_t* d, size_t n) {
       if (reject) return;
+      if (!body_seen_) {
+        body_seen_ = true;
+        trace::event("proxy", sid, "body_first");
+      }
       Bytes b = conn ? conn->rx_view(d, n) : Bytes::copy(d, n);
       for (size_t off = 0; off < n; off += cs)
         sess->send(proto::make_body(proto::MsgType::ReqBody, sid, b.slice(off, cs)));
@@ -554,6 +558,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     chunked_ = false;
     no_body_ = false;
     first_body_ = false;
+    body_seen_ = false;
     response_complete_ = false;
     discard_body_ = false;
     body_sent_ = 0;
@@ -596,6 +601,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
   bool chunked_ = false;
   bool no_body_ = false;
   bool first_body_ = false;
+  bool body_seen_ = false;  // TUNNEL_TRACE: the request's first body byte was stamped
   bool response_complete_ = false;
   bool discard_body_ = false;    // response done mid-upload: drain the body, forward nothing
   bool pipelined_hold_ = false;

@@ -20,10 +20,22 @@ void FrameScheduler::set_watermarks(size_t high, size_t low, std::function<void(
 bool FrameScheduler::emit(const proto::Frame& f, bool urgent) {
   uint8_t hdr[proto::kHeaderLen];
   f.header(hdr);
-  // Trace: a stream's first response body frame leaves the scheduler for the channel.
-  if (f.type == proto::MsgType::ResBody && trace::enabled()) {
+  // Trace: a stream's first body frame and its end frame leave the scheduler
+  // for the channel (serve sends RES_*, the proxy REQ_*).
+  if (trace::enabled()) {
     if (traced_.size() >= (1u << 16)) traced_.clear();  // bounded on long traced runs
-    if (traced_.insert(f.stream_id).second) trace::event("serve", f.stream_id, "chan_tx");
+    const uint64_t key = uint64_t(f.stream_id) << 8;
+    switch (f.type) {
+      case proto::MsgType::ResBody:
+        if (traced_.insert(key | 1).second) trace::event("serve", f.stream_id, "chan_tx");
+        break;
+      case proto::MsgType::ReqBody:
+        if (traced_.insert(key | 2).second) trace::event("proxy", f.stream_id, "chan_tx");
+        break;
+      case proto::MsgType::ResEnd: trace::event("serve", f.stream_id, "chan_end"); break;
+      case proto::MsgType::ReqEnd: trace::event("proxy", f.stream_id, "chan_end"); break;
+      default: break;
+    }
   }
   metrics::frame_sent(uint8_t(f.type), f.wire_size());
   emitted_++;

@@ -61,7 +61,7 @@ class FrameScheduler {
   }();
   uint64_t bypassed_ = 0;  // frames sent through the interactive bypass
   std::map<uint32_t, uint32_t> small_;  // small body frames sent through the bypass, per stream
-  std::unordered_set<uint32_t> traced_;  // TUNNEL_TRACE: streams whose first body frame was stamped
+  std::unordered_set<uint64_t> traced_;  // TUNNEL_TRACE: (stream, kind) whose first body frame was stamped
   size_t queued_bytes() const { return queued_; }
   // Send-path stall watchdog, called about once a second: true when frames
   // or channel bytes are waiting and neither moved since the previous call.

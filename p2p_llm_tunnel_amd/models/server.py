@@ -25,9 +25,13 @@ Sampling: temperature / top_p / seed (and the common top_k extension) from an
 OpenAI request, or "options" of an Ollama one, drawn on device after the LM
 head (ops.sample_, sample.hip: top-k and top-p by radix select, Gumbel-max
 draw); temperature 0 — the default unless --default-temperature — keeps the
-fused LM head's greedy argmax. Parameters that would change the output and are
-not implemented (n > 1, penalties, logit_bias, stop sequences, logprobs,
-Ollama's repeat_penalty, mirostat, ...) are answered with 400.
+fused LM head's greedy argmax. Stop sequences (OpenAI "stop": a string or up
+to 4; Ollama "options.stop") end a completion at the first match in the
+detokenised text, which is left out (finish_reason "stop"); a streamed
+response holds back only a tail that could still begin one. Parameters that
+would change the output and are not implemented (n > 1, penalties,
+logit_bias, logprobs, Ollama's repeat_penalty, mirostat, ...) are answered
+with 400, as is sampling on an engine without the captured HIP step.
 
 Two model sources:
 
@@ -96,9 +100,10 @@ def _number(src: dict, key: str, lo: float, hi: float, default, integer=False, l
 # does not implement: neutral values pass, anything else is refused instead of
 # being silently ignored.
 _OPENAI_NEUTRAL = {"n": (1,), "best_of": (1,), "presence_penalty": (0, 0.0), "frequency_penalty": (0, 0.0),
-                   "logprobs": (False, 0), "top_logprobs": (0,), "logit_bias": ({},), "stop": ([], "")}
+                   "logprobs": (False, 0), "top_logprobs": (0,), "logit_bias": ({},)}
 _OLLAMA_NEUTRAL = {"repeat_penalty": (1, 1.0), "presence_penalty": (0, 0.0), "frequency_penalty": (0, 0.0),
-                   "mirostat": (0,), "tfs_z": (1, 1.0), "typical_p": (1, 1.0), "min_p": (0, 0.0), "stop": ([], "")}
+                   "mirostat": (0,), "tfs_z": (1, 1.0), "typical_p": (1, 1.0), "min_p": (0, 0.0)}
+_MAX_STOPS = 4  # the OpenAI API's limit
 
 
 def sampling_params(body: dict, ollama: bool, default_temperature: float = 0.0) -> Sampling:
@@ -114,13 +119,69 @@ def sampling_params(body: dict, ollama: bool, default_temperature: float = 0.0) 
         if key in src and src[key] is not None and not any(src[key] == x and type(src[key]) is type(x)
                                                             for x in neutral):
             raise SamplingError(f"{key}={src[key]!r} is not supported by this server")
-    if not ollama and "stop" in src and src["stop"] not in (None, [], ""):
-        raise SamplingError("stop sequences are not supported by this server")
     t = _number(src, "temperature", 0.0, 100.0, default_temperature)
     top_p = _number(src, "top_p", 0.0, 1.0, 1.0, lo_open=True)
     top_k = _number(src, "top_k", 0, 1 << 30, 0, integer=True)
     seed = _number(src, "seed", -(1 << 63), (1 << 64) - 1, None, integer=True)
     return Sampling(t, top_k, top_p, seed)
+
+
+def stop_sequences(body: dict, ollama: bool) -> list[str]:
+    """Stop sequences of an OpenAI request ("stop": null, a string, or a list
+    of up to 4 strings) or an Ollama one ("options.stop": a list of strings).
+    Empty strings are dropped (they would match at once); anything else that
+    is not a string is refused."""
+    src = body.get("options", {}) if ollama else body
+    if not isinstance(src, dict):
+        return []
+    v = src.get("stop")
+    if v is None:
+        return []
+    if isinstance(v, str):
+        v = [v]
+    if not isinstance(v, list) or not all(isinstance(x, str) for x in v):
+        raise SamplingError(f"stop must be a string or a list of strings, got {v!r}")
+    if len(v) > _MAX_STOPS and not ollama:
+        raise SamplingError(f"stop takes at most {_MAX_STOPS} sequences, got {len(v)}")
+    return [x for x in v if x]
+
+
+class StopMatcher:
+    """Finds the first stop sequence in a completion's text as pieces arrive.
+
+    ``push(piece)`` returns the text that is safe to emit and whether a stop
+    sequence ended the completion (the text up to the match is emitted, the
+    match and everything after it are not). A tail that could still be the
+    start of a stop sequence is held back until the next piece decides it;
+    ``flush()`` releases it when the completion ends for another reason."""
+    __slots__ = ("stops", "buf")
+
+    def __init__(self, stops: list[str]):
+        self.stops = stops
+        self.buf = ""
+
+    def push(self, piece: str) -> tuple[str, bool]:
+        buf = self.buf + piece
+        hit = -1
+        for s in self.stops:
+            i = buf.find(s)
+            if i >= 0 and (hit < 0 or i < hit):
+                hit = i
+        if hit >= 0:
+            self.buf = ""
+            return buf[:hit], True
+        keep = 0
+        for s in self.stops:
+            for k in range(min(len(s) - 1, len(buf)), keep, -1):
+                if buf.endswith(s[:k]):
+                    keep = k
+                    break
+        self.buf = buf[len(buf) - keep:] if keep else ""
+        return (buf[:len(buf) - keep] if keep else buf), False
+
+    def flush(self) -> str:
+        out, self.buf = self.buf, ""
+        return out
 
 
 class Request:
@@ -455,9 +516,9 @@ class _Stream:
     """Per-request output state on the I/O thread: the writer and the byte
     template around each token piece (token ids render as " t<id>": no JSON
     escaping needed)."""
-    __slots__ = ("writer", "stream", "kind", "rid", "pre", "post", "toks", "done", "detok", "reason")
+    __slots__ = ("writer", "stream", "kind", "rid", "pre", "post", "toks", "done", "detok", "reason", "stop")
 
-    def __init__(self, writer, stream, kind, rid, model, detok=None):
+    def __init__(self, writer, stream, kind, rid, model, detok=None, stop=None):
         self.writer = writer
         self.stream = stream
         self.kind = kind  # "chat" | "text" | "ollama"
@@ -465,6 +526,7 @@ class _Stream:
         self.toks = []  # non-streamed: rendered pieces (bytes, JSON-escaped when detokenised)
         self.detok = detok  # checkpoint tokenizer: incremental text of this request
         self.reason = "length"
+        self.stop = stop  # StopMatcher, or None without stop sequences
         self.done = asyncio.get_running_loop().create_future()
         m = json.dumps(model)
         if kind == "chat":
@@ -549,6 +611,16 @@ class FrontEnd:
                 st.reason = "stop"
                 self._finish(req, st)
                 continue
+            if st.stop is not None:
+                piece = st.detok.push(tok) if st.detok is not None else " t%d" % tok
+                text, stopped = st.stop.push(piece)
+                if text:
+                    self._emit_piece(st, _piece(text))
+                if stopped:  # the engine frees the slot on its next step
+                    req.cancelled = True
+                    st.reason = "stop"
+                    self._finish(req, st)
+                continue
             if st.detok is not None:
                 piece = st.detok.push(tok)
                 if not piece:
@@ -556,13 +628,21 @@ class FrontEnd:
                 body = _piece(piece)
             else:
                 body = b" t%d" % tok
-            if st.stream:
-                st.writer.write(_chunk(st.pre + body + st.post))
-            else:
-                st.toks.append(body)
+            self._emit_piece(st, body)
+
+    @staticmethod
+    def _emit_piece(st, body: bytes):
+        if st.stream:
+            st.writer.write(_chunk(st.pre + body + st.post))
+        else:
+            st.toks.append(body)
 
     def _finish(self, req, st):
         w = st.writer
+        if st.stop is not None and st.reason != "stop":
+            held = st.stop.flush()  # a held-back tail that never became a stop sequence
+            if held:
+                self._emit_piece(st, _piece(held))
         if st.stream:
             if st.kind == "ollama":
                 tail = _chunk((json.dumps({"model": self.model_name, "response": "", "done": True}) + "\n").encode())
@@ -693,6 +773,12 @@ class FrontEnd:
         kind = "ollama" if ollama else ("chat" if "chat" in path else "text")
         try:
             sampling = sampling_params(req_body, ollama, self.default_temperature)
+            stops = stop_sequences(req_body, ollama)
+            if not sampling.greedy and not self.engine.use_graph:
+                # The eager step (CPU stand-ins, injected models) has no sampler:
+                # refuse rather than answer a sampled request greedily.
+                raise SamplingError("sampling (temperature > 0) needs the graph-captured HIP step; "
+                                    "this engine runs eagerly")
         except SamplingError as e:
             writer.write(self._json_response({"error": {"message": str(e), "type": "invalid_request_error"}}, 400))
             return True
@@ -700,7 +786,8 @@ class FrontEnd:
         rid = ("chatcmpl-" if kind == "chat" else "cmpl-") + uuid.uuid4().hex[:12]
         prompt = _prompt_ids(req_body, self.tok)
         req = Request(prompt, max(1, min(max_new, 1024)), batched=True, sampling=sampling)
-        st = _Stream(writer, stream, kind, rid, name, self.tok.detokenizer(prompt) if self.tok is not None else None)
+        st = _Stream(writer, stream, kind, rid, name, self.tok.detokenizer(prompt) if self.tok is not None else None,
+                     StopMatcher(stops) if stops else None)
         req.state = st
         if stream:
             writer.write(b"HTTP/1.1 200 OK\r\nContent-Type: %s\r\nCache-Control: no-cache\r\n"

@@ -772,263 +772,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(TOK == 16 ?
   if (threadIdx.x == 0) st_wt(&counters[blockIdx.y], 0u);
 }
 
-// ------------------------------------------------------------ persistent MLP block
-// O projection -> gate/up + SwiGLU -> down projection of one layer as ONE
-// launch (P2PT_DECODE_BLOCK=1; batch <= 16). The three GEMMs' tiles form one
-// in-order work queue: a workgroup takes the next tile index from a counter
-// and runs it; a tile of a later GEMM first issues its first batch of weight
-// loads (they do not depend on anything), then waits until every tile of the
-// GEMM before it has published, then loads its activations. A workgroup only
-// ever waits for tiles with smaller indices, all of them already taken by
-// running workgroups, so the queue cannot deadlock whatever the grid size or
-// residency; every wait is also bounded (err flag, then the tile runs on).
-// Hand-off (MI355X_MICROARCH, inter-workgroup visibility, valid form "stores
-// all sc1, loads all sc1"): epilogue stores are 4-byte write-through (sc1)
-// stores, every wave drains them (vmcnt(0)) before a workgroup barrier, one
-// lane then adds to a per-phase arrival counter sharded 8 ways; the consumer's
-// lane 0 polls the shards with sc1 loads and the workgroup joins at a barrier
-// before its sc1 loads of the activations, norm partials and residual. The
-// counters reset themselves (the last workgroup to leave zeroes them).
-// The tile body follows k_skinny (kept separate so that kernel's code is not
-// perturbed: compiling a variant into it cost the launched step 0.359 -> 0.372
-// ms in round 3; with this kernel added the launched kernels' ISA is unchanged)
-// with NW = 8, TN = 1, UM = 4, one 16-row tile, no split-K.
-// Measured on MI355X and left off (profiles/r03/decode_block/): correct
-// (tests/test_gpu_model.py::test_block_kernel_matches_launches) but slower,
-// small 0.358 -> 0.61-0.62 ms per step at batch 1, 0.521 -> 0.81 ms at 16,
-// against every variant tried: three inlined bodies (223 VGPRs, one
-// workgroup per CU) or one body (70 VGPRs) at 256 workgroups; 512 or 768
-// workgroups 0.97-1.09 ms; waiters polling one completion word instead of 8
-// shards 0.68; 4 items per dequeue 1.00. Each tile is a serial chain in its
-// workgroup (dependent loads, reduction, write-through drain, barriers,
-// arrival) and the launched GEMMs overlap many such chains per CU; a
-// persistent layer would need each workgroup to stream the next tile's
-// weights while the current one reduces (MI355X_MICROARCH's LDS-DMA loader
-// engine: 0.87-0.89x of the launches at best).
-constexpr int kBlkNW = 8, kBlkUM = 4;
-constexpr int kBlkChunk = 1;  // work-queue items claimed per dequeue (4 measured slower: 0.61 -> 1.00 ms)
-constexpr int kAuxSc1 = 16;  // buffer-load cache policy bit sc1 (CPol::SC1)
-constexpr int kBlkCtr = 8 + 3 * 8;  // queue head, exits, 6 spare, 3 phases x 8 shards
-
-struct BlockArgs {
-  GemmArgs g[3];  // O (RESID), gate/up (SILU), down (RESID)
-  int tiles[3];   // column tiles of each
-  unsigned* ctr;  // [0] queue head, [1] exits, [8 + 8 p + s] arrivals of phase p, shard s
-  int* err;       // a dependency wait timed out
-  int wait_iters; // poll bound per wait (P2PT_DECODE_BLOCK_WAIT, default 2^18)
-};
-
-__device__ __forceinline__ uint4 buf_ld16_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kAuxSc1));
-}
-
-// Lane 0 only: until the 8 arrival shards of a phase sum to `need` (bounded).
-// Polled with atomic adds of 0, which read the counters where the arrivals'
-// atomics land: `sc1` loads of them (flat, then buffer) never saw the
-// arrivals. (A two-level scheme, shards plus one completion word bumped by
-// each shard's last arriver so that waiters poll one word, measured slower.)
-__device__ __forceinline__ void blk_wait(unsigned* done, unsigned need, int* err, int iters) {
-  for (int it = 0; it < iters; it++) {
-    unsigned s = 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) s += __hip_atomic_fetch_add(done + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (s >= need) return;
-    __builtin_amdgcn_s_sleep(4);
-  }
-  __hip_atomic_fetch_add(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ void blk_tile(const GemmArgs& a, const int EPI, int bx, unsigned* wait_done, unsigned wait_need,
-                                         int* err, int iters, float (&red)[kBlkNW][4][kWave],
-                                         float (&red_ss)[kBlkNW][kWave]) {
-  constexpr int NW = kBlkNW, UM = kBlkUM;
-  // Wave-uniform values in SGPRs: the work loop around this body must stay
-  // scalar control flow (barriers inside it).
-  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool norm = a.ss_part != nullptr;
-  const int kparts = 1 << a.kpl, Kp = a.K >> a.kpl;
-  const int m_a = (lane & 15) >> a.kpl;
-  const int p_a = (lane & 15) & (kparts - 1);
-  const bool a_ok = m_a < a.M;
-  const int kq = (lane >> 4) << 3;
-  const int S = Kp >> 5;
-  const int s0 = wv * S / NW, s1 = (wv + 1) * S / NW;
-  const __amdgpu_buffer_rsrc_t ra = rsrc(a.x, uint32_t(a.M) * uint32_t(a.K) * 2u);
-  const __amdgpu_buffer_rsrc_t rw = rsrc(a.w, uint32_t(a.N) * uint32_t(a.K) * 2u);
-  const uint32_t xoff = a_ok ? (uint32_t(m_a) * uint32_t(a.K) + uint32_t(p_a * Kp + kq)) * 2u : kOob;
-  const int p_b = a.kpl ? (lane & 15) >> a.cwl : 0;
-  const uint32_t woff = (uint32_t(tile_col<1>(bx, 0, lane & 15, a.cwl)) * uint32_t(a.K) + uint32_t(p_b * Kp + kq)) * 2u;
-  const int c = lane & 15, lrow0 = (lane >> 4) << 2;
-  const bool col_ok = c < (1 << a.cwl);
-
-  // 1. The first batch's weights: independent of the previous GEMM.
-  Batch<UM, 1> first;
-#pragma unroll
-  for (int u = 0; u < UM; u++) first.b[u][0] = buf_ld16(rw, s0 + u < s1 ? woff + uint32_t(s0 + u) * 64u : kOob);
-  // 2. The previous GEMM's outputs are published.
-  if (wait_done) {
-    if (threadIdx.x == 0) blk_wait(wait_done, wait_need, err, iters);
-    __syncthreads();
-  }
-  // 3. What it wrote: activations, norm partials, residual (sc1 loads).
-#pragma unroll
-  for (int u = 0; u < UM; u++) first.a[u] = buf_ld16_sc1(ra, s0 + u < s1 ? xoff + uint32_t(s0 + u) * 64u : kOob);
-  constexpr int kSsRegs = 8;
-  float ssv[kSsRegs];
-  const int ss_p0 = (lane >> 4) + 4 * wv;
-  if (norm) {
-#pragma unroll
-    for (int i = 0; i < kSsRegs; i++) {
-      const int p = ss_p0 + 4 * NW * i;
-      ssv[i] = p < a.ss_parts ? ld_wt(a.ss_part + p * kMaxM + (lane & 15)) : 0.f;
-    }
-  }
-  float rprev[4];
-  if (EPI == EPI_RESID) {
-    if (wv == 0) {
-      const int col = tile_col<1>(bx, 0, c, a.cwl);
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int m = min(lrow0 + r, a.M - 1);
-        const uint32_t pr = ld_wt(reinterpret_cast<const uint32_t*>(a.out + size_t(m) * a.N + (col & ~1)));
-        rprev[r] = bf2f(uint16_t((col & 1) ? pr >> 16 : pr & 0xFFFF));
-      }
-    }
-  }
-  frag4 acc[1] = {frag4{0.f, 0.f, 0.f, 0.f}};
-  __builtin_amdgcn_sched_barrier(0);
-  mma_apply<UM, 1>(acc, first);
-  for (int s = s0 + UM; s < s1; s += UM) {
-    Batch<UM, 1> p;
-#pragma unroll
-    for (int u = 0; u < UM; u++) {
-      const bool in = s + u < s1;
-      p.b[u][0] = buf_ld16(rw, in ? woff + uint32_t(s + u) * 64u : kOob);
-      p.a[u] = buf_ld16_sc1(ra, in ? xoff + uint32_t(s + u) * 64u : kOob);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    mma_apply<UM, 1>(acc, p);
-  }
-  if (norm) {
-    float ssum = 0.f;
-#pragma unroll
-    for (int i = 0; i < kSsRegs; i++) ssum += ssv[i];
-    for (int p = ss_p0 + 4 * NW * kSsRegs; p < a.ss_parts; p += 4 * NW) ssum += ld_wt(a.ss_part + p * kMaxM + (lane & 15));
-    red_ss[wv][lane] = ssum;
-  }
-#pragma unroll
-  for (int r = 0; r < 4; r++) red[wv][r][lane] = acc[0][r];
-  __syncthreads();
-  if (wv != 0) return;  // the caller's barrier re-joins the waves
-  float v[4];
-#pragma unroll
-  for (int r = 0; r < 4; r++) {
-    float sum = 0.f;
-#pragma unroll
-    for (int w = 0; w < NW; w++) sum += red[w][r][lane];
-    v[r] = sum;
-  }
-  if (a.kpl) {
-    float* cbuf = &red[0][0][0];
-#pragma unroll
-    for (int r = 0; r < 4; r++) cbuf[(lrow0 + r) * 17 + c] = v[r];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const int row = lrow0 + r;
-      float sum = 0.f;
-      if (row < (16 >> a.kpl) && col_ok)
-        for (int p = 0; p < kparts; p++) sum += cbuf[(row * kparts + p) * 17 + c + (p << a.cwl)];
-      v[r] = sum;
-    }
-  }
-  if (norm) {
-    float ssum = 0.f;
-#pragma unroll
-    for (int w = 0; w < NW; w++) ssum += red_ss[w][lane];
-    ssum = xor32_sum(xor16_sum(ssum));
-    const float rs_row = rsqrtf(ssum * (1.f / float(a.K)) + a.eps);
-#pragma unroll
-    for (int r = 0; r < 4; r++) v[r] *= __shfl(rs_row, lrow0 + r, kWave);
-  }
-  const int n = tile_col<1>(bx, 0, c, a.cwl);
-  if (EPI == EPI_SILU) {
-    // Even lane = gate_j, odd = up_j; lanes c and c + 2 hold h_j, h_{j+1}: one 4-byte store per pair.
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const float mine = bf_round(v[r]);
-      const float other = dpp<kDppXor1>(mine);
-      const float h = mine / (1.f + __expf(-mine)) * other;
-      const float h_next = dpp<kDppXor2>(h);
-      if ((c & 3) || !col_ok || lrow0 + r >= a.M) continue;
-      st_wt(reinterpret_cast<uint32_t*>(a.out + size_t(lrow0 + r) * (a.N >> 1) + (n >> 1)),
-            f2bf_bits(h) | (f2bf_bits(h_next) << 16));
-    }
-  } else {
-    float sq[4];
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const int m = lrow0 + r;
-      const bool ok = m < a.M && col_ok;
-      const float nv = ok ? bf_round(rprev[r] + bf_round(v[r])) : 0.f;
-      sq[r] = nv * nv;
-      const float nv_next = dpp<kDppXor1>(nv);
-      if (ok && !(c & 1)) st_wt(reinterpret_cast<uint32_t*>(a.out + size_t(m) * a.N + n), f2bf_bits(nv) | (f2bf_bits(nv_next) << 16));
-    }
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      sq[r] = row16_sum(sq[r]);
-      if (c == 0) st_wt(a.ss_out + bx * kMaxM + lrow0 + r, sq[r]);
-    }
-  }
-}
-
-__global__ __launch_bounds__(kBlkNW * 64) void k_block(BlockArgs ba) {
-  __shared__ float red[kBlkNW][4][kWave];
-  __shared__ float red_ss[kBlkNW][kWave];
-  __shared__ int s_item;
-  const int t0 = ba.tiles[0], t1 = t0 + ba.tiles[1], total = t1 + ba.tiles[2];
-  unsigned* const done = ba.ctr + 8;
-  // Uniform loop: the next item is fetched by lane 0 behind the tile's closing
-  // barrier and read back after another, so the loop condition is one SGPR and
-  // no barrier sits in lane-divergent control flow. (A `for (;;)` with the
-  // fetch at its top and a `break` was restructured by the compiler into
-  // nested loops whose waves passed different barriers: it hung.)
-  // Items are claimed kBlkChunk at a time (a chunk is worked in order, so the
-  // in-order argument holds). One queue word serves about 88 dequeues per
-  // microsecond (MI355X_MICROARCH) against ~1,200 tiles per layer, but
-  // claiming 4 at once made a workgroup's tiles, already serial, longer still.
-  if (threadIdx.x == 0) s_item = int(__hip_atomic_fetch_add(ba.ctr, unsigned(kBlkChunk), __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_AGENT));
-  __syncthreads();
-  int base = __builtin_amdgcn_readfirstlane(s_item);
-  while (base < total) {
-    const int end = min(base + kBlkChunk, total);
-    for (int item = base; item < end; item++) {
-      const int phase = item < t0 ? 0 : item < t1 ? 1 : 2;
-      // One body for the three GEMMs (the phase's arguments read from the
-      // kernel-argument segment with a uniform index): three inlined bodies
-      // held every argument live at once, 223 VGPRs, one workgroup per CU.
-      const GemmArgs& ga = ba.g[phase];
-      const int tile = item - (phase == 0 ? 0 : phase == 1 ? t0 : t1);
-      blk_tile(ga, phase == 1 ? EPI_SILU : EPI_RESID, tile, phase == 0 ? nullptr : done + 8 * (phase - 1),
-               unsigned(phase == 0 ? 0 : ba.tiles[phase - 1]), ba.err, ba.wait_iters, red, red_ss);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores have landed
-      __syncthreads();                                  // ... and every wave's
-      if (threadIdx.x == 0) arrive(done + 8 * phase + (tile & 7));
-    }
-    if (threadIdx.x == 0) s_item = int(__hip_atomic_fetch_add(ba.ctr, unsigned(kBlkChunk), __ATOMIC_RELAXED,
-                                                              __HIP_MEMORY_SCOPE_AGENT));
-    __syncthreads();
-    base = __builtin_amdgcn_readfirstlane(s_item);
-  }
-  if (threadIdx.x == 0 && arrive(ba.ctr + 1) == gridDim.x - 1) {  // the last to leave resets the counters
-    for (int i = 0; i < kBlkCtr; i++) __hip_atomic_exchange(ba.ctr + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
 int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return (e && *e) ? atoi(e) : dflt;
@@ -1090,7 +833,6 @@ struct Workspace {
   unsigned* counters;  // [kMaxM * H] attention split tickets (self-resetting)
   float* kpart;        // split-K slabs of the widest split GEMM
   unsigned* kctr;      // split-K tickets per column tile (self-resetting)
-  unsigned* bctr;      // k_block work queue and arrival counters (self-resetting), then its error flag
   size_t bytes;
 };
 
@@ -1119,7 +861,6 @@ Workspace carve(const LlamaDims& d, uint8_t* base) {
   const int max_n = std::max(std::max(qkv_n, d.dim), 2 * d.ffn);
   w.kpart = reinterpret_cast<float*>(take(size_t(max_n / 16) * kMaxKs * 4 * kWave * 4));
   w.kctr = reinterpret_cast<unsigned*>(take(size_t(max_n / 16) * 4));
-  w.bctr = reinterpret_cast<unsigned*>(take(size_t(kBlkCtr + 1) * 4));
   w.bytes = off;
   return w;
 }
@@ -1239,29 +980,6 @@ hipError_t launch_gemm(GemmArgs a, hipStream_t s, int nw_override = 0) {
   if (nw == 8) return launch_nw<8, TN, EPI>(a, grid, s);
   if (nw == 4) return launch_nw<4, TN, EPI>(a, grid, s);
   return hipErrorInvalidValue;
-}
-
-// The O / gate/up / down GEMMs of one layer as one k_block launch of `wg`
-// workgroups (P2PT_DECODE_BLOCK=wg). Tile shapes as launch_gemm picks them
-// (16-column tiles or K parts), one 16-row tile (B <= 16), no split-K.
-hipError_t launch_block(GemmArgs o, GemmArgs g, GemmArgs dn, const Workspace& W, int wg, hipStream_t s) {
-  BlockArgs ba{};
-  GemmArgs* gs[3] = {&o, &g, &dn};
-  for (int i = 0; i < 3; i++) {
-    GemmArgs& a = *gs[i];
-    if (a.cwl <= 0) a.cwl = pick_cwl(a.N, 1, 0);
-    if (a.M > 16 || (a.kpl && (a.M * (16 >> a.cwl) > 16 || (16 >> a.cwl) != (1 << a.kpl) || a.K % (32 << a.kpl))))
-      return hipErrorInvalidValue;
-    a.ks = 1;
-    ba.g[i] = a;
-    ba.tiles[i] = a.N >> a.cwl;
-  }
-  ba.ctr = W.bctr;
-  ba.err = reinterpret_cast<int*>(W.bctr + kBlkCtr);
-  static const int iters = env_int("P2PT_DECODE_BLOCK_WAIT", 1 << 18);
-  ba.wait_iters = iters;
-  hipLaunchKernelGGL(k_block, dim3(wg), dim3(kBlkNW * 64), 0, s, ba);
-  return hipGetLastError();
 }
 
 bool dims_ok(const LlamaDims& d) {
@@ -1391,10 +1109,11 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
       o.kpl = 0;
       o.cwl = pick_cwl(d.dim, kTnResid, kResidMinTiles);
     }
-    // One persistent launch for O, gate/up and down (k_block) or three.
-    static const int blk_wg = env_int("P2PT_DECODE_BLOCK", 0);
-    const bool block = blk_wg > 0 && B <= 16;
-    if (!block && (e = launch_gemm<EPI_RESID, kTnResid>(o, s)) != hipSuccess) return int(e);
+    // Three launches: a persistent O -> gate/up -> down kernel (one launch, an
+    // in-order tile queue with write-through hand-offs) was built in round 3
+    // and measured slower in every variant (small b1 0.358 -> 0.61-1.09 ms,
+    // profiles/r03/decode_block/), then removed.
+    if ((e = launch_gemm<EPI_RESID, kTnResid>(o, s)) != hipSuccess) return int(e);
     ss_parts = d.dim / (kTnResid << o.cwl);
 
     // gate/up + SwiGLU
@@ -1406,7 +1125,7 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
       g.kpl = 0;
       g.cwl = 0;
     }
-    if (!block && (e = launch_gemm<EPI_SILU, 1>(g, s)) != hipSuccess) return int(e);
+    if ((e = launch_gemm<EPI_SILU, 1>(g, s)) != hipSuccess) return int(e);
 
     // down + residual
     GemmArgs dn{};
@@ -1416,11 +1135,7 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
       dn.kpl = 0;
       dn.cwl = pick_cwl(d.dim, kTnResid, kResidMinTiles);
     }
-    if (block) {
-      if ((e = launch_block(o, g, dn, W, blk_wg, s)) != hipSuccess) return int(e);
-    } else if ((e = launch_gemm<EPI_RESID, kTnResid>(dn, s)) != hipSuccess) {
-      return int(e);
-    }
+    if ((e = launch_gemm<EPI_RESID, kTnResid>(dn, s)) != hipSuccess) return int(e);
     ss_parts = d.dim / (kTnResid << dn.cwl);
   }
 
@@ -1440,13 +1155,6 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
   if ((e = launch_gemm<EPI_ARGMAX, kTnStore>(h, s, 4)) != hipSuccess) return int(e);
   hipLaunchKernelGGL(k_argmax_merge, dim3(emit_rows), dim3(256), 0, s, W.am_val, W.am_idx, parts, ids);
   return int(hipGetLastError());
-}
-
-// Byte offset of the k_block counters in the workspace (tests and probes read
-// them: [0] queue head, [1] exits, [8..31] arrivals, [32] wait time-outs).
-size_t p2pt_llama_block_ctr_offset(const LlamaDims* d) {
-  uint8_t* base = reinterpret_cast<uint8_t*>(uintptr_t(1) << 20);
-  return size_t(reinterpret_cast<uint8_t*>(carve(*d, base).bctr) - base);
 }
 
 // Standalone skinny GEMM (tests/benchmarks): out[M][N] = bf16(x[M][K] @ w[N][K]^T), M <= 64.

@@ -1,0 +1,67 @@
+"""Disjoint CPU sets for the processes of a benchmark on one host.
+
+The bulk and node rows run four kinds of process on one box — the load
+generator, the mock upstream, ``tunnel serve`` and ``tunnel proxy`` — and
+left to the scheduler they share and migrate between cores, which made the
+direct leg of one row move by 40 % between repetitions.
+``cpu_plan()`` splits the CPUs this process may use (``P2PT_CPUS`` overrides,
+e.g. ``0-15``; at most ``P2PT_CPU_BUDGET``, default 16, the pool's share per
+GPU) into one set per role, in the same proportions on every box:
+
+    loadgen 1/8, mock 1/8, serve 3/8, proxy 3/8   (16 CPUs: 2 / 2 / 6 / 6)
+
+Each tunnel process holds an association thread, a DTLS TX lane, a socket
+reader, an RX lane and its HTTP workers; the load generator and the mock are
+single reactors (the direct leg runs on exactly their CPUs too).
+"""
+from __future__ import annotations
+
+import os
+
+
+def parse_cpus(spec: str) -> list[int]:
+    out: list[int] = []
+    for part in spec.split(","):
+        part = part.strip()
+        if not part:
+            continue
+        if "-" in part:
+            lo, hi = part.split("-", 1)
+            out.extend(range(int(lo), int(hi) + 1))
+        else:
+            out.append(int(part))
+    return out
+
+
+def fmt_cpus(cpus: list[int]) -> str:
+    cpus = sorted(cpus)
+    parts, i = [], 0
+    while i < len(cpus):
+        j = i
+        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
+            j += 1
+        parts.append(str(cpus[i]) if i == j else f"{cpus[i]}-{cpus[j]}")
+        i = j + 1
+    return ",".join(parts)
+
+
+def available_cpus() -> list[int]:
+    spec = os.environ.get("P2PT_CPUS")
+    cpus = parse_cpus(spec) if spec else sorted(os.sched_getaffinity(0))
+    budget = int(os.environ.get("P2PT_CPU_BUDGET", "16"))
+    return cpus[:budget]
+
+
+def cpu_plan(cpus: list[int] | None = None) -> dict[str, str]:
+    """Role -> CPU list string (taskset / --cpu-affinity syntax); {} with fewer than 4 CPUs."""
+    cpus = available_cpus() if cpus is None else list(cpus)
+    n = len(cpus)
+    if n < 4:
+        return {}
+    lg = max(1, n // 8)
+    mk = max(1, n // 8)
+    rest = n - lg - mk
+    sv = rest // 2
+    plan = {"loadgen": cpus[:lg], "mock": cpus[lg:lg + mk], "serve": cpus[lg + mk:lg + mk + sv],
+            "proxy": cpus[lg + mk + sv:]}
+    return {k: fmt_cpus(v) for k, v in plan.items()}

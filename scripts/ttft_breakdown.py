@@ -18,6 +18,21 @@ generator, joins the per-stream events (all processes stamp CLOCK_MONOTONIC
     serve sched_in -> serve chan_tx         frame scheduler (queued behind the channel window?)
     serve chan_tx -> proxy chan_rx          SCTP, DTLS, UDP, socket reader, proxy association thread
     proxy chan_rx -> proxy first_body       hand-off to the client connection, its write
+
+--bulk-echo: BASELINE config #3 (N streams x 1 MB POST echoed) as a waterfall.
+Every request is stamped at each hop (TUNNEL_TRACE, buffered), and the steps
+of the load generator (all N requests in flight, the step ends with its
+slowest) are laid out against the direct run of the same load:
+
+  per request   proxy accept -> body_first -> req_end (client upload into the proxy)
+                proxy req_end -> chan_end (REQ_END waits in the proxy's scheduler)
+                proxy chan_end -> serve req_end (the upload's tail crosses)
+                serve req_end -> upstream_sent (buffered body written to the upstream)
+                serve upstream_sent -> res_headers -> res_end (upstream echo)
+                serve res_end -> chan_end -> proxy res_end (the download's tail crosses)
+  per step      when the last upload reached serve, the last upstream send,
+                the first / last echo finished at serve, the last response at
+                the proxy (ms from the step's first accept)
 """
 from __future__ import annotations
 
@@ -45,8 +60,14 @@ def main():
     ap.add_argument("--bulk", type=int, default=0, help="concurrent 64 MB GET /bulk downloads running through the "
                     "same tunnel for the whole measurement (the mixed row's head-of-line load)")
     ap.add_argument("--extra", default="", help="extra flags for both tunnel processes, e.g. --no-jumbo-loopback")
+    ap.add_argument("--bulk-echo", action="store_true", help="N x 1 MB POST echo waterfall (BASELINE config #3)")
+    ap.add_argument("--mb", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=40, help="--bulk-echo: timed steps")
+    ap.add_argument("--pin", action="store_true", help="pin loadgen / mock / serve / proxy to disjoint CPUs")
     a = ap.parse_args()
     ensure_native()
+    if a.bulk_echo:
+        return bulk_echo(a)
     with tempfile.NamedTemporaryFile(suffix=".jsonl", prefix="p2pt-trace-", delete=False) as tf:
         trace = tf.name
     port = free_port()
@@ -118,6 +139,91 @@ def main():
     res = {"transport": a.transport, "streams": a.streams, "bulk": a.bulk, "extra": a.extra, "hops": out}
     if not join_mock:
         res["note"] = "mock hops omitted: mock trace lines cannot be joined to streams when streams > 1"
+    print(json.dumps(res, indent=1))
+
+
+def _pct(v, q):
+    v = sorted(v)
+    return v[min(len(v) - 1, int(q * (len(v) - 1) + 0.5))] if v else None
+
+
+def bulk_echo(a):
+    from p2p_llm_tunnel_amd.utils.pinning import cpu_plan
+    streams = a.streams if a.streams > 1 else 64
+    plan = cpu_plan() if a.pin else {}
+    with tempfile.NamedTemporaryFile(suffix=".jsonl", prefix="p2pt-trace-", delete=False) as tf:
+        trace = tf.name
+    port = free_port()
+    mock = spawn("mock", (["taskset", "-c", plan["mock"]] if plan else []) + [binary("tunnel-mock"), "--port", str(port)])
+    mock.wait_for("Mock LLM server running", 10)
+
+    def run(target):
+        cmd = [binary("tunnel-loadgen"), "--target", f"127.0.0.1:{target}", "--streams", str(streams), "--steps",
+               str(a.steps), "--warmup", "2", "--post-bytes", str(a.mb << 20)]
+        if plan:
+            cmd = ["taskset", "-c", plan["loadgen"]] + cmd
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    try:
+        extra = [x for x in a.extra.split() if x]
+        pin_s = ["--cpu-affinity", plan["serve"]] if plan else []
+        pin_p = ["--cpu-affinity", plan["proxy"]] if plan else []
+        with Tunnel(f"http://127.0.0.1:{port}", transport=a.transport,
+                    env={"TUNNEL_TRACE": trace, "TUNNEL_TRACE_BUFFERED": "1"},
+                    serve_extra=extra + pin_s, proxy_extra=extra + pin_p) as t:
+            path = t.serve.wait_for("connection established", 1).split(" via ", 1)[-1] if a.transport == "webrtc" else ""
+            tr = run(t.proxy_port)
+        dr = run(port)
+        ev = {}
+        with open(trace) as f:
+            for line in f:
+                e = json.loads(line)
+                ev.setdefault(e["sid"], {})[(e["role"], e["ev"])] = e["t_us"]
+    finally:
+        mock.stop()
+        if os.path.exists(trace):
+            os.unlink(trace)
+    hops = [("proxy", "accept", "proxy", "body_first"), ("proxy", "body_first", "proxy", "req_end"),
+            ("proxy", "body_first", "proxy", "chan_tx"), ("proxy", "req_end", "proxy", "chan_end"),
+            ("proxy", "chan_end", "serve", "req_end"), ("serve", "req_headers", "serve", "req_end"),
+            ("serve", "req_end", "serve", "upstream_sent"), ("serve", "upstream_sent", "serve", "res_headers"),
+            ("serve", "res_headers", "serve", "res_end"), ("serve", "res_end", "serve", "chan_end"),
+            ("serve", "chan_end", "proxy", "res_end"), ("proxy", "accept", "proxy", "res_end")]
+    reqs = [e for sid, e in sorted(ev.items()) if ("proxy", "accept") in e and ("proxy", "res_end") in e]
+    per_hop = {}
+    for a_, b_, c_, d_ in hops:
+        v = [e[(c_, d_)] - e[(a_, b_)] for e in reqs if (a_, b_) in e and (c_, d_) in e]
+        if v:
+            per_hop[f"{a_}.{b_} -> {c_}.{d_}"] = {"n": len(v), "p10_ms": _pct(v, .1) / 1e3,
+                                                  "p50_ms": _pct(v, .5) / 1e3, "p90_ms": _pct(v, .9) / 1e3}
+    # Steps: the load generator releases `streams` requests at once; consecutive
+    # groups of that many accepts (the 2 warm-up steps included, then dropped).
+    reqs.sort(key=lambda e: e[("proxy", "accept")])
+    marks = {"last upload at proxy (req_end)": ("proxy", "req_end", max),
+             "last REQ_END into the channel": ("proxy", "chan_end", max),
+             "first upload complete at serve": ("serve", "req_end", min),
+             "last upload complete at serve": ("serve", "req_end", max),
+             "last request written upstream": ("serve", "upstream_sent", max),
+             "first echo complete at serve": ("serve", "res_end", min),
+             "last echo complete at serve": ("serve", "res_end", max),
+             "last response complete at proxy": ("proxy", "res_end", max)}
+    steps = []
+    for i in range(0, len(reqs) - streams + 1, streams):
+        g = reqs[i:i + streams]
+        t0 = min(e[("proxy", "accept")] for e in g)
+        row = {"accept_spread_ms": (max(e[("proxy", "accept")] for e in g) - t0) / 1e3}
+        for name, (role, evn, agg) in marks.items():
+            vals = [e[(role, evn)] for e in g if (role, evn) in e]
+            row[name] = (agg(vals) - t0) / 1e3 if vals else None
+        steps.append(row)
+    steps = steps[2:] if len(steps) > 4 else steps
+    waterfall = {k: statistics.median([s[k] for s in steps if s.get(k) is not None]) for k in steps[0]} if steps else {}
+    res = {"mode": "bulk-echo", "transport": a.transport, "extra": a.extra, "path": path, "pinned": plan,
+           "streams": streams, "mb": a.mb, "steps": a.steps,
+           "tunneled": {"req_s": tr["req_s"], "step_ms_p50": statistics.median(tr["step_ms"]), "errors": tr["errors"]},
+           "direct": {"req_s": dr["req_s"], "step_ms_p50": statistics.median(dr["step_ms"]), "errors": dr["errors"]},
+           "ratio": tr["req_s"] / dr["req_s"] if dr["req_s"] else None,
+           "step_waterfall_ms_median": waterfall, "per_request": per_hop}
     print(json.dumps(res, indent=1))
 
 

@@ -328,40 +328,19 @@ def test_endpoint_honours_and_validates_sampling_parameters():
                                         "options": {"temperature": 0.9, "seed": 7}})
         assert st == 200 and json.loads(o1)["done"]
         for bad in ({"temperature": -1}, {"top_p": 0}, {"top_k": 2.5}, {"n": 2}, {"presence_penalty": 0.3},
-                    {"logit_bias": {"5": 1}}, {"stop": ["\n"]}):
+                    {"logit_bias": {"5": 1}}, {"stop": [7]}):
             st, body = post("/v1/chat/completions", dict(chat, **bad))
             assert st == 400, (bad, body)
+        # Stop sequences: every piece of the random-init model starts with " t",
+        # so " t" ends a completion before its first token; a sequence that
+        # never occurs leaves the completion as it was.
+        st, o = post("/v1/chat/completions", dict(chat, stop=" t", stream=False))
+        j = json.loads(o)
+        assert st == 200 and j["choices"][0]["message"]["content"] == "" and j["choices"][0]["finish_reason"] == "stop"
+        st, o = post("/v1/chat/completions", dict(chat, stop=["never-emitted"], stream=False))
+        assert st == 200 and json.loads(o)["choices"][0]["finish_reason"] == "length"
         st, _ = post("/api/generate", {"prompt": "hi", "options": {"repeat_penalty": 1.1}})
         assert st == 400
     finally:
         engine.stop()
         srv.shutdown()
-
-
-@cuda
-@pytest.mark.parametrize("cfg,B,graph", [("small", 1, True), ("small", 4, False), ("tiny", 3, True), ("micro", 16, False)])
-def test_block_kernel_matches_launches(cfg, B, graph, tmp_path):
-    # P2PT_DECODE_BLOCK: the O / gate-up / down GEMMs of a layer as one
-    # persistent launch (in-order work queue, write-through hand-offs). Same
-    # weights and tokens as the launched kernels, run in two processes (the
-    # switch is read once per process): logits, greedy ids and caches agree,
-    # and both stay within the fp32 reference's tolerance. The graph variants
-    # replay the block many times (its counters must reset themselves).
-    import subprocess
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    res = {}
-    for name, env in (("launch", {}), ("block", {"P2PT_DECODE_BLOCK": "256"})):
-        out = str(tmp_path / f"{name}.pt")
-        args = [sys.executable, os.path.join(here, "gpu_decode_run.py"), cfg, str(B), "40", out] + (["--graph"] if graph else [])
-        subprocess.run(args, check=True, timeout=300, env={**os.environ, **env})
-        res[name] = torch.load(out, weights_only=True)
-    a, b = res["launch"], res["block"]
-    scale = a["logits"].abs().max().item()
-    assert (a["logits"] - b["logits"]).abs().max().item() <= 0.01 * scale
-    top2 = a["logits"].topk(2, -1).values
-    confident = (top2[:, 0] - top2[:, 1]) > 0.03 * scale
-    assert torch.equal(a["ids"][confident], b["ids"][confident])
-    assert (a["k"] - b["k"]).abs().max().item() <= 0.02 * a["k"].abs().max().item()
-    ref = b["ref"]
-    assert (b["logits"] - ref).abs().max().item() < 0.05 * ref.abs().max().item()

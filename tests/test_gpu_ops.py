@@ -212,8 +212,12 @@ def _draws(ops, row, T, k, p, n_launch=200, B=64, seed=1234):
 
 
 @cuda
-@pytest.mark.parametrize("T,k,p", [(0.8, 0, 1.0), (1.0, 20, 1.0), (0.7, 0, 0.9), (1.2, 50, 0.8), (1.0, 0, 0.5)])
-def test_sample_matches_reference_distribution(ops, T, k, p):
+@pytest.mark.parametrize("V,scale,T,k,p", [
+    (1000, 2.0, 0.8, 0, 1.0), (1000, 2.0, 1.0, 20, 1.0), (1000, 2.0, 0.7, 0, 0.9), (1000, 2.0, 1.2, 50, 0.8),
+    (1000, 2.0, 1.0, 0, 0.5),
+    # Real vocab sizes: the radix-select top-k / top-p passes over 32,000 logits.
+    (32000, 2.0, 1.0, 50, 0.9), (32000, 4.0, 0.8, 0, 0.9), (32000, 3.0, 1.0, 50, 1.0)])
+def test_sample_matches_reference_distribution(ops, V, scale, T, k, p):
     """12,800 draws from one logits row vs the fp32 reference distribution:
     a chi-square test (bins of expected count >= 5, the rest pooled) at the
     0.01 % level, and no draw outside the kept set. (Over 20 seeds per case
@@ -221,8 +225,7 @@ def test_sample_matches_reference_distribution(ops, T, k, p):
     reproduces every draw: profiles/r03/sample_diag.json.)"""
     from scipy.stats import chi2
     torch.manual_seed(11)
-    V = 1000
-    row = bf(torch.randn(V, device="cuda") * 2.0)
+    row = bf(torch.randn(V, device="cuda") * scale)
     probs = _ref_probs(row, T, k, p).double().cpu()
     got = _draws(ops, row, T, k, p).cpu()
     n = got.numel()

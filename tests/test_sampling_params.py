@@ -2,6 +2,8 @@
 OpenAI fields (temperature, top_p, seed, the top_k extension) and Ollama
 "options" are parsed and range-checked; parameters that would change the
 output but are not implemented are refused with 400 instead of being ignored.
+Stop sequences (OpenAI "stop", Ollama "options.stop") end a completion at the
+first match in its text, streamed or not.
 The on-device sampler itself is tested on the GPU (tests/test_gpu_ops.py,
 tests/test_gpu_model.py)."""
 import http.client
@@ -9,8 +11,9 @@ import json
 
 import pytest
 
-from p2p_llm_tunnel_amd.models.server import Engine, SamplingError, sampling_params, start_server
-from tests.test_inference_server import FakeModel
+from p2p_llm_tunnel_amd.models.server import (Engine, SamplingError, StopMatcher, sampling_params, start_server,
+                                              stop_sequences)
+from tests.test_inference_server import FakeModel, expected
 
 
 def test_defaults_are_greedy():
@@ -38,9 +41,8 @@ def test_openai_and_ollama_fields():
     ({"top_k": -1}, False), ({"top_k": 3.5}, False), ({"seed": "x"}, False), ({"n": 2}, False),
     ({"best_of": 3}, False), ({"presence_penalty": 0.5}, False), ({"frequency_penalty": -1}, False),
     ({"logprobs": True}, False), ({"top_logprobs": 2}, False), ({"logit_bias": {"1": 5}}, False),
-    ({"stop": ["\n\n"]}, False), ({"stop": "END"}, False),
     ({"options": {"repeat_penalty": 1.1}}, True), ({"options": {"mirostat": 2}}, True),
-    ({"options": {"min_p": 0.05}}, True), ({"options": {"stop": ["x"]}}, True), ({"options": "hot"}, True),
+    ({"options": {"min_p": 0.05}}, True), ({"options": "hot"}, True),
     ({"options": {"temperature": 500}}, True),
 ])
 def test_unsupported_or_out_of_range_is_refused(body, ollama):
@@ -66,6 +68,102 @@ def test_http_400_names_the_parameter():
         c.request("POST", "/v1/chat/completions", body=json.dumps({"messages": [], "max_tokens": 2, "n": 1}))
         r = c.getresponse()
         assert r.status == 200 and r.read()  # the connection stays usable
+    finally:
+        srv.shutdown()
+        eng.stop()
+
+
+@pytest.mark.parametrize("body,ollama,want", [
+    ({}, False, []), ({"stop": None}, False, []), ({"stop": "END"}, False, ["END"]),
+    ({"stop": ["a", "", "bc"]}, False, ["a", "bc"]), ({"options": {"stop": ["\n", "x"]}}, True, ["\n", "x"]),
+    ({"options": None}, True, []),
+])
+def test_stop_sequences_parsed(body, ollama, want):
+    assert stop_sequences(body, ollama) == want
+
+
+@pytest.mark.parametrize("body,ollama", [
+    ({"stop": 5}, False), ({"stop": ["a", 3]}, False), ({"stop": ["a", "b", "c", "d", "e"]}, False),
+    ({"options": {"stop": [1]}}, True), ({"stop": {"a": 1}}, False),
+])
+def test_bad_stop_sequences_refused(body, ollama):
+    with pytest.raises(SamplingError):
+        stop_sequences(body, ollama)
+
+
+def test_stop_matcher_holds_back_only_a_possible_prefix():
+    m = StopMatcher(["END", "\n\n"])
+    assert m.push("hello E") == ("hello ", False)  # "E" could begin END
+    assert m.push("N") == ("", False)
+    assert m.push("X more") == ("ENX more", False)  # it did not
+    assert m.push(" then\n") == (" then", False)
+    assert m.push("\nrest") == ("", True)  # the match and what follows are dropped
+    m = StopMatcher(["abc"])
+    assert m.push("xxab") == ("xx", False) and m.flush() == "ab"
+    m = StopMatcher(["t5", "zz"])
+    assert m.push(" t1 t5") == (" t1 ", True)  # earliest match wins
+    m = StopMatcher(["aa", "b"])
+    assert m.push("xab") == ("xa", True)
+
+
+def _stop_server():
+    eng = Engine(max_batch=4, model=FakeModel())
+    srv, port, _ = start_server(port=0, engine=eng, model_name="fake")
+    return srv, port, eng
+
+
+def _post(port, path, body):
+    c = http.client.HTTPConnection("127.0.0.1", port, timeout=20)
+    c.request("POST", path, body=json.dumps(body), headers={"content-type": "application/json"})
+    r = c.getresponse()
+    return r.status, r.read()
+
+
+def test_stop_sequences_end_completions():
+    """The FakeModel's pieces are " t<id>": stop on the third token's piece
+    (split across two pieces), streamed and not, OpenAI and Ollama."""
+    toks = expected(b"hello", 12)
+    full = "".join(f" t{t}" for t in toks)
+    stop = f"{toks[2]} t{toks[3]}"  # spans the 3rd and 4th pieces
+    cut = full[:full.index(stop)]
+    srv, port, eng = _stop_server()
+    try:
+        msgs = [{"role": "user", "content": "hello"}]
+        st, data = _post(port, "/v1/chat/completions", {"messages": msgs, "max_tokens": 12, "stop": [stop, "nope"]})
+        j = json.loads(data)
+        assert st == 200 and j["choices"][0]["message"]["content"] == cut
+        assert j["choices"][0]["finish_reason"] == "stop"
+        st, data = _post(port, "/v1/chat/completions", {"messages": msgs, "max_tokens": 12, "stop": stop,
+                                                         "stream": True})
+        events = [l[6:] for l in data.split(b"\n") if l.startswith(b"data: ")]
+        assert st == 200 and events[-1] == b"[DONE]"
+        objs = [json.loads(e) for e in events[:-1]]
+        assert "".join(o["choices"][0]["delta"].get("content", "") for o in objs) == cut
+        assert objs[-1]["choices"][0]["finish_reason"] == "stop"
+        st, data = _post(port, "/v1/completions", {"prompt": "hello", "max_tokens": 12, "stop": "zzz"})
+        j = json.loads(data)  # no match: the whole text, held-back tails included
+        assert j["choices"][0]["text"] == full and j["choices"][0]["finish_reason"] == "length"
+        st, data = _post(port, "/api/generate", {"prompt": "hello", "num_predict": 12,
+                                                  "options": {"stop": [stop]}})
+        lines = [json.loads(l) for l in data.split(b"\n") if l.strip()]
+        assert st == 200 and lines[-1]["done"] and "".join(x["response"] for x in lines) == cut
+    finally:
+        srv.shutdown()
+        eng.stop()
+
+
+def test_sampling_refused_on_an_eager_engine():
+    """The eager step (CPU stand-ins) has no sampler: a sampled request is
+    refused instead of silently answered greedily (advice r3)."""
+    srv, port, eng = _stop_server()
+    try:
+        st, data = _post(port, "/v1/chat/completions", {"messages": [], "temperature": 0.8, "max_tokens": 2})
+        assert st == 400 and b"graph-captured" in data
+        st, data = _post(port, "/v1/chat/completions", {"messages": [], "temperature": 0, "max_tokens": 2})
+        assert st == 200
+        st, data = _post(port, "/v1/chat/completions", {"messages": [], "temperature": 1, "top_k": 1,
+                                                         "max_tokens": 2})
+        assert st == 200  # top-1 is the argmax
     finally:
         srv.shutdown()
         eng.stop()
