@@ -163,7 +163,7 @@ def main():
                   file=sys.stderr, flush=True)
             for tr in trs:
                 t = tunnels[tr]
-                path = t.serve.wait_for("connection established", 5).split(" via ", 1)[-1]
+                path = t.serve.wait_for("WebRTC connection established", 5).split(" via ", 1)[-1]
                 base = rss_kb(t.proxy.popen.pid)
                 sse_r, bulk_r, stats, peak = scenario(t.proxy_port, a, t.proxy.popen.pid)
                 run = {"rep": rep, "transport": tr, "path": path,

@@ -40,22 +40,30 @@ def main():
     ap.add_argument("--mb", type=int, default=1)
     ap.add_argument("--profile-dir", default=None)
     ap.add_argument("--extra", default="", help="extra flags for both tunnel processes, e.g. --no-jumbo-loopback")
+    ap.add_argument("--serve-extra", default="", help="extra flags for serve only, e.g. --stream-body-threshold 65536")
+    ap.add_argument("--pin", action="store_true", help="pin loadgen / mock / serve / proxy to disjoint CPUs")
     a = ap.parse_args()
     extra = [x for x in a.extra.split() if x]
+    serve_only = [x for x in a.serve_extra.split() if x]
+    from p2p_llm_tunnel_amd.utils.pinning import cpu_plan
+    plan = cpu_plan() if a.pin else {}
     env = None
     if a.profile_dir:
         os.makedirs(a.profile_dir, exist_ok=True)
         env = {"TUNNEL_PROFILE": os.path.join(os.path.abspath(a.profile_dir), "tunnel.%p.prof"),
                "TUNNEL_PROFILE_HZ": os.environ.get("TUNNEL_PROFILE_HZ", "2000")}
-    mock, port = start_mock("native", 100, 5)
+    mock, port = start_mock("native", 100, 5, plan.get("mock"))
     ms, mp = free_port(), free_port()
     out = {}
     try:
         with Tunnel(f"http://127.0.0.1:{port}", transport=a.transport, env=env,
-                    serve_extra=["--metrics-listen", f"127.0.0.1:{ms}"] + extra,
-                    proxy_extra=["--metrics-listen", f"127.0.0.1:{mp}"] + extra) as t:
+                    serve_extra=["--metrics-listen", f"127.0.0.1:{ms}"] + extra + serve_only +
+                    (["--cpu-affinity", plan["serve"]] if plan else []),
+                    proxy_extra=["--metrics-listen", f"127.0.0.1:{mp}"] + extra +
+                    (["--cpu-affinity", plan["proxy"]] if plan else [])) as t:
             def run(target):
-                r = subprocess.run([binary("tunnel-loadgen"), "--target", f"127.0.0.1:{target}", "--streams",
+                r = subprocess.run((["taskset", "-c", plan["loadgen"]] if plan else []) +
+                                   [binary("tunnel-loadgen"), "--target", f"127.0.0.1:{target}", "--streams",
                                     str(a.streams), "--steps", str(a.steps), "--warmup", "1", "--post-bytes",
                                     str(a.mb << 20)], capture_output=True, text=True, timeout=600)
                 return json.loads(r.stdout.strip().splitlines()[-1])
@@ -66,7 +74,7 @@ def main():
             wall = time.time() - t0
             c1 = {k: cpu_s(v) for k, v in pids.items()}
             dr = run(port)
-            out = {"transport": a.transport, "extra": a.extra, "path": t.serve.wait_for("connection established", 1)
+            out = {"transport": a.transport, "extra": a.extra, "serve_extra": a.serve_extra, "pinned": plan, "path": t.serve.wait_for("WebRTC connection established", 1)
                    .split(" via ", 1)[-1] if a.transport == "webrtc" else "", "streams": a.streams, "body_mb": a.mb, "steps": a.steps,
                    "tunneled_req_s": tr["req_s"], "direct_req_s": dr["req_s"],
                    "tunneled_MBps_each_way": tr["req_s"] * a.mb * 1.048576, "errors": tr["errors"] + dr["errors"],
@@ -76,6 +84,15 @@ def main():
                 txt = urllib.request.urlopen(f"http://127.0.0.1:{p}/metrics", timeout=5).read().decode()
                 out[f"{name}_sctp"] = {l.split()[0]: float(l.split()[1]) for l in txt.splitlines()
                                        if l.startswith(("tunnel_sctp", "tunnel_dtls", "tunnel_udp"))}
+            # Loss the stack could not see and self-inflicted drops, both sides.
+            out["loss"] = {k: sum(out[f"{n}_sctp"].get(m, 0.0) for n in ("serve", "proxy")) for k, m in (
+                ("udp_rx_overflow", "tunnel_udp_rx_overflow_total"), ("lane_send_drops", "tunnel_dtls_lane_send_drops"),
+                ("lane_send_waits", "tunnel_dtls_lane_send_waits"), ("reader_waits", "tunnel_udp_reader_waits"), ("reader_escapes", "tunnel_udp_reader_escapes"),
+                ("fast_retransmits", "tunnel_sctp_fast_retransmits"), ("retransmits", "tunnel_sctp_retransmits"),
+                ("t3_expirations", "tunnel_sctp_t3_expirations"), ("tlp_probes", "tunnel_sctp_tlp_probes"),
+                ("rack_marks", "tunnel_sctp_rack_marks"), ("spurious_undos", "tunnel_sctp_spurious_undos"),
+                ("probe_ambiguous", "tunnel_sctp_probe_ambiguous"), ("dup_tsns_received", "tunnel_sctp_dup_tsns_received"),
+                ("rwnd_drops", "tunnel_sctp_rwnd_drops"), ("dtls_rx_dropped", "tunnel_dtls_rx_dropped"))}
     finally:
         mock.stop()
     print(json.dumps(out))

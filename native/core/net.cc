@@ -33,6 +33,19 @@ uint64_t udp_socket_drops(int fd) {
   return 0;
 }
 
+bool udp_socket_rmem(int fd, size_t* alloc, size_t* limit) {
+#ifdef SO_MEMINFO
+  uint32_t mi[SK_MEMINFO_VARS] = {};
+  socklen_t l = sizeof mi;
+  if (fd >= 0 && getsockopt(fd, SOL_SOCKET, SO_MEMINFO, mi, &l) == 0 && l > SK_MEMINFO_RCVBUF * sizeof(uint32_t)) {
+    *alloc = mi[SK_MEMINFO_RMEM_ALLOC];
+    *limit = mi[SK_MEMINFO_RCVBUF];
+    return true;
+  }
+#endif
+  return false;
+}
+
 size_t udp_socket_rcvbuf(int fd) {
   int v = 0;
   socklen_t l = sizeof v;

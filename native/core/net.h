@@ -49,6 +49,8 @@ struct SockAddr {
 // datagram) and the effective receive buffer size. 0 when unavailable.
 uint64_t udp_socket_drops(int fd);
 size_t udp_socket_rcvbuf(int fd);
+// Bytes (truesize) queued in the socket's receive buffer, and its limit.
+bool udp_socket_rmem(int fd, size_t* alloc, size_t* limit);
 // Sets SO_RCVBUF / SO_SNDBUF to `bytes`, retrying with the *FORCE variants
 // (CAP_NET_ADMIN) when net.core.[rw]mem_max clamps the request, and enables
 // SO_RXQ_OVFL. Returns the effective receive buffer.

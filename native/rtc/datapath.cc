@@ -397,12 +397,22 @@ void RxReader::run() {
   pollfd pf[2] = {{fd_.fd, POLLIN, 0}, {stop_fd_, POLLIN, 0}};
   while (!stop_.load(std::memory_order_acquire)) {
     if (outstanding_.load(std::memory_order_acquire) >= kMaxOutstanding) {
-      waits.fetch_add(1, std::memory_order_relaxed);
-      std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait_for(lk, std::chrono::milliseconds(5), [this] {
-        return stop_.load(std::memory_order_acquire) || outstanding_.load(std::memory_order_acquire) < kMaxOutstanding;
-      });
-      continue;
+      // Back-pressure: the association thread is kMaxOutstanding bursts
+      // behind, so the socket buffer holds what arrives meanwhile. Escape
+      // before that buffer overflows (the kernel would drop what SCTP then
+      // has to retransmit, and nothing in the stack would see why): past half
+      // of it, read on. The sender's windows still bound what can pile up.
+      size_t alloc = 0, limit = 0;
+      if (escape_ && udp_socket_rmem(fd_.fd, &alloc, &limit) && limit && alloc * 2 >= limit) {
+        escapes.fetch_add(1, std::memory_order_relaxed);
+      } else {
+        waits.fetch_add(1, std::memory_order_relaxed);
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait_for(lk, std::chrono::milliseconds(1), [this] {
+          return stop_.load(std::memory_order_acquire) || outstanding_.load(std::memory_order_acquire) < kMaxOutstanding;
+        });
+        continue;
+      }
     }
     if (poll(pf, 2, 100) <= 0 || (pf[1].revents & POLLIN)) continue;  // the loop head sees stop_
     auto burst = std::make_unique<Burst>();

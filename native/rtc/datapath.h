@@ -216,7 +216,10 @@ class RxReader {
   RxReader& operator=(const RxReader&) = delete;
   void done();  // association thread: one delivered burst processed
 
-  std::atomic<uint64_t> bursts{0}, datagrams{0}, records{0}, raw_datagrams{0}, waits{0}, gro_batches{0};
+  // waits: back-pressure pauses (the association thread kMaxOutstanding
+  // bursts behind); escapes: reads taken anyway because the socket buffer was
+  // past half full (a pause there would end in kernel drops).
+  std::atomic<uint64_t> bursts{0}, datagrams{0}, records{0}, raw_datagrams{0}, waits{0}, escapes{0}, gro_batches{0};
   // The socket's drop count as last reported by SO_RXQ_OVFL (cumulative).
   std::atomic<uint32_t> rxq_ovfl{0};
 
@@ -229,6 +232,10 @@ class RxReader {
   std::shared_ptr<const RecordKeys> keys_;
   Deliver deliver_;
   uint64_t id_ = 0;
+  bool escape_ = [] {  // TUNNEL_RX_ESCAPE=0: pause however full the socket buffer is (A/B, tests)
+    const char* e = getenv("TUNNEL_RX_ESCAPE");
+    return !(e && *e == '0');
+  }();
   BufPool pool_{65536};
   std::mutex mu_;
   std::condition_variable cv_;

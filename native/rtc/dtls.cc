@@ -645,6 +645,7 @@ void DtlsTransport::on_datagram(std::shared_ptr<const void> owner, uint8_t* p, s
       size_t ptl;
       if (!fast_decrypt(rec, len, type, rd48(rec + 5), &pt, &ptl)) {
         LOG_TRACE(kT, "dropping DTLS record that fails authentication or replay check");
+        rx_dropped_++;
         continue;
       }
       if (!deliver_plain(owner, type, pt, ptl)) return;
@@ -808,6 +809,7 @@ void DtlsTransport::deliver_opened(RxBatch& b) {
   for (auto& x : b.recs) {
     if (!x.ok || replay_seen(x.seq)) {
       LOG_TRACE(kT, "dropping DTLS record that fails authentication or replay check");
+      rx_dropped_++;
       continue;
     }
     replay_mark(x.seq);

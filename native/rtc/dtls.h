@@ -109,6 +109,9 @@ class DtlsTransport : public std::enable_shared_from_this<DtlsTransport> {
   const TxLaneState* tx_lane_state() const { return tx_state_.get(); }
   uint64_t lane_tx_batches() const { return lane_tx_batches_; }
   uint64_t lane_rx_batches() const { return lane_rx_batches_; }
+  // Records dropped on receive (failed authentication, replayed or older than
+  // the 64-record replay window): loss the SCTP layer sees as a hole.
+  uint64_t rx_dropped() const { return rx_dropped_; }
   uint64_t inline_tx_batches() const { return inline_tx_batches_; }
   void close();
   bool connected() const { return connected_; }
@@ -178,6 +181,7 @@ class DtlsTransport : public std::enable_shared_from_this<DtlsTransport> {
   std::unique_ptr<Lane> tx_lane_, rx_lane_;
   std::shared_ptr<TxLaneState> tx_state_;
   std::shared_ptr<LaneFd> lane_fd_;
+  uint64_t rx_dropped_ = 0;
   std::function<bool(TxTarget&)> tx_target_;
   std::shared_ptr<TxBatch> tx_pend_;
   std::shared_ptr<TxBatchPool> tx_pool_;

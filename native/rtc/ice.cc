@@ -188,7 +188,8 @@ void IceAgent::open_sockets() {
       int one = 1;
       setsockopt(fd, IPPROTO_IPV6, IPV6_V6ONLY, &one, sizeof one);
     }
-    const size_t rb = udp_socket_buffers(fd, 4 << 20);
+    const char* kb = getenv("TUNNEL_UDP_BUF_KB");  // tests / A-B: the socket buffers asked for (default 4 MiB)
+    const size_t rb = udp_socket_buffers(fd, kb && *kb ? std::max(16, atoi(kb)) * 1024 : 4 << 20);
     LOG_DEBUG(kT, "UDP socket %s: receive buffer %zu bytes", ia.addr.str().c_str(), rb);
     enable_gro(fd);
     SockAddr a = ia.addr;

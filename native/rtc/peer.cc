@@ -557,6 +557,26 @@ void PeerConnection::start_sctp() {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().rack_marks) : 0.0;
   });
+  metrics::gauge_fn("tunnel_sctp_spurious_undos", [w] {
+    auto s = w.lock();
+    return s && s->sctp_ ? double(s->sctp_->stats().spurious_undos) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_sctp_probe_ambiguous", [w] {
+    auto s = w.lock();
+    return s && s->sctp_ ? double(s->sctp_->stats().probe_ambiguous) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_sctp_dup_tsns_received", [w] {
+    auto s = w.lock();
+    return s && s->sctp_ ? double(s->sctp_->stats().dup_tsns) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_sctp_rwnd_drops", [w] {
+    auto s = w.lock();
+    return s && s->sctp_ ? double(s->sctp_->stats().rwnd_drops) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_dtls_rx_dropped", [w] {
+    auto s = w.lock();
+    return s && s->dtls_ ? double(s->dtls_->rx_dropped()) : 0.0;
+  });
   metrics::gauge_fn("tunnel_sctp_hystart_exits", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().hystart_exits) : 0.0;
@@ -609,6 +629,10 @@ void PeerConnection::start_sctp() {
   metrics::gauge_fn("tunnel_udp_reader_waits", [w] {
     auto s = w.lock();
     return s && s->rx_reader_ ? double(s->rx_reader_->waits.load()) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_udp_reader_escapes", [w] {
+    auto s = w.lock();
+    return s && s->rx_reader_ ? double(s->rx_reader_->escapes.load()) : 0.0;
   });
   metrics::gauge_fn("tunnel_dtls_lane_gso_msgs", [w] {
     auto s = w.lock();

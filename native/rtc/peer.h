@@ -112,6 +112,7 @@ class PeerConnection : public std::enable_shared_from_this<PeerConnection> {
   size_t sctp_mtu() const { return mtu_; }
   const DtlsTransport* dtls() const { return dtls_.get(); }
   IceAgent* ice() const { return ice_.get(); }
+  const SctpAssociation* sctp() const { return sctp_.get(); }
 
   std::function<void(const std::string& candidate_json)> on_ice_candidate;
   std::function<void()> on_gathering_complete;

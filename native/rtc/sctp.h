@@ -57,13 +57,17 @@ struct SctpStats {
   uint64_t data_chunks_sent = 0, data_chunks_received = 0;
   uint64_t retransmits = 0, fast_retransmits = 0, t3_expirations = 0;
   uint64_t tlp_probes = 0, rack_marks = 0, random_loss_events = 0;
-  uint64_t random_loss_cuts = 0;  // sustained random loss: the periodic 0.85 cut
+  uint64_t random_loss_cuts = 0;  // random-loss episodes that cut cwnd (TUNNEL_SCTP_RANDOM_BETA_PCT)
   uint64_t congestion_cuts = 0;   // loss episodes read as congestion (0.7 cut)
   uint64_t queue_cuts = 0;        // short-path queue bound: cwnd cuts for a standing queue
   uint64_t over_bdp_losses = 0;   // ... of them because cwnd was past the delivery-rate BDP
   uint64_t hystart_exits = 0;     // initial slow starts ended by HyStart++ (rising delay)
   uint64_t dup_copies_sent = 0;  // redundant copies of small messages (lossy paths)
   uint64_t early_deliveries = 0;  // messages handed up ahead of a TSN gap (another stream's loss)
+  uint64_t rwnd_drops = 0;        // out-of-order chunks dropped past the receive window
+  uint64_t probe_ambiguous = 0;   // probe acks not taken as loss evidence (originals arrived with them)
+  uint64_t spurious_undos = 0;    // loss episodes found spurious afterwards: cwnd cut undone
+  uint64_t dup_tsns = 0;          // DATA chunks received again (spurious retransmissions, or lost SACKs)
   uint64_t sacks_sent = 0, sacks_received = 0;
   uint64_t bytes_sent = 0, bytes_received = 0;
 };
@@ -260,6 +264,15 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   static constexpr int kDrRounds = 10;
   bool random_episode_ = false;  // a random-loss episode (no recovery period) is open until random_exit_
   uint32_t random_exit_ = 0;
+  // Spurious-loss undo (after Linux's DSACK undo / RFC 3708): a loss
+  // episode's cwnd cut is taken back if, once the window it covered is
+  // acknowledged, none of its retransmissions was needed — every chunk it
+  // marked was acknowledged before being resent, or its resend was reported
+  // back as a duplicate TSN (the original had arrived).
+  bool ep_active_ = false;
+  uint32_t ep_exit_ = 0;
+  size_t ep_undo_cwnd_ = 0, ep_undo_ssthresh_ = 0;
+  int64_t ep_rtx_ = 0;  // retransmissions sent in the episode, less duplicate reports of them
   bool dr_active_ = false, dr_limited_ = false;
   uint32_t dr_end_ = 0;
   uint64_t dr_start_us_ = 0, dr_bytes_ = 0;
@@ -284,9 +297,7 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   int hs_samples_ = 0, hs_css_rounds_ = 0;
   uint32_t hs_window_end_ = 0;
   uint64_t hs_last_min_ = UINT64_MAX, hs_cur_min_ = UINT64_MAX, hs_css_base_ = 0;
-  int random_streak_ = 0;   // random-loss episodes in a row (see handle_sack)
   uint64_t last_loss_us_ = 0;
-  static constexpr int kRandomStreakCut = 8;
   uint64_t rto_us_;
   uint64_t srtt_us_ = 0, rttvar_us_ = 0;
   uint64_t min_rtt_us_ = 0;  // smallest RTT sample: the path's base RTT

@@ -8,6 +8,7 @@
 #include "core/aesgcm.h"
 #include "core/crypto.h"
 #include "core/json.h"
+#include "core/net.h"
 #include "core/reactor.h"
 #include "http/http.h"
 #include "proto/frame.h"
@@ -381,4 +382,34 @@ TEST(flow_window_autotune) {
   }
   CHECK_EQ(slow.win, kFlowWindow);
   CHECK_EQ(extra, uint64_t(0));
+}
+
+// The receive-overflow counter the bench reports (tunnel_udp_rx_overflow_total)
+// reads the socket's drop count: a socket that is never read and given more
+// datagrams than its buffer holds counts exactly the ones the kernel dropped.
+TEST(udp_socket_drops_counts_receive_overflow) {
+  int rx = ::socket(AF_INET, SOCK_DGRAM | SOCK_CLOEXEC, 0), tx = ::socket(AF_INET, SOCK_DGRAM | SOCK_CLOEXEC, 0);
+  SockAddr a;
+  CHECK(SockAddr::parse("127.0.0.1", 0, a));
+  CHECK(::bind(rx, a.sa(), a.len) == 0);
+  a.len = sizeof a.ss;
+  getsockname(rx, a.sa(), &a.len);
+  int small = 4096;
+  setsockopt(rx, SOL_SOCKET, SO_RCVBUF, &small, sizeof small);
+  CHECK_EQ(udp_socket_drops(rx), uint64_t(0));
+  CHECK(udp_socket_rcvbuf(rx) > 0);
+  std::vector<uint8_t> d(1200, 7);
+  int sent = 0;
+  for (int i = 0; i < 200; i++)
+    if (::sendto(tx, d.data(), d.size(), 0, a.sa(), a.len) == ssize_t(d.size())) sent++;
+  // Count what is still queued, then compare with the drops.
+  int queued = 0;
+  while (::recv(rx, d.data(), d.size(), MSG_DONTWAIT) > 0) queued++;
+  const uint64_t drops = udp_socket_drops(rx);
+  CHECK(drops > 0);
+  CHECK_EQ(drops + uint64_t(queued), uint64_t(sent));
+  // udp_socket_buffers asks for a large buffer (and SO_RXQ_OVFL) and reports what it got.
+  CHECK(udp_socket_buffers(rx, 1 << 20) >= size_t(small));
+  ::close(rx);
+  ::close(tx);
 }

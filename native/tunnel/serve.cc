@@ -498,7 +498,18 @@ void ServeSession::handle_frame(const proto::Frame& f) {
       }
       p.headers = std::move(h);
       Pending& slot = streams_[sid] = std::move(p);
-      if (cfg_.max_request_body && slot.declared > int64_t(cfg_.max_request_body)) reject_too_large(sid);
+      if (cfg_.max_request_body && slot.declared > int64_t(cfg_.max_request_body)) {
+        reject_too_large(sid);
+        break;
+      }
+      // A declared body at or above the streaming threshold: the upstream call
+      // starts now (connect and head while the body is still crossing) and the
+      // body follows frame by frame (cut-through) instead of waiting for REQ_END.
+      if (slot.declared > 0 && uint64_t(slot.declared) >= cfg_.stream_body_threshold) {
+        Pending moved = std::move(slot);
+        streams_.erase(sid);
+        start_request(sid, std::move(moved), true);
+      }
       break;
     }
     case MsgType::ReqBody: {

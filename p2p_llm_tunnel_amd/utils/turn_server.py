@@ -11,16 +11,28 @@ or TLS (transport="tls" with an ssl.SSLContext: turns:...); over a stream,
 STUN messages and ChannelData (padded to 4 bytes) are framed back to back
 (RFC 8656 §12.5) and each connection is its own allocation. Relays to peers
 are UDP in every case.
+
+Shared bottleneck (``link=Link(...)``): everything the server relays towards
+peers leaves through ONE emulated link — a rate, a drop-tail queue, a one-way
+delay and Bernoulli loss — and everything relayed back to clients through a
+second one (same delay; rate and queue only if given). Every tunnel relayed
+through one server therefore competes for the same queue, which the
+per-agent WAN emulator in native/rtc/ice.cc (one emulator per ICE agent)
+cannot model: that is what the congestion response's fairness is measured on
+(bench/bench_fairness.py).
 """
 from __future__ import annotations
 
 import hashlib
+import heapq
 import hmac
 import os
+import random
 import select
 import socket
 import struct
 import threading
+import time
 import zlib
 
 MAGIC = 0x2112A442
@@ -88,9 +100,62 @@ def frames(buf: bytearray):
     return out
 
 
+class Link:
+    """One direction of an emulated bottleneck: serialisation at ``rate_mbps``
+    (0 = unlimited) into a drop-tail queue of ``queue_kb``, then ``delay_ms``
+    of propagation; each packet is lost with probability ``loss``. Packets
+    wait in a heap until their delivery time (the server's loop sends them)."""
+
+    def __init__(self, rate_mbps=0.0, delay_ms=0.0, queue_kb=0, loss=0.0, seed=1):
+        self.rate = rate_mbps * 1e6 / 8  # bytes/s
+        self.delay = delay_ms / 1e3
+        self.queue = queue_kb * 1024 if queue_kb else (int(self.rate * 0.05) if self.rate else 0)  # default 50 ms
+        self.loss = loss
+        self.rng = random.Random(seed)
+        self.free_at = 0.0  # when the link finishes serialising what it holds
+        self.heap = []
+        self.seq = 0
+        self.stats = {"packets": 0, "bytes": 0, "queue_drops": 0, "loss_drops": 0, "max_queue_bytes": 0}
+
+    def reverse(self):
+        return Link(0.0, self.delay * 1e3, 0, 0.0)
+
+    def submit(self, data, send, now=None):
+        now = time.monotonic() if now is None else now
+        n = len(data)
+        if self.loss and self.rng.random() < self.loss:
+            self.stats["loss_drops"] += 1
+            return
+        if self.rate:
+            backlog = max(0.0, self.free_at - now) * self.rate
+            if backlog + n > self.queue:
+                self.stats["queue_drops"] += 1
+                return
+            self.stats["max_queue_bytes"] = max(self.stats["max_queue_bytes"], int(backlog + n))
+            self.free_at = max(now, self.free_at) + n / self.rate
+            at = self.free_at + self.delay
+        else:
+            at = now + self.delay
+        self.stats["packets"] += 1
+        self.stats["bytes"] += n
+        if at <= now:
+            send(data)
+            return
+        self.seq += 1
+        heapq.heappush(self.heap, (at, self.seq, data, send))
+
+    def due(self, now):
+        """Sends what is due; returns the time of the next packet (or None)."""
+        h = self.heap
+        while h and h[0][0] <= now:
+            _, _, data, send = heapq.heappop(h)
+            send(data)
+        return h[0][0] if h else None
+
+
 class TurnServer:
     def __init__(self, user="user", password="pass", realm="p2pt.test", host="127.0.0.1", transport="udp",
-                 ssl_ctx=None):
+                 ssl_ctx=None, link: Link | None = None, back: Link | None = None):
         self.user, self.password, self.realm = user, password, realm
         self.key = hashlib.md5(f"{user}:{realm}:{password}".encode()).digest()
         self.nonce = os.urandom(8).hex().encode()
@@ -112,7 +177,22 @@ class TurnServer:
         self.stats = {"bindings": 0, "allocations": 0, "relayed_to_peer": 0, "relayed_to_client": 0, "channel_binds": 0,
                       "stream_connections": 0}
         self._stop = False
+        self.link = link  # towards peers (the shared bottleneck)
+        self.back = back if back is not None else (link.reverse() if link is not None else None)
         self.thread = threading.Thread(target=self._run, daemon=True)
+
+    def _to_peer(self, relay, data, peer):
+        if self.link is None:
+            relay.sendto(data, peer)
+        else:
+            self.link.submit(data, lambda d, r=relay, p=peer: self._sendto(r, d, p))
+
+    @staticmethod
+    def _sendto(sock, data, addr):
+        try:
+            sock.sendto(data, addr)
+        except OSError:
+            pass
 
     @property
     def url(self):
@@ -215,7 +295,7 @@ class TurnServer:
             ch, ln = struct.unpack(">HH", data[:4])
             a = self.allocs.get(addr)
             if a and ch in a["chans"]:
-                a["relay"].sendto(data[4:4 + ln], a["chans"][ch])
+                self._to_peer(a["relay"], data[4:4 + ln], a["chans"][ch])
                 self.stats["relayed_to_peer"] += 1
             return
         m = parse(data)
@@ -229,7 +309,7 @@ class TurnServer:
             if a and 0x0012 in d and 0x0013 in d:
                 peer = unxor_addr(d[0x0012])
                 if peer[0] in a["perms"]:
-                    a["relay"].sendto(d[0x0013], peer)
+                    self._to_peer(a["relay"], d[0x0013], peer)
                     self.stats["relayed_to_peer"] += 1
             return
         if t & 0x0110:  # not a request
@@ -276,10 +356,14 @@ class TurnServer:
             self._send(build(0x0109, tid, [], self.key), addr)
 
     def _handle_relay(self, r):
-        try:
-            data, peer = r.recvfrom(65536)
-        except OSError:
-            return
+        for _ in range(64):  # drain what is queued on the relay socket
+            try:
+                data, peer = r.recvfrom(65536, socket.MSG_DONTWAIT)
+            except OSError:
+                return
+            self._relay_one(r, data, peer)
+
+    def _relay_one(self, r, data, peer):
         client = self.by_relay.get(r)
         a = self.allocs.get(client)
         if not a or peer[0] not in a["perms"]:
@@ -289,14 +373,23 @@ class TurnServer:
             msg = struct.pack(">HH", ch, len(data)) + data + b"\0" * _pad(len(data))
         else:
             msg = build(0x0017, os.urandom(12), [(0x0012, xor_addr(*peer)), (0x0013, data)], fingerprint=False)
-        self._send(msg, client)
+        if self.back is None:
+            self._send(msg, client)
+        else:
+            self.back.submit(msg, lambda m, c=client: self._send(m, c))
         self.stats["relayed_to_client"] += 1
 
     def _run(self):
         while not self._stop:
             socks = [self.sock] + list(self.by_relay) + list(self.conns) + ([self.lsock] if self.lsock else [])
+            timeout = 0.1
+            if self.link is not None:
+                now = time.monotonic()
+                nxt = [t for t in (self.link.due(now), self.back.due(now)) if t is not None]
+                if nxt:
+                    timeout = max(0.0, min(nxt) - now)
             try:
-                ready, _, _ = select.select(socks, [], [], 0.1)
+                ready, _, _ = select.select(socks, [], [], timeout)
             except (OSError, ValueError):
                 continue
             for s in ready:
@@ -305,10 +398,11 @@ class TurnServer:
                 elif s in self.conns:
                     self._read_conn(s)
                 elif s is self.sock:
-                    try:
-                        data, addr = s.recvfrom(65536)
-                    except OSError:
-                        continue
-                    self._handle_client(data, addr)
+                    for _ in range(64):  # drain what is queued
+                        try:
+                            data, addr = s.recvfrom(65536, socket.MSG_DONTWAIT)
+                        except OSError:
+                            break
+                        self._handle_client(data, addr)
                 else:
                     self._handle_relay(s)

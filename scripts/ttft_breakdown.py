@@ -171,7 +171,7 @@ def bulk_echo(a):
         with Tunnel(f"http://127.0.0.1:{port}", transport=a.transport,
                     env={"TUNNEL_TRACE": trace, "TUNNEL_TRACE_BUFFERED": "1"},
                     serve_extra=extra + pin_s, proxy_extra=extra + pin_p) as t:
-            path = t.serve.wait_for("connection established", 1).split(" via ", 1)[-1] if a.transport == "webrtc" else ""
+            path = t.serve.wait_for("WebRTC connection established", 1).split(" via ", 1)[-1] if a.transport == "webrtc" else ""
             tr = run(t.proxy_port)
         dr = run(port)
         ev = {}
