@@ -80,6 +80,46 @@ def summary(vals):
     return {"median": round(statistics.median(v), 4), "min": round(v[0], 4), "max": round(v[-1], 4)}
 
 
+HOPS = [("proxy", "accept", "proxy", "req_end"), ("proxy", "req_end", "serve", "req_headers"),
+        ("serve", "req_headers", "serve", "req_end"), ("serve", "req_end", "serve", "upstream_sent"),
+        ("serve", "upstream_sent", "serve", "first_body"), ("serve", "first_body", "serve", "sched_in"),
+        ("serve", "sched_in", "serve", "chan_tx"), ("serve", "chan_tx", "proxy", "chan_rx"),
+        ("proxy", "chan_rx", "proxy", "first_body"), ("proxy", "accept", "proxy", "first_body")]
+
+
+def node_hops(traces, windows):
+    """Per (workers, streams): hop p50 over all requests of the tunneled runs,
+    and the hops of the slowest 1 % by time inside the tunnel (proxy accept ->
+    proxy first_body), median over those requests."""
+    ev = {}
+    for i, tf in enumerate(traces):  # stream ids restart with every tunnel
+        with open(tf) as f:
+            for line in f:
+                try:
+                    e = json.loads(line)
+                except ValueError:
+                    continue
+                ev.setdefault((i, e["sid"]), {})[(e["role"], e["ev"])] = e["t_us"]
+    out = []
+    for w, s, t0, t1 in windows:
+        reqs = [e for e in ev.values() if ("proxy", "accept") in e and ("proxy", "first_body") in e
+                and t0 <= e[("proxy", "accept")] <= t1]
+        if not reqs:
+            continue
+        reqs.sort(key=lambda e: e[("proxy", "first_body")] - e[("proxy", "accept")])
+        tail = reqs[int(len(reqs) * 0.99):] or reqs[-1:]
+        row = {"workers": w, "streams": s, "requests": len(reqs), "tail_requests": len(tail)}
+        for a_, b_, c_, d_ in HOPS:
+            k = f"{a_}.{b_} -> {c_}.{d_}"
+            allv = sorted(e[(c_, d_)] - e[(a_, b_)] for e in reqs if (a_, b_) in e and (c_, d_) in e)
+            tv = sorted(e[(c_, d_)] - e[(a_, b_)] for e in tail if (a_, b_) in e and (c_, d_) in e)
+            if allv:
+                row[k] = {"p50_us": allv[len(allv) // 2], "p99_us": allv[int(0.99 * (len(allv) - 1))],
+                          "tail_p50_us": tv[len(tv) // 2] if tv else None}
+        out.append(row)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--streams", default="256,512,1024")
@@ -93,6 +133,9 @@ def main():
     ap.add_argument("--transport", default="webrtc")
     ap.add_argument("--extra", default="", help="extra flags for both tunnel processes")
     ap.add_argument("--profile-dir", default=None)
+    ap.add_argument("--trace", action="store_true",
+                    help="stamp every request's hops (TUNNEL_TRACE, buffered) and report where the slowest 1 %% "
+                         "of first tokens spent their time inside the tunnel (\"hops\" per stream count)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     ensure_native()
@@ -102,23 +145,37 @@ def main():
            "upstreams": a.upstreams, "interval_us": a.interval_us, "tokens": a.tokens, "seconds_per_run": a.seconds,
            "reps": a.reps, "transport": a.transport, "cpus": os.cpu_count(), "runs": [], "rows": []}
     dur = ["--duration-s", str(a.seconds)]
+    windows = []  # (workers, streams, t0_us, t1_us): the tunneled runs, CLOCK_MONOTONIC like the trace
+    traces = []
     try:
         for w in [x for x in a.workers.split(",") if x]:
             extra = ["--workers", w] + [x for x in a.extra.split() if x]
             env = {"RUST_LOG": "warn,tunnel::serve=info,tunnel::proxy=info"}
+            trace = None
+            if a.trace:
+                import tempfile
+                trace = tempfile.NamedTemporaryFile(suffix=".jsonl", prefix="p2pt-node-trace-", delete=False).name
+                env.update({"TUNNEL_TRACE": trace, "TUNNEL_TRACE_BUFFERED": "1"})
             if a.profile_dir:
                 os.makedirs(a.profile_dir, exist_ok=True)
                 env["TUNNEL_PROFILE"] = os.path.join(os.path.abspath(a.profile_dir), f"tunnel.w{w}.%p.prof")
                 env["TUNNEL_PROFILE_HZ"] = "1000"
             up = ",".join(f"http://127.0.0.1:{p}" for p in ports)
+            if trace:
+                traces.append(trace)
             with Tunnel(up, transport=a.transport, serve_extra=extra, proxy_extra=extra, env=env) as t:
                 for s in counts:
                     loadgen([t.proxy_port], s, 1, a.lg_threads, warmup=0)
+                    sid_lo = None
                     for rep in range(a.reps):
                         d = loadgen(ports, s, 1 << 20, a.lg_threads, extra=dur)
                         c0 = (cpu_s(t.serve.popen.pid), cpu_s(t.proxy.popen.pid))
+                        t_tr0 = time.monotonic_ns() // 1000
                         tr = loadgen([t.proxy_port], s, 1 << 20, a.lg_threads, extra=dur)
+                        t_tr1 = time.monotonic_ns() // 1000
                         c1 = (cpu_s(t.serve.popen.pid), cpu_s(t.proxy.popen.pid))
+                        if trace:
+                            windows.append((w, s, t_tr0, t_tr1))
                         r = {"workers": w, "streams": s, "rep": rep, **row("tunneled", tr), **row("direct", d),
                              "events_ratio": tr["events_s"] / d["events_s"] if d["events_s"] else None,
                              "added_p50_ttft_ms": tr["p50_ttft_ms"] - d["p50_ttft_ms"],
@@ -141,9 +198,14 @@ def main():
                     row_[k] = summary([r[k] for r in runs])
                 res["rows"].append(row_)
                 print(json.dumps({"summary": row_}), file=sys.stderr, flush=True)
+        if traces:
+            res["hops"] = node_hops(traces, windows)
     finally:
         for m in mocks:
             m.stop()
+        for tf in traces:
+            if os.path.exists(tf):
+                os.unlink(tf)
     doc = json.dumps(res, indent=1)
     if a.out:
         with open(a.out, "w") as f:

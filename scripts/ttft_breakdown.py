@@ -110,7 +110,11 @@ def main():
             # thread, then the hand-off to the client connection and its write
             ("serve", "first_body", "serve", "sched_in"), ("serve", "sched_in", "serve", "chan_tx"),
             ("serve", "chan_tx", "proxy", "chan_rx"),
-            ("proxy", "chan_rx", "proxy", "first_body")]
+            ("proxy", "chan_rx", "proxy", "first_body"),
+            # the upstream's own turnaround (joinable per stream at serve) and
+            # the whole time inside the tunnel processes
+            ("serve", "upstream_sent", "serve", "first_body"),
+            ("proxy", "accept", "proxy", "first_body")]
     rows = {f"{a_}.{b_} -> {c_}.{d_}": [] for a_, b_, c_, d_ in hops}
     # The mock's trace line carries no stream id, so a mock request can only be
     # paired with the upstream send that preceded it when one stream runs at a
@@ -135,8 +139,22 @@ def main():
     for k, v in rows.items():
         if v:
             v.sort()
-            out[k] = {"n": len(v), "p50_us": statistics.median(v), "p90_us": v[int(0.9 * (len(v) - 1))]}
-    res = {"transport": a.transport, "streams": a.streams, "bulk": a.bulk, "extra": a.extra, "hops": out}
+            out[k] = {"n": len(v), "p50_us": statistics.median(v), "p90_us": v[int(0.9 * (len(v) - 1))],
+                      "p99_us": v[int(0.99 * (len(v) - 1))], "max_us": v[-1]}
+    # The slowest requests inside the tunnel (proxy accept -> proxy first_body):
+    # every hop of each, so a tail is pinned on the hop that made it.
+    tot = ("proxy", "accept"), ("proxy", "first_body")
+    done = [(sid, e) for sid, e in ev.items() if tot[0] in e and tot[1] in e and ("proxy", "get") not in e]
+    done.sort(key=lambda x: x[1][tot[1]] - x[1][tot[0]])
+    worst = []
+    for sid, e in done[-max(3, len(done) // 50):]:
+        w = {"sid": sid, "total_us": e[tot[1]] - e[tot[0]]}
+        for a_, b_, c_, d_ in hops:
+            if (a_, b_) in e and (c_, d_) in e:
+                w[f"{a_}.{b_} -> {c_}.{d_}"] = e[(c_, d_)] - e[(a_, b_)]
+        worst.append(w)
+    res = {"transport": a.transport, "streams": a.streams, "bulk": a.bulk, "extra": a.extra, "hops": out,
+           "worst": worst}
     if not join_mock:
         res["note"] = "mock hops omitted: mock trace lines cannot be joined to streams when streams > 1"
     print(json.dumps(res, indent=1))
