@@ -175,12 +175,13 @@ def bulk_echo(a):
     mock = spawn("mock", (["taskset", "-c", plan["mock"]] if plan else []) + [binary("tunnel-mock"), "--port", str(port)])
     mock.wait_for("Mock LLM server running", 10)
 
-    def run(target):
+    def run(target, trace_file=None):
         cmd = [binary("tunnel-loadgen"), "--target", f"127.0.0.1:{target}", "--streams", str(streams), "--steps",
                str(a.steps), "--warmup", "2", "--post-bytes", str(a.mb << 20)]
         if plan:
             cmd = ["taskset", "-c", plan["loadgen"]] + cmd
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        env = dict(os.environ, LOADGEN_TRACE=trace_file) if trace_file else None
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
         return json.loads(r.stdout.strip().splitlines()[-1])
     try:
         extra = [x for x in a.extra.split() if x]
@@ -190,12 +191,15 @@ def bulk_echo(a):
                     env={"TUNNEL_TRACE": trace, "TUNNEL_TRACE_BUFFERED": "1"},
                     serve_extra=extra + pin_s, proxy_extra=extra + pin_p) as t:
             path = t.serve.wait_for("WebRTC connection established", 1).split(" via ", 1)[-1] if a.transport == "webrtc" else ""
-            tr = run(t.proxy_port)
+            tr = run(t.proxy_port, trace)
         dr = run(port)
-        ev = {}
+        ev, lg = {}, {}
         with open(trace) as f:
             for line in f:
                 e = json.loads(line)
+                if e["role"] == "loadgen":  # the client's step boundaries
+                    lg.setdefault(e["sid"], {})[e["ev"]] = e["t_us"]
+                    continue
                 ev.setdefault(e["sid"], {})[(e["role"], e["ev"])] = e["t_us"]
     finally:
         mock.stop()
@@ -226,14 +230,28 @@ def bulk_echo(a):
              "last echo complete at serve": ("serve", "res_end", max),
              "last response complete at proxy": ("proxy", "res_end", max)}
     steps = []
-    for i in range(0, len(reqs) - streams + 1, streams):
-        g = reqs[i:i + streams]
-        t0 = min(e[("proxy", "accept")] for e in g)
-        row = {"accept_spread_ms": (max(e[("proxy", "accept")] for e in g) - t0) / 1e3}
-        for name, (role, evn, agg) in marks.items():
-            vals = [e[(role, evn)] for e in g if (role, evn) in e]
-            row[name] = (agg(vals) - t0) / 1e3 if vals else None
-        steps.append(row)
+    if lg:  # the client's own steps: marks from its step start
+        bounds = sorted((v["step_start"], v["step_end"]) for v in lg.values() if "step_start" in v and "step_end" in v)
+        for t0, t1 in bounds:
+            g = [e for e in reqs if t0 <= e[("proxy", "accept")] <= t1]
+            if not g:
+                continue
+            acc = [e[("proxy", "accept")] for e in g]
+            row = {"first request parsed at proxy": (min(acc) - t0) / 1e3, "last request parsed at proxy": (max(acc) - t0) / 1e3}
+            for name, (role, evn, agg) in marks.items():
+                vals = [e[(role, evn)] for e in g if (role, evn) in e]
+                row[name] = (agg(vals) - t0) / 1e3 if vals else None
+            row["step end at the client"] = (t1 - t0) / 1e3
+            steps.append(row)
+    else:
+        for i in range(0, len(reqs) - streams + 1, streams):
+            g = reqs[i:i + streams]
+            t0 = min(e[("proxy", "accept")] for e in g)
+            row = {"accept_spread_ms": (max(e[("proxy", "accept")] for e in g) - t0) / 1e3}
+            for name, (role, evn, agg) in marks.items():
+                vals = [e[(role, evn)] for e in g if (role, evn) in e]
+                row[name] = (agg(vals) - t0) / 1e3 if vals else None
+            steps.append(row)
     steps = steps[2:] if len(steps) > 4 else steps
     waterfall = {k: statistics.median([s[k] for s in steps if s.get(k) is not None]) for k in steps[0]} if steps else {}
     res = {"mode": "bulk-echo", "transport": a.transport, "extra": a.extra, "path": path, "pinned": plan,
