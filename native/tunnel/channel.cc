@@ -1,5 +1,6 @@
 #include "tunnel/channel.h"
 
+#include <algorithm>
 #include <cstring>
 
 #include "core/log.h"
@@ -41,28 +42,55 @@ bool TcpMessageChannel::send(const uint8_t* hdr, size_t hlen, const Bytes& paylo
   return true;
 }
 
+// Messages wholly inside one read are delivered as views of the connection's
+// receive buffer (zero-copy); a message split over reads is assembled once,
+// straight into a buffer of its own size (it used to be copied into a staging
+// vector and then again into the message: two copies per byte on the one
+// thread that also runs the session).
 void TcpMessageChannel::on_data(const uint8_t* p, size_t n) {
-  inbuf_.insert(inbuf_.end(), p, p + n);
   auto self = shared_from_this();
-  while (inbuf_.size() - inoff_ >= 4) {
-    uint32_t len = rd32(inbuf_.data() + inoff_);
-    if (len > kMaxTcpMessage) {
-      LOG_ERROR("tunnel::transport", "tcp transport: oversized message (%u bytes)", len);
-      close();
-      return;
+  while (n) {
+    if (need_ == 0) {  // reading the 4-byte length prefix
+      while (n && hdr_len_ < 4) {
+        hdr_[hdr_len_++] = *p++;
+        n--;
+      }
+      if (hdr_len_ < 4) return;
+      hdr_len_ = 0;
+      const uint32_t len = rd32(hdr_);
+      if (len > kMaxTcpMessage) {
+        LOG_ERROR("tunnel::transport", "tcp transport: oversized message (%u bytes)", len);
+        close();
+        return;
+      }
+      if (len == 0) {
+        if (on_message) on_message(Bytes());
+        if (!conn_) return;
+        continue;
+      }
+      if (n >= len) {  // whole message in this read
+        Bytes msg = conn_ ? conn_->rx_view(p, len) : Bytes::copy(p, len);
+        p += len;
+        n -= len;
+        if (on_message) on_message(std::move(msg));
+        if (!conn_) return;
+        continue;
+      }
+      need_ = len;
+      cur_.clear();
+      cur_.reserve(len);
     }
-    if (inbuf_.size() - inoff_ < 4 + size_t(len)) break;
-    Bytes msg = Bytes::copy(inbuf_.data() + inoff_ + 4, len);
-    inoff_ += 4 + len;
-    if (on_message) on_message(std::move(msg));
-    if (!conn_) return;
-  }
-  if (inoff_ == inbuf_.size()) {
-    inbuf_.clear();
-    inoff_ = 0;
-  } else if (inoff_ > 1 << 20) {
-    inbuf_.erase(inbuf_.begin(), inbuf_.begin() + long(inoff_));
-    inoff_ = 0;
+    const size_t take = std::min(n, need_ - cur_.size());
+    cur_.insert(cur_.end(), p, p + take);
+    p += take;
+    n -= take;
+    if (cur_.size() == need_) {
+      need_ = 0;
+      Bytes msg = Bytes::take(std::move(cur_));
+      cur_ = std::vector<uint8_t>();
+      if (on_message) on_message(std::move(msg));
+      if (!conn_) return;
+    }
   }
 }
 

@@ -90,8 +90,10 @@ class TcpMessageChannel : public MessageChannel, public std::enable_shared_from_
  private:
   void on_data(const uint8_t* p, size_t n);
   std::shared_ptr<TcpConn> conn_;
-  std::vector<uint8_t> inbuf_;
-  size_t inoff_ = 0;
+  uint8_t hdr_[4] = {};
+  size_t hdr_len_ = 0;       // bytes of the length prefix read so far
+  size_t need_ = 0;          // length of the message being assembled (0: none)
+  std::vector<uint8_t> cur_;  // its bytes so far
 };
 
 }  // namespace p2pt
