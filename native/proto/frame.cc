@@ -50,6 +50,35 @@ Bytes Frame::encode() const {
   return Bytes::take(std::move(v));
 }
 
+Bytes Frame::flat_payload() const {
+  if (more.empty()) return payload;
+  std::vector<uint8_t> v;
+  v.reserve(payload_size());
+  v.insert(v.end(), payload.data(), payload.data() + payload.size());
+  for (auto& b : more) v.insert(v.end(), b.data(), b.data() + b.size());
+  return Bytes::take(std::move(v));
+}
+
+bool decode_chain(const Bytes& raw, std::vector<Bytes>& more, Frame& out, std::string* err) {
+  if (more.empty() || raw.size() < kHeaderLen) {
+    Bytes flat = raw;
+    if (!more.empty()) {  // a first fragment shorter than the header: one piece
+      std::vector<uint8_t> v(raw.data(), raw.data() + raw.size());
+      for (auto& b : more) v.insert(v.end(), b.data(), b.data() + b.size());
+      flat = Bytes::take(std::move(v));
+    }
+    out.more.clear();
+    return decode(flat, out, err);
+  }
+  if (!decode(raw, out, err)) return false;
+  out.more = std::move(more);
+  if (out.type != MsgType::ReqBody && out.type != MsgType::ResBody) {
+    out.payload = out.flat_payload();
+    out.more.clear();
+  }
+  return true;
+}
+
 bool decode(const Bytes& raw, Frame& out, std::string* err) {
   if (raw.size() < kHeaderLen) {
     if (err) *err = "message too short: " + std::to_string(raw.size()) + " bytes";

@@ -62,17 +62,32 @@ struct Frame {
   MsgType type;
   uint32_t stream_id;
   Bytes payload;
+  // A received body frame that came as several transport fragments keeps the
+  // rest of its payload here (zero-copy views, in order); empty otherwise.
+  // Frames built for sending never use it.
+  std::vector<Bytes> more = {};
 
   // [type][stream_id] header.
   void header(uint8_t out[kHeaderLen]) const;
   // Header + payload in one buffer (tests / small control frames).
   Bytes encode() const;
-  size_t wire_size() const { return kHeaderLen + payload.size(); }
+  size_t payload_size() const {
+    size_t n = payload.size();
+    for (auto& b : more) n += b.size();
+    return n;
+  }
+  size_t wire_size() const { return kHeaderLen + payload_size(); }
+  // payload + more as one contiguous view (a copy only when chained).
+  Bytes flat_payload() const;
 };
 
 // Decode a received message. Errors mirror the reference text:
 // "message too short: N bytes", "unknown message type: T".
 bool decode(const Bytes& raw, Frame& out, std::string* err);
+// A message that arrived as fragments (`raw` the first, `more` the rest):
+// body frames keep the fragments as their payload chain, every other type is
+// made contiguous (headers are JSON, parsed in one piece).
+bool decode_chain(const Bytes& raw, std::vector<Bytes>& more, Frame& out, std::string* err);
 
 // ---- handshake
 struct Hello {

@@ -81,6 +81,7 @@ void DataChannel::close() {
   if (pc && pc->sctp_ && stream_ >= 0) pc->sctp_->request_stream_reset(uint16_t(stream_));
   closed_ = true;
   on_message = nullptr;
+  on_message_chain = nullptr;
   on_open = nullptr;
   on_closed = nullptr;
   on_buffered_low = nullptr;
@@ -476,7 +477,10 @@ void PeerConnection::start_sctp() {
     s->open_pending_channels();
   };
   sctp_->on_message = [w](uint16_t st, uint32_t ppid, Bytes m) {
-    if (auto s = w.lock()) s->on_sctp_message(st, ppid, std::move(m));
+    if (auto s = w.lock()) s->on_sctp_message(st, ppid, std::move(m), nullptr);
+  };
+  sctp_->on_message_chain = [w](uint16_t st, uint32_t ppid, Bytes m, std::vector<Bytes>& more) {
+    if (auto s = w.lock()) s->on_sctp_message(st, ppid, std::move(m), &more);
   };
   sctp_->on_stream_reset = [w](uint16_t st) {
     auto s = w.lock();
@@ -700,7 +704,13 @@ void PeerConnection::open_pending_channels() {
   pending_.clear();
 }
 
-void PeerConnection::on_sctp_message(uint16_t st, uint32_t ppid, Bytes msg) {
+void PeerConnection::on_sctp_message(uint16_t st, uint32_t ppid, Bytes msg, std::vector<Bytes>* more) {
+  if (more && !more->empty() && ppid == kPpidDcep) {  // DCEP in fragments: one piece
+    std::vector<uint8_t> v(msg.data(), msg.data() + msg.size());
+    for (auto& b : *more) v.insert(v.end(), b.data(), b.data() + b.size());
+    msg = Bytes::take(std::move(v));
+    more = nullptr;
+  }
   if (ppid == kPpidDcep) {
     if (msg.empty()) return;
     if (msg[0] == kDcepOpen && msg.size() >= 12) {
@@ -735,8 +745,11 @@ void PeerConnection::on_sctp_message(uint16_t st, uint32_t ppid, Bytes msg) {
     // treats the first data from the peer as an implicit ACK (RFC 8832 §6).
     dc->set_open();
   }
-  if (ppid == kPpidBinaryEmpty || ppid == kPpidStringEmpty) msg = Bytes();
-  if (dc->on_message) dc->on_message(std::move(msg));
+  if (ppid == kPpidBinaryEmpty || ppid == kPpidStringEmpty) {
+    msg = Bytes();
+    more = nullptr;
+  }
+  dc->deliver(std::move(msg), more);
 }
 
 std::string PeerConnection::describe_path() const {

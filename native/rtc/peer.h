@@ -125,7 +125,7 @@ class PeerConnection : public std::enable_shared_from_this<PeerConnection> {
   void on_ice_state(IceState s);
   void start_dtls();
   void start_sctp();
-  void on_sctp_message(uint16_t stream, uint32_t ppid, Bytes msg);
+  void on_sctp_message(uint16_t stream, uint32_t ppid, Bytes msg, std::vector<Bytes>* more);
   void open_pending_channels();
   void set_state(PcState s);
   void fail(const std::string& why);

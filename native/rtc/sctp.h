@@ -140,6 +140,10 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
 
   std::function<void()> on_established;
   std::function<void(uint16_t stream, uint32_t ppid, Bytes msg)> on_message;
+  // Optional: a fragmented message as the views of its fragments (the first
+  // in `msg`, the rest in `more`, all zero-copy slices of the received
+  // packets) instead of one reassembled copy. Unset: on_message gets a copy.
+  std::function<void(uint16_t stream, uint32_t ppid, Bytes msg, std::vector<Bytes>& more)> on_message_chain;
   std::function<void(uint16_t stream)> on_stream_reset;  // peer reset its outgoing stream
   std::function<void(const std::string&)> on_closed;
   std::function<void()> on_sent;  // unsent_bytes_ decreased (back-pressure relief)
@@ -174,7 +178,9 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   void build_sack(std::vector<uint8_t>& body);
   void deliver_ready();
   void deliver_chunk(uint8_t fl, uint16_t st, uint16_t ssn, uint32_t pp, const Bytes& d);
-  void deliver_message(uint16_t st, uint16_t ssn, bool unordered, uint32_t pp, Bytes msg);
+  void deliver_message(uint16_t st, uint16_t ssn, bool unordered, uint32_t pp, Bytes msg,
+                       std::vector<Bytes> more = {});
+  void hand_up(uint16_t st, uint32_t pp, Bytes msg, std::vector<Bytes>& more);
   void release_ready(uint16_t st);
   void drain_in_order();
   void reset_inbound_stream(uint16_t st);
@@ -320,8 +326,15 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
     RawBufPtr buf;  // pooled (reasm_pool_): a whole tunnel frame fits
     size_t len = 0;
     std::vector<uint8_t> big;  // only for messages beyond the pooled size
+    std::vector<Bytes> frags;  // chained delivery: the fragments' views (no copy)
+    size_t frag_bytes = 0;
     bool active = false;
-    size_t size() const { return big.empty() ? len : big.size(); }
+    size_t size() const { return !frags.empty() ? frag_bytes : big.empty() ? len : big.size(); }
+  };
+  struct Held {  // a complete message waiting for its turn in its stream
+    uint32_t ppid = 0;
+    Bytes msg;
+    std::vector<Bytes> more;
   };
   BufPool reasm_pool_{kReasmBuf, 256};
   static constexpr size_t kReasmBuf = 65536 + 1024;
@@ -332,7 +345,7 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   // Complete ordered messages that arrived in TSN order but ahead of their
   // stream's sequence (a peer may send a later small message of a stream
   // before an earlier large one: RFC 9260 orders by SSN, not TSN).
-  std::map<uint32_t, std::pair<uint32_t, Bytes>> held_;  // (stream, ssn) -> (ppid, message)
+  std::map<uint32_t, Held> held_;  // (stream, ssn) -> message
   size_t held_bytes_ = 0;
 
   std::vector<std::vector<uint8_t>> ctrl_;  // control chunks to bundle at next flush

@@ -943,6 +943,62 @@ TEST(slow_association_thread_loses_nothing_uncounted) {
   unsetenv("TUNNEL_RX_ESCAPE");
 }
 
+// Zero-copy reassembly: a consumer that takes chains (the tunnel sessions)
+// gets a fragmented message as views of its fragments, in order, byte for
+// byte what was sent; a message that fits one chunk still arrives whole.
+TEST(fragmented_messages_arrive_as_zero_copy_chains) {
+  if (!AesGcm::supported()) return;
+  Reactor r;
+  PcConfig cfg;
+  cfg.ice.include_loopback = true;
+  cfg.allow_jumbo = false;
+  auto off = PeerConnection::create(r, cfg, true);
+  auto ans = PeerConnection::create(r, cfg, false);
+  off->on_ice_candidate = [&](const std::string& c) { ans->add_ice_candidate(c, nullptr); };
+  ans->on_ice_candidate = [&](const std::string& c) { off->add_ice_candidate(c, nullptr); };
+  auto dc = off->create_data_channel("tunnel");
+  std::shared_ptr<DataChannel> rdc;
+  size_t got = 0, chains = 0, pieces = 0, whole = 0;
+  bool ok = true;
+  const std::string big = payload(65000, 21), small = payload(300, 22);
+  ans->on_data_channel = [&](std::shared_ptr<DataChannel> d) {
+    rdc = d;
+    d->on_message = [&](Bytes m) {  // single-chunk messages
+      whole++;
+      got++;
+      ok &= m.size() == small.size() + 5 && memcmp(m.data() + 5, small.data(), small.size()) == 0;
+    };
+    d->on_message_chain = [&](Bytes m, std::vector<Bytes>& more) {
+      chains++;
+      got++;
+      pieces += 1 + more.size();
+      std::string all(reinterpret_cast<const char*>(m.data()), m.size());
+      for (auto& b : more) {
+        ok &= b.owner() != nullptr;  // a view kept alive by its packet buffer
+        all.append(reinterpret_cast<const char*>(b.data()), b.size());
+      }
+      ok &= all.size() == big.size() + 5 && all.compare(5, std::string::npos, big) == 0;
+    };
+  };
+  off->start_gathering();
+  ans->start_gathering();
+  CHECK(r.run_until([&] { return off->gathering_complete(); }, 3000));
+  std::string err;
+  CHECK(ans->set_remote_description(off->local_description(), &err));
+  CHECK(off->set_remote_description(ans->local_description(), &err));
+  CHECK(r.run_until([&] { return dc->is_open() && rdc && rdc->is_open(); }, 5000));
+  Bytes b1 = Bytes::copy(big), b2 = Bytes::copy(small);
+  uint8_t hdr[5] = {21, 0, 0, 0, 1};
+  for (int i = 0; i < 40; i++) dc->send(hdr, 5, (i % 2) ? b2 : b1);
+  CHECK(r.run_until([&] { return got == 40; }, 10000));
+  CHECK(ok);
+  CHECK_EQ(chains, size_t(20));
+  CHECK_EQ(whole, size_t(20));
+  CHECK(pieces >= 20 * 50);  // 65 KB in ~1.1 KB DATA chunks at 1200-byte MTU
+  off->close();
+  ans->close();
+}
+
 TEST(sctp_probe_rearms_t3_at_small_cwnd) {
   // 50 ms RTT, 2 % loss, a token trickle with 240 KB bursts: after a few loss
   // events cwnd is ~3 packets, so a lost burst tail is found only by a

@@ -12,6 +12,7 @@
 #include <functional>
 #include <memory>
 #include <string>
+#include <vector>
 
 #include "core/buf.h"
 #include "core/net.h"
@@ -68,6 +69,23 @@ class MessageChannel {
 
   // Message arrived (whole message, zero-copy view where possible).
   std::function<void(Bytes)> on_message;
+  // Optional: a message that arrived in fragments, as their views (first in
+  // the Bytes, the rest in the vector, which the callee may take). Unset:
+  // such a message reaches on_message as one copy.
+  std::function<void(Bytes, std::vector<Bytes>&)> on_message_chain;
+  // Hands a received message to the callbacks above.
+  void deliver(Bytes msg, std::vector<Bytes>* more) {
+    if (more && !more->empty()) {
+      if (on_message_chain) {
+        on_message_chain(std::move(msg), *more);
+        return;
+      }
+      std::vector<uint8_t> v(msg.data(), msg.data() + msg.size());
+      for (auto& b : *more) v.insert(v.end(), b.data(), b.data() + b.size());
+      msg = Bytes::take(std::move(v));
+    }
+    if (on_message) on_message(std::move(msg));
+  }
   // Channel became open (may already be open when handed out).
   std::function<void()> on_open;
   // Channel or the underlying connection failed / closed.

@@ -108,7 +108,9 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     write_response_head(rh);
   }
 
-  void on_res_body(const Bytes& payload) {
+  // `more`: the rest of a body frame that arrived in transport fragments
+  // (each piece written zero-copy, one chunk for the whole frame).
+  void on_res_body(const Bytes& payload, const std::vector<Bytes>* more = nullptr) {
     if (!conn_ || conn_->closed() || aborted_) return;
     if (!head_written_) {
       LOG_WARN(kT, "received body chunk before headers for stream %u", sid_);
@@ -118,8 +120,26 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
       first_body_ = true;
       trace::event("proxy", sid_, "first_body");
     }
-    if (payload.empty() || no_body_) return;
-    body_sent_ += payload.size();
+    size_t total = payload.size();
+    if (more)
+      for (auto& b : *more) total += b.size();
+    if (!total || no_body_) return;
+    body_sent_ += total;
+    if (more && !more->empty()) {
+      if (chunked_) {
+        char hdr[24];
+        int n = snprintf(hdr, sizeof hdr, "%zx\r\n", total);
+        conn_->write(slab_copy(hdr, size_t(n)));
+      }
+      conn_->write(payload);
+      for (auto& b : *more) conn_->write(b);
+      if (chunked_) conn_->write(slab_copy("\r\n", 2));
+      if (stream_registered_ && sess_flow()) {
+        owed_ += total;
+        maybe_grant();
+      }
+      return;
+    }
     if (chunked_) {
       char hdr[24];
       int n = snprintf(hdr, sizeof hdr, "%zx\r\n", payload.size());
@@ -677,7 +697,7 @@ void ProxyWorker::handle(ProxySession::Cmd& c) {
       if (conn) conn->on_res_headers(*c.rh);
       break;
     case Cmd::Body:
-      if (conn) conn->on_res_body(c.data);
+      if (conn) conn->on_res_body(c.data, &c.more);
       break;
     case Cmd::End:
       streams_.erase(it);
@@ -711,6 +731,9 @@ std::shared_ptr<ProxySession> ProxySession::start(Reactor& r, std::shared_ptr<Me
   std::weak_ptr<ProxySession> w = s;
   ch->on_message = [w](Bytes b) {
     if (auto x = w.lock()) x->on_message(std::move(b));
+  };
+  ch->on_message_chain = [w](Bytes b, std::vector<Bytes>& more) {
+    if (auto x = w.lock()) x->on_message(std::move(b), &more);
   };
   ch->on_closed = [w](const std::string& why) {
     if (auto x = w.lock()) x->stop("data channel closed: " + why);
@@ -801,6 +824,7 @@ ProxySession::~ProxySession() {
   wd_timer_ = 0;
   if (ch_) {
     ch_->on_message = nullptr;
+    ch_->on_message_chain = nullptr;
     ch_->on_closed = nullptr;
     ch_->on_open = nullptr;
     ch_->on_buffered_low = nullptr;
@@ -857,24 +881,26 @@ void ProxySession::on_open() {
   });
 }
 
-void ProxySession::on_message(Bytes raw) {
+void ProxySession::on_message(Bytes raw, std::vector<Bytes>* more) {
   if (stopped_) return;
   proto::Frame f;
   std::string err;
+  std::vector<Bytes> none;
+  const bool ok = proto::decode_chain(raw, more ? *more : none, f, &err);
   if (!ready_) {
-    if (!proto::decode(raw, f, &err)) {
+    if (!ok) {
       stop(err);
       return;
     }
-    metrics::frame_recv(uint8_t(f.type), raw.size());
+    metrics::frame_recv(uint8_t(f.type), f.wire_size());
     on_agree(f);
     return;
   }
-  if (!proto::decode(raw, f, &err)) {
+  if (!ok) {
     LOG_WARN(kT, "failed to decode tunnel message: %s", err.c_str());
     return;
   }
-  metrics::frame_recv(uint8_t(f.type), raw.size());
+  metrics::frame_recv(uint8_t(f.type), f.wire_size());
   route(f);
 }
 
@@ -1082,6 +1108,7 @@ void ProxySession::route(const proto::Frame& f) {
         }
         Cmd c{Cmd::Body, f.stream_id};
         c.data = f.payload;
+        c.more = f.more;
         command(it->second.thread, std::move(c));
       }
       break;

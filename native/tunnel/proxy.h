@@ -95,6 +95,7 @@ class ProxySession : public std::enable_shared_from_this<ProxySession> {
     uint32_t sid = 0;
     int fd = -1;                                  // Adopt
     Bytes data;                                   // Body / Error message; Adopt: bytes already read
+    std::vector<Bytes> more;                      // Body: the rest of a frame that arrived in fragments
     std::shared_ptr<proto::ResponseHeaders> rh;   // Headers
     uint32_t bytes = 0;                           // Credit: REQ_BODY bytes granted by serve
   };
@@ -124,7 +125,7 @@ class ProxySession : public std::enable_shared_from_this<ProxySession> {
   void init_links(WorkerPool* pool);
   void release_links(const std::string& fail_why);
   void on_open();
-  void on_message(Bytes raw);
+  void on_message(Bytes raw, std::vector<Bytes>* more = nullptr);
   void on_agree(const proto::Frame& f);
   void route(const proto::Frame& f);
   void send_ping();

@@ -68,6 +68,10 @@ class ServeWorker : public std::enable_shared_from_this<ServeWorker> {
         }
         it->second.owed += c.data.size();
         it->second.call->write_body(std::move(c.data));
+        for (auto& b : c.more) {
+          it->second.owed += b.size();
+          it->second.call->write_body(std::move(b));
+        }
         maybe_grant(c.sid, it->second);
         break;
       }
@@ -228,6 +232,9 @@ std::shared_ptr<ServeSession> ServeSession::start(Reactor& r, std::shared_ptr<Me
   ch->on_message = [w](Bytes b) {
     if (auto x = w.lock()) x->on_message(std::move(b));
   };
+  ch->on_message_chain = [w](Bytes b, std::vector<Bytes>& more) {
+    if (auto x = w.lock()) x->on_message(std::move(b), &more);
+  };
   ch->on_closed = [w](const std::string& why) {
     if (auto x = w.lock()) {
       LOG_INFO(kT, "data channel closed, serve ending");
@@ -323,6 +330,7 @@ ServeSession::~ServeSession() {
   release_links();
   if (ch_) {
     ch_->on_message = nullptr;
+    ch_->on_message_chain = nullptr;
     ch_->on_closed = nullptr;
     ch_->on_open = nullptr;
     ch_->on_buffered_low = nullptr;
@@ -362,24 +370,26 @@ void ServeSession::on_open() {
   });
 }
 
-void ServeSession::on_message(Bytes raw) {
+void ServeSession::on_message(Bytes raw, std::vector<Bytes>* more) {
   if (stopped_) return;
   proto::Frame f;
   std::string err;
+  std::vector<Bytes> none;
+  const bool ok = proto::decode_chain(raw, more ? *more : none, f, &err);
   if (!handshaken_) {
-    if (!proto::decode(raw, f, &err)) {
+    if (!ok) {
       stop(err);
       return;
     }
-    metrics::frame_recv(uint8_t(f.type), raw.size());
+    metrics::frame_recv(uint8_t(f.type), f.wire_size());
     on_hello(f);
     return;
   }
-  if (!proto::decode(raw, f, &err)) {
+  if (!ok) {
     LOG_WARN(kT, "failed to decode tunnel message: %s", err.c_str());
     return;
   }
-  metrics::frame_recv(uint8_t(f.type), raw.size());
+  metrics::frame_recv(uint8_t(f.type), f.wire_size());
   handle_frame(f);
 }
 
@@ -513,14 +523,16 @@ void ServeSession::handle_frame(const proto::Frame& f) {
       break;
     }
     case MsgType::ReqBody: {
-      if (f.payload.empty()) break;
+      const size_t n = f.payload_size();
+      if (!n) break;
       auto it = streams_.find(f.stream_id);
       if (it != streams_.end()) {
         Pending& p = it->second;
-        if (flow_) grant(f.stream_id, p.owed, f.payload.size());  // buffered here: bounded by the threshold
+        if (flow_) grant(f.stream_id, p.owed, n);  // buffered here: bounded by the threshold
         if (p.rejected) break;
-        p.body_len += f.payload.size();
-        p.body.push_back(f.payload);  // zero-copy: keeps the message alive
+        p.body_len += n;
+        p.body.push_back(f.payload);  // zero-copy: keeps the message (or its fragments) alive
+        for (auto& b : f.more) p.body.push_back(b);
         if (cfg_.max_request_body && p.body_len > cfg_.max_request_body) {
           reject_too_large(f.stream_id);
           break;
@@ -535,7 +547,7 @@ void ServeSession::handle_frame(const proto::Frame& f) {
       }
       auto fl = inflight_.find(f.stream_id);
       if (fl != inflight_.end() && fl->second.uploading) {
-        fl->second.uploaded += f.payload.size();
+        fl->second.uploaded += n;
         if (cfg_.max_request_body && fl->second.uploaded > cfg_.max_request_body) {
           LOG_WARN(kT, "stream %u: request body over %llu bytes, aborting", f.stream_id,
                    static_cast<unsigned long long>(cfg_.max_request_body));
@@ -551,6 +563,7 @@ void ServeSession::handle_frame(const proto::Frame& f) {
         }
         Cmd c{Cmd::Body, f.stream_id};
         c.data = f.payload;
+        c.more = f.more;
         command(fl->second.thread, std::move(c));
       }
       break;

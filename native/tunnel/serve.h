@@ -90,6 +90,7 @@ class ServeSession : public std::enable_shared_from_this<ServeSession> {
     bool retryable = false;   // Start: hand the request back if the upstream is unreachable
     bool grant = false;       // Start: report consumed streamed-body bytes (Ev::Credit)
     Bytes data;               // Body
+    std::vector<Bytes> more;  // Body: the rest of a frame that arrived in fragments
   };
   // An upstream call that never connected, handed back for another upstream.
   struct Unreachable {
@@ -157,7 +158,7 @@ class ServeSession : public std::enable_shared_from_this<ServeSession> {
   void init_links(WorkerPool* pool);
   void release_links();
   void on_open();
-  void on_message(Bytes raw);
+  void on_message(Bytes raw, std::vector<Bytes>* more = nullptr);
   void on_hello(const proto::Frame& f);
   void handle_frame(const proto::Frame& f);
   void start_request(uint32_t sid, Pending p, bool streaming);
