@@ -479,9 +479,16 @@ void PeerConnection::start_sctp() {
   sctp_->on_message = [w](uint16_t st, uint32_t ppid, Bytes m) {
     if (auto s = w.lock()) s->on_sctp_message(st, ppid, std::move(m), nullptr);
   };
-  sctp_->on_message_chain = [w](uint16_t st, uint32_t ppid, Bytes m, std::vector<Bytes>& more) {
-    if (auto s = w.lock()) s->on_sctp_message(st, ppid, std::move(m), &more);
-  };
+  // Fragmented messages as chains of packet views (TUNNEL_SCTP_CHAIN=0: one
+  // reassembled copy each, as before; A/B).
+  static const bool chains = [] {
+    const char* e = getenv("TUNNEL_SCTP_CHAIN");
+    return !(e && *e == '0');
+  }();
+  if (chains)
+    sctp_->on_message_chain = [w](uint16_t st, uint32_t ppid, Bytes m, std::vector<Bytes>& more) {
+      if (auto s = w.lock()) s->on_sctp_message(st, ppid, std::move(m), &more);
+    };
   sctp_->on_stream_reset = [w](uint16_t st) {
     auto s = w.lock();
     if (!s) return;
