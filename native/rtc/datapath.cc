@@ -448,7 +448,7 @@ void RxReader::run() {
         }
       }
       for (auto& sl : slots) sl.reset();  // the burst holds what it uses
-      if (n < kBatch) break;
+      if (n < kBatch || burst->opened.bytes >= burst_cap_) break;
     }
     if (burst->opened.recs.empty() && burst->raw.empty()) continue;
     bursts.fetch_add(1, std::memory_order_relaxed);

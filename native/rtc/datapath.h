@@ -33,7 +33,10 @@
 
 #include <sys/uio.h>
 
+#include <algorithm>
 #include <atomic>
+#include <cstdint>
+#include <cstdlib>
 #include <condition_variable>
 #include <functional>
 #include <memory>
@@ -232,6 +235,13 @@ class RxReader {
   std::shared_ptr<const RecordKeys> keys_;
   Deliver deliver_;
   uint64_t id_ = 0;
+  // TUNNEL_RX_BURST_KB: hand a burst over once it holds this much (default:
+  // whatever 8 recvmmsg rounds found). A smaller burst is processed — and
+  // acknowledged — sooner, at more hand-offs per byte.
+  size_t burst_cap_ = [] {
+    const char* e = getenv("TUNNEL_RX_BURST_KB");
+    return e && *e ? size_t(std::max(16, atoi(e))) * 1024 : SIZE_MAX;
+  }();
   bool escape_ = [] {  // TUNNEL_RX_ESCAPE=0: pause however full the socket buffer is (A/B, tests)
     const char* e = getenv("TUNNEL_RX_ESCAPE");
     return !(e && *e == '0');
