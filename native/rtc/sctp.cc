@@ -47,6 +47,13 @@ void put32(std::vector<uint8_t>& v, uint32_t x) {
   v.push_back(uint8_t(x >> 8));
   v.push_back(uint8_t(x));
 }
+// n bytes appended at the end of v (capacity reserved by the caller: no
+// reallocation on the per-chunk path), for direct stores.
+inline uint8_t* grow(std::vector<uint8_t>& v, size_t n) {
+  const size_t o = v.size();
+  v.resize(o + n);
+  return v.data() + o;
+}
 void pad4(std::vector<uint8_t>& v) {
   while (v.size() % 4) v.push_back(0);
 }
@@ -200,10 +207,11 @@ void SctpAssociation::emit_packet(std::vector<uint8_t>& pkt) {
 void SctpAssociation::begin_gather() {
   if (pkt_.capacity() < cfg_.mtu + 64) pkt_.reserve(cfg_.mtu + 64);  // no pointers into pkt_ exist yet
   pkt_.clear();
-  put16(pkt_, cfg_.local_port);
-  put16(pkt_, cfg_.remote_port);
-  put32(pkt_, peer_vtag_);
-  put32(pkt_, 0);
+  uint8_t* h = grow(pkt_, kCommonHdr);
+  wr16(h, cfg_.local_port);
+  wr16(h + 2, cfg_.remote_port);
+  wr32(h + 4, peer_vtag_);
+  wr32(h + 8, 0);
   iov_.clear();
   iov_own_.clear();
   run_start_ = 0;
@@ -1598,13 +1606,14 @@ void SctpAssociation::flush() {
     size_t need = kDataHdr + padded;
     if (pkt_len_ + need > mtu) flush_pkt();
     std::vector<uint8_t>& pkt = pkt_;
-    pkt.push_back(kData);
-    pkt.push_back(ch->flags);
-    put16(pkt, uint16_t(kDataHdr + ch->len));
-    put32(pkt, ch->tsn);
-    put16(pkt, ch->stream);
-    put16(pkt, ch->ssn);
-    put32(pkt, ch->ppid);
+    uint8_t* h = grow(pkt, kDataHdr);  // one store sequence per header (12 push_backs were a hot spot)
+    h[0] = kData;
+    h[1] = ch->flags;
+    wr16(h + 2, uint16_t(kDataHdr + ch->len));
+    wr32(h + 4, ch->tsn);
+    wr16(h + 8, ch->stream);
+    wr16(h + 10, ch->ssn);
+    wr32(h + 12, ch->ppid);
     // Inline header bytes and small pieces are copied into the packet buffer;
     // large pieces are referenced in place (the chunk keeps its slices alive
     // until acknowledged).
