@@ -282,7 +282,9 @@ class Stream : public std::enable_shared_from_this<Stream> {
 FILE* step_trace() {
   static FILE* f = [] () -> FILE* {
     const char* p = getenv("LOADGEN_TRACE");
-    return p && *p ? fopen(p, "a") : nullptr;
+    FILE* o = p && *p ? fopen(p, "a") : nullptr;
+    if (o) setvbuf(o, nullptr, _IOLBF, 1 << 16);  // whole lines per write: the tunnel appends to the same file
+    return o;
   }();
   return f;
 }

@@ -196,7 +196,10 @@ def bulk_echo(a):
         ev, lg = {}, {}
         with open(trace) as f:
             for line in f:
-                e = json.loads(line)
+                try:
+                    e = json.loads(line)
+                except ValueError:  # a torn line (should not happen: whole-line appends)
+                    continue
                 if e["role"] == "loadgen":  # the client's step boundaries
                     lg.setdefault(e["sid"], {})[e["ev"]] = e["t_us"]
                     continue
