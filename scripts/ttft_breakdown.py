@@ -126,6 +126,8 @@ def main():
     for sid, e in sorted(ev.items()):
         if ("serve", "upstream_sent") not in e or ("proxy", "first_body") not in e or ("proxy", "get") in e:
             continue
+        if sid <= a.streams:  # the load generator's warm-up step (cold pools, first connections)
+            continue
         if join_mock:
             up = e[("serve", "upstream_sent")]
             m = next((x for x in mock_t if x >= up), None)  # the mock request that followed this send
@@ -144,7 +146,8 @@ def main():
     # The slowest requests inside the tunnel (proxy accept -> proxy first_body):
     # every hop of each, so a tail is pinned on the hop that made it.
     tot = ("proxy", "accept"), ("proxy", "first_body")
-    done = [(sid, e) for sid, e in ev.items() if tot[0] in e and tot[1] in e and ("proxy", "get") not in e]
+    done = [(sid, e) for sid, e in ev.items() if tot[0] in e and tot[1] in e and ("proxy", "get") not in e
+            and sid > a.streams]
     done.sort(key=lambda x: x[1][tot[1]] - x[1][tot[0]])
     worst = []
     for sid, e in done[-max(3, len(done) // 50):]:
