@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--extra", default="", help="extra flags for both tunnel processes, e.g. --no-jumbo-loopback")
     ap.add_argument("--serve-extra", default="", help="extra flags for serve only, e.g. --stream-body-threshold 65536")
     ap.add_argument("--pin", action="store_true", help="pin loadgen / mock / serve / proxy to disjoint CPUs")
+    ap.add_argument("--timeline", action="store_true",
+                    help="per-thread CPU utilisation in 2 ms intervals (TUNNEL_THREAD_TIMELINE), summarised per thread")
     a = ap.parse_args()
     extra = [x for x in a.extra.split() if x]
     serve_only = [x for x in a.serve_extra.split() if x]
@@ -52,6 +54,11 @@ def main():
         os.makedirs(a.profile_dir, exist_ok=True)
         env = {"TUNNEL_PROFILE": os.path.join(os.path.abspath(a.profile_dir), "tunnel.%p.prof"),
                "TUNNEL_PROFILE_HZ": os.environ.get("TUNNEL_PROFILE_HZ", "2000")}
+    tl_dir = None
+    if a.timeline:
+        import tempfile
+        tl_dir = tempfile.mkdtemp(prefix="p2pt-timeline-")
+        env = dict(env or {}, TUNNEL_THREAD_TIMELINE=os.path.join(tl_dir, "tl.%p.json"))
     mock, port = start_mock("native", 100, 5, plan.get("mock"))
     ms, mp = free_port(), free_port()
     out = {}
@@ -95,6 +102,24 @@ def main():
                 ("rwnd_drops", "tunnel_sctp_rwnd_drops"), ("dtls_rx_dropped", "tunnel_dtls_rx_dropped"))}
     finally:
         mock.stop()
+    if tl_dir and out:
+        # Share of each thread's active 2 ms intervals (>= 10 % CPU) spent at
+        # >= 90 % / >= 75 % CPU, over the process's life (warm-up, tunneled and
+        # direct runs; the direct run adds idle intervals only).
+        names = {0: "assoc", 90: "tx_lane", 91: "rx_lane", 92: "udp_reader"}
+        out["timeline"] = {}
+        for role, pid in out.get("pids", {}).items():
+            f = os.path.join(tl_dir, f"tl.{pid}.json")
+            if not os.path.exists(f):
+                continue
+            d = json.load(open(f))
+            for t in d["threads"]:
+                h = t["hist"]
+                busy = sum(h[1:])
+                out["timeline"][f"{role}.{names.get(t['tag'], 'worker%d' % t['tag'])}"] = {
+                    "busy_s": t["busy_s"], "active_intervals": busy,
+                    "sat90_share_of_active": round(h[5] / busy, 3) if busy else 0.0,
+                    "sat75_share_of_active": round((h[4] + h[5]) / busy, 3) if busy else 0.0}
     print(json.dumps(out))
     if a.profile_dir:
         for f in sorted(glob.glob(os.path.join(a.profile_dir, "tunnel.*.prof"))):

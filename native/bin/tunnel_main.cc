@@ -448,5 +448,6 @@ int main(int argc, char** argv) {
   }
   if (cfg.rtc.turn.set()) LOG_INFO("tunnel", "TURN server configured: %s", cfg.rtc.turn.url.c_str());
   profiler::start_from_env();
+  profiler::start_timeline_from_env();
   return run_app(cfg);
 }

@@ -15,7 +15,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <thread>
+#include <vector>
 
 namespace p2pt::profiler {
 namespace {
@@ -132,8 +135,100 @@ void resolve(FILE* f, uint64_t a) {
 
 }  // namespace
 
+namespace timeline {
+constexpr int kBuckets = 6;  // < 10 %, < 25 %, < 50 %, < 75 %, < 90 %, >= 90 % of an interval
+struct Th {
+  int tag;
+  clockid_t cid;
+  uint64_t last_ns = 0;
+  uint64_t busy_ns = 0;
+  uint32_t hist[kBuckets] = {};
+  bool dead = false;
+};
+std::mutex mu;
+std::vector<Th> threads;
+std::atomic<bool> on{false};
+std::string path;
+uint64_t intervals = 0;
+
+uint64_t cpu_ns(clockid_t c, bool* ok) {
+  timespec ts;
+  *ok = clock_gettime(c, &ts) == 0;
+  return uint64_t(ts.tv_sec) * 1000000000ull + uint64_t(ts.tv_nsec);
+}
+
+void add_self(int tag) {
+  clockid_t c;
+  if (pthread_getcpuclockid(pthread_self(), &c) != 0) return;
+  bool ok;
+  Th t{tag, c};
+  t.last_ns = cpu_ns(c, &ok);
+  std::lock_guard<std::mutex> lk(mu);
+  threads.push_back(t);
+}
+
+void write_out() {
+  if (!on.exchange(false)) return;
+  std::lock_guard<std::mutex> lk(mu);
+  FILE* f = fopen(path.c_str(), "w");
+  if (!f) return;
+  fprintf(f, "{\"interval_ms\": 2, \"intervals\": %llu, \"buckets\": [\"<10\", \"<25\", \"<50\", \"<75\", \"<90\", \">=90\"], "
+          "\"threads\": [", static_cast<unsigned long long>(intervals));
+  for (size_t i = 0; i < threads.size(); i++) {
+    const Th& t = threads[i];
+    fprintf(f, "%s{\"tag\": %d, \"busy_s\": %.3f, \"hist\": [", i ? ", " : "", t.tag, double(t.busy_ns) / 1e9);
+    for (int b = 0; b < kBuckets; b++) fprintf(f, "%s%u", b ? ", " : "", t.hist[b]);
+    fprintf(f, "]}");
+  }
+  fprintf(f, "]}\n");
+  fclose(f);
+}
+
+void run() {
+  pthread_setname_np(pthread_self(), "p2pt-timeline");
+  sigset_t mask;
+  sigfillset(&mask);
+  pthread_sigmask(SIG_BLOCK, &mask, nullptr);
+  constexpr uint64_t kIntervalNs = 2000000;
+  while (on.load(std::memory_order_relaxed)) {
+    std::this_thread::sleep_for(std::chrono::nanoseconds(kIntervalNs));
+    std::lock_guard<std::mutex> lk(mu);
+    intervals++;
+    for (auto& t : threads) {
+      if (t.dead) continue;
+      bool ok;
+      const uint64_t now = cpu_ns(t.cid, &ok);
+      if (!ok) {  // the thread has exited
+        t.dead = true;
+        continue;
+      }
+      const uint64_t d = now - t.last_ns;
+      t.last_ns = now;
+      t.busy_ns += d;
+      const double u = double(d) / double(kIntervalNs);
+      const int b = u < 0.10 ? 0 : u < 0.25 ? 1 : u < 0.50 ? 2 : u < 0.75 ? 3 : u < 0.90 ? 4 : 5;
+      t.hist[b]++;
+    }
+  }
+}
+}  // namespace timeline
+
+bool start_timeline_from_env() {
+  const char* p = getenv("TUNNEL_THREAD_TIMELINE");
+  if (!p || !*p || timeline::on.load()) return false;
+  timeline::path = p;
+  if (size_t at = timeline::path.find("%p"); at != std::string::npos)
+    timeline::path.replace(at, 2, std::to_string(getpid()));
+  timeline::on.store(true);
+  timeline::add_self(0);
+  std::thread(timeline::run).detach();
+  atexit(timeline::write_out);
+  return true;
+}
+
 void register_thread(int tag) {
   t_tag = uint64_t(tag);
+  if (timeline::on.load(std::memory_order_relaxed)) timeline::add_self(tag);
   pthread_attr_t attr;
   if (pthread_getattr_np(pthread_self(), &attr) == 0) {
     void* lo = nullptr;

@@ -23,4 +23,12 @@ void dump();
 // `tag` labels the thread's samples in the dump ("T<tag>"; 0 = main).
 void register_thread(int tag);
 
+// TUNNEL_THREAD_TIMELINE=<path> ("%p" = pid): every 2 ms a sampler thread
+// reads each registered thread's CPU clock; at exit it writes, per thread, how
+// many 2 ms intervals it spent at each utilisation level (JSON). A pipeline
+// stage that saturates only in one phase of a workload (the upload half of a
+// bulk echo step, say) shows as intervals at >= 90 % although its average is
+// far lower. Call after start_from_env() on the main thread.
+bool start_timeline_from_env();
+
 }  // namespace p2pt::profiler

@@ -1,6 +1,9 @@
 #include "proto/frame.h"
 
 #include <algorithm>
+#include <cstdlib>
+
+#include <algorithm>
 #include <cstring>
 
 #include "core/crypto.h"
@@ -57,6 +60,14 @@ Bytes Frame::flat_payload() const {
   v.insert(v.end(), payload.data(), payload.data() + payload.size());
   for (auto& b : more) v.insert(v.end(), b.data(), b.data() + b.size());
   return Bytes::take(std::move(v));
+}
+
+int64_t flow_window() {
+  static const int64_t w = [] {
+    const char* e = getenv("TUNNEL_FLOW_WINDOW_KB");
+    return e && *e ? int64_t(std::max(64, atoi(e))) * 1024 : kFlowWindow;
+  }();
+  return w;
 }
 
 bool decode_chain(const Bytes& raw, std::vector<Bytes>& more, Frame& out, std::string* err) {

@@ -175,6 +175,9 @@ uint32_t credit_bytes(const Frame& f);
 // "flow" extension: initial per-stream, per-direction body credit, and the
 // backlog below which a receiver hands consumed bytes back as credit.
 constexpr int64_t kFlowWindow = 256 * 1024;
+// The initial per-stream window both peers assume: kFlowWindow, or
+// TUNNEL_FLOW_WINDOW_KB (A/B; both peers must be given the same value).
+int64_t flow_window();
 constexpr size_t kFlowGrantMin = 16 * 1024;
 
 // "flow" receive-window autotuning, done by the receiver alone (no wire
@@ -193,7 +196,7 @@ constexpr uint64_t kFlowGrowUs = 100 * 1000;
 constexpr uint64_t kFlowGrowSlackUs = 20 * 1000;
 
 struct FlowWindow {
-  int64_t win = kFlowWindow;
+  int64_t win = flow_window();
   uint64_t epoch_bytes = 0;  // granted since epoch_t0
   uint64_t epoch_t0 = 0;     // 0: no grant yet
   // `n` consumed bytes are about to be granted back at `now_us` on a path of

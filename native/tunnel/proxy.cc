@@ -354,7 +354,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
       simple_and_close(431, "text/plain", "Request header fields too large for the tunnel");
       return false;
     }
-    send_credit_ = proto::kFlowWindow;
+    send_credit_ = proto::flow_window();
     credit_paused_ = false;
     owed_ = 0;
     rwin_ = proto::FlowWindow{};
@@ -628,7 +628,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
   bool reject_not_ready_ = false;
   bool flow_paused_ = false;
   bool credit_paused_ = false;   // "flow": upload out of serve's credit
-  int64_t send_credit_ = proto::kFlowWindow;
+  int64_t send_credit_ = proto::flow_window();
   uint64_t owed_ = 0;            // "flow": RES_BODY bytes delivered, not yet granted back
   proto::FlowWindow rwin_;       // "flow": RES_BODY window autotuning
   static constexpr size_t kGrantLow = 64 * 1024;

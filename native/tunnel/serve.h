@@ -127,7 +127,7 @@ class ServeSession : public std::enable_shared_from_this<ServeSession> {
     bool fc = false;    // paused because the peer's credit ran out ("flow")
     bool uploading = false;   // request body still streaming to the upstream
     uint64_t uploaded = 0;    // request-body bytes received
-    int64_t credit = proto::kFlowWindow;  // "flow": RES_BODY bytes we may still send
+    int64_t credit = proto::flow_window();  // "flow": RES_BODY bytes we may still send
     proto::FlowWindow upwin;              // "flow": streamed REQ_BODY window autotuning
     std::string route;                    // BulkRoutes key
     uint64_t res_bytes = 0;               // response body bytes so far

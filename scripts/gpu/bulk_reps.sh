@@ -5,6 +5,7 @@
 # steps each (150 steps: ~10 s tunneled + the direct run of the same load).
 # JSON per run under gpurun_out/$TAG/; summary: python scripts/bulk_summary.py DIR.
 # PIN=1: loadgen / mock / serve / proxy on disjoint CPUs (utils/pinning.py).
+# TIMELINE=1: per-thread CPU utilisation in 2 ms intervals (which stage saturates).
 set -o pipefail
 TAG=${TAG:-bulk_reps}
 REPS=${REPS:-5}
@@ -31,7 +32,7 @@ for i in $(seq 1 $REPS); do
       [ $p = tcp ] && t=tcp
       n=$p
       [ $nvar -gt 1 ] && n=$label.$p
-      env ${envs//,/ } P2PT_BIN_DIR=$PWD/$bindir/bin timeout -k 10 300 python bench/profile_bulk.py --transport $t --steps $STEPS --extra="$x" ${PIN:+--pin} > gpurun_out/$TAG/${n}_$i.json 2>> gpurun_out/$TAG/err.log || { tail -5 gpurun_out/$TAG/err.log; exit 1; }
+      env ${envs//,/ } P2PT_BIN_DIR=$PWD/$bindir/bin timeout -k 10 300 python bench/profile_bulk.py --transport $t --steps $STEPS --extra="$x" ${PIN:+--pin} ${TIMELINE:+--timeline} > gpurun_out/$TAG/${n}_$i.json 2>> gpurun_out/$TAG/err.log || { tail -5 gpurun_out/$TAG/err.log; exit 1; }
       python -c "import json; d=json.load(open('gpurun_out/$TAG/${n}_$i.json')); print('$n $i', round(d['tunneled_req_s'],1), round(d['direct_req_s'],1), round(d['tunneled_req_s']/d['direct_req_s'],3), d['cpu_s_incl_warmup'], d.get('loss'), flush=True)"
     done
   done

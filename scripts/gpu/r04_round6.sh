@@ -1,0 +1,11 @@
+# Round 4, sixth host batch: which thread saturates in the 64 x 1 MB echo
+# (per-thread 2 ms utilisation timeline), with the per-stream flow window A/B
+# (256 KiB default vs 1 MiB), both MTUs, pinned; then the 1024-stream node
+# profile.
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r04
+echo "== flow A/B + timeline"; TAG=r04/flow_ab PIN=1 TIMELINE=1 REPS=2 PATHS="std jumbo" \
+  VARIANTS="w256:build:TUNNEL_SCTP_CHAIN=0 w1m:build:TUNNEL_SCTP_CHAIN=0,TUNNEL_FLOW_WINDOW_KB=1024" \
+  timeout -k 10 900 bash scripts/gpu/bulk_reps.sh > gpurun_out/r04/flow_ab.log 2>&1; rc=$?; tail -4 gpurun_out/r04/flow_ab.log; [ $rc -eq 0 ] || exit $rc
+echo "== node prof"; timeout -k 10 400 bash scripts/gpu/r04_node_prof.sh > gpurun_out/r04/node_prof.log 2>&1; rc=$?; tail -3 gpurun_out/r04/node_prof.log; exit $rc
