@@ -192,9 +192,12 @@ def _ref_probs(logits_row: torch.Tensor, T: float, k: int, p: float) -> torch.Te
         pr = torch.softmax(zk, -1)
         order = torch.argsort(pr, descending=True)
         before = torch.cumsum(pr[order], 0) - pr[order]
-        kp = torch.zeros_like(keep)
-        kp[order] = before < p
-        keep &= kp
+        # The cut is a value: every token whose z equals that of the last one
+        # needed to reach p is kept too (the kernel keeps z >= z_(p)). bf16
+        # logits tie often at V = 32,000, and an order-based cut kept an
+        # arbitrary part of the tied tokens.
+        cut = zk[order][before < p].min()
+        keep &= zk >= cut
     zf = torch.where(keep, z, torch.tensor(-float("inf"), device=z.device))
     return torch.softmax(zf, -1)
 
