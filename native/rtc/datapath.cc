@@ -289,9 +289,10 @@ void TxLaneState::run(const TxBatch& b, const RecordKeys& k, int fd, const SockA
 
 // ------------------------------------------------------------------ RX reader
 
-RxReader::RxReader(int fd, const SockAddr& remote, std::shared_ptr<const RecordKeys> keys, Deliver deliver, uint64_t id)
+RxReader::RxReader(int fd, const SockAddr& remote, std::shared_ptr<const RecordKeys> keys, Deliver deliver, uint64_t id,
+                   size_t slot)
     : fd_(fd), stop_fd_(eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC)), remote_(remote), keys_(std::move(keys)),
-      deliver_(std::move(deliver)), id_(id) {
+      deliver_(std::move(deliver)), id_(id), slot_(slot), pool_(slot) {
   th_ = std::thread([this] {
     sigset_t mask;
     sigemptyset(&mask);
@@ -422,7 +423,7 @@ void RxReader::run() {
         slots[i] = pool_.get();
         memset(&msgs[i], 0, sizeof msgs[i]);
         iovs[i].iov_base = slots[i]->data.get();
-        iovs[i].iov_len = 65536;
+        iovs[i].iov_len = slot_;
         msgs[i].msg_hdr.msg_iov = &iovs[i];
         msgs[i].msg_hdr.msg_iovlen = 1;
         msgs[i].msg_hdr.msg_name = &from[i];
@@ -437,6 +438,10 @@ void RxReader::run() {
         memcpy(&a.ss, &from[i], msgs[i].msg_hdr.msg_namelen);
         a.len = msgs[i].msg_hdr.msg_namelen;
         const uint32_t total = msgs[i].msg_len;
+        if (msgs[i].msg_hdr.msg_flags & MSG_TRUNC) {  // larger than a slot: never expected, counted
+          truncated.fetch_add(1, std::memory_order_relaxed);
+          continue;
+        }
         uint32_t ovfl = 0;
         const uint32_t seg = uint32_t(gro_seg(&msgs[i].msg_hdr, &ovfl));
         if (ovfl > rxq_ovfl.load(std::memory_order_relaxed)) rxq_ovfl.store(ovfl, std::memory_order_relaxed);

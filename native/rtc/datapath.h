@@ -212,8 +212,13 @@ class RxReader {
   using Deliver = std::function<void(std::unique_ptr<Burst>)>;
   static constexpr int kMaxOutstanding = 4;
 
-  RxReader(int fd, const SockAddr& remote, std::shared_ptr<const RecordKeys> keys, Deliver deliver, uint64_t id = 0);
+  // `slot`: receive buffer per datagram — 64 KiB when the socket coalesces
+  // (UDP GRO), else the largest datagram the path carries (a 1200-byte
+  // datagram in a 64 KiB slot pinned ~50x its size per burst).
+  RxReader(int fd, const SockAddr& remote, std::shared_ptr<const RecordKeys> keys, Deliver deliver, uint64_t id = 0,
+           size_t slot = 65536);
   uint64_t id() const { return id_; }
+  size_t slot() const { return slot_; }
   ~RxReader();  // stops and joins; bursts already delivered stay valid
   RxReader(const RxReader&) = delete;
   RxReader& operator=(const RxReader&) = delete;
@@ -225,6 +230,7 @@ class RxReader {
   std::atomic<uint64_t> bursts{0}, datagrams{0}, records{0}, raw_datagrams{0}, waits{0}, escapes{0}, gro_batches{0};
   // The socket's drop count as last reported by SO_RXQ_OVFL (cumulative).
   std::atomic<uint32_t> rxq_ovfl{0};
+  std::atomic<uint64_t> truncated{0};  // datagrams larger than a slot (MSG_TRUNC): lost
 
  private:
   void run();
@@ -246,6 +252,7 @@ class RxReader {
     const char* e = getenv("TUNNEL_RX_ESCAPE");
     return !(e && *e == '0');
   }();
+  size_t slot_ = 65536;
   BufPool pool_{65536};
   std::mutex mu_;
   std::condition_variable cv_;

@@ -128,6 +128,8 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   // Bumped whenever the selected pair (local socket or remote address)
   // changes: readers and lanes bound to the old path restart on it.
   uint64_t path_generation() const { return path_gen_; }
+  bool gro_enabled() const { return gro_enabled_; }
+  size_t coalesce_limit() const { return coalesce_limit_; }
   void test_bump_path_generation() { path_gen_++; }  // tests: as if the pair had switched
   // An outside reader (the DTLS RX reader, rtc/datapath.h) takes over the
   // selected direct pair's socket: its reactor reads stop until reattach().

@@ -237,8 +237,18 @@ void PeerConnection::start_rx_reader() {
     r->post_threadsafe([w, sb] {
       if (auto s = w.lock()) s->on_rx_burst(*sb);
     });
-  }, ++rx_reader_ids_);
+  }, ++rx_reader_ids_, rx_slot_bytes());
   LOG_DEBUG(kT, "UDP socket reader on for %s", remote.str().c_str());
+}
+
+// Receive slot of the socket reader: with UDP GRO a read may hold ~50
+// coalesced datagrams (64 KiB); without it one datagram, at most the path's
+// packet (several records on a coalescing same-host path) plus the DTLS record
+// overhead, rounded up.
+size_t PeerConnection::rx_slot_bytes() const {
+  if (!ice_ || ice_->gro_enabled()) return 65536;
+  const size_t pkt = std::max<size_t>(mtu_, ice_->coalesce_limit()) + 256;
+  return std::max<size_t>(2048, (pkt + 1023) & ~size_t(1023));
 }
 
 void PeerConnection::restart_rx_reader() {
@@ -640,6 +650,10 @@ void PeerConnection::start_sctp() {
   metrics::gauge_fn("tunnel_udp_reader_waits", [w] {
     auto s = w.lock();
     return s && s->rx_reader_ ? double(s->rx_reader_->waits.load()) : 0.0;
+  });
+  metrics::gauge_fn("tunnel_udp_reader_truncated", [w] {
+    auto s = w.lock();
+    return s && s->rx_reader_ ? double(s->rx_reader_->truncated.load()) : 0.0;
   });
   metrics::gauge_fn("tunnel_udp_reader_escapes", [w] {
     auto s = w.lock();

@@ -155,6 +155,7 @@ class PeerConnection : public std::enable_shared_from_this<PeerConnection> {
   uint64_t rx_reader_gen_ = 0;   // ICE path generation the reader was started for
   uint64_t rx_reader_ids_ = 0;
   void restart_rx_reader();
+  size_t rx_slot_bytes() const;
  public:
   uint64_t rx_reader_restarts_ = 0;
  private:

@@ -999,6 +999,53 @@ TEST(fragmented_messages_arrive_as_zero_copy_chains) {
   ans->close();
 }
 
+// Without UDP GRO every read holds one datagram: the socket reader's slots
+// are sized to the path's packet (2 KiB at a 1200-byte MTU), not 64 KiB, and
+// nothing is truncated.
+TEST(rx_reader_slots_follow_the_path_without_gro) {
+  if (!AesGcm::supported()) return;
+  set_rx_reader_enabled(true);
+  setenv("TUNNEL_NO_GRO", "1", 1);
+  Reactor r;
+  PcConfig cfg;
+  cfg.ice.include_loopback = true;
+  cfg.allow_jumbo = false;
+  auto off = PeerConnection::create(r, cfg, true);
+  auto ans = PeerConnection::create(r, cfg, false);
+  off->on_ice_candidate = [&](const std::string& c) { ans->add_ice_candidate(c, nullptr); };
+  ans->on_ice_candidate = [&](const std::string& c) { off->add_ice_candidate(c, nullptr); };
+  auto dc = off->create_data_channel("tunnel");
+  std::shared_ptr<DataChannel> rdc;
+  size_t got = 0, bytes = 0;
+  ans->on_data_channel = [&](std::shared_ptr<DataChannel> d) {
+    rdc = d;
+    d->on_message = [&](Bytes m) {
+      got++;
+      bytes += m.size();
+    };
+  };
+  off->start_gathering();
+  ans->start_gathering();  // sockets open here, without UDP_GRO
+  unsetenv("TUNNEL_NO_GRO");
+  CHECK(r.run_until([&] { return off->gathering_complete(); }, 3000));
+  std::string err;
+  CHECK(ans->set_remote_description(off->local_description(), &err));
+  CHECK(off->set_remote_description(ans->local_description(), &err));
+  CHECK(r.run_until([&] { return dc->is_open() && rdc && rdc->is_open(); }, 5000));
+  Bytes body = Bytes::copy(payload(65000, 3));
+  uint8_t hdr[5] = {21, 0, 0, 0, 1};
+  for (int i = 0; i < 60; i++) dc->send(hdr, 5, body);
+  CHECK(r.run_until([&] { return got == 60; }, 10000));
+  CHECK_EQ(bytes, size_t(60 * 65005));
+  if (ans->rx_reader()) {
+    CHECK_EQ(ans->rx_reader()->slot(), size_t(2048));
+    CHECK_EQ(ans->rx_reader()->truncated.load(), uint64_t(0));
+    CHECK(ans->rx_reader()->records.load() > 0);
+  }
+  off->close();
+  ans->close();
+}
+
 TEST(sctp_probe_rearms_t3_at_small_cwnd) {
   // 50 ms RTT, 2 % loss, a token trickle with 240 KB bursts: after a few loss
   // events cwnd is ~3 packets, so a lost burst tail is found only by a
