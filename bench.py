@@ -274,6 +274,7 @@ def main():
             "added_p99_ttft_ms": added_p99,
             "p50_ttft_ms": head["p50_ttft_ms"],
             "p99_ttft_ms": head["p99_ttft_ms"],
+            "step_max_ttft_ms_rank0": head.get("step_max_ttft_ms"),
             "errors": errors,
             "curve_rank0": curve,
             "jumbo_rank0": jumbo,

@@ -62,6 +62,8 @@ struct Result {
   uint64_t body_bytes = 0;
   uint64_t events = 0;
   std::vector<uint64_t> step_end;
+  std::vector<double> step_ttft_max_us;  // per step: the slowest first byte (thread 0)
+  size_t step_base = 0;                  // ttft_us entries before the current step
   uint64_t t_start = 0, t_end = 0;
 };
 
@@ -329,7 +331,13 @@ void run_thread(const Opts& o, int first, int count, Result& res, Result& warm_r
       s->on_done = [&] {
         if (--pending == 0) {
           trace_step(first, step, "step_end");
-          if (step >= o.warmup) res.step_end.push_back(Reactor::now_us());
+          if (step >= o.warmup) {
+            res.step_end.push_back(Reactor::now_us());
+            double mx = 0;
+            for (size_t k = res.step_base; k < res.ttft_us.size(); k++) mx = std::max(mx, res.ttft_us[k]);
+            res.step_ttft_max_us.push_back(mx);
+            res.step_base = res.ttft_us.size();
+          }
           step++;
           // --duration-s: timed steps repeat until the duration has passed
           // (the step in progress finishes), whatever --steps says.
@@ -419,7 +427,12 @@ int main(int argc, char** argv) {
   if (all.t_start == UINT64_MAX) all.t_start = all.t_end;
   double secs = double(all.t_end - all.t_start) / 1e6;
   // Per-step durations (thread 0's steps; every thread runs the same count).
-  std::string steps_ms;
+  std::string steps_ms, step_ttft;
+  for (size_t i = 0; i < res[0].step_ttft_max_us.size(); i++) {
+    char b[32];
+    snprintf(b, sizeof b, "%s%.3f", i ? ", " : "", res[0].step_ttft_max_us[i] / 1e3);
+    step_ttft += b;
+  }
   auto& se = res[0].step_end;
   for (size_t i = 0; i < se.size(); i++) {
     char b[32];
@@ -434,13 +447,13 @@ int main(int argc, char** argv) {
          "\"req_s\": %.4f, \"p50_ttft_ms\": %.4f, \"p90_ttft_ms\": %.4f, \"p99_ttft_ms\": %.4f, \"mean_ttft_ms\": %.4f, "
          "\"p50_total_ms\": %.4f, \"body_bytes\": %llu, \"MBps\": %.2f, \"events\": %llu, \"events_s\": %.1f, "
          "\"p50_itl_ms\": %.4f, \"p90_itl_ms\": %.4f, \"p99_itl_ms\": %.4f, \"p999_itl_ms\": %.4f, \"max_itl_ms\": %.4f, "
-         "\"step_ms\": [%s]}\n",
+         "\"step_ms\": [%s], \"step_max_ttft_ms\": [%s]}\n",
          o.streams, o.steps, T, all.ttft_us.size(), all.errors + warm_errors, secs,
          secs > 0 ? double(all.ttft_us.size()) / secs : 0.0, pct(all.ttft_us, 50) / 1e3, pct(all.ttft_us, 90) / 1e3,
          pct(all.ttft_us, 99) / 1e3, mean / 1e3, pct(all.total_us, 50) / 1e3,
          static_cast<unsigned long long>(all.body_bytes), secs > 0 ? double(all.body_bytes) / secs / 1e6 : 0.0,
          static_cast<unsigned long long>(all.events), secs > 0 ? double(all.events) / secs : 0.0,
          pct(all.itl_us, 50) / 1e3, pct(all.itl_us, 90) / 1e3, pct(all.itl_us, 99) / 1e3, pct(all.itl_us, 99.9) / 1e3,
-         itl_max / 1e3, steps_ms.c_str());
+         itl_max / 1e3, steps_ms.c_str(), step_ttft.c_str());
   return all.errors + warm_errors ? 1 : 0;
 }

@@ -209,11 +209,15 @@ Sink* sink() {
 bool enabled() { return sink() != nullptr; }
 
 void event(const char* role, uint32_t sid, const char* ev) {
+  if (sink()) event_at(role, sid, ev, Reactor::now_us());
+}
+
+void event_at(const char* role, uint32_t sid, const char* ev, uint64_t t_us) {
   Sink* k = sink();
   if (!k) return;
   char line[160];
   int n = snprintf(line, sizeof line, "{\"t_us\":%llu,\"role\":\"%s\",\"sid\":%u,\"ev\":\"%s\"}\n",
-                   static_cast<unsigned long long>(Reactor::now_us()), role, sid, ev);
+                   static_cast<unsigned long long>(t_us), role, sid, ev);
   if (n <= 0) return;
   n = std::min(n, int(sizeof line) - 1);
   std::lock_guard<std::mutex> lk(k->mu);

@@ -35,5 +35,8 @@ namespace p2pt::trace {
 bool enabled();
 // Append {"t_us":..,"role":..,"sid":..,"ev":..} to $TUNNEL_TRACE.
 void event(const char* role, uint32_t stream_id, const char* ev);
+// The same with a time taken earlier (CLOCK_MONOTONIC us), e.g. a
+// connection's accept stamped once its first request has a stream id.
+void event_at(const char* role, uint32_t stream_id, const char* ev, uint64_t t_us);
 void flush();  // buffered mode (TUNNEL_TRACE_BUFFERED=1): write out what is held
 }  // namespace p2pt::trace

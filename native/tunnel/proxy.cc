@@ -63,7 +63,7 @@ class ProxyWorker : public std::enable_shared_from_this<ProxyWorker> {
   BulkRoutes& bulk_routes() { return bulk_routes_; }
 
  private:
-  void adopt(int fd, Bytes unparsed = Bytes());
+  void adopt(int fd, Bytes unparsed = Bytes(), uint64_t accepted_us = 0);
   Reactor& r_;
   Reactor& assoc_;
   std::weak_ptr<ProxySession> sess_;
@@ -81,6 +81,13 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
  public:
   ProxyConn(std::weak_ptr<ProxyWorker> s, std::shared_ptr<TcpConn> c) : sess_(std::move(s)), conn_(std::move(c)) {}
   ~ProxyConn() { cancel_timer(); }
+
+  // TUNNEL_TRACE: when the listener accepted this connection and when its
+  // connection thread took it over, stamped under its first request's id.
+  void set_conn_times(uint64_t accepted_us, uint64_t adopted_us) {
+    accepted_us_ = accepted_us;
+    adopted_us_ = adopted_us;
+  }
 
   void start() {
     std::weak_ptr<ProxyConn> w = shared_from_this();
@@ -333,6 +340,11 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     sid_ = sess->next_stream_id();
     metrics::counter_add("tunnel_streams_opened_total");
     trace::event("proxy", sid_, "accept");
+    if (adopted_us_) {  // the connection's first request
+      if (accepted_us_) trace::event_at("proxy", sid_, "tcp_accept", accepted_us_);
+      trace::event_at("proxy", sid_, "conn_adopt", adopted_us_);
+      accepted_us_ = adopted_us_ = 0;
+    }
     if (req_.method == "GET") trace::event("proxy", sid_, "get");  // tells bulk downloads apart in the traces
     std::string path = req_.target;
     if (path.rfind("http://", 0) == 0 || path.rfind("https://", 0) == 0) {
@@ -622,6 +634,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
   bool no_body_ = false;
   bool first_body_ = false;
   bool body_seen_ = false;  // TUNNEL_TRACE: the request's first body byte was stamped
+  uint64_t accepted_us_ = 0, adopted_us_ = 0;
   bool response_complete_ = false;
   bool discard_body_ = false;    // response done mid-upload: drain the body, forward nothing
   bool pipelined_hold_ = false;
@@ -652,10 +665,10 @@ ProxyWorker::~ProxyWorker() {
   out_.reset();
 }
 
-void ProxyWorker::adopt(int fd, Bytes unparsed) {
-  trace::event("proxy", uint32_t(fd), "tcp_accept");
+void ProxyWorker::adopt(int fd, Bytes unparsed, uint64_t accepted_us) {
   auto tc = TcpConn::adopt(r_, fd);
   auto pc = std::make_shared<ProxyConn>(weak_from_this(), tc);
+  if (trace::enabled()) pc->set_conn_times(accepted_us, Reactor::now_us());
   conns_[pc.get()] = pc;
   pc->start();
   if (!unparsed.empty()) pc->on_data(unparsed.data(), unparsed.size());
@@ -686,7 +699,7 @@ void ProxyWorker::fail_all(const std::string& why) {
 void ProxyWorker::handle(ProxySession::Cmd& c) {
   using Cmd = ProxySession::Cmd;
   if (c.kind == Cmd::Adopt) {
-    adopt(c.fd, std::move(c.data));
+    adopt(c.fd, std::move(c.data), c.t_us);
     return;
   }
   auto it = streams_.find(c.sid);
@@ -974,6 +987,7 @@ void ProxySession::accept(int fd) {
   size_t k = place_->pick();
   Cmd c{Cmd::Adopt};
   c.fd = fd;
+  if (trace::enabled()) c.t_us = Reactor::now_us();
   command(k, std::move(c));
 }
 

@@ -94,6 +94,7 @@ class ProxySession : public std::enable_shared_from_this<ProxySession> {
     explicit Cmd(Kind k, uint32_t s = 0) : kind(k), sid(s) {}
     uint32_t sid = 0;
     int fd = -1;                                  // Adopt
+    uint64_t t_us = 0;                            // Adopt: accept time (TUNNEL_TRACE)
     Bytes data;                                   // Body / Error message; Adopt: bytes already read
     std::vector<Bytes> more;                      // Body: the rest of a frame that arrived in fragments
     std::shared_ptr<proto::ResponseHeaders> rh;   // Headers

@@ -101,7 +101,8 @@ def main():
         mock.stop()
         if os.path.exists(trace):
             os.unlink(trace)
-    hops = [("proxy", "accept", "proxy", "req_end"), ("proxy", "req_end", "serve", "req_headers"),
+    hops = [("proxy", "tcp_accept", "proxy", "conn_adopt"), ("proxy", "conn_adopt", "proxy", "accept"),
+            ("proxy", "accept", "proxy", "req_end"), ("proxy", "req_end", "serve", "req_headers"),
             ("serve", "req_headers", "serve", "req_end"), ("serve", "req_end", "serve", "upstream_sent"),
             ("serve", "upstream_sent", "mock", "req"), ("mock", "req", "serve", "first_body"),
             ("serve", "first_body", "proxy", "first_body"),
