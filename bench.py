@@ -175,15 +175,35 @@ def main():
         if dist:
             dist.barrier()
 
-    # Warmup (untimed): connections, SCTP cwnd, upstream prewarm pool.
-    if a.warmup and drive:
-        loadgen(tun.proxy_port, streams, a.warmup)
+    # Warmup (untimed) on the very keep-alive connections the timed steps then
+    # use: the load generator runs its W warm-up steps, reports READY and
+    # waits; the timed region brackets only its K timed steps. (Run as a
+    # separate process, the warm-up left the timed steps on fresh client
+    # connections, and the first timed step's TTFT — 0.76-0.82 ms against
+    # 0.2-0.34 ms for the others on the MI355X host — set the p99.)
+    from p2p_llm_tunnel_amd import binary
+    lg = None
+    if drive:
+        lg = subprocess.Popen([binary("tunnel-loadgen"), "--target", f"127.0.0.1:{tun.proxy_port}", "--streams",
+                               str(streams), "--steps", str(a.steps), "--warmup", str(max(1, a.warmup)), "--hold", "1"],
+                              stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        ready = lg.stdout.readline()
+        if ready.strip() != "READY":
+            raise RuntimeError(f"loadgen did not get ready: {ready!r} {lg.stderr.read()[-500:]}")
 
     # ---- headline: exactly K timed steps at S streams per GPU
     barrier()
     sync_device()
     t0 = time.perf_counter()
-    head = loadgen(tun.proxy_port, streams, a.steps) if drive else {"requests": 0, "errors": 0}
+    head = {"requests": 0, "errors": 0}
+    if lg:
+        lg.stdin.write("go\n")
+        lg.stdin.flush()
+        out, err = lg.communicate(timeout=600)
+        try:
+            head = json.loads(out.strip().splitlines()[-1])
+        except (IndexError, ValueError):
+            raise RuntimeError(f"loadgen failed (rc={lg.returncode}): {out[-500:]} {err[-500:]}")
     barrier()
     sync_device()
     dt_wall = time.perf_counter() - t0

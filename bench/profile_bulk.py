@@ -106,7 +106,7 @@ def main():
         # Share of each thread's active 2 ms intervals (>= 10 % CPU) spent at
         # >= 90 % / >= 75 % CPU, over the process's life (warm-up, tunneled and
         # direct runs; the direct run adds idle intervals only).
-        names = {0: "assoc", 90: "tx_lane", 91: "rx_lane", 92: "udp_reader"}
+        names = {0: "assoc", 90: "tx_seal", 93: "tx_send", 91: "rx_lane", 92: "udp_reader"}
         out["timeline"] = {}
         for role, pid in out.get("pids", {}).items():
             f = os.path.join(tl_dir, f"tl.{pid}.json")

@@ -47,6 +47,10 @@ struct Opts {
   int warmup = 1;
   int threads = 1;
   bool warm_conns = false;
+  // --hold 1: after the warm-up steps print "READY" and wait for a line on
+  // stdin before the timed steps (one thread): a caller times exactly the
+  // timed steps, on connections the warm-up already opened.
+  bool hold = false;
   std::string method = "POST";
   std::string path = "/v1/chat/completions";
   std::string body = R"({"model": "test-model", "stream": true, "messages": [{"role": "user", "content": "hi"}]})";
@@ -317,6 +321,13 @@ void run_thread(const Opts& o, int first, int count, Result& res, Result& warm_r
     for (auto& s : live) s->set_result(&warm_res);
   std::function<void()> launch = [&] {
     auto& set = step < o.warmup && !o.warm_conns ? warmers : live;
+    if (step == o.warmup && o.hold) {
+      printf("READY\n");
+      fflush(stdout);
+      char line[64];
+      if (!fgets(line, sizeof line, stdin)) {  // the caller went away: run anyway
+      }
+    }
     if (step == o.warmup) {
       res.t_start = Reactor::now_us();
       if (o.warm_conns)
@@ -388,6 +399,10 @@ int main(int argc, char** argv) {
     } else if (a == "--streams") o.streams = atoi(v.c_str());
     else if (a == "--steps") o.steps = atoi(v.c_str());
     else if (a == "--warmup") o.warmup = atoi(v.c_str());
+    else if (a == "--hold") {  // --hold 1
+      o.hold = v != "0";
+      if (o.hold) o.warm_conns = true;
+    }
     else if (a == "--threads") o.threads = std::max(1, atoi(v.c_str()));
     else if (a == "--method") o.method = v;
     else if (a == "--path") {

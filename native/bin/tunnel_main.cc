@@ -99,7 +99,7 @@ const std::vector<Opt>& ext_opts() {
       {"busy-poll-us", "TUNNEL_BUSY_POLL_US", "0",
        "Keep polling for N us after I/O instead of sleeping (lower per-hop latency, more CPU)", Kind::U64},
       {"workers", "TUNNEL_WORKERS", "auto",
-       "HTTP worker threads beside the association thread (auto: one per 4 CPUs, 1..4; 0: single thread)", Kind::U64OrAuto, Role::Both, 0, 256},
+       "HTTP worker threads beside the association thread (auto: half the usable CPUs less one, 1..4; 0: single thread)", Kind::U64OrAuto, Role::Both, 0, 256},
       {"inline-streams", "TUNNEL_INLINE_STREAMS", "16",
        "Concurrent streams handled on the association thread before new ones go to workers", Kind::U64},
       {"max-request-body", "TUNNEL_MAX_REQUEST_BODY", "0",

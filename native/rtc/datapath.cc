@@ -38,7 +38,8 @@ Lane::Lane(const char* name) {
     for (int sig : {SIGINT, SIGTERM, SIGHUP, SIGQUIT, SIGUSR1, SIGUSR2, SIGPIPE}) sigaddset(&mask, sig);
     pthread_sigmask(SIG_BLOCK, &mask, nullptr);
     pthread_setname_np(pthread_self(), n.c_str());
-    profiler::register_thread(n.find("-tx") != std::string::npos ? 90 : 91);  // T90 / T91 in profiles
+    // T90 seal / T93 send / T91 rx in profiles and timelines
+    profiler::register_thread(n.find("-txsend") != std::string::npos ? 93 : n.find("-tx") != std::string::npos ? 90 : 91);
     run();
   });
 }
@@ -187,9 +188,29 @@ bool open_record(const AesGcm& g, const uint8_t iv[4], uint8_t* rec, size_t len,
 
 // ------------------------------------------------------------------ TX lane
 
+std::shared_ptr<SealedBatch> TxLaneState::get_sealed() {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (free_.empty()) return std::make_shared<SealedBatch>();
+  auto s = std::move(free_.back());
+  free_.pop_back();
+  return s;
+}
+
+void TxLaneState::put_sealed(std::shared_ptr<SealedBatch> s) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (free_.size() < 16) free_.push_back(std::move(s));
+}
+
 void TxLaneState::run(const TxBatch& b, const RecordKeys& k, int fd, const SockAddr& to, size_t coalesce) {
-  // 1. Seal every record into one contiguous buffer; datagram boundaries are
+  seal(b, k, coalesce, one_);
+  send(one_, fd, to);
+}
+
+void TxLaneState::seal(const TxBatch& b, const RecordKeys& k, size_t coalesce, SealedBatch& sb) {
+  // Seal every record into one contiguous buffer; datagram boundaries are
   // kept aside (several records per datagram on same-host jumbo paths).
+  std::vector<uint8_t>& out_ = sb.out;
+  auto& dgs_ = sb.dgs;
   size_t need = 0;
   for (auto& r : b.recs) need += record_size(r.total);
   if (out_.size() < need) out_.resize(need);
@@ -207,6 +228,11 @@ void TxLaneState::run(const TxBatch& b, const RecordKeys& k, int fd, const SockA
   records.fetch_add(b.recs.size(), std::memory_order_relaxed);
   batches.fetch_add(1, std::memory_order_relaxed);
   datagrams.fetch_add(dgs_.size(), std::memory_order_relaxed);
+}
+
+void TxLaneState::send(SealedBatch& sb, int fd, const SockAddr& to) {
+  std::vector<uint8_t>& out_ = sb.out;
+  auto& dgs_ = sb.dgs;
   // 2. sendmmsg: runs of equal-size datagrams leave as one UDP GSO message
   // (contiguous in out_, so one iovec each); a shorter datagram ends a run.
   constexpr int kBatch = 64;

@@ -172,20 +172,42 @@ void seal_record(const AesGcm& g, const uint8_t iv[4], uint8_t* out, uint8_t typ
 // Authenticates and decrypts one record in place; false if it fails.
 bool open_record(const AesGcm& g, const uint8_t iv[4], uint8_t* rec, size_t len, uint8_t** pt, size_t* ptl);
 
-// TX lane state (lane thread only): the output buffer and GSO availability.
+// One TX batch after sealing: the records back to back in `out`, datagram
+// boundaries aside (several records per datagram on same-host jumbo paths).
+struct SealedBatch {
+  std::vector<uint8_t> out;
+  std::vector<std::pair<size_t, size_t>> dgs;  // (offset, length) in out
+};
+
+// TX lane state. The lane is a two-stage pipeline: the seal stage encrypts a
+// batch into a SealedBatch, the send stage (a thread of its own) hands it to
+// the kernel with sendmmsg + UDP GSO, in batch order, while the seal stage
+// works on the next batch. On the MI355X host the single TX lane that did
+// both was the saturated stage of the 64 x 1 MB echo (>= 90 % CPU in 54-82 %
+// of its active 2 ms intervals at 1200-byte MTU, the association thread
+// under 10 %; profiles/r04/flow_ab), its time split about evenly between
+// AES-GCM and sendmmsg.
 class TxLaneState {
  public:
-  // Seals the batch and sends it to target (runs on the lane).
+  // Seal stage: encrypts the batch (runs on the seal lane).
+  void seal(const TxBatch& b, const RecordKeys& k, size_t coalesce, SealedBatch& out);
+  // Send stage: sends a sealed batch to target (runs on the send lane).
+  void send(SealedBatch& s, int fd, const SockAddr& to);
+  // Both stages in a row (tests; the single-lane path).
   void run(const TxBatch& b, const RecordKeys& k, int fd, const SockAddr& to, size_t coalesce);
+  // Sealed batches are recycled between the stages (buffers allocated once).
+  std::shared_ptr<SealedBatch> get_sealed();
+  void put_sealed(std::shared_ptr<SealedBatch> s);
   // send_drops: datagrams dropped (socket buffer still full after kSendWaitMs
   // of POLLOUT waits, or unreachable); send_waits: POLLOUT waits taken.
   std::atomic<uint64_t> batches{0}, records{0}, datagrams{0}, gso_msgs{0}, send_drops{0}, send_waits{0};
   static constexpr int kSendWaitMs = 20;
 
  private:
-  std::vector<uint8_t> out_;
-  std::vector<std::pair<size_t, size_t>> dgs_;  // (offset, length) in out_
-  bool gso_ok_ = true;
+  SealedBatch one_;  // run()'s buffer
+  bool gso_ok_ = true;  // send stage only
+  std::mutex mu_;
+  std::vector<std::shared_ptr<SealedBatch>> free_;
 };
 
 // Socket reader: the selected pair's UDP socket read on a thread of its own

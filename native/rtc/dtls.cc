@@ -703,6 +703,7 @@ void DtlsTransport::enable_lanes(std::function<bool(TxTarget&)> target) {
   tx_state_ = std::make_shared<TxLaneState>();
   tx_pool_ = std::make_shared<TxBatchPool>();
   tx_pend_ = tx_pool_->get();
+  tx_send_lane_ = std::make_unique<Lane>("p2pt-dtls-txsend");
   tx_lane_ = std::make_unique<Lane>("p2pt-dtls-tx");
   rx_lane_ = std::make_unique<Lane>("p2pt-dtls-rx");
   LOG_DEBUG(kT, "DTLS crypto lanes on (inline below %zu bytes)", datapath_inline_bytes());
@@ -733,7 +734,7 @@ void DtlsTransport::commit_tx() {
   }
   TxTarget t;
   const bool direct = tx_target_ && tx_target_(t) && t.fd >= 0;
-  if (!direct || (tx_pend_->bytes < datapath_inline_bytes() && tx_lane_->idle())) {
+  if (!direct || (tx_pend_->bytes < datapath_inline_bytes() && tx_lane_->idle() && tx_send_lane_->idle())) {
     // A small flush with nothing ahead of it on the lane (or no direct path):
     // sealed here, sent by the ICE agent's flush — no thread hop on the
     // latency path of a token.
@@ -746,11 +747,19 @@ void DtlsTransport::commit_tx() {
   auto b = std::move(tx_pend_);
   tx_pend_ = tx_pool_->get();
   lane_tx_batches_++;
+  // Seal stage, then the send stage on its own thread: while one batch is
+  // in sendmmsg the next is being encrypted (wire order is the batch order).
+  Lane* send_lane = tx_send_lane_.get();
   tx_lane_->submit([b = std::move(b), st = tx_state_, k = keys_, fd = lane_fd_, to = t.to, co = t.coalesce,
-                    pool = tx_pool_]() mutable {
-    st->run(*b, *k, fd->fd, to, co);
-    b->clear();  // the body references go here, once the records are sent
+                    pool = tx_pool_, send_lane]() mutable {
+    auto sb = st->get_sealed();
+    st->seal(*b, *k, co, *sb);
+    b->clear();  // the body references go here, once the records are sealed
     pool->put(std::move(b));
+    send_lane->submit([sb = std::move(sb), st, fd = std::move(fd), to]() mutable {
+      st->send(*sb, fd->fd, to);
+      st->put_sealed(std::move(sb));
+    });
   });
 }
 

@@ -178,7 +178,10 @@ class DtlsTransport : public std::enable_shared_from_this<DtlsTransport> {
   std::shared_ptr<RecordKeys> keys_;
   uint8_t wiv_[4] = {}, riv_[4] = {};
   // --- crypto/IO lanes
-  std::unique_ptr<Lane> tx_lane_, rx_lane_;
+  // Declared before the seal lane so it is destroyed after it: the seal
+  // lane's last jobs still hand their batches to the send lane.
+  std::unique_ptr<Lane> tx_send_lane_;
+  std::unique_ptr<Lane> tx_lane_, rx_lane_;  // tx_lane_: the seal stage
   std::shared_ptr<TxLaneState> tx_state_;
   std::shared_ptr<LaneFd> lane_fd_;
   uint64_t rx_dropped_ = 0;

@@ -47,15 +47,18 @@ WorkerThread::~WorkerThread() {
   r_->run_until([] { return false; }, 20);
 }
 
-// One worker per 4 CPUs the process may use, 1..4: measured on the MI355X
-// host (bench/bench_node.py, profiles/node_r02/), 4 workers carried 1024
-// 1 ms-token streams at direct speed while 8 lost to contention with the
-// association thread, and a single worker already halves the 256-stream TTFT.
+// Half the CPUs the process may use less one (the association thread, the
+// TX seal and send stages and the socket reader take the rest), 1..4:
+// measured on the MI355X host (bench/bench_node.py, profiles/node_r02/), 4
+// workers carried 1024 1 ms-token streams at direct speed while 8 lost to
+// contention with the association thread. One worker per 4 CPUs (round 3)
+// gave a process pinned to 6 CPUs a single worker, which then saturated on
+// the 64 x 1 MB echo (all 64 upstream sockets' I/O; profiles/r04/flow_ab).
 int WorkerPool::auto_count() {
   long n = sysconf(_SC_NPROCESSORS_ONLN);
   cpu_set_t set;
   if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
-  return int(std::clamp<long>(n / 4, 1, 4));
+  return int(std::clamp<long>(n / 2 - 1, 1, 4));
 }
 
 WorkerPool::WorkerPool(int n) {
