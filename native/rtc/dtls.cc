@@ -1,3 +1,4 @@
+#include <cstdlib>
 #include "rtc/dtls.h"
 
 #include <openssl/bio.h>
@@ -749,7 +750,24 @@ void DtlsTransport::commit_tx() {
   lane_tx_batches_++;
   // Seal stage, then the send stage on its own thread: while one batch is
   // in sendmmsg the next is being encrypted (wire order is the batch order).
+  // TUNNEL_TX_PIPELINE=0 keeps both stages on the seal thread (round-3 lane).
+  static const bool pipelined = [] {
+    const char* e = getenv("TUNNEL_TX_PIPELINE");
+    return !(e && e[0] == '0');
+  }();
   Lane* send_lane = tx_send_lane_.get();
+  if (!pipelined) {
+    tx_lane_->submit([b = std::move(b), st = tx_state_, k = keys_, fd = lane_fd_, to = t.to, co = t.coalesce,
+                      pool = tx_pool_]() mutable {
+      auto sb = st->get_sealed();
+      st->seal(*b, *k, co, *sb);
+      b->clear();
+      pool->put(std::move(b));
+      st->send(*sb, fd->fd, to);
+      st->put_sealed(std::move(sb));
+    });
+    return;
+  }
   tx_lane_->submit([b = std::move(b), st = tx_state_, k = keys_, fd = lane_fd_, to = t.to, co = t.coalesce,
                     pool = tx_pool_, send_lane]() mutable {
     auto sb = st->get_sealed();

@@ -44,6 +44,9 @@ struct PcConfig {
   // answers what it receives (serve: a request's SACK rides on its response);
   // 0 on the side that mostly receives streams (proxy).
   uint64_t sack_delay_us = 0;
+  // Fragmented messages handed to chain consumers as views of their packets
+  // instead of one reassembled copy (also TUNNEL_SCTP_CHAIN=1).
+  bool message_chains = false;
 };
 
 class PeerConnection;

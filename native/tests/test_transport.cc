@@ -952,6 +952,7 @@ TEST(fragmented_messages_arrive_as_zero_copy_chains) {
   PcConfig cfg;
   cfg.ice.include_loopback = true;
   cfg.allow_jumbo = false;
+  cfg.message_chains = true;
   auto off = PeerConnection::create(r, cfg, true);
   auto ans = PeerConnection::create(r, cfg, false);
   off->on_ice_candidate = [&](const std::string& c) { ans->add_ice_candidate(c, nullptr); };
