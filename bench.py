@@ -145,6 +145,11 @@ def direct(ups, streams, steps):
 def main():
     a = parse()
     dist, rank, world = dist_init()
+    # Bring the GPU runtime up now: its first synchronise (import torch, HIP
+    # init and its threads) used to land between the warm-up and the first
+    # timed step, and that step's TTFT (0.82-0.91 ms against 0.26-0.39 ms for
+    # the other nine on the MI355X host, profiles/r04/head_hold) set the p99.
+    sync_device()
     if world > 1:  # disjoint port blocks: ranks start their tunnels concurrently
         os.environ.setdefault("P2PT_PORT_BASE", str(20000 + 500 * int(os.environ.get("LOCAL_RANK", rank))))
     from p2p_llm_tunnel_amd.utils.build import ensure_native

@@ -35,6 +35,7 @@ sys.path.insert(0, ROOT)
 
 from p2p_llm_tunnel_amd import binary  # noqa: E402
 from p2p_llm_tunnel_amd.utils.build import ensure_native  # noqa: E402
+from p2p_llm_tunnel_amd.utils.pinning import cgroup_cpu_stat, cpu_stat_delta  # noqa: E402
 from p2p_llm_tunnel_amd.utils.procs import Tunnel, free_port, spawn  # noqa: E402
 
 
@@ -168,12 +169,15 @@ def main():
                     loadgen([t.proxy_port], s, 1, a.lg_threads, warmup=0)
                     sid_lo = None
                     for rep in range(a.reps):
+                        g0 = cgroup_cpu_stat()
                         d = loadgen(ports, s, 1 << 20, a.lg_threads, extra=dur)
+                        g1 = cgroup_cpu_stat()
                         c0 = (cpu_s(t.serve.popen.pid), cpu_s(t.proxy.popen.pid))
                         t_tr0 = time.monotonic_ns() // 1000
                         tr = loadgen([t.proxy_port], s, 1 << 20, a.lg_threads, extra=dur)
                         t_tr1 = time.monotonic_ns() // 1000
                         c1 = (cpu_s(t.serve.popen.pid), cpu_s(t.proxy.popen.pid))
+                        g2 = cgroup_cpu_stat()
                         if trace:
                             windows.append((w, s, t_tr0, t_tr1))
                         r = {"workers": w, "streams": s, "rep": rep, **row("tunneled", tr), **row("direct", d),
@@ -182,7 +186,9 @@ def main():
                              "added_p99_ttft_ms": tr["p99_ttft_ms"] - d["p99_ttft_ms"],
                              "added_p99_itl_ms": tr["p99_itl_ms"] - d["p99_itl_ms"],
                              "serve_cpu_s": round(c1[0] - c0[0], 3), "proxy_cpu_s": round(c1[1] - c0[1], 3),
-                             "seconds": tr["seconds"], "direct_seconds": d["seconds"]}
+                             "seconds": tr["seconds"], "direct_seconds": d["seconds"],
+                             # job-wide CPU use and quota throttling during each leg
+                             "direct_cgroup": cpu_stat_delta(g0, g1), "tunneled_cgroup": cpu_stat_delta(g1, g2)}
                         res["runs"].append(r)
                         print(json.dumps(r), file=sys.stderr, flush=True)
         keys = ["events_ratio", "tunneled_events_s", "direct_events_s", "added_p50_ttft_ms", "added_p99_ttft_ms",

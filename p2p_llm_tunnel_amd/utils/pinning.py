@@ -65,3 +65,28 @@ def cpu_plan(cpus: list[int] | None = None) -> dict[str, str]:
     plan = {"loadgen": cpus[:lg], "mock": cpus[lg:lg + mk], "serve": cpus[lg + mk:lg + mk + sv],
             "proxy": cpus[lg + mk + sv:]}
     return {k: fmt_cpus(v) for k, v in plan.items()}
+
+
+def cgroup_cpu_stat() -> dict[str, int]:
+    """The job cgroup's CPU accounting (cgroup v2 ``cpu.stat``): ``usage_usec``
+    (CPU time of every process in the job), ``nr_periods``, ``nr_throttled`` and
+    ``throttled_usec``. On the GPU pool the job's quota is 16 CPUs
+    (``cpu.max`` 1600000/100000): a burst past it stalls EVERY process of the
+    job, loadgen and mock included, until the next 100 ms period — a tail that
+    is no stage's own. {} where the file is absent."""
+    out: dict[str, int] = {}
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            for line in f:
+                k, _, v = line.partition(" ")
+                if v.strip().isdigit():
+                    out[k] = int(v)
+    except OSError:
+        pass
+    return out
+
+
+def cpu_stat_delta(a: dict[str, int], b: dict[str, int]) -> dict[str, int]:
+    """b - a for the throttling keys of two cgroup_cpu_stat() snapshots."""
+    keys = ("usage_usec", "nr_periods", "nr_throttled", "throttled_usec")
+    return {k: b[k] - a[k] for k in keys if k in a and k in b}
