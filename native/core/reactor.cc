@@ -188,8 +188,21 @@ void Reactor::run_flush() {
 void Reactor::run_once(int timeout_ms) {
   epoll_event evs[256];
   if (busy_poll_us_ && timeout_ms > 0 && now_us() - last_io_us_ < busy_poll_us_) timeout_ms = 0;
+  const uint64_t t_wait = now_us();
+  if (wake_us_) win_busy_us_ += t_wait - wake_us_;
+  if (t_wait - win_start_us_ >= 2000) {
+    load_ = win_start_us_ ? double(win_busy_us_) / double(t_wait - win_start_us_) : 0.0;
+    win_start_us_ = t_wait;
+    win_busy_us_ = 0;
+  }
   int n = epoll_wait(epfd_, evs, 256, timeout_ms);
   if (n < 0 && errno != EINTR) throw std::runtime_error(std::string("epoll_wait: ") + strerror(errno));
+  wake_us_ = now_us();
+  if (wake_us_ - win_start_us_ >= 2000 && win_start_us_) {  // a long sleep ends the window idle
+    load_ = double(win_busy_us_) / double(wake_us_ - win_start_us_);
+    win_start_us_ = wake_us_;
+    win_busy_us_ = 0;
+  }
   if (n > 0 && busy_poll_us_) last_io_us_ = now_us();
   for (int i = 0; i < n; i++) {
     uint64_t tag = evs[i].data.u64;

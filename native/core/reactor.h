@@ -70,6 +70,9 @@ class Reactor {
   // scheduler wake-up latency out of each hop of a token's path at the cost
   // of spinning one core while traffic flows (0 = always block).
   void set_busy_poll_us(uint64_t us) { busy_poll_us_ = us; }
+  // Share of wall time this loop spent outside epoll_wait over the last
+  // window of >= 2 ms (0..1): lets a transport move work off a saturated loop.
+  double load() const { return load_; }
 
   static uint64_t now_us();
   static uint64_t now_ms() { return now_us() / 1000; }
@@ -91,6 +94,8 @@ class Reactor {
   bool stop_ = false;
   uint64_t busy_poll_us_ = 0;
   uint64_t last_io_us_ = 0;
+  uint64_t win_start_us_ = 0, win_busy_us_ = 0, wake_us_ = 0;
+  double load_ = 0.0;
   uint64_t gen_ = 1;
   std::unordered_map<int, FdEntry> fds_;
   std::multimap<uint64_t, TimerId> timer_order_;

@@ -496,6 +496,14 @@ size_t datapath_inline_bytes() {
   return v;
 }
 
+double datapath_inline_load() {
+  static const double v = [] {
+    const char* e = getenv("TUNNEL_INLINE_LOAD_PCT");
+    return e && *e ? double(strtoull(e, nullptr, 10)) / 100.0 : 0.5;
+  }();
+  return v;
+}
+
 namespace {
 std::atomic<int> g_rx_reader{-1};  // -1: from the environment
 }

@@ -1,5 +1,6 @@
-#include <cstdlib>
 #include "rtc/dtls.h"
+
+#include <cstdlib>
 
 #include <openssl/bio.h>
 #include <openssl/err.h>
@@ -735,10 +736,13 @@ void DtlsTransport::commit_tx() {
   }
   TxTarget t;
   const bool direct = tx_target_ && tx_target_(t) && t.fd >= 0;
-  if (!direct || (tx_pend_->bytes < datapath_inline_bytes() && tx_lane_->idle() && tx_send_lane_->idle())) {
+  Reactor* loop = Reactor::current();
+  if (!direct || (tx_pend_->bytes < datapath_inline_bytes() && tx_lane_->idle() && tx_send_lane_->idle() &&
+                  !(loop && loop->load() >= datapath_inline_load()))) {
     // A small flush with nothing ahead of it on the lane (or no direct path):
     // sealed here, sent by the ICE agent's flush — no thread hop on the
-    // latency path of a token.
+    // latency path of a token. A loop that is itself near saturation hands
+    // even small flushes to the lanes (the sendmmsg is the costly part).
     seal_inline(*tx_pend_);
     tx_pend_->clear();
     inline_tx_batches_++;

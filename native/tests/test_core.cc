@@ -123,6 +123,27 @@ TEST(reactor_timers_order_and_cancel) {
   CHECK(seen.size() == 3 && seen[0] == 0 && seen[1] == 1 && seen[2] == 3);
 }
 
+// The loop's load estimate: ~1 while every pass spins, ~0 while it sleeps.
+TEST(reactor_load_tracks_busy_share) {
+  Reactor r;
+  std::function<void()> spin = [&] {
+    uint64_t t = Reactor::now_us();
+    while (Reactor::now_us() - t < 300) {
+    }
+    r.post_threadsafe(spin);  // through epoll, so every pass is a loop iteration
+  };
+  r.post_threadsafe(spin);
+  r.run_until([] { return false; }, 30);
+  const double busy = r.load();
+  Reactor q;
+  q.call_later_ms(25, [] {});
+  q.run_until([] { return false; }, 30);
+  const double idle = q.load();
+  printf("  load busy %.2f idle %.2f\n", busy, idle);
+  CHECK(busy > 0.7);
+  CHECK(idle < 0.2);
+}
+
 TEST(frame_codec) {
   proto::Frame f{proto::MsgType::ResBody, 0xDEADBEEF, Bytes::copy("abc")};
   Bytes e = f.encode();
