@@ -191,11 +191,24 @@ def bulk_echo(a):
         extra = [x for x in a.extra.split() if x]
         pin_s = ["--cpu-affinity", plan["serve"]] if plan else []
         pin_p = ["--cpu-affinity", plan["proxy"]] if plan else []
+        ms, mp = free_port(), free_port()
         with Tunnel(f"http://127.0.0.1:{port}", transport=a.transport,
                     env={"TUNNEL_TRACE": trace, "TUNNEL_TRACE_BUFFERED": "1"},
-                    serve_extra=extra + pin_s, proxy_extra=extra + pin_p) as t:
+                    serve_extra=extra + pin_s + ["--metrics-listen", f"127.0.0.1:{ms}"],
+                    proxy_extra=extra + pin_p + ["--metrics-listen", f"127.0.0.1:{mp}"]) as t:
             path = t.serve.wait_for("WebRTC connection established", 1).split(" via ", 1)[-1] if a.transport == "webrtc" else ""
             tr = run(t.proxy_port, trace)
+            # Recovery events during the run (a timer-driven retransmission
+            # stalls a step by its timeout): both sides summed.
+            import urllib.request
+            counters = {}
+            for p_ in (ms, mp):
+                txt = urllib.request.urlopen(f"http://127.0.0.1:{p_}/metrics", timeout=5).read().decode()
+                for l in txt.splitlines():
+                    if l.startswith(("tunnel_sctp_", "tunnel_udp_rx_overflow", "tunnel_dtls_lane_send")):
+                        k, v = l.split()[0], float(l.split()[1])
+                        if any(x in k for x in ("retransmits", "t3_", "tlp_", "rack_marks", "overflow", "drops", "undos")):
+                            counters[k] = counters.get(k, 0.0) + v
         dr = run(port)
         ev, lg = {}, {}
         with open(trace) as f:
@@ -261,12 +274,18 @@ def bulk_echo(a):
             steps.append(row)
     steps = steps[2:] if len(steps) > 4 else steps
     waterfall = {k: statistics.median([s[k] for s in steps if s.get(k) is not None]) for k in steps[0]} if steps else {}
+    slowest = sorted(steps, key=lambda s: s.get("step end at the client") or 0)[-3:]
+
+    def step_stats(r):
+        v = r["step_ms"]
+        return {"req_s": r["req_s"], "step_ms_p50": statistics.median(v), "step_ms_mean": statistics.fmean(v),
+                "step_ms_p90": _pct(v, .9), "step_ms_max": max(v), "errors": r["errors"]}
     res = {"mode": "bulk-echo", "transport": a.transport, "extra": a.extra, "path": path, "pinned": plan,
            "streams": streams, "mb": a.mb, "steps": a.steps,
-           "tunneled": {"req_s": tr["req_s"], "step_ms_p50": statistics.median(tr["step_ms"]), "errors": tr["errors"]},
-           "direct": {"req_s": dr["req_s"], "step_ms_p50": statistics.median(dr["step_ms"]), "errors": dr["errors"]},
+           "tunneled": step_stats(tr), "direct": step_stats(dr),
            "ratio": tr["req_s"] / dr["req_s"] if dr["req_s"] else None,
-           "step_waterfall_ms_median": waterfall, "per_request": per_hop}
+           "step_waterfall_ms_median": waterfall, "slowest_steps": slowest, "recovery": counters,
+           "tunneled_step_ms": tr["step_ms"], "direct_step_ms": dr["step_ms"], "per_request": per_hop}
     print(json.dumps(res, indent=1))
 
 
