@@ -499,7 +499,10 @@ size_t datapath_inline_bytes() {
 double datapath_inline_load() {
   static const double v = [] {
     const char* e = getenv("TUNNEL_INLINE_LOAD_PCT");
-    return e && *e ? double(strtoull(e, nullptr, 10)) / 100.0 : 0.5;
+    // Off by default (1.0: a loop is never that busy): on the MI355X host the
+    // 64 x 1 MB echo lost 4-14 % with it at 0.5, and the node row's 1024-stream
+    // tail did not separate from run-to-run noise (profiles/r04/inl_ab, node9).
+    return e && *e ? double(strtoull(e, nullptr, 10)) / 100.0 : 1.0;
   }();
   return v;
 }

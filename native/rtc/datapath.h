@@ -284,7 +284,7 @@ class RxReader {
 };
 
 size_t datapath_inline_bytes();  // TUNNEL_DATAPATH_INLINE_BYTES (default 32 KiB)
-double datapath_inline_load();   // TUNNEL_INLINE_LOAD_PCT / 100 (default 0.5): loop load above which nothing is sealed inline
+double datapath_inline_load();   // TUNNEL_INLINE_LOAD_PCT / 100 (default 1.0 = off): loop load above which nothing is sealed inline
 bool rx_reader_enabled();        // TUNNEL_RX_READER (default on; 0 = the association thread reads the socket)
 void set_rx_reader_enabled(bool on);  // tests: both receive paths in one process
 bool datapath_enabled();         // TUNNEL_DATAPATH (default on; 0 = everything on the association thread)

@@ -741,8 +741,8 @@ void DtlsTransport::commit_tx() {
                   !(loop && loop->load() >= datapath_inline_load()))) {
     // A small flush with nothing ahead of it on the lane (or no direct path):
     // sealed here, sent by the ICE agent's flush — no thread hop on the
-    // latency path of a token. A loop that is itself near saturation hands
-    // even small flushes to the lanes (the sendmmsg is the costly part).
+    // latency path of a token. With TUNNEL_INLINE_LOAD_PCT set, a loop that
+    // is itself that busy hands even small flushes to the lanes.
     seal_inline(*tx_pend_);
     tx_pend_->clear();
     inline_tx_batches_++;
