@@ -135,12 +135,18 @@ def main():
     ap.add_argument("--extra", default="", help="extra flags for both tunnel processes")
     ap.add_argument("--mock-threads", type=int, default=4,
                     help="reactor threads of the native mock (it serves the SSE and the downloads, tunneled and direct)")
+    ap.add_argument("--timeline", action="store_true",
+                    help="per-thread CPU utilisation of both tunnels in 2 ms intervals (which stage saturates)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     ensure_native()
     mport = free_port()
     mock = spawn("mock", [binary("tunnel-mock"), "--port", str(mport), "--interval-ms", str(a.interval_ms),
                           "--tokens", str(a.tokens), "--threads", str(a.mock_threads)])
+    tl_dir, tl_env = None, None
+    if a.timeline:
+        from p2p_llm_tunnel_amd.utils import timeline
+        tl_dir, tl_env = timeline.new_dir()
     mock.wait_for("Mock LLM server running", 10)
     trs = [x for x in a.transports.split(",") if x]
     res = {"host": os.uname().nodename, "time": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
@@ -153,7 +159,7 @@ def main():
     try:
         for tr in trs:
             extra = [x for x in a.extra.split() if x] + (["--no-jumbo-loopback"] if tr == "std" else [])
-            t = Tunnel(f"http://127.0.0.1:{mport}", transport="webrtc", serve_extra=extra, proxy_extra=extra)
+            t = Tunnel(f"http://127.0.0.1:{mport}", transport="webrtc", serve_extra=extra, proxy_extra=extra, env=tl_env)
             t.__enter__()
             tunnels[tr] = t
         for rep in range(a.reps):
@@ -192,9 +198,12 @@ def main():
                 row[k] = summary([r[k] for r in runs])
             res["rows"].append(row)
     finally:
+        pids = {f"{tr}.{role}": getattr(t, role).popen.pid for tr, t in tunnels.items() for role in ("serve", "proxy")}
         for t in tunnels.values():
             t.__exit__(None, None, None)
         mock.stop()
+    if tl_dir:  # over each process's life; the direct runs add idle intervals only
+        res["timeline"] = timeline.summarise(tl_dir, pids)
     doc = json.dumps(res, indent=1)
     if a.out:
         with open(a.out, "w") as f:

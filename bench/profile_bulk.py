@@ -56,9 +56,9 @@ def main():
                "TUNNEL_PROFILE_HZ": os.environ.get("TUNNEL_PROFILE_HZ", "2000")}
     tl_dir = None
     if a.timeline:
-        import tempfile
-        tl_dir = tempfile.mkdtemp(prefix="p2pt-timeline-")
-        env = dict(env or {}, TUNNEL_THREAD_TIMELINE=os.path.join(tl_dir, "tl.%p.json"))
+        from p2p_llm_tunnel_amd.utils import timeline
+        tl_dir, tl_env = timeline.new_dir()
+        env = dict(env or {}, **tl_env)
     mock, port = start_mock("native", 100, 5, plan.get("mock"))
     ms, mp = free_port(), free_port()
     out = {}
@@ -110,20 +110,7 @@ def main():
         # Share of each thread's active 2 ms intervals (>= 10 % CPU) spent at
         # >= 90 % / >= 75 % CPU, over the process's life (warm-up, tunneled and
         # direct runs; the direct run adds idle intervals only).
-        names = {0: "assoc", 90: "tx_seal", 93: "tx_send", 91: "rx_lane", 92: "udp_reader"}
-        out["timeline"] = {}
-        for role, pid in out.get("pids", {}).items():
-            f = os.path.join(tl_dir, f"tl.{pid}.json")
-            if not os.path.exists(f):
-                continue
-            d = json.load(open(f))
-            for t in d["threads"]:
-                h = t["hist"]
-                busy = sum(h[1:])
-                out["timeline"][f"{role}.{names.get(t['tag'], 'worker%d' % t['tag'])}"] = {
-                    "busy_s": t["busy_s"], "active_intervals": busy,
-                    "sat90_share_of_active": round(h[5] / busy, 3) if busy else 0.0,
-                    "sat75_share_of_active": round((h[4] + h[5]) / busy, 3) if busy else 0.0}
+        out["timeline"] = timeline.summarise(tl_dir, out.get("pids", {}))
     print(json.dumps(out))
     if a.profile_dir:
         for f in sorted(glob.glob(os.path.join(a.profile_dir, "tunnel.*.prof"))):
