@@ -47,6 +47,7 @@ def main():
     a = ap.parse_args()
     extra = [x for x in a.extra.split() if x]
     serve_only = [x for x in a.serve_extra.split() if x]
+    from p2p_llm_tunnel_amd.utils import netstat
     from p2p_llm_tunnel_amd.utils.pinning import cgroup_cpu_stat, cpu_plan, cpu_stat_delta
     plan = cpu_plan() if a.pin else {}
     env = None
@@ -76,21 +77,23 @@ def main():
                 return json.loads(r.stdout.strip().splitlines()[-1])
             pids = {"serve": t.serve.popen.pid, "proxy": t.proxy.popen.pid, "mock": mock.popen.pid}
             c0 = {k: cpu_s(v) for k, v in pids.items()}
-            g0 = cgroup_cpu_stat()
+            g0, k0 = cgroup_cpu_stat(), netstat.snapshot()
             t0 = time.time()
             tr = run(t.proxy_port)
             wall = time.time() - t0
             c1 = {k: cpu_s(v) for k, v in pids.items()}
-            g1 = cgroup_cpu_stat()
+            g1, k1 = cgroup_cpu_stat(), netstat.snapshot()
             dr = run(port)
-            g2 = cgroup_cpu_stat()
+            g2, k2 = cgroup_cpu_stat(), netstat.snapshot()
             out = {"transport": a.transport, "extra": a.extra, "serve_extra": a.serve_extra, "pinned": plan, "path": t.serve.wait_for("WebRTC connection established", 1)
                    .split(" via ", 1)[-1] if a.transport == "webrtc" else "", "streams": a.streams, "body_mb": a.mb, "steps": a.steps,
                    "tunneled_req_s": tr["req_s"], "direct_req_s": dr["req_s"],
                    "tunneled_MBps_each_way": tr["req_s"] * a.mb * 1.048576, "errors": tr["errors"] + dr["errors"],
                    "wall_s_incl_warmup": round(wall, 3),
                    "cpu_s_incl_warmup": {k: round(c1[k] - c0[k], 3) for k in pids}, "pids": pids,
-                   "tunneled_cgroup": cpu_stat_delta(g0, g1), "direct_cgroup": cpu_stat_delta(g1, g2)}
+                   "tunneled_cgroup": cpu_stat_delta(g0, g1), "direct_cgroup": cpu_stat_delta(g1, g2),
+                   "kernel_tunneled": netstat.delta(k0, k1), "kernel_direct": netstat.delta(k1, k2),
+                   "tunneled_step_ms": tr.get("step_ms"), "direct_step_ms": dr.get("step_ms")}
             for name, p in (("serve", ms), ("proxy", mp)):
                 txt = urllib.request.urlopen(f"http://127.0.0.1:{p}/metrics", timeout=5).read().decode()
                 out[f"{name}_sctp"] = {l.split()[0]: float(l.split()[1]) for l in txt.splitlines()

@@ -170,6 +170,7 @@ def _pct(v, q):
 
 
 def bulk_echo(a):
+    from p2p_llm_tunnel_amd.utils import netstat
     from p2p_llm_tunnel_amd.utils.pinning import cpu_plan
     streams = a.streams if a.streams > 1 else 64
     plan = cpu_plan() if a.pin else {}
@@ -197,7 +198,9 @@ def bulk_echo(a):
                     serve_extra=extra + pin_s + ["--metrics-listen", f"127.0.0.1:{ms}"],
                     proxy_extra=extra + pin_p + ["--metrics-listen", f"127.0.0.1:{mp}"]) as t:
             path = t.serve.wait_for("WebRTC connection established", 1).split(" via ", 1)[-1] if a.transport == "webrtc" else ""
+            n0 = netstat.snapshot()
             tr = run(t.proxy_port, trace)
+            n1 = netstat.snapshot()
             # Recovery events during the run (a timer-driven retransmission
             # stalls a step by its timeout): both sides summed.
             import urllib.request
@@ -209,7 +212,9 @@ def bulk_echo(a):
                         k, v = l.split()[0], float(l.split()[1])
                         if any(x in k for x in ("retransmits", "t3_", "tlp_", "rack_marks", "overflow", "drops", "undos")):
                             counters[k] = counters.get(k, 0.0) + v
+        n2 = netstat.snapshot()
         dr = run(port)
+        n3 = netstat.snapshot()
         ev, lg = {}, {}
         with open(trace) as f:
             for line in f:
@@ -285,6 +290,7 @@ def bulk_echo(a):
            "tunneled": step_stats(tr), "direct": step_stats(dr),
            "ratio": tr["req_s"] / dr["req_s"] if dr["req_s"] else None,
            "step_waterfall_ms_median": waterfall, "slowest_steps": slowest, "recovery": counters,
+           "kernel_tunneled": netstat.delta(n0, n1), "kernel_direct": netstat.delta(n2, n3),
            "tunneled_step_ms": tr["step_ms"], "direct_step_ms": dr["step_ms"], "per_request": per_hop}
     print(json.dumps(res, indent=1))
 
