@@ -34,6 +34,9 @@ def snapshot() -> dict[str, int]:
     return out
 
 
-def delta(a: dict[str, int], b: dict[str, int]) -> dict[str, int]:
-    """b - a over KEYS (keys missing on this kernel are left out)."""
+def delta(a: dict[str, int], b: dict[str, int], everything: bool = False) -> dict[str, int]:
+    """b - a over KEYS (keys missing on this kernel are left out); with
+    everything=True, every counter that moved."""
+    if everything:
+        return {k: b[k] - a[k] for k in sorted(b) if k in a and b[k] != a[k]}
     return {k: b[k] - a[k] for k in KEYS if k in a and k in b}

@@ -267,6 +267,11 @@ def bulk_echo(a):
                 vals = [e[(role, evn)] for e in g if (role, evn) in e]
                 row[name] = (agg(vals) - t0) / 1e3 if vals else None
             row["step end at the client"] = (t1 - t0) / 1e3
+            row["new connections"] = sum(1 for e in g if ("proxy", "tcp_accept") in e)
+            # The straggler: the request whose upload ended last, every stamp
+            # it has relative to the step start (ms).
+            late = max(g, key=lambda e: e.get(("proxy", "req_end"), 0))
+            row["straggler"] = {f"{r_}.{n_}": round((v - t0) / 1e3, 3) for (r_, n_), v in sorted(late.items(), key=lambda x: x[1])}
             steps.append(row)
     else:
         for i in range(0, len(reqs) - streams + 1, streams):
@@ -278,7 +283,8 @@ def bulk_echo(a):
                 row[name] = (agg(vals) - t0) / 1e3 if vals else None
             steps.append(row)
     steps = steps[2:] if len(steps) > 4 else steps
-    waterfall = {k: statistics.median([s[k] for s in steps if s.get(k) is not None]) for k in steps[0]} if steps else {}
+    waterfall = {k: statistics.median([s[k] for s in steps if s.get(k) is not None]) for k in steps[0]
+                 if k != "straggler"} if steps else {}
     slowest = sorted(steps, key=lambda s: s.get("step end at the client") or 0)[-3:]
 
     def step_stats(r):
@@ -290,7 +296,7 @@ def bulk_echo(a):
            "tunneled": step_stats(tr), "direct": step_stats(dr),
            "ratio": tr["req_s"] / dr["req_s"] if dr["req_s"] else None,
            "step_waterfall_ms_median": waterfall, "slowest_steps": slowest, "recovery": counters,
-           "kernel_tunneled": netstat.delta(n0, n1), "kernel_direct": netstat.delta(n2, n3),
+           "kernel_tunneled": netstat.delta(n0, n1, True), "kernel_direct": netstat.delta(n2, n3, True),
            "tunneled_step_ms": tr["step_ms"], "direct_step_ms": dr["step_ms"], "per_request": per_hop}
     print(json.dumps(res, indent=1))
 
