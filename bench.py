@@ -97,14 +97,14 @@ def sync_device():
         pass
 
 
-def start_mock(kind, interval_ms, tokens, cpus=None):
+def start_mock(kind, interval_ms, tokens, cpus=None, threads=1):
     from p2p_llm_tunnel_amd import binary
     from p2p_llm_tunnel_amd.utils.procs import free_port, spawn
     port = free_port()
     pin = ["taskset", "-c", cpus] if cpus else []
     if kind == "native":
         p = spawn("mock", pin + [binary("tunnel-mock"), "--port", str(port), "--interval-ms", str(int(interval_ms)),
-                                 "--tokens", str(tokens)])
+                                 "--tokens", str(tokens), "--threads", str(threads)])
     else:
         p = spawn("mock", [sys.executable, "-m", "p2p_llm_tunnel_amd.utils.mock_llm", "--port", str(port),
                            "--threaded", "--interval-ms", str(interval_ms), "--tokens", str(tokens)])

@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--profile-dir", default=None)
     ap.add_argument("--extra", default="", help="extra flags for both tunnel processes, e.g. --no-jumbo-loopback")
     ap.add_argument("--serve-extra", default="", help="extra flags for serve only, e.g. --stream-body-threshold 65536")
+    ap.add_argument("--mock-threads", type=int, default=int(os.environ.get("P2PT_MOCK_THREADS", "1")),
+                    help="reactor threads of the echo upstream (one thread saturates at ~2500 req/s of this row)")
     ap.add_argument("--pin", action="store_true", help="pin loadgen / mock / serve / proxy to disjoint CPUs")
     ap.add_argument("--timeline", action="store_true",
                     help="per-thread CPU utilisation in 2 ms intervals (TUNNEL_THREAD_TIMELINE), summarised per thread")
@@ -60,7 +62,7 @@ def main():
         from p2p_llm_tunnel_amd.utils import timeline
         tl_dir, tl_env = timeline.new_dir()
         env = dict(env or {}, **tl_env)
-    mock, port = start_mock("native", 100, 5, plan.get("mock"))
+    mock, port = start_mock("native", 100, 5, plan.get("mock"), a.mock_threads)
     ms, mp = free_port(), free_port()
     out = {}
     try:
@@ -85,7 +87,7 @@ def main():
             g1, k1 = cgroup_cpu_stat(), netstat.snapshot()
             dr = run(port)
             g2, k2 = cgroup_cpu_stat(), netstat.snapshot()
-            out = {"transport": a.transport, "extra": a.extra, "serve_extra": a.serve_extra, "pinned": plan, "path": t.serve.wait_for("WebRTC connection established", 1)
+            out = {"transport": a.transport, "extra": a.extra, "mock_threads": a.mock_threads, "serve_extra": a.serve_extra, "pinned": plan, "path": t.serve.wait_for("WebRTC connection established", 1)
                    .split(" via ", 1)[-1] if a.transport == "webrtc" else "", "streams": a.streams, "body_mb": a.mb, "steps": a.steps,
                    "tunneled_req_s": tr["req_s"], "direct_req_s": dr["req_s"],
                    "tunneled_MBps_each_way": tr["req_s"] * a.mb * 1.048576, "errors": tr["errors"] + dr["errors"],

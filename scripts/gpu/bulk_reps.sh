@@ -6,6 +6,7 @@
 # JSON per run under gpurun_out/$TAG/; summary: python scripts/bulk_summary.py DIR.
 # PIN=1: loadgen / mock / serve / proxy on disjoint CPUs (utils/pinning.py).
 # TIMELINE=1: per-thread CPU utilisation in 2 ms intervals (which stage saturates).
+# P2PT_MOCK_THREADS=n (in VARIANTS too): reactor threads of the echo upstream (default 1).
 set -o pipefail
 TAG=${TAG:-bulk_reps}
 REPS=${REPS:-5}

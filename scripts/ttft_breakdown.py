@@ -64,6 +64,7 @@ def main():
     ap.add_argument("--mb", type=int, default=1)
     ap.add_argument("--steps", type=int, default=40, help="--bulk-echo: timed steps")
     ap.add_argument("--pin", action="store_true", help="pin loadgen / mock / serve / proxy to disjoint CPUs")
+    ap.add_argument("--mock-threads", type=int, default=1, help="--bulk-echo: reactor threads of the echo upstream")
     a = ap.parse_args()
     ensure_native()
     if a.bulk_echo:
@@ -177,7 +178,8 @@ def bulk_echo(a):
     with tempfile.NamedTemporaryFile(suffix=".jsonl", prefix="p2pt-trace-", delete=False) as tf:
         trace = tf.name
     port = free_port()
-    mock = spawn("mock", (["taskset", "-c", plan["mock"]] if plan else []) + [binary("tunnel-mock"), "--port", str(port)])
+    mock = spawn("mock", (["taskset", "-c", plan["mock"]] if plan else []) + [binary("tunnel-mock"), "--port", str(port),
+                                                                               "--threads", str(a.mock_threads)])
     mock.wait_for("Mock LLM server running", 10)
 
     def run(target, trace_file=None):
