@@ -69,6 +69,24 @@ def cpu_s(pid):
     return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
 
 
+SCRAPE = ("tunnel_sctp_packets_sent", "tunnel_frames_sent_total", "tunnel_frames_received_total",
+          "tunnel_dtls_inline_tx_batches", "tunnel_dtls_lane_tx_batches", "tunnel_dtls_lane_datagrams",
+          "tunnel_udp_gso_sends", "tunnel_udp_reader_bursts", "tunnel_udp_reader_datagrams", "tunnel_udp_reader_raw",
+          "tunnel_sctp_retransmits", "tunnel_sctp_tlp_probes")
+
+
+def scrape(port):
+    """The SCRAPE counters of one tunnel process's /metrics."""
+    import urllib.request
+    txt = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5).read().decode()
+    out = {}
+    for line in txt.splitlines():
+        parts = line.split()
+        if len(parts) == 2 and parts[0] in SCRAPE:
+            out[parts[0]] = float(parts[1])
+    return out
+
+
 def row(kind, r):
     return {f"{kind}_{k}": r[k] for k in ("events_s", "req_s", "p50_ttft_ms", "p99_ttft_ms", "p50_itl_ms",
                                            "p99_itl_ms", "p999_itl_ms", "max_itl_ms", "errors")}
@@ -137,6 +155,8 @@ def main():
     ap.add_argument("--trace", action="store_true",
                     help="stamp every request's hops (TUNNEL_TRACE, buffered) and report where the slowest 1 %% "
                          "of first tokens spent their time inside the tunnel (\"hops\" per stream count)")
+    ap.add_argument("--metrics", action="store_true",
+                    help="per tunneled run, the packet / batch / syscall counters of both tunnel processes (deltas)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     ensure_native()
@@ -164,7 +184,10 @@ def main():
             up = ",".join(f"http://127.0.0.1:{p}" for p in ports)
             if trace:
                 traces.append(trace)
-            with Tunnel(up, transport=a.transport, serve_extra=extra, proxy_extra=extra, env=env) as t:
+            mports = (free_port(), free_port()) if a.metrics else None
+            mx = (["--metrics-listen", f"127.0.0.1:{mports[0]}"], ["--metrics-listen", f"127.0.0.1:{mports[1]}"]) \
+                if mports else ([], [])
+            with Tunnel(up, transport=a.transport, serve_extra=extra + mx[0], proxy_extra=extra + mx[1], env=env) as t:
                 for s in counts:
                     loadgen([t.proxy_port], s, 1, a.lg_threads, warmup=0)
                     sid_lo = None
@@ -173,11 +196,13 @@ def main():
                         d = loadgen(ports, s, 1 << 20, a.lg_threads, extra=dur)
                         g1 = cgroup_cpu_stat()
                         c0 = (cpu_s(t.serve.popen.pid), cpu_s(t.proxy.popen.pid))
+                        m0 = (scrape(mports[0]), scrape(mports[1])) if mports else None
                         t_tr0 = time.monotonic_ns() // 1000
                         tr = loadgen([t.proxy_port], s, 1 << 20, a.lg_threads, extra=dur)
                         t_tr1 = time.monotonic_ns() // 1000
                         c1 = (cpu_s(t.serve.popen.pid), cpu_s(t.proxy.popen.pid))
                         g2 = cgroup_cpu_stat()
+                        m1 = (scrape(mports[0]), scrape(mports[1])) if mports else None
                         if trace:
                             windows.append((w, s, t_tr0, t_tr1))
                         r = {"workers": w, "streams": s, "rep": rep, **row("tunneled", tr), **row("direct", d),
@@ -189,6 +214,9 @@ def main():
                              "seconds": tr["seconds"], "direct_seconds": d["seconds"],
                              # job-wide CPU use and quota throttling during each leg
                              "direct_cgroup": cpu_stat_delta(g0, g1), "tunneled_cgroup": cpu_stat_delta(g1, g2)}
+                        if m0:
+                            for side, x0, x1 in (("serve", m0[0], m1[0]), ("proxy", m0[1], m1[1])):
+                                r[f"{side}_counters"] = {k[len("tunnel_"):]: x1[k] - x0.get(k, 0.0) for k in x1}
                         res["runs"].append(r)
                         print(json.dumps(r), file=sys.stderr, flush=True)
         keys = ["events_ratio", "tunneled_events_s", "direct_events_s", "added_p50_ttft_ms", "added_p99_ttft_ms",
