@@ -103,6 +103,7 @@ def main():
             # Loss the stack could not see and self-inflicted drops, both sides.
             out["loss"] = {k: sum(out[f"{n}_sctp"].get(m, 0.0) for n in ("serve", "proxy")) for k, m in (
                 ("udp_rx_overflow", "tunnel_udp_rx_overflow_total"), ("lane_send_drops", "tunnel_dtls_lane_send_drops"),
+                ("udp_send_drops", "tunnel_udp_send_drops"),
                 ("lane_send_waits", "tunnel_dtls_lane_send_waits"), ("reader_waits", "tunnel_udp_reader_waits"), ("reader_escapes", "tunnel_udp_reader_escapes"),
                 ("fast_retransmits", "tunnel_sctp_fast_retransmits"), ("retransmits", "tunnel_sctp_retransmits"),
                 ("t3_expirations", "tunnel_sctp_t3_expirations"), ("tlp_probes", "tunnel_sctp_tlp_probes"),

@@ -764,8 +764,10 @@ void IceAgent::flush() {
           sent++;
           continue;
         }
-        // EAGAIN (socket buffer full) or unreachable: drop; SCTP retransmits.
+        // EAGAIN (socket buffer full) or unreachable: drop (counted); SCTP
+        // retransmits.
         if (errno != EAGAIN) LOG_TRACE(kT, "sendmmsg: %s", strerror(errno));
+        send_drops_ += uint64_t(cnt - sent);
         break;
       }
       sent += rc;

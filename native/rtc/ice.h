@@ -305,6 +305,7 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   bool gro_enabled_ = false;
  public:
   uint64_t gso_sends_ = 0, gro_batches_ = 0;  // counters (metrics, tests)
+  uint64_t send_drops_ = 0;  // messages flush() dropped (EAGAIN / unreachable)
  private:
   DgVec drop_;                      // reserve_append target with no path
   friend class TurnClient;

@@ -684,6 +684,10 @@ void PeerConnection::start_sctp() {
     const uint64_t cmsg = s->rx_reader_ ? s->rx_reader_->rxq_ovfl.load() : 0;
     return double(std::max(meminfo, cmsg));
   });
+  metrics::gauge_fn("tunnel_udp_send_drops", [w] {
+    auto s = w.lock();
+    return s && s->ice_ ? double(s->ice_->send_drops_) : 0.0;
+  });
   metrics::gauge_fn("tunnel_udp_rcvbuf_bytes", [w] {
     auto s = w.lock();
     return s && s->ice_ ? double(s->ice_->rcvbuf_bytes()) : 0.0;

@@ -911,7 +911,7 @@ TEST(slow_association_thread_loses_nothing_uncounted) {
   const auto& st = off->sctp()->stats();
   const uint64_t overflow = ans->ice()->rx_overflow();
   const auto* lane = off->dtls() ? off->dtls()->tx_lane_state() : nullptr;
-  const uint64_t lane_drops = lane ? lane->send_drops.load() : 0;
+  const uint64_t lane_drops = (lane ? lane->send_drops.load() : 0) + off->ice()->send_drops_;
   const auto* rd = ans->rx_reader();
   printf("  receiver: %llu dup TSNs, %llu rwnd drops, %llu DTLS drops, %llu chunks\n",
          (unsigned long long)ans->sctp()->stats().dup_tsns, (unsigned long long)ans->sctp()->stats().rwnd_drops,

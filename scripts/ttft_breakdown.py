@@ -210,7 +210,8 @@ def bulk_echo(a):
             for p_ in (ms, mp):
                 txt = urllib.request.urlopen(f"http://127.0.0.1:{p_}/metrics", timeout=5).read().decode()
                 for l in txt.splitlines():
-                    if l.startswith(("tunnel_sctp_", "tunnel_udp_rx_overflow", "tunnel_dtls_lane_send")):
+                    if l.startswith(("tunnel_sctp_", "tunnel_udp_rx_overflow", "tunnel_udp_send_drops", "tunnel_dtls_lane_send",
+                                     "tunnel_dtls_rx_dropped")):
                         k, v = l.split()[0], float(l.split()[1])
                         if any(x in k for x in ("retransmits", "t3_", "tlp_", "rack_marks", "overflow", "drops", "undos")):
                             counters[k] = counters.get(k, 0.0) + v
