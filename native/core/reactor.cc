@@ -7,6 +7,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cstring>
 #include <stdexcept>
@@ -137,14 +138,13 @@ void Reactor::on_signal(int signo, Fn fn) {
   }
 }
 
-int Reactor::next_timeout_ms() const {
+int64_t Reactor::next_timeout_us() const {
   if (!posted_.empty()) return 0;
-  if (timer_order_.empty()) return 1000;
+  if (timer_order_.empty()) return 1000000;
   uint64_t now = now_us();
   uint64_t when = timer_order_.begin()->first;
   if (when <= now) return 0;
-  uint64_t ms = (when - now + 999) / 1000;
-  return ms > 1000 ? 1000 : int(ms);
+  return int64_t(std::min<uint64_t>(when - now, 1000000));
 }
 
 void Reactor::run_timers() {
@@ -185,9 +185,22 @@ void Reactor::run_flush() {
   flush_hooks_.resize(w);
 }
 
-void Reactor::run_once(int timeout_ms) {
+// Microsecond timeouts (epoll_pwait2): a timer due in 50 us must not sleep
+// for epoll_wait's whole millisecond.
+static int wait_events(int epfd, epoll_event* evs, int max, int64_t timeout_us) {
+  static bool pwait2 = true;
+  if (timeout_us > 0 && pwait2) {
+    timespec ts{time_t(timeout_us / 1000000), long(timeout_us % 1000000) * 1000};
+    int n = epoll_pwait2(epfd, evs, max, &ts, nullptr);
+    if (n >= 0 || errno != ENOSYS) return n;
+    pwait2 = false;
+  }
+  return epoll_wait(epfd, evs, max, timeout_us <= 0 ? 0 : int((timeout_us + 999) / 1000));
+}
+
+void Reactor::run_once(int64_t timeout_us) {
   epoll_event evs[256];
-  if (busy_poll_us_ && timeout_ms > 0 && now_us() - last_io_us_ < busy_poll_us_) timeout_ms = 0;
+  if (busy_poll_us_ && timeout_us > 0 && now_us() - last_io_us_ < busy_poll_us_) timeout_us = 0;
   const uint64_t t_wait = now_us();
   if (wake_us_) win_busy_us_ += t_wait - wake_us_;
   if (t_wait - win_start_us_ >= 2000) {
@@ -195,7 +208,7 @@ void Reactor::run_once(int timeout_ms) {
     win_start_us_ = t_wait;
     win_busy_us_ = 0;
   }
-  int n = epoll_wait(epfd_, evs, 256, timeout_ms);
+  int n = wait_events(epfd_, evs, 256, timeout_us);
   if (n < 0 && errno != EINTR) throw std::runtime_error(std::string("epoll_wait: ") + strerror(errno));
   wake_us_ = now_us();
   if (wake_us_ - win_start_us_ >= 2000 && win_start_us_) {  // a long sleep ends the window idle
@@ -245,20 +258,20 @@ void Reactor::run() {
   Reactor* prev = t_current;
   t_current = this;
   stop_ = false;
-  while (!stop_) run_once(next_timeout_ms());
+  while (!stop_) run_once(next_timeout_us());
   t_current = prev;
 }
 
 bool Reactor::run_until(const std::function<bool()>& pred, uint64_t timeout_ms) {
   Reactor* prev = t_current;
   t_current = this;
-  uint64_t deadline = now_ms() + timeout_ms;
+  uint64_t deadline = now_us() + timeout_ms * 1000;
   stop_ = false;
   while (!stop_ && !pred()) {
-    uint64_t now = now_ms();
+    uint64_t now = now_us();
     if (now >= deadline) break;
-    int t = next_timeout_ms();
-    int left = int(deadline - now);
+    int64_t t = next_timeout_us();
+    int64_t left = int64_t(deadline - now);
     run_once(t < left ? t : left);
   }
   t_current = prev;

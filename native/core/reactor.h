@@ -78,8 +78,8 @@ class Reactor {
   static uint64_t now_ms() { return now_us() / 1000; }
 
  private:
-  void run_once(int timeout_ms);
-  int next_timeout_ms() const;
+  void run_once(int64_t timeout_us);
+  int64_t next_timeout_us() const;
   void run_timers();
   void run_posted();
   void run_flush();

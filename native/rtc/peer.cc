@@ -206,7 +206,12 @@ std::shared_ptr<PeerConnection> PeerConnection::create(Reactor& r, PcConfig cfg,
 }
 
 PeerConnection::PeerConnection(Reactor& r, PcConfig cfg, bool offerer)
-    : r_(r), cfg_(std::move(cfg)), offerer_(offerer), mtu_(cfg_.sctp_mtu) {}
+    : r_(r), cfg_(std::move(cfg)), offerer_(offerer), mtu_(cfg_.sctp_mtu) {
+  const char* e = getenv("TUNNEL_COALESCE_US");
+  coalesce_us_ = cfg_.coalesce_us ? cfg_.coalesce_us : (e && *e ? strtoull(e, nullptr, 10) : 0);
+  const char* l = getenv("TUNNEL_COALESCE_LOAD_PCT");
+  coalesce_load_ = cfg_.coalesce_load >= 0 ? cfg_.coalesce_load : (l && *l ? double(strtoull(l, nullptr, 10)) / 100.0 : 0.5);
+}
 
 PeerConnection::~PeerConnection() { close(); }
 
@@ -217,6 +222,24 @@ void PeerConnection::flush() {
   // new pair's instead of forwarding everything through the slow path.
   if (rx_reader_ && ice_ && ice_->path_generation() != rx_reader_gen_) restart_rx_reader();
   if (dtls_) dtls_->commit_rx();
+  if (sctp_ && coalesce_us_) {
+    // A busy loop with a partial packet queued: let the next pass (or the
+    // timer, at most coalesce_us after the previous flush) add to it.
+    const uint64_t now = Reactor::now_us();
+    const size_t q = sctp_->buffered_amount();
+    if (q > 0 && q < mtu_ && now - last_flush_us_ < coalesce_us_ && r_.load() >= coalesce_load_) {
+      coalesced_flushes_++;
+      if (!coalesce_timer_) {
+        std::weak_ptr<PeerConnection> w = shared_from_this();
+        coalesce_timer_ = r_.call_at(last_flush_us_ + coalesce_us_, [w] {
+          if (auto s = w.lock()) s->coalesce_timer_ = 0;  // the flush hook runs after timers
+        });
+      }
+      if (ice_) ice_->flush();
+      return;
+    }
+    last_flush_us_ = now;
+  }
   if (sctp_) sctp_->flush();
   if (dtls_) dtls_->commit_tx();
   if (ice_) ice_->flush();
@@ -288,6 +311,8 @@ void PeerConnection::close() {
     if (ice_) ice_->flush();
   }
   closed_ = true;
+  if (coalesce_timer_) r_.cancel(coalesce_timer_);
+  coalesce_timer_ = 0;
   rx_reader_.reset();  // joins the reader; bursts already posted find closed_ set
   if (flush_hook_) r_.remove_flush_hook(flush_hook_);
   flush_hook_ = 0;
@@ -683,6 +708,10 @@ void PeerConnection::start_sctp() {
     const uint64_t meminfo = s->ice_->rx_overflow();
     const uint64_t cmsg = s->rx_reader_ ? s->rx_reader_->rxq_ovfl.load() : 0;
     return double(std::max(meminfo, cmsg));
+  });
+  metrics::gauge_fn("tunnel_sctp_coalesced_flushes", [w] {
+    auto s = w.lock();
+    return s ? double(s->coalesced_flushes_) : 0.0;
   });
   metrics::gauge_fn("tunnel_udp_send_drops", [w] {
     auto s = w.lock();

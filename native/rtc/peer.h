@@ -47,6 +47,14 @@ struct PcConfig {
   // Fragmented messages handed to chain consumers as views of their packets
   // instead of one reassembled copy (also TUNNEL_SCTP_CHAIN=1).
   bool message_chains = false;
+  // Flush coalescing on a busy loop: while the association loop is at least
+  // `coalesce_load` busy (Reactor::load) and less than one packet of data is
+  // queued, the SCTP flush waits up to `coalesce_us` after the previous one,
+  // so token-sized frames of many streams share packets (and sendmmsg calls,
+  // reader wake-ups and SACKs on the far side). 0 = off; also
+  // TUNNEL_COALESCE_US / TUNNEL_COALESCE_LOAD_PCT.
+  uint64_t coalesce_us = 0;
+  double coalesce_load = -1;  // < 0: TUNNEL_COALESCE_LOAD_PCT or 0.5
 };
 
 class PeerConnection;
@@ -113,6 +121,7 @@ class PeerConnection : public std::enable_shared_from_this<PeerConnection> {
   std::string describe_path() const;
   const SctpStats* sctp_stats() const { return sctp_ ? &sctp_->stats() : nullptr; }
   size_t sctp_mtu() const { return mtu_; }
+  uint64_t coalesced_flushes() const { return coalesced_flushes_; }
   const DtlsTransport* dtls() const { return dtls_.get(); }
   IceAgent* ice() const { return ice_.get(); }
   const SctpAssociation* sctp() const { return sctp_.get(); }
@@ -151,6 +160,11 @@ class PeerConnection : public std::enable_shared_from_this<PeerConnection> {
   uint16_t next_stream_ = 0;
   uint64_t flush_hook_ = 0;
   size_t mtu_ = 1200;
+  uint64_t coalesce_us_ = 0;
+  double coalesce_load_ = 0.5;
+  uint64_t last_flush_us_ = 0;
+  uint64_t coalesce_timer_ = 0;
+  uint64_t coalesced_flushes_ = 0;  // flushes held back (metrics, tests)
   bool closed_ = false;
   // The selected direct pair's socket read off this thread (rtc/datapath.h).
   std::unique_ptr<RxReader> rx_reader_;

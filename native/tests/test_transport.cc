@@ -943,6 +943,74 @@ TEST(slow_association_thread_loses_nothing_uncounted) {
   unsetenv("TUNNEL_RX_ESCAPE");
 }
 
+// Flush coalescing: small messages queued one per loop pass share packets
+// when coalescing is on (load threshold 0: always while a packet is partial),
+// arrive complete and in order, and leave in about one packet per pass when
+// it is off.
+static void coalesce_run(uint64_t coalesce_us, uint64_t* packets, uint64_t* held, size_t* got_out, bool* order) {
+  Reactor r;
+  PcConfig cfg;
+  cfg.ice.include_loopback = true;
+  cfg.allow_jumbo = false;
+  cfg.coalesce_us = coalesce_us;
+  cfg.coalesce_load = 0;
+  auto off = PeerConnection::create(r, cfg, true);
+  auto ans = PeerConnection::create(r, cfg, false);
+  off->on_ice_candidate = [&](const std::string& c) { ans->add_ice_candidate(c, nullptr); };
+  ans->on_ice_candidate = [&](const std::string& c) { off->add_ice_candidate(c, nullptr); };
+  auto dc = off->create_data_channel("tunnel");
+  std::shared_ptr<DataChannel> rdc;
+  size_t got = 0;
+  bool ok = true;
+  ans->on_data_channel = [&](std::shared_ptr<DataChannel> d) {
+    rdc = d;
+    d->on_message = [&](Bytes m) {
+      ok &= m.size() == 5 + 40 && rd32(m.data() + 1) == uint32_t(got + 1);
+      got++;
+    };
+  };
+  off->start_gathering();
+  ans->start_gathering();
+  CHECK(r.run_until([&] { return off->gathering_complete(); }, 3000));
+  std::string err;
+  CHECK(ans->set_remote_description(off->local_description(), &err));
+  CHECK(off->set_remote_description(ans->local_description(), &err));
+  CHECK(r.run_until([&] { return dc->is_open() && rdc && rdc->is_open(); }, 5000));
+  const int n = 2000;
+  const uint64_t p0 = off->sctp()->stats().packets_sent;
+  Bytes body = Bytes::copy(std::string(40, 't'));
+  int sent = 0;
+  std::function<void()> tick = [&] {  // one message per loop pass
+    uint8_t hdr[5] = {21, 0, 0, 0, 0};
+    wr32(hdr + 1, uint32_t(++sent));
+    dc->send(hdr, 5, body);
+    if (sent < n) r.post_threadsafe(tick);
+  };
+  r.post_threadsafe(tick);
+  CHECK(r.run_until([&] { return got == size_t(n); }, 20000));
+  *packets = off->sctp()->stats().packets_sent - p0;
+  *held = off->coalesced_flushes();
+  *got_out = got;
+  *order = ok;
+}
+
+TEST(busy_loop_flushes_coalesce_small_messages) {
+  if (!AesGcm::supported()) return;
+  uint64_t pk_off = 0, held_off = 0, pk_on = 0, held_on = 0;
+  size_t got_off = 0, got_on = 0;
+  bool ok_off = false, ok_on = false;
+  coalesce_run(0, &pk_off, &held_off, &got_off, &ok_off);
+  coalesce_run(200, &pk_on, &held_on, &got_on, &ok_on);
+  printf("  2000 x 45 B, one per pass: %llu packets without coalescing, %llu with (%llu flushes held)\n",
+         (unsigned long long)pk_off, (unsigned long long)pk_on, (unsigned long long)held_on);
+  CHECK_EQ(got_off, size_t(2000));
+  CHECK_EQ(got_on, size_t(2000));
+  CHECK(ok_off && ok_on);
+  CHECK_EQ(held_off, uint64_t(0));
+  CHECK(held_on > 0);
+  CHECK(pk_on * 3 < pk_off);
+}
+
 // Zero-copy reassembly: a consumer that takes chains (the tunnel sessions)
 // gets a fragmented message as views of its fragments, in order, byte for
 // byte what was sent; a message that fits one chunk still arrives whole.

@@ -1,0 +1,14 @@
+# Round 4, fourteenth host batch: flush coalescing on a busy association loop
+# (TUNNEL_COALESCE_US: while the loop is >= 50 % busy and less than a packet
+# is queued, the SCTP flush waits up to that long after the previous one), on
+# the node row. At 1024 streams the serve sent 105 k packets/s of ~7 tokens,
+# one sendmmsg each (profiles/r04/node13).
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r04/node14
+echo "== node 1024"; NODE_EXTRA=--metrics STREAMS=1024 REPS=3 VARIANTS="off: c50:TUNNEL_COALESCE_US=50 c200:TUNNEL_COALESCE_US=200" \
+  timeout -k 10 700 bash scripts/gpu/node_env_ab.sh > gpurun_out/r04/node14/s1024.log 2>&1; rc=$?; grep -v "^{\\|^ \\|^}\\|^\\]" gpurun_out/r04/node14/s1024.log | tail -9; [ $rc -eq 0 ] || exit $rc
+mv gpurun_out/node_ab gpurun_out/r04/node14/s1024
+echo "== node 256"; NODE_EXTRA=--metrics STREAMS=256 REPS=2 VARIANTS="off: c50:TUNNEL_COALESCE_US=50 c200:TUNNEL_COALESCE_US=200" \
+  timeout -k 10 500 bash scripts/gpu/node_env_ab.sh > gpurun_out/r04/node14/s256.log 2>&1; rc=$?; grep -v "^{\\|^ \\|^}\\|^\\]" gpurun_out/r04/node14/s256.log | tail -6; [ $rc -eq 0 ] || exit $rc
+mv gpurun_out/node_ab gpurun_out/r04/node14/s256
