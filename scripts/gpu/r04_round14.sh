@@ -2,7 +2,8 @@
 # (TUNNEL_COALESCE_US: while the loop is >= 50 % busy and less than a packet
 # is queued, the SCTP flush waits up to that long after the previous one), on
 # the node row. At 1024 streams the serve sent 105 k packets/s of ~7 tokens,
-# one sendmmsg each (profiles/r04/node13).
+# one sendmmsg each (profiles/r04/node13). Then cut-through uploads again (the
+# 1-thread echo upstream bounds the direct leg; store-and-forward leaves it idle).
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r04/node14
@@ -12,3 +13,6 @@ mv gpurun_out/node_ab gpurun_out/r04/node14/s1024
 echo "== node 256"; NODE_EXTRA=--metrics STREAMS=256 REPS=2 VARIANTS="off: c50:TUNNEL_COALESCE_US=50 c200:TUNNEL_COALESCE_US=200" \
   timeout -k 10 500 bash scripts/gpu/node_env_ab.sh > gpurun_out/r04/node14/s256.log 2>&1; rc=$?; grep -v "^{\\|^ \\|^}\\|^\\]" gpurun_out/r04/node14/s256.log | tail -6; [ $rc -eq 0 ] || exit $rc
 mv gpurun_out/node_ab gpurun_out/r04/node14/s256
+echo "== cut-through A/B"; TAG=r04/ct14 PIN=1 REPS=2 PATHS="std jumbo" \
+  VARIANTS="sf:build: ct:build:TUNNEL_STREAM_BODY_THRESHOLD=65536" \
+  timeout -k 10 600 bash scripts/gpu/bulk_reps.sh > gpurun_out/r04/ct14.log 2>&1; rc=$?; tail -4 gpurun_out/r04/ct14.log; exit $rc
