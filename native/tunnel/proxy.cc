@@ -189,6 +189,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     send_credit_ += n;
     if (credit_paused_ && send_credit_ > 0) {
       credit_paused_ = false;
+      if (trace::enabled()) waits_.end(0);
       update_reading();
       if (conn_ && !inbuf_.empty()) process();
     }
@@ -226,10 +227,12 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
   // Per-stream back-pressure from the session: this upload's frames pile up.
   void flow_pause() {
     flow_paused_ = true;
+    if (trace::enabled()) waits_.begin(1);
     update_reading();
   }
   void flow_resume() {
     flow_paused_ = false;
+    if (trace::enabled()) waits_.end(1);
     update_reading();
     if (conn_ && !inbuf_.empty()) process();
   }
@@ -415,6 +418,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     }
     if (flow && send_credit_ <= 0 && !credit_paused_) {  // wait for serve's credit
       credit_paused_ = true;
+      if (trace::enabled()) waits_.begin(0);
       update_reading();
     }
     return false;
@@ -433,6 +437,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     if (!discard_body_) {
       sess->send(proto::make_empty(proto::MsgType::ReqEnd, sid_));
       trace::event("proxy", sid_, "req_end");
+      if (trace::enabled()) waits_.emit(sid_);
     }
     if (state_ == State::ReadingBody) state_ = head_written_ ? State::Responding : State::Awaiting;
     if (!head_written_) {
@@ -641,6 +646,32 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
   bool reject_not_ready_ = false;
   bool flow_paused_ = false;
   bool credit_paused_ = false;   // "flow": upload out of serve's credit
+  // TUNNEL_TRACE: the longest wait of this upload for serve's credit (0) and
+  // for the session's per-stream back-pressure (1), stamped at req_end as
+  // credit_wait/credit_go and flow_wait/flow_go.
+  struct Waits {
+    uint64_t start[2] = {0, 0}, best_from[2] = {0, 0}, best_to[2] = {0, 0};
+    void begin(int k) { start[k] = Reactor::now_us(); }
+    void end(int k) {
+      if (!start[k]) return;
+      const uint64_t now = Reactor::now_us();
+      if (now - start[k] > best_to[k] - best_from[k]) {
+        best_from[k] = start[k];
+        best_to[k] = now;
+      }
+      start[k] = 0;
+    }
+    void emit(uint32_t sid) {
+      static const char* names[2][2] = {{"credit_wait", "credit_go"}, {"flow_wait", "flow_go"}};
+      for (int k = 0; k < 2; k++) {
+        if (best_to[k]) {
+          trace::event_at("proxy", sid, names[k][0], best_from[k]);
+          trace::event_at("proxy", sid, names[k][1], best_to[k]);
+        }
+      }
+      *this = Waits{};
+    }
+  } waits_;
   int64_t send_credit_ = proto::flow_window();
   uint64_t owed_ = 0;            // "flow": RES_BODY bytes delivered, not yet granted back
   proto::FlowWindow rwin_;       // "flow": RES_BODY window autotuning

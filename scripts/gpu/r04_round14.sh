@@ -15,4 +15,9 @@ echo "== node 256"; NODE_EXTRA=--metrics STREAMS=256 REPS=2 VARIANTS="off: c50:T
 mv gpurun_out/node_ab gpurun_out/r04/node14/s256
 echo "== cut-through A/B"; TAG=r04/ct14 PIN=1 REPS=2 PATHS="std jumbo" \
   VARIANTS="sf:build: ct:build:TUNNEL_STREAM_BODY_THRESHOLD=65536" \
-  timeout -k 10 600 bash scripts/gpu/bulk_reps.sh > gpurun_out/r04/ct14.log 2>&1; rc=$?; tail -4 gpurun_out/r04/ct14.log; exit $rc
+  timeout -k 10 600 bash scripts/gpu/bulk_reps.sh > gpurun_out/r04/ct14.log 2>&1; rc=$?; tail -4 gpurun_out/r04/ct14.log; [ $rc -eq 0 ] || exit $rc
+echo "== wf std (credit / flow wait stamps)"; mkdir -p gpurun_out/r04/wf14
+timeout -k 10 200 python scripts/ttft_breakdown.py --bulk-echo --steps 100 --pin --extra=--no-jumbo-loopback > gpurun_out/r04/wf14/std.json 2> gpurun_out/r04/wf14/std.err || exit 1
+python -c "
+import json; d=json.load(open('gpurun_out/r04/wf14/std.json')); print(d['tunneled'], d['direct'], round(d['ratio'],3))
+for s in d['slowest_steps']: print(s['step end at the client'], s['new connections'], s['straggler'])"
