@@ -1,7 +1,7 @@
 # Decode attention grid sweep at HEAD: wall-clock of the device-side decode
 # loop (small, ctx 1024) under the attention grid knobs, 2 interleaved
 # repetitions. Each case: "batch ENV=VAL ...".
-#   bash scripts/gpu/attn_grid_sweep.sh
+#   bash scripts/gpu/archive/attn_grid_sweep.sh
 set -o pipefail
 mkdir -p gpurun_out
 CASES=(

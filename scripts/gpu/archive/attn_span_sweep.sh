@@ -1,6 +1,6 @@
 # Decode attention span sweep at HEAD: wall-clock of the device-side decode
 # loop (small, ctx 1024) under P2PT_ATTN_MINSPAN, 2 interleaved repetitions.
-#   bash scripts/gpu/attn_span_sweep.sh
+#   bash scripts/gpu/archive/attn_span_sweep.sh
 set -o pipefail
 mkdir -p gpurun_out
 for rep in 1 2; do

@@ -1,7 +1,7 @@
 # A/B of the decode attention piece size (P2PT_ATTN_TOK 32 vs 16: 16 halves
 # the K/V registers so two 8-wave workgroups fit a CU), numerics first, then
 # wall-clock of the device-side decode loop (small, ctx 1024), interleaved.
-#   bash scripts/gpu/attn_tok_ab.sh
+#   bash scripts/gpu/archive/attn_tok_ab.sh
 set -o pipefail
 mkdir -p gpurun_out
 P2PT_ATTN_TOK=16 timeout -k 10 300 python -u -m pytest tests/test_gpu_model.py -x -q -m gpu --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_attn_tok16.log 2>&1; rc=$?; tail -2 gpurun_out/pytest_attn_tok16.log; [ $rc -eq 0 ] || exit $rc

@@ -1,6 +1,6 @@
 # Interleaved wall-clock A/B of two in-tree builds of the HIP kernels (and env
 # variants) on one box: scripts/profile_decode.py --loop, 3 rounds each.
-#   bash scripts/gpu/decode_ab.sh TAG "label|LIB|ENV..." ...   (LIB: file under ops/)
+#   bash scripts/gpu/archive/decode_ab.sh TAG "label|LIB|ENV..." ...   (LIB: file under ops/)
 set -o pipefail
 mkdir -p gpurun_out
 TAG=$1; shift

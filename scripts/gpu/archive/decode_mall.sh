@@ -5,7 +5,7 @@
 # 2) Prefetch workgroups (P2PT_DECODE_PF bit mask, decode_fused.hip
 #    prefetch_range): wall-clock loops per mask at batch 1 and 16, then a
 #    kernel trace of mask $PFT.
-#   bash scripts/gpu/decode_mall.sh [TAG]
+#   bash scripts/gpu/archive/decode_mall.sh [TAG]
 set -o pipefail
 mkdir -p gpurun_out/decode_mall
 export TMPDIR=/tmp

@@ -1,6 +1,6 @@
 # Per-position kernel timing of the fused decode step (rocprofv3 kernel trace):
 # small config at batch 1 and 16, tiny at batch 1, plus wall-clock tokens/s.
-#   bash scripts/gpu/decode_steps.sh [TAG]
+#   bash scripts/gpu/archive/decode_steps.sh [TAG]
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -2,7 +2,7 @@
 # of the device-side decode loop (scripts/profile_decode.py --loop) under the
 # kernel tunables (P2PT_DECODE_MIN_TILES, P2PT_ATTN_MINSPAN, P2PT_ATTN_SLOTS),
 # then a per-position rocprofv3 kernel trace of the default settings.
-#   bash scripts/gpu/decode_sweep.sh TAG
+#   bash scripts/gpu/archive/decode_sweep.sh TAG
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -11,7 +11,7 @@ export TMPDIR=/tmp
 V=""
 for x in $VARS; do V="$V ${x%%:*}:build:${x#*:}"; done
 if [ -z "$SKIP_BULK" ]; then
-  TAG=$TAG/bulk REPS=${REPS:-3} STEPS=${STEPS:-150} VARIANTS="$V" bash scripts/gpu/bulk_reps.sh || exit 1
+  TAG=$TAG/bulk REPS=${REPS:-3} STEPS=${STEPS:-150} VARIANTS="$V" bash scripts/gpu/archive/bulk_reps.sh || exit 1
 fi
 for x in $VARS; do
   l=${x%%:*}; e=${x#*:}

@@ -1,6 +1,6 @@
 # Node row (1 serve over 8 mocks, 1 ms tokens) A/B of tunnel environments at
 # one stream count, interleaved per repetition. VARIANTS="label:VAR=v,VAR2=w ...".
-#   STREAMS=256 REPS=3 VARIANTS="dflt: old:TUNNEL_SCHED_BYPASS=0" bash scripts/gpu/node_env_ab.sh
+#   STREAMS=256 REPS=3 VARIANTS="dflt: old:TUNNEL_SCHED_BYPASS=0" bash scripts/gpu/archive/node_env_ab.sh
 # NODE_EXTRA="--metrics" adds bench_node flags (packet / batch counters per run).
 set -o pipefail
 mkdir -p gpurun_out/node_ab

@@ -4,4 +4,4 @@
 set -o pipefail
 export TMPDIR=/tmp
 TAG=${TAG:-r04/bulk_ct} PIN=1 REPS=${REPS:-4} VARIANTS="sf:build: ct:build:TUNNEL_STREAM_BODY_THRESHOLD=65536" \
-  timeout -k 10 1000 bash scripts/gpu/bulk_reps.sh
+  timeout -k 10 1000 bash scripts/gpu/archive/bulk_reps.sh

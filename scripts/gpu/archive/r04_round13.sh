@@ -16,4 +16,4 @@ for r in d["runs"]:
 PY
 echo "== mock threads A/B"; TAG=r04/mock_ab PIN=1 TIMELINE=1 REPS=3 PATHS="std jumbo" \
   VARIANTS="m1:build:P2PT_MOCK_THREADS=1 m2:build:P2PT_MOCK_THREADS=2" \
-  timeout -k 10 900 bash scripts/gpu/bulk_reps.sh > gpurun_out/r04/mock_ab.log 2>&1; rc=$?; tail -4 gpurun_out/r04/mock_ab.log; exit $rc
+  timeout -k 10 900 bash scripts/gpu/archive/bulk_reps.sh > gpurun_out/r04/mock_ab.log 2>&1; rc=$?; tail -4 gpurun_out/r04/mock_ab.log; exit $rc

@@ -12,5 +12,5 @@ for i in 1 2; do
 done
 echo "== pipeline A/B + timeline"; TAG=r04/pipe_ab PIN=1 TIMELINE=1 REPS=2 PATHS="std jumbo" \
   VARIANTS="pipe:build: lane:build:TUNNEL_TX_PIPELINE=0" \
-  timeout -k 10 700 bash scripts/gpu/bulk_reps.sh > gpurun_out/r04/pipe_ab.log 2>&1; rc=$?; tail -4 gpurun_out/r04/pipe_ab.log; [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 700 bash scripts/gpu/archive/bulk_reps.sh > gpurun_out/r04/pipe_ab.log 2>&1; rc=$?; tail -4 gpurun_out/r04/pipe_ab.log; [ $rc -eq 0 ] || exit $rc
 echo "== mixed"; timeout -k 10 300 python bench/bench_mixed.py --seconds 10 --reps 2 --mock-threads 8 --out gpurun_out/r04/mixed7.json > /dev/null 2> gpurun_out/r04/mixed7.err; rc=$?; tail -2 gpurun_out/r04/mixed7.err; exit $rc

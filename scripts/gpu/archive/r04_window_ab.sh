@@ -6,4 +6,4 @@ set -o pipefail
 export TMPDIR=/tmp
 TAG=${TAG:-r04/window_ab} PIN=1 REPS=${REPS:-3} PATHS=${PATHS:-std} STEPS=${STEPS:-150} \
   VARIANTS="f1:build:TUNNEL_STREAM_BODY_THRESHOLD=65536 f2:build:TUNNEL_STREAM_BODY_THRESHOLD=65536,TUNNEL_SCTP_QUEUE_FLOOR_KB=2048 f4:build:TUNNEL_STREAM_BODY_THRESHOLD=65536,TUNNEL_SCTP_QUEUE_FLOOR_KB=4096 qoff:build:TUNNEL_STREAM_BODY_THRESHOLD=65536,TUNNEL_SCTP_QUEUE_US=0" \
-  timeout -k 10 1000 bash scripts/gpu/bulk_reps.sh
+  timeout -k 10 1000 bash scripts/gpu/archive/bulk_reps.sh
