@@ -108,7 +108,7 @@ def main():
                 ("fast_retransmits", "tunnel_sctp_fast_retransmits"), ("retransmits", "tunnel_sctp_retransmits"),
                 ("t3_expirations", "tunnel_sctp_t3_expirations"), ("tlp_probes", "tunnel_sctp_tlp_probes"),
                 ("rack_marks", "tunnel_sctp_rack_marks"), ("spurious_undos", "tunnel_sctp_spurious_undos"),
-                ("probe_ambiguous", "tunnel_sctp_probe_ambiguous"), ("dup_tsns_received", "tunnel_sctp_dup_tsns_received"),
+                ("probe_ambiguous", "tunnel_sctp_probe_ambiguous"), ("dup_tsns_received", "tunnel_sctp_dup_tsns_received"), ("late_tsns_received", "tunnel_sctp_late_tsns_received"),
                 ("rwnd_drops", "tunnel_sctp_rwnd_drops"), ("dtls_rx_dropped", "tunnel_dtls_rx_dropped"))}
     finally:
         mock.stop()

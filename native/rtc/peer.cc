@@ -617,6 +617,10 @@ void PeerConnection::start_sctp() {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().dup_tsns) : 0.0;
   });
+  metrics::gauge_fn("tunnel_sctp_late_tsns_received", [w] {
+    auto s = w.lock();
+    return s && s->sctp_ ? double(s->sctp_->stats().late_tsns) : 0.0;
+  });
   metrics::gauge_fn("tunnel_sctp_rwnd_drops", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().rwnd_drops) : 0.0;

@@ -753,6 +753,14 @@ void SctpAssociation::handle_data(uint8_t flags, const uint8_t* c, size_t len, c
   stats_.bytes_received += dlen;
   sack_needed_ = true;
   int32_t d = int32_t(tsn - peer_cum_tsn_);
+  // Arrivals below the highest TSN seen: retransmissions filling holes, or
+  // packets the path (or this stack) reordered — more of them than the peer
+  // retransmitted means reordering.
+  if (have_rx_high_ && d > 0 && tsn_lt(tsn, rx_high_tsn_)) stats_.late_tsns++;
+  if (!have_rx_high_ || tsn_lt(rx_high_tsn_, tsn)) {
+    rx_high_tsn_ = tsn;
+    have_rx_high_ = true;
+  }
   if (d <= 0) {
     stats_.dup_tsns++;
     if (dups_.size() < 32) dups_.push_back(tsn);

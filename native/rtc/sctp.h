@@ -55,6 +55,7 @@ struct SctpConfig {
 struct SctpStats {
   uint64_t packets_sent = 0, packets_received = 0;
   uint64_t data_chunks_sent = 0, data_chunks_received = 0;
+  uint64_t late_tsns = 0;  // new TSNs that arrived below the highest one seen (holes filled, reordering)
   uint64_t retransmits = 0, fast_retransmits = 0, t3_expirations = 0;
   uint64_t tlp_probes = 0, rack_marks = 0, random_loss_events = 0;
   uint64_t random_loss_cuts = 0;  // random-loss episodes that cut cwnd (TUNNEL_SCTP_RANDOM_BETA_PCT)
@@ -314,6 +315,8 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   bool peer_zero_checksum_ = false;  // peer advertised RFC 9653 EDMID 1
   bool have_peer_tsn_ = false;
   uint32_t peer_cum_tsn_ = 0;  // highest in-order TSN received
+  uint32_t rx_high_tsn_ = 0;   // highest TSN received (stats: late arrivals)
+  bool have_rx_high_ = false;
   std::map<uint32_t, InChunk*> ooo_;  // out-of-order (by TSN, serial order via custom cmp)
   size_t ooo_bytes_ = 0;
   std::vector<uint32_t> dups_;

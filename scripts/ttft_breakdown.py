@@ -213,7 +213,8 @@ def bulk_echo(a):
                     if l.startswith(("tunnel_sctp_", "tunnel_udp_rx_overflow", "tunnel_udp_send_drops", "tunnel_dtls_lane_send",
                                      "tunnel_dtls_rx_dropped")):
                         k, v = l.split()[0], float(l.split()[1])
-                        if any(x in k for x in ("retransmits", "t3_", "tlp_", "rack_marks", "overflow", "drops", "undos")):
+                        if any(x in k for x in ("retransmits", "t3_", "tlp_", "rack_marks", "overflow", "drops", "undos", "late_tsns",
+                                                    "dup_tsns", "rx_dropped")):
                             counters[k] = counters.get(k, 0.0) + v
         n2 = netstat.snapshot()
         dr = run(port)
