@@ -208,7 +208,7 @@ std::shared_ptr<PeerConnection> PeerConnection::create(Reactor& r, PcConfig cfg,
 PeerConnection::PeerConnection(Reactor& r, PcConfig cfg, bool offerer)
     : r_(r), cfg_(std::move(cfg)), offerer_(offerer), mtu_(cfg_.sctp_mtu) {
   const char* e = getenv("TUNNEL_COALESCE_US");
-  coalesce_us_ = cfg_.coalesce_us ? cfg_.coalesce_us : (e && *e ? strtoull(e, nullptr, 10) : 0);
+  coalesce_us_ = cfg_.coalesce_us >= 0 ? uint64_t(cfg_.coalesce_us) : (e && *e ? strtoull(e, nullptr, 10) : 50);
   const char* l = getenv("TUNNEL_COALESCE_LOAD_PCT");
   coalesce_load_ = cfg_.coalesce_load >= 0 ? cfg_.coalesce_load : (l && *l ? double(strtoull(l, nullptr, 10)) / 100.0 : 0.5);
 }

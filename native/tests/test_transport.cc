@@ -947,7 +947,7 @@ TEST(slow_association_thread_loses_nothing_uncounted) {
 // when coalescing is on (load threshold 0: always while a packet is partial),
 // arrive complete and in order, and leave in about one packet per pass when
 // it is off.
-static void coalesce_run(uint64_t coalesce_us, uint64_t* packets, uint64_t* held, size_t* got_out, bool* order) {
+static void coalesce_run(int64_t coalesce_us, uint64_t* packets, uint64_t* held, size_t* got_out, bool* order) {
   Reactor r;
   PcConfig cfg;
   cfg.ice.include_loopback = true;
