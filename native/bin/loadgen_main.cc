@@ -71,6 +71,30 @@ struct Result {
   uint64_t t_start = 0, t_end = 0;
 };
 
+// LOADGEN_TRACE=path: step boundaries of thread 0 as JSON lines in the
+// tunnel's trace format (CLOCK_MONOTONIC us), so a waterfall can place the
+// tunnel's per-request stamps inside the client's steps.
+FILE* step_trace() {
+  static FILE* f = [] () -> FILE* {
+    const char* p = getenv("LOADGEN_TRACE");
+    FILE* o = p && *p ? fopen(p, "a") : nullptr;
+    if (o) setvbuf(o, nullptr, _IOLBF, 1 << 16);  // whole lines per write: the tunnel appends to the same file
+    return o;
+  }();
+  return f;
+}
+
+void trace_step(int first, int step, const char* ev) {
+  FILE* f = step_trace();
+  if (!f || first != 0) return;
+  fprintf(f, "{\"t_us\":%llu,\"role\":\"loadgen\",\"sid\":%d,\"ev\":\"%s\"}\n",
+          static_cast<unsigned long long>(Reactor::now_us()), step, ev);
+}
+
+// The step thread 0 is in (for connection stamps: a step that opens new
+// connections records when the last of them completed, as "connected").
+std::atomic<int> g_step{0};
+
 class Stream : public std::enable_shared_from_this<Stream> {
  public:
   Stream(Reactor& r, const Opts& o, const Target& t, Result* res) : r_(r), o_(o), t_(t), res_(res) {}
@@ -87,6 +111,7 @@ class Stream : public std::enable_shared_from_this<Stream> {
           return;
         }
         self->conn_ = c;
+        trace_step(0, g_step.load(std::memory_order_relaxed), "connected");
         std::weak_ptr<Stream> w = self;
         c->on_data([w](const uint8_t* p, size_t n) {
           if (auto s = w.lock()) s->on_data(p, n);
@@ -282,26 +307,6 @@ class Stream : public std::enable_shared_from_this<Stream> {
   int sep_run_ = 0;
 };
 
-// LOADGEN_TRACE=path: step boundaries of thread 0 as JSON lines in the
-// tunnel's trace format (CLOCK_MONOTONIC us), so a waterfall can place the
-// tunnel's per-request stamps inside the client's steps.
-FILE* step_trace() {
-  static FILE* f = [] () -> FILE* {
-    const char* p = getenv("LOADGEN_TRACE");
-    FILE* o = p && *p ? fopen(p, "a") : nullptr;
-    if (o) setvbuf(o, nullptr, _IOLBF, 1 << 16);  // whole lines per write: the tunnel appends to the same file
-    return o;
-  }();
-  return f;
-}
-
-void trace_step(int first, int step, const char* ev) {
-  FILE* f = step_trace();
-  if (!f || first != 0) return;
-  fprintf(f, "{\"t_us\":%llu,\"role\":\"loadgen\",\"sid\":%d,\"ev\":\"%s\"}\n",
-          static_cast<unsigned long long>(Reactor::now_us()), step, ev);
-}
-
 // One reactor thread driving streams [first, first + count).
 void run_thread(const Opts& o, int first, int count, Result& res, Result& warm_res) {
   Reactor r;
@@ -334,6 +339,7 @@ void run_thread(const Opts& o, int first, int count, Result& res, Result& warm_r
         for (auto& s : live) s->set_result(&res);
     }
     pending = count;
+    if (first == 0) g_step.store(step, std::memory_order_relaxed);
     trace_step(first, step, "step_start");
     for (auto& s : set) s->request();
   };

@@ -260,8 +260,9 @@ def bulk_echo(a):
              "last response complete at proxy": ("proxy", "res_end", max)}
     steps = []
     if lg:  # the client's own steps: marks from its step start
-        bounds = sorted((v["step_start"], v["step_end"]) for v in lg.values() if "step_start" in v and "step_end" in v)
-        for t0, t1 in bounds:
+        bounds = sorted((v["step_start"], v["step_end"], v.get("connected")) for v in lg.values()
+                        if "step_start" in v and "step_end" in v)
+        for t0, t1, conn in bounds:
             g = [e for e in reqs if t0 <= e[("proxy", "accept")] <= t1]
             if not g:
                 continue
@@ -272,6 +273,8 @@ def bulk_echo(a):
                 row[name] = (agg(vals) - t0) / 1e3 if vals else None
             row["step end at the client"] = (t1 - t0) / 1e3
             row["new connections"] = sum(1 for e in g if ("proxy", "tcp_accept") in e)
+            # the client's last connect() of this step completing (new connections only)
+            row["last client connect done"] = (conn - t0) / 1e3 if conn and conn >= t0 else None
             # The straggler: the request whose upload ended last, every stamp
             # it has relative to the step start (ms).
             late = max(g, key=lambda e: e.get(("proxy", "req_end"), 0))
