@@ -121,6 +121,11 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
 
   // Bytes accepted by send() that have not been transmitted yet.
   size_t buffered_amount() const { return unsent_bytes_; }
+  // A SACK the next flush sends right away (>= 2 data packets unacknowledged,
+  // a gap or duplicate to report, or the delayed-SACK timer fired).
+  bool ack_due() const {
+    return sack_needed_ && (sack_urgent_ || data_pkts_unacked_ >= 2 || !ooo_.empty() || !dups_.empty());
+  }
   size_t bytes_in_flight() const { return flight_size_; }
   State state() const { return state_; }
   bool established() const { return state_ == State::Established; }
