@@ -135,6 +135,8 @@ def main():
     ap.add_argument("--extra", default="", help="extra flags for both tunnel processes")
     ap.add_argument("--mock-threads", type=int, default=4,
                     help="reactor threads of the native mock (it serves the SSE and the downloads, tunneled and direct)")
+    ap.add_argument("--profile-dir", default=None,
+                    help="sampling CPU profile of every tunnel process (TUNNEL_PROFILE), reports next to it")
     ap.add_argument("--timeline", action="store_true",
                     help="per-thread CPU utilisation of both tunnels in 2 ms intervals (which stage saturates)")
     ap.add_argument("--out", default=None)
@@ -147,6 +149,10 @@ def main():
     if a.timeline:
         from p2p_llm_tunnel_amd.utils import timeline
         tl_dir, tl_env = timeline.new_dir()
+    if a.profile_dir:
+        os.makedirs(a.profile_dir, exist_ok=True)
+        tl_env = dict(tl_env or {}, TUNNEL_PROFILE=os.path.join(os.path.abspath(a.profile_dir), "tunnel.%p.prof"),
+                      TUNNEL_PROFILE_HZ="1000")
     mock.wait_for("Mock LLM server running", 10)
     trs = [x for x in a.transports.split(",") if x]
     res = {"host": os.uname().nodename, "time": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
@@ -204,6 +210,16 @@ def main():
         mock.stop()
     if tl_dir:  # over each process's life; the direct runs add idle intervals only
         res["timeline"] = timeline.summarise(tl_dir, pids)
+    if a.profile_dir:
+        res["profiles"] = {k: f"tunnel.{v}.prof" for k, v in pids.items()}
+        for k, v in pids.items():
+            f = os.path.join(a.profile_dir, f"tunnel.{v}.prof")
+            if os.path.exists(f):
+                for thread, suffix in ((None, ""), ("0", ".main")):
+                    rep = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "profile_report.py"), f, "--top", "30"] +
+                                         (["--thread", thread] if thread else []), capture_output=True, text=True).stdout
+                    with open(os.path.join(a.profile_dir, f"{k}{suffix}.txt"), "w") as fh:
+                        fh.write(rep)
     doc = json.dumps(res, indent=1)
     if a.out:
         with open(a.out, "w") as f:

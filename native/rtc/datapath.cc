@@ -38,8 +38,11 @@ Lane::Lane(const char* name) {
     for (int sig : {SIGINT, SIGTERM, SIGHUP, SIGQUIT, SIGUSR1, SIGUSR2, SIGPIPE}) sigaddset(&mask, sig);
     pthread_sigmask(SIG_BLOCK, &mask, nullptr);
     pthread_setname_np(pthread_self(), n.c_str());
-    // T90 seal / T93 send / T91 rx in profiles and timelines
-    profiler::register_thread(n.find("-txsend") != std::string::npos ? 93 : n.find("-tx") != std::string::npos ? 90 : 91);
+    // T90 seal / T94 second sealer / T93 send / T91 rx in profiles and timelines
+    profiler::register_thread(n.find("-txsend") != std::string::npos  ? 93
+                              : n.find("-seal2") != std::string::npos ? 94
+                              : n.find("-tx") != std::string::npos    ? 90
+                                                                      : 91);
     run();
   });
 }
@@ -206,24 +209,58 @@ void TxLaneState::run(const TxBatch& b, const RecordKeys& k, int fd, const SockA
   send(one_, fd, to);
 }
 
+static size_t seal_split_bytes() {
+  static const size_t v = [] {
+    const char* e = getenv("TUNNEL_SEAL_SPLIT_KB");
+    return (e && *e ? size_t(strtoull(e, nullptr, 10)) : size_t(128)) * 1024;
+  }();
+  return v;
+}
+
+void TxLaneState::seal_range(const TxBatch& b, const RecordKeys& k, SealedBatch& sb, size_t lo, size_t hi) {
+  iovec iov[64];
+  for (size_t i = lo; i < hi; i++) {
+    const auto& r = b.recs[i];
+    int cnt = b.gather(r, iov, 64);
+    seal_record(*k.w, k.wiv, sb.out.data() + offs_[i], r.type, r.seq, iov, cnt, r.total);
+  }
+}
+
 void TxLaneState::seal(const TxBatch& b, const RecordKeys& k, size_t coalesce, SealedBatch& sb) {
   // Seal every record into one contiguous buffer; datagram boundaries are
   // kept aside (several records per datagram on same-host jumbo paths).
   std::vector<uint8_t>& out_ = sb.out;
   auto& dgs_ = sb.dgs;
-  size_t need = 0;
-  for (auto& r : b.recs) need += record_size(r.total);
-  if (out_.size() < need) out_.resize(need);
+  const size_t n = b.recs.size();
+  offs_.resize(n);
   dgs_.clear();
   size_t off = 0;
-  iovec iov[64];
-  for (auto& r : b.recs) {
-    const size_t sz = record_size(r.total);
+  for (size_t i = 0; i < n; i++) {
+    const size_t sz = record_size(b.recs[i].total);
     if (coalesce && !dgs_.empty() && dgs_.back().second + sz <= coalesce) dgs_.back().second += sz;
     else dgs_.emplace_back(off, sz);
-    int cnt = b.gather(r, iov, 64);
-    seal_record(*k.w, k.wiv, out_.data() + off, r.type, r.seq, iov, cnt, r.total);
+    offs_[i] = off;
     off += sz;
+  }
+  if (out_.size() < off) out_.resize(off);
+  const size_t split = seal_split_bytes();
+  if (split && off >= split && n >= 2) {
+    // First half (by bytes) on the helper, the rest here; both write disjoint
+    // ranges of out_ and read the batch and keys only.
+    size_t mid = 0;
+    while (mid + 1 < n && offs_[mid + 1] < off / 2) mid++;
+    mid = std::max<size_t>(mid, 1);
+    if (!helper_) helper_ = std::make_unique<Lane>("p2pt-dtls-seal2");
+    std::atomic<bool> done{false};
+    helper_->submit([&, mid] {
+      seal_range(b, k, sb, 0, mid);
+      done.store(true, std::memory_order_release);
+    });
+    seal_range(b, k, sb, mid, n);
+    while (!done.load(std::memory_order_acquire)) std::this_thread::yield();
+    split_batches.fetch_add(1, std::memory_order_relaxed);
+  } else {
+    seal_range(b, k, sb, 0, n);
   }
   records.fetch_add(b.recs.size(), std::memory_order_relaxed);
   batches.fetch_add(1, std::memory_order_relaxed);

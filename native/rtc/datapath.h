@@ -201,10 +201,20 @@ class TxLaneState {
   // send_drops: datagrams dropped (socket buffer still full after kSendWaitMs
   // of POLLOUT waits, or unreachable); send_waits: POLLOUT waits taken.
   std::atomic<uint64_t> batches{0}, records{0}, datagrams{0}, gso_msgs{0}, send_drops{0}, send_waits{0};
+  std::atomic<uint64_t> split_batches{0};  // batches sealed by two threads
   static constexpr int kSendWaitMs = 20;
 
  private:
+  void seal_range(const TxBatch& b, const RecordKeys& k, SealedBatch& sb, size_t lo, size_t hi);
   SealedBatch one_;  // run()'s buffer
+  // Large batches are sealed by two threads: a helper takes the first half of
+  // the records while the seal lane does the rest (record offsets are fixed
+  // before either starts). On the MI355X host's mixed row the seal lane was
+  // at >= 90 % CPU in 73-96 % of its active intervals at 1200-byte MTU
+  // (profiles/r04/co16). TUNNEL_SEAL_SPLIT_KB: batch size from which to split
+  // (default 128; 0 = never).
+  std::unique_ptr<Lane> helper_;
+  std::vector<size_t> offs_;    // record offsets in out (seal stage only)
   bool gso_ok_ = true;  // send stage only
   std::mutex mu_;
   std::vector<std::shared_ptr<SealedBatch>> free_;

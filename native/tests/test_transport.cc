@@ -618,6 +618,42 @@ TEST(peerconnection_pair_loopback) {
 // datagram, a datagram from another sender, a record that fails
 // authentication (handed over with ok = false for the association thread to
 // drop), and a datagram mixing an alert with data.
+// A batch large enough to be sealed by two threads comes out byte for byte
+// as sealing each record alone would make it, datagram boundaries included.
+TEST(tx_seal_split_matches_one_thread) {
+  if (!AesGcm::supported()) return;
+  RecordKeys keys;
+  auto g = std::make_shared<AesGcm>();
+  uint8_t key[16];
+  for (int i = 0; i < 16; i++) key[i] = uint8_t(i * 7 + 1);
+  CHECK(g->init(key, 16));
+  keys.w = keys.r = g;
+  for (int i = 0; i < 4; i++) keys.wiv[i] = keys.riv[i] = uint8_t(0x30 + i);
+  TxBatch b;
+  std::vector<std::string> pts;
+  for (int i = 0; i < 300; i++) {  // ~360 KB: over the 128 KiB split size
+    pts.push_back(std::string(1100 + (i * 37) % 100, char('a' + i % 26)));
+    iovec v{const_cast<char*>(pts.back().data()), pts.back().size()};
+    b.add(uint64_t(1000 + i), 23, &v, nullptr, 1);
+  }
+  TxLaneState st;
+  SealedBatch sb;
+  st.seal(b, keys, 0, sb);
+  CHECK_EQ(st.split_batches.load(), uint64_t(1));
+  CHECK_EQ(sb.dgs.size(), size_t(300));
+  size_t off = 0;
+  bool same = true;
+  for (int i = 0; i < 300; i++) {
+    std::vector<uint8_t> one(record_size(pts[size_t(i)].size()));
+    iovec v{const_cast<char*>(pts[size_t(i)].data()), pts[size_t(i)].size()};
+    seal_record(*g, keys.wiv, one.data(), 23, uint64_t(1000 + i), &v, 1, pts[size_t(i)].size());
+    same &= sb.dgs[size_t(i)].first == off && sb.dgs[size_t(i)].second == one.size() &&
+            memcmp(sb.out.data() + off, one.data(), one.size()) == 0;
+    off += one.size();
+  }
+  CHECK(same);
+}
+
 TEST(rx_reader_opens_app_records_and_passes_the_rest) {
   if (!AesGcm::supported()) return;
   auto keys = std::make_shared<RecordKeys>();

@@ -15,7 +15,7 @@ import os
 import tempfile
 
 # Thread tags (native/rtc/datapath.cc Lane/RxReader, native/tunnel/workers.cc).
-NAMES = {0: "assoc", 90: "tx_seal", 93: "tx_send", 91: "rx_lane", 92: "udp_reader"}
+NAMES = {0: "assoc", 90: "tx_seal", 94: "tx_seal2", 93: "tx_send", 91: "rx_lane", 92: "udp_reader"}
 
 
 def new_dir() -> tuple[str, dict[str, str]]:
