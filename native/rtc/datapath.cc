@@ -212,10 +212,16 @@ void TxLaneState::run(const TxBatch& b, const RecordKeys& k, int fd, const SockA
 static size_t seal_split_bytes() {
   static const size_t v = [] {
     const char* e = getenv("TUNNEL_SEAL_SPLIT_KB");
-    return (e && *e ? size_t(strtoull(e, nullptr, 10)) : size_t(128)) * 1024;
+    // Off by default: on the MI355X host the mixed row's jumbo download gained
+    // (0.391 -> 0.433 of direct) but the 64 x 1 MB echo lost (1797 -> 1539
+    // req/s jumbo, same box): with the serve pinned to 6 CPUs the second
+    // sealer competes with the other six threads (profiles/r04/mix17, split17).
+    return (e && *e ? size_t(strtoull(e, nullptr, 10)) : size_t(0)) * 1024;
   }();
   return v;
 }
+
+TxLaneState::TxLaneState() : split_bytes_(seal_split_bytes()) {}
 
 void TxLaneState::seal_range(const TxBatch& b, const RecordKeys& k, SealedBatch& sb, size_t lo, size_t hi) {
   iovec iov[64];
@@ -243,7 +249,7 @@ void TxLaneState::seal(const TxBatch& b, const RecordKeys& k, size_t coalesce, S
     off += sz;
   }
   if (out_.size() < off) out_.resize(off);
-  const size_t split = seal_split_bytes();
+  const size_t split = split_bytes_;
   if (split && off >= split && n >= 2) {
     // First half (by bytes) on the helper, the rest here; both write disjoint
     // ranges of out_ and read the batch and keys only.

@@ -189,12 +189,15 @@ struct SealedBatch {
 // AES-GCM and sendmmsg.
 class TxLaneState {
  public:
+  TxLaneState();
   // Seal stage: encrypts the batch (runs on the seal lane).
   void seal(const TxBatch& b, const RecordKeys& k, size_t coalesce, SealedBatch& out);
   // Send stage: sends a sealed batch to target (runs on the send lane).
   void send(SealedBatch& s, int fd, const SockAddr& to);
   // Both stages in a row (tests; the single-lane path).
   void run(const TxBatch& b, const RecordKeys& k, int fd, const SockAddr& to, size_t coalesce);
+  // Batches of at least this many bytes are sealed by two threads (0: never).
+  void set_split_bytes(size_t n) { split_bytes_ = n; }
   // Sealed batches are recycled between the stages (buffers allocated once).
   std::shared_ptr<SealedBatch> get_sealed();
   void put_sealed(std::shared_ptr<SealedBatch> s);
@@ -212,7 +215,8 @@ class TxLaneState {
   // before either starts). On the MI355X host's mixed row the seal lane was
   // at >= 90 % CPU in 73-96 % of its active intervals at 1200-byte MTU
   // (profiles/r04/co16). TUNNEL_SEAL_SPLIT_KB: batch size from which to split
-  // (default 128; 0 = never).
+  // (0 = never, the default; see seal_split_bytes()).
+  size_t split_bytes_;           // TUNNEL_SEAL_SPLIT_KB * 1024 unless set
   std::unique_ptr<Lane> helper_;
   std::vector<size_t> offs_;    // record offsets in out (seal stage only)
   bool gso_ok_ = true;  // send stage only

@@ -637,6 +637,7 @@ TEST(tx_seal_split_matches_one_thread) {
     b.add(uint64_t(1000 + i), 23, &v, nullptr, 1);
   }
   TxLaneState st;
+  st.set_split_bytes(128 * 1024);
   SealedBatch sb;
   st.seal(b, keys, 0, sb);
   CHECK_EQ(st.split_batches.load(), uint64_t(1));
