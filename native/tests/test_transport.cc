@@ -1037,8 +1037,8 @@ TEST(busy_loop_flushes_coalesce_small_messages) {
   size_t got_off = 0, got_on = 0;
   bool ok_off = false, ok_on = false;
   coalesce_run(0, &pk_off, &held_off, &got_off, &ok_off);
-  coalesce_run(200, &pk_on, &held_on, &got_on, &ok_on);
-  printf("  2000 x 45 B, one per pass: %llu packets without coalescing, %llu with (%llu flushes held)\n",
+  coalesce_run(2000, &pk_on, &held_on, &got_on, &ok_on);  // a window far above a pass, even under TSan
+  printf("  2000 x 45 B, one per pass: %llu packets without coalescing, %llu with 2 ms (%llu flushes held)\n",
          (unsigned long long)pk_off, (unsigned long long)pk_on, (unsigned long long)held_on);
   CHECK_EQ(got_off, size_t(2000));
   CHECK_EQ(got_on, size_t(2000));
