@@ -297,6 +297,20 @@ void TcpConn::update_interest() {
   }
 }
 
+// TUNNEL_TCP_QUICKACK=1: after each batch of reads, TCP_QUICKACK on the
+// socket (not sticky in Linux), so the ACKs and window updates for what was
+// just consumed leave now instead of after the delayed-ACK timer. A flow-
+// controlled reader (the proxy pausing an upload for credit) otherwise leaves
+// the sender window-limited with one sub-MSS segment unacknowledged, which on
+// loopback ends in a TCP loss probe 10 ms later.
+static bool tcp_quickack() {
+  static const bool v = [] {
+    const char* e = getenv("TUNNEL_TCP_QUICKACK");
+    return e && *e == '1';
+  }();
+  return v;
+}
+
 void TcpConn::on_events(uint32_t ev) {
   auto self = shared_from_this();
   if (handshaking_) {
@@ -313,7 +327,13 @@ void TcpConn::on_events(uint32_t ev) {
     if (fd_ < 0) return;
   }
   if (ev & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) {
-    if (!paused_ || (ev & (EPOLLHUP | EPOLLERR))) do_read();
+    if (!paused_ || (ev & (EPOLLHUP | EPOLLERR))) {
+      do_read();
+      if (tcp_quickack() && fd_ >= 0 && !ssl_) {
+        int one = 1;
+        setsockopt(fd_, IPPROTO_TCP, TCP_QUICKACK, &one, sizeof one);
+      }
+    }
   }
 }
 
