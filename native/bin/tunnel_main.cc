@@ -19,6 +19,7 @@
 #include <string>
 #include <vector>
 
+#include "core/affinity.h"
 #include "core/log.h"
 #include "core/profiler.h"
 #include "rtc/dtls.h"
@@ -413,6 +414,7 @@ int main(int argc, char** argv) {
     }
     LOG_INFO("tunnel", "pinned to CPUs %s", m["cpu-affinity"].c_str());
   }
+  affinity::pin_this_thread(true);  // TUNNEL_PIN_THREADS=1: one CPU per thread
 
   if (!m["identity"].empty()) {
     std::string err;

@@ -1,0 +1,43 @@
+#include "core/affinity.h"
+
+#include <sched.h>
+
+#include <atomic>
+#include <cstdlib>
+#include <mutex>
+#include <vector>
+
+namespace p2pt::affinity {
+
+bool enabled() {
+  static const bool v = [] {
+    const char* e = getenv("TUNNEL_PIN_THREADS");
+    return e && *e == '1';
+  }();
+  return v;
+}
+
+namespace {
+std::once_flag g_once;
+std::vector<int> g_cpus;  // the process's CPU set, captured once
+std::atomic<unsigned> g_next{0};
+}  // namespace
+
+void pin_this_thread(bool assoc) {
+  if (!enabled()) return;
+  std::call_once(g_once, [] {
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) != 0) return;
+    for (int c = 0; c < CPU_SETSIZE; c++)
+      if (CPU_ISSET(c, &set)) g_cpus.push_back(c);
+  });
+  const size_t n = g_cpus.size();
+  if (n < 2) return;
+  const int cpu = assoc ? g_cpus[0] : g_cpus[1 + g_next.fetch_add(1, std::memory_order_relaxed) % (n - 1)];
+  cpu_set_t one;
+  CPU_ZERO(&one);
+  CPU_SET(cpu, &one);
+  sched_setaffinity(0, sizeof one, &one);
+}
+
+}  // namespace p2pt::affinity

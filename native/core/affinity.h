@@ -1,0 +1,20 @@
+// Per-thread CPU pinning inside the process's CPU set (TUNNEL_PIN_THREADS=1).
+//
+// A thread that migrates between CPUs in the middle of a large loopback TCP
+// write leaves segments of one connection on two CPUs' receive backlogs; the
+// second CPU's softirq can deliver its segments first. On the MI355X host the
+// tunneled leg of the 64 x 1 MB echo showed exactly that (TCPOFOQueue 33-74,
+// TCPSACKReorder 19-28, DSACK-undone fast retransmits per run; the direct leg
+// none), and each spurious recovery shrinks that connection's window. With
+// the switch on, the association thread takes the set's first CPU and every
+// other registered thread (workers, lanes, socket reader) one of the rest,
+// round robin, so none of them migrates.
+#pragma once
+
+namespace p2pt::affinity {
+
+bool enabled();
+// Pins the calling thread (the association thread: the set's first CPU).
+void pin_this_thread(bool assoc);
+
+}  // namespace p2pt::affinity

@@ -1,5 +1,7 @@
 #include "core/profiler.h"
 
+#include "core/affinity.h"
+
 #include <dlfcn.h>
 #include <pthread.h>
 #include <signal.h>
@@ -228,6 +230,7 @@ bool start_timeline_from_env() {
 
 void register_thread(int tag) {
   t_tag = uint64_t(tag);
+  if (tag != 0) affinity::pin_this_thread(false);
   if (timeline::on.load(std::memory_order_relaxed)) timeline::add_self(tag);
   pthread_attr_t attr;
   if (pthread_getattr_np(pthread_self(), &attr) == 0) {
