@@ -413,8 +413,9 @@ int main(int argc, char** argv) {
       return 2;
     }
     LOG_INFO("tunnel", "pinned to CPUs %s", m["cpu-affinity"].c_str());
+    affinity::set_default(true);  // given its CPUs: one per thread (TUNNEL_PIN_THREADS=0: off)
   }
-  affinity::pin_this_thread(true);  // TUNNEL_PIN_THREADS=1: one CPU per thread
+  affinity::pin_this_thread(true);
 
   if (!m["identity"].empty()) {
     std::string err;

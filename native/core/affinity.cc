@@ -9,12 +9,16 @@
 
 namespace p2pt::affinity {
 
+namespace {
+std::atomic<bool> g_default{false};
+}  // namespace
+
+void set_default(bool on) { g_default.store(on, std::memory_order_relaxed); }
+
 bool enabled() {
-  static const bool v = [] {
-    const char* e = getenv("TUNNEL_PIN_THREADS");
-    return e && *e == '1';
-  }();
-  return v;
+  const char* e = getenv("TUNNEL_PIN_THREADS");
+  if (e && *e) return *e == '1';
+  return g_default.load(std::memory_order_relaxed);
 }
 
 namespace {

@@ -125,7 +125,7 @@ class TcpConn : public std::enable_shared_from_this<TcpConn> {
  private:
   TcpConn(Reactor& r, int fd);
   void on_events(uint32_t ev);
-  void do_read();
+  size_t do_read();  // bytes read
   void do_write();
   void update_interest();
   void fail(const std::string& err);
