@@ -27,14 +27,23 @@ std::vector<int> g_cpus;  // the process's CPU set, captured once
 std::atomic<unsigned> g_next{0};
 }  // namespace
 
-void pin_this_thread(bool assoc) {
-  if (!enabled()) return;
+static void capture() {
   std::call_once(g_once, [] {
     cpu_set_t set;
     if (sched_getaffinity(0, sizeof set, &set) != 0) return;
     for (int c = 0; c < CPU_SETSIZE; c++)
       if (CPU_ISSET(c, &set)) g_cpus.push_back(c);
   });
+}
+
+long process_cpu_count() {
+  capture();
+  return long(g_cpus.size());
+}
+
+void pin_this_thread(bool assoc) {
+  if (!enabled()) return;
+  capture();
   const size_t n = g_cpus.size();
   if (n < 2) return;
   const int cpu = assoc ? g_cpus[0] : g_cpus[1 + g_next.fetch_add(1, std::memory_order_relaxed) % (n - 1)];

@@ -21,5 +21,8 @@ void set_default(bool on);
 bool enabled();
 // Pins the calling thread (the association thread: the set's first CPU).
 void pin_this_thread(bool assoc);
+// CPUs of the process's set as it was before any thread pinned itself (the
+// calling thread's set when nothing was pinned).
+long process_cpu_count();
 
 }  // namespace p2pt::affinity

@@ -1,5 +1,7 @@
 #include "tunnel/workers.h"
 
+#include "core/affinity.h"
+
 #include <pthread.h>
 #include <signal.h>
 #include <unistd.h>
@@ -55,9 +57,8 @@ WorkerThread::~WorkerThread() {
 // gave a process pinned to 6 CPUs a single worker, which then saturated on
 // the 64 x 1 MB echo (all 64 upstream sockets' I/O; profiles/r04/flow_ab).
 int WorkerPool::auto_count() {
-  long n = sysconf(_SC_NPROCESSORS_ONLN);
-  cpu_set_t set;
-  if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
+  long n = affinity::process_cpu_count();  // the set from before this thread pinned itself to one CPU
+  if (n <= 0) n = sysconf(_SC_NPROCESSORS_ONLN);
   return int(std::clamp<long>(n / 2 - 1, 1, 4));
 }
 
