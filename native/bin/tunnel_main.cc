@@ -415,7 +415,7 @@ int main(int argc, char** argv) {
     LOG_INFO("tunnel", "pinned to CPUs %s", m["cpu-affinity"].c_str());
     affinity::set_default(true);  // given its CPUs: one per thread (TUNNEL_PIN_THREADS=0: off)
   }
-  affinity::pin_this_thread(true);
+  affinity::pin_this_thread(0);
 
   if (!m["identity"].empty()) {
     std::string err;

@@ -41,12 +41,22 @@ long process_cpu_count() {
   return long(g_cpus.size());
 }
 
-void pin_this_thread(bool assoc) {
+void pin_this_thread(int tag) {
   if (!enabled()) return;
   capture();
   const size_t n = g_cpus.size();
   if (n < 2) return;
-  const int cpu = assoc ? g_cpus[0] : g_cpus[1 + g_next.fetch_add(1, std::memory_order_relaxed) % (n - 1)];
+  size_t slot;
+  if (tag == 0) {
+    slot = 0;
+  } else if (n >= 6 && (tag == 92 || tag == 90 || tag == 93)) {
+    slot = tag == 92 ? 1 : tag == 90 ? 2 : 3;  // reader, seal, send: a CPU each
+  } else if (n >= 6) {
+    slot = 4 + g_next.fetch_add(1, std::memory_order_relaxed) % (n - 4);  // workers, RX lane, second sealer
+  } else {
+    slot = 1 + g_next.fetch_add(1, std::memory_order_relaxed) % (n - 1);
+  }
+  const int cpu = g_cpus[slot];
   cpu_set_t one;
   CPU_ZERO(&one);
   CPU_SET(cpu, &one);

@@ -6,9 +6,8 @@
 // tunneled leg of the 64 x 1 MB echo showed exactly that (TCPOFOQueue 33-74,
 // TCPSACKReorder 19-28, DSACK-undone fast retransmits per run; the direct leg
 // none), and each spurious recovery shrinks that connection's window. With
-// the switch on, the association thread takes the set's first CPU and every
-// other registered thread (workers, lanes, socket reader) one of the rest,
-// round robin, so none of them migrates. Default: on when the process was
+// the switch on, every tunnel thread is pinned to one CPU of the set (see
+// pin_this_thread for the layout), so none of them migrates. Default: on when the process was
 // given its CPUs (--cpu-affinity; A/B on the host: +18-22 % at 1200 MTU,
 // +18 % jumbo on the echo, profiles/r04/pt20), off otherwise (a process
 // that may run anywhere is not packed onto the machine's first CPUs).
@@ -19,8 +18,13 @@ namespace p2pt::affinity {
 // The default when TUNNEL_PIN_THREADS is not set (called before any thread starts).
 void set_default(bool on);
 bool enabled();
-// Pins the calling thread (the association thread: the set's first CPU).
-void pin_this_thread(bool assoc);
+// Pins the calling thread by its role (profiler tags): 0 the association
+// thread, 1.. HTTP workers, 90 TX seal lane, 91 RX lane, 92 socket reader,
+// 93 TX send lane, 94 second sealer. With n >= 6 CPUs the association thread,
+// the reader and the two TX stages get one CPU each (the set's first four) and
+// the workers share the rest; the RX lane (idle while the reader runs) and the
+// second sealer go with the workers. With fewer CPUs: round robin.
+void pin_this_thread(int tag);
 // CPUs of the process's set as it was before any thread pinned itself (the
 // calling thread's set when nothing was pinned).
 long process_cpu_count();

@@ -230,7 +230,7 @@ bool start_timeline_from_env() {
 
 void register_thread(int tag) {
   t_tag = uint64_t(tag);
-  if (tag != 0) affinity::pin_this_thread(false);
+  if (tag != 0) affinity::pin_this_thread(tag);
   if (timeline::on.load(std::memory_order_relaxed)) timeline::add_self(tag);
   pthread_attr_t attr;
   if (pthread_getattr_np(pthread_self(), &attr) == 0) {
