@@ -91,10 +91,16 @@ def test_tunnel_threads_pinned_one_cpu_each(mock_upstream):
         sets = thread_sets(t.serve.popen.pid)
         assert all(s == frozenset(cpus[:3]) for s in sets.values())
     if len(cpus) >= 6:
-        # auto workers follow the set given (6 CPUs: 2), not the one CPU the
-        # association thread pinned itself to before the pool was sized
+        # auto workers follow the set given (6 CPUs, one per thread: the
+        # association thread, reader and TX stages take four, 1 worker), not
+        # the one CPU the association thread pinned itself to first
         spec6 = ",".join(str(c) for c in cpus[:6])
         with Tunnel(mock_upstream, transport="webrtc", serve_extra=["--cpu-affinity", spec6]) as t:
+            pid = t.serve.popen.pid
+            names = [open(f"/proc/{pid}/task/{tid}/comm").read().strip() for tid in os.listdir(f"/proc/{pid}/task")]
+            assert sum(n.startswith("p2pt-w") for n in names) == 1, names
+        with Tunnel(mock_upstream, transport="webrtc", serve_extra=["--cpu-affinity", spec6],
+                    env={"TUNNEL_PIN_THREADS": "0"}) as t:  # floating threads: half the CPUs less one
             pid = t.serve.popen.pid
             names = [open(f"/proc/{pid}/task/{tid}/comm").read().strip() for tid in os.listdir(f"/proc/{pid}/task")]
             assert sum(n.startswith("p2pt-w") for n in names) == 2, names
