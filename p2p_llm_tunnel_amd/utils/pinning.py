@@ -10,6 +10,9 @@ GPU) into one set per role, in the same proportions on every box:
 
     loadgen 1/8, mock 1/8, serve 3/8, proxy 3/8   (16 CPUs: 2 / 2 / 6 / 6)
 
+When the CPUs span two L3 domains (two CCDs), the client side (loadgen,
+proxy) takes one and the server side (serve, mock) the other (cpu_plan).
+
 Each tunnel process holds an association thread, a DTLS TX lane, a socket
 reader, an RX lane and its HTTP workers; the load generator and the mock are
 single reactors (the direct leg runs on exactly their CPUs too).
@@ -52,12 +55,45 @@ def available_cpus() -> list[int]:
     return cpus[:budget]
 
 
-def cpu_plan(cpus: list[int] | None = None) -> dict[str, str]:
-    """Role -> CPU list string (taskset / --cpu-affinity syntax); {} with fewer than 4 CPUs."""
+def l3_groups(cpus: list[int]) -> list[list[int]]:
+    """cpus grouped by shared L3 (one CCD on EPYC), in order; one group when
+    the topology is unknown."""
+    groups: dict[str, list[int]] = {}
+    for c in cpus:
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list") as f:
+                key = f.read().strip()
+        except OSError:
+            key = ""
+        groups.setdefault(key, []).append(c)
+    return list(groups.values())
+
+
+def cpu_plan(cpus: list[int] | None = None, by_side: bool | None = None) -> dict[str, str]:
+    """Role -> CPU list string (taskset / --cpu-affinity syntax); {} with fewer than 4 CPUs.
+
+    by_side (default: when the CPUs span exactly two L3 domains of equal size,
+    e.g. two 8-core CCDs of the pool's EPYC 9575F): the client side (load
+    generator, proxy) on one L3, the server side (serve, mock upstream) on the
+    other, as two machines would be — the direct leg and the tunnel each cross
+    between them once. Otherwise the split above, in CPU order: load generator
+    and mock on the first CPUs (on a 16-CPU budget that put them, the serve's
+    first four threads and nothing of the proxy on one CCD, so the direct leg
+    never left its L3 while the tunneled leg crossed twice)."""
     cpus = available_cpus() if cpus is None else list(cpus)
     n = len(cpus)
     if n < 4:
         return {}
+    if by_side is None and os.environ.get("P2PT_PIN_PLAN") in ("order", "side"):
+        by_side = os.environ["P2PT_PIN_PLAN"] == "side"  # A/B of the two layouts
+    groups = l3_groups(cpus) if by_side is None or by_side else [cpus]
+    if by_side is None:
+        by_side = len(groups) == 2 and len(groups[0]) == len(groups[1]) and len(groups[0]) >= 4
+    if by_side and len(groups) == 2:
+        a, b = groups
+        k = max(1, len(a) // 4)
+        plan = {"loadgen": a[:k], "proxy": a[k:], "serve": b[:len(b) - k], "mock": b[len(b) - k:]}
+        return {k_: fmt_cpus(v) for k_, v in plan.items()}
     lg = max(1, n // 8)
     mk = max(1, n // 8)
     rest = n - lg - mk

@@ -33,9 +33,13 @@ def test_ab_stops_on_a_failed_run(tmp_path):
     assert "exit 2" in r.stdout and r.stdout.count("rep ") == 1
 
 
-def test_cpu_plan_splits_sixteen():
-    plan = pinning.cpu_plan(list(range(16)))
+def test_cpu_plan_splits_sixteen(monkeypatch):
+    plan = pinning.cpu_plan(list(range(16)), by_side=False)
     assert plan == {"loadgen": "0-1", "mock": "2-3", "serve": "4-9", "proxy": "10-15"}
+    # two 8-CPU L3 domains: client side on one, server side on the other
+    monkeypatch.setattr(pinning, "l3_groups", lambda cpus: [cpus[:8], cpus[8:]])
+    plan = pinning.cpu_plan(list(range(16)))
+    assert plan == {"loadgen": "0-1", "proxy": "2-7", "serve": "8-13", "mock": "14-15"}
     assert pinning.cpu_plan([0, 1, 2]) == {}
     assert pinning.parse_cpus("0-2,5") == [0, 1, 2, 5]
 
