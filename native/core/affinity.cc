@@ -49,10 +49,17 @@ void pin_this_thread(int tag) {
   size_t slot;
   if (tag == 0) {
     slot = 0;
-  } else if (n >= 6 && (tag == 92 || tag == 90 || tag == 93)) {
-    slot = tag == 92 ? 1 : tag == 90 ? 2 : 3;  // reader, seal, send: a CPU each
   } else if (n >= 6) {
-    slot = 4 + g_next.fetch_add(1, std::memory_order_relaxed) % (n - 4);  // workers, RX lane, second sealer
+    // [assoc][workers ...][seal][send][reader][RX lane]: the workers (which
+    // talk to the upstreams / clients over TCP) next to the association
+    // thread, the socket reader last (on a set that spans two L3 domains,
+    // nearest the peer's side).
+    const size_t nw = n - 5;
+    if (tag >= 1 && tag < 90) slot = 1 + size_t(tag - 1) % nw;
+    else if (tag == 90) slot = n - 4;
+    else if (tag == 93) slot = n - 3;
+    else if (tag == 92) slot = n - 2;
+    else slot = n - 1;  // RX lane (idle while the reader runs), second sealer
   } else {
     slot = 1 + g_next.fetch_add(1, std::memory_order_relaxed) % (n - 1);
   }

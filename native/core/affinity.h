@@ -20,10 +20,10 @@ void set_default(bool on);
 bool enabled();
 // Pins the calling thread by its role (profiler tags): 0 the association
 // thread, 1.. HTTP workers, 90 TX seal lane, 91 RX lane, 92 socket reader,
-// 93 TX send lane, 94 second sealer. With n >= 6 CPUs the association thread,
-// the reader and the two TX stages get one CPU each (the set's first four) and
-// the workers share the rest; the RX lane (idle while the reader runs) and the
-// second sealer go with the workers. With fewer CPUs: round robin.
+// 93 TX send lane, 94 second sealer. With n >= 6 CPUs, in the set's order:
+// the association thread, the workers (n - 5 of them by default), the seal
+// and send stages, the socket reader, and last the RX lane (idle while the
+// reader runs) with the second sealer. With fewer CPUs: round robin.
 void pin_this_thread(int tag);
 // CPUs of the process's set as it was before any thread pinned itself (the
 // calling thread's set when nothing was pinned).

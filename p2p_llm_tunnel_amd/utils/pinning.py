@@ -69,25 +69,29 @@ def l3_groups(cpus: list[int]) -> list[list[int]]:
     return list(groups.values())
 
 
-def cpu_plan(cpus: list[int] | None = None, by_side: bool | None = None) -> dict[str, str]:
+def cpu_plan(cpus: list[int] | None = None, by_side=None) -> dict[str, str]:
     """Role -> CPU list string (taskset / --cpu-affinity syntax); {} with fewer than 4 CPUs.
 
-    by_side (default: when the CPUs span exactly two L3 domains of equal size,
-    e.g. two 8-core CCDs of the pool's EPYC 9575F): the client side (load
-    generator, proxy) on one L3, the server side (serve, mock upstream) on the
-    other, as two machines would be — the direct leg and the tunnel each cross
-    between them once. Otherwise the split above, in CPU order: load generator
-    and mock on the first CPUs (on a 16-CPU budget that put them, the serve's
-    first four threads and nothing of the proxy on one CCD, so the direct leg
-    never left its L3 while the tunneled leg crossed twice)."""
+    Default (P2PT_PIN_PLAN=order, or by_side False): the split above, in CPU
+    order: load generator and mock on the first CPUs. On the pool's 16-CPU
+    budget over two 8-core CCDs (own L3 each) that keeps the direct leg
+    (load generator <-> mock) inside one L3 while the tunneled leg crosses
+    between them.
+    by_side True (P2PT_PIN_PLAN=side; "auto": when the CPUs span exactly two
+    L3 domains of equal size): the client side (load generator, proxy) on
+    one L3, the server side (serve, mock) on the other, as two machines would
+    be, so the direct leg and the tunnel each cross once. On the host that
+    moves the direct leg more than the tunnel (2660 -> 1850 req/s against
+    1760 -> 1810 at 1200 MTU; profiles/r04/plan26), so the published rows use
+    the default."""
     cpus = available_cpus() if cpus is None else list(cpus)
     n = len(cpus)
     if n < 4:
         return {}
-    if by_side is None and os.environ.get("P2PT_PIN_PLAN") in ("order", "side"):
-        by_side = os.environ["P2PT_PIN_PLAN"] == "side"  # A/B of the two layouts
-    groups = l3_groups(cpus) if by_side is None or by_side else [cpus]
-    if by_side is None:
+    if by_side is None:  # P2PT_PIN_PLAN: order (default), side, auto
+        by_side = {"order": False, "side": True}.get(os.environ.get("P2PT_PIN_PLAN", "order"), "auto")
+    groups = l3_groups(cpus) if by_side else [cpus]
+    if by_side == "auto":
         by_side = len(groups) == 2 and len(groups[0]) == len(groups[1]) and len(groups[0]) >= 4
     if by_side and len(groups) == 2:
         a, b = groups

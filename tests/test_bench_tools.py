@@ -38,7 +38,11 @@ def test_cpu_plan_splits_sixteen(monkeypatch):
     assert plan == {"loadgen": "0-1", "mock": "2-3", "serve": "4-9", "proxy": "10-15"}
     # two 8-CPU L3 domains: client side on one, server side on the other
     monkeypatch.setattr(pinning, "l3_groups", lambda cpus: [cpus[:8], cpus[8:]])
-    plan = pinning.cpu_plan(list(range(16)))
+    monkeypatch.delenv("P2PT_PIN_PLAN", raising=False)
+    assert pinning.cpu_plan(list(range(16))) == {"loadgen": "0-1", "mock": "2-3", "serve": "4-9", "proxy": "10-15"}
+    monkeypatch.setenv("P2PT_PIN_PLAN", "side")
+    assert pinning.cpu_plan(list(range(16)))["proxy"] == "2-7"
+    plan = pinning.cpu_plan(list(range(16)), by_side="auto")
     assert plan == {"loadgen": "0-1", "proxy": "2-7", "serve": "8-13", "mock": "14-15"}
     assert pinning.cpu_plan([0, 1, 2]) == {}
     assert pinning.parse_cpus("0-2,5") == [0, 1, 2, 5]
