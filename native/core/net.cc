@@ -446,10 +446,13 @@ void TcpConn::do_write() {
         return;
       }
     } else {
-      iovec iov[64];
+      // Up to 512 pieces per writev: a body relayed as a chain of SCTP
+      // fragment views (TUNNEL_SCTP_CHAIN=1) is ~55 pieces per 64 KiB frame.
+      constexpr int kIov = 512;
+      iovec iov[kIov];
       int cnt = 0;
       size_t off = out_off_;
-      for (auto it = out_.begin(); it != out_.end() && cnt < 64; ++it) {
+      for (auto it = out_.begin(); it != out_.end() && cnt < kIov; ++it) {
         iov[cnt].iov_base = const_cast<uint8_t*>(it->data() + off);
         iov[cnt].iov_len = it->size() - off;
         off = 0;
