@@ -36,6 +36,11 @@ static void capture() {
   });
 }
 
+bool tx_shared() {
+  const char* e = getenv("TUNNEL_PIN_TX_SHARED");
+  return e && *e == '1';
+}
+
 long process_cpu_count() {
   capture();
   return long(g_cpus.size());
@@ -47,16 +52,18 @@ void pin_this_thread(int tag) {
   const size_t n = g_cpus.size();
   if (n < 2) return;
   size_t slot;
+  const bool shared_tx = tx_shared();
   if (tag == 0) {
     slot = 0;
   } else if (n >= 6) {
     // [assoc][workers ...][seal][send][reader][RX lane]: the workers (which
     // talk to the upstreams / clients over TCP) next to the association
     // thread, the socket reader last (on a set that spans two L3 domains,
-    // nearest the peer's side).
-    const size_t nw = n - 5;
+    // nearest the peer's side). TUNNEL_PIN_TX_SHARED=1: the seal and send
+    // stages share one CPU and the workers get it.
+    const size_t nw = shared_tx ? n - 4 : n - 5;
     if (tag >= 1 && tag < 90) slot = 1 + size_t(tag - 1) % nw;
-    else if (tag == 90) slot = n - 4;
+    else if (tag == 90) slot = shared_tx ? n - 3 : n - 4;
     else if (tag == 93) slot = n - 3;
     else if (tag == 92) slot = n - 2;
     else slot = n - 1;  // RX lane (idle while the reader runs), second sealer
