@@ -2,6 +2,7 @@
 
 #include <sched.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdlib>
 #include <mutex>
@@ -55,18 +56,20 @@ void pin_this_thread(int tag) {
   const bool shared_tx = tx_shared();
   if (tag == 0) {
     slot = 0;
-  } else if (n >= 6) {
+  } else if (n >= 5) {
     // [assoc][workers ...][seal][send][reader][RX lane]: the workers (which
     // talk to the upstreams / clients over TCP) next to the association
     // thread, the socket reader last (on a set that spans two L3 domains,
-    // nearest the peer's side). TUNNEL_PIN_TX_SHARED=1: the seal and send
-    // stages share one CPU and the workers get it.
-    const size_t nw = shared_tx ? n - 4 : n - 5;
+    // nearest the peer's side); on 5 CPUs the idle RX lane shares the
+    // reader's. TUNNEL_PIN_TX_SHARED=1: the seal and send stages share one
+    // CPU and the workers get it.
+    const size_t nw = n >= 6 ? (shared_tx ? n - 4 : n - 5) : 1;
+    const size_t seal = 1 + nw, send = shared_tx ? seal : seal + 1, reader = send + 1;
     if (tag >= 1 && tag < 90) slot = 1 + size_t(tag - 1) % nw;
-    else if (tag == 90) slot = shared_tx ? n - 3 : n - 4;
-    else if (tag == 93) slot = n - 3;
-    else if (tag == 92) slot = n - 2;
-    else slot = n - 1;  // RX lane (idle while the reader runs), second sealer
+    else if (tag == 90) slot = seal;
+    else if (tag == 93) slot = send;
+    else if (tag == 92) slot = reader;
+    else slot = std::min(reader + 1, n - 1);  // RX lane (idle while the reader runs), second sealer
   } else {
     slot = 1 + g_next.fetch_add(1, std::memory_order_relaxed) % (n - 1);
   }

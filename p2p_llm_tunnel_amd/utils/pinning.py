@@ -88,8 +88,9 @@ def cpu_plan(cpus: list[int] | None = None, by_side=None) -> dict[str, str]:
     n = len(cpus)
     if n < 4:
         return {}
-    if by_side is None:  # P2PT_PIN_PLAN: order (default), side, auto
-        by_side = {"order": False, "side": True}.get(os.environ.get("P2PT_PIN_PLAN", "order"), "auto")
+    mode = os.environ.get("P2PT_PIN_PLAN", "order")
+    if by_side is None:  # P2PT_PIN_PLAN: order (default), order75 (serve one CPU more), side, auto
+        by_side = {"order": False, "order75": False, "side": True}.get(mode, "auto")
     groups = l3_groups(cpus) if by_side else [cpus]
     if by_side == "auto":
         by_side = len(groups) == 2 and len(groups[0]) == len(groups[1]) and len(groups[0]) >= 4
@@ -101,7 +102,7 @@ def cpu_plan(cpus: list[int] | None = None, by_side=None) -> dict[str, str]:
     lg = max(1, n // 8)
     mk = max(1, n // 8)
     rest = n - lg - mk
-    sv = rest // 2
+    sv = rest // 2 + (1 if mode == "order75" and rest >= 10 else 0)
     plan = {"loadgen": cpus[:lg], "mock": cpus[lg:lg + mk], "serve": cpus[lg + mk:lg + mk + sv],
             "proxy": cpus[lg + mk + sv:]}
     return {k: fmt_cpus(v) for k, v in plan.items()}
