@@ -124,7 +124,7 @@ def loadgen(port, streams, steps, warmup=0, path=None):
         raise RuntimeError(f"loadgen failed (rc={out.returncode}): {out.stdout[-500:]} {out.stderr[-500:]}")
 
 
-def direct(ups, streams, steps):
+def direct(ups, streams, steps, warmup=1):
     """The same load straight to the upstreams (no tunnel): streams split
     evenly over them, one load generator each, run concurrently; merged
     req/s and the p50/p99 TTFT of the most loaded one."""
@@ -132,7 +132,8 @@ def direct(ups, streams, steps):
     n = len(ups)
     share = [streams // n + (1 if i < streams % n else 0) for i in range(n)]
     procs = [subprocess.Popen([binary("tunnel-loadgen"), "--target", f"127.0.0.1:{p}", "--streams", str(k),
-                               "--steps", str(steps), "--warmup", "1"], stdout=subprocess.PIPE, text=True)
+                               "--steps", str(steps), "--warmup", str(max(1, warmup))], stdout=subprocess.PIPE,
+                              text=True)
              for p, k in zip(ups, share) if k]
     res = []
     for pr in procs:
@@ -199,6 +200,7 @@ def main():
     # ---- headline: exactly K timed steps at S streams per GPU
     barrier()
     sync_device()
+    cpu0 = tun.serve.cpu_s() + tun.proxy.cpu_s() if tun else 0.0
     t0 = time.perf_counter()
     head = {"requests": 0, "errors": 0}
     if lg:
@@ -212,6 +214,9 @@ def main():
     barrier()
     sync_device()
     dt_wall = time.perf_counter() - t0
+    # CPU the two tunnel processes used in the timed region (every thread,
+    # busy polling included): the price of the latency, reported beside it.
+    tunnel_cpu_s = (tun.serve.cpu_s() + tun.proxy.cpu_s() - cpu0) if tun else 0.0
 
     # ---- untimed: curve points + direct baseline (the same load straight to
     # the upstream; node topology: S x N streams split evenly over the N upstreams)
@@ -219,7 +224,9 @@ def main():
     for s in sorted({int(x) for x in a.curve.split(",") if x} | {a.streams}) if drive else []:
         n = s * (world if node else 1)
         tun_r = head if s == a.streams else loadgen(tun.proxy_port, n, a.curve_steps, warmup=1)
-        dir_r = direct(ups, n, a.curve_steps)
+        # The direct leg of the headline point runs the headline's own steps
+        # and warm-up: added p50 / p99 then compare samples of equal size.
+        dir_r = direct(ups, n, a.steps, a.warmup) if s == a.streams else direct(ups, n, a.curve_steps)
         curve[str(s)] = {
             "tunneled_req_s": tun_r["req_s"],
             "direct_req_s": dir_r["req_s"],
@@ -297,6 +304,8 @@ def main():
             },
             "added_p50_ttft_ms": added,
             "added_p99_ttft_ms": added_p99,
+            "tunnel_cpu_s_rank0": round(tunnel_cpu_s, 3),
+            "tunnel_cpu_cores_rank0": round(tunnel_cpu_s / dt_wall, 4) if dt_wall > 0 else None,
             "p50_ttft_ms": head["p50_ttft_ms"],
             "p99_ttft_ms": head["p99_ttft_ms"],
             "step_max_ttft_ms_rank0": head.get("step_max_ttft_ms"),

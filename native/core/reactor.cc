@@ -200,9 +200,16 @@ static int wait_events(int epfd, epoll_event* evs, int max, int64_t timeout_us) 
 
 void Reactor::run_once(int64_t timeout_us) {
   epoll_event evs[256];
-  if (busy_poll_us_ && timeout_us > 0 && now_us() - last_io_us_ < busy_poll_us_) timeout_us = 0;
+  bool spin = false;
+  if (busy_poll_us_ && timeout_us > 0 && now_us() - last_io_us_ < busy_poll_us_) {
+    timeout_us = 0;
+    spin = true;
+  }
   const uint64_t t_wait = now_us();
-  if (wake_us_) win_busy_us_ += t_wait - wake_us_;
+  // An empty polling turn is idle time, not load (a transport reads load() to
+  // decide whether to hold small flushes: counting the spin would make every
+  // polling loop look half busy).
+  if (wake_us_ && !idle_turn_) win_busy_us_ += t_wait - wake_us_;
   if (t_wait - win_start_us_ >= 2000) {
     load_ = win_start_us_ ? double(win_busy_us_) / double(t_wait - win_start_us_) : 0.0;
     win_start_us_ = t_wait;
@@ -217,6 +224,10 @@ void Reactor::run_once(int64_t timeout_us) {
     win_busy_us_ = 0;
   }
   if (n > 0 && busy_poll_us_) last_io_us_ = now_us();
+  // Nothing ready, no timer due and nothing posted: no hook has new work.
+  idle_turn_ = spin && n <= 0 && posted_.empty() &&
+               (timer_order_.empty() || timer_order_.begin()->first > wake_us_);
+  if (idle_turn_) return;
   for (int i = 0; i < n; i++) {
     uint64_t tag = evs[i].data.u64;
     if (tag == kWakeTag) {

@@ -95,6 +95,7 @@ class Reactor {
   uint64_t busy_poll_us_ = 0;
   uint64_t last_io_us_ = 0;
   uint64_t win_start_us_ = 0, win_busy_us_ = 0, wake_us_ = 0;
+  bool idle_turn_ = false;  // the last turn was an empty busy-polling one
   double load_ = 0.0;
   uint64_t gen_ = 1;
   std::unordered_map<int, FdEntry> fds_;

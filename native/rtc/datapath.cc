@@ -16,6 +16,8 @@
 
 #include "core/log.h"
 #include "core/profiler.h"
+#include "core/reactor.h"
+#include "tunnel/metrics.h"
 
 #ifndef UDP_SEGMENT
 #define UDP_SEGMENT 103
@@ -359,9 +361,9 @@ void TxLaneState::send(SealedBatch& sb, int fd, const SockAddr& to) {
 // ------------------------------------------------------------------ RX reader
 
 RxReader::RxReader(int fd, const SockAddr& remote, std::shared_ptr<const RecordKeys> keys, Deliver deliver, uint64_t id,
-                   size_t slot)
+                   size_t slot, bool adaptive)
     : fd_(fd), stop_fd_(eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC)), remote_(remote), keys_(std::move(keys)),
-      deliver_(std::move(deliver)), id_(id), slot_(slot), pool_(slot) {
+      deliver_(std::move(deliver)), id_(id), slot_(slot), pool_(slot), adaptive_(adaptive), active_(!adaptive) {
   th_ = std::thread([this] {
     sigset_t mask;
     sigemptyset(&mask);
@@ -384,6 +386,15 @@ RxReader::~RxReader() {
   cv_.notify_all();
   th_.join();
   if (stop_fd_ >= 0) ::close(stop_fd_);
+}
+
+void RxReader::engage() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    active_.store(true, std::memory_order_release);
+  }
+  engages.fetch_add(1, std::memory_order_relaxed);
+  cv_.notify_all();
 }
 
 void RxReader::done() {
@@ -462,10 +473,42 @@ void RxReader::run() {
   mmsghdr msgs[kBatch];
   iovec iovs[kBatch];
   sockaddr_storage from[kBatch];
-  alignas(cmsghdr) char ctrl[kBatch][CMSG_SPACE(sizeof(int)) + CMSG_SPACE(sizeof(uint32_t))];
+  alignas(cmsghdr) char ctrl[kBatch][CMSG_SPACE(sizeof(int)) + CMSG_SPACE(sizeof(uint32_t)) +
+                                      CMSG_SPACE(sizeof(timespec))];
   RawBufPtr slots[kBatch];
+  const bool traced = trace::enabled();
   pollfd pf[2] = {{fd_.fd, POLLIN, 0}, {stop_fd_, POLLIN, 0}};
+  uint64_t win_start = 0, win_bytes = 0;  // adaptive: what was read since win_start
   while (!stop_.load(std::memory_order_acquire)) {
+    if (!active_.load(std::memory_order_acquire)) {
+      // Paused (adaptive): the association thread reads the socket.
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [this] {
+        return stop_.load(std::memory_order_acquire) || active_.load(std::memory_order_acquire);
+      });
+      win_start = Reactor::now_us();
+      win_bytes = 0;
+      continue;
+    }
+    if (adaptive_) {
+      const uint64_t now = Reactor::now_us();
+      if (now - win_start >= kIdleUs) {
+        if (win_bytes < kIdleBytes) {
+          // Interactive again: pause, and give the socket back behind every
+          // burst already delivered (the association thread reads on in order).
+          active_.store(false, std::memory_order_release);
+          handbacks.fetch_add(1, std::memory_order_relaxed);
+          auto hb = std::make_unique<Burst>();
+          hb->reader = id_;
+          hb->handback = true;
+          outstanding_.fetch_add(1, std::memory_order_acq_rel);
+          deliver_(std::move(hb));
+          continue;
+        }
+        win_start = now;
+        win_bytes = 0;
+      }
+    }
     if (outstanding_.load(std::memory_order_acquire) >= kMaxOutstanding) {
       // Back-pressure: the association thread is kMaxOutstanding bursts
       // behind, so the socket buffer holds what arrives meanwhile. Escape
@@ -484,15 +527,22 @@ void RxReader::run() {
         continue;
       }
     }
-    if (poll(pf, 2, 100) <= 0 || (pf[1].revents & POLLIN)) continue;  // the loop head sees stop_
+    // Adaptive: wake by the end of the window even when nothing arrives.
+    int wait_ms = 100;
+    if (adaptive_) {
+      const uint64_t end = win_start + kIdleUs, now = Reactor::now_us();
+      wait_ms = now >= end ? 1 : int((end - now + 999) / 1000);
+    }
+    if (poll(pf, 2, wait_ms) <= 0 || (pf[1].revents & POLLIN)) continue;  // the loop head sees stop_ / the window
     auto burst = std::make_unique<Burst>();
     burst->reader = id_;
+    const size_t slot = slot_.load(std::memory_order_relaxed);
     for (int round = 0; round < 8; round++) {
       for (int i = 0; i < kBatch; i++) {
         slots[i] = pool_.get();
         memset(&msgs[i], 0, sizeof msgs[i]);
         iovs[i].iov_base = slots[i]->data.get();
-        iovs[i].iov_len = slot_;
+        iovs[i].iov_len = slot;
         msgs[i].msg_hdr.msg_iov = &iovs[i];
         msgs[i].msg_hdr.msg_iovlen = 1;
         msgs[i].msg_hdr.msg_name = &from[i];
@@ -502,13 +552,26 @@ void RxReader::run() {
       }
       const int n = recvmmsg(fd_.fd, msgs, kBatch, MSG_DONTWAIT, nullptr);
       if (n <= 0) break;
+      if (round == 0 && traced) {
+        burst->t_read = Reactor::now_us();
+        burst->t_kernel = trace::kernel_rx_us(&msgs[0].msg_hdr);
+      }
       for (int i = 0; i < n; i++) {
         SockAddr a;
         memcpy(&a.ss, &from[i], msgs[i].msg_hdr.msg_namelen);
         a.len = msgs[i].msg_hdr.msg_namelen;
         const uint32_t total = msgs[i].msg_len;
-        if (msgs[i].msg_hdr.msg_flags & MSG_TRUNC) {  // larger than a slot: never expected, counted
-          truncated.fetch_add(1, std::memory_order_relaxed);
+        if (msgs[i].msg_hdr.msg_flags & MSG_TRUNC) {
+          // Larger than a slot: the peer sends bigger packets than this side's
+          // path settings predicted. This one is lost (counted, SCTP resends
+          // it); later reads use 64 KiB slots so the resend gets through.
+          if (truncated.fetch_add(1, std::memory_order_relaxed) == 0)
+            LOG_WARN(kT, "UDP datagram larger than the %zu-byte receive slot; reading with 64 KiB slots from now on",
+                     slot);
+          if (slot_.load(std::memory_order_relaxed) < 65536) {
+            slot_.store(65536, std::memory_order_relaxed);
+            pool_ = BufPool(65536);
+          }
           continue;
         }
         uint32_t ovfl = 0;
@@ -522,9 +585,11 @@ void RxReader::run() {
         }
       }
       for (auto& sl : slots) sl.reset();  // the burst holds what it uses
-      if (n < kBatch || burst->opened.bytes >= burst_cap_) break;
+      if (n < kBatch || slot_.load(std::memory_order_relaxed) != slot) break;
     }
     if (burst->opened.recs.empty() && burst->raw.empty()) continue;
+    win_bytes += burst->opened.bytes;
+    for (auto& r : burst->raw) win_bytes += r.len;
     bursts.fetch_add(1, std::memory_order_relaxed);
     outstanding_.fetch_add(1, std::memory_order_acq_rel);
     deliver_(std::move(burst));
@@ -539,32 +604,21 @@ size_t datapath_inline_bytes() {
   return v;
 }
 
-double datapath_inline_load() {
-  static const double v = [] {
-    const char* e = getenv("TUNNEL_INLINE_LOAD_PCT");
-    // Off by default (1.0: a loop is never that busy): on the MI355X host the
-    // 64 x 1 MB echo lost 4-14 % with it at 0.5, and the node row's 1024-stream
-    // tail did not separate from run-to-run noise (profiles/r04/inl_ab, node9).
-    return e && *e ? double(strtoull(e, nullptr, 10)) / 100.0 : 1.0;
-  }();
-  return v;
-}
-
 namespace {
 std::atomic<int> g_rx_reader{-1};  // -1: from the environment
 }
 
-bool rx_reader_enabled() {
+int rx_reader_mode() {
   int v = g_rx_reader.load(std::memory_order_relaxed);
   if (v < 0) {
     const char* e = getenv("TUNNEL_RX_READER");
-    v = (e && *e == '0') ? 0 : 1;
+    v = !(e && *e) ? kRxReaderAdaptive : *e == '0' ? kRxReaderOff : *e == '1' ? kRxReaderAlways : kRxReaderAdaptive;
     g_rx_reader.store(v, std::memory_order_relaxed);
   }
-  return v != 0;
+  return v;
 }
 
-void set_rx_reader_enabled(bool on) { g_rx_reader.store(on ? 1 : 0, std::memory_order_relaxed); }
+void set_rx_reader_mode(int mode) { g_rx_reader.store(mode, std::memory_order_relaxed); }
 
 bool datapath_enabled() {
   static const bool v = [] {

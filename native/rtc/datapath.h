@@ -232,6 +232,17 @@ class TxLaneState {
 // thread calls done() once it has processed one, and the reader stops
 // reading (the socket buffer holds, then drops) while kMaxOutstanding bursts
 // wait, so a slow association thread never piles up pinned buffers.
+//
+// Engaged only under bulk (adaptive, the default): every datagram the reader
+// reads reaches the association thread through a second wake-up, and on the
+// MI355X host that hop put the headline's added p50 TTFT at 0.244 ms against
+// 0.162 ms with the association thread reading the socket itself (3
+// interleaved runs each, profiles/r05/b01). So an adaptive reader starts
+// paused: the association thread reads the socket (one thread per hop for
+// tokens and requests) until its receive rate is bulk-like, then hands the
+// socket over (engage()); the reader hands it back — a Burst with `handback`
+// set, after everything it read — once it has read less than kIdleBytes in
+// kIdleUs.
 class RxReader {
  public:
   struct Raw {
@@ -244,21 +255,32 @@ class RxReader {
     std::vector<Raw> raw;   // datagrams for the ICE agent / DTLS state machine
     uint64_t reader = 0;    // id of the RxReader that read it (done() goes to that one only)
     int si = -1;            // the ICE socket index it was read from (set by the deliver hook)
+    bool handback = false;  // adaptive reader: paused; the socket is the association thread's again
+    uint64_t t_read = 0, t_kernel = 0;  // traced runs: when it was read / queued by the kernel (us)
   };
   using Deliver = std::function<void(std::unique_ptr<Burst>)>;
   static constexpr int kMaxOutstanding = 4;
+  static constexpr uint64_t kIdleUs = 20000;         // adaptive: hand back after this long ...
+  static constexpr size_t kIdleBytes = 256 * 1024;   // ... with less than this read in it (12.8 MB/s)
 
   // `slot`: receive buffer per datagram — 64 KiB when the socket coalesces
   // (UDP GRO), else the largest datagram the path carries (a 1200-byte
-  // datagram in a 64 KiB slot pinned ~50x its size per burst).
+  // datagram in a 64 KiB slot pinned ~50x its size per burst); a datagram
+  // larger than the slot (a peer with larger packets) grows it to 64 KiB.
+  // `adaptive`: start paused, run only between engage() and a handback.
   RxReader(int fd, const SockAddr& remote, std::shared_ptr<const RecordKeys> keys, Deliver deliver, uint64_t id = 0,
-           size_t slot = 65536);
+           size_t slot = 65536, bool adaptive = false);
   uint64_t id() const { return id_; }
-  size_t slot() const { return slot_; }
+  size_t slot() const { return slot_.load(std::memory_order_relaxed); }
   ~RxReader();  // stops and joins; bursts already delivered stay valid
   RxReader(const RxReader&) = delete;
   RxReader& operator=(const RxReader&) = delete;
   void done();  // association thread: one delivered burst processed
+  // Association thread, adaptive reader: it has detached the socket from its
+  // reactor (everything it read is processed); the reader reads from now on.
+  void engage();
+  bool engaged() const { return active_.load(std::memory_order_acquire); }
+  std::atomic<uint64_t> engages{0}, handbacks{0};
 
   // waits: back-pressure pauses (the association thread kMaxOutstanding
   // bursts behind); escapes: reads taken anyway because the socket buffer was
@@ -277,19 +299,14 @@ class RxReader {
   std::shared_ptr<const RecordKeys> keys_;
   Deliver deliver_;
   uint64_t id_ = 0;
-  // TUNNEL_RX_BURST_KB: hand a burst over once it holds this much (default:
-  // whatever 8 recvmmsg rounds found). A smaller burst is processed — and
-  // acknowledged — sooner, at more hand-offs per byte.
-  size_t burst_cap_ = [] {
-    const char* e = getenv("TUNNEL_RX_BURST_KB");
-    return e && *e ? size_t(std::max(16, atoi(e))) * 1024 : SIZE_MAX;
-  }();
-  bool escape_ = [] {  // TUNNEL_RX_ESCAPE=0: pause however full the socket buffer is (A/B, tests)
+  bool escape_ = [] {  // TUNNEL_RX_ESCAPE=0: pause however full the socket buffer is (tests)
     const char* e = getenv("TUNNEL_RX_ESCAPE");
     return !(e && *e == '0');
   }();
-  size_t slot_ = 65536;
+  std::atomic<size_t> slot_{65536};
   BufPool pool_{65536};
+  bool adaptive_ = false;
+  std::atomic<bool> active_{true};
   std::mutex mu_;
   std::condition_variable cv_;
   std::atomic<int> outstanding_{0};
@@ -298,9 +315,13 @@ class RxReader {
 };
 
 size_t datapath_inline_bytes();  // TUNNEL_DATAPATH_INLINE_BYTES (default 32 KiB)
-double datapath_inline_load();   // TUNNEL_INLINE_LOAD_PCT / 100 (default 1.0 = off): loop load above which nothing is sealed inline
-bool rx_reader_enabled();        // TUNNEL_RX_READER (default on; 0 = the association thread reads the socket)
-void set_rx_reader_enabled(bool on);  // tests: both receive paths in one process
+// TUNNEL_RX_READER: 0 = the association thread always reads the socket, 1 =
+// a reader always does (round 4), unset = adaptive (engaged under bulk).
+enum RxReaderMode { kRxReaderOff = 0, kRxReaderAlways = 1, kRxReaderAdaptive = 2 };
+int rx_reader_mode();
+void set_rx_reader_mode(int mode);  // tests: every receive path in one process
+inline bool rx_reader_enabled() { return rx_reader_mode() != kRxReaderOff; }
+inline void set_rx_reader_enabled(bool on) { set_rx_reader_mode(on ? kRxReaderAlways : kRxReaderOff); }
 bool datapath_enabled();         // TUNNEL_DATAPATH (default on; 0 = everything on the association thread)
 
 }  // namespace p2pt::rtc

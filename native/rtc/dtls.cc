@@ -736,13 +736,12 @@ void DtlsTransport::commit_tx() {
   }
   TxTarget t;
   const bool direct = tx_target_ && tx_target_(t) && t.fd >= 0;
-  Reactor* loop = Reactor::current();
-  if (!direct || (tx_pend_->bytes < datapath_inline_bytes() && tx_lane_->idle() && tx_send_lane_->idle() &&
-                  !(loop && loop->load() >= datapath_inline_load()))) {
+  if (!direct || (tx_pend_->bytes < datapath_inline_bytes() && tx_lane_->idle() && tx_send_lane_->idle())) {
     // A small flush with nothing ahead of it on the lane (or no direct path):
     // sealed here, sent by the ICE agent's flush — no thread hop on the
-    // latency path of a token. With TUNNEL_INLINE_LOAD_PCT set, a loop that
-    // is itself that busy hands even small flushes to the lanes.
+    // latency path of a token. (Handing small flushes to the lanes off a
+    // >= 50 %-busy loop cost the 64 x 1 MB echo 4-14 % on the MI355X host,
+    // profiles/r04/inl_ab: removed in round 5.)
     seal_inline(*tx_pend_);
     tx_pend_->clear();
     inline_tx_batches_++;

@@ -109,6 +109,9 @@ class DtlsTransport : public std::enable_shared_from_this<DtlsTransport> {
   const TxLaneState* tx_lane_state() const { return tx_state_.get(); }
   uint64_t lane_tx_batches() const { return lane_tx_batches_; }
   uint64_t lane_rx_batches() const { return lane_rx_batches_; }
+  // Receive bursts on the RX lane not yet back on this thread (a socket
+  // reader engaging now could overtake them).
+  int rx_outstanding() const { return rx_outstanding_ + (rx_pend_.recs.empty() ? 0 : 1); }
   // Records dropped on receive (failed authentication, replayed or older than
   // the 64-record replay window): loss the SCTP layer sees as a hole.
   uint64_t rx_dropped() const { return rx_dropped_; }

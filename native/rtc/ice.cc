@@ -1,5 +1,7 @@
 #include "rtc/ice.h"
 
+#include "tunnel/metrics.h"
+
 #include <netinet/udp.h>
 
 #include <arpa/inet.h>
@@ -143,8 +145,10 @@ void IceAgent::set_state(IceState s) {
 }
 
 void IceAgent::enable_gro(int fd) {
-  if (getenv("TUNNEL_NO_GRO")) return;
   int one = 1;
+  // Traced runs: kernel receive timestamps (the udp_kernel hop of a frame).
+  if (trace::enabled()) setsockopt(fd, SOL_SOCKET, SO_TIMESTAMPNS, &one, sizeof one);
+  if (getenv("TUNNEL_NO_GRO")) return;
   if (setsockopt(fd, SOL_UDP, UDP_GRO, &one, sizeof one) == 0) gro_enabled_ = true;
 }
 
@@ -580,6 +584,13 @@ bool IceAgent::detach_reader(int* fd, int* si, SockAddr* remote) {
   return true;
 }
 
+bool IceAgent::reader_target(int* fd, int* si, SockAddr* remote) const {
+  size_t co;
+  if (detached_ >= 0 || !direct_target(fd, remote, &co)) return false;
+  *si = locals_[sel_local_].sock;
+  return true;
+}
+
 void IceAgent::reattach_reader(int si) {
   if (detached_ != si) return;
   detached_ = -1;
@@ -774,6 +785,7 @@ void IceAgent::flush() {
     }
     i = j;
   }
+  trace::tx_done();
 }
 
 int IceAgent::local_for_socket(int si, bool relay) const {
@@ -791,7 +803,8 @@ void IceAgent::on_readable(int si) {
   sockaddr_storage from[kBatch];
   // Room for UDP_GRO and SO_RXQ_OVFL (a truncated GRO cmsg would read a
   // coalesced burst as one datagram).
-  alignas(cmsghdr) char ctrl[kBatch][CMSG_SPACE(sizeof(int)) + CMSG_SPACE(sizeof(uint32_t))];
+  alignas(cmsghdr) char ctrl[kBatch][CMSG_SPACE(sizeof(int)) + CMSG_SPACE(sizeof(uint32_t)) +
+                                      CMSG_SPACE(sizeof(timespec))];
   for (int round = 0; round < 8 && !closed_; round++) {
     for (int i = 0; i < kBatch; i++) rxpool_[i].reset();
     for (int i = 0; i < kBatch; i++) {
@@ -811,6 +824,10 @@ void IceAgent::on_readable(int si) {
     }
     int n = recvmmsg(socks_[si].fd, msgs, kBatch, MSG_DONTWAIT, nullptr);
     if (n <= 0) break;
+    if (round == 0 && trace::enabled()) {
+      const uint64_t now = Reactor::now_us();
+      trace::set_rx(trace::kernel_rx_us(&msgs[0].msg_hdr), now, now);
+    }
     for (int i = 0; i < n && !closed_; i++) {
       if (nat_mode_) {  // private address: unreachable from outside the emulated NAT
         nat_dropped_++;
@@ -819,6 +836,7 @@ void IceAgent::on_readable(int si) {
       SockAddr a;
       memcpy(&a.ss, &from[i], msgs[i].msg_hdr.msg_namelen);
       a.len = msgs[i].msg_hdr.msg_namelen;
+      rx_bytes_ += msgs[i].msg_len;
       dispatch_segments(si, a, rxpool_[i], msgs[i].msg_len, gro_segment(&msgs[i].msg_hdr));
     }
     if (n < kBatch) break;

@@ -136,6 +136,12 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   // False when direct_target() does not hold.
   bool detach_reader(int* fd, int* si, SockAddr* remote);
   void reattach_reader(int si);
+  // The socket detach_reader() would hand over, without handing it over (a
+  // reader that starts paused and engages only under bulk).
+  bool reader_target(int* fd, int* si, SockAddr* remote) const;
+  // Bytes this agent's own reads took off its sockets (cumulative): the
+  // association thread's receive rate, which decides when a reader engages.
+  uint64_t rx_bytes() const { return rx_bytes_; }
   // From that reader, on this agent's thread: a datagram it did not handle
   // (STUN, non-application records, other senders), and proof of life for
   // the ones it did (consent freshness).
@@ -305,6 +311,7 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   bool gro_enabled_ = false;
  public:
   uint64_t gso_sends_ = 0, gro_batches_ = 0;  // counters (metrics, tests)
+  uint64_t rx_bytes_ = 0;
   uint64_t send_drops_ = 0;  // messages flush() dropped (EAGAIN / unreachable)
  private:
   DgVec drop_;                      // reserve_append target with no path

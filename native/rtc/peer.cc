@@ -222,6 +222,7 @@ void PeerConnection::flush() {
   // new pair's instead of forwarding everything through the slow path.
   if (rx_reader_ && ice_ && ice_->path_generation() != rx_reader_gen_) restart_rx_reader();
   if (dtls_) dtls_->commit_rx();
+  if (rx_reader_ && !rx_engaged_) maybe_engage_rx_reader();
   if (sctp_ && coalesce_us_) {
     // A busy loop with a partial packet queued: let the next pass (or the
     // timer, at most coalesce_us after the previous flush) add to it.
@@ -246,12 +247,19 @@ void PeerConnection::flush() {
 }
 
 void PeerConnection::start_rx_reader() {
-  if (rx_reader_ || closed_ || !dtls_ || !ice_ || !dtls_->lanes_enabled() || !rx_reader_enabled()) return;
+  if (rx_reader_ || closed_ || !dtls_ || !ice_ || !dtls_->lanes_enabled()) return;
+  const int mode = rx_reader_mode();
+  if (mode == kRxReaderOff) return;
+  const bool adaptive = mode == kRxReaderAdaptive;
   int fd = -1, si = -1;
   SockAddr remote;
-  if (!ice_->detach_reader(&fd, &si, &remote)) return;
+  // Adaptive: the reader starts paused and this thread keeps the socket.
+  if (!(adaptive ? ice_->reader_target(&fd, &si, &remote) : ice_->detach_reader(&fd, &si, &remote))) return;
   rx_reader_si_ = si;
   rx_reader_gen_ = ice_->path_generation();
+  rx_engaged_ = !adaptive;
+  rx_win_start_us_ = Reactor::now_us();
+  rx_win_bytes0_ = ice_->rx_bytes();
   std::weak_ptr<PeerConnection> w = shared_from_this();
   Reactor* r = &r_;
   rx_reader_ = std::make_unique<RxReader>(fd, remote, dtls_->record_keys(), [w, r, si](std::unique_ptr<RxReader::Burst> b) {
@@ -260,8 +268,33 @@ void PeerConnection::start_rx_reader() {
     r->post_threadsafe([w, sb] {
       if (auto s = w.lock()) s->on_rx_burst(*sb);
     });
-  }, ++rx_reader_ids_, rx_slot_bytes());
-  LOG_DEBUG(kT, "UDP socket reader on for %s", remote.str().c_str());
+  }, ++rx_reader_ids_, rx_slot_bytes(), adaptive);
+  LOG_DEBUG(kT, "UDP socket reader %s for %s", adaptive ? "ready (engaged under bulk)" : "on", remote.str().c_str());
+}
+
+// Adaptive reader: hand the socket over once this thread's receive rate is
+// bulk-like. Not while receive bursts are out on the RX lane: their records
+// come back through this thread's queue and the reader's first burst could
+// overtake them.
+void PeerConnection::maybe_engage_rx_reader() {
+  const uint64_t now = Reactor::now_us(), rx = ice_->rx_bytes();
+  if (rx - rx_win_bytes0_ < kEngageBytes) {
+    if (now - rx_win_start_us_ >= kEngageWindowUs) {
+      rx_win_start_us_ = now;
+      rx_win_bytes0_ = rx;
+    }
+    return;
+  }
+  if (dtls_->rx_outstanding()) return;
+  int fd = -1, si = -1;
+  SockAddr remote;
+  if (!ice_->detach_reader(&fd, &si, &remote)) return;
+  if (si != rx_reader_si_) {  // not the socket the reader holds (the path generation check restarts it)
+    ice_->reattach_reader(si);
+    return;
+  }
+  rx_engaged_ = true;
+  rx_reader_->engage();
 }
 
 // Receive slot of the socket reader: with UDP GRO a read may hold ~50
@@ -278,7 +311,8 @@ void PeerConnection::restart_rx_reader() {
   LOG_DEBUG(kT, "selected pair changed (generation %llu -> %llu): restarting the UDP socket reader",
             static_cast<unsigned long long>(rx_reader_gen_), static_cast<unsigned long long>(ice_->path_generation()));
   rx_reader_.reset();  // joins; bursts it already posted still arrive (their done() is ignored)
-  ice_->reattach_reader(rx_reader_si_);
+  if (rx_engaged_) ice_->reattach_reader(rx_reader_si_);
+  rx_engaged_ = false;
   rx_reader_si_ = -1;
   rx_reader_restarts_++;
   start_rx_reader();
@@ -287,8 +321,21 @@ void PeerConnection::restart_rx_reader() {
 // A burst from the socket reader: opened records up the stack (replay check
 // in DTLS), the rest through the ICE agent as if it had read them.
 void PeerConnection::on_rx_burst(RxReader::Burst& b) {
-  if (rx_reader_ && rx_reader_->id() == b.reader) rx_reader_->done();
+  const bool current = rx_reader_ && rx_reader_->id() == b.reader;
+  if (current) rx_reader_->done();
   if (closed_) return;
+  if (b.t_read) trace::set_rx(b.t_kernel, b.t_read, Reactor::now_us());
+  if (b.handback) {
+    // The reader paused behind its last burst: this thread reads again (and
+    // at once, whatever arrived since).
+    if (current && rx_engaged_) {
+      rx_engaged_ = false;
+      rx_win_start_us_ = Reactor::now_us();
+      rx_win_bytes0_ = ice_ ? ice_->rx_bytes() : 0;
+      if (ice_) ice_->reattach_reader(rx_reader_si_);
+    }
+    return;
+  }
   auto self = shared_from_this();
   if (!b.opened.recs.empty()) {
     if (ice_) ice_->note_rx();

@@ -170,18 +170,25 @@ class PeerConnection : public std::enable_shared_from_this<PeerConnection> {
   uint64_t coalesce_timer_ = 0;
   uint64_t coalesced_flushes_ = 0;  // flushes held back (metrics, tests)
   bool closed_ = false;
-  // The selected direct pair's socket read off this thread (rtc/datapath.h).
+  // The selected direct pair's socket read off this thread (rtc/datapath.h):
+  // always (TUNNEL_RX_READER=1), or, adaptive, only while the receive rate
+  // is bulk-like: engaged once this thread has read kEngageBytes within
+  // kEngageWindowUs, until the reader hands the socket back.
+  static constexpr uint64_t kEngageWindowUs = 2000;
+  static constexpr uint64_t kEngageBytes = 256 * 1024;  // 128 MB/s
   std::unique_ptr<RxReader> rx_reader_;
   int rx_reader_si_ = -1;
   uint64_t rx_reader_gen_ = 0;   // ICE path generation the reader was started for
   uint64_t rx_reader_ids_ = 0;
+  bool rx_engaged_ = false;      // the reader (not this thread) reads the socket
+  uint64_t rx_win_start_us_ = 0, rx_win_bytes0_ = 0;
   void restart_rx_reader();
+  void maybe_engage_rx_reader();
   size_t rx_slot_bytes() const;
  public:
   uint64_t rx_reader_restarts_ = 0;
- private:
- public:
   const RxReader* rx_reader() const { return rx_reader_.get(); }
+  bool rx_reader_engaged() const { return rx_engaged_; }
 };
 
 }  // namespace p2pt::rtc

@@ -91,6 +91,7 @@ struct SctpAssociation::Chunk {
   bool retransmit = false;  // marked for retransmission
   bool fast = false;        // marked by fast retransmit (may bypass cwnd once)
   bool probe = false;       // latest transmission was a tail-loss probe
+  bool copied = false;      // a redundant copy went out (a duplicate report may be that copy's)
 };
 
 struct SctpAssociation::InChunk {
@@ -994,8 +995,15 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
     stats_.probe_ambiguous++;
   }
   // Duplicate TSN reports: copies the peer already had. A retransmission of
-  // the current loss episode reported back this way was not needed.
-  if (ep_active_ && ndup && ep_rtx_ > 0) ep_rtx_ = std::max<int64_t>(0, ep_rtx_ - int64_t(ndup));
+  // the current loss episode reported back this way was not needed — but only
+  // a TSN this episode retransmitted counts, once: a duplicate of a redundant
+  // copy (TUNNEL_SCTP_DUP) or of an earlier episode's retransmission says
+  // nothing about this one's losses.
+  if (ep_active_ && ndup && ep_rtx_ > 0) {
+    const uint8_t* d = c + 12 + 4u * ngap;
+    for (uint16_t i = 0; i < ndup && ep_rtx_ > 0; i++)
+      if (ep_rtx_tsns_.erase(rd32(d + 4u * i))) ep_rtx_--;
+  }
   if (cum_advanced && newest_cum_sent) rack_xmit_us_ = std::max(rack_xmit_us_, newest_cum_sent);
   const uint64_t rtt_sample = cum_sample && !cum_probe ? cum_sample : (cum_sample ? 0 : gap_sample);
   if (rtt_sample) {
@@ -1127,6 +1135,7 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
   if (random_episode_ && !tsn_lt(cum, random_exit_)) random_episode_ = false;
   if (ep_active_ && !tsn_lt(cum, ep_exit_)) {
     ep_active_ = false;
+    ep_rtx_tsns_.clear();
     if (ep_rtx_ == 0 && ep_undo_cwnd_ > cwnd_) {  // nothing it marked was lost: undo the cut
       cwnd_ = ep_undo_cwnd_;
       ssthresh_ = std::max(ssthresh_, ep_undo_ssthresh_);
@@ -1181,6 +1190,7 @@ void SctpAssociation::loss_response(bool random_loss, bool over_bdp, uint64_t no
     ep_undo_cwnd_ = cwnd_;
     ep_undo_ssthresh_ = ssthresh_;
     ep_rtx_ = 0;
+    ep_rtx_tsns_.clear();
   }
   ep_exit_ = next_tsn_ - 1;
   ssthresh_ = std::max(keep, 4 * cfg_.mtu);
@@ -1639,6 +1649,8 @@ void SctpAssociation::flush() {
     pkt.insert(pkt.end(), padded - ch->len, 0);
     pkt_len_ += need;
     if (copy) {  // redundant copy: bytes on the wire only, no sender state
+      ch->copied = true;
+      ep_rtx_tsns_.erase(ch->tsn);
       stats_.dup_copies_sent++;
       return;
     }
@@ -1673,7 +1685,9 @@ void SctpAssociation::flush() {
     ch->miss = 0;
     add_data(ch, false);
     stats_.retransmits++;
-    if (ep_active_) ep_rtx_++;
+    // Counted once per TSN; a chunk that also went out as a redundant copy
+    // counts but can never be undone (its duplicate may be the copy's).
+    if (ep_active_ && (ch->copied || ep_rtx_tsns_.insert(ch->tsn).second)) ep_rtx_++;
     sent_any = true;
   }
   // New data. After each drain the producer (data channel -> frame scheduler)
@@ -1805,6 +1819,7 @@ bool SctpAssociation::dup_small_enabled() const {
     const char* e = getenv("TUNNEL_SCTP_DUP");
     return e && *e ? atoi(e) : -1;
   }();
+  if (cfg_.dup_small >= 0) return cfg_.dup_small != 0;
   if (mode >= 0) return mode != 0;
   const uint64_t losses = stats_.fast_retransmits + stats_.tlp_probes + stats_.t3_expirations;
   return losses >= 8 && losses * 400 > stats_.data_chunks_sent;

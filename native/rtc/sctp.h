@@ -26,6 +26,7 @@
 #include <memory>
 #include <set>
 #include <string>
+#include <unordered_set>
 #include <vector>
 
 #include "core/buf.h"
@@ -50,6 +51,9 @@ struct SctpConfig {
   // INIT-ACK; once both sides did, packets after setup carry checksum 0 and a
   // received checksum of 0 is not verified.
   bool zero_checksum = false;
+  // Redundant copies of small whole messages: 1 always, 0 never, -1 from
+  // TUNNEL_SCTP_DUP or, unset, once the path has shown random loss.
+  int dup_small = -1;
 };
 
 struct SctpStats {
@@ -130,6 +134,7 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   State state() const { return state_; }
   bool established() const { return state_ == State::Established; }
   const SctpStats& stats() const { return stats_; }
+  void set_dup_small(int mode) { cfg_.dup_small = mode; }  // tests: SctpConfig::dup_small after creation
   size_t cwnd() const { return cwnd_; }
   uint64_t srtt_us() const { return srtt_us_; }
   uint64_t min_rtt_us() const { return min_rtt_us_; }  // smallest RTT sample: the path's base RTT
@@ -284,7 +289,8 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   bool ep_active_ = false;
   uint32_t ep_exit_ = 0;
   size_t ep_undo_cwnd_ = 0, ep_undo_ssthresh_ = 0;
-  int64_t ep_rtx_ = 0;  // retransmissions sent in the episode, less duplicate reports of them
+  int64_t ep_rtx_ = 0;  // TSNs retransmitted in the episode, less those reported back as duplicates
+  std::unordered_set<uint32_t> ep_rtx_tsns_;  // this episode's retransmitted TSNs a duplicate report may undo
   bool dr_active_ = false, dr_limited_ = false;
   uint32_t dr_end_ = 0;
   uint64_t dr_start_us_ = 0, dr_bytes_ = 0;

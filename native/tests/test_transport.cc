@@ -105,6 +105,12 @@ struct SctpPair {
   }
 };
 
+// The socket reader's mode for one test (the default, adaptive, after it).
+struct ReaderMode {
+  explicit ReaderMode(int m) { set_rx_reader_mode(m); }
+  ~ReaderMode() { set_rx_reader_mode(kRxReaderAdaptive); }
+};
+
 std::string payload(size_t n, uint32_t seed) {
   std::string s(n, '\0');
   std::mt19937 g(seed);
@@ -206,6 +212,51 @@ TEST(sctp_wan_tail_losses_recover_without_t3) {
   // still delivered each message exactly once (got_b holds 1200, above).
   CHECK(p.a->stats().dup_copies_sent > 100);
   printf("  redundant copies: %llu\n", (unsigned long long)p.a->stats().dup_copies_sent);
+}
+
+TEST(sctp_redundant_copies_never_undo_a_real_loss_episode) {
+  // the spurious-loss undo counted every duplicate TSN report
+  // against the episode's retransmissions. With redundant copies of small
+  // messages on, the copy of a token that arrived next to its original comes
+  // back as a duplicate too, and brought the count to 0 in real loss episodes:
+  // the cwnd cut was undone although the retransmissions were needed. Here
+  // only data packets are lost (SACKs always arrive, no reordering), so every
+  // retransmission is needed and no episode may be undone.
+  SctpPair p(0, 0, 0, 1200, false, false, 100);
+  p.link.fixed_delay_us = 10000;
+  std::mt19937 rng(7);
+  std::weak_ptr<SctpAssociation> to_b = p.b;
+  p.link.blackout = [&](const std::weak_ptr<SctpAssociation>& to) {
+    const bool data_dir = !to.owner_before(to_b) && !to_b.owner_before(to);
+    return data_dir && p.a->established() && std::uniform_real_distribution<double>(0, 1)(rng) < 0.03;
+  };
+  p.a->connect();
+  p.b->connect();
+  CHECK(p.r.run_until([&] { return p.a->established() && p.b->established(); }, 5000));
+  p.a->set_dup_small(1);
+  size_t sent = 0;
+  uint64_t next = Reactor::now_us();
+  // Tokens every 2 ms with an 8 KB body every 10th: loss episodes with small
+  // whole messages (copied) in flight.
+  CHECK(p.r.run_until([&] {
+    if (Reactor::now_us() >= next && sent < 1500) {
+      const size_t n = sent % 10 == 0 ? 8000 : 150;
+      p.a->send(1, 53, {Bytes::copy(payload(n, uint32_t(sent)))});
+      sent++;
+      next += 2000;
+    }
+    return sent == 1500 && p.got_b.size() == sent && p.a->bytes_in_flight() == 0;
+  }, 30000));
+  CHECK_EQ(p.got_b.size(), size_t(1500));
+  const auto& st = p.a->stats();
+  printf("  %llu dropped, %llu retransmits, %llu copies, %llu dup TSNs at the receiver, %llu spurious undos\n",
+         (unsigned long long)p.link.dropped, (unsigned long long)st.retransmits,
+         (unsigned long long)st.dup_copies_sent, (unsigned long long)p.b->stats().dup_tsns,
+         (unsigned long long)st.spurious_undos);
+  CHECK(p.link.dropped > 20);
+  CHECK(st.dup_copies_sent > 100);
+  CHECK(p.b->stats().dup_tsns > 100);
+  CHECK_EQ(st.spurious_undos, uint64_t(0));
 }
 
 TEST(sctp_tail_blackout_recovers_without_rtt_inflation) {
@@ -749,12 +800,15 @@ TEST(rx_reader_opens_app_records_and_passes_the_rest) {
 }
 
 TEST(peerconnection_bulk_through_crypto_lanes) {
-  // Standard and jumbo paths, each with the socket reader (default) and with
-  // the association thread reading the socket (records opened on the RX lane).
-  for (int mode = 0; mode < 4; mode++) {
+  // Standard and jumbo paths, each with the socket reader always on, with the
+  // association thread reading the socket (records opened on the RX lane), and
+  // with the adaptive reader (the default: engaged by the bulk, handed back
+  // once it is over, small messages after it read by the association thread).
+  for (int mode = 0; mode < 6; mode++) {
     const int jumbo = mode & 1;
-    const bool reader = mode < 2;
-    set_rx_reader_enabled(reader);
+    const int rmode = mode >> 1 == 0 ? kRxReaderAlways : mode >> 1 == 1 ? kRxReaderOff : kRxReaderAdaptive;
+    const bool reader = rmode != kRxReaderOff;
+    set_rx_reader_mode(rmode);
     Reactor r;
     PcConfig cfg;
     cfg.ice.include_loopback = true;
@@ -815,6 +869,26 @@ TEST(peerconnection_bulk_through_crypto_lanes) {
       CHECK(d->lane_tx_batches() > 0);
       if (reader) CHECK(ans->rx_reader() && ans->rx_reader()->records.load() > 0);
       else CHECK(!ans->rx_reader() && ans->dtls()->lane_rx_batches() > 0);
+      if (rmode == kRxReaderAdaptive && ans->rx_reader()) {
+        CHECK(ans->rx_reader()->engages.load() >= 1);
+        // Idle for more than the reader's window: both readers hand back, and
+        // small messages then arrive through the association thread.
+        r.run_until([] { return false; }, 2 * RxReader::kIdleUs / 1000 + 20);
+        CHECK(!ans->rx_reader_engaged() && !off->rx_reader_engaged());
+        CHECK(ans->rx_reader()->handbacks.load() >= 1);
+        const uint64_t before = ans->rx_reader()->records.load();
+        size_t small = 0;
+        ans->on_data_channel = nullptr;
+        rdc->on_message = [&](Bytes m) { small += m.size() == 5 + 150; };
+        for (int i = 0; i < 20; i++) {
+          uint8_t hdr[5] = {21, 0, 0, 0, 9};
+          dc->send(hdr, 5, Bytes::copy(payload(150, uint32_t(i))));
+          r.run_until([] { return false; }, 1);
+        }
+        CHECK(r.run_until([&] { return small == 20; }, 3000));
+        CHECK_EQ(ans->rx_reader()->records.load(), before);
+        CHECK(!ans->rx_reader_engaged());
+      }
     }
     printf("  %s: %zu + %zu MB, lane tx batches %llu, inline %llu, rx batches %llu, reader records %llu\n",
            off->describe_path().c_str(), bytes_ans >> 20, bytes_off >> 20,
@@ -824,7 +898,7 @@ TEST(peerconnection_bulk_through_crypto_lanes) {
     off->close();
     ans->close();
   }
-  set_rx_reader_enabled(true);
+  set_rx_reader_mode(kRxReaderAdaptive);
 }
 
 // The socket reader follows the selected pair: when the ICE agent's path
@@ -834,7 +908,7 @@ TEST(peerconnection_bulk_through_crypto_lanes) {
 // flight across the restart arrives whole and in order.
 TEST(rx_reader_restarts_on_path_change) {
   if (!AesGcm::supported()) return;
-  set_rx_reader_enabled(true);
+  ReaderMode always(kRxReaderAlways);
   Reactor r;
   PcConfig cfg;
   cfg.ice.include_loopback = true;
@@ -898,7 +972,7 @@ TEST(rx_reader_restarts_on_path_change) {
 // escape (it reads on once the socket buffer is half full) there are none.
 TEST(slow_association_thread_loses_nothing_uncounted) {
   if (!AesGcm::supported()) return;
-  set_rx_reader_enabled(true);
+  ReaderMode always(kRxReaderAlways);
   // Small socket buffers (256 KiB asked, so the kernel's doubling gives 512)
   // make the pressure real on any host; run once with the reader's escape
   // and once without it (the drops then happen, and must all be counted).
@@ -1114,7 +1188,7 @@ TEST(fragmented_messages_arrive_as_zero_copy_chains) {
 // nothing is truncated.
 TEST(rx_reader_slots_follow_the_path_without_gro) {
   if (!AesGcm::supported()) return;
-  set_rx_reader_enabled(true);
+  ReaderMode always(kRxReaderAlways);
   setenv("TUNNEL_NO_GRO", "1", 1);
   Reactor r;
   PcConfig cfg;

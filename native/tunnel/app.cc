@@ -151,7 +151,7 @@ int run_app(const AppConfig& cfg) {
   r.set_busy_poll_us(cfg.busy_poll_us);
   // Worker threads for per-stream HTTP work (tunnel/workers.h); they outlive
   // sessions, so reconnects reuse them.
-  WorkerPool pool(cfg.workers);
+  WorkerPool pool(cfg.workers, cfg.busy_poll_us);
   if (pool.size()) LOG_INFO(kT, "%zu worker threads (streams beyond %zu per session spill onto them)", pool.size(),
                             cfg.inline_streams);
   struct State {

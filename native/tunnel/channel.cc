@@ -78,7 +78,9 @@ void TcpMessageChannel::on_data(const uint8_t* p, size_t n) {
       }
       need_ = len;
       cur_.clear();
-      cur_.reserve(len);
+      // Up front only what arrived plus a window's worth: the length prefix
+      // alone must not make a peer's 16 MiB allocation (it grows as data does).
+      cur_.reserve(std::min<size_t>(len, std::max<size_t>(n, 256 * 1024)));
     }
     const size_t take = std::min(n, need_ - cur_.size());
     cur_.insert(cur_.end(), p, p + take);

@@ -1,5 +1,11 @@
 #include "tunnel/metrics.h"
 
+#include <sys/socket.h>
+#include <time.h>
+
+#include <cstring>
+#include <vector>
+
 #include <algorithm>
 
 #include <unistd.h>
@@ -230,5 +236,52 @@ void flush() {
   if (!k) return;
   std::lock_guard<std::mutex> lk(k->mu);
   k->drain();
+}
+
+namespace {
+thread_local uint64_t t_rx_kernel = 0, t_rx_read = 0, t_rx_assoc = 0;
+thread_local std::vector<std::pair<const char*, uint32_t>> t_tx_pending;
+}  // namespace
+
+void set_rx(uint64_t kernel_us, uint64_t read_us, uint64_t assoc_us) {
+  t_rx_kernel = kernel_us;
+  t_rx_read = read_us;
+  t_rx_assoc = assoc_us;
+}
+
+void rx_stamps(const char* role, uint32_t sid) {
+  if (!sink() || !t_rx_read) return;
+  if (t_rx_kernel) event_at(role, sid, "udp_kernel", t_rx_kernel);
+  event_at(role, sid, "udp_read", t_rx_read);
+  event_at(role, sid, "rx_assoc", t_rx_assoc);
+}
+
+void mark_tx(const char* role, uint32_t sid) {
+  if (sink() && t_tx_pending.size() < 4096) t_tx_pending.emplace_back(role, sid);
+}
+
+void tx_done() {
+  if (t_tx_pending.empty()) return;
+  const uint64_t now = Reactor::now_us();
+  for (auto& p : t_tx_pending) event_at(p.first, p.second, "udp_tx", now);
+  t_tx_pending.clear();
+}
+
+uint64_t kernel_rx_us(const void* mh_) {
+  const msghdr* mh = static_cast<const msghdr*>(mh_);
+  for (cmsghdr* c = CMSG_FIRSTHDR(const_cast<msghdr*>(mh)); c; c = CMSG_NXTHDR(const_cast<msghdr*>(mh), c)) {
+    if (c->cmsg_level == SOL_SOCKET && c->cmsg_type == SCM_TIMESTAMPNS) {
+      timespec ts;
+      memcpy(&ts, CMSG_DATA(c), sizeof ts);
+      timespec rt, mt;
+      clock_gettime(CLOCK_REALTIME, &rt);
+      clock_gettime(CLOCK_MONOTONIC, &mt);
+      const int64_t real_ns = int64_t(ts.tv_sec) * 1000000000 + ts.tv_nsec;
+      const int64_t off = (int64_t(mt.tv_sec) - int64_t(rt.tv_sec)) * 1000000000 + (mt.tv_nsec - rt.tv_nsec);
+      const int64_t mono_ns = real_ns + off;
+      return mono_ns > 0 ? uint64_t(mono_ns / 1000) : 0;
+    }
+  }
+  return 0;
 }
 }  // namespace p2pt::trace

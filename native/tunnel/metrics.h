@@ -39,4 +39,18 @@ void event(const char* role, uint32_t stream_id, const char* ev);
 // connection's accept stamped once its first request has a stream id.
 void event_at(const char* role, uint32_t stream_id, const char* ev, uint64_t t_us);
 void flush();  // buffered mode (TUNNEL_TRACE_BUFFERED=1): write out what is held
+
+// Transport hops of a traced frame (this thread's current datagrams):
+// the receive side records when the kernel queued the datagram (SO_TIMESTAMPNS,
+// converted to CLOCK_MONOTONIC), when a thread read it, and when the
+// association thread took it up; rx_stamps() writes them for a stream as
+// udp_kernel / udp_read / rx_assoc. The send side queues a stream with
+// mark_tx() and the datagram flush that carries it stamps udp_tx (tx_done()).
+void set_rx(uint64_t kernel_us, uint64_t read_us, uint64_t assoc_us);
+void rx_stamps(const char* role, uint32_t stream_id);
+void mark_tx(const char* role, uint32_t stream_id);
+void tx_done();
+// Monotonic microseconds of a SCM_TIMESTAMPNS (CLOCK_REALTIME) cmsg in the
+// message, 0 if none.
+uint64_t kernel_rx_us(const void* msghdr);
 }  // namespace p2pt::trace

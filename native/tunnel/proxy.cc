@@ -1150,6 +1150,7 @@ void ProxySession::route(const proto::Frame& f) {
         if (!it->second.body_seen) {
           it->second.body_seen = true;
           trace::event("proxy", f.stream_id, "chan_rx");
+          trace::rx_stamps("proxy", f.stream_id);
         }
         Cmd c{Cmd::Body, f.stream_id};
         c.data = f.payload;

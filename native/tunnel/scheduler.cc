@@ -27,7 +27,13 @@ bool FrameScheduler::emit(const proto::Frame& f, bool urgent) {
     const uint64_t key = uint64_t(f.stream_id) << 8;
     switch (f.type) {
       case proto::MsgType::ResBody:
-        if (traced_.insert(key | 1).second) trace::event("serve", f.stream_id, "chan_tx");
+        if (traced_.insert(key | 1).second) {
+          trace::event("serve", f.stream_id, "chan_tx");
+          trace::mark_tx("serve", f.stream_id);
+        }
+        break;
+      case proto::MsgType::ReqHeaders:
+        trace::mark_tx("proxy", f.stream_id);
         break;
       case proto::MsgType::ReqBody:
         if (traced_.insert(key | 2).second) trace::event("proxy", f.stream_id, "chan_tx");

@@ -499,6 +499,7 @@ void ServeSession::handle_frame(const proto::Frame& f) {
       }
       LOG_DEBUG(kT, "request %u %s %s", h.stream_id, h.method.c_str(), h.path.c_str());
       trace::event("serve", h.stream_id, "req_headers");
+      trace::rx_stamps("serve", h.stream_id);
       uint32_t sid = h.stream_id;  // keyed by the JSON stream_id (serve.rs:118)
       Pending p;
       if (const std::string* cl = proto::header_get(h.headers, "content-length")) {

@@ -14,12 +14,12 @@
 
 namespace p2pt {
 
-WorkerThread::WorkerThread(int index) : index_(index) {
+WorkerThread::WorkerThread(int index, uint64_t busy_poll_us) : index_(index) {
   std::promise<Reactor*> ready;
   auto fut = ready.get_future();
   // The reactor is created on its own thread so thread-affine state (the
   // thread_local current reactor) belongs to that thread.
-  th_ = std::thread([this, &ready] {
+  th_ = std::thread([this, &ready, busy_poll_us] {
     // Process signals (Ctrl-C, SIGTERM) belong to the main reactor's signalfd;
     // a worker must never take them with the default action. SIGPROF stays
     // open so the sampling profiler sees worker time too.
@@ -28,6 +28,7 @@ WorkerThread::WorkerThread(int index) : index_(index) {
     for (int sig : {SIGINT, SIGTERM, SIGHUP, SIGQUIT, SIGUSR1, SIGUSR2, SIGPIPE}) sigaddset(&mask, sig);
     pthread_sigmask(SIG_BLOCK, &mask, nullptr);
     auto r = std::make_unique<Reactor>();
+    r->set_busy_poll_us(busy_poll_us);
     Reactor* rp = r.get();
     r_ = std::move(r);
     char name[16];
@@ -67,9 +68,9 @@ int WorkerPool::auto_count() {
   return int(std::clamp<long>(n / 2 - 1, 1, 4));
 }
 
-WorkerPool::WorkerPool(int n) {
+WorkerPool::WorkerPool(int n, uint64_t busy_poll_us) {
   if (n < 0) n = auto_count();
-  for (int i = 0; i < n; i++) threads_.push_back(std::make_unique<WorkerThread>(i + 1));
+  for (int i = 0; i < n; i++) threads_.push_back(std::make_unique<WorkerThread>(i + 1, busy_poll_us));
 }
 
 WorkerPool::~WorkerPool() = default;

@@ -41,7 +41,7 @@ namespace p2pt {
 // A Reactor running on its own thread until destroyed.
 class WorkerThread {
  public:
-  explicit WorkerThread(int index);
+  explicit WorkerThread(int index, uint64_t busy_poll_us = 0);
   ~WorkerThread();
   Reactor& reactor() { return *r_; }
   int index() const { return index_; }
@@ -55,8 +55,8 @@ class WorkerThread {
 // The process's worker threads; they outlive sessions (reconnects reuse them).
 class WorkerPool {
  public:
-  // n < 0: auto_count().
-  explicit WorkerPool(int n);
+  // n < 0: auto_count(). busy_poll_us: Reactor::set_busy_poll_us of each.
+  explicit WorkerPool(int n, uint64_t busy_poll_us = 0);
   ~WorkerPool();
   size_t size() const { return threads_.size(); }
   Reactor& reactor(size_t i) { return threads_[i]->reactor(); }

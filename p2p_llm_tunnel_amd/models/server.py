@@ -516,7 +516,8 @@ class _Stream:
     """Per-request output state on the I/O thread: the writer and the byte
     template around each token piece (token ids render as " t<id>": no JSON
     escaping needed)."""
-    __slots__ = ("writer", "stream", "kind", "rid", "pre", "post", "toks", "done", "detok", "reason", "stop")
+    __slots__ = ("writer", "stream", "kind", "rid", "pre", "post", "toks", "done", "detok", "reason", "stop",
+                 "stop_hit")
 
     def __init__(self, writer, stream, kind, rid, model, detok=None, stop=None):
         self.writer = writer
@@ -527,6 +528,7 @@ class _Stream:
         self.detok = detok  # checkpoint tokenizer: incremental text of this request
         self.reason = "length"
         self.stop = stop  # StopMatcher, or None without stop sequences
+        self.stop_hit = False  # a stop sequence matched (its held-back text is the match, never emitted)
         self.done = asyncio.get_running_loop().create_future()
         m = json.dumps(model)
         if kind == "chat":
@@ -619,6 +621,7 @@ class FrontEnd:
                 if stopped:  # the engine frees the slot on its next step
                     req.cancelled = True
                     st.reason = "stop"
+                    st.stop_hit = True
                     self._finish(req, st)
                 continue
             if st.detok is not None:
@@ -639,8 +642,11 @@ class FrontEnd:
 
     def _finish(self, req, st):
         w = st.writer
-        if st.stop is not None and st.reason != "stop":
-            held = st.stop.flush()  # a held-back tail that never became a stop sequence
+        if st.stop is not None and not st.stop_hit:
+            # A held-back tail that never became a stop sequence: the completion
+            # ended otherwise (length, EOS — also finish_reason "stop"), so it is
+            # real text.
+            held = st.stop.flush()
             if held:
                 self._emit_piece(st, _piece(held))
         if st.stream:

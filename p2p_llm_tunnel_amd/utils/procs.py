@@ -93,6 +93,15 @@ class Proc:
                 self.popen.kill()
                 self.popen.wait()
 
+    def cpu_s(self) -> float:
+        """User + system CPU seconds the process has used so far (all threads)."""
+        try:
+            with open(f"/proc/{self.popen.pid}/stat") as f:
+                fields = f.read().rsplit(")", 1)[1].split()
+            return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
+        except (OSError, IndexError, ValueError):
+            return 0.0
+
     def kill(self):
         if self.popen.poll() is None:
             self.popen.kill()

@@ -16,8 +16,22 @@ generator, joins the per-stream events (all processes stamp CLOCK_MONOTONIC
   serve first_body -> proxy first_body    response crosses the tunnel, split into
     serve first_body -> serve sched_in      upstream reader -> serve association thread
     serve sched_in -> serve chan_tx         frame scheduler (queued behind the channel window?)
-    serve chan_tx -> proxy chan_rx          SCTP, DTLS, UDP, socket reader, proxy association thread
+    serve chan_tx -> proxy chan_rx          SCTP, DTLS, UDP, socket reader, proxy association thread:
+      serve chan_tx -> serve udp_tx           SCTP + DTLS seal + sendmmsg returned
+      serve udp_tx -> proxy udp_kernel        loopback delivery (kernel receive timestamp; may be < 0:
+                                              the kernel stamps before the sender's syscall returns)
+      proxy udp_kernel -> proxy udp_read      the receiving thread's wake-up and recvmmsg
+      proxy udp_read -> proxy rx_assoc        socket reader -> association thread (0 when it reads itself)
+      proxy rx_assoc -> proxy chan_rx         DTLS open + SCTP + frame dispatch
     proxy chan_rx -> proxy first_body       hand-off to the client connection, its write
+  the request crossing, split the same way: proxy req_end -> udp_tx -> serve
+    udp_kernel -> udp_read -> rx_assoc -> req_headers
+  client TTFT (the load generator's p50) minus proxy accept -> first_body: the
+    client's own hops (its write to the proxy's wake-up, the proxy's write to
+    its wake-up)
+
+Tracing is buffered in memory (TUNNEL_TRACE_BUFFERED=1) and written at exit,
+so stamping costs no syscall on the measured path.
 
 --bulk-echo: BASELINE config #3 (N streams x 1 MB POST echoed) as a waterfall.
 Every request is stamped at each hop (TUNNEL_TRACE, buffered), and the steps
@@ -76,7 +90,8 @@ def main():
     mock.wait_for("Mock LLM server running", 10)
     try:
         extra = [x for x in a.extra.split() if x]
-        with Tunnel(f"http://127.0.0.1:{port}", transport=a.transport, env={"TUNNEL_TRACE": trace},
+        with Tunnel(f"http://127.0.0.1:{port}", transport=a.transport,
+                    env={"TUNNEL_TRACE": trace, "TUNNEL_TRACE_BUFFERED": "1"},
                     serve_extra=extra, proxy_extra=extra) as t:
             bulk = None
             if a.bulk:
@@ -85,9 +100,10 @@ def main():
                                          "--path", f"/bulk?bytes={64 << 20}", "--events", "none", "--duration-s", "600"],
                                         stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
                 time.sleep(0.5)
-            subprocess.run([binary("tunnel-loadgen"), "--target", f"127.0.0.1:{t.proxy_port}", "--streams",
-                            str(a.streams), "--steps", str(a.requests // a.streams), "--warmup", "1"],
-                           check=True, capture_output=True)
+            lg = subprocess.run([binary("tunnel-loadgen"), "--target", f"127.0.0.1:{t.proxy_port}", "--streams",
+                                 str(a.streams), "--steps", str(a.requests // a.streams), "--warmup", "1"],
+                                check=True, capture_output=True, text=True)
+            client = json.loads(lg.stdout.strip().splitlines()[-1])
             if bulk:
                 bulk.kill()
                 bulk.wait()
@@ -112,7 +128,16 @@ def main():
             # thread, then the hand-off to the client connection and its write
             ("serve", "first_body", "serve", "sched_in"), ("serve", "sched_in", "serve", "chan_tx"),
             ("serve", "chan_tx", "proxy", "chan_rx"),
+            ("serve", "chan_tx", "serve", "udp_tx"), ("serve", "udp_tx", "proxy", "udp_kernel"),
+            ("serve", "chan_tx", "proxy", "udp_kernel"),
+            ("proxy", "udp_kernel", "proxy", "udp_read"), ("proxy", "udp_read", "proxy", "rx_assoc"),
+            ("proxy", "rx_assoc", "proxy", "chan_rx"),
             ("proxy", "chan_rx", "proxy", "first_body"),
+            # the request crossing split the same way
+            ("proxy", "req_end", "proxy", "udp_tx"), ("proxy", "udp_tx", "serve", "udp_kernel"),
+            ("proxy", "req_end", "serve", "udp_kernel"),
+            ("serve", "udp_kernel", "serve", "udp_read"), ("serve", "udp_read", "serve", "rx_assoc"),
+            ("serve", "rx_assoc", "serve", "req_headers"),
             # the upstream's own turnaround (joinable per stream at serve) and
             # the whole time inside the tunnel processes
             ("serve", "upstream_sent", "serve", "first_body"),
@@ -158,8 +183,13 @@ def main():
             if (a_, b_) in e and (c_, d_) in e:
                 w[f"{a_}.{b_} -> {c_}.{d_}"] = e[(c_, d_)] - e[(a_, b_)]
         worst.append(w)
-    res = {"transport": a.transport, "streams": a.streams, "bulk": a.bulk, "extra": a.extra, "hops": out,
+    res = {"transport": a.transport, "streams": a.streams, "bulk": a.bulk, "extra": a.extra,
+           "env": {k: v for k, v in os.environ.items() if k.startswith("TUNNEL_")}, "hops": out,
+           "client_p50_ttft_us": client.get("p50_ttft_ms", 0) * 1000, "client_p99_ttft_us": client.get("p99_ttft_ms", 0) * 1000,
            "worst": worst}
+    inside = out.get("proxy.accept -> proxy.first_body")
+    if inside:
+        res["client_hops_p50_us"] = res["client_p50_ttft_us"] - inside["p50_us"]
     if not join_mock:
         res["note"] = "mock hops omitted: mock trace lines cannot be joined to streams when streams > 1"
     print(json.dumps(res, indent=1))

@@ -152,6 +152,31 @@ def test_stop_sequences_end_completions():
         eng.stop()
 
 
+def test_eos_flushes_a_held_back_tail():
+    """EOS also ends with finish_reason "stop"; a tail the matcher
+    held back because it could begin a stop sequence is real completion text
+    then and must be emitted (streamed and not)."""
+    toks = expected(b"hello", 12)
+    srv, port, eng = _stop_server()
+    srv.eos = frozenset({toks[3]})  # the 4th token is EOS
+    try:
+        text = "".join(f" t{t}" for t in toks[:3])
+        stop = f" t{toks[2]}QQ"  # the 3rd piece is a prefix of it: held back until EOS
+        msgs = [{"role": "user", "content": "hello"}]
+        st, data = _post(port, "/v1/chat/completions", {"messages": msgs, "max_tokens": 12, "stop": stop})
+        j = json.loads(data)
+        assert st == 200 and j["choices"][0]["message"]["content"] == text
+        assert j["choices"][0]["finish_reason"] == "stop"
+        st, data = _post(port, "/v1/chat/completions", {"messages": msgs, "max_tokens": 12, "stop": stop,
+                                                         "stream": True})
+        events = [l[6:] for l in data.split(b"\n") if l.startswith(b"data: ")]
+        objs = [json.loads(e) for e in events[:-1]]
+        assert "".join(o["choices"][0]["delta"].get("content", "") for o in objs) == text
+    finally:
+        srv.shutdown()
+        eng.stop()
+
+
 def test_sampling_refused_on_an_eager_engine():
     """The eager step (CPU stand-ins) has no sampler: a sampled request is
     refused instead of silently answered greedily (advice r3)."""
