@@ -65,6 +65,10 @@ def parse():
                          "this repo's same-host 16 KiB extension (a=x-p2pt-jumbo)")
     ap.add_argument("--no-jumbo-extra", action="store_true",
                     help="skip the untimed jumbo-path point reported beside a std headline")
+    ap.add_argument("--pin", choices=["ccd", "none"], default=os.environ.get("P2PT_BENCH_PIN", "ccd"),
+                    help="ccd (default, one GPU): load generator, mock, serve and proxy on the cores of one L3 "
+                         "domain (utils/pinning.py ccd_plan), the direct leg on the same cores as the tunneled one; "
+                         "none: wherever the scheduler puts them")
     ap.add_argument("--out", default=None, help="also write the JSON line here")
     return ap.parse_args()
 
@@ -112,10 +116,17 @@ def start_mock(kind, interval_ms, tokens, cpus=None, threads=1):
     return p, port
 
 
+PLAN: dict = {}  # role -> CPU list (--pin ccd), {} unpinned
+
+
+def taskset(role):
+    return ["taskset", "-c", PLAN[role]] if PLAN.get(role) else []
+
+
 def loadgen(port, streams, steps, warmup=0, path=None):
     from p2p_llm_tunnel_amd import binary
     extra = ["--path", path] if path else []
-    out = subprocess.run([binary("tunnel-loadgen"), "--target", f"127.0.0.1:{port}", "--streams", str(streams),
+    out = subprocess.run(taskset("loadgen") + [binary("tunnel-loadgen"), "--target", f"127.0.0.1:{port}", "--streams", str(streams),
                           "--steps", str(steps), "--warmup", str(warmup)] + extra, capture_output=True, text=True,
                          timeout=600)
     try:
@@ -131,7 +142,7 @@ def direct(ups, streams, steps, warmup=1):
     from p2p_llm_tunnel_amd import binary
     n = len(ups)
     share = [streams // n + (1 if i < streams % n else 0) for i in range(n)]
-    procs = [subprocess.Popen([binary("tunnel-loadgen"), "--target", f"127.0.0.1:{p}", "--streams", str(k),
+    procs = [subprocess.Popen(taskset("loadgen") + [binary("tunnel-loadgen"), "--target", f"127.0.0.1:{p}", "--streams", str(k),
                                "--steps", str(steps), "--warmup", str(max(1, warmup))], stdout=subprocess.PIPE,
                               text=True)
              for p, k in zip(ups, share) if k]
@@ -161,7 +172,11 @@ def main():
     if dist:
         dist.barrier()
 
-    mock, up_port = start_mock(a.mock, a.interval_ms, a.tokens)
+    global PLAN
+    if a.pin == "ccd" and world == 1:  # one GPU's share of the host; N > 1 ranks leave placement to the scheduler
+        from p2p_llm_tunnel_amd.utils.pinning import ccd_plan
+        PLAN = ccd_plan()
+    mock, up_port = start_mock(a.mock, a.interval_ms, a.tokens, cpus=PLAN.get("mock"))
     node = dist is not None and a.topology == "node"
     ups = [up_port]
     if node:
@@ -172,9 +187,12 @@ def main():
     tun = None
     log_env = {"RUST_LOG": "warn,tunnel::serve=info,tunnel::proxy=info,tunnel::transport=info,tunnel::rtc=info"}
     mtu_flags = ["--no-jumbo-loopback"] if a.mtu == "std" and a.transport == "webrtc" else []
+    pin_s = ["--cpu-affinity", PLAN["serve"]] if PLAN else []
+    pin_p = ["--cpu-affinity", PLAN["proxy"]] if PLAN else []
     upstreams = ",".join(f"http://127.0.0.1:{p}" for p in ups)
     if drive:
-        tun = Tunnel(upstreams, transport=a.transport, env=log_env, serve_extra=mtu_flags, proxy_extra=mtu_flags)
+        tun = Tunnel(upstreams, transport=a.transport, env=log_env, serve_extra=mtu_flags + pin_s,
+                     proxy_extra=mtu_flags + pin_p)
         tun.start(timeout=60)
 
     def barrier():
@@ -190,7 +208,7 @@ def main():
     from p2p_llm_tunnel_amd import binary
     lg = None
     if drive:
-        lg = subprocess.Popen([binary("tunnel-loadgen"), "--target", f"127.0.0.1:{tun.proxy_port}", "--streams",
+        lg = subprocess.Popen(taskset("loadgen") + [binary("tunnel-loadgen"), "--target", f"127.0.0.1:{tun.proxy_port}", "--streams",
                                str(streams), "--steps", str(a.steps), "--warmup", str(max(1, a.warmup)), "--hold", "1"],
                               stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
         ready = lg.stdout.readline()
@@ -247,7 +265,7 @@ def main():
     # Untimed extra: the same headline load on the same-host jumbo path.
     jumbo = None
     if drive and a.mtu == "std" and a.transport == "webrtc" and not a.no_jumbo_extra:
-        with Tunnel(upstreams, transport=a.transport, env=log_env) as tj:
+        with Tunnel(upstreams, transport=a.transport, env=log_env, serve_extra=pin_s, proxy_extra=pin_p) as tj:
             loadgen(tj.proxy_port, streams, max(1, a.warmup))
             r = loadgen(tj.proxy_port, streams, a.steps)
             jp = ""
@@ -301,6 +319,7 @@ def main():
                 "transport": a.transport,
                 "mtu": a.mtu if a.transport == "webrtc" else "n/a",
                 "path_rank0": path,
+                "pinned_rank0": PLAN or None,
             },
             "added_p50_ttft_ms": added,
             "added_p99_ttft_ms": added_p99,

@@ -6,7 +6,7 @@ repetition runs every variant once, in turn, on the same box, so a slow box
 or a noisy minute hits all variants alike; the summary gives the median and
 min-max of each variant's key numbers.
 
-    python bench/ab.py KIND --variants "base: pipe:TUNNEL_TX_PIPELINE=0" --reps 3 \\
+    python bench/ab.py KIND --variants "base: co0:TUNNEL_COALESCE_US=0" --reps 3 \\
         --out gpurun_out/ab/x [--paths std,jumbo] [-- extra args for the bench]
 
 KIND and what one run is:

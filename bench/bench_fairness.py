@@ -14,11 +14,11 @@ link's utilisation and drops.
 
 Competitors (--pairs): ``default:default`` (two tunnels with the shipped
 loss response) and ``default:reno`` (the second serve with
-TUNNEL_SCTP_RANDOM_BETA_PCT=50 and TUNNEL_SCTP_QUEUE_US=0: every loss cuts cwnd
+TUNNEL_SCTP_CC=reno: every loss cuts cwnd
 by half, no delay response — a Reno-like competitor); a single policy (e.g.
 ``reno``) runs one flow alone, the reference for how much a competitor harms
 it. ``keep`` is round 3's default (random losses keep cwnd:
-TUNNEL_SCTP_RANDOM_BETA_PCT=100).
+TUNNEL_SCTP_CC=beta=100).
 
     python bench/bench_fairness.py --rates 50,200 --rtt-ms 20 --losses 0,0.005 --seconds 20
 """
@@ -41,8 +41,8 @@ from p2p_llm_tunnel_amd.utils.turn_server import Link, TurnServer  # noqa: E402
 
 POLICIES = {
     "default": {},
-    "reno": {"TUNNEL_SCTP_RANDOM_BETA_PCT": "50", "TUNNEL_SCTP_QUEUE_US": "0"},
-    "keep": {"TUNNEL_SCTP_RANDOM_BETA_PCT": "100"},
+    "reno": {"TUNNEL_SCTP_CC": "reno"},
+    "keep": {"TUNNEL_SCTP_CC": "beta=100"},
 }
 
 

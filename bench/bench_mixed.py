@@ -151,8 +151,7 @@ def main():
         tl_dir, tl_env = timeline.new_dir()
     if a.profile_dir:
         os.makedirs(a.profile_dir, exist_ok=True)
-        tl_env = dict(tl_env or {}, TUNNEL_PROFILE=os.path.join(os.path.abspath(a.profile_dir), "tunnel.%p.prof"),
-                      TUNNEL_PROFILE_HZ="1000")
+        tl_env = dict(tl_env or {}, TUNNEL_PROFILE=os.path.join(os.path.abspath(a.profile_dir), "tunnel.%p.prof@1000"))
     mock.wait_for("Mock LLM server running", 10)
     trs = [x for x in a.transports.split(",") if x]
     res = {"host": os.uname().nodename, "time": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),

@@ -176,11 +176,10 @@ def main():
             if a.trace:
                 import tempfile
                 trace = tempfile.NamedTemporaryFile(suffix=".jsonl", prefix="p2pt-node-trace-", delete=False).name
-                env.update({"TUNNEL_TRACE": trace, "TUNNEL_TRACE_BUFFERED": "1"})
+                env.update({"TUNNEL_TRACE": trace})
             if a.profile_dir:
                 os.makedirs(a.profile_dir, exist_ok=True)
-                env["TUNNEL_PROFILE"] = os.path.join(os.path.abspath(a.profile_dir), f"tunnel.w{w}.%p.prof")
-                env["TUNNEL_PROFILE_HZ"] = "1000"
+                env["TUNNEL_PROFILE"] = os.path.join(os.path.abspath(a.profile_dir), f"tunnel.w{w}.%p.prof@1000")
             up = ",".join(f"http://127.0.0.1:{p}" for p in ports)
             if trace:
                 traces.append(trace)

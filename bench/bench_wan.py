@@ -3,7 +3,7 @@
 
 Both peers' datagrams go through the ICE agent's WAN shim (native/rtc/ice.cc):
 a bottleneck link of --rate-mbps with a drop-tail queue, a fixed round-trip
-time and Bernoulli loss (TUNNEL_FAULT_RTT_MS / _RATE_MBPS / _LOSS). For each
+time and Bernoulli loss (TUNNEL_FAULT rtt_ms / rate_mbps / loss). For each
 (RTT, loss) it measures
 
   * SSE alone: 8 streams, a token every 10 ms — inter-token latency (ITL);
@@ -90,8 +90,8 @@ def steady_row(mport, rtt, loss, rate, qkb, mb, streams, extra):
     """Steady-state goodput: `streams` downloads of `mb` MB each over the
     emulated path, alone; MB/s against the bottleneck rate, and the CPU share
     of every thread of the sending side (serve) over the transfer."""
-    env = {"TUNNEL_FAULT_RTT_MS": str(rtt), "TUNNEL_FAULT_RATE_MBPS": str(rate), "TUNNEL_FAULT_QUEUE_KB": str(qkb),
-           "TUNNEL_FAULT_LOSS": str(loss), "RUST_LOG": "warn,tunnel::rtc=info,tunnel::serve=info,tunnel::proxy=info"}
+    env = {"TUNNEL_FAULT": f"rtt_ms={rtt},rate_mbps={rate},queue_kb={qkb},loss={loss}",
+           "RUST_LOG": "warn,tunnel::rtc=info,tunnel::serve=info,tunnel::proxy=info"}
     sm, pm = free_port(), free_port()
     with Tunnel(f"http://127.0.0.1:{mport}", transport="webrtc",
                 serve_extra=extra + ["--metrics-listen", f"127.0.0.1:{sm}"],
@@ -164,8 +164,7 @@ def main():
         for rtt in [float(x) for x in a.rtts.split(",") if x]:
             for loss in [float(x) for x in a.losses.split(",") if x]:
                 qkb = a.queue_kb or max(64.0, a.rate_mbps * 1e6 / 8 * rtt / 1e3 / 1024)
-                env = {"TUNNEL_FAULT_RTT_MS": str(rtt), "TUNNEL_FAULT_RATE_MBPS": str(a.rate_mbps),
-                       "TUNNEL_FAULT_QUEUE_KB": str(qkb), "TUNNEL_FAULT_LOSS": str(loss),
+                env = {"TUNNEL_FAULT": f"rtt_ms={rtt},rate_mbps={a.rate_mbps},queue_kb={qkb},loss={loss}",
                        "RUST_LOG": "warn,tunnel::rtc=info,tunnel::serve=info,tunnel::proxy=info"}
                 sm, pm = free_port(), free_port()
                 with Tunnel(f"http://127.0.0.1:{mport}", transport="webrtc",

@@ -55,8 +55,7 @@ def main():
     env = None
     if a.profile_dir:
         os.makedirs(a.profile_dir, exist_ok=True)
-        env = {"TUNNEL_PROFILE": os.path.join(os.path.abspath(a.profile_dir), "tunnel.%p.prof"),
-               "TUNNEL_PROFILE_HZ": os.environ.get("TUNNEL_PROFILE_HZ", "2000")}
+        env = {"TUNNEL_PROFILE": os.path.join(os.path.abspath(a.profile_dir), "tunnel.%p.prof@2000")}
     tl_dir = None
     if a.timeline:
         from p2p_llm_tunnel_amd.utils import timeline

@@ -37,11 +37,6 @@ static void capture() {
   });
 }
 
-bool tx_shared() {
-  const char* e = getenv("TUNNEL_PIN_TX_SHARED");
-  return e && *e == '1';
-}
-
 long process_cpu_count() {
   capture();
   return long(g_cpus.size());
@@ -53,7 +48,6 @@ void pin_this_thread(int tag) {
   const size_t n = g_cpus.size();
   if (n < 2) return;
   size_t slot;
-  const bool shared_tx = tx_shared();
   if (tag == 0) {
     slot = 0;
   } else if (n >= 5) {
@@ -61,10 +55,10 @@ void pin_this_thread(int tag) {
     // talk to the upstreams / clients over TCP) next to the association
     // thread, the socket reader last (on a set that spans two L3 domains,
     // nearest the peer's side); on 5 CPUs the idle RX lane shares the
-    // reader's. TUNNEL_PIN_TX_SHARED=1: the seal and send stages share one
-    // CPU and the workers get it.
-    const size_t nw = n >= 6 ? (shared_tx ? n - 4 : n - 5) : 1;
-    const size_t seal = 1 + nw, send = shared_tx ? seal : seal + 1, reader = send + 1;
+    // reader's. (Seal and send sharing one CPU, the workers getting the
+    // other, lost on the 64 x 1 MB echo: 1576 vs 1940 req/s, profiles/r04/txs30.)
+    const size_t nw = n >= 6 ? n - 5 : 1;
+    const size_t seal = 1 + nw, send = seal + 1, reader = send + 1;
     if (tag >= 1 && tag < 90) slot = 1 + size_t(tag - 1) % nw;
     else if (tag == 90) slot = seal;
     else if (tag == 93) slot = send;

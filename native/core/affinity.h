@@ -25,8 +25,6 @@ bool enabled();
 // and send stages, the socket reader, and last the RX lane (idle while the
 // reader runs) with the second sealer. With fewer CPUs: round robin.
 void pin_this_thread(int tag);
-// TUNNEL_PIN_TX_SHARED=1: the two TX stages share a CPU, one more for workers.
-bool tx_shared();
 // CPUs of the process's set as it was before any thread pinned itself (the
 // calling thread's set when nothing was pinned).
 long process_cpu_count();

@@ -304,14 +304,6 @@ void TcpConn::update_interest() {
 // with a sub-MSS segment unacknowledged. On the MI355X host's 64 x 1 MB echo:
 // +7 % (1200 MTU) and +10 % (jumbo) tunneled req/s (profiles/r04/qa19), and
 // on top of one CPU per thread +21 % / +29 % over neither (pt20).
-// TUNNEL_TCP_QUICKACK=0 turns it off.
-static bool tcp_quickack() {
-  static const bool v = [] {
-    const char* e = getenv("TUNNEL_TCP_QUICKACK");
-    return !(e && *e == '0');
-  }();
-  return v;
-}
 
 void TcpConn::on_events(uint32_t ev) {
   auto self = shared_from_this();
@@ -332,7 +324,7 @@ void TcpConn::on_events(uint32_t ev) {
     if (!paused_ || (ev & (EPOLLHUP | EPOLLERR))) {
       // Bulk reads only: a token-sized read keeps the delayed ACK (one ACK
       // per SSE token would double the loopback packets of a node's streams).
-      if (do_read() >= 16384 && tcp_quickack() && fd_ >= 0 && !ssl_) {
+      if (do_read() >= 16384 && fd_ >= 0 && !ssl_) {
         int one = 1;
         setsockopt(fd_, IPPROTO_TCP, TCP_QUICKACK, &one, sizeof one);
       }
@@ -447,7 +439,7 @@ void TcpConn::do_write() {
       }
     } else {
       // Up to 512 pieces per writev: a body relayed as a chain of SCTP
-      // fragment views (TUNNEL_SCTP_CHAIN=1) is ~55 pieces per 64 KiB frame.
+      // fragment views (PcConfig::message_chains) is ~55 pieces per 64 KiB frame.
       constexpr int kIov = 512;
       iovec iov[kIov];
       int cnt = 0;

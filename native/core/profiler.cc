@@ -248,9 +248,12 @@ bool start_from_env() {
   const char* p = getenv("TUNNEL_PROFILE");
   if (!p || !*p) return false;
   g_path = p;
-  if (size_t at = g_path.find("%p"); at != std::string::npos) g_path.replace(at, 2, std::to_string(getpid()));
   int hz = 2000;
-  if (const char* h = getenv("TUNNEL_PROFILE_HZ")) hz = std::min(20000, std::max(10, atoi(h)));
+  if (size_t at = g_path.rfind('@'); at != std::string::npos) {  // PATH@HZ
+    hz = std::min(20000, std::max(10, atoi(g_path.c_str() + at + 1)));
+    g_path.resize(at);
+  }
+  if (size_t at = g_path.find("%p"); at != std::string::npos) g_path.replace(at, 2, std::to_string(getpid()));
   g_slots = new Slot[kSlots];
   // Resolve dladdr's lazy state before the first signal.
   Dl_info di;

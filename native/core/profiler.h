@@ -1,7 +1,7 @@
 // In-process sampling CPU profiler for the tunnel binaries (the
 // reference has no profiler hooks at all; this container has no `perf`).
 //
-// TUNNEL_PROFILE=<path> ("%p" = pid) arms ITIMER_PROF at TUNNEL_PROFILE_HZ (default 2000)
+// TUNNEL_PROFILE=<path>[@HZ] ("%p" = pid) arms ITIMER_PROF at HZ (default 2000)
 // (process CPU time: whichever thread runs gets sampled). The SIGPROF handler records the interrupted PC, the
 // word at the stack pointer (the return address when a frameless leaf such as
 // memcpy or an AES routine was interrupted) and up to kDepth frame-pointer

@@ -62,13 +62,6 @@ Bytes Frame::flat_payload() const {
   return Bytes::take(std::move(v));
 }
 
-int64_t flow_window() {
-  static const int64_t w = [] {
-    const char* e = getenv("TUNNEL_FLOW_WINDOW_KB");
-    return e && *e ? int64_t(std::max(64, atoi(e))) * 1024 : kFlowWindow;
-  }();
-  return w;
-}
 
 bool decode_chain(const Bytes& raw, std::vector<Bytes>& more, Frame& out, std::string* err) {
   if (more.empty() || raw.size() < kHeaderLen) {

@@ -175,9 +175,9 @@ uint32_t credit_bytes(const Frame& f);
 // "flow" extension: initial per-stream, per-direction body credit, and the
 // backlog below which a receiver hands consumed bytes back as credit.
 constexpr int64_t kFlowWindow = 256 * 1024;
-// The initial per-stream window both peers assume: kFlowWindow, or
-// TUNNEL_FLOW_WINDOW_KB (A/B; both peers must be given the same value).
-int64_t flow_window();
+// The initial per-stream window both peers assume (a 1 MiB window lost on
+// the MI355X host's 64 x 1 MB echo at jumbo MTU, profiles/r04/flow_ab).
+inline int64_t flow_window() { return kFlowWindow; }
 constexpr size_t kFlowGrantMin = 16 * 1024;
 
 // "flow" receive-window autotuning, done by the receiver alone (no wire

@@ -40,11 +40,10 @@ Lane::Lane(const char* name) {
     for (int sig : {SIGINT, SIGTERM, SIGHUP, SIGQUIT, SIGUSR1, SIGUSR2, SIGPIPE}) sigaddset(&mask, sig);
     pthread_sigmask(SIG_BLOCK, &mask, nullptr);
     pthread_setname_np(pthread_self(), n.c_str());
-    // T90 seal / T94 second sealer / T93 send / T91 rx in profiles and timelines
-    profiler::register_thread(n.find("-txsend") != std::string::npos  ? 93
-                              : n.find("-seal2") != std::string::npos ? 94
-                              : n.find("-tx") != std::string::npos    ? 90
-                                                                      : 91);
+    // T90 seal / T93 send / T91 rx in profiles and timelines
+    profiler::register_thread(n.find("-txsend") != std::string::npos ? 93
+                              : n.find("-tx") != std::string::npos   ? 90
+                                                                     : 91);
     run();
   });
 }
@@ -211,28 +210,7 @@ void TxLaneState::run(const TxBatch& b, const RecordKeys& k, int fd, const SockA
   send(one_, fd, to);
 }
 
-static size_t seal_split_bytes() {
-  static const size_t v = [] {
-    const char* e = getenv("TUNNEL_SEAL_SPLIT_KB");
-    // Off by default: on the MI355X host the mixed row's jumbo download gained
-    // (0.391 -> 0.433 of direct) but the 64 x 1 MB echo lost (1797 -> 1539
-    // req/s jumbo, same box): with the serve pinned to 6 CPUs the second
-    // sealer competes with the other six threads (profiles/r04/mix17, split17).
-    return (e && *e ? size_t(strtoull(e, nullptr, 10)) : size_t(0)) * 1024;
-  }();
-  return v;
-}
-
-TxLaneState::TxLaneState() : split_bytes_(seal_split_bytes()) {}
-
-void TxLaneState::seal_range(const TxBatch& b, const RecordKeys& k, SealedBatch& sb, size_t lo, size_t hi) {
-  iovec iov[64];
-  for (size_t i = lo; i < hi; i++) {
-    const auto& r = b.recs[i];
-    int cnt = b.gather(r, iov, 64);
-    seal_record(*k.w, k.wiv, sb.out.data() + offs_[i], r.type, r.seq, iov, cnt, r.total);
-  }
-}
+TxLaneState::TxLaneState() = default;
 
 void TxLaneState::seal(const TxBatch& b, const RecordKeys& k, size_t coalesce, SealedBatch& sb) {
   // Seal every record into one contiguous buffer; datagram boundaries are
@@ -251,24 +229,11 @@ void TxLaneState::seal(const TxBatch& b, const RecordKeys& k, size_t coalesce, S
     off += sz;
   }
   if (out_.size() < off) out_.resize(off);
-  const size_t split = split_bytes_;
-  if (split && off >= split && n >= 2) {
-    // First half (by bytes) on the helper, the rest here; both write disjoint
-    // ranges of out_ and read the batch and keys only.
-    size_t mid = 0;
-    while (mid + 1 < n && offs_[mid + 1] < off / 2) mid++;
-    mid = std::max<size_t>(mid, 1);
-    if (!helper_) helper_ = std::make_unique<Lane>("p2pt-dtls-seal2");
-    std::atomic<bool> done{false};
-    helper_->submit([&, mid] {
-      seal_range(b, k, sb, 0, mid);
-      done.store(true, std::memory_order_release);
-    });
-    seal_range(b, k, sb, mid, n);
-    while (!done.load(std::memory_order_acquire)) std::this_thread::yield();
-    split_batches.fetch_add(1, std::memory_order_relaxed);
-  } else {
-    seal_range(b, k, sb, 0, n);
+  iovec iov[64];
+  for (size_t i = 0; i < n; i++) {
+    const auto& r = b.recs[i];
+    const int cnt = b.gather(r, iov, 64);
+    seal_record(*k.w, k.wiv, out_.data() + offs_[i], r.type, r.seq, iov, cnt, r.total);
   }
   records.fetch_add(b.recs.size(), std::memory_order_relaxed);
   batches.fetch_add(1, std::memory_order_relaxed);
@@ -596,17 +561,14 @@ void RxReader::run() {
   }
 }
 
-size_t datapath_inline_bytes() {
-  static const size_t v = [] {
-    const char* e = getenv("TUNNEL_DATAPATH_INLINE_BYTES");
-    return e && *e ? size_t(strtoull(e, nullptr, 10)) : size_t(32 * 1024);
-  }();
-  return v;
-}
 
 namespace {
 std::atomic<int> g_rx_reader{-1};  // -1: from the environment
+std::atomic<bool> g_rx_escape{true};
 }
+
+bool rx_escape_enabled() { return g_rx_escape.load(std::memory_order_relaxed); }
+void set_rx_escape_enabled(bool on) { g_rx_escape.store(on, std::memory_order_relaxed); }
 
 int rx_reader_mode() {
   int v = g_rx_reader.load(std::memory_order_relaxed);
@@ -620,12 +582,5 @@ int rx_reader_mode() {
 
 void set_rx_reader_mode(int mode) { g_rx_reader.store(mode, std::memory_order_relaxed); }
 
-bool datapath_enabled() {
-  static const bool v = [] {
-    const char* e = getenv("TUNNEL_DATAPATH");
-    return !(e && *e == '0');
-  }();
-  return v;
-}
 
 }  // namespace p2pt::rtc

@@ -194,35 +194,28 @@ class TxLaneState {
   void seal(const TxBatch& b, const RecordKeys& k, size_t coalesce, SealedBatch& out);
   // Send stage: sends a sealed batch to target (runs on the send lane).
   void send(SealedBatch& s, int fd, const SockAddr& to);
-  // Both stages in a row (tests; the single-lane path).
+  // Both stages in a row (tests).
   void run(const TxBatch& b, const RecordKeys& k, int fd, const SockAddr& to, size_t coalesce);
-  // Batches of at least this many bytes are sealed by two threads (0: never).
-  void set_split_bytes(size_t n) { split_bytes_ = n; }
   // Sealed batches are recycled between the stages (buffers allocated once).
   std::shared_ptr<SealedBatch> get_sealed();
   void put_sealed(std::shared_ptr<SealedBatch> s);
   // send_drops: datagrams dropped (socket buffer still full after kSendWaitMs
   // of POLLOUT waits, or unreachable); send_waits: POLLOUT waits taken.
   std::atomic<uint64_t> batches{0}, records{0}, datagrams{0}, gso_msgs{0}, send_drops{0}, send_waits{0};
-  std::atomic<uint64_t> split_batches{0};  // batches sealed by two threads
   static constexpr int kSendWaitMs = 20;
 
  private:
-  void seal_range(const TxBatch& b, const RecordKeys& k, SealedBatch& sb, size_t lo, size_t hi);
   SealedBatch one_;  // run()'s buffer
-  // Large batches are sealed by two threads: a helper takes the first half of
-  // the records while the seal lane does the rest (record offsets are fixed
-  // before either starts). On the MI355X host's mixed row the seal lane was
-  // at >= 90 % CPU in 73-96 % of its active intervals at 1200-byte MTU
-  // (profiles/r04/co16). TUNNEL_SEAL_SPLIT_KB: batch size from which to split
-  // (0 = never, the default; see seal_split_bytes()).
-  size_t split_bytes_;           // TUNNEL_SEAL_SPLIT_KB * 1024 unless set
-  std::unique_ptr<Lane> helper_;
   std::vector<size_t> offs_;    // record offsets in out (seal stage only)
   bool gso_ok_ = true;  // send stage only
   std::mutex mu_;
   std::vector<std::shared_ptr<SealedBatch>> free_;
 };
+
+// Tests: a paused reader's escape (it reads on once the socket buffer is half
+// full) on or off for readers created afterwards (default on).
+bool rx_escape_enabled();
+void set_rx_escape_enabled(bool on);
 
 // Socket reader: the selected pair's UDP socket read on a thread of its own
 // (recvmmsg + GRO), application records from the selected remote opened
@@ -299,10 +292,7 @@ class RxReader {
   std::shared_ptr<const RecordKeys> keys_;
   Deliver deliver_;
   uint64_t id_ = 0;
-  bool escape_ = [] {  // TUNNEL_RX_ESCAPE=0: pause however full the socket buffer is (tests)
-    const char* e = getenv("TUNNEL_RX_ESCAPE");
-    return !(e && *e == '0');
-  }();
+  bool escape_ = rx_escape_enabled();
   std::atomic<size_t> slot_{65536};
   BufPool pool_{65536};
   bool adaptive_ = false;
@@ -314,7 +304,10 @@ class RxReader {
   std::thread th_;
 };
 
-size_t datapath_inline_bytes();  // TUNNEL_DATAPATH_INLINE_BYTES (default 32 KiB)
+// Flushes and receive bursts below this are sealed / opened on the association
+// thread itself (no hand-off on a token's path).
+constexpr size_t kInlineBytes = 32 * 1024;
+inline size_t datapath_inline_bytes() { return kInlineBytes; }
 // TUNNEL_RX_READER: 0 = the association thread always reads the socket, 1 =
 // a reader always does (round 4), unset = adaptive (engaged under bulk).
 enum RxReaderMode { kRxReaderOff = 0, kRxReaderAlways = 1, kRxReaderAdaptive = 2 };
@@ -322,6 +315,5 @@ int rx_reader_mode();
 void set_rx_reader_mode(int mode);  // tests: every receive path in one process
 inline bool rx_reader_enabled() { return rx_reader_mode() != kRxReaderOff; }
 inline void set_rx_reader_enabled(bool on) { set_rx_reader_mode(on ? kRxReaderAlways : kRxReaderOff); }
-bool datapath_enabled();         // TUNNEL_DATAPATH (default on; 0 = everything on the association thread)
 
 }  // namespace p2pt::rtc

@@ -340,8 +340,20 @@ void DtlsTransport::bio_wrote(const uint8_t* p, size_t n) {
 
 // TLS 1.2 key block for the AES-GCM suites (RFC 5246 §6.3, RFC 5288 §3):
 // client_write_key | server_write_key | client_write_IV[4] | server_write_IV[4].
+// TUNNEL_DTLS_RECORDS: the record layer after the handshake. Unset: this
+// build's own (vector AES-GCM where the CPU has VAES, OpenSSL's EVP cipher
+// otherwise); "evp": own records, EVP cipher; "openssl": OpenSSL's record
+// layer throughout (a standard DTLS 1.2 stack on the wire, for interop tests).
+static std::string record_layer() {
+  static const std::string v = [] {
+    const char* e = getenv("TUNNEL_DTLS_RECORDS");
+    return std::string(e ? e : "");
+  }();
+  return v;
+}
+
 void DtlsTransport::setup_fast_path() {
-  if (getenv("TUNNEL_DTLS_OPENSSL_RECORDS")) return;  // diagnostics: keep OpenSSL's record layer
+  if (record_layer() == "openssl") return;  // diagnostics: keep OpenSSL's record layer
   const SSL_CIPHER* c = SSL_get_current_cipher(ssl_);
   if (!c) return;
   uint16_t id = SSL_CIPHER_get_protocol_id(c);
@@ -425,7 +437,7 @@ void DtlsTransport::setup_fast_path() {
     keys_ = std::make_shared<RecordKeys>();
     memcpy(keys_->wiv, wiv_, 4);
     memcpy(keys_->riv, riv_, 4);
-    if (probe_ok && AesGcm::supported() && !getenv("TUNNEL_DTLS_EVP")) {
+    if (probe_ok && AesGcm::supported() && record_layer() != "evp") {
       auto w = std::make_shared<AesGcm>(), r = std::make_shared<AesGcm>();
       uint8_t ct[sizeof kProbe];
       if (w->init(wkey, klen) && r->init(rkey, klen) &&
@@ -700,7 +712,7 @@ void DtlsTransport::flush_batch() {
 }
 
 void DtlsTransport::enable_lanes(std::function<bool(TxTarget&)> target) {
-  if (tx_lane_ || !lanes_possible() || !datapath_enabled()) return;
+  if (tx_lane_ || !lanes_possible()) return;
   tx_target_ = std::move(target);
   tx_state_ = std::make_shared<TxLaneState>();
   tx_pool_ = std::make_shared<TxBatchPool>();
@@ -753,24 +765,9 @@ void DtlsTransport::commit_tx() {
   lane_tx_batches_++;
   // Seal stage, then the send stage on its own thread: while one batch is
   // in sendmmsg the next is being encrypted (wire order is the batch order).
-  // TUNNEL_TX_PIPELINE=0 keeps both stages on the seal thread (round-3 lane).
-  static const bool pipelined = [] {
-    const char* e = getenv("TUNNEL_TX_PIPELINE");
-    return !(e && e[0] == '0');
-  }();
+  // (Both stages on one thread lost: 0.633 against 0.729 of direct on the
+  // 1200-MTU 64 x 1 MB echo, profiles/r04/pipe_ab.)
   Lane* send_lane = tx_send_lane_.get();
-  if (!pipelined) {
-    tx_lane_->submit([b = std::move(b), st = tx_state_, k = keys_, fd = lane_fd_, to = t.to, co = t.coalesce,
-                      pool = tx_pool_]() mutable {
-      auto sb = st->get_sealed();
-      st->seal(*b, *k, co, *sb);
-      b->clear();
-      pool->put(std::move(b));
-      st->send(*sb, fd->fd, to);
-      st->put_sealed(std::move(sb));
-    });
-    return;
-  }
   tx_lane_->submit([b = std::move(b), st = tx_state_, k = keys_, fd = lane_fd_, to = t.to, co = t.coalesce,
                     pool = tx_pool_, send_lane]() mutable {
     auto sb = st->get_sealed();

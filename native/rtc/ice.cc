@@ -144,11 +144,18 @@ void IceAgent::set_state(IceState s) {
   }
 }
 
+bool udp_offload_enabled(const char* which) {
+  const char* e = getenv("TUNNEL_UDP_OFFLOAD");
+  if (!e) return true;
+  const std::string list = std::string(",") + e + ",";
+  return list.find(std::string(",") + which + ",") != std::string::npos;
+}
+
 void IceAgent::enable_gro(int fd) {
   int one = 1;
   // Traced runs: kernel receive timestamps (the udp_kernel hop of a frame).
   if (trace::enabled()) setsockopt(fd, SOL_SOCKET, SO_TIMESTAMPNS, &one, sizeof one);
-  if (getenv("TUNNEL_NO_GRO")) return;
+  if (!udp_offload_enabled("gro")) return;
   if (setsockopt(fd, SOL_UDP, UDP_GRO, &one, sizeof one) == 0) gro_enabled_ = true;
 }
 
@@ -510,19 +517,18 @@ void IceAgent::send(const uint8_t* p, size_t n) {
 }
 
 // Test-only fault injection on the datagram path (SURVEY §4.2 "fault
-// injection"): TUNNEL_FAULT_DROP (alias TUNNEL_FAULT_LOSS) / TUNNEL_FAULT_DUP
-// are probabilities, TUNNEL_FAULT_DELAY_MS a uniform random extra delay (which
-// also reorders); STUN (connectivity checks) is exempt from those so the path
-// still comes up. TUNNEL_FAULT_BLACKHOLE=<start_ms>:<duration_ms> drops every
-// outbound datagram, STUN included, in that window after the first send (a
-// path that dies and later comes back).
-//
-// WAN emulation (order-preserving, every datagram): TUNNEL_FAULT_RTT_MS adds
-// half the given round-trip time to each outbound datagram (set it on both
-// peers for that RTT); TUNNEL_FAULT_RATE_MBPS makes the outbound path a
-// bottleneck link of that rate with a drop-tail queue of
-// TUNNEL_FAULT_QUEUE_KB (default 256) — serialization and queueing delay,
-// congestion losses — so SCTP's congestion control meets a realistic path.
+// injection"), one switch: TUNNEL_FAULT="key=value,..." with
+//   drop (alias loss), dup   probabilities per outbound datagram;
+//   delay_ms                 a uniform random extra delay (which also reorders);
+//     STUN (connectivity checks) is exempt from those so the path still comes up;
+//   blackhole=START:LEN      (ms) drops every outbound datagram, STUN included,
+//     in that window after the first send (a path that dies and comes back).
+// WAN emulation (order-preserving, every datagram): rtt_ms adds half the
+// given round-trip time to each outbound datagram (set it on both peers for
+// that RTT); rate_mbps makes the outbound path a bottleneck link of that rate
+// with a drop-tail queue of queue_kb (default 256) — serialization and
+// queueing delay, congestion losses — so SCTP's congestion control meets a
+// realistic path.
 namespace {
 struct FaultCfg {
   double drop = 0, dup = 0;
@@ -534,16 +540,29 @@ struct FaultCfg {
   bool on = false;
   uint64_t rng = 0x9E3779B97F4A7C15ull;
   FaultCfg() {
-    if (const char* e = getenv("TUNNEL_FAULT_DROP")) drop = atof(e);
-    if (const char* e = getenv("TUNNEL_FAULT_LOSS")) drop = atof(e);
-    if (const char* e = getenv("TUNNEL_FAULT_DUP")) dup = atof(e);
-    if (const char* e = getenv("TUNNEL_FAULT_DELAY_MS")) delay_us = uint64_t(atof(e) * 1000);
-    if (const char* e = getenv("TUNNEL_FAULT_RTT_MS")) fixed_us = uint64_t(atof(e) * 500);
-    if (const char* e = getenv("TUNNEL_FAULT_RATE_MBPS")) rate_bps = atof(e) * 1e6;
-    if (const char* e = getenv("TUNNEL_FAULT_QUEUE_KB")) queue_bytes = uint64_t(atof(e) * 1024);
-    if (const char* e = getenv("TUNNEL_FAULT_BLACKHOLE")) {
-      bh_start_ms = strtoull(e, nullptr, 10);
-      if (const char* c = strchr(e, ':')) bh_len_ms = strtoull(c + 1, nullptr, 10);
+    const char* spec = getenv("TUNNEL_FAULT");
+    std::string s = spec ? spec : "";
+    for (size_t p = 0; p < s.size();) {
+      size_t q = s.find(',', p);
+      if (q == std::string::npos) q = s.size();
+      const std::string kv = s.substr(p, q - p);
+      p = q + 1;
+      const size_t eq = kv.find('=');
+      if (eq == std::string::npos) continue;
+      const std::string k = kv.substr(0, eq);
+      const char* v = kv.c_str() + eq + 1;
+      if (k == "drop" || k == "loss") drop = atof(v);
+      else if (k == "dup") dup = atof(v);
+      else if (k == "delay_ms") delay_us = uint64_t(atof(v) * 1000);
+      else if (k == "rtt_ms") fixed_us = uint64_t(atof(v) * 500);
+      else if (k == "rate_mbps") rate_bps = atof(v) * 1e6;
+      else if (k == "queue_kb") queue_bytes = uint64_t(atof(v) * 1024);
+      else if (k == "blackhole") {
+        bh_start_ms = strtoull(v, nullptr, 10);
+        if (const char* c = strchr(v, ':')) bh_len_ms = strtoull(c + 1, nullptr, 10);
+      } else {
+        LOG_WARN(kT, "TUNNEL_FAULT: unknown key '%s'", k.c_str());
+      }
     }
     t0_ms = Reactor::now_ms();
     on = drop > 0 || dup > 0 || delay_us > 0 || bh_len_ms > 0 || fixed_us > 0 || rate_bps > 0;

@@ -93,6 +93,11 @@ struct IceConfig {
 enum class IceState { New, Checking, Connected, Disconnected, Failed, Closed };
 const char* ice_state_name(IceState s);
 
+// TUNNEL_UDP_OFFLOAD: the UDP offloads to use, a comma list of "gso" (send
+// segmentation) and "gro" (receive coalescing); unset = both, "none" = neither
+// (tests of the plain paths).
+bool udp_offload_enabled(const char* which);
+
 class IceAgent : public std::enable_shared_from_this<IceAgent> {
  public:
   static std::shared_ptr<IceAgent> create(Reactor& r, IceConfig cfg, bool controlling);
@@ -279,7 +284,7 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
     bool coalesce = false; // more records may be appended
   };
   std::vector<Out> outq_;
-  // WAN emulation (TUNNEL_FAULT_RTT_MS / _RATE_MBPS): datagrams waiting for
+  // WAN emulation (TUNNEL_FAULT rtt_ms / rate_mbps): datagrams waiting for
   // their release time, in order.
   std::deque<std::pair<uint64_t, Out>> delayq_;
   uint64_t link_free_us_ = 0;
@@ -307,7 +312,7 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   // arrive coalesced. Falls back to one datagram per send if the kernel refuses.
   static constexpr int kGsoMaxSegs = 64;
   static constexpr size_t kGsoMaxBytes = 60000;
-  bool gso_ok_ = getenv("TUNNEL_NO_GSO") == nullptr;
+  bool gso_ok_ = udp_offload_enabled("gso");
   bool gro_enabled_ = false;
  public:
   uint64_t gso_sends_ = 0, gro_batches_ = 0;  // counters (metrics, tests)

@@ -55,17 +55,12 @@ bool DataChannel::send_impl(const uint8_t* hdr, size_t hlen, const Bytes& payloa
     uint32_t sid = rd32(hdr + 1);
     if (sid) st = uint16_t(stream_ + 2 * (1 + int(sid % uint32_t(lanes_))));
   }
-  // TUNNEL_SCTP_PRIORITY=1: small frames (SSE tokens, headers, control,
-  // credit) take the SCTP priority queue, ahead of queued bulk bodies. Off by
-  // default: on the emulated WAN it did not shorten the SSE-next-to-bulk tail
-  // (a token mostly waits behind a bulk message already being fragmented,
-  // which it may not interrupt), and 64 x 1 MB bulk ran ~20 % slower.
-  static const bool prio = [] {
-    const char* e = getenv("TUNNEL_SCTP_PRIORITY");
-    return e && *e == '1';
-  }();
-  const bool small = urgent || (prio && hlen + payload.size() <= kPrioritySmallFrame);
-  bool ok = pc->sctp_->send_framed(st, kPpidBinary, hdr, hlen, payload, false, small);
+  // Only urgent frames on a lane take the SCTP priority queue. (Every small
+  // frame there — SSE tokens, headers, credit — did not shorten the
+  // SSE-next-to-bulk tail on the emulated WAN: a token mostly waits behind a
+  // bulk message already being fragmented, which it may not interrupt; and
+  // 64 x 1 MB bulk ran ~20 % slower. Removed in round 5.)
+  bool ok = pc->sctp_->send_framed(st, kPpidBinary, hdr, hlen, payload, false, urgent);
   if (ok && buffered_amount() > buffered_low_threshold) above_low_ = true;
   return ok;
 }
@@ -209,8 +204,7 @@ PeerConnection::PeerConnection(Reactor& r, PcConfig cfg, bool offerer)
     : r_(r), cfg_(std::move(cfg)), offerer_(offerer), mtu_(cfg_.sctp_mtu) {
   const char* e = getenv("TUNNEL_COALESCE_US");
   coalesce_us_ = cfg_.coalesce_us >= 0 ? uint64_t(cfg_.coalesce_us) : (e && *e ? strtoull(e, nullptr, 10) : 50);
-  const char* l = getenv("TUNNEL_COALESCE_LOAD_PCT");
-  coalesce_load_ = cfg_.coalesce_load >= 0 ? cfg_.coalesce_load : (l && *l ? double(strtoull(l, nullptr, 10)) / 100.0 : 0.5);
+  coalesce_load_ = cfg_.coalesce_load >= 0 ? cfg_.coalesce_load : 0.5;
 }
 
 PeerConnection::~PeerConnection() { close(); }
@@ -536,8 +530,6 @@ void PeerConnection::start_sctp() {
   sc.remote_port = remote_.sctp_port;
   sc.zero_checksum = true;  // SCTP runs over DTLS (RFC 8261), EDMID 1
   if (jumbo) sc.initial_cwnd = cfg_.jumbo_initial_cwnd;
-  if (const char* e = getenv("TUNNEL_SCTP_RWND_KB"); e && *e)  // advertised receive window (default 8 MiB)
-    sc.rwnd = uint32_t(std::clamp(atoi(e), 256, 1 << 20)) * 1024u;
   std::weak_ptr<PeerConnection> w = shared_from_this();
   // Record crypto and UDP sends of bulk flushes off this thread (rtc/datapath.h).
   dtls_->enable_lanes([w](TxTarget& t) {
@@ -561,15 +553,13 @@ void PeerConnection::start_sctp() {
   sctp_->on_message = [w](uint16_t st, uint32_t ppid, Bytes m) {
     if (auto s = w.lock()) s->on_sctp_message(st, ppid, std::move(m), nullptr);
   };
-  // Fragmented messages as chains of packet views (TUNNEL_SCTP_CHAIN=1). Off
-  // by default: on the 64 x 1 MB echo one reassembled copy per message measured
-  // 1432 vs 1350 req/s (profiles/r04/chain_ab) — the copy is cheaper than
-  // walking ~900 small views through the frame decoder and upstream writes.
-  static const bool chains = [] {
-    const char* e = getenv("TUNNEL_SCTP_CHAIN");
-    return e && *e == '1';
-  }();
-  if (chains || cfg_.message_chains)
+  // Fragmented messages as chains of packet views (PcConfig::message_chains).
+  // Off by default: on the 64 x 1 MB echo one reassembled copy per message
+  // measured 1432 vs 1350 req/s (profiles/r04/chain_ab) — the copy is cheaper
+  // than walking ~900 small views through the frame decoder and upstream
+  // writes — and it raised the 1200-MTU SSE p99 next to bulk (1.04 -> 1.83 ms,
+  // profiles/r04/chain29).
+  if (cfg_.message_chains)
     sctp_->on_message_chain = [w](uint16_t st, uint32_t ppid, Bytes m, std::vector<Bytes>& more) {
       if (auto s = w.lock()) s->on_sctp_message(st, ppid, std::move(m), &more);
     };

@@ -45,20 +45,20 @@ struct PcConfig {
   // 0 on the side that mostly receives streams (proxy).
   uint64_t sack_delay_us = 0;
   // Fragmented messages handed to chain consumers as views of their packets
-  // instead of one reassembled copy (also TUNNEL_SCTP_CHAIN=1).
+  // instead of one reassembled copy (the default copies; see start_sctp).
   bool message_chains = false;
   // Flush coalescing on a busy loop: while the association loop is at least
   // `coalesce_load` busy (Reactor::load) and less than one packet of data is
   // queued, the SCTP flush waits up to `coalesce_us` after the previous one,
   // so token-sized frames of many streams share packets (and sendmmsg calls,
   // reader wake-ups and SACKs on the far side). 0 = off; < 0: the
-  // environment (TUNNEL_COALESCE_US, TUNNEL_COALESCE_LOAD_PCT) or 50 us at
+  // environment (TUNNEL_COALESCE_US) or 50 us at
   // 50 %: on the MI355X host's node row (1 serve, 8 upstreams, 1 ms tokens)
   // it cut the serve's packets at 1024 streams from 680-930 k to 255-270 k
   // per 10 s and the added p50 TTFT from 2.25 to 1.04 ms (median of 3,
   // profiles/r04/node14); below the load threshold nothing changes.
   int64_t coalesce_us = -1;
-  double coalesce_load = -1;  // < 0: TUNNEL_COALESCE_LOAD_PCT or 0.5
+  double coalesce_load = -1;  // < 0: 0.5
 };
 
 class PeerConnection;

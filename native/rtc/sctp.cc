@@ -166,6 +166,28 @@ void SctpAssociation::unref(BodyRef* b) {
   else ref_free_.push_back(b);
 }
 
+// TUNNEL_SCTP_CC: the congestion response. Unset: this build's (Veno-style
+// random-loss cut to 80 %, CUBIC's 0.7 on congestion, the short-path queue
+// bound). "reno": a Reno-like competitor for the shared-bottleneck fairness
+// bench (every loss halves cwnd, no queue bound). "beta=NN": random-loss cut
+// to NN % (50..100) (tuning runs).
+const CcPolicy& cc_policy() {
+  static const CcPolicy p = [] {
+    CcPolicy c;
+    const char* e = getenv("TUNNEL_SCTP_CC");
+    if (!e || !*e) return c;
+    const std::string v = e;
+    if (v == "reno") {
+      c.random_beta_pct = 50;
+      c.queue_bound = false;
+    } else if (v.rfind("beta=", 0) == 0) {
+      c.random_beta_pct = std::clamp(atoi(v.c_str() + 5), 50, 100);
+    }
+    return c;
+  }();
+  return p;
+}
+
 SctpAssociation::Chunk* SctpAssociation::new_chunk() {
   if (chunk_free_.empty()) return new Chunk();
   Chunk* c = chunk_free_.back();
@@ -997,7 +1019,7 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
   // Duplicate TSN reports: copies the peer already had. A retransmission of
   // the current loss episode reported back this way was not needed — but only
   // a TSN this episode retransmitted counts, once: a duplicate of a redundant
-  // copy (TUNNEL_SCTP_DUP) or of an earlier episode's retransmission says
+  // copy (SctpConfig::dup_small) or of an earlier episode's retransmission says
   // nothing about this one's losses.
   if (ep_active_ && ndup && ep_rtx_ > 0) {
     const uint8_t* d = c + 12 + 4u * ngap;
@@ -1172,10 +1194,7 @@ void SctpAssociation::loss_response(bool random_loss, bool over_bdp, uint64_t no
   // sqrt((2 - b) / (2 b p)) against Reno's sqrt(1.5 / p): b = 0.2 is 1.7x
   // Reno, within the 2x bound; the cost is bulk on paths with genuinely
   // random loss.
-  static const int random_beta_pct = [] {
-    const char* e = getenv("TUNNEL_SCTP_RANDOM_BETA_PCT");
-    return e && *e ? std::clamp(atoi(e), 50, 100) : 80;
-  }();
+  const int random_beta_pct = cc_policy().random_beta_pct;
   last_loss_us_ = now;
   size_t keep = cwnd_ * 7 / 10;
   if (random_loss) {
@@ -1419,21 +1438,16 @@ void SctpAssociation::dr_on_sack(uint32_t cum, size_t newly_acked, bool cwnd_lim
 // them: on the MI355X host the mixed row's SSE TTFT p50 was 1.0-1.4 ms next to
 // bulk (direct 0.13-0.27 ms), the SCTP SRTT 1-2.5 ms over a 50 us path. Per
 // round trip the smallest RTT sample, less the base RTT (the smallest sample
-// of the last 5-10 s), is the standing queue; above TUNNEL_SCTP_QUEUE_US it takes cwnd down by a quarter (and ends
-// slow start), never below TUNNEL_SCTP_QUEUE_FLOOR_KB. WAN paths (base RTT >=
+// of the last 5-10 s), is the standing queue; above the target it takes cwnd
+// down by a quarter (and ends slow start), never below the floor. WAN paths (base RTT >=
 // kLongPathUs) keep the loss-based response alone, as do paths whose queue
 // stays under the target.
 void SctpAssociation::note_interactive() { interactive_until_us_ = Reactor::now_us() + 200000; }
 
 void SctpAssociation::queue_bound(uint32_t cum, uint64_t rtt_sample) {
-  auto env_or = [](const char* name, int dflt, int lo) {
-    const char* e = getenv(name);
-    return e && *e ? std::max(lo, atoi(e)) : dflt;
-  };
-  static const uint64_t target_bulk = uint64_t(env_or("TUNNEL_SCTP_QUEUE_US", 300, 0));
-  static const size_t floor_bulk = size_t(env_or("TUNNEL_SCTP_QUEUE_FLOOR_KB", 1024, 64)) * 1024;
-  static const uint64_t target_inter = uint64_t(env_or("TUNNEL_SCTP_QUEUE_US_INTERACTIVE", 150, 0));
-  static const size_t floor_inter = size_t(env_or("TUNNEL_SCTP_QUEUE_FLOOR_KB_INTERACTIVE", 512, 64)) * 1024;
+  if (!cc_policy().queue_bound) return;
+  constexpr uint64_t target_bulk = 300, target_inter = 150;
+  constexpr size_t floor_bulk = 1024 * 1024, floor_inter = 512 * 1024;
   // Two settings: bulk alone keeps a 300 us / 1 MiB bound (64 x 1 MB echo on
   // the MI355X host unchanged by tighter ones, -15 % in the build container);
   // while interactive frames flow (note_interactive) 150 us / 512 KiB:
@@ -1702,8 +1716,8 @@ void SctpAssociation::flush() {
   // adds to a congested path (interactive traffic is a trickle).
   const size_t pri_allow = 4 * mtu;
   const bool dup = dup_small_enabled();
-  // New data per flush is bounded (TUNNEL_SCTP_FLUSH_PKTS packets' worth, 0 =
-  // a whole window): fragmenting a megabyte of bulk into 1200-byte chunks
+  // New data per flush is bounded (kFlushQuantumPkts packets' worth):
+  // fragmenting a megabyte of bulk into 1200-byte chunks
   // keeps this thread busy for a few hundred microseconds, and a request or
   // SACK that arrived meanwhile waited for all of it. Past the quantum the
   // reactor takes one non-blocking turn (its I/O first) and the next flush
@@ -1711,11 +1725,8 @@ void SctpAssociation::flush() {
   // are 150 KB at a 1200-byte MTU (MI355X host mixed row: SSE TTFT p50 0.99 ->
   // 0.59 ms at 128 KB) and 2 MB on a same-host jumbo path, where a 128 KB
   // quantum (8 packets) cost bulk throughput for little latency.
-  static const size_t quantum_pkts = [] {
-    const char* e = getenv("TUNNEL_SCTP_FLUSH_PKTS");
-    return size_t(e && *e ? std::max(0, atoi(e)) : 128);
-  }();
-  const size_t quantum = quantum_pkts * max_payload;
+  constexpr size_t kFlushQuantumPkts = 128;
+  const size_t quantum = kFlushQuantumPkts * max_payload;
   size_t new_bytes = 0;
   bool yielded = false;
   for (int round = 0; round < 256 && !yielded; round++) {
@@ -1810,17 +1821,12 @@ std::string SctpAssociation::debug_state() const {
   return b;
 }
 
-// Redundant copies of small messages: TUNNEL_SCTP_DUP=1 always, =0 never;
-// by default on once the path has shown random loss (at least 8 loss
+// Redundant copies of small messages: SctpConfig::dup_small 1 always, 0
+// never; by default on once the path has shown random loss (at least 8 loss
 // events, more than 1 in 400 data chunks sent). A lossless LAN path never
 // pays for it; tokens are ~100-300 bytes, so doubling them costs little.
 bool SctpAssociation::dup_small_enabled() const {
-  static const int mode = [] {
-    const char* e = getenv("TUNNEL_SCTP_DUP");
-    return e && *e ? atoi(e) : -1;
-  }();
   if (cfg_.dup_small >= 0) return cfg_.dup_small != 0;
-  if (mode >= 0) return mode != 0;
   const uint64_t losses = stats_.fast_retransmits + stats_.tlp_probes + stats_.t3_expirations;
   return losses >= 8 && losses * 400 > stats_.data_chunks_sent;
 }

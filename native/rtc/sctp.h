@@ -56,6 +56,13 @@ struct SctpConfig {
   int dup_small = -1;
 };
 
+// Congestion response (TUNNEL_SCTP_CC, read once; see sctp.cc).
+struct CcPolicy {
+  int random_beta_pct = 80;  // cwnd kept after a random (no standing queue) loss, in %
+  bool queue_bound = true;   // the short-path queue bound
+};
+const CcPolicy& cc_policy();
+
 struct SctpStats {
   uint64_t packets_sent = 0, packets_received = 0;
   uint64_t data_chunks_sent = 0, data_chunks_received = 0;

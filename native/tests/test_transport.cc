@@ -669,43 +669,6 @@ TEST(peerconnection_pair_loopback) {
 // datagram, a datagram from another sender, a record that fails
 // authentication (handed over with ok = false for the association thread to
 // drop), and a datagram mixing an alert with data.
-// A batch large enough to be sealed by two threads comes out byte for byte
-// as sealing each record alone would make it, datagram boundaries included.
-TEST(tx_seal_split_matches_one_thread) {
-  if (!AesGcm::supported()) return;
-  RecordKeys keys;
-  auto g = std::make_shared<AesGcm>();
-  uint8_t key[16];
-  for (int i = 0; i < 16; i++) key[i] = uint8_t(i * 7 + 1);
-  CHECK(g->init(key, 16));
-  keys.w = keys.r = g;
-  for (int i = 0; i < 4; i++) keys.wiv[i] = keys.riv[i] = uint8_t(0x30 + i);
-  TxBatch b;
-  std::vector<std::string> pts;
-  for (int i = 0; i < 300; i++) {  // ~360 KB: over the 128 KiB split size
-    pts.push_back(std::string(1100 + (i * 37) % 100, char('a' + i % 26)));
-    iovec v{const_cast<char*>(pts.back().data()), pts.back().size()};
-    b.add(uint64_t(1000 + i), 23, &v, nullptr, 1);
-  }
-  TxLaneState st;
-  st.set_split_bytes(128 * 1024);
-  SealedBatch sb;
-  st.seal(b, keys, 0, sb);
-  CHECK_EQ(st.split_batches.load(), uint64_t(1));
-  CHECK_EQ(sb.dgs.size(), size_t(300));
-  size_t off = 0;
-  bool same = true;
-  for (int i = 0; i < 300; i++) {
-    std::vector<uint8_t> one(record_size(pts[size_t(i)].size()));
-    iovec v{const_cast<char*>(pts[size_t(i)].data()), pts[size_t(i)].size()};
-    seal_record(*g, keys.wiv, one.data(), 23, uint64_t(1000 + i), &v, 1, pts[size_t(i)].size());
-    same &= sb.dgs[size_t(i)].first == off && sb.dgs[size_t(i)].second == one.size() &&
-            memcmp(sb.out.data() + off, one.data(), one.size()) == 0;
-    off += one.size();
-  }
-  CHECK(same);
-}
-
 TEST(rx_reader_opens_app_records_and_passes_the_rest) {
   if (!AesGcm::supported()) return;
   auto keys = std::make_shared<RecordKeys>();
@@ -978,7 +941,7 @@ TEST(slow_association_thread_loses_nothing_uncounted) {
   // and once without it (the drops then happen, and must all be counted).
   setenv("TUNNEL_UDP_BUF_KB", "256", 1);
   for (int escape = 1; escape >= 0; escape--) {
-  setenv("TUNNEL_RX_ESCAPE", escape ? "1" : "0", 1);
+  set_rx_escape_enabled(escape == 1);
   Reactor r;
   PcConfig cfg;
   cfg.ice.include_loopback = true;
@@ -1051,7 +1014,7 @@ TEST(slow_association_thread_loses_nothing_uncounted) {
   ans->close();
   }
   unsetenv("TUNNEL_UDP_BUF_KB");
-  unsetenv("TUNNEL_RX_ESCAPE");
+  set_rx_escape_enabled(true);
 }
 
 // Flush coalescing: small messages queued one per loop pass share packets
@@ -1189,7 +1152,7 @@ TEST(fragmented_messages_arrive_as_zero_copy_chains) {
 TEST(rx_reader_slots_follow_the_path_without_gro) {
   if (!AesGcm::supported()) return;
   ReaderMode always(kRxReaderAlways);
-  setenv("TUNNEL_NO_GRO", "1", 1);
+  setenv("TUNNEL_UDP_OFFLOAD", "gso", 1);  // GRO off
   Reactor r;
   PcConfig cfg;
   cfg.ice.include_loopback = true;
@@ -1210,7 +1173,7 @@ TEST(rx_reader_slots_follow_the_path_without_gro) {
   };
   off->start_gathering();
   ans->start_gathering();  // sockets open here, without UDP_GRO
-  unsetenv("TUNNEL_NO_GRO");
+  unsetenv("TUNNEL_UDP_OFFLOAD");
   CHECK(r.run_until([&] { return off->gathering_complete(); }, 3000));
   std::string err;
   CHECK(ans->set_remote_description(off->local_description(), &err));

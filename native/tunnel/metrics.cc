@@ -171,14 +171,12 @@ std::shared_ptr<void> serve(Reactor& r, const std::string& addr, std::string* er
 
 namespace p2pt::trace {
 namespace {
-// TUNNEL_TRACE_BUFFERED=1: events collect in memory and go out in whole-line
-// write()s of up to 512 KiB (and at exit): bulk waterfalls stamp ~10 events
-// per request, and a flush per event would cost a syscall each on the
-// measured path. Several processes append to one file (O_APPEND), so a write
-// never ends inside a line. Default: one write per event.
+// Events collect in memory and go out in whole-line write()s of up to 512
+// KiB (and at exit): a waterfall stamps ~10 events per request, and a write
+// per event cost a syscall each on the measured path. Several processes
+// append to one file (O_APPEND), so a write never ends inside a line.
 struct Sink {
   int fd = -1;
-  bool buffered = false;
   std::mutex mu;
   std::string buf;
   void drain() {  // mu held
@@ -200,12 +198,8 @@ Sink* sink() {
     if (fd < 0) return nullptr;
     auto* k = new Sink;
     k->fd = fd;
-    const char* b = getenv("TUNNEL_TRACE_BUFFERED");
-    k->buffered = b && *b == '1';
-    if (k->buffered) {
-      k->buf.reserve(1 << 20);
-      std::atexit([] { flush(); });
-    }
+    k->buf.reserve(1 << 20);
+    std::atexit([] { flush(); });
     return k;
   }();
   return s;
@@ -228,7 +222,7 @@ void event_at(const char* role, uint32_t sid, const char* ev, uint64_t t_us) {
   n = std::min(n, int(sizeof line) - 1);
   std::lock_guard<std::mutex> lk(k->mu);
   k->buf.append(line, size_t(n));
-  if (!k->buffered || k->buf.size() >= (512u << 10)) k->drain();
+  if (k->buf.size() >= (512u << 10)) k->drain();
 }
 
 void flush() {

@@ -38,7 +38,7 @@ void event(const char* role, uint32_t stream_id, const char* ev);
 // The same with a time taken earlier (CLOCK_MONOTONIC us), e.g. a
 // connection's accept stamped once its first request has a stream id.
 void event_at(const char* role, uint32_t stream_id, const char* ev, uint64_t t_us);
-void flush();  // buffered mode (TUNNEL_TRACE_BUFFERED=1): write out what is held
+void flush();  // write out what is held (also done at exit)
 
 // Transport hops of a traced frame (this thread's current datagrams):
 // the receive side records when the kernel queued the datagram (SO_TIMESTAMPNS,

@@ -55,10 +55,7 @@ class FrameScheduler {
   void send(proto::Frame f);
   // Bytes held here plus bytes buffered in the channel.
   size_t pending_bytes() const { return queued_ + (ch_ ? ch_->buffered_amount() : 0); }
-  bool bypass_ = [] {  // TUNNEL_SCHED_BYPASS=0 turns the interactive bypass off (A/B)
-    const char* e = getenv("TUNNEL_SCHED_BYPASS");
-    return !(e && *e == '0');
-  }();
+  bool bypass_ = true;  // the interactive bypass (tests turn it off to compare)
   uint64_t bypassed_ = 0;  // frames sent through the interactive bypass
   std::map<uint32_t, uint32_t> small_;  // small body frames sent through the bypass, per stream
   std::unordered_set<uint64_t> traced_;  // TUNNEL_TRACE: (stream, kind) whose first body frame was stamped

@@ -64,7 +64,7 @@ int WorkerPool::auto_count() {
   // reader and the two TX stages take four, the workers the rest. On 6 CPUs
   // one worker beat two on the 64 x 1 MB echo (1916 vs 1633 req/s at 1200 MTU,
   // 1920 vs 1876 jumbo, same box; profiles/r04/w24).
-  if (affinity::enabled()) return int(std::clamp<long>(n - (affinity::tx_shared() ? 4 : 5), 1, 4));
+  if (affinity::enabled()) return int(std::clamp<long>(n - 5, 1, 4));
   return int(std::clamp<long>(n / 2 - 1, 1, 4));
 }
 

@@ -179,14 +179,7 @@ class BulkRoutes {
   static bool streaming_type(std::string_view ctype) {
     return ctype.find("event-stream") != std::string_view::npos || ctype.find("ndjson") != std::string_view::npos;
   }
-  bool bulk(const std::string& k) const { return !m_.empty() && enabled() && m_.count(k) != 0; }
-  static bool enabled() {  // TUNNEL_BULK_ROUTES=0 turns the learning off (A/B)
-    static const bool on = [] {
-      const char* e = getenv("TUNNEL_BULK_ROUTES");
-      return !(e && *e == '0');
-    }();
-    return on;
-  }
+  bool bulk(const std::string& k) const { return !m_.empty() && m_.count(k) != 0; }
   void note(const std::string& k, uint64_t bytes, bool streaming) {
     if (bytes >= Placement::kBulkBytes && !streaming) {
       if (m_.size() >= kMax) m_.clear();

@@ -108,6 +108,13 @@ class Proc:
             self.popen.wait()
 
 
+def fault_env(**kw) -> dict:
+    """The datagram-path fault injector's environment (native/rtc/ice.cc):
+    fault_env(drop=0.02, dup=0.05, delay_ms=8, rtt_ms=20, rate_mbps=100,
+    queue_kb=256, blackhole="3000:4000") -> {"TUNNEL_FAULT": "drop=0.02,..."}."""
+    return {"TUNNEL_FAULT": ",".join(f"{k}={v}" for k, v in kw.items())}
+
+
 def spawn(name: str, argv: list[str], env: dict | None = None) -> Proc:
     e = dict(os.environ)
     e.setdefault("RUST_LOG", "info")

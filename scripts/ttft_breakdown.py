@@ -30,7 +30,7 @@ generator, joins the per-stream events (all processes stamp CLOCK_MONOTONIC
     client's own hops (its write to the proxy's wake-up, the proxy's write to
     its wake-up)
 
-Tracing is buffered in memory (TUNNEL_TRACE_BUFFERED=1) and written at exit,
+Tracing is buffered in memory and written at exit,
 so stamping costs no syscall on the measured path.
 
 --bulk-echo: BASELINE config #3 (N streams x 1 MB POST echoed) as a waterfall.
@@ -91,7 +91,7 @@ def main():
     try:
         extra = [x for x in a.extra.split() if x]
         with Tunnel(f"http://127.0.0.1:{port}", transport=a.transport,
-                    env={"TUNNEL_TRACE": trace, "TUNNEL_TRACE_BUFFERED": "1"},
+                    env={"TUNNEL_TRACE": trace},
                     serve_extra=extra, proxy_extra=extra) as t:
             bulk = None
             if a.bulk:
@@ -226,7 +226,7 @@ def bulk_echo(a):
         pin_p = ["--cpu-affinity", plan["proxy"]] if plan else []
         ms, mp = free_port(), free_port()
         with Tunnel(f"http://127.0.0.1:{port}", transport=a.transport,
-                    env={"TUNNEL_TRACE": trace, "TUNNEL_TRACE_BUFFERED": "1"},
+                    env={"TUNNEL_TRACE": trace},
                     serve_extra=extra + pin_s + ["--metrics-listen", f"127.0.0.1:{ms}"],
                     proxy_extra=extra + pin_p + ["--metrics-listen", f"127.0.0.1:{mp}"]) as t:
             path = t.serve.wait_for("WebRTC connection established", 1).split(" via ", 1)[-1] if a.transport == "webrtc" else ""

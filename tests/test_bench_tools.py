@@ -16,8 +16,8 @@ from p2p_llm_tunnel_amd.utils import netstat, pinning, timeline  # noqa: E402
 
 
 def test_ab_variants_and_key_numbers():
-    v = ab.parse_variants("base: qa:TUNNEL_TCP_QUICKACK=1 both:A=1,B=2")
-    assert v == [("base", {}), ("qa", {"TUNNEL_TCP_QUICKACK": "1"}), ("both", {"A": "1", "B": "2"})]
+    v = ab.parse_variants("base: co:TUNNEL_COALESCE_US=0 both:A=1,B=2")
+    assert v == [("base", {}), ("co", {"TUNNEL_COALESCE_US": "0"}), ("both", {"A": "1", "B": "2"})]
     k = ab.key_numbers("bulk", {"tunneled_req_s": 1500.0, "direct_req_s": 2000.0})
     assert k == {"tunneled_req_s": 1500.0, "direct_req_s": 2000.0, "ratio": 0.75}
     node = {"runs": [{"streams": 256, "added_p50_ttft_ms": 0.3, "tunneled_p99_ttft_ms": 1.6,

@@ -1,8 +1,8 @@
 """DTLS record-layer interop: our AES-GCM record layer (VAES/VPCLMULQDQ when
 the CPU has it, OpenSSL EVP otherwise; native/core/aesgcm.h,
 native/rtc/dtls.cc) against a peer that keeps OpenSSL's own DTLS record
-layer (TUNNEL_DTLS_OPENSSL_RECORDS, i.e. a standard DTLS 1.2 stack on the
-wire) and against a peer on the EVP record path (TUNNEL_DTLS_EVP).
+layer (TUNNEL_DTLS_RECORDS=openssl, i.e. a standard DTLS 1.2 stack on the
+wire) and against a peer on the EVP record path (TUNNEL_DTLS_RECORDS=evp).
 
 Large echoed bodies cross every record size the SCTP packer produces, in
 both directions; the SSE stream checks small records.
@@ -16,9 +16,9 @@ import pytest
 from p2p_llm_tunnel_amd.utils.procs import free_port, start_proxy, start_serve, start_signal
 
 CASES = {
-    "openssl-records-vs-own": ({"TUNNEL_DTLS_OPENSSL_RECORDS": "1"}, None),
-    "own-vs-openssl-records": (None, {"TUNNEL_DTLS_OPENSSL_RECORDS": "1"}),
-    "evp-vs-vector": ({"TUNNEL_DTLS_EVP": "1"}, None),
+    "openssl-records-vs-own": ({"TUNNEL_DTLS_RECORDS": "openssl"}, None),
+    "own-vs-openssl-records": (None, {"TUNNEL_DTLS_RECORDS": "openssl"}),
+    "evp-vs-vector": ({"TUNNEL_DTLS_RECORDS": "evp"}, None),
 }
 
 
@@ -45,11 +45,11 @@ def test_record_layer_interop(mock_upstream, case):
         c.close()
         armed = {p.name: [l for l in p.text().splitlines() if "own record layer armed" in l] for p in (serve, proxy)}
         for name, env in (("serve", serve_env), ("proxy", proxy_env)):
-            if env and "TUNNEL_DTLS_OPENSSL_RECORDS" in env:
+            if env and env.get("TUNNEL_DTLS_RECORDS") == "openssl":
                 assert armed[name] == []
             else:
                 assert len(armed[name]) == 1
-                if env and "TUNNEL_DTLS_EVP" in env:
+                if env and env.get("TUNNEL_DTLS_RECORDS") == "evp":
                     assert "EVP AES-GCM" in armed[name][0]
     finally:
         for p in (proxy, serve, signal):

@@ -1,7 +1,7 @@
 """Fault injection and failure recovery (the reference tests none of this).
 
 * Datagram loss / duplication / reordering on the WebRTC path (built-in
-  injector: TUNNEL_FAULT_DROP / _DUP / _DELAY_MS) — SCTP must deliver every
+  injector: TUNNEL_FAULT drop / dup / delay_ms) — SCTP must deliver every
   frame intact and in order.
 * Peer death: the surviving side detects it (SCTP ABORT on graceful exit,
   ICE consent timeout on kill -9), the supervisor backs off and reconnects,
@@ -26,8 +26,8 @@ def sse(port):
 
 
 @pytest.mark.parametrize("fault", [
-    {"TUNNEL_FAULT_DROP": "0.05"},
-    {"TUNNEL_FAULT_DROP": "0.02", "TUNNEL_FAULT_DUP": "0.05", "TUNNEL_FAULT_DELAY_MS": "8"},
+    {"TUNNEL_FAULT": "drop=0.05"},
+    {"TUNNEL_FAULT": "drop=0.02,dup=0.05,delay_ms=8"},
 ], ids=["loss5", "loss2-dup5-reorder"])
 def test_lossy_path_integrity(mock_upstream, fault):
     with Tunnel(mock_upstream, transport="webrtc", env=fault) as t:
@@ -122,7 +122,7 @@ def test_blackholed_path_fails_and_recovers(mock_upstream):
     alive): ICE consent freshness declares the session dead, the supervisor
     backs off and re-establishes once packets flow again."""
     extra = ["--ice-timeout-ms", "1500"]
-    env = {"TUNNEL_FAULT_BLACKHOLE": "3000:4000"}
+    env = {"TUNNEL_FAULT": "blackhole=3000:4000"}
     with Tunnel(mock_upstream, transport="webrtc", serve_extra=extra, proxy_extra=extra, env=env) as t:
         assert urllib.request.urlopen(t.url + "/health", timeout=5).read() == b"ok"
         t.proxy.wait_for(r"proxy failed \(attempt 1\)", 15)

@@ -2,7 +2,7 @@
 reference rtc.rs:31-72 via webrtc-rs defaults), forced on loopback with
 --no-jumbo-loopback: bulk bodies and SSE stay correct with UDP GSO/GRO on
 (runs of equal-size DTLS datagrams leave as one message and arrive
-coalesced) and with both switched off (TUNNEL_NO_GSO / TUNNEL_NO_GRO)."""
+coalesced) and with both switched off (TUNNEL_UDP_OFFLOAD=none)."""
 import http.client
 import os
 import json
@@ -24,7 +24,7 @@ def _metrics(port):
 @pytest.mark.parametrize("offload", [True, False])
 def test_standard_mtu_bulk_and_sse(mock_upstream, offload):
     ms, mp = free_port(), free_port()
-    env = None if offload else {"TUNNEL_NO_GSO": "1", "TUNNEL_NO_GRO": "1"}
+    env = None if offload else {"TUNNEL_UDP_OFFLOAD": "none"}
     with Tunnel(mock_upstream, transport="webrtc", env=env,
                 serve_extra=STD + ["--metrics-listen", f"127.0.0.1:{ms}"],
                 proxy_extra=STD + ["--metrics-listen", f"127.0.0.1:{mp}"]) as t:
@@ -54,7 +54,7 @@ def test_emulated_wan_path_with_loss(mock_upstream):
     repaired without T3 collapse, and a slow path keeps the scheduler's
     channel window small without stalling it (adaptive window + low-water)."""
     ms = free_port()
-    env = {"TUNNEL_FAULT_RTT_MS": "20", "TUNNEL_FAULT_RATE_MBPS": "100", "TUNNEL_FAULT_LOSS": "0.01"}
+    env = {"TUNNEL_FAULT": "rtt_ms=20,rate_mbps=100,loss=0.01"}
     with Tunnel(mock_upstream, transport="webrtc", env=env, serve_extra=STD + ["--metrics-listen", f"127.0.0.1:{ms}"],
                 proxy_extra=STD) as t:
         c = http.client.HTTPConnection("127.0.0.1", t.proxy_port, timeout=60)
@@ -78,8 +78,7 @@ def test_flow_window_grows_on_a_long_rtt_path(mock_upstream):
     autotuning); the proxy's receive-window autotuning doubles it while
     windows are taken within two round trips (measured 16 MB/s)."""
     mp = free_port()
-    env = {"TUNNEL_FAULT_RTT_MS": "50", "TUNNEL_FAULT_RATE_MBPS": "400", "TUNNEL_FAULT_LOSS": "0",
-           "TUNNEL_FAULT_QUEUE_KB": "2441"}
+    env = {"TUNNEL_FAULT": "rtt_ms=50,rate_mbps=400,loss=0,queue_kb=2441"}
     n = 12 << 20
     with Tunnel(mock_upstream, transport="webrtc", env=env, serve_extra=STD,
                 proxy_extra=STD + ["--metrics-listen", f"127.0.0.1:{mp}"]) as t:
