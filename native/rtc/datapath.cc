@@ -486,7 +486,10 @@ void RxReader::run() {
       } else {
         waits.fetch_add(1, std::memory_order_relaxed);
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait_for(lk, std::chrono::milliseconds(1), [this] {
+        // Short waits: without UDP GRO every datagram is its own skb (about
+        // twice its size in buffer accounting), and a 1 ms pause let a 512 KiB
+        // buffer go from under half to overflowing (TUNNEL_UDP_OFFLOAD=none).
+        cv_.wait_for(lk, std::chrono::microseconds(100), [this] {
           return stop_.load(std::memory_order_acquire) || outstanding_.load(std::memory_order_acquire) < kMaxOutstanding;
         });
         continue;

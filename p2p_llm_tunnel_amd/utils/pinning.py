@@ -148,22 +148,62 @@ def physical_cores(cpus: list[int]) -> list[int]:
     return out
 
 
-def ccd_plan(cpus: list[int] | None = None) -> dict[str, str]:
+def cpu_busy(sample_s: float = 0.3) -> dict[int, float]:
+    """Per-CPU busy share over a short sample of /proc/stat (0..1)."""
+    import time
+
+    def snap():
+        out = {}
+        with open("/proc/stat") as f:
+            for line in f:
+                if line.startswith("cpu") and line[3].isdigit():
+                    parts = line.split()
+                    v = [int(x) for x in parts[1:]]
+                    idle = v[3] + (v[4] if len(v) > 4 else 0)
+                    out[int(parts[0][3:])] = (sum(v), idle)
+        return out
+
+    try:
+        a = snap()
+        time.sleep(sample_s)
+        b = snap()
+    except OSError:
+        return {}
+    busy = {}
+    for c, (tot, idle) in b.items():
+        if c in a:
+            dt, di = tot - a[c][0], idle - a[c][1]
+            busy[c] = 1.0 - di / dt if dt > 0 else 0.0
+    return busy
+
+
+def ccd_plan(cpus: list[int] | None = None, busy: dict[int, float] | None = None) -> dict[str, str]:
     """The headline's layout: every process of the benchmark on the cores of
     ONE L3 domain (a CCD on EPYC), one core per role thread — load generator,
     mock, serve (association thread first), proxy — so no hop of either leg
     crosses an L3 or a socket, and the direct leg (load generator <-> mock)
-    gets the same placement as the tunneled one. Left to the scheduler the
-    pool's processes may run on any of the host's 256 CPUs (the job has a
-    16-CPU quota, not a CPU set), and where a wake-up lands moved the
-    headline's added p50 TTFT 0.07-0.19 ms between runs of one build
-    (profiles/r05/b02). {} when no L3 domain has 6 cores."""
-    cpus = available_cpus() if cpus is None else list(cpus)
+    gets the same placement as the tunneled one.
+
+    The pool's jobs have a 16-CPU quota but may run on any of the host's 256
+    CPUs, and other jobs run on some of them: the CCD is the idlest one
+    (/proc/stat over 0.3 s, SMT siblings included, CPU 0's CCD avoided).
+    Pinned to CPUs 0-7 regardless, steps stalled ~10 ms behind other runnable
+    work in both legs; left to the scheduler, where the wake-ups landed moved
+    the added p50 TTFT 0.08-0.20 ms between runs of one build
+    (profiles/r05/b03). {} when no L3 domain has 6 cores."""
+    cpus = sorted(os.sched_getaffinity(0)) if cpus is None else list(cpus)
+    busy = cpu_busy() if busy is None else busy
+    best, best_load = None, None
     for g in l3_groups(cpus):
         cores = physical_cores(g)
-        if len(cores) >= 6:
-            n = len(cores)
-            sv = (n - 2 + 1) // 2
-            return {"loadgen": fmt_cpus(cores[:1]), "mock": fmt_cpus(cores[1:2]),
-                    "serve": fmt_cpus(cores[2:2 + sv]), "proxy": fmt_cpus(cores[2 + sv:])}
-    return {}
+        if len(cores) < 6:
+            continue
+        load = max((busy.get(c, 0.0) for c in g), default=0.0) + (1.0 if 0 in g else 0.0)
+        if best is None or load < best_load:
+            best, best_load = cores, load
+    if not best:
+        return {}
+    n = len(best)
+    sv = (n - 2 + 1) // 2
+    return {"loadgen": fmt_cpus(best[:1]), "mock": fmt_cpus(best[1:2]),
+            "serve": fmt_cpus(best[2:2 + sv]), "proxy": fmt_cpus(best[2 + sv:])}
