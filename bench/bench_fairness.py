@@ -3,7 +3,9 @@
 
 Both tunnels' serve sides reach their proxies through ONE TURN server whose
 relay towards peers is an emulated link (rate, drop-tail queue of one BDP,
-one-way delay, Bernoulli loss: utils/turn_server.py ``Link``), so the two
+one-way delay, Bernoulli loss): the native ``tunnel-relay``
+(native/bin/relay_main.cc, default) or, with ``--relay python``, the Python
+one of utils/turn_server.py (``Link``; it tops out near 17 MB/s), so the two
 associations' downloads compete for the same queue — unlike the per-agent WAN
 emulator (native/rtc/ice.cc), which gives every association a link of its own.
 
@@ -51,10 +53,32 @@ def jain(xs):
     return s * s / (len(xs) * q) if q else 0.0
 
 
-def run_row(rate, rtt_ms, loss, pair, seconds, mb, mtu_extra):
-    link = Link(rate_mbps=rate, delay_ms=rtt_ms / 2, queue_kb=max(32, int(rate * 1e6 / 8 * rtt_ms / 1e3 / 1024)),
-                loss=loss)
-    turn = TurnServer(user="u", password="p", link=link).start()
+class NativeRelay:
+    """tunnel-relay as a subprocess with the TurnServer surface run_row uses."""
+
+    def __init__(self, rate, delay_ms, queue_kb, loss):
+        self.proc = spawn("relay", [binary("tunnel-relay"), "--rate-mbps", str(rate), "--delay-ms", str(delay_ms),
+                                    "--queue-kb", str(queue_kb), "--loss", str(loss)])
+        line = self.proc.wait_for(r"relay listening on turn:", 10)
+        self.url = line.split("relay listening on ", 1)[1].split()[0]
+        self.stats = {}
+
+    def stop(self):
+        self.proc.stop()
+        for line in reversed(self.proc.lines):
+            if line.startswith("{"):
+                self.stats = json.loads(line)
+                break
+
+
+def run_row(rate, rtt_ms, loss, pair, seconds, mb, mtu_extra, relay="native"):
+    queue_kb = max(32, int(rate * 1e6 / 8 * rtt_ms / 1e3 / 1024))
+    link = None
+    if relay == "native":
+        turn = NativeRelay(rate, rtt_ms / 2, queue_kb, loss)
+    else:
+        link = Link(rate_mbps=rate, delay_ms=rtt_ms / 2, queue_kb=queue_kb, loss=loss)
+        turn = TurnServer(user="u", password="p", link=link).start()
     port = free_port()
     mock = spawn("mock", [binary("tunnel-mock"), "--port", str(port)])
     mock.wait_for("Mock LLM server running", 10)
@@ -62,7 +86,8 @@ def run_row(rate, rtt_ms, loss, pair, seconds, mb, mtu_extra):
     try:
         for i, pol in enumerate(pair):
             serve_extra = ["--turn", turn.url, "--turn-user", "u", "--turn-pass", "p", "--ice-relay-only"] + mtu_extra
-            env = dict(POLICIES[pol])
+            # "betaNN": the random-loss cut to NN % (TUNNEL_SCTP_CC=beta=NN)
+            env = dict(POLICIES[pol]) if pol in POLICIES else {"TUNNEL_SCTP_CC": "beta=" + pol[4:]}
             t = Tunnel(f"http://127.0.0.1:{port}", transport="webrtc", serve_extra=serve_extra,
                        proxy_extra=list(mtu_extra), env=env,
                        room=f"fair-{os.getpid()}-{i}-{time.time_ns()}")
@@ -88,7 +113,8 @@ def run_row(rate, rtt_ms, loss, pair, seconds, mb, mtu_extra):
             "MBps": [round(x, 3) for x in mbps], "share": [round(x / sum(mbps), 3) if sum(mbps) else 0 for x in mbps],
             "jain": round(jain(mbps), 4) if two else None, "utilisation": round(sum(mbps) / cap, 3),
             "ratio_first_to_second": round(mbps[0] / mbps[1], 3) if two and mbps[1] else None,
-            "errors": [o["errors"] for o in outs], "link": link.stats, "queue_kb": link.queue // 1024}
+            "errors": [o["errors"] for o in outs], "relay": relay,
+            "link": link.stats if link is not None else turn.stats.get("link", {}), "queue_kb": queue_kb}
 
 
 def main():
@@ -100,6 +126,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=20.0)
     ap.add_argument("--mb", type=int, default=8, help="size of each download in the loop")
     ap.add_argument("--jumbo", action="store_true", help="allow the jumbo path (default: 1200-byte MTU)")
+    ap.add_argument("--relay", choices=["native", "python"], default="native")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     ensure_native()
@@ -108,7 +135,7 @@ def main():
     for rate in [float(x) for x in a.rates.split(",")]:
         for loss in [float(x) for x in a.losses.split(",")]:
             for pair in a.pairs.split(","):
-                r = run_row(rate, a.rtt_ms, loss, pair.split(":"), a.seconds, a.mb, mtu_extra)
+                r = run_row(rate, a.rtt_ms, loss, pair.split(":"), a.seconds, a.mb, mtu_extra, a.relay)
                 rows.append(r)
                 print(json.dumps(r), file=sys.stderr, flush=True)
     res = {"bench": "fairness", "rows": rows}
