@@ -65,10 +65,13 @@ def parse():
                          "this repo's same-host 16 KiB extension (a=x-p2pt-jumbo)")
     ap.add_argument("--no-jumbo-extra", action="store_true",
                     help="skip the untimed jumbo-path point reported beside a std headline")
-    ap.add_argument("--pin", choices=["ccd", "none"], default=os.environ.get("P2PT_BENCH_PIN", "ccd"),
-                    help="ccd (default, one GPU): load generator, mock, serve and proxy on the cores of one L3 "
-                         "domain (utils/pinning.py ccd_plan), the direct leg on the same cores as the tunneled one; "
-                         "none: wherever the scheduler puts them")
+    ap.add_argument("--pin", choices=["ccd", "l3", "none"], default=os.environ.get("P2PT_BENCH_PIN", "none"),
+                    help="none (default): wherever the scheduler puts them; ccd (one GPU): load generator, mock, "
+                         "serve and proxy on the cores of the idlest L3 domain (utils/pinning.py ccd_plan), the "
+                         "direct leg on the same cores. On the shared pool hosts pinned runs stalled ~10 ms behind "
+                         "other jobs' work on those cores in both legs (profiles/r05/b03, b04); l3: every process "
+                         "on one CPU set, a hardware thread per core of the idlest L3 domain, threads placed by the "
+                         "scheduler within it (pinning.l3_set_plan)")
     ap.add_argument("--out", default=None, help="also write the JSON line here")
     return ap.parse_args()
 
@@ -173,9 +176,9 @@ def main():
         dist.barrier()
 
     global PLAN
-    if a.pin == "ccd" and world == 1:  # one GPU's share of the host; N > 1 ranks leave placement to the scheduler
-        from p2p_llm_tunnel_amd.utils.pinning import ccd_plan
-        PLAN = ccd_plan()
+    if a.pin != "none" and world == 1:  # one GPU's share of the host; N > 1 ranks leave placement to the scheduler
+        from p2p_llm_tunnel_amd.utils.pinning import ccd_plan, l3_set_plan
+        PLAN = ccd_plan() if a.pin == "ccd" else l3_set_plan()
     mock, up_port = start_mock(a.mock, a.interval_ms, a.tokens, cpus=PLAN.get("mock"))
     node = dist is not None and a.topology == "node"
     ups = [up_port]
@@ -186,6 +189,8 @@ def main():
     streams = a.streams * (world if node else 1)
     tun = None
     log_env = {"RUST_LOG": "warn,tunnel::serve=info,tunnel::proxy=info,tunnel::transport=info,tunnel::rtc=info"}
+    if PLAN.get("set"):
+        log_env["TUNNEL_PIN_THREADS"] = "0"  # the process on the set, its threads placed by the scheduler
     mtu_flags = ["--no-jumbo-loopback"] if a.mtu == "std" and a.transport == "webrtc" else []
     pin_s = ["--cpu-affinity", PLAN["serve"]] if PLAN else []
     pin_p = ["--cpu-affinity", PLAN["proxy"]] if PLAN else []
@@ -235,6 +240,9 @@ def main():
     # CPU the two tunnel processes used in the timed region (every thread,
     # busy polling included): the price of the latency, reported beside it.
     tunnel_cpu_s = (tun.serve.cpu_s() + tun.proxy.cpu_s() - cpu0) if tun else 0.0
+    from p2p_llm_tunnel_amd.utils.pinning import where
+    placement = {"serve": where(tun.serve.popen.pid), "proxy": where(tun.proxy.popen.pid),
+                 "mock": where(mock.popen.pid)} if tun else None
 
     # ---- untimed: curve points + direct baseline (the same load straight to
     # the upstream; node topology: S x N streams split evenly over the N upstreams)
@@ -319,11 +327,12 @@ def main():
                 "transport": a.transport,
                 "mtu": a.mtu if a.transport == "webrtc" else "n/a",
                 "path_rank0": path,
-                "pinned_rank0": PLAN or None,
+                "pinned_rank0": {k: v for k, v in PLAN.items() if k != "set"} or None,
             },
             "added_p50_ttft_ms": added,
             "added_p99_ttft_ms": added_p99,
             "tunnel_cpu_s_rank0": round(tunnel_cpu_s, 3),
+            "cpus_rank0": placement,
             "tunnel_cpu_cores_rank0": round(tunnel_cpu_s / dt_wall, 4) if dt_wall > 0 else None,
             "p50_ttft_ms": head["p50_ttft_ms"],
             "p99_ttft_ms": head["p99_ttft_ms"],

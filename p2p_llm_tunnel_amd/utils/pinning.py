@@ -188,9 +188,9 @@ def ccd_plan(cpus: list[int] | None = None, busy: dict[int, float] | None = None
     CPUs, and other jobs run on some of them: the CCD is the idlest one
     (/proc/stat over 0.3 s, SMT siblings included, CPU 0's CCD avoided).
     Pinned to CPUs 0-7 regardless, steps stalled ~10 ms behind other runnable
-    work in both legs; left to the scheduler, where the wake-ups landed moved
-    the added p50 TTFT 0.08-0.20 ms between runs of one build
-    (profiles/r05/b03). {} when no L3 domain has 6 cores."""
+    work in both legs (profiles/r05/b03); on the idlest CCD they still did in
+    3 of 12 runs (b04), so bench.py leaves placement to the scheduler by
+    default. {} when no L3 domain has 6 cores."""
     cpus = sorted(os.sched_getaffinity(0)) if cpus is None else list(cpus)
     busy = cpu_busy() if busy is None else busy
     best, best_load = None, None
@@ -207,3 +207,39 @@ def ccd_plan(cpus: list[int] | None = None, busy: dict[int, float] | None = None
     sv = (n - 2 + 1) // 2
     return {"loadgen": fmt_cpus(best[:1]), "mock": fmt_cpus(best[1:2]),
             "serve": fmt_cpus(best[2:2 + sv]), "proxy": fmt_cpus(best[2 + sv:])}
+
+
+def l3_set_plan(cpus: list[int] | None = None, busy: dict[int, float] | None = None) -> dict[str, str]:
+    """Every role on the same CPU SET: one hardware thread of each core of the
+    idlest L3 domain (the SMT siblings left out), and the scheduler places the
+    threads within it. Unlike one CPU per role (ccd_plan), a thread whose CPU
+    another job's work takes is moved to a free one of the set instead of
+    waiting behind it; unlike no pinning, no hop leaves the L3 and no thread
+    runs on the sibling of a busy core (a run whose every hop was 30-40 %
+    slower than another's, mock and client included: profiles/r05/b05)."""
+    cpus = sorted(os.sched_getaffinity(0)) if cpus is None else list(cpus)
+    busy = cpu_busy() if busy is None else busy
+    best, best_load = None, None
+    for g in l3_groups(cpus):
+        cores = physical_cores(g)
+        if len(cores) < 6:
+            continue
+        load = max((busy.get(c, 0.0) for c in g), default=0.0) + (1.0 if 0 in g else 0.0)
+        if best is None or load < best_load:
+            best, best_load = cores, load
+    if not best:
+        return {}
+    s = fmt_cpus(best)
+    return {"loadgen": s, "mock": s, "serve": s, "proxy": s, "set": True}
+
+
+def where(pid: int) -> list[int]:
+    """The CPU each thread of a process last ran on."""
+    out = []
+    try:
+        for t in os.listdir(f"/proc/{pid}/task"):
+            with open(f"/proc/{pid}/task/{t}/stat") as f:
+                out.append(int(f.read().rsplit(")", 1)[1].split()[36]))
+    except (OSError, ValueError, IndexError):
+        pass
+    return sorted(out)
