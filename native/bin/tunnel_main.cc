@@ -97,8 +97,9 @@ const std::vector<Opt>& ext_opts() {
       {"listen-early", nullptr, nullptr, "proxy: bind before the tunnel is up and answer 503 until ready", Kind::Flag,
        Role::Proxy},
       {"metrics-listen", "TUNNEL_METRICS_LISTEN", "", "Serve Prometheus metrics on HOST:PORT"},
-      {"busy-poll-us", "TUNNEL_BUSY_POLL_US", "0",
-       "Keep polling for N us after I/O instead of sleeping (lower per-hop latency, more CPU)", Kind::U64},
+      {"busy-poll-us", "TUNNEL_BUSY_POLL_US", "250",
+       "Keep polling for N us after I/O instead of sleeping: a token's hop then costs no wake-up (0 = always sleep)",
+       Kind::U64},
       {"workers", "TUNNEL_WORKERS", "auto",
        "HTTP worker threads beside the association thread (auto: half the usable CPUs less one, 1..4; 0: single thread)", Kind::U64OrAuto, Role::Both, 0, 256},
       {"inline-streams", "TUNNEL_INLINE_STREAMS", "16",

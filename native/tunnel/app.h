@@ -59,7 +59,15 @@ struct AppConfig {
   std::string metrics_listen;
   size_t upstream_prewarm = 4;
   uint64_t upstream_prewarm_ttl_ms = 1000;
-  uint64_t busy_poll_us = 0;
+  // Adaptive busy polling (Reactor::set_busy_poll_us) on the association
+  // thread and the workers: after any I/O a loop polls epoll for this long
+  // before it sleeps, so the next hop of a request or token (often tens of
+  // microseconds later) finds it awake. A deep-idle CPU on the MI355X host
+  // (C2, 100 us exit latency) took 10-20 us longer per hand-off
+  // (tunnel-wakebench, profiles/r05/b01); the headline's added p50 TTFT went
+  // 0.157 -> 0.115 ms over 12 interleaved runs of 0 vs 250 us (b02-b04) for
+  // 0.4-1 % of a core per tunnel process.
+  uint64_t busy_poll_us = 250;
   // HTTP worker threads next to the association thread (-1 = auto: one per
   // 4 CPUs, 1..4; 0 = everything on one reactor thread).
   int workers = -1;
