@@ -65,13 +65,14 @@ def parse():
                          "this repo's same-host 16 KiB extension (a=x-p2pt-jumbo)")
     ap.add_argument("--no-jumbo-extra", action="store_true",
                     help="skip the untimed jumbo-path point reported beside a std headline")
-    ap.add_argument("--pin", choices=["ccd", "l3", "none"], default=os.environ.get("P2PT_BENCH_PIN", "none"),
+    ap.add_argument("--pin", choices=["ccd", "l3", "numa", "none"], default=os.environ.get("P2PT_BENCH_PIN", "none"),
                     help="none (default): wherever the scheduler puts them; ccd (one GPU): load generator, mock, "
                          "serve and proxy on the cores of the idlest L3 domain (utils/pinning.py ccd_plan), the "
                          "direct leg on the same cores. On the shared pool hosts pinned runs stalled ~10 ms behind "
                          "other jobs' work on those cores in both legs (profiles/r05/b03, b04); l3: every process "
                          "on one CPU set, a hardware thread per core of the idlest L3 domain, threads placed by the "
-                         "scheduler within it (pinning.l3_set_plan)")
+                         "scheduler within it (pinning.l3_set_plan); numa: every process on the CPUs of the idlest "
+                         "NUMA node (pinning.numa_plan)")
     ap.add_argument("--out", default=None, help="also write the JSON line here")
     return ap.parse_args()
 
@@ -177,8 +178,8 @@ def main():
 
     global PLAN
     if a.pin != "none" and world == 1:  # one GPU's share of the host; N > 1 ranks leave placement to the scheduler
-        from p2p_llm_tunnel_amd.utils.pinning import ccd_plan, l3_set_plan
-        PLAN = ccd_plan() if a.pin == "ccd" else l3_set_plan()
+        from p2p_llm_tunnel_amd.utils import pinning
+        PLAN = {"ccd": pinning.ccd_plan, "l3": pinning.l3_set_plan, "numa": pinning.numa_plan}[a.pin]()
     mock, up_port = start_mock(a.mock, a.interval_ms, a.tokens, cpus=PLAN.get("mock"))
     node = dist is not None and a.topology == "node"
     ups = [up_port]

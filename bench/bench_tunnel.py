@@ -117,7 +117,11 @@ def idle_burst(transport, idle_s=30, burst=16):
                     env={"RUST_LOG": "info,tunnel::serve=debug"}) as t:
             loadgen(t.proxy_port, 1, 1)
             pings0 = t.serve.count("sent keepalive ping")
-            time.sleep(idle_s)
+            t_end = time.time() + idle_s
+            while time.time() < t_end:  # a progress line every 30 s (long idles must not look hung)
+                time.sleep(min(30.0, max(0.0, t_end - time.time())))
+                print(json.dumps({"idle_progress_s": round(idle_s - max(0.0, t_end - time.time()), 1),
+                                  "pings": t.serve.count("sent keepalive ping") - pings0}), file=sys.stderr, flush=True)
             pings = t.serve.count("sent keepalive ping") - pings0
             r = loadgen(t.proxy_port, burst, 1)
             d = loadgen(port, burst, 1)

@@ -243,3 +243,41 @@ def where(pid: int) -> list[int]:
     except (OSError, ValueError, IndexError):
         pass
     return sorted(out)
+
+
+def numa_nodes() -> dict[int, list[int]]:
+    """NUMA node -> its CPUs (one node holding every CPU where sysfs has none)."""
+    out: dict[int, list[int]] = {}
+    base = "/sys/devices/system/node"
+    try:
+        for name in sorted(os.listdir(base)):
+            if name.startswith("node") and name[4:].isdigit():
+                with open(os.path.join(base, name, "cpulist")) as f:
+                    out[int(name[4:])] = parse_cpus(f.read().strip())
+    except OSError:
+        pass
+    return out or {0: sorted(os.sched_getaffinity(0))}
+
+
+def numa_plan(busy: dict[int, float] | None = None) -> dict:
+    """Every role on the CPUs of ONE NUMA node (one socket here: 64 cores and
+    their SMT siblings), the node with the most idle CPUs; threads placed by
+    the scheduler within it. Left to the scheduler over both sockets, runs
+    whose threads ended up split across the sockets were the slow ones (the
+    round trip of a frame through a remote L3; profiles/r05/b06, b07
+    cpus_rank0); one CPU per role stalled behind other jobs' work (b03, b04),
+    which a 128-CPU set avoids."""
+    allowed = set(os.sched_getaffinity(0))
+    busy = cpu_busy() if busy is None else busy
+    best, best_idle = None, -1.0
+    for node, cpus in numa_nodes().items():
+        cpus = [c for c in cpus if c in allowed]
+        if not cpus:
+            continue
+        idle = sum(1.0 - busy.get(c, 0.0) for c in cpus)
+        if idle > best_idle:
+            best, best_idle = cpus, idle
+    if not best:
+        return {}
+    s = fmt_cpus(best)
+    return {"loadgen": s, "mock": s, "serve": s, "proxy": s, "set": True}
