@@ -201,11 +201,22 @@ static int wait_events(int epfd, epoll_event* evs, int max, int64_t timeout_us) 
 void Reactor::run_once(int64_t timeout_us) {
   epoll_event evs[256];
   bool spin = false;
-  if (busy_poll_us_ && timeout_us > 0 && now_us() - last_io_us_ < busy_poll_us_) {
-    timeout_us = 0;
-    spin = true;
-  }
   const uint64_t t_wait = now_us();
+  if (busy_poll_us_) {
+    if (t_wait - spin_win_start_us_ >= kSpinWindowUs) {
+      spin_win_start_us_ = t_wait;
+      spin_win_used_us_ = 0;
+    }
+    // Within the window's spin budget only: a loop woken every few
+    // microseconds (the node row, 1024 streams of 1 ms tokens) would
+    // otherwise poll through all its idle time — 4.8 cores per tunnel process
+    // against 1.1-1.7 sleeping, and the job's CPU quota throttled
+    // (profiles/r05/b07 node).
+    if (timeout_us > 0 && t_wait - last_io_us_ < busy_poll_us_ && spin_win_used_us_ < kSpinBudgetUs) {
+      timeout_us = 0;
+      spin = true;
+    }
+  }
   // An empty polling turn is idle time, not load (a transport reads load() to
   // decide whether to hold small flushes: counting the spin would make every
   // polling loop look half busy).
@@ -227,7 +238,10 @@ void Reactor::run_once(int64_t timeout_us) {
   // Nothing ready, no timer due and nothing posted: no hook has new work.
   idle_turn_ = spin && n <= 0 && posted_.empty() &&
                (timer_order_.empty() || timer_order_.begin()->first > wake_us_);
-  if (idle_turn_) return;
+  if (idle_turn_) {
+    spin_win_used_us_ += wake_us_ - t_wait;
+    return;
+  }
   for (int i = 0; i < n; i++) {
     uint64_t tag = evs[i].data.u64;
     if (tag == kWakeTag) {
