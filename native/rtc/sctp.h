@@ -134,6 +134,9 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   size_t buffered_amount() const { return unsent_bytes_; }
   // A SACK the next flush sends right away (>= 2 data packets unacknowledged,
   // a gap or duplicate to report, or the delayed-SACK timer fired).
+  // Retransmissions or control chunks (stream reset, FORWARD-TSN, ...) are
+  // waiting: a flush must not be held back for coalescing.
+  bool urgent_pending() const { return !rtx_.empty() || !ctrl_.empty(); }
   bool ack_due() const {
     return sack_needed_ && (sack_urgent_ || data_pkts_unacked_ >= 2 || !ooo_.empty() || !dups_.empty());
   }
