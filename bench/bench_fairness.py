@@ -71,8 +71,8 @@ class NativeRelay:
                 break
 
 
-def run_row(rate, rtt_ms, loss, pair, seconds, mb, mtu_extra, relay="native"):
-    queue_kb = max(32, int(rate * 1e6 / 8 * rtt_ms / 1e3 / 1024))
+def run_row(rate, rtt_ms, loss, pair, seconds, mb, mtu_extra, relay="native", queue_kb=0):
+    queue_kb = queue_kb or max(32, int(rate * 1e6 / 8 * rtt_ms / 1e3 / 1024))
     link = None
     if relay == "native":
         turn = NativeRelay(rate, rtt_ms / 2, queue_kb, loss)
@@ -127,6 +127,7 @@ def main():
     ap.add_argument("--mb", type=int, default=8, help="size of each download in the loop")
     ap.add_argument("--jumbo", action="store_true", help="allow the jumbo path (default: 1200-byte MTU)")
     ap.add_argument("--relay", choices=["native", "python"], default="native")
+    ap.add_argument("--queue-kb", type=float, default=0, help="bottleneck queue (default: one BDP, at least 32 KiB)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     ensure_native()
@@ -135,7 +136,7 @@ def main():
     for rate in [float(x) for x in a.rates.split(",")]:
         for loss in [float(x) for x in a.losses.split(",")]:
             for pair in a.pairs.split(","):
-                r = run_row(rate, a.rtt_ms, loss, pair.split(":"), a.seconds, a.mb, mtu_extra, a.relay)
+                r = run_row(rate, a.rtt_ms, loss, pair.split(":"), a.seconds, a.mb, mtu_extra, a.relay, a.queue_kb)
                 rows.append(r)
                 print(json.dumps(r), file=sys.stderr, flush=True)
     res = {"bench": "fairness", "rows": rows}

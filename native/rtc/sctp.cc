@@ -1194,7 +1194,8 @@ void SctpAssociation::loss_response(bool random_loss, bool over_bdp, uint64_t no
   // sqrt((2 - b) / (2 b p)) against Reno's sqrt(1.5 / p): b = 0.2 is 1.7x
   // Reno, within the 2x bound; the cost is bulk on paths with genuinely
   // random loss.
-  const int random_beta_pct = cc_policy().random_beta_pct;
+  const int random_beta_pct = cfg_.random_beta_pct >= 0 ? std::clamp(cfg_.random_beta_pct, 50, 100)
+                                                        : cc_policy().random_beta_pct;
   last_loss_us_ = now;
   size_t keep = cwnd_ * 7 / 10;
   if (random_loss) {

@@ -51,9 +51,12 @@ struct SctpConfig {
   // INIT-ACK; once both sides did, packets after setup carry checksum 0 and a
   // received checksum of 0 is not verified.
   bool zero_checksum = false;
-  // Redundant copies of small whole messages: 1 always, 0 never, -1 from
-  // TUNNEL_SCTP_DUP or, unset, once the path has shown random loss.
+  // Redundant copies of small whole messages: 1 always, 0 never, -1 once
+  // the path has shown random loss.
   int dup_small = -1;
+  // cwnd kept after a random loss, in % (50..100); -1: cc_policy() (tests
+  // compare policies on one link with it).
+  int random_beta_pct = -1;
 };
 
 // Congestion response (TUNNEL_SCTP_CC, read once; see sctp.cc).

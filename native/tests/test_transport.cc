@@ -77,9 +77,10 @@ struct SctpPair {
   std::vector<std::pair<uint16_t, std::string>> got_a, got_b;
   size_t zero_sums_a = 0, zero_sums_b = 0;  // packets sent with checksum 0
   SctpPair(double loss, double dup, uint64_t delay, size_t mtu = 1200, bool zc_a = false, bool zc_b = false,
-           uint64_t rto_min_ms = 20)
+           uint64_t rto_min_ms = 20, int random_beta_pct = -1)
       : link(r, loss, dup, delay) {
     SctpConfig cfg;
+    cfg.random_beta_pct = random_beta_pct;
     cfg.mtu = mtu;
     cfg.rto_initial_ms = 100;
     cfg.rto_min_ms = rto_min_ms;
