@@ -72,7 +72,7 @@ struct SctpStats {
   uint64_t late_tsns = 0;  // new TSNs that arrived below the highest one seen (holes filled, reordering)
   uint64_t retransmits = 0, fast_retransmits = 0, t3_expirations = 0;
   uint64_t tlp_probes = 0, rack_marks = 0, random_loss_events = 0;
-  uint64_t random_loss_cuts = 0;  // random-loss episodes that cut cwnd (TUNNEL_SCTP_RANDOM_BETA_PCT)
+  uint64_t random_loss_cuts = 0;  // random-loss episodes that cut cwnd
   uint64_t congestion_cuts = 0;   // loss episodes read as congestion (0.7 cut)
   uint64_t queue_cuts = 0;        // short-path queue bound: cwnd cuts for a standing queue
   uint64_t over_bdp_losses = 0;   // ... of them because cwnd was past the delivery-rate BDP
