@@ -85,6 +85,16 @@ using RawBufPtr = std::shared_ptr<RawBuf>;
 // relaxed load, so this orders the reuse after their last reads.
 inline void reuse_fence() { std::atomic_thread_fence(std::memory_order_acquire); }
 
+// A received chunk whose payload another thread (a receive lane) already
+// copied into a reassembly buffer: `body` identifies the chunk inside its
+// decrypted packet; the payload sits at buf[off, off + payload length).
+// (rtc/sctp.h SctpPreassembler.)
+struct PreCopied {
+  const uint8_t* body;
+  uint32_t off;
+  RawBufPtr buf;
+};
+
 // Recycling pool of fixed-size receive buffers whose contents are handed up
 // the stack as zero-copy views (datagram receive: DTLS decrypts in place and
 // SCTP messages are views of the datagram). A buffer goes back into service

@@ -326,9 +326,9 @@ void TxLaneState::send(SealedBatch& sb, int fd, const SockAddr& to) {
 // ------------------------------------------------------------------ RX reader
 
 RxReader::RxReader(int fd, const SockAddr& remote, std::shared_ptr<const RecordKeys> keys, Deliver deliver, uint64_t id,
-                   size_t slot, bool adaptive)
+                   size_t slot, bool adaptive, RxScan scan)
     : fd_(fd), stop_fd_(eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC)), remote_(remote), keys_(std::move(keys)),
-      deliver_(std::move(deliver)), id_(id), slot_(slot), pool_(slot), adaptive_(adaptive), active_(!adaptive) {
+      deliver_(std::move(deliver)), scan_(std::move(scan)), id_(id), slot_(slot), pool_(slot), adaptive_(adaptive), active_(!adaptive) {
   th_ = std::thread([this] {
     sigset_t mask;
     sigemptyset(&mask);
@@ -426,6 +426,7 @@ void RxReader::segment(const RawBufPtr& buf, uint32_t off, uint32_t len, const S
     size_t ptl = 0;
     r.ok = open_record(*keys_->r, keys_->riv, rec, rl, &r.pt, &ptl);
     r.ptl = uint32_t(ptl);
+    if (r.ok && scan_) scan_(r.pt, ptl, b.opened.pre);
     r.owner = buf;
     b.opened.bytes += rl;
     b.opened.recs.push_back(std::move(r));
