@@ -441,12 +441,12 @@ void SctpPreassembler::scan(const uint8_t* p, size_t n, std::vector<PreCopied>& 
       if (r->buf && r->off + dlen > r->buf->cap) r->buf.reset();  // larger than a tunnel frame
       if (r->buf) {
         memcpy(r->buf->data.get() + r->off, body + 12, dlen);
-        out.push_back(PreCopied{body, uint32_t(r->off), r->buf});
+        out.push_back(PreCopied{body, uint32_t(r->off), r->buf.get(), r->off ? nullptr : r->buf});
         r->off += dlen;
         r->next_tsn = tsn + 1;
         if (flags & 1) r->buf.reset();  // E: complete
       } else {
-        out.push_back(PreCopied{body, 0, nullptr});  // one entry per fragment keeps take_pre's lookup O(1)
+        out.push_back(PreCopied{body, 0, nullptr, nullptr});  // one entry per fragment keeps take_pre's lookup O(1)
       }
     }
     off += (clen + 3) & ~size_t(3);
@@ -699,8 +699,8 @@ void SctpAssociation::deliver_chunk(uint8_t fl, uint16_t st, uint16_t ssn, uint3
     // are gone — possibly on a worker thread) — or into the receive lane's,
     // which copied this fragment already (SctpPreassembler).
     if (!chain) {
-      if (pc && pc->buf && pc->off == 0) {
-        pa.buf = pc->buf;
+      if (pc && pc->keep && pc->off == 0) {
+        pa.buf = pc->keep;
         pa.lane = true;
       } else {
         pa.buf = reasm_pool_.get();
@@ -710,7 +710,10 @@ void SctpAssociation::deliver_chunk(uint8_t fl, uint16_t st, uint16_t ssn, uint3
     pa.active = true;
   }
   if (!pa.active) return;  // middle fragment without a beginning (after FORWARD-TSN)
-  if (pa.lane && !(pc && pc->buf == pa.buf && pc->off == pa.len)) {
+  // A lane entry without a reference is safe to take only for the buffer
+  // held here (pa.buf keeps it from going back to the lane's pool, so an
+  // entry naming it was made for this message).
+  if (pa.lane && !(pc && pc->buf == pa.buf.get() && pc->off == pa.len)) {
     // The lane lost the sequence (a loss, a retransmission, a burst opened
     // inline): continue in a buffer of our own — the lane may still write
     // past this point into its own.

@@ -1153,7 +1153,7 @@ void ProxySession::route(const proto::Frame& f) {
           trace::rx_stamps("proxy", f.stream_id);
         }
         Cmd c{Cmd::Body, f.stream_id};
-        c.data = f.payload;
+        c.data = f.more.empty() ? links_[it->second.thread].to->stage(f.payload) : f.payload;
         c.more = f.more;
         command(it->second.thread, std::move(c));
       }

@@ -107,6 +107,7 @@ class ServeWorker : public std::enable_shared_from_this<ServeWorker> {
 
   void emit(uint32_t sid, proto::Frame f) {
     ServeSession::Ev ev(ServeSession::Ev::Frame, sid);
+    if (f.type == proto::MsgType::ResBody && f.more.empty()) f.payload = out_->stage(f.payload);
     ev.frame = std::move(f);
     out_->push(std::move(ev));
   }

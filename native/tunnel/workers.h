@@ -25,6 +25,7 @@
 
 #include <atomic>
 #include <cstdlib>
+#include <cstring>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -34,6 +35,7 @@
 #include <thread>
 #include <vector>
 
+#include "core/buf.h"
 #include "core/reactor.h"
 
 namespace p2pt {
@@ -87,6 +89,7 @@ class Pipe {
         auto batch = std::make_shared<std::vector<M>>(std::move(st->buf));
         st->buf.clear();
         st->buf.reserve(batch->size());
+        st->arena.reset();  // the next batch stages into another one
         d->post_threadsafe([st, batch] {
           if (st->closed) return;
           for (auto& m : *batch) st->sink(m);
@@ -108,6 +111,27 @@ class Pipe {
     }
     state_->buf.push_back(std::move(m));
   }
+  // A small payload for a message of this pipe, copied into the current
+  // batch's own arena (src thread). The arena's reference count is updated by
+  // src while the batch fills and by dst after it: one cache-line transfer per
+  // batch. A view of a buffer that both threads keep referencing — a slab of
+  // token copies the association thread fills while workers release earlier
+  // tokens of it — moves that line once per message each way: 1 ms tokens at
+  // 1024 streams had the association threads spend ~30 % (proxy) and ~10 %
+  // (serve) of their time in such updates (profiles/r05/b11/nodeprof).
+  Bytes stage(const Bytes& b) {
+    if (!hook_ || b.empty() || b.size() > kStageMax) return b;
+    State& st = *state_;
+    if (!st.arena || st.arena_off + b.size() > kArena) {
+      st.arena = st.arenas.get();
+      st.arena_off = 0;
+    }
+    uint8_t* d = st.arena->data.get() + st.arena_off;
+    memcpy(d, b.data(), b.size());
+    st.arena_off += (b.size() + 15) & ~size_t(15);
+    return Bytes::adopt(st.arena, d, b.size());
+  }
+  static constexpr size_t kStageMax = 2048, kArena = 32 * 1024;
   // Stop delivering (also batches already posted). src thread only; the flag
   // is read on dst's thread, so it is atomic.
   void close() { state_->closed = true; }
@@ -119,6 +143,9 @@ class Pipe {
     Sink sink;
     std::vector<M> buf;  // src thread only
     std::atomic<bool> closed{false};
+    BufPool arenas{kArena, 64};  // stage(): src thread only
+    RawBufPtr arena;
+    size_t arena_off = 0;
   };
   Reactor& src_;
   Reactor& dst_;
