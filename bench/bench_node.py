@@ -103,7 +103,14 @@ HOPS = [("proxy", "accept", "proxy", "req_end"), ("proxy", "req_end", "serve", "
         ("serve", "req_headers", "serve", "req_end"), ("serve", "req_end", "serve", "upstream_sent"),
         ("serve", "upstream_sent", "serve", "first_body"), ("serve", "first_body", "serve", "sched_in"),
         ("serve", "sched_in", "serve", "chan_tx"), ("serve", "chan_tx", "proxy", "chan_rx"),
-        ("proxy", "chan_rx", "proxy", "first_body"), ("proxy", "accept", "proxy", "first_body")]
+        ("proxy", "chan_rx", "proxy", "first_body"), ("proxy", "accept", "proxy", "first_body"),
+        # the two crossings split at the transport stamps (scripts/ttft_breakdown.py)
+        ("proxy", "req_end", "proxy", "udp_tx"), ("proxy", "udp_tx", "serve", "udp_kernel"),
+        ("serve", "udp_kernel", "serve", "udp_read"), ("serve", "udp_read", "serve", "rx_assoc"),
+        ("serve", "rx_assoc", "serve", "req_headers"),
+        ("serve", "chan_tx", "serve", "udp_tx"), ("serve", "udp_tx", "proxy", "udp_kernel"),
+        ("proxy", "udp_kernel", "proxy", "udp_read"), ("proxy", "udp_read", "proxy", "rx_assoc"),
+        ("proxy", "rx_assoc", "proxy", "chan_rx")]
 
 
 def node_hops(traces, windows):

@@ -45,8 +45,9 @@ class ProxyWorker : public std::enable_shared_from_this<ProxyWorker> {
   }
   void send(proto::Frame f) {
     ProxySession::Ev ev(ProxySession::Ev::Frame, f.stream_id);
+    const bool urgent = f.type == proto::MsgType::ReqHeaders || f.type == proto::MsgType::ReqEnd;
     ev.frame = std::move(f);
-    out_->push(std::move(ev));
+    out_->push(std::move(ev), urgent);
   }
   bool ready() const { return shared_->ready.load(std::memory_order_relaxed); }
   size_t body_chunk() const { return shared_->body_chunk; }
@@ -1137,6 +1138,7 @@ void ProxySession::route(const proto::Frame& f) {
       auto it = routes_.find(sid);
       if (it != routes_.end()) {
         Cmd c{Cmd::Headers, sid};
+        c.urgent = true;
         c.rh = std::move(rh);
         command(it->second.thread, std::move(c));
       }
@@ -1147,12 +1149,14 @@ void ProxySession::route(const proto::Frame& f) {
       if (shared_->flow.load(std::memory_order_relaxed))
         shared_->rtt_us.store(ch_ ? ch_->rtt_hint_us() : 0, std::memory_order_relaxed);
       if (it != routes_.end()) {
-        if (!it->second.body_seen) {
+        const bool first = !it->second.body_seen;
+        if (first) {
           it->second.body_seen = true;
           trace::event("proxy", f.stream_id, "chan_rx");
           trace::rx_stamps("proxy", f.stream_id);
         }
         Cmd c{Cmd::Body, f.stream_id};
+        c.urgent = first;
         c.data = f.more.empty() ? links_[it->second.thread].to->stage(f.payload) : f.payload;
         c.more = f.more;
         command(it->second.thread, std::move(c));

@@ -99,6 +99,7 @@ class ProxySession : public std::enable_shared_from_this<ProxySession> {
     std::vector<Bytes> more;                      // Body: the rest of a frame that arrived in fragments
     std::shared_ptr<proto::ResponseHeaders> rh;   // Headers
     uint32_t bytes = 0;                           // Credit: REQ_BODY bytes granted by serve
+    bool urgent = false;                          // the start of a response: handed over at once (Pipe::push)
   };
   // A connection thread -> association thread.
   struct Ev {
@@ -134,7 +135,10 @@ class ProxySession : public std::enable_shared_from_this<ProxySession> {
   bool bind_listener();
   void on_event(size_t thread, Ev& ev);
   void check_paused();
-  void command(size_t thread, Cmd c) { links_[thread].to->push(std::move(c)); }
+  void command(size_t thread, Cmd c) {
+    const bool urgent = c.urgent;
+    links_[thread].to->push(std::move(c), urgent);
+  }
 
   Reactor& r_;
   std::shared_ptr<MessageChannel> ch_;

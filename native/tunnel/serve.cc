@@ -105,11 +105,13 @@ class ServeWorker : public std::enable_shared_from_this<ServeWorker> {
     out_->push(std::move(ev));
   }
 
-  void emit(uint32_t sid, proto::Frame f) {
+  // urgent: the start of a response (headers, first body): handed to the
+  // association thread at once, not at the end of this loop turn.
+  void emit(uint32_t sid, proto::Frame f, bool urgent = false) {
     ServeSession::Ev ev(ServeSession::Ev::Frame, sid);
     if (f.type == proto::MsgType::ResBody && f.more.empty()) f.payload = out_->stage(f.payload);
     ev.frame = std::move(f);
-    out_->push(std::move(ev));
+    out_->push(std::move(ev), urgent);
   }
 
   void simple_response(uint32_t sid, uint16_t status, const std::string& body) {
@@ -152,7 +154,7 @@ class ServeWorker : public std::enable_shared_from_this<ServeWorker> {
       rh.status = uint16_t(h.status);
       for (auto& hd : h.headers)
         if (http::is_visible_ascii(hd.value)) proto::header_set(rh.headers, http::to_lower(hd.name), hd.value);
-      s->emit(sid, proto::make_res_headers(rh));
+      s->emit(sid, proto::make_res_headers(rh), true);
       trace::event("serve", sid, "res_headers");
     };
     auto first = std::make_shared<bool>(true);
@@ -160,6 +162,7 @@ class ServeWorker : public std::enable_shared_from_this<ServeWorker> {
     cb.on_data = [w, sid, first, cs](Bytes chunk) {
       auto s = w.lock();
       if (!s) return;
+      const bool urgent = *first;
       if (*first) {
         *first = false;
         trace::event("serve", sid, "first_body");
@@ -168,7 +171,7 @@ class ServeWorker : public std::enable_shared_from_this<ServeWorker> {
       // private copy (small ones, e.g. SSE tokens); frames slice it, no copy.
       size_t n = chunk.size();
       for (size_t off = 0; off < n; off += cs)
-        s->emit(sid, proto::make_body(proto::MsgType::ResBody, sid, chunk.slice(off, cs)));
+        s->emit(sid, proto::make_body(proto::MsgType::ResBody, sid, chunk.slice(off, cs)), urgent && off + cs >= n);
     };
     cb.on_done = [w, sid, back, unreachable](const std::string& err, bool before_head) {
       auto s = w.lock();

@@ -170,7 +170,10 @@ class ServeSession : public std::enable_shared_from_this<ServeSession> {
   void set_paused(uint32_t sid, Inflight& fl);
   void grant(uint32_t sid, uint64_t& owed, uint64_t n, bool force = false);
   void reject_too_large(uint32_t sid);
-  void command(size_t thread, Cmd c) { links_[thread].to->push(std::move(c)); }
+  void command(size_t thread, Cmd c) {
+    const bool urgent = c.kind == Cmd::Start;  // a new request: handed over at once (Pipe::push)
+    links_[thread].to->push(std::move(c), urgent);
+  }
 
   Reactor& r_;
   std::shared_ptr<MessageChannel> ch_;
