@@ -212,7 +212,11 @@ void Reactor::run_once(int64_t timeout_us) {
     // otherwise poll through all its idle time — 4.8 cores per tunnel process
     // against 1.1-1.7 sleeping, and the job's CPU quota throttled
     // (profiles/r05/b07 node).
-    if (timeout_us > 0 && t_wait - last_io_us_ < busy_poll_us_ && spin_win_used_us_ < kSpinBudgetUs) {
+    // Not on a saturated loop either: it rarely sleeps, so polling buys it
+    // little latency, and at node scale its polling turns were CPU the job's
+    // quota did not have (profiles/r05/b14/node).
+    if (timeout_us > 0 && t_wait - last_io_us_ < busy_poll_us_ && spin_win_used_us_ < kSpinBudgetUs &&
+        lightly_loaded()) {
       timeout_us = 0;
       spin = true;
     }
@@ -253,7 +257,10 @@ void Reactor::run_once(int64_t timeout_us) {
         std::lock_guard<std::mutex> lk(ts_mu_);
         fns.swap(ts_posted_);
       }
-      for (auto& f : fns) f();
+      for (auto& f : fns) {
+        f();
+        maybe_flush_soon();
+      }
       continue;
     }
     if (tag == kSigTag) {
@@ -273,9 +280,11 @@ void Reactor::run_once(int64_t timeout_us) {
     if (it == fds_.end() || it->second.gen != g) continue;
     auto cb = it->second.cb;  // keep alive across the call
     (*cb)(evs[i].events);
+    maybe_flush_soon();
   }
   run_timers();
   run_posted();
+  flush_soon_ = false;
   run_flush();
 }
 

@@ -56,6 +56,23 @@ class Reactor {
   // Hook that runs after each event batch; returns an id for removal.
   uint64_t add_flush_hook(Fn fn);
   void remove_flush_hook(uint64_t id);
+  // Latency-critical work was just queued (a request, the start of a
+  // response): run posted work and the flush hooks as soon as the current
+  // callback returns instead of after the rest of this turn's events — on a
+  // loaded loop a turn of token work took 0.5-1.8 ms (profiles/r05/b13).
+  // flushing_soon(): inside such an early flush (transports send what they
+  // hold instead of coalescing it). Only while the loop is not saturated
+  // (lightly_loaded()): a saturated loop would pay a flush's syscalls per
+  // request, and the node row's job then spent more time throttled at its CPU
+  // quota than it saved (profiles/r05/b14/node).
+  void flush_soon() {
+    if (lightly_loaded()) flush_soon_ = true;
+  }
+  // Below half busy over the last load window: latency shortcuts (early
+  // flushes, urgent hand-offs, busy polling) pay for themselves.
+  static constexpr double kLightLoad = 0.5;
+  bool lightly_loaded() const { return load_ < kLightLoad; }
+  bool flushing_soon() const { return soon_active_; }
 
   // SIGINT/SIGTERM etc. delivered via signalfd on the loop thread.
   void on_signal(int signo, Fn fn);
@@ -83,6 +100,14 @@ class Reactor {
   void run_timers();
   void run_posted();
   void run_flush();
+  void maybe_flush_soon() {
+    if (!flush_soon_) return;
+    flush_soon_ = false;
+    soon_active_ = true;
+    run_posted();
+    run_flush();
+    soon_active_ = false;
+  }
 
   struct FdEntry {
     uint64_t gen;
@@ -96,6 +121,7 @@ class Reactor {
   uint64_t last_io_us_ = 0;
   uint64_t win_start_us_ = 0, win_busy_us_ = 0, wake_us_ = 0;
   bool idle_turn_ = false;  // the last turn was an empty busy-polling one
+  bool flush_soon_ = false, soon_active_ = false;
   // Busy polling may use at most kSpinBudgetUs of every kSpinWindowUs (10 % of
   // a core): sparse traffic (a token every few ms) polls through every gap
   // that matters, dense traffic sleeps between events as without polling.

@@ -223,7 +223,7 @@ void PeerConnection::flush() {
     const uint64_t now = Reactor::now_us();
     const size_t q = sctp_->buffered_amount();
     if (q > 0 && q < mtu_ && now - last_flush_us_ < coalesce_us_ && !sctp_->ack_due() && !sctp_->urgent_pending() &&
-        r_.load() >= coalesce_load_) {
+        !r_.flushing_soon() && r_.load() >= coalesce_load_) {
       coalesced_flushes_++;
       if (!coalesce_timer_) {
         std::weak_ptr<PeerConnection> w = shared_from_this();

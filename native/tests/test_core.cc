@@ -144,6 +144,36 @@ TEST(reactor_load_tracks_busy_share) {
   CHECK(idle < 0.2);
 }
 
+// flush_soon(): posted work and the flush hooks run right after the callback
+// that asked, ahead of the rest of the turn's events; without it they run
+// once, at the end of the turn.
+TEST(reactor_flush_soon_runs_hooks_before_the_rest_of_the_turn) {
+  Reactor r;
+  std::vector<std::string> seen;
+  r.add_flush_hook([&] { seen.push_back("flush"); });
+  // Both queued before the loop runs: one wake-up, one turn.
+  r.post_threadsafe([&] {
+    seen.push_back("a");
+    r.post([&] { seen.push_back("a-posted"); });
+    r.flush_soon();
+  });
+  r.post_threadsafe([&] {
+    seen.push_back("b");
+    CHECK(!r.flushing_soon());
+  });
+  r.run_until([&] { return seen.size() >= 5; }, 500);
+  const std::vector<std::string> want = {"a", "a-posted", "flush", "b", "flush"};
+  CHECK(seen == want);
+  Reactor q;
+  std::vector<std::string> seen2;
+  q.add_flush_hook([&] { seen2.push_back("flush"); });
+  q.post_threadsafe([&] { seen2.push_back("a"); });
+  q.post_threadsafe([&] { seen2.push_back("b"); });
+  q.run_until([&] { return seen2.size() >= 3; }, 500);
+  const std::vector<std::string> want2 = {"a", "b", "flush"};
+  CHECK(seen2 == want2);
+}
+
 TEST(frame_codec) {
   proto::Frame f{proto::MsgType::ResBody, 0xDEADBEEF, Bytes::copy("abc")};
   Bytes e = f.encode();

@@ -737,6 +737,7 @@ void ProxyWorker::handle(ProxySession::Cmd& c) {
   auto it = streams_.find(c.sid);
   if (it == streams_.end()) return;
   auto conn = it->second.lock();
+  if (c.urgent) r_.flush_soon();  // the client write of a response's start, now
   switch (c.kind) {
     case Cmd::Headers:
       if (conn) conn->on_res_headers(*c.rh);
@@ -1090,6 +1091,9 @@ void ProxySession::on_event(size_t thread, Ev& ev) {
   }
   bool body = ev.frame.type == proto::MsgType::ReqBody;
   uint32_t sid = ev.frame.stream_id;
+  // A request goes out on the transport now, not after the rest of this
+  // loop turn (Reactor::flush_soon).
+  if (ev.frame.type == proto::MsgType::ReqHeaders || ev.frame.type == proto::MsgType::ReqEnd) r_.flush_soon();
   sched_->send(std::move(ev.frame));
   if (!body) return;
   auto it = routes_.find(sid);

@@ -39,7 +39,10 @@ class ServeWorker : public std::enable_shared_from_this<ServeWorker> {
   void handle(ServeSession::Cmd& c) {
     using Cmd = ServeSession::Cmd;
     switch (c.kind) {
-      case Cmd::Start: start(c.sid, std::move(c.req), c.body_chunk, c.retryable, c.grant); break;
+      case Cmd::Start:
+        start(c.sid, std::move(c.req), c.body_chunk, c.retryable, c.grant);
+        r_.flush_soon();  // the upstream request is written now, not after this turn's token work
+        break;
       case Cmd::Cancel: {
         auto it = calls_.find(c.sid);
         if (it == calls_.end()) break;
@@ -802,6 +805,9 @@ void ServeSession::on_event(Ev& ev) {
   size_t n = ev.frame.payload.size();
   if (ev.frame.type == proto::MsgType::ResHeaders) fl.res_streaming = BulkRoutes::streaming_type(ev.frame.payload.view());
   if (body && fl.res_bytes == 0) trace::event("serve", ev.sid, "sched_in");  // first body frame reaches the scheduler
+  // The start of a response goes out on the transport now, not after the
+  // rest of this loop turn (Reactor::flush_soon).
+  if (ev.frame.type == proto::MsgType::ResHeaders || (body && fl.res_bytes == 0)) r_.flush_soon();
   sched_->send(std::move(ev.frame));
   if (!body) return;
   fl.res_bytes += n;

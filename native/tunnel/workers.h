@@ -106,7 +106,7 @@ class Pipe {
       return;
     }
     state_->buf.push_back(std::move(m));
-    if (urgent) send(state_, dst_);
+    if (urgent && src_.lightly_loaded()) send(state_, dst_);  // a saturated src batches (Reactor::flush_soon)
   }
   // A small payload for a message of this pipe, copied into the current
   // batch's own arena (src thread). The arena's reference count is updated by
