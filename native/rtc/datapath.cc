@@ -329,6 +329,7 @@ RxReader::RxReader(int fd, const SockAddr& remote, std::shared_ptr<const RecordK
                    size_t slot, bool adaptive, RxScan scan)
     : fd_(fd), stop_fd_(eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC)), remote_(remote), keys_(std::move(keys)),
       deliver_(std::move(deliver)), scan_(std::move(scan)), id_(id), slot_(slot), pool_(slot), adaptive_(adaptive), active_(!adaptive) {
+  for (auto& l : open_) l = std::make_unique<Lane>("p2pt-udp-open");
   th_ = std::thread([this] {
     sigset_t mask;
     sigemptyset(&mask);
@@ -350,6 +351,7 @@ RxReader::~RxReader() {
   }
   cv_.notify_all();
   th_.join();
+  for (auto& l : open_) l.reset();  // runs (and delivers) what is queued, then joins
   if (stop_fd_ >= 0) ::close(stop_fd_);
 }
 
@@ -423,14 +425,39 @@ void RxReader::segment(const RawBufPtr& buf, uint32_t off, uint32_t len, const S
     uint64_t seq = 0;
     for (int i = 0; i < 6; i++) seq = (seq << 8) | rec[5 + i];
     r.seq = seq;
-    size_t ptl = 0;
-    r.ok = open_record(*keys_->r, keys_->riv, rec, rl, &r.pt, &ptl);
-    r.ptl = uint32_t(ptl);
-    if (r.ok && scan_) scan_(r.pt, ptl, b.opened.pre);
     r.owner = buf;
     b.opened.bytes += rl;
     b.opened.recs.push_back(std::move(r));
     records.fetch_add(1, std::memory_order_relaxed);
+  }
+}
+
+// Authenticates and decrypts a burst's records in place (a lane or the reader).
+void RxReader::open_burst(Burst& b) const {
+  for (auto& r : b.opened.recs) {
+    size_t ptl = 0;
+    r.ok = open_record(*keys_->r, keys_->riv, r.rec, r.len, &r.pt, &ptl);
+    r.ptl = uint32_t(ptl);
+  }
+}
+
+void RxReader::complete(uint64_t seq, std::unique_ptr<Burst> b) {
+  std::lock_guard<std::mutex> lk(ord_mu_);
+  ready_.emplace_back(seq, std::move(b));
+  for (bool more = true; more;) {
+    more = false;
+    for (size_t i = 0; i < ready_.size(); i++) {
+      if (ready_[i].first != seq_deliver_) continue;
+      std::unique_ptr<Burst> next = std::move(ready_[i].second);
+      ready_.erase(ready_.begin() + long(i));
+      if (scan_)
+        for (auto& r : next->opened.recs)
+          if (r.ok) scan_(r.pt, r.ptl, next->opened.pre);
+      seq_deliver_++;
+      deliver_(std::move(next));
+      more = true;
+      break;
+    }
   }
 }
 
@@ -468,7 +495,7 @@ void RxReader::run() {
           hb->reader = id_;
           hb->handback = true;
           outstanding_.fetch_add(1, std::memory_order_acq_rel);
-          deliver_(std::move(hb));
+          complete(seq_next_++, std::move(hb));  // after every burst still on a lane
           continue;
         }
         win_start = now;
@@ -561,7 +588,20 @@ void RxReader::run() {
     for (auto& r : burst->raw) win_bytes += r.len;
     bursts.fetch_add(1, std::memory_order_relaxed);
     outstanding_.fetch_add(1, std::memory_order_acq_rel);
-    deliver_(std::move(burst));
+    const uint64_t seq = seq_next_++;
+    if (burst->opened.bytes >= kLaneBytes && open_[0]) {
+      lane_bursts.fetch_add(1, std::memory_order_relaxed);
+      Burst* raw = burst.release();
+      open_[next_lane_]->submit([this, seq, raw] {
+        std::unique_ptr<Burst> b(raw);
+        open_burst(*b);
+        complete(seq, std::move(b));
+      });
+      next_lane_ = (next_lane_ + 1) % kOpenLanes;
+    } else {
+      open_burst(*burst);
+      complete(seq, std::move(burst));
+    }
   }
 }
 
