@@ -85,20 +85,6 @@ using RawBufPtr = std::shared_ptr<RawBuf>;
 // relaxed load, so this orders the reuse after their last reads.
 inline void reuse_fence() { std::atomic_thread_fence(std::memory_order_acquire); }
 
-// A received chunk whose payload another thread (a receive lane) already
-// copied into a reassembly buffer: `body` identifies the chunk inside its
-// decrypted packet; the payload sits at buf[off, off + payload length).
-// Only a message's first fragment (off 0) holds a reference (`keep`): one
-// per fragment cost a locked count update on the lane and another on the
-// association thread for every ~1.1 KiB at 1200 MTU. (rtc/sctp.h
-// SctpPreassembler.)
-struct PreCopied {
-  const uint8_t* body;
-  uint32_t off;
-  const RawBuf* buf;  // null: not copied
-  RawBufPtr keep;     // first fragment only
-};
-
 // Recycling pool of fixed-size receive buffers whose contents are handed up
 // the stack as zero-copy views (datagram receive: DTLS decrypts in place and
 // SCTP messages are views of the datagram). A buffer goes back into service

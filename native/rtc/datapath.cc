@@ -326,9 +326,9 @@ void TxLaneState::send(SealedBatch& sb, int fd, const SockAddr& to) {
 // ------------------------------------------------------------------ RX reader
 
 RxReader::RxReader(int fd, const SockAddr& remote, std::shared_ptr<const RecordKeys> keys, Deliver deliver, uint64_t id,
-                   size_t slot, bool adaptive, RxScan scan)
+                   size_t slot, bool adaptive)
     : fd_(fd), stop_fd_(eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC)), remote_(remote), keys_(std::move(keys)),
-      deliver_(std::move(deliver)), scan_(std::move(scan)), id_(id), slot_(slot), pool_(slot), adaptive_(adaptive), active_(!adaptive) {
+      deliver_(std::move(deliver)), id_(id), slot_(slot), pool_(slot), adaptive_(adaptive), active_(!adaptive) {
   for (auto& l : open_) l = std::make_unique<Lane>("p2pt-udp-open");
   th_ = std::thread([this] {
     sigset_t mask;
@@ -450,9 +450,6 @@ void RxReader::complete(uint64_t seq, std::unique_ptr<Burst> b) {
       if (ready_[i].first != seq_deliver_) continue;
       std::unique_ptr<Burst> next = std::move(ready_[i].second);
       ready_.erase(ready_.begin() + long(i));
-      if (scan_)
-        for (auto& r : next->opened.recs)
-          if (r.ok) scan_(r.pt, r.ptl, next->opened.pre);
       seq_deliver_++;
       deliver_(std::move(next));
       more = true;

@@ -141,11 +141,6 @@ class TxBatchPool {
 };
 
 // Application records of one receive burst, decrypted in place by the lane.
-// Runs where an application record is opened off the association thread (the
-// RX lane, a socket reader), on its plaintext: may copy SCTP fragments ahead
-// into reassembly buffers (rtc/sctp.h SctpPreassembler), listed in `out`.
-using RxScan = std::function<void(const uint8_t* pt, size_t n, std::vector<PreCopied>& out)>;
-
 struct RxBatch {
   struct Rec {
     uint8_t* rec;
@@ -159,7 +154,6 @@ struct RxBatch {
   };
   std::vector<Rec> recs;
   size_t bytes = 0;
-  std::vector<PreCopied> pre;  // fragments the lane copied ahead (DtlsTransport::set_rx_scan)
 };
 
 // Record crypto shared by the association thread and the lanes (the keys are
@@ -267,9 +261,8 @@ class RxReader {
   // datagram in a 64 KiB slot pinned ~50x its size per burst); a datagram
   // larger than the slot (a peer with larger packets) grows it to 64 KiB.
   // `adaptive`: start paused, run only between engage() and a handback.
-  // `scan`: run on each opened application record (this reader's own state).
   RxReader(int fd, const SockAddr& remote, std::shared_ptr<const RecordKeys> keys, Deliver deliver, uint64_t id = 0,
-           size_t slot = 65536, bool adaptive = false, RxScan scan = nullptr);
+           size_t slot = 65536, bool adaptive = false);
   uint64_t id() const { return id_; }
   size_t slot() const { return slot_.load(std::memory_order_relaxed); }
   ~RxReader();  // stops and joins; bursts already delivered stay valid
@@ -303,16 +296,13 @@ class RxReader {
   void run();
   void segment(const RawBufPtr& buf, uint32_t off, uint32_t len, const SockAddr& from, Burst& b);
   void open_burst(Burst& b) const;
-  // Bursts go up in read order whichever thread opened them: `seq` is the
-  // read order; the fragment scan runs here, in that order (its state follows
-  // messages across bursts).
+  // Bursts go up in read order whichever thread opened them (`seq`).
   void complete(uint64_t seq, std::unique_ptr<Burst> b);
   LaneFd fd_;
   int stop_fd_ = -1;
   SockAddr remote_;
   std::shared_ptr<const RecordKeys> keys_;
   Deliver deliver_;
-  RxScan scan_;
   uint64_t id_ = 0;
   bool escape_ = rx_escape_enabled();
   std::atomic<size_t> slot_{65536};

@@ -706,9 +706,7 @@ void DtlsTransport::flush_batch() {
   if (batch_.empty()) return;
   std::vector<Bytes> b;
   b.swap(batch_);
-  const PreCopied* pre = batch_pre_ && !batch_pre_->empty() ? batch_pre_->data() : nullptr;
-  if (on_data_batch && !closed_) on_data_batch(b.data(), b.size(), pre, pre ? batch_pre_->size() : 0);
-  batch_pre_ = nullptr;  // one delivery per burst
+  if (on_data_batch && !closed_) on_data_batch(b.data(), b.size());
   b.clear();
   if (batch_.empty()) batch_.swap(b);  // keep the capacity
 }
@@ -810,12 +808,11 @@ void DtlsTransport::commit_rx() {
   lane_rx_batches_++;
   std::weak_ptr<DtlsTransport> w = self;
   Reactor* r = &r_;
-  rx_lane_->submit([b, k = keys_, w, r, scan = rx_scan_] {
+  rx_lane_->submit([b, k = keys_, w, r] {
     for (auto& x : b->recs) {
       size_t ptl = 0;
       x.ok = open_record(*k->r, k->riv, x.rec, x.len, &x.pt, &ptl);
       x.ptl = uint32_t(ptl);
-      if (x.ok && scan && x.type == kAppData) (*scan)(x.pt, ptl, b->pre);
     }
     r->post_threadsafe([b, w] {
       if (auto s = w.lock()) s->rx_done(*b);
@@ -836,7 +833,6 @@ void DtlsTransport::deliver_opened(RxBatch& b) {
   if (closed_) return;
   auto self = shared_from_this();
   batching_ = true;
-  batch_pre_ = &b.pre;
   for (auto& x : b.recs) {
     if (!x.ok || replay_seen(x.seq)) {
       LOG_TRACE(kT, "dropping DTLS record that fails authentication or replay check");
@@ -848,7 +844,6 @@ void DtlsTransport::deliver_opened(RxBatch& b) {
   }
   batching_ = false;
   flush_batch();
-  batch_pre_ = nullptr;
 }
 
 bool DtlsTransport::send(const uint8_t* p, size_t n) {

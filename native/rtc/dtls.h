@@ -126,12 +126,8 @@ class DtlsTransport : public std::enable_shared_from_this<DtlsTransport> {
   std::function<void()> on_connected;
   std::function<void(Bytes)> on_data;
   // Records of one receive burst together (set: used for bursts; on_data for
-  // single datagrams). The views may be moved from. `pre`: what the RX lane's
-  // scan (set_rx_scan) copied ahead for this burst, in record order.
-  std::function<void(Bytes*, size_t, const PreCopied* pre, size_t npre)> on_data_batch;
-  // Runs on the RX lane after each application record it opens (before the
-  // association thread sees the burst); may copy fragments ahead into `out`.
-  void set_rx_scan(RxScan scan) { rx_scan_ = scan ? std::make_shared<RxScan>(std::move(scan)) : nullptr; }
+  // single datagrams). The views may be moved from.
+  std::function<void(Bytes*, size_t)> on_data_batch;
   std::function<void(const std::string&)> on_closed;
 
  private:
@@ -152,8 +148,6 @@ class DtlsTransport : public std::enable_shared_from_this<DtlsTransport> {
   void flush_batch();
   bool batching_ = false;
   std::vector<Bytes> batch_;
-  const std::vector<PreCopied>* batch_pre_ = nullptr;  // deliver_opened's burst
-  std::shared_ptr<RxScan> rx_scan_;
   void seal_inline(const TxBatch& b);
   void rx_done(RxBatch& b);
   void feed_openssl(const uint8_t* p, size_t n);

@@ -241,15 +241,6 @@ void PeerConnection::flush() {
   if (ice_) ice_->flush();
 }
 
-// A fragment scanner for one thread that opens records (the RX lane, a socket
-// reader): each has its own, so no scanner state is shared between threads.
-// None with chained delivery, which copies nothing to begin with.
-RxScan PeerConnection::rx_scan() const {
-  if (cfg_.message_chains) return nullptr;
-  auto pre = std::make_shared<SctpPreassembler>();
-  return [pre](const uint8_t* pt, size_t n, std::vector<PreCopied>& out) { pre->scan(pt, n, out); };
-}
-
 void PeerConnection::start_rx_reader() {
   if (rx_reader_ || closed_ || !dtls_ || !ice_ || !dtls_->lanes_enabled()) return;
   const int mode = rx_reader_mode();
@@ -272,7 +263,7 @@ void PeerConnection::start_rx_reader() {
     r->post_threadsafe([w, sb] {
       if (auto s = w.lock()) s->on_rx_burst(*sb);
     });
-  }, ++rx_reader_ids_, rx_slot_bytes(), adaptive, rx_scan());
+  }, ++rx_reader_ids_, rx_slot_bytes(), adaptive);
   LOG_DEBUG(kT, "UDP socket reader %s for %s", adaptive ? "ready (engaged under bulk)" : "on", remote.str().c_str());
 }
 
@@ -514,10 +505,10 @@ void PeerConnection::start_dtls() {
   };
   // A receive burst's packets under one reference to this connection (a
   // lock per packet was 10-14 % of the association thread at 1200 MTU).
-  dtls_->on_data_batch = [w](Bytes* pkts, size_t n, const PreCopied* pre, size_t npre) {
+  dtls_->on_data_batch = [w](Bytes* pkts, size_t n) {
     auto s = w.lock();
     if (!s) return;
-    if (s->sctp_ && !s->closed_) s->sctp_->on_packets(pkts, n, pre, npre);
+    if (s->sctp_ && !s->closed_) s->sctp_->on_packets(pkts, n);
   };
   dtls_->on_closed = [w](const std::string& why) {
     if (auto s = w.lock()) {
@@ -548,9 +539,6 @@ void PeerConnection::start_sctp() {
     t.gen = s->ice_->path_generation();
     return true;
   });
-  // Fragments copied into reassembly buffers on the RX lane, not here
-  // (SctpPreassembler; chained delivery copies nothing to begin with).
-  dtls_->set_rx_scan(rx_scan());
   start_rx_reader();
   // Packets straight to the DTLS transport, held strongly (it never refers
   // back to the association): no lock of this connection per packet.

@@ -147,7 +147,6 @@ class PeerConnection : public std::enable_shared_from_this<PeerConnection> {
   void fail(const std::string& why);
   void flush();
   void start_rx_reader();
-  RxScan rx_scan() const;
   void on_rx_burst(RxReader::Burst& b);
 
   Reactor& r_;

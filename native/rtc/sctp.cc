@@ -392,65 +392,9 @@ void SctpAssociation::on_packet(const Bytes& pkt) {
 // A receive burst under one reference (one shared_from_this per burst, not
 // per packet: after a fragment's copy the reference count's locked update
 // waited for the copy's stores, ~15 % of the association thread at 1200 MTU).
-void SctpAssociation::on_packets(const Bytes* pkts, size_t n, const PreCopied* pre, size_t npre) {
+void SctpAssociation::on_packets(const Bytes* pkts, size_t n) {
   auto self = shared_from_this();
-  pre_ = pre;
-  pre_n_ = npre;
-  pre_i_ = 0;
   for (size_t i = 0; i < n && !closed_fired_; i++) packet_in(pkts[i]);
-  pre_ = nullptr;
-  pre_n_ = pre_i_ = 0;
-}
-
-// The lane's copy of the chunk at `body`, if it made one. Entries are in the
-// order the lane scanned the chunks, which is the order they arrive here;
-// entries of packets dropped before their chunks were handled are skipped.
-const PreCopied* SctpAssociation::take_pre(const uint8_t* body) {
-  for (size_t j = pre_i_; j < pre_n_; j++)
-    if (pre_[j].body == body) {
-      pre_i_ = j + 1;
-      return &pre_[j];
-    }
-  return nullptr;
-}
-
-void SctpPreassembler::scan(const uint8_t* p, size_t n, std::vector<PreCopied>& out) {
-  size_t off = kCommonHdr;
-  while (off + 4 <= n) {
-    const uint8_t type = p[off], flags = p[off + 1];
-    const size_t clen = rd16(p + off + 2);
-    if (clen < 4 || off + clen > n) return;
-    if (type == kData && clen >= 16 && (flags & 3) != 3) {  // a fragment (B/E not both)
-      const uint8_t* body = p + off + 4;
-      const uint32_t tsn = rd32(body);
-      const uint32_t key = uint32_t(rd16(body + 4)) | (flags & 4 ? 0x10000u : 0u);
-      const size_t dlen = clen - 16;
-      Run* r = nullptr;
-      for (auto& x : runs_)
-        if (x.key == key) r = &x;
-      if (!r) {
-        r = &runs_.emplace_back();
-        r->key = key;
-      }
-      if (flags & 2) {  // B: a new message on this stream
-        r->buf = pool_.get();
-        r->off = 0;
-      } else if (r->buf && tsn != r->next_tsn) {  // out of sequence: the association copies the rest
-        r->buf.reset();
-      }
-      if (r->buf && r->off + dlen > r->buf->cap) r->buf.reset();  // larger than a tunnel frame
-      if (r->buf) {
-        memcpy(r->buf->data.get() + r->off, body + 12, dlen);
-        out.push_back(PreCopied{body, uint32_t(r->off), r->buf.get(), r->off ? nullptr : r->buf});
-        r->off += dlen;
-        r->next_tsn = tsn + 1;
-        if (flags & 1) r->buf.reset();  // E: complete
-      } else {
-        out.push_back(PreCopied{body, 0, nullptr, nullptr});  // one entry per fragment keeps take_pre's lookup O(1)
-      }
-    }
-    off += (clen + 3) & ~size_t(3);
-  }
 }
 
 void SctpAssociation::packet_in(const Bytes& pkt) {
@@ -674,10 +618,8 @@ void SctpAssociation::abort(const std::string& reason) {
 // (on_message_chain) the fragments' views are handed up as they are: no copy
 // (the association thread spent 19-25 % of its time copying fragments of
 // bulk frames at 1200-byte MTU, profiles/r03/bulk_threads). `d` is an owning
-// view then; without a chain consumer fragments are copied as they come,
-// unless the receive lane copied them already (`pc`, SctpPreassembler).
-void SctpAssociation::deliver_chunk(uint8_t fl, uint16_t st, uint16_t ssn, uint32_t pp, const Bytes& d,
-                                    const PreCopied* pc) {
+// view then; without a chain consumer fragments are copied as they come.
+void SctpAssociation::deliver_chunk(uint8_t fl, uint16_t st, uint16_t ssn, uint32_t pp, const Bytes& d) {
   bool B = fl & 2, E = fl & 1, U = fl & 4;
   const uint8_t* dp = d.data();
   size_t dn = d.size();
@@ -693,41 +635,17 @@ void SctpAssociation::deliver_chunk(uint8_t fl, uint16_t st, uint16_t ssn, uint3
     pa.frags.clear();
     pa.frag_bytes = 0;
     pa.buf.reset();
-    pa.lane = false;
     // Reassembled into a pooled buffer sized for a whole tunnel frame (one
     // copy per fragment, no reallocation, recycled once the message's views
-    // are gone — possibly on a worker thread) — or into the receive lane's,
-    // which copied this fragment already (SctpPreassembler).
-    if (!chain) {
-      if (pc && pc->keep && pc->off == 0) {
-        pa.buf = pc->keep;
-        pa.lane = true;
-      } else {
-        pa.buf = reasm_pool_.get();
-      }
-    }
+    // are gone — possibly on a worker thread).
+    if (!chain) pa.buf = reasm_pool_.get();
     pa.ppid = pp;
     pa.active = true;
   }
   if (!pa.active) return;  // middle fragment without a beginning (after FORWARD-TSN)
-  // A lane entry without a reference is safe to take only for the buffer
-  // held here (pa.buf keeps it from going back to the lane's pool, so an
-  // entry naming it was made for this message).
-  if (pa.lane && !(pc && pc->buf == pa.buf.get() && pc->off == pa.len)) {
-    // The lane lost the sequence (a loss, a retransmission, a burst opened
-    // inline): continue in a buffer of our own — the lane may still write
-    // past this point into its own.
-    RawBufPtr own = reasm_pool_.get();
-    memcpy(own->data.get(), pa.buf->data.get(), pa.len);
-    pa.buf = std::move(own);
-    pa.lane = false;
-  }
   if (chain) {
     pa.frags.push_back(d);
     pa.frag_bytes += dn;
-  } else if (pa.lane) {  // the lane's copy is in place already
-    pa.len += dn;
-    stats_.precopied_fragments++;
   } else if (pa.big.empty() && pa.len + dn <= pa.buf->cap) {
     memcpy(pa.buf->data.get() + pa.len, dp, dn);
     pa.len += dn;
@@ -866,10 +784,6 @@ void SctpAssociation::handle_data(uint8_t flags, const uint8_t* c, size_t len, c
     rx_high_tsn_ = tsn;
     have_rx_high_ = true;
   }
-  // The lane's entry for this fragment (taken even if unused: entries are
-  // consumed in chunk order).
-  const PreCopied* pc = pre_n_ && (flags & 3) != 3 ? take_pre(c) : nullptr;
-  if (pc && !pc->buf) pc = nullptr;
   if (d <= 0) {
     stats_.dup_tsns++;
     if (dups_.size() < 32) dups_.push_back(tsn);
@@ -890,8 +804,7 @@ void SctpAssociation::handle_data(uint8_t flags, const uint8_t* c, size_t len, c
     // Fragments are copied on arrival unless the consumer takes chains, so a
     // non-owning view is enough then.
     deliver_chunk(flags, stream, ssn, ppid,
-                  whole || on_message_chain ? hold(data, dlen) : Bytes::adopt(nullptr, data, dlen),
-                  pc);
+                  whole || on_message_chain ? hold(data, dlen) : Bytes::adopt(nullptr, data, dlen));
     drain_in_order();
     return;
   }

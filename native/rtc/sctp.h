@@ -66,36 +66,6 @@ struct CcPolicy {
 };
 const CcPolicy& cc_policy();
 
-// Reassembly buffers: a whole tunnel frame (64 KiB body + header) fits.
-constexpr size_t kReasmBufBytes = 65536 + 1024;
-
-// The receive lane's half of reassembly (crypto lanes on, no message
-// chains). The lane that opens a burst's records scans each SCTP packet and,
-// for every fragment that continues — in TSN sequence — a message it saw
-// begin, copies the payload into a pooled buffer and reports it
-// (PreCopied); the association thread then takes those fragments without a
-// copy (deliver_chunk) instead of copying ~2 M fragments/s itself at 1200
-// MTU (profiles/r05 mixed and bulk profiles). What the lane did not see in
-// sequence — a loss, a retransmission, a burst opened inline — the
-// association thread copies as before, into a buffer of its own: a lane
-// buffer is only ever written by the lane. Checksum and verification tag are
-// the association's to check; a copy it never takes is dropped. One instance
-// per association, used only on the lane's thread.
-class SctpPreassembler {
- public:
-  void scan(const uint8_t* pkt, size_t n, std::vector<PreCopied>& out);
-
- private:
-  struct Run {
-    uint32_t key;  // stream | unordered << 16
-    uint32_t next_tsn = 0;
-    size_t off = 0;
-    RawBufPtr buf;  // null: not following a message on this stream
-  };
-  std::vector<Run> runs_;
-  BufPool pool_{kReasmBufBytes, 256};
-};
-
 struct SctpStats {
   uint64_t packets_sent = 0, packets_received = 0;
   uint64_t data_chunks_sent = 0, data_chunks_received = 0;
@@ -103,7 +73,6 @@ struct SctpStats {
   uint64_t retransmits = 0, fast_retransmits = 0, t3_expirations = 0;
   uint64_t tlp_probes = 0, rack_marks = 0, random_loss_events = 0;
   uint64_t random_loss_cuts = 0;  // random-loss episodes that cut cwnd
-  uint64_t precopied_fragments = 0;  // fragments a receive lane copied ahead (SctpPreassembler)
   uint64_t congestion_cuts = 0;   // loss episodes read as congestion (0.7 cut)
   uint64_t queue_cuts = 0;        // short-path queue bound: cwnd cuts for a standing queue
   uint64_t over_bdp_losses = 0;   // ... of them because cwnd was past the delivery-rate BDP
@@ -147,9 +116,7 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   // never pins a whole receive buffer.
   void on_packet(const Bytes& pkt);
   void on_packet(const uint8_t* p, size_t n) { on_packet(Bytes::copy(p, n)); }
-  // A receive burst; `pre`: fragments a receive lane already copied into
-  // reassembly buffers (SctpPreassembler), taken without a copy here.
-  void on_packets(const Bytes* pkts, size_t n, const PreCopied* pre = nullptr, size_t npre = 0);
+  void on_packets(const Bytes* pkts, size_t n);  // a receive burst
   // Queue a message made of gathered pieces (a single piece is never copied).
   bool send(uint16_t stream, uint32_t ppid, const std::vector<Bytes>& pieces, bool unordered = false);
   // Queue a message = a short header (copied, <= kMsgHdrMax bytes) followed by
@@ -234,8 +201,7 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   void queue_control(uint8_t type, uint8_t flags, std::vector<uint8_t> body);
   void build_sack(std::vector<uint8_t>& body);
   void deliver_ready();
-  void deliver_chunk(uint8_t fl, uint16_t st, uint16_t ssn, uint32_t pp, const Bytes& d,
-                     const PreCopied* pc = nullptr);
+  void deliver_chunk(uint8_t fl, uint16_t st, uint16_t ssn, uint32_t pp, const Bytes& d);
   void deliver_message(uint16_t st, uint16_t ssn, bool unordered, uint32_t pp, Bytes msg,
                        std::vector<Bytes> more = {});
   void hand_up(uint16_t st, uint32_t pp, Bytes msg, std::vector<Bytes>& more);
@@ -386,7 +352,6 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
     uint32_t ppid = 0;
     RawBufPtr buf;  // pooled (reasm_pool_): a whole tunnel frame fits
     size_t len = 0;
-    bool lane = false;  // buf is a receive lane's (SctpPreassembler): never written here
     std::vector<uint8_t> big;  // only for messages beyond the pooled size
     std::vector<Bytes> frags;  // chained delivery: the fragments' views (no copy)
     size_t frag_bytes = 0;
@@ -398,11 +363,8 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
     Bytes msg;
     std::vector<Bytes> more;
   };
-  BufPool reasm_pool_{kReasmBufBytes, 256};
-  // This burst's lane copies (on_packets), consumed in chunk order.
-  const PreCopied* pre_ = nullptr;
-  size_t pre_n_ = 0, pre_i_ = 0;
-  const PreCopied* take_pre(const uint8_t* body);
+  BufPool reasm_pool_{kReasmBuf, 256};
+  static constexpr size_t kReasmBuf = 65536 + 1024;
   std::map<uint16_t, Partial> partial_;  // per-stream reassembly (ordered)
   std::map<uint16_t, Partial> partial_u_;  // unordered
   std::map<uint16_t, uint16_t> next_ssn_in_;      // per inbound stream: next SSN to deliver

@@ -30,8 +30,6 @@ struct LossyLink {
   uint64_t dropped = 0;
   LossyLink(Reactor& rr, double l, double d, uint64_t delay) : r(rr), loss(l), dup(d), max_delay_us(delay) {}
   std::function<bool(const std::weak_ptr<SctpAssociation>&)> blackout;  // true: drop this packet
-  // Set: hands each carried packet over instead of on_packet().
-  std::function<void(const std::shared_ptr<SctpAssociation>&, const std::vector<uint8_t>&)> deliver;
   // Optional bottleneck on the path towards `bottleneck_to` (bits/s, drop-tail
   // queue of queue_bytes): serialisation + queueing delay, overflow drops.
   double rate_bps = 0;
@@ -65,11 +63,8 @@ struct LossyLink {
     for (int i = 0; i < copies; i++) {
       auto pkt = std::make_shared<std::vector<uint8_t>>(p, p + n);
       uint64_t d = fixed_delay_us + (max_delay_us ? std::uniform_int_distribution<uint64_t>(0, max_delay_us)(rng) : 0);
-      r.call_later_us(d, [this, to, pkt] {
-        if (auto s = to.lock()) {
-          if (deliver) deliver(s, *pkt);
-          else s->on_packet(pkt->data(), pkt->size());
-        }
+      r.call_later_us(d, [to, pkt] {
+        if (auto s = to.lock()) s->on_packet(pkt->data(), pkt->size());
       });
     }
   }
@@ -141,52 +136,6 @@ TEST(sctp_simultaneous_open_and_messages) {
   for (size_t i = 0; i < p.got_b.size() && i < sent.size(); i++) CHECK(p.got_b[i].second == sent[i]);
   CHECK(!p.got_a.empty() && p.got_a[0].second == "xyz");
   CHECK_EQ(p.a->stats().retransmits, uint64_t(0));
-}
-
-// Fragments copied ahead by a receive lane (SctpPreassembler) over a path
-// that loses, duplicates and reorders packets, with every 7th packet opened
-// "inline" (not scanned): the association takes the lane's copies while
-// they continue its own reassembly in sequence and copies everything else
-// itself; every message arrives intact and in order.
-TEST(sctp_lane_precopied_fragments_survive_loss_and_reordering) {
-  SctpPair p(0.03, 0.02, 3000);
-  auto pre = std::make_shared<SctpPreassembler>();
-  uint64_t carried_b = 0;
-  p.link.deliver = [&](const std::shared_ptr<SctpAssociation>& to, const std::vector<uint8_t>& f) {
-    if (to != p.b) {
-      to->on_packet(f.data(), f.size());
-      return;
-    }
-    Bytes pkt = Bytes::copy(f.data(), f.size());
-    std::vector<PreCopied> out;
-    if (++carried_b % 7) pre->scan(pkt.data(), pkt.size(), out);
-    to->on_packets(&pkt, 1, out.data(), out.size());
-  };
-  p.a->connect();
-  CHECK(p.r.run_until([&] { return p.a->established() && p.b->established(); }, 3000));
-  std::vector<std::string> sent[2];
-  for (int i = 0; i < 120; i++) {
-    const int st = i % 3 == 0 ? 1 : 0;  // stream 2 unordered
-    sent[st].push_back(payload(size_t(1 + (i * 15485863u) % 65000), uint32_t(i)));
-    p.a->send(uint16_t(1 + st), 53, {Bytes::copy(sent[st].back())}, st == 1);
-  }
-  CHECK(p.r.run_until([&] { return p.got_b.size() == 120; }, 30000));
-  size_t k[2] = {0, 0}, bad = 0;
-  std::vector<std::string> unordered;
-  for (auto& [st, m] : p.got_b) {
-    if (st == 1) bad += k[0] >= sent[0].size() || m != sent[0][k[0]++];
-    else unordered.push_back(m);
-  }
-  std::sort(unordered.begin(), unordered.end());
-  std::sort(sent[1].begin(), sent[1].end());
-  CHECK_EQ(bad, size_t(0));
-  CHECK(unordered == sent[1]);
-  const auto& s = p.b->stats();
-  printf("  %llu of %llu chunks taken from the lane's copies, %llu retransmissions, %llu dups\n",
-         (unsigned long long)s.precopied_fragments, (unsigned long long)s.data_chunks_received,
-         (unsigned long long)p.a->stats().retransmits, (unsigned long long)s.dup_tsns);
-  CHECK(s.precopied_fragments > 0);
-  CHECK(s.precopied_fragments < s.data_chunks_received);  // and some copied here
 }
 
 TEST(sctp_zero_checksum_negotiation) {
@@ -900,9 +849,9 @@ TEST(peerconnection_bulk_through_crypto_lanes) {
       CHECK(d->lane_tx_batches() > 0);
       if (reader) CHECK(ans->rx_reader() && ans->rx_reader()->records.load() > 0);
       else CHECK(!ans->rx_reader() && ans->dtls()->lane_rx_batches() > 0);
-      // Fragments copied ahead where the records were opened (the reader or
-      // the RX lane): the association thread took them without a copy.
-      CHECK(ans->sctp_stats()->precopied_fragments > 0 && off->sctp_stats()->precopied_fragments > 0);
+      // Bulk bursts were opened on the reader's open lanes (in read order:
+      // order_ok above).
+      if (reader) CHECK(ans->rx_reader()->lane_bursts.load() > 0);
       if (rmode == kRxReaderAdaptive && ans->rx_reader()) {
         CHECK(ans->rx_reader()->engages.load() >= 1);
         // Idle for more than the reader's window: both readers hand back, and
@@ -925,13 +874,12 @@ TEST(peerconnection_bulk_through_crypto_lanes) {
       }
     }
     printf("  %s: %zu + %zu MB, lane tx batches %llu, inline %llu, rx batches %llu, reader records %llu, "
-           "fragments copied ahead %llu of %llu\n",
+           "reader bursts on open lanes %llu\n",
            off->describe_path().c_str(), bytes_ans >> 20, bytes_off >> 20,
            (unsigned long long)(d ? d->lane_tx_batches() : 0), (unsigned long long)(d ? d->inline_tx_batches() : 0),
            (unsigned long long)(ans->dtls() ? ans->dtls()->lane_rx_batches() : 0),
            (unsigned long long)(ans->rx_reader() ? ans->rx_reader()->records.load() : 0),
-           (unsigned long long)ans->sctp_stats()->precopied_fragments,
-           (unsigned long long)ans->sctp_stats()->data_chunks_received);
+           (unsigned long long)(ans->rx_reader() ? ans->rx_reader()->lane_bursts.load() : 0));
     off->close();
     ans->close();
   }
