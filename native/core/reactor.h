@@ -13,6 +13,7 @@
 
 #include <cstdint>
 #include <deque>
+#include <atomic>
 #include <functional>
 #include <map>
 #include <memory>
@@ -136,6 +137,13 @@ class Reactor {
   std::deque<Fn> posted_;
   std::mutex ts_mu_;
   std::vector<Fn> ts_posted_;
+  // post_threadsafe() skips the eventfd write while this loop is awake: it
+  // looks at ts_pending_ itself before it sleeps and after every wait. Both
+  // flags are sequentially consistent (poster: set pending, read sleeping;
+  // loop: set sleeping, read pending), so one of the two sides always sees
+  // the other and no post is left waiting behind a sleep.
+  std::atomic<bool> sleeping_{false}, ts_pending_{false};
+  void run_threadsafe_posts();
   std::vector<std::pair<uint64_t, Fn>> flush_hooks_;
   uint64_t next_hook_ = 1;
   std::unordered_map<int, Fn> signals_;
