@@ -514,7 +514,10 @@ void RxReader::run() {
         // Short waits: without UDP GRO every datagram is its own skb (about
         // twice its size in buffer accounting), and a 1 ms pause let a 512 KiB
         // buffer go from under half to overflowing (TUNNEL_UDP_OFFLOAD=none).
-        cv_.wait_for(lk, std::chrono::microseconds(100), [this] {
+        // wait_until on the system clock: libstdc++ 11's steady-clock wait_for
+        // goes through pthread_cond_clockwait, which GCC 11's ThreadSanitizer
+        // does not intercept (it then reports the mutex as locked twice).
+        cv_.wait_until(lk, std::chrono::system_clock::now() + std::chrono::microseconds(100), [this] {
           return stop_.load(std::memory_order_acquire) || outstanding_.load(std::memory_order_acquire) < kMaxOutstanding;
         });
         continue;
