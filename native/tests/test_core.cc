@@ -1,6 +1,8 @@
 // Core: JSON, checksums, encodings, reactor timers, frame codec, HTTP parser.
 #include <algorithm>
+#include <atomic>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include <openssl/evp.h>
@@ -172,6 +174,36 @@ TEST(reactor_flush_soon_runs_hooks_before_the_rest_of_the_turn) {
   q.run_until([&] { return seen2.size() >= 3; }, 500);
   const std::vector<std::string> want2 = {"a", "b", "flush"};
   CHECK(seen2 == want2);
+}
+
+// Cross-thread posts to a loop that alternates between sleeping and running:
+// the eventfd write is skipped while the loop is awake, and no post may be
+// left behind a sleep (each is run within a bounded time).
+TEST(reactor_threadsafe_posts_never_wait_behind_a_sleep) {
+  Reactor r;
+  std::atomic<int> ran{0};
+  std::atomic<uint64_t> worst_us{0};
+  constexpr int kPosts = 3000;
+  std::thread t([&] {
+    for (int i = 0; i < kPosts; i++) {
+      const uint64_t t0 = Reactor::now_us();
+      r.post_threadsafe([&, t0] {
+        const uint64_t d = Reactor::now_us() - t0;
+        uint64_t w = worst_us.load();
+        while (d > w && !worst_us.compare_exchange_weak(w, d)) {
+        }
+        ran++;
+      });
+      if (i % 7 == 0) std::this_thread::sleep_for(std::chrono::microseconds(50 + (i % 5) * 40));
+    }
+  });
+  // A far timer keeps every wait long: only a post can end it early.
+  r.call_later_ms(60000, [] {});
+  r.run_until([&] { return ran.load() == kPosts; }, 10000);
+  t.join();
+  printf("  %d posts run, slowest %llu us from post to run\n", ran.load(), (unsigned long long)worst_us.load());
+  CHECK_EQ(ran.load(), kPosts);
+  if (kTimingChecks) CHECK(worst_us.load() < 200000);  // a lost wake-up would wait for the 60 s timer
 }
 
 TEST(frame_codec) {

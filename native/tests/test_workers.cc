@@ -1,6 +1,7 @@
 // Worker-thread plumbing (tunnel/workers.h) and the scheduler's lanes
 // (tunnel/scheduler.h).
 #include <atomic>
+#include <mutex>
 #include <thread>
 
 #include "tests/testing.h"
@@ -60,6 +61,64 @@ TEST(pipe_same_thread_is_synchronous) {
 
 // Streams stay on the association thread up to the inline limit, then go to
 // the least-loaded worker; releases make room again.
+// stage(): small payloads are copied into an arena owned by the batch being
+// filled (a later batch gets another), larger ones and same-thread pipes pass
+// through untouched; urgent pushes are handed over before the loop turn ends.
+TEST(pipe_stage_copies_small_payloads_per_batch_and_urgent_hands_over) {
+  WorkerPool pool(1);
+  Reactor main;
+  struct Msg {
+    Bytes b;
+    int i = 0;
+  };
+  std::mutex mu;
+  std::vector<std::pair<int, std::string>> got;
+  std::atomic<int> n{0};
+  Pipe<Msg> pipe(main, pool.reactor(0), [&](Msg& m) {
+    std::lock_guard<std::mutex> lk(mu);
+    got.emplace_back(m.i, m.b.str());
+    n++;
+  });
+  std::vector<std::string> sent;
+  const void* owner1 = nullptr;
+  const void* owner2 = nullptr;
+  Bytes keep1;  // holds the first batch's arena, so the pool cannot hand it out again
+  Bytes big = Bytes::copy(std::string(Pipe<Msg>::kStageMax + 1, 'x'));
+  main.post([&] {
+    for (int i = 0; i < 10; i++) {
+      sent.push_back("token " + std::to_string(i));
+      Bytes src = Bytes::copy(sent.back());
+      Bytes st = pipe.stage(src);
+      CHECK(st.data() != src.data() && st.str() == sent.back());
+      if (i == 0) {
+        owner1 = st.owner().get();
+        keep1 = st;
+      }
+      CHECK(st.owner().get() == owner1);  // one arena for the batch
+      pipe.push(Msg{st, i});
+    }
+    Bytes kept = pipe.stage(big);
+    CHECK(kept.data() == big.data());  // too large: not copied
+  });
+  main.run_until([&] { return n.load() == 10; }, 2000);
+  main.post([&] {
+    Bytes st = pipe.stage(Bytes::copy(std::string("next batch")));
+    owner2 = st.owner().get();
+    pipe.push(Msg{st, 10}, true);
+    // Handed over now: the worker may deliver it before this turn ends.
+    sent.push_back("next batch");
+  });
+  main.run_until([&] { return n.load() == 11; }, 2000);
+  CHECK_EQ(n.load(), 11);
+  CHECK(owner2 != nullptr && owner2 != owner1);  // a new batch stages into another arena
+  std::lock_guard<std::mutex> lk(mu);
+  for (size_t i = 0; i < got.size(); i++) CHECK(got[i].first == int(i) && got[i].second == sent[i]);
+  Reactor same;
+  Pipe<Msg> inline_pipe(same, same, [](Msg&) {});
+  Bytes src = Bytes::copy(std::string("inline"));
+  CHECK(inline_pipe.stage(src).data() == src.data());  // same thread: nothing to stage
+}
+
 TEST(placement_inline_then_least_loaded) {
   Placement pl(4, 2);
   CHECK_EQ(pl.pick(), size_t(0));
