@@ -73,8 +73,14 @@ class Bytes {
 
 // Fixed-size, uninitialised, refcounted buffer (datagram receive/send pools).
 // A pool hands one out again once use_count() drops back to 1, i.e. once no
-// Bytes view into it is alive.
-struct RawBuf {
+// Bytes view into it is alive. Cache-line aligned so that make_shared puts
+// every buffer's reference counts on a line of their own: buffers handed out
+// one after another (token slabs, pipe arenas) are filled by one thread while
+// another drops the views of the previous one, and counts sharing a line made
+// each update a cross-core miss (the proxy's association thread spent 12 % of
+// its time copying a buffer reference in ProxySession::route at 1024 streams,
+// profiles/r05/b20/nodeprof).
+struct alignas(64) RawBuf {
   explicit RawBuf(size_t n) : data(new uint8_t[n]), cap(n) {}
   std::unique_ptr<uint8_t[]> data;
   size_t cap;
