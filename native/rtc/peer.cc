@@ -47,9 +47,17 @@ void DataChannel::note_interactive() {
 
 // `urgent`: the SCTP priority queue (one-chunk messages only), ahead of bulk
 // messages not yet started; the receiver keeps each stream's order (SSN).
-bool DataChannel::send_impl(const uint8_t* hdr, size_t hlen, const Bytes& payload, bool urgent) {
+SctpAssociation* DataChannel::assoc() const {
+  if (assoc_) return assoc_;
   auto pc = pc_.lock();
-  if (!pc || !is_open() || !pc->sctp_) return false;
+  if (!pc || pc->closed_ || !pc->sctp_) return nullptr;
+  assoc_ = pc->sctp_.get();
+  return assoc_;
+}
+
+bool DataChannel::send_impl(const uint8_t* hdr, size_t hlen, const Bytes& payload, bool urgent) {
+  SctpAssociation* a = is_open() ? assoc() : nullptr;
+  if (!a) return false;
   uint16_t st = uint16_t(stream_);
   if (lanes_ && hlen >= 5) {
     uint32_t sid = rd32(hdr + 1);
@@ -60,14 +68,14 @@ bool DataChannel::send_impl(const uint8_t* hdr, size_t hlen, const Bytes& payloa
   // SSE-next-to-bulk tail on the emulated WAN: a token mostly waits behind a
   // bulk message already being fragmented, which it may not interrupt; and
   // 64 x 1 MB bulk ran ~20 % slower. Removed in round 5.)
-  bool ok = pc->sctp_->send_framed(st, kPpidBinary, hdr, hlen, payload, false, urgent);
+  bool ok = a->send_framed(st, kPpidBinary, hdr, hlen, payload, false, urgent);
   if (ok && buffered_amount() > buffered_low_threshold) above_low_ = true;
   return ok;
 }
 
 size_t DataChannel::buffered_amount() const {
-  auto pc = pc_.lock();
-  return pc && pc->sctp_ ? pc->sctp_->buffered_amount() : 0;
+  SctpAssociation* a = assoc();
+  return a ? a->buffered_amount() : 0;
 }
 
 void DataChannel::close() {
@@ -83,8 +91,8 @@ void DataChannel::close() {
 }
 
 size_t DataChannel::send_window_hint() const {
-  auto pc = pc_.lock();
-  return pc && pc->sctp_ ? pc->sctp_->cwnd() : 0;
+  SctpAssociation* a = assoc();
+  return a ? a->cwnd() : 0;
 }
 
 std::string DataChannel::debug_state() const {
@@ -96,8 +104,8 @@ std::string DataChannel::debug_state() const {
 }
 
 uint64_t DataChannel::rtt_hint_us() const {
-  auto pc = pc_.lock();
-  return pc && pc->sctp_ ? pc->sctp_->min_rtt_us() : 0;
+  SctpAssociation* a = assoc();
+  return a ? a->min_rtt_us() : 0;
 }
 
 // On same-host jumbo paths (16 KiB SCTP packets) body frames are sized to one
@@ -358,7 +366,10 @@ void PeerConnection::close() {
   rx_reader_.reset();  // joins the reader; bursts already posted find closed_ set
   if (flush_hook_) r_.remove_flush_hook(flush_hook_);
   flush_hook_ = 0;
-  for (auto& kv : channels_) kv.second->set_closed("peer connection closed");
+  for (auto& kv : channels_) {
+    kv.second->assoc_ = nullptr;  // the association goes with this connection
+    kv.second->set_closed("peer connection closed");
+  }
   for (auto& dc : pending_) dc->set_closed("peer connection closed");
   if (ice_) {
     ice_->on_state = nullptr;

@@ -95,6 +95,13 @@ class DataChannel : public MessageChannel, public std::enable_shared_from_this<D
   friend class PeerConnection;
   void set_open();
   void set_closed(const std::string& why);
+  // The association, without locking pc_ (a scheduler asks for the buffered
+  // amount and window several times per frame: 6 % of the serve's association
+  // thread at 1024 streams, profiles/r05/b20/nodeprof). Cached once the
+  // connection has one, cleared by PeerConnection::close() — which runs before
+  // the association is destroyed — so it never dangles. Association thread.
+  SctpAssociation* assoc() const;
+  mutable SctpAssociation* assoc_ = nullptr;
   std::weak_ptr<PeerConnection> pc_;
   std::string label_;
   int stream_ = -1;
