@@ -469,16 +469,13 @@ void ClientCall::attach(std::shared_ptr<TcpConn> c, bool reused) {
   if (req_.body_len <= 16384) {
     for (auto& b : req_.body) head.append(reinterpret_cast<const char*>(b.data()), b.size());
     conn_->write(std::move(head));
+    conn_->flush_now();  // to the upstream now, not after the rest of this burst of requests
   } else {
     conn_->write(std::move(head));
     for (auto& b : req_.body) conn_->write(b);
   }
   if (paused_) conn_->pause_reading();
   if (cb_.on_sent) cb_.on_sent(reused);
-  // To the upstream now, not after the rest of this burst of requests. Last:
-  // a write into a stale pooled connection fails and closes it from inside
-  // (on_close retries on a fresh one or finishes the call).
-  if (conn_ && req_.body_len <= 16384) conn_->flush_now();
 }
 
 void ClientCall::on_data(const uint8_t* p, size_t n) {

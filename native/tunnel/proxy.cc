@@ -167,13 +167,11 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     } else {
       conn_->write(payload);
     }
+    if (first) conn_->flush_now();  // the first token (and the head before it) now, not after this burst
     if (stream_registered_ && sess_flow()) {
       owed_ += payload.size();
       maybe_grant();
     }
-    // The first token (and the head before it) now, not after this burst.
-    // Last: a failing write closes the connection from inside.
-    if (first && conn_) conn_->flush_now();
   }
 
   // "flow": RES_BODY bytes the client has taken (our output backlog for it is
