@@ -424,12 +424,6 @@ void TcpConn::write(Bytes b) {
   if (low_water_ && out_bytes_ > low_water_) above_low_ = true;
 }
 
-void TcpConn::flush_now() {
-  if (fd_ < 0 || out_.empty() || handshaking_ || !r_.lightly_loaded()) return;
-  auto self = shared_from_this();
-  do_write();  // the posted write finds the queue empty
-}
-
 void TcpConn::do_write() {
   while (fd_ >= 0 && !out_.empty() && !handshaking_) {
     ssize_t n;

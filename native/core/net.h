@@ -100,12 +100,6 @@ class TcpConn : public std::enable_shared_from_this<TcpConn> {
 
   void write(Bytes b);
   void write(std::string s);
-  // Writes what is queued now instead of at the end of the loop turn (the
-  // start of a response or a request, several of which arrive in one burst:
-  // the first need not wait for the parsing of the others). Only on a loop
-  // under half busy (Reactor::lightly_loaded); otherwise the turn-end write
-  // keeps coalescing.
-  void flush_now();
   void write(const void* p, size_t n) { write(Bytes::copy(p, n)); }
   size_t pending_out() const { return out_bytes_; }
   void pause_reading();

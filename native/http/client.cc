@@ -469,7 +469,6 @@ void ClientCall::attach(std::shared_ptr<TcpConn> c, bool reused) {
   if (req_.body_len <= 16384) {
     for (auto& b : req_.body) head.append(reinterpret_cast<const char*>(b.data()), b.size());
     conn_->write(std::move(head));
-    conn_->flush_now();  // to the upstream now, not after the rest of this burst of requests
   } else {
     conn_->write(std::move(head));
     for (auto& b : req_.body) conn_->write(b);

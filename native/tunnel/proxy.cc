@@ -124,8 +124,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
       LOG_WARN(kT, "received body chunk before headers for stream %u", sid_);
       return;
     }
-    const bool first = !first_body_;
-    if (first) {
+    if (!first_body_) {
       first_body_ = true;
       trace::event("proxy", sid_, "first_body");
     }
@@ -167,7 +166,6 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     } else {
       conn_->write(payload);
     }
-    if (first) conn_->flush_now();  // the first token (and the head before it) now, not after this burst
     if (stream_registered_ && sess_flow()) {
       owed_ += payload.size();
       maybe_grant();
