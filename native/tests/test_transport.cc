@@ -1004,6 +1004,10 @@ TEST(slow_association_thread_loses_nothing_uncounted) {
   }, 60000));
   CHECK_EQ(got, size_t(n));
   CHECK(order_ok);
+  // A tail-loss probe sent just before the last message arrived can still be
+  // on its way through the reader and its lanes: let transmissions in flight
+  // land before counting (a real loss keeps the counts apart until timeout).
+  r.run_until([&] { return off->sctp()->stats().data_chunks_sent <= ans->sctp()->stats().data_chunks_received; }, 500);
   const auto& st = off->sctp()->stats();
   const uint64_t overflow = ans->ice()->rx_overflow();
   const auto* lane = off->dtls() ? off->dtls()->tx_lane_state() : nullptr;
