@@ -2,7 +2,6 @@
 
 #include <signal.h>
 #include <sys/epoll.h>
-#include <sys/prctl.h>
 #include <sys/eventfd.h>
 #include <sys/signalfd.h>
 #include <time.h>
@@ -312,18 +311,7 @@ void Reactor::run_once(int64_t timeout_us) {
   run_flush();
 }
 
-// Microsecond timeouts need microsecond timers: the kernel's default 50 us
-// timer slack let a 50 us coalescing window or a link emulator's packet
-// timer fire up to 50 us late. Set once per thread that runs a loop.
-static void precise_timers() {
-  thread_local bool done = false;
-  if (done) return;
-  done = true;
-  prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // 1 us
-}
-
 void Reactor::run() {
-  precise_timers();
   Reactor* prev = t_current;
   t_current = this;
   stop_ = false;
@@ -332,7 +320,6 @@ void Reactor::run() {
 }
 
 bool Reactor::run_until(const std::function<bool()>& pred, uint64_t timeout_ms) {
-  precise_timers();
   Reactor* prev = t_current;
   t_current = this;
   uint64_t deadline = now_us() + timeout_ms * 1000;
