@@ -215,12 +215,11 @@ static int wait_events(int epfd, epoll_event* evs, int max, int64_t timeout_us) 
   return epoll_wait(epfd, evs, max, timeout_us <= 0 ? 0 : int((timeout_us + 999) / 1000));
 }
 
-// At most kMaxEvents ready descriptors per turn: the flush hooks (transport
-// flushes, cross-thread hand-offs) run at the end of a turn, so a turn of 256
-// token sockets made every request and first token crossing between threads
-// wait behind all of them; with 64 the node row's 1024-stream p99 TTFT went
-// 15.2 -> 11.4 ms and its events 0.931 -> 0.971 of direct (profiles/r05/b27).
-constexpr int kMaxEvents = 64;
+// Ready descriptors taken per turn. 64 (shorter turns, earlier flushes and
+// hand-offs) looked better on one box's node row (profiles/r05/b27) and worse
+// on two others (b28, b29: 1024-stream p99 11.2 -> 15.6 ms, download 0.235 ->
+// 0.203 of direct).
+constexpr int kMaxEvents = 256;
 
 void Reactor::run_once(int64_t timeout_us) {
   epoll_event evs[kMaxEvents];
