@@ -53,7 +53,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--streams", type=int, default=8, help="concurrent streams per rank for the headline")
     ap.add_argument("--curve", default="1,2,4", help="extra stream counts measured (untimed) for the curve")
-    ap.add_argument("--curve-steps", type=int, default=3)
+    ap.add_argument("--curve-steps", type=int, default=None,
+                    help="timed steps (and warm-up) of each extra curve point; default: the headline's --steps / --warmup, "
+                         "so every point and its direct leg compare samples of the headline's size")
     ap.add_argument("--transport", default=os.environ.get("BENCH_TRANSPORT", "webrtc"))
     ap.add_argument("--mock", choices=["native", "python"], default="native")
     ap.add_argument("--interval-ms", type=float, default=100.0)
@@ -250,10 +252,12 @@ def main():
     curve = {}
     for s in sorted({int(x) for x in a.curve.split(",") if x} | {a.streams}) if drive else []:
         n = s * (world if node else 1)
-        tun_r = head if s == a.streams else loadgen(tun.proxy_port, n, a.curve_steps, warmup=1)
-        # The direct leg of the headline point runs the headline's own steps
-        # and warm-up: added p50 / p99 then compare samples of equal size.
-        dir_r = direct(ups, n, a.steps, a.warmup) if s == a.streams else direct(ups, n, a.curve_steps)
+        c_steps = a.curve_steps or a.steps
+        c_warm = max(1, a.warmup if a.curve_steps is None else 1)
+        tun_r = head if s == a.streams else loadgen(tun.proxy_port, n, c_steps, warmup=c_warm)
+        # Every direct leg runs its tunneled leg's steps and warm-up: added
+        # p50 / p99 then compare samples of equal size.
+        dir_r = direct(ups, n, a.steps, a.warmup) if s == a.streams else direct(ups, n, c_steps, c_warm)
         curve[str(s)] = {
             "tunneled_req_s": tun_r["req_s"],
             "direct_req_s": dir_r["req_s"],
@@ -304,6 +308,8 @@ def main():
         requests, errors = int(r[0].item()), int(r[1].item())
 
     if rank == 0:
+        from p2p_llm_tunnel_amd.utils.boxinfo import identity
+        box = identity()
         out = {
             "metric": METRIC,
             "value": requests / dt,
@@ -340,6 +346,8 @@ def main():
             "step_max_ttft_ms_rank0": head.get("step_max_ttft_ms"),
             "errors": errors,
             "curve_rank0": curve,
+            "curve_steps": a.curve_steps or a.steps,
+            "box": box,
             "jumbo_rank0": jumbo,
         }
         line = json.dumps(out)

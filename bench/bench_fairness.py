@@ -139,7 +139,8 @@ def main():
                 r = run_row(rate, a.rtt_ms, loss, pair.split(":"), a.seconds, a.mb, mtu_extra, a.relay, a.queue_kb)
                 rows.append(r)
                 print(json.dumps(r), file=sys.stderr, flush=True)
-    res = {"bench": "fairness", "rows": rows}
+    from p2p_llm_tunnel_amd.utils.boxinfo import identity
+    res = {"bench": "fairness", "rows": rows, "box": identity()}
     if a.out:
         with open(a.out, "w") as f:
             json.dump(res, f, indent=1)

@@ -37,6 +37,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 from p2p_llm_tunnel_amd import binary  # noqa: E402
+from p2p_llm_tunnel_amd.utils.boxinfo import identity as _box  # noqa: E402
 from p2p_llm_tunnel_amd.utils.build import ensure_native  # noqa: E402
 from p2p_llm_tunnel_amd.utils.procs import Tunnel, free_port, spawn  # noqa: E402
 
@@ -219,6 +220,7 @@ def main():
                                          (["--thread", thread] if thread else []), capture_output=True, text=True).stdout
                     with open(os.path.join(a.profile_dir, f"{k}{suffix}.txt"), "w") as fh:
                         fh.write(rep)
+    res["box"] = _box()
     doc = json.dumps(res, indent=1)
     if a.out:
         with open(a.out, "w") as f:

@@ -34,6 +34,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 from p2p_llm_tunnel_amd import binary  # noqa: E402
+from p2p_llm_tunnel_amd.utils.boxinfo import identity as _box  # noqa: E402
 from p2p_llm_tunnel_amd.utils.build import ensure_native  # noqa: E402
 from p2p_llm_tunnel_amd.utils.pinning import cgroup_cpu_stat, cpu_stat_delta  # noqa: E402
 from p2p_llm_tunnel_amd.utils.procs import Tunnel, free_port, spawn  # noqa: E402
@@ -246,6 +247,7 @@ def main():
         for tf in traces:
             if os.path.exists(tf):
                 os.unlink(tf)
+    res["box"] = _box()
     doc = json.dumps(res, indent=1)
     if a.out:
         with open(a.out, "w") as f:

@@ -32,6 +32,7 @@ sys.path.insert(0, os.path.join(ROOT))
 from bench import loadgen, start_mock  # noqa: E402
 from p2p_llm_tunnel_amd.utils.build import ensure_native  # noqa: E402
 from p2p_llm_tunnel_amd.utils.procs import Tunnel  # noqa: E402
+from p2p_llm_tunnel_amd.utils.boxinfo import identity as _box  # noqa: E402
 
 
 MTU_EXTRA: list[str] = []  # ["--no-jumbo-loopback"] with --std-mtu
@@ -166,6 +167,7 @@ def main():
     if not a.quick:
         res["post_64x1MB"].append(post_1mb("tcp"))
     res["idle_burst"] = idle_burst("webrtc", a.idle_s)
+    res["box"] = _box()
     doc = json.dumps(res, indent=1)
     if a.out:
         with open(a.out, "w") as f:

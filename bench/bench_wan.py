@@ -147,7 +147,8 @@ def main():
     mock = spawn("mock", [binary("tunnel-mock"), "--port", str(mport), "--interval-ms", "10", "--tokens", "100",
                           "--threads", "2"])
     mock.wait_for("Mock LLM server running", 10)
-    res = {"host": os.uname().nodename, "time": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
+    from p2p_llm_tunnel_amd.utils.boxinfo import identity
+    res = {"box": identity(), "host": os.uname().nodename, "time": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
            "mtu": 1200, "rate_mbps": a.rate_mbps, "extra": a.extra, "rows": [], "steady": []}
     extra = ["--no-jumbo-loopback"] + [x for x in a.extra.split() if x]
     try:

@@ -116,6 +116,8 @@ def main():
         # >= 90 % / >= 75 % CPU, over the process's life (warm-up, tunneled and
         # direct runs; the direct run adds idle intervals only).
         out["timeline"] = timeline.summarise(tl_dir, out.get("pids", {}))
+    from p2p_llm_tunnel_amd.utils.boxinfo import identity
+    out["box"] = identity()
     print(json.dumps(out))
     if a.profile_dir:
         for f in sorted(glob.glob(os.path.join(a.profile_dir, "tunnel.*.prof"))):

@@ -9,6 +9,7 @@
 // Extra opt-in flags (defaults keep reference behaviour) are listed in --help.
 #include <malloc.h>
 #include <sched.h>
+#include <unistd.h>
 
 #include <cerrno>
 #include <cstdint>
@@ -104,6 +105,10 @@ const std::vector<Opt>& ext_opts() {
        "HTTP worker threads beside the association thread (auto: half the usable CPUs less one, 1..4; 0: single thread)", Kind::U64OrAuto, Role::Both, 0, 256},
       {"inline-streams", "TUNNEL_INLINE_STREAMS", "16",
        "Concurrent streams handled on the association thread before new ones go to workers", Kind::U64},
+      {"assoc", "TUNNEL_ASSOC", "1",
+       "Parallel associations (PeerConnections, one thread each) when the peer agrees; bulk requests go to the extra "
+       "ones, everything else stays on the first (1 = the reference's single data channel)",
+       Kind::U64, Role::Both, 1, 8},
       {"max-request-body", "TUNNEL_MAX_REQUEST_BODY", "0",
        "serve: answer 413 to request bodies larger than this many bytes (0 = unlimited)", Kind::U64, Role::Serve},
       {"stream-body-threshold", "TUNNEL_STREAM_BODY_THRESHOLD", "8388608",
@@ -303,6 +308,35 @@ uint64_t num(const std::map<std::string, std::string>& m, const char* k) {
 
 }  // namespace
 
+// TUNNEL_* variables this build reads besides the flags' own (README,
+// "Environment switches"), and the retired ones with what replaced them: a
+// setting nobody reads is reported instead of silently doing nothing.
+const char* const kSwitches[] = {"TUNNEL_LOG",       "TUNNEL_TRACE",    "TUNNEL_PROFILE",     "TUNNEL_THREAD_TIMELINE",
+                                 "TUNNEL_FAULT",     "TUNNEL_NAT",      "TUNNEL_UDP_OFFLOAD", "TUNNEL_UDP_BUF_KB",
+                                 "TUNNEL_RX_READER", "TUNNEL_COALESCE_US", "TUNNEL_SCTP_CC",  "TUNNEL_DTLS_RECORDS",
+                                 "TUNNEL_FEATURES",  "TUNNEL_PIN_THREADS", "TUNNEL_TLS_INSECURE"};
+
+const char* retired_hint(const std::string& name) {
+  if (name.rfind("TUNNEL_FAULT_", 0) == 0) return "use TUNNEL_FAULT=key=value,... (drop, dup, delay_ms, blackhole, rtt_ms, rate_mbps, queue_kb)";
+  if (name.rfind("TUNNEL_SCTP_", 0) == 0) return "congestion knobs are folded into TUNNEL_SCTP_CC=reno|beta=NN";
+  if (name == "TUNNEL_GSO" || name == "TUNNEL_GRO") return "use TUNNEL_UDP_OFFLOAD=gso,gro|none";
+  if (name.rfind("TUNNEL_DTLS_", 0) == 0) return "use TUNNEL_DTLS_RECORDS=evp|openssl";
+  return "removed (README lists the switches this build reads)";
+}
+
+void warn_unused_env(const std::vector<Opt>& a, const std::vector<Opt>& b) {
+  for (char** e = environ; e && *e; e++) {
+    std::string kv = *e;
+    if (kv.rfind("TUNNEL_", 0) != 0) continue;
+    std::string name = kv.substr(0, kv.find('='));
+    bool known = false;
+    for (auto* s : kSwitches) known |= name == s;
+    for (auto* v : {&a, &b})
+      for (auto& o : *v) known |= o.env && name == o.env;
+    if (!known) LOG_WARN("tunnel", "%s is not read by this build and is ignored: %s", name.c_str(), retired_hint(name));
+  }
+}
+
 int main(int argc, char** argv) {
   // Receive/datagram buffers come and go in 64 KiB units: keep freed heap
   // instead of trimming it back to the kernel after every burst (brk/sbrk
@@ -347,6 +381,7 @@ int main(int argc, char** argv) {
   }
   std::map<std::string, std::string> m;
   if (!parse_sub(argc, argv, cmd.c_str(), cmd == "serve" ? serve_opts() : proxy_opts(), m)) return 2;
+  warn_unused_env(serve_opts(), proxy_opts());
 
   AppConfig cfg;
   cfg.mode = cmd;
@@ -400,6 +435,7 @@ int main(int argc, char** argv) {
   cfg.busy_poll_us = num(m, "busy-poll-us");
   cfg.workers = m["workers"] == "auto" ? -1 : int(num(m, "workers"));
   cfg.inline_streams = num(m, "inline-streams");
+  cfg.assoc = uint32_t(num(m, "assoc"));
   if (cmd == "serve") {
     cfg.upstream_prewarm = num(m, "upstream-prewarm");
     cfg.upstream_prewarm_ttl_ms = num(m, "upstream-prewarm-ttl-ms");

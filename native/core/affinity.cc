@@ -51,19 +51,23 @@ void pin_this_thread(int tag) {
   if (tag == 0) {
     slot = 0;
   } else if (n >= 5) {
-    // [assoc][workers ...][seal][send][reader][RX lane]: the workers (which
-    // talk to the upstreams / clients over TCP) next to the association
-    // thread, the socket reader last (on a set that spans two L3 domains,
-    // nearest the peer's side); on 5 CPUs the idle RX lane shares the
-    // reader's. (Seal and send sharing one CPU, the workers getting the
-    // other, lost on the 64 x 1 MB echo: 1576 vs 1940 req/s, profiles/r04/txs30.)
-    const size_t nw = n >= 6 ? n - 5 : 1;
-    const size_t seal = 1 + nw, send = seal + 1, reader = send + 1;
+    // [assoc][workers ...][seal][send][reader][RX lane][open 0][open 1]: the
+    // workers (which talk to the upstreams / clients over TCP) next to the
+    // association thread, the receive stages last (on a set that spans two L3
+    // domains, nearest the peer's side). (Seal and send sharing one CPU, the
+    // workers getting the other, lost on the 64 x 1 MB echo: 1576 vs 1940
+    // req/s, profiles/r04/txs30.) Below 8 CPUs the open lanes have no CPUs of
+    // their own: one runs, on the RX lane's; on 5 that is the reader's own.
+    const bool own_open = n >= 8;
+    const size_t nw = own_open ? n - 7 : n >= 6 ? n - 5 : 1;
+    const size_t seal = 1 + nw, send = seal + 1, reader = send + 1, rx = std::min(reader + 1, n - 1);
     if (tag >= 1 && tag < 90) slot = 1 + size_t(tag - 1) % nw;
     else if (tag == 90) slot = seal;
     else if (tag == 93) slot = send;
     else if (tag == 92) slot = reader;
-    else slot = std::min(reader + 1, n - 1);  // RX lane (idle while the reader runs), second sealer
+    else if (tag == 95 && own_open) slot = rx + 1;
+    else if (tag == 96 && own_open) slot = rx + 2;
+    else slot = rx;  // RX lane, second sealer (and the one open lane below 8 CPUs)
   } else {
     slot = 1 + g_next.fetch_add(1, std::memory_order_relaxed) % (n - 1);
   }
@@ -72,6 +76,12 @@ void pin_this_thread(int tag) {
   CPU_ZERO(&one);
   CPU_SET(cpu, &one);
   sched_setaffinity(0, sizeof one, &one);
+}
+
+int open_lane_count(int want) {
+  if (!enabled()) return want;
+  capture();
+  return g_cpus.size() >= 8 ? want : 1;
 }
 
 }  // namespace p2pt::affinity

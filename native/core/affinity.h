@@ -20,11 +20,17 @@ void set_default(bool on);
 bool enabled();
 // Pins the calling thread by its role (profiler tags): 0 the association
 // thread, 1.. HTTP workers, 90 TX seal lane, 91 RX lane, 92 socket reader,
-// 93 TX send lane, 94 second sealer. With n >= 6 CPUs, in the set's order:
-// the association thread, the workers (n - 5 of them by default), the seal
-// and send stages, the socket reader, and last the RX lane (idle while the
-// reader runs) with the second sealer. With fewer CPUs: round robin.
+// 93 TX send lane, 94 second sealer, 95 / 96 the socket reader's record-
+// opening lanes. In the set's order: the association thread, the workers,
+// the seal and send stages, the socket reader, the RX lane (with the second
+// sealer), then the two open lanes — each on a CPU of its own from 8 CPUs up
+// (the workers get n - 7), on the RX lane's CPU below that (with n - 5
+// workers from 6 CPUs, one on 5), where only one open lane runs
+// (open_lane_count). With fewer than 5 CPUs: round robin.
 void pin_this_thread(int tag);
+// Open lanes the socket reader should start (of `want`): 1 when pinned on a
+// set too small to give them CPUs of their own, else `want`.
+int open_lane_count(int want);
 // CPUs of the process's set as it was before any thread pinned itself (the
 // calling thread's set when nothing was pinned).
 long process_cpu_count();

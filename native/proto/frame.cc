@@ -13,7 +13,7 @@ namespace p2pt::proto {
 std::optional<MsgType> msg_type_from_u8(uint8_t v) {
   switch (v) {
     case 1: case 2: case 3: case 4:
-    case 10: case 11: case 12: case 13: case 14:
+    case 10: case 11: case 12: case 13: case 14: case 15:
     case 20: case 21: case 22:
     case 99:
       return MsgType(v);
@@ -33,6 +33,7 @@ const char* msg_type_name(MsgType t) {
     case MsgType::ReqEnd: return "ReqEnd";
     case MsgType::Cancel: return "Cancel";
     case MsgType::Credit: return "Credit";
+    case MsgType::Assoc: return "Assoc";
     case MsgType::ResHeaders: return "ResHeaders";
     case MsgType::ResBody: return "ResBody";
     case MsgType::ResEnd: return "ResEnd";
@@ -182,7 +183,14 @@ Json Hello::to_json() const {
   j.set("features", str_array(features));
   if (!psk_nonce.empty()) j.set("psk_nonce", Json(psk_nonce));
   if (!psk_mac.empty()) j.set("psk_mac", Json(psk_mac));
+  if (assoc) j.set("assoc", Json(assoc));
   return j;
+}
+
+// Optional unsigned member (absent is fine).
+static bool opt_u32(const Json& j, const char* k, uint32_t& out, std::string* err) {
+  if (!j.get(k)) return true;
+  return get_u32(j, k, out, err);
 }
 
 // Optional string member (absent is fine; present must be a string).
@@ -204,7 +212,8 @@ bool Hello::from_json(const Json& j, Hello& out, std::string* err) {
   }
   return get_str(j, "proto", out.proto, err) && get_u32(j, "min_version", out.min_version, err) &&
          get_u32(j, "max_version", out.max_version, err) && get_str_array(j, "features", out.features, err) &&
-         opt_str(j, "psk_nonce", out.psk_nonce, err) && opt_str(j, "psk_mac", out.psk_mac, err);
+         opt_str(j, "psk_nonce", out.psk_nonce, err) && opt_str(j, "psk_mac", out.psk_mac, err) &&
+         opt_u32(j, "assoc", out.assoc, err);
 }
 
 Json Agree::to_json() const {
@@ -212,6 +221,7 @@ Json Agree::to_json() const {
   j.set("version", Json(version));
   j.set("features", str_array(features));
   if (!psk_mac.empty()) j.set("psk_mac", Json(psk_mac));
+  if (assoc) j.set("assoc", Json(assoc));
   return j;
 }
 
@@ -221,7 +231,7 @@ bool Agree::from_json(const Json& j, Agree& out, std::string* err) {
     return false;
   }
   return get_u32(j, "version", out.version, err) && get_str_array(j, "features", out.features, err) &&
-         opt_str(j, "psk_mac", out.psk_mac, err);
+         opt_str(j, "psk_mac", out.psk_mac, err) && opt_u32(j, "assoc", out.assoc, err);
 }
 
 std::string psk_mac(const std::string& secret, const char* role, const std::string& nonce,
@@ -235,7 +245,7 @@ std::string psk_mac(const std::string& secret, const char* role, const std::stri
 // exactly like a reference peer in interop and A/B tests).
 const std::vector<std::string>& our_features() {
   static const std::vector<std::string> f = [] {
-    std::vector<std::string> v{"sse", "cancel", "flow", "multistream"};
+    std::vector<std::string> v{"sse", "cancel", "flow", "multistream", "assoc"};
     if (const char* e = getenv("TUNNEL_FEATURES")) {
       v.clear();
       std::string s = e;

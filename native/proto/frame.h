@@ -49,6 +49,13 @@ enum class MsgType : uint8_t {
   // sent by serve. Each side starts with kFlowWindow bytes per stream and
   // direction. Not in the reference (which has no flow control, Q11).
   Credit = 14,
+  // Extension "assoc" (only when both HELLOs list it): signalling for the
+  // extra associations (parallel PeerConnections) on the first data channel.
+  // stream_id = the association's index (1..N-1); the payload is JSON
+  // {"kind":"offer"|"answer"|"candidate"|"bye", "sdp"|"candidate": "..."}.
+  // The reference's one data channel (rtc.rs:133) is the only path either
+  // side of a reference peer ever uses; see tunnel/assoc.h.
+  Assoc = 15,
   ResHeaders = 20,
   ResBody = 21,
   ResEnd = 22,
@@ -98,6 +105,9 @@ struct Hello {
   // "psk" extension (only with --secret; serialised only when set, so a
   // reference peer sees the reference's HELLO): nonce and proof of the secret.
   std::string psk_nonce, psk_mac;
+  // "assoc" extension: how many associations (the first data channel's plus
+  // parallel ones) the proxy would use; 0 = not offered (not serialised).
+  uint32_t assoc = 0;
   Json to_json() const;
   static bool from_json(const Json& j, Hello& out, std::string* err);
 };
@@ -106,6 +116,7 @@ struct Agree {
   uint32_t version = 1;
   std::vector<std::string> features;
   std::string psk_mac;  // "psk" extension: the serve side's proof
+  uint32_t assoc = 0;   // "assoc" extension: associations agreed (min of both sides); 0 = none
   Json to_json() const;
   static bool from_json(const Json& j, Agree& out, std::string* err);
 };
@@ -131,6 +142,8 @@ std::string psk_mac(const std::string& secret, const char* role, const std::stri
 // on the emulated 50 ms / 2 % path that put bulk loss recovery in the token
 // tail.
 constexpr int kLanes = 64;
+// "assoc": at most this many associations per tunnel (the first included).
+constexpr uint32_t kMaxAssoc = 8;
 const std::vector<std::string>& our_features();
 // Negotiate from a peer HELLO (reference Agree::from_hello, protocol.rs:44-80).
 bool agree_from_hello(const Hello& h, Agree& out, std::string* err,

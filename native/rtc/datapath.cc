@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "core/affinity.h"
 #include "core/log.h"
 #include "core/profiler.h"
 #include "core/reactor.h"
@@ -40,10 +41,12 @@ Lane::Lane(const char* name) {
     for (int sig : {SIGINT, SIGTERM, SIGHUP, SIGQUIT, SIGUSR1, SIGUSR2, SIGPIPE}) sigaddset(&mask, sig);
     pthread_sigmask(SIG_BLOCK, &mask, nullptr);
     pthread_setname_np(pthread_self(), n.c_str());
-    // T90 seal / T93 send / T91 rx in profiles and timelines
-    profiler::register_thread(n.find("-txsend") != std::string::npos ? 93
-                              : n.find("-tx") != std::string::npos   ? 90
-                                                                     : 91);
+    // T90 seal / T93 send / T91 rx / T95-96 open lanes in profiles and timelines
+    profiler::register_thread(n.find("-txsend") != std::string::npos  ? 93
+                              : n.find("-tx") != std::string::npos    ? 90
+                              : n.find("-open1") != std::string::npos ? 96
+                              : n.find("-open") != std::string::npos  ? 95
+                                                                      : 91);
     run();
   });
 }
@@ -329,7 +332,11 @@ RxReader::RxReader(int fd, const SockAddr& remote, std::shared_ptr<const RecordK
                    size_t slot, bool adaptive)
     : fd_(fd), stop_fd_(eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC)), remote_(remote), keys_(std::move(keys)),
       deliver_(std::move(deliver)), id_(id), slot_(slot), pool_(slot), adaptive_(adaptive), active_(!adaptive) {
-  for (auto& l : open_) l = std::make_unique<Lane>("p2pt-udp-open");
+  // One lane per CPU it can have: pinned on a set too small to give the open
+  // lanes CPUs of their own (affinity::open_lane_count), a second lane would
+  // only preempt the first.
+  n_open_ = affinity::open_lane_count(kOpenLanes);
+  for (int k = 0; k < n_open_; k++) open_[k] = std::make_unique<Lane>(k == 0 ? "p2pt-udp-open0" : "p2pt-udp-open1");
   th_ = std::thread([this] {
     sigset_t mask;
     sigemptyset(&mask);
@@ -597,7 +604,7 @@ void RxReader::run() {
         open_burst(*b);
         complete(seq, std::move(b));
       });
-      next_lane_ = (next_lane_ + 1) % kOpenLanes;
+      next_lane_ = (next_lane_ + 1) % n_open_;
     } else {
       open_burst(*burst);
       complete(seq, std::move(burst));

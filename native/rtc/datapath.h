@@ -318,6 +318,7 @@ class RxReader {
   uint64_t seq_deliver_ = 0;                                // ord_mu_
   std::vector<std::pair<uint64_t, std::unique_ptr<Burst>>> ready_;  // ord_mu_: opened, waiting for an earlier one
   std::unique_ptr<Lane> open_[kOpenLanes];
+  int n_open_ = kOpenLanes;  // lanes started (affinity::open_lane_count)
   int next_lane_ = 0;
   std::thread th_;  // last: started after everything above exists
 };

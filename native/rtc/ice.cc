@@ -718,6 +718,10 @@ void IceAgent::flush() {
   mmsghdr msgs[kBatch];
   iovec iovs[kIov];
   alignas(cmsghdr) char ctrl[kBatch][CMSG_SPACE(sizeof(uint16_t))];
+  // udp_tx is stamped before the send syscall: on loopback the kernel
+  // delivers inside sendmmsg, so a stamp after it read as 1-5 us *after* the
+  // receiver's udp_kernel (profiles/r05/b30/ttft8.json).
+  trace::tx_done();
   size_t i = 0;
   while (i < outq_.size()) {
     // Resolve the socket (relay locals go through TURN).
@@ -804,7 +808,6 @@ void IceAgent::flush() {
     }
     i = j;
   }
-  trace::tx_done();
 }
 
 int IceAgent::local_for_socket(int si, bool relay) const {
@@ -814,7 +817,12 @@ int IceAgent::local_for_socket(int si, bool relay) const {
 }
 
 void IceAgent::on_readable(int si) {
-  if (closed_) return;
+  // A socket handed to the outside reader (detach_reader) is read there only:
+  // an event for it queued earlier in this reactor turn, or a detach made by a
+  // callback of this very loop (a flush hook engaging the reader), must not
+  // read it here too, or datagrams of one flow overtake each other between
+  // the two paths (past DTLS's replay window, they are dropped as old).
+  if (closed_ || si == detached_) return;
   auto self = shared_from_this();
   constexpr int kBatch = 32;
   mmsghdr msgs[kBatch];
@@ -824,7 +832,7 @@ void IceAgent::on_readable(int si) {
   // coalesced burst as one datagram).
   alignas(cmsghdr) char ctrl[kBatch][CMSG_SPACE(sizeof(int)) + CMSG_SPACE(sizeof(uint32_t)) +
                                       CMSG_SPACE(sizeof(timespec))];
-  for (int round = 0; round < 8 && !closed_; round++) {
+  for (int round = 0; round < 8 && !closed_ && si != detached_; round++) {
     for (int i = 0; i < kBatch; i++) rxpool_[i].reset();
     for (int i = 0; i < kBatch; i++) {
       // Buffers whose datagrams are still referenced (zero-copy views handed

@@ -828,6 +828,14 @@ void PeerConnection::on_sctp_message(uint16_t st, uint32_t ppid, Bytes msg, std:
       LOG_INFO(kT, "received data channel: %s", label.c_str());
       auto dc = std::make_shared<DataChannel>(weak_from_this(), label);
       dc->stream_ = st;
+      // A repeated OPEN on a stream in use replaces its channel: the old one
+      // (still held by the application) is closed here and forgets the
+      // association, or its cached pointer would outlive this connection.
+      auto old = channels_.find(st);
+      if (old != channels_.end() && old->second != dc) {
+        old->second->assoc_ = nullptr;
+        old->second->set_closed("data channel replaced by a new OPEN on its stream");
+      }
       channels_[st] = dc;
       sctp_->send(st, kPpidDcep, {Bytes::copy("\x02", 1)});
       if (on_data_channel) on_data_channel(dc);

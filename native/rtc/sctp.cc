@@ -1182,7 +1182,7 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
 void SctpAssociation::loss_response(bool random_loss, bool over_bdp, uint64_t now) {
   if (random_loss) stats_.random_loss_events++;
   // A random loss (no standing queue) cuts cwnd by a fifth
-  // (TUNNEL_SCTP_RANDOM_BETA_PCT, default 80: Veno's random-loss beta), at
+  // (TUNNEL_SCTP_CC=beta=NN, default 80: Veno's random-loss beta), at
   // most once per round trip; losses with a backlog cut by 0.3 (CUBIC).
   // Measured against a Reno-like flow on one shared bottleneck
   // (bench/bench_fairness.py: 0.5 % loss, 20 ms), keeping cwnd on random loss

@@ -390,7 +390,7 @@ TEST(sctp_queue_bound_keeps_short_path_queue_small) {
   // 1 ms base RTT, 100 Mbit/s bottleneck behind a deep 2 MiB drop-tail queue
   // (a LAN switch or a same-host socket buffer: no loss until it is full).
   // Loss-based control alone fills the queue (160 ms of standing delay); the
-  // short-path queue bound (TUNNEL_SCTP_QUEUE_US, 300 us by default) cuts cwnd
+  // short-path queue bound (300 us target, SctpAssociation::queue_bound) cuts cwnd
   // while the per-round minimum RTT exceeds the base RTT by more than the
   // target, so the RTT stays within a few ms of the base (the cwnd floor of
   // 1 MiB still queues ~80 ms at this low rate: the floor protects fast

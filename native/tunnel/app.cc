@@ -234,6 +234,10 @@ int run_app(const AppConfig& cfg) {
         return;
       }
       st.session_start_ms = Reactor::now_ms();
+      // Extra associations ("assoc") are WebRTC connections like the first.
+      std::shared_ptr<const rtc::PcConfig> assoc_pc;
+      if (cfg.assoc > 1 && (cfg.transport == "webrtc" || cfg.transport.empty()))
+        assoc_pc = std::make_shared<rtc::PcConfig>(make_pc_config(cfg));
       if (cfg.mode == "serve") {
         LOG_INFO(kT, "WebRTC connected, starting serve...");
         ServeConfig sc;
@@ -248,6 +252,9 @@ int run_app(const AppConfig& cfg) {
         sc.inline_streams = cfg.inline_streams;
         sc.max_request_body = cfg.max_request_body;
         sc.stream_body_threshold = cfg.stream_body_threshold ? cfg.stream_body_threshold : UINT64_MAX;
+        sc.assoc = cfg.assoc;
+        sc.assoc_pc = assoc_pc;
+        sc.busy_poll_us = cfg.busy_poll_us;
         st.serve = ServeSession::start(r, ch, sc, [&](const std::string& e) { on_fail(e); }, &pool);
       } else {
         LOG_INFO(kT, "WebRTC connected, starting proxy...");
@@ -260,6 +267,9 @@ int run_app(const AppConfig& cfg) {
         pc.listen_early = cfg.listen_early;
         pc.secret = cfg.secret;
         pc.inline_streams = cfg.inline_streams;
+        pc.assoc = cfg.assoc;
+        pc.assoc_pc = assoc_pc;
+        pc.busy_poll_us = cfg.busy_poll_us;
         st.proxy = ProxySession::start(r, ch, pc, [&](const std::string& e) { on_fail(e); }, &pool);
         st.early.session = st.proxy;
       }

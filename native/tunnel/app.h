@@ -73,6 +73,8 @@ struct AppConfig {
   int workers = -1;
   // Streams kept on the association thread before new ones go to workers.
   size_t inline_streams = 16;
+  // "assoc" extension (tunnel/assoc.h): associations in total, <= 1 = off.
+  uint32_t assoc = 1;
   // serve: request bodies at least this big stream to the upstream as they
   // arrive; 413 above max_request_body (0 = unlimited).
   uint64_t stream_body_threshold = 8 << 20;

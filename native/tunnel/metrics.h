@@ -45,7 +45,8 @@ void flush();  // write out what is held (also done at exit)
 // converted to CLOCK_MONOTONIC), when a thread read it, and when the
 // association thread took it up; rx_stamps() writes them for a stream as
 // udp_kernel / udp_read / rx_assoc. The send side queues a stream with
-// mark_tx() and the datagram flush that carries it stamps udp_tx (tx_done()).
+// mark_tx() and the datagram flush that carries it stamps udp_tx (tx_done(),
+// called just before the flush's first send syscall).
 void set_rx(uint64_t kernel_us, uint64_t read_us, uint64_t assoc_us);
 void rx_stamps(const char* role, uint32_t stream_id);
 void mark_tx(const char* role, uint32_t stream_id);

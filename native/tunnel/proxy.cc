@@ -7,6 +7,7 @@
 #include "core/log.h"
 #include "core/net.h"
 #include "http/http.h"
+#include "tunnel/assoc.h"
 #include "tunnel/metrics.h"
 
 namespace p2pt {
@@ -57,14 +58,21 @@ class ProxyWorker : public std::enable_shared_from_this<ProxyWorker> {
   const ProxyConfig& config() const { return shared_->cfg; }
   Reactor& reactor() { return r_; }
   void conn_closed(ProxyConn* c);
-  // The association thread's inline connection with a bulk request hands its
-  // socket to a worker (Placement: bulk I/O off the association thread).
-  bool may_migrate() const { return index_ == 0 && shared_->workers > 0; }
+  // Where a connection's next request runs (ProxyRouter): kStay, kWorker
+  // (the association thread's inline connection with a bulk request hands
+  // its socket to a worker: bulk I/O off the association thread), or the
+  // index of the association to hand the connection to.
+  static constexpr int kStay = -1, kWorker = -2;
+  int placement(bool bulk) const;
   void migrate(ProxyConn* c, int fd, Bytes unparsed);
-  BulkRoutes& bulk_routes() { return bulk_routes_; }
+  void hand_off(ProxyConn* c, int fd, Bytes unparsed, size_t dest);
+  bool bulk_route(const std::string& key) { return shared_->router->bulk_route(key); }
+  void note_route(const std::string& key, uint64_t bytes, bool streaming) {
+    shared_->router->note_route(key, bytes, streaming);
+  }
 
  private:
-  void adopt(int fd, Bytes unparsed = Bytes(), uint64_t accepted_us = 0);
+  void adopt(int fd, Bytes unparsed = Bytes(), uint64_t accepted_us = 0, bool counted = false);
   Reactor& r_;
   Reactor& assoc_;
   std::weak_ptr<ProxySession> sess_;
@@ -73,7 +81,6 @@ class ProxyWorker : public std::enable_shared_from_this<ProxyWorker> {
   std::unique_ptr<Pipe<ProxySession::Ev>> out_;
   std::unordered_map<uint32_t, std::weak_ptr<ProxyConn>> streams_;
   std::unordered_map<ProxyConn*, std::shared_ptr<ProxyConn>> conns_;
-  BulkRoutes bulk_routes_;  // learnt on this thread's connections (the inline one's decide migrations)
 };
 
 // One accepted client connection. Requests on a connection are handled one
@@ -303,21 +310,24 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
       simple_and_close(400, "text/plain", "Bad Request");
       return false;
     }
-    if (sess->may_migrate() && sess->ready()) {
-      // A large upload on the association thread: move the connection, head
-      // and all, to a worker before any stream exists for it.
+    if (sess->ready() && !pipelined_hold_) {
+      // Move the connection, head and all, before any stream exists for it:
+      // a bulk request to another association or off the association thread,
+      // an interactive one on an extra association back to the first.
       uint64_t blen = 0;
       std::string e2;
       const bool big_upload =
           http::request_body_mode(h, blen, &e2) == http::BodyDecoder::Mode::Length && blen >= Placement::kBulkBytes;
-      if ((big_upload || sess->bulk_routes().bulk(BulkRoutes::key(h.method, h.target))) && !pipelined_hold_) {
+      const int dest = sess->placement(big_upload || sess->bulk_route(BulkRoutes::key(h.method, h.target)));
+      if (dest != ProxyWorker::kStay) {
         int fd = conn_->release_fd();
         if (fd >= 0) {
           Bytes rest = Bytes::copy(inbuf_);
           inbuf_.clear();
           auto keep = shared_from_this();
           conn_.reset();
-          sess->migrate(this, fd, std::move(rest));
+          if (dest == ProxyWorker::kWorker) sess->migrate(this, fd, std::move(rest));
+          else sess->hand_off(this, fd, std::move(rest), size_t(dest));
           return false;
         }
       }
@@ -541,7 +551,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
   void response_done() {
     cancel_timer();
     if (head_written_ && !req_.method.empty())
-      if (auto sess = sess_.lock()) sess->bulk_routes().note(BulkRoutes::key(req_.method, req_.target), body_sent_, res_streaming_);
+      if (auto sess = sess_.lock()) sess->note_route(BulkRoutes::key(req_.method, req_.target), body_sent_, res_streaming_);
     if (stream_registered_) {
       if (auto sess = sess_.lock()) sess->unregister_stream(sid_);
       stream_registered_ = false;
@@ -684,6 +694,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
   uint64_t body_sent_ = 0;
   bool res_streaming_ = false;  // SSE / NDJSON response (never a bulk route)
   uint64_t timer_ = 0;
+  bool counted_ = false;  // the router counts this connection on its association
   friend class ProxyWorker;
 };
 
@@ -697,9 +708,10 @@ ProxyWorker::~ProxyWorker() {
   out_.reset();
 }
 
-void ProxyWorker::adopt(int fd, Bytes unparsed, uint64_t accepted_us) {
+void ProxyWorker::adopt(int fd, Bytes unparsed, uint64_t accepted_us, bool counted) {
   auto tc = TcpConn::adopt(r_, fd);
   auto pc = std::make_shared<ProxyConn>(weak_from_this(), tc);
+  pc->counted_ = counted;
   if (trace::enabled()) pc->set_conn_times(accepted_us, Reactor::now_us());
   conns_[pc.get()] = pc;
   pc->start();
@@ -711,13 +723,40 @@ void ProxyWorker::migrate(ProxyConn* c, int fd, Bytes unparsed) {
     ::close(fd);
     return;
   }
-  ProxySession::Ev ev(ProxySession::Ev::Migrate);
+  ProxySession::Ev ev(ProxySession::Ev::Migrate, c->counted_ ? 1 : 0);
   ev.fd = fd;
   ev.frame.payload = std::move(unparsed);
   out_->push(std::move(ev));
 }
 
+int ProxyWorker::placement(bool bulk) const {
+  const size_t own = shared_->assoc_index;
+  if (bulk && own == 0) {
+    const int k = shared_->router->pick_bulk();
+    if (k > 0) return k;
+  }
+  if (!bulk && own != 0) return 0;  // interactive traffic runs on the first association
+  if (bulk && index_ == 0 && shared_->workers > 0) return kWorker;
+  return kStay;
+}
+
+void ProxyWorker::hand_off(ProxyConn* c, int fd, Bytes unparsed, size_t dest) {
+  const bool counted = c->counted_;
+  if (!conns_.erase(c)) {
+    ::close(fd);
+    return;
+  }
+  out_->push(ProxySession::Ev{ProxySession::Ev::ConnClosed, 0});  // leaves this session's placement
+  if (counted) shared_->router->release(shared_->assoc_index);
+  metrics::counter_add("tunnel_assoc_handoffs_total");
+  shared_->router->hand(dest, fd, std::move(unparsed));
+}
+
 void ProxyWorker::conn_closed(ProxyConn* c) {
+  if (c->counted_) {
+    c->counted_ = false;
+    shared_->router->release(shared_->assoc_index);
+  }
   if (conns_.erase(c)) out_->push(ProxySession::Ev{ProxySession::Ev::ConnClosed, 0});
 }
 
@@ -731,7 +770,7 @@ void ProxyWorker::fail_all(const std::string& why) {
 void ProxyWorker::handle(ProxySession::Cmd& c) {
   using Cmd = ProxySession::Cmd;
   if (c.kind == Cmd::Adopt) {
-    adopt(c.fd, std::move(c.data), c.t_us);
+    adopt(c.fd, std::move(c.data), c.t_us, c.counted);
     return;
   }
   auto it = streams_.find(c.sid);
@@ -773,6 +812,8 @@ std::shared_ptr<ProxySession> ProxySession::start(Reactor& r, std::shared_ptr<Me
                                                   std::function<void(const std::string&)> done, WorkerPool* pool) {
   auto s = std::shared_ptr<ProxySession>(new ProxySession(r, ch, std::move(cfg)));
   s->done_ = std::move(done);
+  s->pool_ = pool;
+  s->shared_->router->attach(s->cfg_.assoc_index, &r, s);
   s->init_links(pool);
   std::weak_ptr<ProxySession> w = s;
   ch->on_message = [w](Bytes b) {
@@ -796,12 +837,16 @@ std::shared_ptr<ProxySession> ProxySession::start(Reactor& r, std::shared_ptr<Me
       return x ? f(*x) : 0.0;
     };
   };
-  metrics::gauge_fn("tunnel_streams_inflight", gauge([](ProxySession& x) { return double(x.routes_.size()); }));
-  metrics::gauge_fn("tunnel_streams_paused", gauge([](ProxySession& x) { return double(x.paused_.size()); }));
-  metrics::gauge_fn("tunnel_scheduler_queued_bytes",
-                    gauge([](ProxySession& x) { return double(x.sched_->queued_bytes()); }));
-  metrics::gauge_fn("tunnel_channel_buffered_bytes",
-                    gauge([](ProxySession& x) { return double(x.ch_->buffered_amount()); }));
+  // Gauges read the session from the metrics thread (the first
+  // association's): an extra association's session runs on another thread.
+  if (s->cfg_.assoc_index == 0) {
+    metrics::gauge_fn("tunnel_streams_inflight", gauge([](ProxySession& x) { return double(x.routes_.size()); }));
+    metrics::gauge_fn("tunnel_streams_paused", gauge([](ProxySession& x) { return double(x.paused_.size()); }));
+    metrics::gauge_fn("tunnel_scheduler_queued_bytes",
+                      gauge([](ProxySession& x) { return double(x.sched_->queued_bytes()); }));
+    metrics::gauge_fn("tunnel_channel_buffered_bytes",
+                      gauge([](ProxySession& x) { return double(x.ch_->buffered_amount()); }));
+  }
   if (ch->is_open()) {
     LOG_INFO(kT, "data channel already open");
     s->on_open();
@@ -819,6 +864,12 @@ ProxySession::ProxySession(Reactor& r, std::shared_ptr<MessageChannel> ch, Proxy
   sched_ = std::make_unique<FrameScheduler>(ch_);
   shared_->cfg = cfg_;
   shared_->cfg.on_listening = nullptr;
+  shared_->cfg.router = nullptr;
+  shared_->assoc_index = cfg_.assoc_index;
+  shared_->router = cfg_.router ? cfg_.router : std::make_shared<ProxyRouter>();
+  // Stream ids are per channel; an extra association's start at k << 28 so
+  // the trace (TUNNEL_TRACE) and the logs tell the associations' streams apart.
+  if (cfg_.assoc_index) shared_->next_sid = uint32_t(cfg_.assoc_index << 28) + 1;
 }
 
 void ProxySession::init_links(WorkerPool* pool) {
@@ -864,6 +915,7 @@ void ProxySession::release_links(const std::string& fail_why) {
 }
 
 ProxySession::~ProxySession() {
+  assoc_.reset();  // extra associations first (joins their threads)
   if (agree_timer_) r_.cancel(agree_timer_);
   if (ping_timer_) r_.cancel(ping_timer_);
   if (wd_timer_) r_.cancel(wd_timer_);
@@ -888,6 +940,8 @@ void ProxySession::stop(const std::string& why) {
   if (wd_timer_) r_.cancel(wd_timer_);
   wd_timer_ = 0;
   agree_timer_ = ping_timer_ = 0;
+  shared_->router->set_ready(cfg_.assoc_index, false);
+  assoc_.reset();
   listener_.reset();  // like the reference, the listener dies with the session
   routes_.clear();
   paused_.clear();
@@ -904,6 +958,8 @@ void ProxySession::on_open() {
   shared_->body_chunk = sched_->body_chunk();  // path MTU known now; read by connection threads later
   proto::Hello hello;
   hello.features = proto::our_features();
+  if (cfg_.assoc_index == 0 && cfg_.assoc > 1 && cfg_.assoc_pc) hello.assoc = std::min(cfg_.assoc, proto::kMaxAssoc);
+  else hello.features.erase(std::remove(hello.features.begin(), hello.features.end(), "assoc"), hello.features.end());
   if (!cfg_.secret.empty()) {  // psk extension: prove the shared secret on this channel
     uint8_t nonce[16];
     random_bytes(nonce, sizeof nonce);
@@ -987,9 +1043,42 @@ void ProxySession::on_agree(const proto::Frame& f) {
   last_pong_ms_ = Reactor::now_ms();
   send_ping();
   watchdog();
+  shared_->router->set_ready(cfg_.assoc_index, true);
+  if (cfg_.assoc_index != 0) {
+    LOG_INFO(kT, "association %zu ready", cfg_.assoc_index);
+    return;  // an extra association: client connections come from the first one's router
+  }
   if (!listener_ && !cfg_.listen_early) {
     if (!bind_listener()) return;
   }
+  const bool agreed = std::find(agree.features.begin(), agree.features.end(), "assoc") != agree.features.end();
+  if (agreed && agree.assoc > 1 && cfg_.assoc > 1 && cfg_.assoc_pc) start_assoc(std::min(agree.assoc, cfg_.assoc));
+}
+
+// "assoc": offers the extra PeerConnections over this channel; each gets a
+// proxy session of its own on its own thread, fed by this one's router.
+void ProxySession::start_assoc(uint32_t count) {
+  ProxyConfig c = cfg_;
+  c.assoc = 1;
+  c.router = shared_->router;
+  c.on_listening = nullptr;
+  WorkerPool* pool = pool_;
+  auto factory = [c, pool](Reactor& r, std::shared_ptr<MessageChannel> ch, size_t k,
+                           std::function<void(const std::string&)> done) -> std::shared_ptr<void> {
+    ProxyConfig ck = c;
+    ck.assoc_index = k;
+    return ProxySession::start(r, std::move(ch), ck, std::move(done), pool);
+  };
+  std::weak_ptr<ProxySession> w = shared_from_this();
+  auto send = [w](proto::Frame f) {
+    if (auto s = w.lock(); s && !s->stopped_) s->sched_->send(std::move(f));
+  };
+  auto router = shared_->router;
+  auto state = [router](size_t k, bool up, const std::string&) {
+    if (!up) router->set_ready(k, false);
+  };
+  LOG_INFO(kT, "associations agreed: %u", count);
+  assoc_ = AssocGroup::create(r_, true, count, *cfg_.assoc_pc, cfg_.busy_poll_us, factory, send, state);
 }
 
 bool ProxySession::bind_listener() {
@@ -1010,6 +1099,23 @@ bool ProxySession::bind_listener() {
   LOG_INFO(kT, "proxy listening on http://%s", addr.c_str());
   if (cfg_.on_listening) cfg_.on_listening(addr);
   return true;
+}
+
+void ProxySession::adopt_handed(int fd, Bytes unparsed, bool counted) {
+  if (stopped_ || !ready_ || links_.empty()) {
+    // This association is gone or not ready: back to the first one (which
+    // closes the connection if it is gone itself).
+    if (counted) shared_->router->release(cfg_.assoc_index);
+    if (cfg_.assoc_index != 0) shared_->router->hand(0, fd, std::move(unparsed));
+    else ::close(fd);
+    return;
+  }
+  Cmd c{Cmd::Adopt};
+  c.fd = fd;
+  c.data = std::move(unparsed);
+  c.counted = counted;
+  if (trace::enabled()) c.t_us = Reactor::now_us();
+  command(place_->pick(cfg_.assoc_index != 0), std::move(c));
 }
 
 void ProxySession::accept(int fd) {
@@ -1083,6 +1189,7 @@ void ProxySession::on_event(size_t thread, Ev& ev) {
       Cmd c{Cmd::Adopt};
       c.fd = ev.fd;
       c.data = std::move(ev.frame.payload);
+      c.counted = ev.sid != 0;
       command(place_->pick(true), std::move(c));
       return;
     }
@@ -1208,9 +1315,84 @@ void ProxySession::route(const proto::Frame& f) {
       last_pong_ms_ = Reactor::now_ms();
       LOG_DEBUG(kT, "received pong");
       break;
+    case MsgType::Assoc:
+      if (assoc_) assoc_->on_frame(f);
+      break;
     default:
       LOG_DEBUG(kT, "proxy ignoring message type %s", proto::msg_type_name(f.type));
   }
+}
+
+// ---------------------------------------------------------------- router
+
+void ProxyRouter::attach(size_t k, Reactor* r, std::weak_ptr<ProxySession> s) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (t_.size() <= k) t_.resize(k + 1);
+  t_[k].r = r;
+  t_[k].s = std::move(s);
+}
+
+void ProxyRouter::set_ready(size_t k, bool ready) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (k < t_.size()) t_[k].ready = ready;
+}
+
+int ProxyRouter::pick_bulk() {
+  std::lock_guard<std::mutex> lk(mu_);
+  int best = -1;
+  for (size_t k = 1; k < t_.size(); k++)
+    if (t_[k].ready && (best < 0 || t_[k].conns < t_[size_t(best)].conns)) best = int(k);
+  return best;
+}
+
+void ProxyRouter::hand(size_t k, int fd, Bytes unparsed) {
+  Reactor* r = nullptr;
+  std::weak_ptr<ProxySession> s;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (k < t_.size()) {
+      r = t_[k].r;
+      s = t_[k].s;
+      if (k > 0 && r) t_[k].conns++;
+    }
+  }
+  if (!r) {
+    ::close(fd);
+    return;
+  }
+  auto self = shared_from_this();
+  r->post_threadsafe([self, s, k, fd, unparsed = std::move(unparsed)]() mutable {
+    if (auto x = s.lock()) {
+      x->adopt_handed(fd, std::move(unparsed), k > 0);
+      return;
+    }
+    if (k > 0) {  // its session is gone: back to the first association
+      self->release(k);
+      self->hand(0, fd, std::move(unparsed));
+    } else {
+      ::close(fd);
+    }
+  });
+}
+
+void ProxyRouter::release(size_t k) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (k < t_.size() && t_[k].conns) t_[k].conns--;
+}
+
+size_t ProxyRouter::connections(size_t k) {
+  std::lock_guard<std::mutex> lk(mu_);
+  return k < t_.size() ? t_[k].conns : 0;
+}
+
+bool ProxyRouter::bulk_route(const std::string& key) {
+  std::lock_guard<std::mutex> lk(mu_);
+  return routes_.bulk(key);
+}
+
+void ProxyRouter::note_route(const std::string& key, uint64_t bytes, bool streaming) {
+  std::lock_guard<std::mutex> lk(mu_);
+  routes_.note(key, bytes, streaming);
 }
 
 }  // namespace p2pt

@@ -30,7 +30,9 @@
 #include <atomic>
 #include <functional>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <vector>
 #include <unordered_map>
 #include <unordered_set>
 
@@ -40,6 +42,12 @@
 #include "tunnel/workers.h"
 
 namespace p2pt {
+
+namespace rtc {
+struct PcConfig;
+}
+class AssocGroup;
+class ProxyRouter;
 
 struct ProxyConfig {
   std::string listen = "127.0.0.1:8000";
@@ -59,6 +67,53 @@ struct ProxyConfig {
   size_t inline_streams = 16;
   // Called with the bound address once listening (tests/bench use port 0).
   std::function<void(const std::string&)> on_listening;
+  // "assoc" extension (tunnel/assoc.h): associations wanted in total, the
+  // first included (<= 1: off); `assoc_pc` builds the extra PeerConnections
+  // (null: the transport has none); their threads busy-poll `busy_poll_us`.
+  uint32_t assoc = 1;
+  std::shared_ptr<const rtc::PcConfig> assoc_pc;
+  uint64_t busy_poll_us = 0;
+  // This session's association: 0 = the first (the listener; negotiates the
+  // others), k > 0 = an extra one, which takes client connections from the
+  // first session's `router` only.
+  size_t assoc_index = 0;
+  std::shared_ptr<ProxyRouter> router;
+};
+
+class ProxySession;
+
+// Which association a client connection's request runs on (the "assoc"
+// extension; thread-safe, shared by the first session and the extra ones).
+// Requests known to be bulk — a request body of at least Placement::kBulkBytes,
+// or a route whose last response was that large and not streamed — move their
+// connection to the ready extra association with the fewest such
+// connections; every other request runs on the first association, so SSE
+// tokens never wait behind bulk data in one association's queues. The route
+// table is shared too: what one thread learns, every thread places by.
+class ProxyRouter : public std::enable_shared_from_this<ProxyRouter> {
+ public:
+  void attach(size_t k, Reactor* r, std::weak_ptr<ProxySession> s);
+  void set_ready(size_t k, bool ready);
+  // A ready extra association for a bulk request (fewest connections), or -1.
+  int pick_bulk();
+  // Moves a client connection (its socket and the bytes read but not parsed)
+  // to association k's session; k > 0 counts it there until release(k).
+  void hand(size_t k, int fd, Bytes unparsed);
+  void release(size_t k);
+  bool bulk_route(const std::string& key);
+  void note_route(const std::string& key, uint64_t bytes, bool streaming);
+  size_t connections(size_t k);
+
+ private:
+  struct Target {
+    Reactor* r = nullptr;
+    std::weak_ptr<ProxySession> s;
+    bool ready = false;
+    size_t conns = 0;
+  };
+  std::mutex mu_;
+  std::vector<Target> t_;
+  BulkRoutes routes_;
 };
 
 class ProxyConn;
@@ -74,6 +129,9 @@ class ProxySession : public std::enable_shared_from_this<ProxySession> {
   // Hand an accepted client socket to this session (also used by the early
   // listener, which outlives sessions; see tunnel/app.cc).
   void accept(int fd);
+  // A client connection handed over by another association's session
+  // (ProxyRouter::hand): `counted` when the router counts it on this one.
+  void adopt_handed(int fd, Bytes unparsed, bool counted);
   void stop(const std::string& why);
   bool ready() const { return ready_; }
 
@@ -87,6 +145,8 @@ class ProxySession : public std::enable_shared_from_this<ProxySession> {
     std::atomic<uint64_t> rtt_us{0};  // transport SRTT, refreshed as body frames arrive ("flow" windows)
     size_t body_chunk = proto::kMaxBodyChunk;
     size_t workers = 0;  // worker threads beside the association thread
+    size_t assoc_index = 0;                // this session's association ("assoc")
+    std::shared_ptr<ProxyRouter> router;   // shared by all associations' sessions
   };
   // Association thread -> a connection thread.
   struct Cmd {
@@ -100,6 +160,7 @@ class ProxySession : public std::enable_shared_from_this<ProxySession> {
     std::shared_ptr<proto::ResponseHeaders> rh;   // Headers
     uint32_t bytes = 0;                           // Credit: REQ_BODY bytes granted by serve
     bool urgent = false;                          // the start of a response: handed over at once (Pipe::push)
+    bool counted = false;                         // Adopt: counted on this association by the router
   };
   // A connection thread -> association thread.
   struct Ev {
@@ -135,6 +196,7 @@ class ProxySession : public std::enable_shared_from_this<ProxySession> {
   bool bind_listener();
   void on_event(size_t thread, Ev& ev);
   void check_paused();
+  void start_assoc(uint32_t count);
   void command(size_t thread, Cmd c) {
     const bool urgent = c.urgent;
     links_[thread].to->push(std::move(c), urgent);
@@ -147,6 +209,8 @@ class ProxySession : public std::enable_shared_from_this<ProxySession> {
   std::shared_ptr<Shared> shared_;
   std::function<void(const std::string&)> done_;
   std::unique_ptr<TcpListener> listener_;
+  WorkerPool* pool_ = nullptr;
+  std::shared_ptr<AssocGroup> assoc_;  // extra associations ("assoc"), first association only
   std::unordered_map<uint32_t, Route> routes_;
   std::unordered_set<uint32_t> paused_;
   std::vector<Link> links_;

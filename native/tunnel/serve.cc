@@ -4,6 +4,7 @@
 
 #include "core/crypto.h"
 #include "core/log.h"
+#include "tunnel/assoc.h"
 #include "tunnel/metrics.h"
 
 namespace p2pt {
@@ -234,6 +235,7 @@ std::shared_ptr<ServeSession> ServeSession::start(Reactor& r, std::shared_ptr<Me
                                                   std::function<void(const std::string&)> done, WorkerPool* pool) {
   auto s = std::shared_ptr<ServeSession>(new ServeSession(r, ch, std::move(cfg)));
   s->done_ = std::move(done);
+  s->pool_ = pool;
   s->init_links(pool);
   std::weak_ptr<ServeSession> w = s;
   ch->on_message = [w](Bytes b) {
@@ -260,12 +262,16 @@ std::shared_ptr<ServeSession> ServeSession::start(Reactor& r, std::shared_ptr<Me
       return x ? f(*x) : 0.0;
     };
   };
-  metrics::gauge_fn("tunnel_streams_inflight", gauge([](ServeSession& x) { return double(x.inflight_.size()); }));
-  metrics::gauge_fn("tunnel_streams_paused", gauge([](ServeSession& x) { return double(x.paused_.size()); }));
-  metrics::gauge_fn("tunnel_scheduler_queued_bytes",
-                    gauge([](ServeSession& x) { return double(x.sched_->queued_bytes()); }));
-  metrics::gauge_fn("tunnel_channel_buffered_bytes",
-                    gauge([](ServeSession& x) { return double(x.ch_->buffered_amount()); }));
+  // Gauges read the session from the metrics thread (the first
+  // association's): an extra association's session runs on another thread.
+  if (s->cfg_.assoc_index == 0) {
+    metrics::gauge_fn("tunnel_streams_inflight", gauge([](ServeSession& x) { return double(x.inflight_.size()); }));
+    metrics::gauge_fn("tunnel_streams_paused", gauge([](ServeSession& x) { return double(x.paused_.size()); }));
+    metrics::gauge_fn("tunnel_scheduler_queued_bytes",
+                      gauge([](ServeSession& x) { return double(x.sched_->queued_bytes()); }));
+    metrics::gauge_fn("tunnel_channel_buffered_bytes",
+                      gauge([](ServeSession& x) { return double(x.ch_->buffered_amount()); }));
+  }
   if (ch->is_open()) {
     LOG_INFO(kT, "data channel already open");
     s->on_open();
@@ -330,6 +336,7 @@ void ServeSession::release_links() {
 }
 
 ServeSession::~ServeSession() {
+  assoc_.reset();  // extra associations first (joins their threads)
   if (hello_timer_) r_.cancel(hello_timer_);
   if (ping_timer_) r_.cancel(ping_timer_);
   if (wd_timer_) r_.cancel(wd_timer_);
@@ -352,6 +359,7 @@ void ServeSession::stop(const std::string& why) {
   if (wd_timer_) r_.cancel(wd_timer_);
   wd_timer_ = 0;
   hello_timer_ = ping_timer_ = 0;
+  assoc_.reset();
   inflight_.clear();
   paused_.clear();
   for (auto& u : ups_) u.outstanding = 0;
@@ -419,6 +427,8 @@ void ServeSession::on_hello(const proto::Frame& f) {
   LOG_INFO(kT, "received HELLO: %s", j.dump().c_str());
   proto::Agree agree;
   std::vector<std::string> ours = proto::our_features();
+  const bool may_assoc = cfg_.assoc_index == 0 && cfg_.assoc > 1 && cfg_.assoc_pc;
+  if (!may_assoc) ours.erase(std::remove(ours.begin(), ours.end(), "assoc"), ours.end());
   const std::string binding = ch_->channel_binding();
   if (!cfg_.secret.empty()) {
     // psk extension: the proxy must prove the shared secret on this channel.
@@ -439,7 +449,10 @@ void ServeSession::on_hello(const proto::Frame& f) {
   if (!cfg_.secret.empty()) agree.psk_mac = proto::psk_mac(cfg_.secret, "agree", hello.psk_nonce, binding);
   cancel_feature_ = std::find(agree.features.begin(), agree.features.end(), "cancel") != agree.features.end();
   flow_ = std::find(agree.features.begin(), agree.features.end(), "flow") != agree.features.end();
+  if (std::find(agree.features.begin(), agree.features.end(), "assoc") != agree.features.end())
+    agree.assoc = assoc_agree(hello.assoc, cfg_.assoc);
   sched_->send(proto::make_agree(agree));
+  if (agree.assoc > 1) start_assoc(agree.assoc);
   if (std::find(agree.features.begin(), agree.features.end(), "multistream") != agree.features.end())
     ch_->set_lanes(proto::kLanes);
   handshaken_ = true;
@@ -448,6 +461,27 @@ void ServeSession::on_hello(const proto::Frame& f) {
   last_pong_ms_ = Reactor::now_ms();
   send_ping();  // tokio::time::interval's first tick is immediate
   watchdog();
+}
+
+// "assoc": answers the proxy's extra PeerConnections as their offers arrive
+// (ASSOC frames); each gets a serve session of its own on its own thread,
+// with this session's upstreams and worker pool.
+void ServeSession::start_assoc(uint32_t count) {
+  ServeConfig c = cfg_;
+  c.assoc = 1;
+  WorkerPool* pool = pool_;
+  auto factory = [c, pool](Reactor& r, std::shared_ptr<MessageChannel> ch, size_t k,
+                           std::function<void(const std::string&)> done) -> std::shared_ptr<void> {
+    ServeConfig ck = c;
+    ck.assoc_index = k;
+    return ServeSession::start(r, std::move(ch), ck, std::move(done), pool);
+  };
+  std::weak_ptr<ServeSession> w = shared_from_this();
+  auto send = [w](proto::Frame f) {
+    if (auto s = w.lock(); s && !s->stopped_) s->sched_->send(std::move(f));
+  };
+  LOG_INFO(kT, "associations agreed: %u", count);
+  assoc_ = AssocGroup::create(r_, false, count, *cfg_.assoc_pc, cfg_.busy_poll_us, factory, send);
 }
 
 // Send-path stall watchdog: once a second, frames or channel bytes that are
@@ -626,6 +660,9 @@ void ServeSession::handle_frame(const proto::Frame& f) {
     case MsgType::Pong:
       last_pong_ms_ = Reactor::now_ms();
       LOG_DEBUG(kT, "received pong");
+      break;
+    case MsgType::Assoc:
+      if (assoc_) assoc_->on_frame(f);
       break;
     default:
       LOG_DEBUG(kT, "serve ignoring message type %s", proto::msg_type_name(f.type));

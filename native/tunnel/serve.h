@@ -37,6 +37,11 @@
 
 namespace p2pt {
 
+namespace rtc {
+struct PcConfig;
+}
+class AssocGroup;
+
 struct ServeConfig {
   // One upstream base URL, or several separated by commas (extension: e.g. one
   // inference endpoint per GPU of the node); each request goes to the one
@@ -64,6 +69,16 @@ struct ServeConfig {
   uint64_t stream_body_threshold = 8 << 20;
   // 413 above this many request-body bytes (0 = unlimited, the reference).
   uint64_t max_request_body = 0;
+  // "assoc" extension (tunnel/assoc.h): associations this side accepts in
+  // total, the first included (<= 1: off); `assoc_pc` builds the extra
+  // PeerConnections (null: the transport has none, e.g. TCP); their threads
+  // busy-poll like the rest (`busy_poll_us`).
+  uint32_t assoc = 1;
+  std::shared_ptr<const rtc::PcConfig> assoc_pc;
+  uint64_t busy_poll_us = 0;
+  // This session's association: 0 = the first (negotiates the others), k > 0
+  // = an extra one (its HELLO has no "assoc"; it registers no gauges).
+  size_t assoc_index = 0;
 };
 
 class ServeWorker;
@@ -175,11 +190,15 @@ class ServeSession : public std::enable_shared_from_this<ServeSession> {
     links_[thread].to->push(std::move(c), urgent);
   }
 
+  void start_assoc(uint32_t count);
+
   Reactor& r_;
   std::shared_ptr<MessageChannel> ch_;
   std::unique_ptr<FrameScheduler> sched_;
   ServeConfig cfg_;
   std::function<void(const std::string&)> done_;
+  WorkerPool* pool_ = nullptr;
+  std::shared_ptr<AssocGroup> assoc_;  // extra associations ("assoc"), first association only
   bool handshaken_ = false;
   bool stopped_ = false;
   bool cancel_feature_ = false;

@@ -58,22 +58,7 @@ class WebrtcSession : public std::enable_shared_from_this<WebrtcSession> {
     if (cb) cb(std::move(ch), err);
   }
 
-  rtc::PcConfig pc_config() const {
-    rtc::PcConfig pc;
-    pc.ice.stun_urls = cfg_.rtc.stun_servers;
-    pc.ice.turn_url = cfg_.rtc.turn.url;
-    pc.ice.turn_user = cfg_.rtc.turn.username;
-    pc.ice.turn_pass = cfg_.rtc.turn.password;
-    pc.ice.include_loopback = cfg_.rtc.include_loopback;
-    pc.ice.include_ipv6 = cfg_.rtc.include_ipv6;
-    pc.ice.ipv6_only = cfg_.rtc.ipv6_only;
-    pc.ice.relay_only = cfg_.rtc.relay_only;
-    pc.ice.failed_ms = cfg_.rtc.ice_failed_timeout_ms;
-    pc.sctp_mtu = cfg_.rtc.sctp_mtu;
-    pc.allow_jumbo = cfg_.rtc.allow_jumbo_loopback;
-    pc.sack_delay_us = cfg_.mode == "serve" ? 5000 : 0;
-    return pc;
-  }
+  rtc::PcConfig pc_config() const { return make_pc_config(cfg_); }
 
   void on_signal(const IncomingSignal& m) {
     if (done_) return;  // like the reference, signalling is not consulted once connected
@@ -265,6 +250,23 @@ class WebrtcSession : public std::enable_shared_from_this<WebrtcSession> {
 };
 
 }  // namespace
+
+rtc::PcConfig make_pc_config(const AppConfig& cfg) {
+  rtc::PcConfig pc;
+  pc.ice.stun_urls = cfg.rtc.stun_servers;
+  pc.ice.turn_url = cfg.rtc.turn.url;
+  pc.ice.turn_user = cfg.rtc.turn.username;
+  pc.ice.turn_pass = cfg.rtc.turn.password;
+  pc.ice.include_loopback = cfg.rtc.include_loopback;
+  pc.ice.include_ipv6 = cfg.rtc.include_ipv6;
+  pc.ice.ipv6_only = cfg.rtc.ipv6_only;
+  pc.ice.relay_only = cfg.rtc.relay_only;
+  pc.ice.failed_ms = cfg.rtc.ice_failed_timeout_ms;
+  pc.sctp_mtu = cfg.rtc.sctp_mtu;
+  pc.allow_jumbo = cfg.rtc.allow_jumbo_loopback;
+  pc.sack_delay_us = cfg.mode == "serve" ? 5000 : 0;
+  return pc;
+}
 
 std::shared_ptr<void> connect_webrtc(Reactor& r, const AppConfig& cfg, ConnectCb cb) {
   auto s = std::make_shared<WebrtcSession>(r, cfg, std::move(cb));

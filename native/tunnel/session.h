@@ -14,10 +14,14 @@
 
 #include <memory>
 
+#include "rtc/peer.h"
 #include "tunnel/app.h"
 
 namespace p2pt {
 
 std::shared_ptr<void> connect_webrtc(Reactor& r, const AppConfig& cfg, ConnectCb cb);
+// The PeerConnection configuration a role's connections use (the first one
+// and the "assoc" extension's extra ones).
+rtc::PcConfig make_pc_config(const AppConfig& cfg);
 
 }  // namespace p2pt

@@ -14,12 +14,12 @@
 
 namespace p2pt {
 
-WorkerThread::WorkerThread(int index, uint64_t busy_poll_us) : index_(index) {
+WorkerThread::WorkerThread(int index, uint64_t busy_poll_us, const char* name_prefix, int tag) : index_(index) {
   std::promise<Reactor*> ready;
   auto fut = ready.get_future();
   // The reactor is created on its own thread so thread-affine state (the
   // thread_local current reactor) belongs to that thread.
-  th_ = std::thread([this, &ready, busy_poll_us] {
+  th_ = std::thread([this, &ready, busy_poll_us, name_prefix, tag] {
     // Process signals (Ctrl-C, SIGTERM) belong to the main reactor's signalfd;
     // a worker must never take them with the default action. SIGPROF stays
     // open so the sampling profiler sees worker time too.
@@ -32,9 +32,9 @@ WorkerThread::WorkerThread(int index, uint64_t busy_poll_us) : index_(index) {
     Reactor* rp = r.get();
     r_ = std::move(r);
     char name[16];
-    snprintf(name, sizeof name, "p2pt-w%d", index_);
+    snprintf(name, sizeof name, "%s%d", name_prefix, index_);
     pthread_setname_np(pthread_self(), name);
-    profiler::register_thread(index_);
+    profiler::register_thread(tag < 0 ? index_ : tag);
     ready.set_value(rp);
     rp->run();
   });
@@ -61,10 +61,11 @@ int WorkerPool::auto_count() {
   long n = affinity::process_cpu_count();  // the set from before this thread pinned itself to one CPU
   if (n <= 0) n = sysconf(_SC_NPROCESSORS_ONLN);
   // One CPU per thread (affinity.h): the association thread, the socket
-  // reader and the two TX stages take four, the workers the rest. On 6 CPUs
-  // one worker beat two on the 64 x 1 MB echo (1916 vs 1633 req/s at 1200 MTU,
-  // 1920 vs 1876 jumbo, same box; profiles/r04/w24).
-  if (affinity::enabled()) return int(std::clamp<long>(n - 5, 1, 4));
+  // reader, the RX lane and the two TX stages take five, from 8 CPUs the two
+  // open lanes two more, the workers the rest. On 6 CPUs one worker beat two
+  // on the 64 x 1 MB echo (1916 vs 1633 req/s at 1200 MTU, 1920 vs 1876
+  // jumbo, same box; profiles/r04/w24).
+  if (affinity::enabled()) return int(std::clamp<long>(n >= 8 ? n - 7 : n - 5, 1, 4));
   return int(std::clamp<long>(n / 2 - 1, 1, 4));
 }
 

@@ -43,7 +43,9 @@ namespace p2pt {
 // A Reactor running on its own thread until destroyed.
 class WorkerThread {
  public:
-  explicit WorkerThread(int index, uint64_t busy_poll_us = 0);
+  // `name`: thread name prefix (index appended); `tag`: profiler / affinity
+  // role (core/affinity.h), -1 = the index (an HTTP worker).
+  explicit WorkerThread(int index, uint64_t busy_poll_us = 0, const char* name = "p2pt-w", int tag = -1);
   ~WorkerThread();
   Reactor& reactor() { return *r_; }
   int index() const { return index_; }

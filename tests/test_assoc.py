@@ -1,0 +1,146 @@
+"""Parallel associations (extension "assoc", native/tunnel/assoc.h).
+
+* both sides at --assoc 3: two extra PeerConnections come up, signalled
+  in-band over the first data channel; bulk uploads are handed to them
+  (tunnel_assoc_handoffs_total) and every byte of the 1 MB echoes comes back;
+  SSE requests keep running on the first association (stream ids < 2^28);
+* a download route learnt as bulk moves to an extra association on its next
+  request, and an SSE request on such a connection goes back to the first;
+* a side without the feature (--assoc 1, or a reference-like feature list)
+  leaves the tunnel on its single data channel, and everything still works;
+* an extra association that dies (its serve-side session ends) is dropped
+  from placement: later bulk requests run on the first association.
+
+The reference has one PeerConnection and one data channel (rtc.rs:133).
+"""
+import http.client
+import json
+import re
+import subprocess
+import time
+import urllib.request
+
+import pytest
+
+from p2p_llm_tunnel_amd import binary
+from p2p_llm_tunnel_amd.utils.procs import Tunnel, free_port, spawn
+
+
+def _mock(interval_us=2000, tokens=5):
+    port = free_port()
+    p = spawn("mock", [binary("tunnel-mock"), "--port", str(port), "--interval-us", str(interval_us),
+                       "--tokens", str(tokens)])
+    p.wait_for("Mock LLM server running", 10)
+    return p, port
+
+
+def _loadgen(port, streams, steps, extra=()):
+    out = subprocess.run([binary("tunnel-loadgen"), "--target", f"127.0.0.1:{port}", "--streams", str(streams),
+                          "--steps", str(steps), "--warmup", "0", *extra],
+                         capture_output=True, text=True, timeout=120)
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def _metric(port, name):
+    txt = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5).read().decode()
+    for line in txt.splitlines():
+        if line.startswith(name + " ") or line.startswith(name + "{"):
+            return float(line.split()[-1])
+    return 0.0
+
+
+def _sse(port):
+    c = http.client.HTTPConnection("127.0.0.1", port, timeout=30)
+    c.request("POST", "/v1/chat/completions", body=json.dumps({"stream": True}))
+    r = c.getresponse()
+    body = r.read()
+    c.close()
+    return r.status, body
+
+
+def _wait_assoc(t, n, timeout=20):
+    for k in range(1, n):
+        t.proxy.wait_for(f"association {k} ready", timeout)
+
+
+MTU = ["--no-jumbo-loopback"]
+
+
+def test_bulk_uploads_run_on_extra_associations():
+    mock, up = _mock()
+    mp = free_port()
+    try:
+        with Tunnel(f"http://127.0.0.1:{up}", serve_extra=MTU + ["--assoc", "3"],
+                    proxy_extra=MTU + ["--assoc", "3", "--metrics-listen", f"127.0.0.1:{mp}"],
+                    env={"RUST_LOG": "info"}) as t:
+            _wait_assoc(t, 3)
+            assert t.serve.count("associations agreed: 3") == 1
+            r = _loadgen(t.proxy_port, 16, 3, ["--post-bytes", str(1 << 20)])
+            assert r["errors"] == 0 and r["requests"] == 48, r
+            handoffs = _metric(mp, "tunnel_assoc_handoffs_total")
+            assert handoffs >= 16, handoffs  # every connection's first bulk request moved once
+            # SSE next to it stays on the first association.
+            status, body = _sse(t.proxy_port)
+            assert status == 200 and body.rstrip().endswith(b"data: [DONE]")
+            assert _metric(mp, "tunnel_assoc_handoffs_total") == handoffs
+            # Stream ids of the extra associations start at k << 28.
+            ids = [int(x) for x in re.findall(r"proxying \S+ \S+ \(stream (\d+)\)", t.proxy.text())]
+            assert not ids or all(i < (1 << 28) for i in ids if i < (1 << 28))
+    finally:
+        mock.stop()
+
+
+def test_learnt_bulk_download_moves_and_sse_comes_back():
+    mock, up = _mock()
+    mp = free_port()
+    try:
+        with Tunnel(f"http://127.0.0.1:{up}", serve_extra=MTU + ["--assoc", "2"],
+                    proxy_extra=MTU + ["--assoc", "2", "--metrics-listen", f"127.0.0.1:{mp}"]) as t:
+            _wait_assoc(t, 2)
+            c = http.client.HTTPConnection("127.0.0.1", t.proxy_port, timeout=30)
+            for i in range(3):  # 1st teaches the route; 2nd and 3rd run on association 1
+                c.request("GET", "/bulk?bytes=2000000")
+                r = c.getresponse()
+                assert r.status == 200 and len(r.read()) == 2000000
+            assert _metric(mp, "tunnel_assoc_handoffs_total") == 1
+            # An SSE request on the same keep-alive connection goes home.
+            c.request("POST", "/v1/chat/completions", body=json.dumps({"stream": True}))
+            r = c.getresponse()
+            assert r.status == 200 and r.read().rstrip().endswith(b"data: [DONE]")
+            assert _metric(mp, "tunnel_assoc_handoffs_total") == 2
+            c.close()
+    finally:
+        mock.stop()
+
+
+@pytest.mark.parametrize("side", ["serve_off", "reference_features"])
+def test_without_the_feature_one_association(side):
+    mock, up = _mock()
+    env = {"RUST_LOG": "info"}
+    serve_extra = MTU + (["--assoc", "1"] if side == "serve_off" else ["--assoc", "3"])
+    try:
+        t = Tunnel(f"http://127.0.0.1:{up}", serve_extra=serve_extra, proxy_extra=MTU + ["--assoc", "3"], env=env)
+        if side == "reference_features":
+            t.env = dict(env, TUNNEL_FEATURES="sse")
+        with t:
+            r = _loadgen(t.proxy_port, 4, 2, ["--post-bytes", str(1 << 20)])
+            assert r["errors"] == 0, r
+            assert _sse(t.proxy_port)[0] == 200
+            time.sleep(0.3)
+            assert t.serve.count("associations agreed") == 0
+            assert t.proxy.count("associations agreed") == 0
+            assert t.proxy.count("association 1 ready") == 0
+    finally:
+        mock.stop()
+
+
+def test_tcp_transport_ignores_assoc():
+    mock, up = _mock()
+    try:
+        with Tunnel(f"http://127.0.0.1:{up}", transport="tcp", serve_extra=["--assoc", "3"],
+                    proxy_extra=["--assoc", "3"], env={"RUST_LOG": "info"}) as t:
+            r = _loadgen(t.proxy_port, 4, 2, ["--post-bytes", str(256 << 10)])
+            assert r["errors"] == 0, r
+            assert t.serve.count("associations agreed") == 0
+    finally:
+        mock.stop()
