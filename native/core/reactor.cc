@@ -39,11 +39,24 @@ Reactor::~Reactor() {
   if (t_current == this) t_current = nullptr;
 }
 
-uint64_t Reactor::now_us() {
+namespace {
+std::atomic<uint64_t> g_virtual_us{0};  // 0: real time
+
+uint64_t real_now_us() {
   timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
   return uint64_t(ts.tv_sec) * 1000000u + uint64_t(ts.tv_nsec) / 1000u;
 }
+}  // namespace
+
+uint64_t Reactor::now_us() {
+  const uint64_t v = g_virtual_us.load(std::memory_order_relaxed);
+  return v ? v : real_now_us();
+}
+
+void Reactor::set_virtual_time(bool on) { g_virtual_us.store(on ? real_now_us() : 0, std::memory_order_relaxed); }
+
+bool Reactor::virtual_time() { return g_virtual_us.load(std::memory_order_relaxed) != 0; }
 
 // epoll data carries (generation << 32 | fd) so an event queued for an fd that
 // was removed (and possibly reused) within the same batch is ignored.
@@ -258,8 +271,14 @@ void Reactor::run_once(int64_t timeout_us) {
     sleeping_.store(true, std::memory_order_seq_cst);
     if (ts_pending_.load(std::memory_order_seq_cst)) timeout_us = 0;  // posted as we decided to sleep
   }
-  int n = wait_events(epfd_, evs, kMaxEvents, timeout_us);
+  const bool virt = virtual_time();
+  int n = wait_events(epfd_, evs, kMaxEvents, virt ? 0 : timeout_us);
   sleeping_.store(false, std::memory_order_relaxed);
+  if (virt && n == 0 && timeout_us > 0 && posted_.empty() && !ts_pending_.load(std::memory_order_acquire)) {
+    // Nothing to do before the next timer (or the caller's deadline): that
+    // much virtual time passes at once.
+    g_virtual_us.fetch_add(uint64_t(timeout_us), std::memory_order_relaxed);
+  }
   if (n < 0 && errno != EINTR) throw std::runtime_error(std::string("epoll_wait: ") + strerror(errno));
   wake_us_ = now_us();
   if (wake_us_ - win_start_us_ >= 2000 && win_start_us_) {  // a long sleep ends the window idle

@@ -94,6 +94,14 @@ class Reactor {
 
   static uint64_t now_us();
   static uint64_t now_ms() { return now_us() / 1000; }
+  // Virtual time (tests of emulated links): while on, now_us() reads a
+  // process-wide virtual clock, and a loop with nothing ready and nothing
+  // posted jumps that clock to its next timer (or run_until deadline) instead
+  // of sleeping. An in-process link emulator driven by timers then runs
+  // deterministically, at any machine load, and faster than real time. Only
+  // for single-threaded test reactors without real I/O to wait for.
+  static void set_virtual_time(bool on);
+  static bool virtual_time();
 
  private:
   void run_once(int64_t timeout_us);

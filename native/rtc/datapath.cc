@@ -329,9 +329,10 @@ void TxLaneState::send(SealedBatch& sb, int fd, const SockAddr& to) {
 // ------------------------------------------------------------------ RX reader
 
 RxReader::RxReader(int fd, const SockAddr& remote, std::shared_ptr<const RecordKeys> keys, Deliver deliver, uint64_t id,
-                   size_t slot, bool adaptive)
+                   size_t slot, bool adaptive, uint64_t idle_us, size_t idle_bytes)
     : fd_(fd), stop_fd_(eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC)), remote_(remote), keys_(std::move(keys)),
-      deliver_(std::move(deliver)), id_(id), slot_(slot), pool_(slot), adaptive_(adaptive), active_(!adaptive) {
+      deliver_(std::move(deliver)), id_(id), slot_(slot), pool_(slot), adaptive_(adaptive), idle_us_(idle_us),
+      idle_bytes_(idle_bytes), active_(!adaptive) {
   // One lane per CPU it can have: pinned on a set too small to give the open
   // lanes CPUs of their own (affinity::open_lane_count), a second lane would
   // only preempt the first.
@@ -489,8 +490,8 @@ void RxReader::run() {
     }
     if (adaptive_) {
       const uint64_t now = Reactor::now_us();
-      if (now - win_start >= kIdleUs) {
-        if (win_bytes < kIdleBytes) {
+      if (now - win_start >= idle_us_) {
+        if (win_bytes < idle_bytes_) {
           // Interactive again: pause, and give the socket back behind every
           // burst already delivered (the association thread reads on in order).
           active_.store(false, std::memory_order_release);
@@ -533,7 +534,7 @@ void RxReader::run() {
     // Adaptive: wake by the end of the window even when nothing arrives.
     int wait_ms = 100;
     if (adaptive_) {
-      const uint64_t end = win_start + kIdleUs, now = Reactor::now_us();
+      const uint64_t end = win_start + idle_us_, now = Reactor::now_us();
       wait_ms = now >= end ? 1 : int((end - now + 999) / 1000);
     }
     if (poll(pf, 2, wait_ms) <= 0 || (pf[1].revents & POLLIN)) continue;  // the loop head sees stop_ / the window

@@ -261,8 +261,9 @@ class RxReader {
   // datagram in a 64 KiB slot pinned ~50x its size per burst); a datagram
   // larger than the slot (a peer with larger packets) grows it to 64 KiB.
   // `adaptive`: start paused, run only between engage() and a handback.
+  // `idle_us` / `idle_bytes`: the adaptive reader's handback window.
   RxReader(int fd, const SockAddr& remote, std::shared_ptr<const RecordKeys> keys, Deliver deliver, uint64_t id = 0,
-           size_t slot = 65536, bool adaptive = false);
+           size_t slot = 65536, bool adaptive = false, uint64_t idle_us = kIdleUs, size_t idle_bytes = kIdleBytes);
   uint64_t id() const { return id_; }
   size_t slot() const { return slot_.load(std::memory_order_relaxed); }
   ~RxReader();  // stops and joins; bursts already delivered stay valid
@@ -308,6 +309,8 @@ class RxReader {
   std::atomic<size_t> slot_{65536};
   BufPool pool_{65536};
   bool adaptive_ = false;
+  uint64_t idle_us_ = kIdleUs;
+  size_t idle_bytes_ = kIdleBytes;
   std::atomic<bool> active_{true};
   std::mutex mu_;
   std::condition_variable cv_;

@@ -141,6 +141,9 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   // False when direct_target() does not hold.
   bool detach_reader(int* fd, int* si, SockAddr* remote);
   void reattach_reader(int si);
+  // Tests: the reactor's readable callback for socket `si`, as an event queued
+  // earlier in the same turn would run it (a detached socket is not read).
+  void readable_for_test(int si) { on_readable(si); }
   // The socket detach_reader() would hand over, without handing it over (a
   // reader that starts paused and engages only under bulk).
   bool reader_target(int* fd, int* si, SockAddr* remote) const;

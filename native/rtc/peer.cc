@@ -271,7 +271,7 @@ void PeerConnection::start_rx_reader() {
     r->post_threadsafe([w, sb] {
       if (auto s = w.lock()) s->on_rx_burst(*sb);
     });
-  }, ++rx_reader_ids_, rx_slot_bytes(), adaptive);
+  }, ++rx_reader_ids_, rx_slot_bytes(), adaptive, cfg_.rx_idle_us, cfg_.rx_idle_bytes);
   LOG_DEBUG(kT, "UDP socket reader %s for %s", adaptive ? "ready (engaged under bulk)" : "on", remote.str().c_str());
 }
 
@@ -281,8 +281,8 @@ void PeerConnection::start_rx_reader() {
 // overtake them.
 void PeerConnection::maybe_engage_rx_reader() {
   const uint64_t now = Reactor::now_us(), rx = ice_->rx_bytes();
-  if (rx - rx_win_bytes0_ < kEngageBytes) {
-    if (now - rx_win_start_us_ >= kEngageWindowUs) {
+  if (rx - rx_win_bytes0_ < cfg_.rx_engage_bytes) {
+    if (now - rx_win_start_us_ >= cfg_.rx_engage_window_us) {
       rx_win_start_us_ = now;
       rx_win_bytes0_ = rx;
     }

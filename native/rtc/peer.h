@@ -59,6 +59,16 @@ struct PcConfig {
   // profiles/r04/node14); below the load threshold nothing changes.
   int64_t coalesce_us = -1;
   double coalesce_load = -1;  // < 0: 0.5
+  // Adaptive socket reader (rtc/datapath.h RxReader): engaged once the
+  // association thread has read `rx_engage_bytes` within `rx_engage_window_us`
+  // (128 MB/s: bulk), handed back once it reads less than `rx_idle_bytes` in
+  // `rx_idle_us` (12.8 MB/s). Measured defaults (docs/ROUND5.md, item 1);
+  // tests lower them so sanitizer builds, several times slower, still cycle
+  // through engage and handback (native test rx_reader_engage_handback_cycles).
+  uint64_t rx_engage_window_us = 2000;
+  size_t rx_engage_bytes = 256 * 1024;
+  uint64_t rx_idle_us = RxReader::kIdleUs;
+  size_t rx_idle_bytes = RxReader::kIdleBytes;
 };
 
 class PeerConnection;
@@ -179,10 +189,8 @@ class PeerConnection : public std::enable_shared_from_this<PeerConnection> {
   bool closed_ = false;
   // The selected direct pair's socket read off this thread (rtc/datapath.h):
   // always (TUNNEL_RX_READER=1), or, adaptive, only while the receive rate
-  // is bulk-like: engaged once this thread has read kEngageBytes within
-  // kEngageWindowUs, until the reader hands the socket back.
-  static constexpr uint64_t kEngageWindowUs = 2000;
-  static constexpr uint64_t kEngageBytes = 256 * 1024;  // 128 MB/s
+  // is bulk-like: engaged once this thread has read cfg_.rx_engage_bytes
+  // within cfg_.rx_engage_window_us, until the reader hands the socket back.
   std::unique_ptr<RxReader> rx_reader_;
   int rx_reader_si_ = -1;
   uint64_t rx_reader_gen_ = 0;   // ICE path generation the reader was started for
