@@ -14,6 +14,7 @@
 #include "core/reactor.h"
 #include "http/http.h"
 #include "proto/frame.h"
+#include "tunnel/assoc.h"
 #include "tests/testing.h"
 #include "ws/ws.h"
 
@@ -217,6 +218,51 @@ TEST(frame_codec) {
   CHECK(d.type == proto::MsgType::ResBody && d.stream_id == 0xDEADBEEF && d.payload.str() == "abc");
   CHECK(!proto::decode(Bytes::copy("\x01\x00", 2), d, &err));
   CHECK_EQ(err, std::string("message too short: 2 bytes"));
+}
+
+// "assoc" negotiation (tunnel/assoc.h): the extra associations come up only
+// when both HELLO/AGREE list the feature and both counts exceed one; a
+// reference peer's HELLO (no "assoc", no count) and a side at --assoc 1 keep
+// the tunnel on its single data channel, and a HELLO without a count
+// serialises exactly as the reference's (no "assoc" member).
+TEST(assoc_negotiation_falls_back_to_one_channel) {
+  CHECK_EQ(assoc_agree(3, 3), 3u);
+  CHECK_EQ(assoc_agree(4, 2), 2u);
+  CHECK_EQ(assoc_agree(3, 1), 0u);   // serve side off
+  CHECK_EQ(assoc_agree(0, 3), 0u);   // reference HELLO: no count
+  CHECK_EQ(assoc_agree(64, 64), proto::kMaxAssoc);
+  proto::Hello ref;  // the reference's HELLO
+  CHECK(ref.to_json().dump().find("assoc") == std::string::npos);
+  proto::Hello h;
+  h.features = {"sse", "cancel", "flow", "multistream", "assoc"};
+  h.assoc = 3;
+  proto::Hello back;
+  std::string err;
+  CHECK(proto::Hello::from_json(h.to_json(), back, &err));
+  CHECK_EQ(back.assoc, 3u);
+  // A serve side whose features lack "assoc" (e.g. TUNNEL_FEATURES=sse)
+  // agrees without it; its AGREE carries no count.
+  proto::Agree a;
+  CHECK(proto::agree_from_hello(back, a, &err, {"sse", "cancel", "flow"}));
+  CHECK(std::find(a.features.begin(), a.features.end(), "assoc") == a.features.end());
+  CHECK(a.to_json().dump().find("assoc") == std::string::npos);
+  // Both list it: the count travels in AGREE.
+  CHECK(proto::agree_from_hello(back, a, &err, proto::our_features()));
+  CHECK(std::find(a.features.begin(), a.features.end(), "assoc") != a.features.end());
+  a.assoc = assoc_agree(back.assoc, 3);
+  proto::Agree ab;
+  CHECK(proto::Agree::from_json(a.to_json(), ab, &err));
+  CHECK_EQ(ab.assoc, 3u);
+  // ASSOC frames (type 15, stream = the association) decode; a malformed
+  // count is rejected.
+  proto::Frame f = make_assoc_frame(2, "offer", "sdp", "v=0");
+  proto::Frame d;
+  CHECK(proto::decode(f.encode(), d, &err));
+  CHECK(d.type == proto::MsgType::Assoc && d.stream_id == 2);
+  CHECK_EQ(d.payload.str(), std::string("{\"kind\":\"offer\",\"sdp\":\"v=0\"}"));
+  Json bad;
+  CHECK(Json::parse("{\"proto\":\"httptunnel\",\"min_version\":1,\"max_version\":1,\"features\":[],\"assoc\":-1}", bad, &err));
+  CHECK(!proto::Hello::from_json(bad, back, &err));
 }
 
 TEST(http_request_head) {

@@ -63,7 +63,10 @@ class ProxyWorker : public std::enable_shared_from_this<ProxyWorker> {
   // its socket to a worker: bulk I/O off the association thread), or the
   // index of the association to hand the connection to.
   static constexpr int kStay = -1, kWorker = -2;
-  int placement(bool bulk) const;
+  int placement(ProxyConn* c, bool bulk);
+  // Interactive requests in flight on the first association (router).
+  void interactive(int delta) { shared_->router->interactive(delta); }
+  bool first_association() const { return shared_->assoc_index == 0; }
   void migrate(ProxyConn* c, int fd, Bytes unparsed);
   void hand_off(ProxyConn* c, int fd, Bytes unparsed, size_t dest);
   bool bulk_route(const std::string& key) { return shared_->router->bulk_route(key); }
@@ -88,7 +91,10 @@ class ProxyWorker : public std::enable_shared_from_this<ProxyWorker> {
 class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
  public:
   ProxyConn(std::weak_ptr<ProxyWorker> s, std::shared_ptr<TcpConn> c) : sess_(std::move(s)), conn_(std::move(c)) {}
-  ~ProxyConn() { cancel_timer(); }
+  ~ProxyConn() {
+    cancel_timer();
+    end_interactive();
+  }
 
   // TUNNEL_TRACE: when the listener accepted this connection and when its
   // connection thread took it over, stamped under its first request's id.
@@ -318,7 +324,12 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
       std::string e2;
       const bool big_upload =
           http::request_body_mode(h, blen, &e2) == http::BodyDecoder::Mode::Length && blen >= Placement::kBulkBytes;
-      const int dest = sess->placement(big_upload || sess->bulk_route(BulkRoutes::key(h.method, h.target)));
+      const bool bulk = big_upload || sess->bulk_route(BulkRoutes::key(h.method, h.target));
+      const int dest = sess->placement(this, bulk);
+      if (dest == ProxyWorker::kStay && !bulk && sess->first_association() && !interactive_) {
+        interactive_ = true;  // keeps bulk off this association while it runs (ProxyRouter::pick_bulk)
+        sess->interactive(+1);
+      }
       if (dest != ProxyWorker::kStay) {
         int fd = conn_->release_fd();
         if (fd >= 0) {
@@ -548,8 +559,15 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
     conn_->close_after_flush();
   }
 
+  void end_interactive() {
+    if (!interactive_) return;
+    interactive_ = false;
+    if (auto sess = sess_.lock()) sess->interactive(-1);
+  }
+
   void response_done() {
     cancel_timer();
+    end_interactive();
     if (head_written_ && !req_.method.empty())
       if (auto sess = sess_.lock()) sess->note_route(BulkRoutes::key(req_.method, req_.target), body_sent_, res_streaming_);
     if (stream_registered_) {
@@ -615,6 +633,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
   void on_client_closed(const std::string& err) {
     auto keep = shared_from_this();
     cancel_timer();
+    end_interactive();
     auto sess = sess_.lock();
     if (stream_registered_ && sess) {
       LOG_DEBUG(kT, "HTTP client disconnected for stream %u%s%s", sid_, err.empty() ? "" : ": ", err.c_str());
@@ -694,7 +713,8 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
   uint64_t body_sent_ = 0;
   bool res_streaming_ = false;  // SSE / NDJSON response (never a bulk route)
   uint64_t timer_ = 0;
-  bool counted_ = false;  // the router counts this connection on its association
+  bool counted_ = false;      // the router counts this connection on its association
+  bool interactive_ = false;  // an interactive request of the first association in flight (router)
   friend class ProxyWorker;
 };
 
@@ -729,11 +749,23 @@ void ProxyWorker::migrate(ProxyConn* c, int fd, Bytes unparsed) {
   out_->push(std::move(ev));
 }
 
-int ProxyWorker::placement(bool bulk) const {
+int ProxyWorker::placement(ProxyConn* c, bool bulk) {
   const size_t own = shared_->assoc_index;
+  auto& rt = *shared_->router;
   if (bulk && own == 0) {
-    const int k = shared_->router->pick_bulk();
+    // The first association takes bulk too while no interactive request runs
+    // on it (a bulk-only load, e.g. the 64 x 1 MB echo, then uses every
+    // association); counted there like on the others.
+    const int k = rt.pick_bulk(c->counted_);
     if (k > 0) return k;
+    if (k == 0 && !c->counted_) {
+      rt.count(0);
+      c->counted_ = true;
+    }
+  }
+  if (!bulk && own == 0 && c->counted_) {  // an interactive request on a connection counted as bulk here
+    rt.release(0);
+    c->counted_ = false;
   }
   if (!bulk && own != 0) return 0;  // interactive traffic runs on the first association
   if (bulk && index_ == 0 && shared_->workers > 0) return kWorker;
@@ -1337,12 +1369,32 @@ void ProxyRouter::set_ready(size_t k, bool ready) {
   if (k < t_.size()) t_[k].ready = ready;
 }
 
-int ProxyRouter::pick_bulk() {
+int ProxyRouter::pick_bulk(bool counted_on_first) {
   std::lock_guard<std::mutex> lk(mu_);
   int best = -1;
   for (size_t k = 1; k < t_.size(); k++)
     if (t_[k].ready && (best < 0 || t_[k].conns < t_[size_t(best)].conns)) best = int(k);
+  if (best < 0) return -1;  // no extra association: placement as without the extension
+  // The first association is a candidate while no interactive request runs on
+  // it (ties go to an extra one; a connection already counted there stays
+  // unless another association has fewer).
+  if (!t_.empty() && t_[0].ready && t_[0].interactive == 0) {
+    const size_t c0 = t_[0].conns - (counted_on_first && t_[0].conns ? 1 : 0);
+    if (c0 < t_[size_t(best)].conns || (counted_on_first && c0 <= t_[size_t(best)].conns)) return 0;
+  }
   return best;
+}
+
+void ProxyRouter::count(size_t k) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (k < t_.size()) t_[k].conns++;
+}
+
+void ProxyRouter::interactive(int delta) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (t_.empty()) return;
+  if (delta > 0) t_[0].interactive += size_t(delta);
+  else t_[0].interactive -= std::min(t_[0].interactive, size_t(-delta));
 }
 
 void ProxyRouter::hand(size_t k, int fd, Bytes unparsed) {

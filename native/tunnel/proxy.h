@@ -94,8 +94,14 @@ class ProxyRouter : public std::enable_shared_from_this<ProxyRouter> {
  public:
   void attach(size_t k, Reactor* r, std::weak_ptr<ProxySession> s);
   void set_ready(size_t k, bool ready);
-  // A ready extra association for a bulk request (fewest connections), or -1.
-  int pick_bulk();
+  // The association for a bulk request: the ready one with the fewest bulk
+  // connections — the first association only while no interactive request
+  // runs on it — or -1 when no extra association is ready.
+  // `counted_on_first`: the asking connection is counted on the first one.
+  int pick_bulk(bool counted_on_first = false);
+  void count(size_t k);
+  // Interactive requests in flight on the first association (+1 / -1).
+  void interactive(int delta);
   // Moves a client connection (its socket and the bytes read but not parsed)
   // to association k's session; k > 0 counts it there until release(k).
   void hand(size_t k, int fd, Bytes unparsed);
@@ -110,6 +116,7 @@ class ProxyRouter : public std::enable_shared_from_this<ProxyRouter> {
     std::weak_ptr<ProxySession> s;
     bool ready = false;
     size_t conns = 0;
+    size_t interactive = 0;  // the first association's interactive requests in flight
   };
   std::mutex mu_;
   std::vector<Target> t_;
