@@ -15,6 +15,12 @@ time and Bernoulli loss (TUNNEL_FAULT rtt_ms / rate_mbps / loss). For each
 
     python bench/bench_wan.py [--rtts 20,50] [--losses 0,0.005,0.02]
 
+--relay puts the path in the native TURN relay instead (bin/relay_main.cc:
+serve relays through it, --ice-relay-only; the relay's forward link has the
+rate, a one-BDP drop-tail queue, RTT/2 of delay each way and the loss), the
+shared-bottleneck emulator of bench/bench_fairness.py. --policy keep runs the
+serve side with TUNNEL_SCTP_CC=beta=100 (random losses keep cwnd).
+
 --steady-mb N adds steady-state rows (run alone with --rtts ''): 4 downloads of
 N MB each at every (rate, RTT, loss, queue) of --steady-*, reporting goodput
 as a share of the bottleneck and the sending process's per-thread CPU.
@@ -140,6 +146,9 @@ def main():
     ap.add_argument("--steady-rtts", default="20,50")
     ap.add_argument("--steady-losses", default="0,0.005")
     ap.add_argument("--steady-queues", default="0", help="queue KB per steady row (0: one BDP), e.g. 0,16")
+    ap.add_argument("--relay", action="store_true", help="rows through the native TURN relay's emulated link")
+    ap.add_argument("--policy", choices=["default", "keep"], default="default",
+                    help="serve's congestion response: default, or keep (TUNNEL_SCTP_CC=beta=100)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     ensure_native()
@@ -149,7 +158,9 @@ def main():
     mock.wait_for("Mock LLM server running", 10)
     from p2p_llm_tunnel_amd.utils.boxinfo import identity
     res = {"box": identity(), "host": os.uname().nodename, "time": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
-           "mtu": 1200, "rate_mbps": a.rate_mbps, "extra": a.extra, "rows": [], "steady": []}
+           "mtu": 1200, "rate_mbps": a.rate_mbps, "extra": a.extra, "relay": a.relay, "policy": a.policy,
+           "rows": [], "steady": []}
+    policy_env = {"TUNNEL_SCTP_CC": "beta=100"} if a.policy == "keep" else {}
     extra = ["--no-jumbo-loopback"] + [x for x in a.extra.split() if x]
     try:
         if a.steady_mb:
@@ -165,12 +176,20 @@ def main():
         for rtt in [float(x) for x in a.rtts.split(",") if x]:
             for loss in [float(x) for x in a.losses.split(",") if x]:
                 qkb = a.queue_kb or max(64.0, a.rate_mbps * 1e6 / 8 * rtt / 1e3 / 1024)
-                env = {"TUNNEL_FAULT": f"rtt_ms={rtt},rate_mbps={a.rate_mbps},queue_kb={qkb},loss={loss}",
-                       "RUST_LOG": "warn,tunnel::rtc=info,tunnel::serve=info,tunnel::proxy=info"}
+                env = {"RUST_LOG": "warn,tunnel::rtc=info,tunnel::serve=info,tunnel::proxy=info", **policy_env}
+                relay, turn = None, []
+                if a.relay:
+                    sys.path.insert(0, os.path.join(ROOT, "bench"))
+                    from bench_fairness import NativeRelay
+                    relay = NativeRelay(a.rate_mbps, rtt / 2, qkb, loss)
+                    turn = ["--turn", relay.url, "--turn-user", "u", "--turn-pass", "p", "--ice-relay-only"]
+                else:
+                    env["TUNNEL_FAULT"] = f"rtt_ms={rtt},rate_mbps={a.rate_mbps},queue_kb={qkb},loss={loss}"
                 sm, pm = free_port(), free_port()
                 with Tunnel(f"http://127.0.0.1:{mport}", transport="webrtc",
-                            serve_extra=extra + ["--metrics-listen", f"127.0.0.1:{sm}"],
-                            proxy_extra=extra + ["--metrics-listen", f"127.0.0.1:{pm}"], env=env) as t:
+                            serve_extra=extra + turn + ["--metrics-listen", f"127.0.0.1:{sm}"],
+                            proxy_extra=extra + ["--metrics-listen", f"127.0.0.1:{pm}"], env=env,
+                            room=f"wan-{os.getpid()}-{time.time_ns()}") as t:
                     result(sse(t.proxy_port, 1))  # warm: connections, cwnd
                     alone = result(sse(t.proxy_port, a.sse_steps))
                     bulk = lg(t.proxy_port, "--streams", 4, "--steps", 1, "--warmup", 0, "--method", "GET",
@@ -190,7 +209,12 @@ def main():
                            "echo_MBps_each_way": echo["req_s"] * 1.048576,
                            "errors": alone["errors"] + mixed["errors"] + bulk_r["errors"] + echo["errors"],
                            "echo_wall_s": round(time.time() - t0, 2),
-                           "serve_sctp": scrape(sm), "proxy_sctp": scrape(pm)}
+                           "serve_sctp": scrape(sm), "proxy_sctp": scrape(pm),
+                           "path": t.serve.wait_for("WebRTC connection established", 1).split(" via ", 1)[-1]}
+                if relay:
+                    relay.stop()
+                    row["relay"] = relay.stats
+                if True:
                     res["rows"].append(row)
                     print(json.dumps(row), file=sys.stderr, flush=True)
     finally:

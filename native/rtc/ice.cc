@@ -1112,6 +1112,10 @@ void IceAgent::handle_response(const SockAddr& from, const stun::Message& m, con
     return;
   }
   (void)from;
+  if (pr.sent_us) {
+    const uint64_t rtt = std::max<uint64_t>(1, Reactor::now_us() - pr.sent_us);
+    if (!check_rtt_us_ || rtt < check_rtt_us_) check_rtt_us_ = rtt;
+  }
   pr.st = Pair::St::Succeeded;
   if (controlling_ && pr.use_cand) {
     if (sel_pair_ < 0) select_pair(pi);
@@ -1172,6 +1176,7 @@ void IceAgent::send_check(Pair& pr) {
   auto b = m.serialize(&remote_pwd_, true);
   if (!pr.tid.empty()) tx_pairs_.erase(pr.tid);
   pr.tid = m.tid_key();
+  pr.sent_us = Reactor::now_us();
   int pi = int(&pr - pairs_.data());
   tx_pairs_[pr.tid] = pi;
   send_raw(pr.local, rc.addr, b.data(), b.size());

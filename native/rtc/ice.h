@@ -150,6 +150,9 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   // Bytes this agent's own reads took off its sockets (cumulative): the
   // association thread's receive rate, which decides when a reader engages.
   uint64_t rx_bytes() const { return rx_bytes_; }
+  // Round-trip time of the connectivity checks (the smallest answered one;
+  // 0 = none yet): the path's RTT without any transport's ack delays.
+  uint64_t check_rtt_us() const { return check_rtt_us_; }
   // From that reader, on this agent's thread: a datagram it did not handle
   // (STUN, non-application records, other senders), and proof of life for
   // the ones it did (consent freshness).
@@ -197,6 +200,7 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
     uint64_t rto = 0;
     bool use_cand = false;
     bool nominate_on_success = false;
+    uint64_t sent_us = 0;  // when the check with `tid` went out
   };
 
   IceAgent(Reactor& r, IceConfig cfg, bool controlling);
@@ -250,6 +254,7 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   std::vector<Candidate> remotes_;
   std::vector<Pair> pairs_;
   std::map<std::string, int> tx_pairs_;  // STUN tid -> pair index
+  uint64_t check_rtt_us_ = 0;
   struct SrflxWindow {  // one STUN server's gathering window
     bool done = false;
     int outstanding = 0;

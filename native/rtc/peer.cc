@@ -108,6 +108,12 @@ uint64_t DataChannel::rtt_hint_us() const {
   return a ? a->min_rtt_us() : 0;
 }
 
+uint64_t DataChannel::path_rtt_us() const {
+  auto pc = pc_.lock();
+  const uint64_t ice = pc && pc->ice_ ? pc->ice_->check_rtt_us() : 0;
+  return ice ? ice : rtt_hint_us();
+}
+
 // On same-host jumbo paths (16 KiB SCTP packets) body frames are sized to one
 // DATA chunk: no fragmentation on send, no reassembly copy on receive, and
 // finer interleaving of streams. On network paths (~1200 B packets) the

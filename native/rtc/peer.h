@@ -86,6 +86,7 @@ class DataChannel : public MessageChannel, public std::enable_shared_from_this<D
   size_t body_chunk() const override;
   size_t send_window_hint() const override;
   uint64_t rtt_hint_us() const override;
+  uint64_t path_rtt_us() const override;
   std::string debug_state() const override;
   void set_lanes(int lanes) override { lanes_ = std::clamp(lanes, 0, kMaxLanes); }
   std::string channel_binding() const override;

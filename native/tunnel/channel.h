@@ -57,6 +57,9 @@ class MessageChannel {
   // 0 = unknown. "flow" receivers size their per-stream windows from it: the
   // path's bandwidth-delay product, not the queueing a bulk load adds.
   virtual uint64_t rtt_hint_us() const { return 0; }
+  // The path's round-trip time as its connectivity checks measured it (no
+  // transport ack delays in it); 0 = unknown. Falls back to rtt_hint_us().
+  virtual uint64_t path_rtt_us() const { return rtt_hint_us(); }
   // Transport state for the send-path stall watchdog (empty: nothing to add).
   virtual std::string debug_state() const { return ""; }
   // "multistream" extension: spread the frames of tunnel stream ids over

@@ -1084,7 +1084,17 @@ void ProxySession::on_agree(const proto::Frame& f) {
     if (!bind_listener()) return;
   }
   const bool agreed = std::find(agree.features.begin(), agree.features.end(), "assoc") != agree.features.end();
-  if (agreed && agree.assoc > 1 && cfg_.assoc > 1 && cfg_.assoc_pc) start_assoc(std::min(agree.assoc, cfg_.assoc));
+  if (agreed && agree.assoc > 1 && cfg_.assoc > 1 && cfg_.assoc_pc) {
+    // Only where one association's thread is the limit: a same-host or LAN
+    // path. On a WAN path the limit is the path (its RTT and loss), and
+    // parallel associations would only take N congestion windows' share of
+    // a shared bottleneck (bench/bench_fairness.py's criterion).
+    const uint64_t a = ch_->path_rtt_us(), b = ch_->rtt_hint_us();
+    const uint64_t rtt = a && b ? std::min(a, b) : a | b;
+    if (rtt && rtt <= kAssocMaxRttUs) start_assoc(std::min(agree.assoc, cfg_.assoc));
+    else LOG_INFO(kT, "extra associations not used: path RTT %.1f ms (> %.1f ms or unknown)", double(rtt) / 1e3,
+                  double(kAssocMaxRttUs) / 1e3);
+  }
 }
 
 // "assoc": offers the extra PeerConnections over this channel; each gets a

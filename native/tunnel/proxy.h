@@ -204,6 +204,10 @@ class ProxySession : public std::enable_shared_from_this<ProxySession> {
   void on_event(size_t thread, Ev& ev);
   void check_paused();
   void start_assoc(uint32_t count);
+  // "assoc": extra associations only on paths with a base RTT up to this
+  // (same host, LAN, metro). Early samples of a loopback path read 2-5 ms in
+  // a loaded build container (startup work on both loops), a WAN path tens.
+  static constexpr uint64_t kAssocMaxRttUs = 10000;
   void command(size_t thread, Cmd c) {
     const bool urgent = c.urgent;
     links_[thread].to->push(std::move(c), urgent);

@@ -23,21 +23,24 @@ _next_port = [0]
 
 
 def free_port(host: str = "127.0.0.1") -> int:
-    """A currently free TCP port. With P2PT_PORT_BASE set (bench.py sets a
-    disjoint block per rank), ports are taken in order from that block, so
-    ranks starting tunnels at the same instant never race for one the kernel
-    handed to both between our close() and the child's bind()."""
-    base = int(os.environ.get("P2PT_PORT_BASE", "0"))
-    if base:
-        for _ in range(500):
-            port = base + _next_port[0] % 500
-            _next_port[0] += 1
-            with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-                try:
-                    s.bind((host, port))
-                except OSError:
-                    continue
-                return port
+    """A currently free TCP port, taken in order from a block below the
+    kernel's ephemeral range (32768-60999 by default). A port from bind(0)
+    comes from that range, so an outgoing connection made between our close()
+    and the child's bind() (an upstream pre-warm, a load generator) could take
+    it: on the MI355X host a proxy's listen port was once held that way for a
+    whole bench run (profiles/r06/b03). P2PT_PORT_BASE picks the block (bench.py
+    sets a disjoint one per rank); by default it follows the pid, so
+    concurrent test processes rarely meet."""
+    base = int(os.environ.get("P2PT_PORT_BASE", "0")) or 10000 + (os.getpid() * 500) % 20000
+    for _ in range(500):
+        port = base + _next_port[0] % 500
+        _next_port[0] += 1
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+            try:
+                s.bind((host, port))
+            except OSError:
+                continue
+            return port
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind((host, 0))
         return s.getsockname()[1]

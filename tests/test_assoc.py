@@ -8,6 +8,7 @@
   moves off it;
 * a download route learnt as bulk moves to an extra association on its next
   request, and an SSE request on such a connection goes back to the first;
+* a WAN path (20 ms RTT) keeps the single association;
 * a side without the feature (--assoc 1, or a reference-like feature list)
   leaves the tunnel on its single data channel, and everything still works
   (native: assoc_negotiation_falls_back_to_one_channel).
@@ -162,5 +163,20 @@ def test_tcp_transport_ignores_assoc():
             r = _loadgen(t.proxy_port, 4, 2, ["--post-bytes", str(256 << 10)])
             assert r["errors"] == 0, r
             assert t.serve.count("associations agreed") == 0
+    finally:
+        mock.stop()
+
+
+def test_wan_path_keeps_one_association():
+    # 20 ms emulated RTT (TUNNEL_FAULT): the path, not a thread, is the limit,
+    # and parallel associations would take N windows' share of a bottleneck.
+    mock, up = _mock()
+    env = {"RUST_LOG": "info", "TUNNEL_FAULT": "rtt_ms=20"}
+    try:
+        with Tunnel(f"http://127.0.0.1:{up}", serve_extra=MTU + ["--assoc", "3"], proxy_extra=MTU + ["--assoc", "3"],
+                    env=env) as t:
+            t.proxy.wait_for("extra associations not used: path RTT", 10)
+            assert _sse(t.proxy_port)[0] == 200
+            assert t.proxy.count("association 1 ready") == 0
     finally:
         mock.stop()
