@@ -247,7 +247,7 @@ TEST(assoc_negotiation_falls_back_to_one_channel) {
   CHECK(std::find(a.features.begin(), a.features.end(), "assoc") == a.features.end());
   CHECK(a.to_json().dump().find("assoc") == std::string::npos);
   // Both list it: the count travels in AGREE.
-  CHECK(proto::agree_from_hello(back, a, &err, proto::our_features()));
+  CHECK(proto::agree_from_hello(back, a, &err, {"sse", "cancel", "flow", "multistream", "assoc"}));
   CHECK(std::find(a.features.begin(), a.features.end(), "assoc") != a.features.end());
   a.assoc = assoc_agree(back.assoc, 3);
   proto::Agree ab;

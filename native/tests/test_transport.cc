@@ -1014,6 +1014,12 @@ TEST(rx_reader_engage_handback_cycles) {
     CHECK(ans->set_remote_description(off->local_description(), &err));
     CHECK(off->set_remote_description(ans->local_description(), &err));
     CHECK(r.run_until([&] { return dc->is_open() && rdc && rdc->is_open(); }, 5000));
+    if (!ans->dtls() || !ans->dtls()->lanes_possible()) {  // TUNNEL_DTLS_RECORDS=evp|openssl: no socket reader
+      printf("  no socket reader on this record path: skipped\n");
+      off->close();
+      ans->close();
+      return;
+    }
     uint32_t seq = 0;
     auto send = [&](size_t n) {
       seq++;
