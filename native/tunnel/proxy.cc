@@ -64,8 +64,8 @@ class ProxyWorker : public std::enable_shared_from_this<ProxyWorker> {
   // index of the association to hand the connection to.
   static constexpr int kStay = -1, kWorker = -2;
   int placement(ProxyConn* c, bool bulk);
-  // Interactive requests in flight on the first association (router).
-  void interactive(int delta) { shared_->router->interactive(delta); }
+  // Interactive requests in flight on this association (router).
+  void interactive(int delta) { shared_->router->interactive(shared_->assoc_index, delta); }
   bool first_association() const { return shared_->assoc_index == 0; }
   void migrate(ProxyConn* c, int fd, Bytes unparsed);
   void hand_off(ProxyConn* c, int fd, Bytes unparsed, size_t dest);
@@ -326,8 +326,8 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
           http::request_body_mode(h, blen, &e2) == http::BodyDecoder::Mode::Length && blen >= Placement::kBulkBytes;
       const bool bulk = big_upload || sess->bulk_route(BulkRoutes::key(h.method, h.target));
       const int dest = sess->placement(this, bulk);
-      if (dest == ProxyWorker::kStay && !bulk && sess->first_association() && !interactive_) {
-        interactive_ = true;  // keeps bulk off this association while it runs (ProxyRouter::pick_bulk)
+      if (dest == ProxyWorker::kStay && !bulk && !interactive_) {
+        interactive_ = true;  // counted until it ends (ProxyRouter::pick_bulk, pick_interactive)
         sess->interactive(+1);
       }
       if (dest != ProxyWorker::kStay) {
@@ -714,7 +714,7 @@ class ProxyConn : public std::enable_shared_from_this<ProxyConn> {
   bool res_streaming_ = false;  // SSE / NDJSON response (never a bulk route)
   uint64_t timer_ = 0;
   bool counted_ = false;      // the router counts this connection on its association
-  bool interactive_ = false;  // an interactive request of the first association in flight (router)
+  bool interactive_ = false;  // an interactive request in flight, counted on this association (router)
   friend class ProxyWorker;
 };
 
@@ -767,8 +767,13 @@ int ProxyWorker::placement(ProxyConn* c, bool bulk) {
     rt.release(0);
     c->counted_ = false;
   }
-  if (!bulk && own != 0) return 0;  // interactive traffic runs on the first association
-  if (bulk && index_ == 0 && shared_->workers > 0) return kWorker;
+  if (!bulk) {
+    // Interactive traffic runs on the first association, spilling over to
+    // the others only under node-scale load (ProxyRouter::kSpill).
+    const int k = rt.pick_interactive(own);
+    return k >= 0 && size_t(k) != own ? k : kStay;
+  }
+  if (index_ == 0 && shared_->workers > 0) return kWorker;
   return kStay;
 }
 
@@ -1400,11 +1405,29 @@ void ProxyRouter::count(size_t k) {
   if (k < t_.size()) t_[k].conns++;
 }
 
-void ProxyRouter::interactive(int delta) {
+void ProxyRouter::interactive(size_t k, int delta) {
   std::lock_guard<std::mutex> lk(mu_);
-  if (t_.empty()) return;
-  if (delta > 0) t_[0].interactive += size_t(delta);
-  else t_[0].interactive -= std::min(t_[0].interactive, size_t(-delta));
+  if (k >= t_.size()) return;
+  if (delta > 0) t_[k].interactive += size_t(delta);
+  else t_[k].interactive -= std::min(t_[k].interactive, size_t(-delta));
+}
+
+int ProxyRouter::pick_interactive(size_t own) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (t_.empty()) return -1;
+  if (own != 0 && own < t_.size() && t_[own].ready) {
+    // A connection that spilled over stays until the first association is
+    // well below the threshold again (hysteresis: no move per request while
+    // the load hovers around it).
+    return t_[0].ready && t_[0].interactive < kSpill / 2 ? 0 : int(own);
+  }
+  if (t_[0].interactive < kSpill || t_.size() < 2) return t_[0].ready || own == 0 ? 0 : -1;
+  // Node-scale load: the ready association with the fewest interactive
+  // requests (the first keeps it on a tie: no move for nothing).
+  size_t best = 0;
+  for (size_t k = 1; k < t_.size(); k++)
+    if (t_[k].ready && t_[k].interactive < t_[best].interactive) best = k;
+  return int(best);
 }
 
 void ProxyRouter::hand(size_t k, int fd, Bytes unparsed) {

@@ -100,8 +100,15 @@ class ProxyRouter : public std::enable_shared_from_this<ProxyRouter> {
   // `counted_on_first`: the asking connection is counted on the first one.
   int pick_bulk(bool counted_on_first = false);
   void count(size_t k);
-  // Interactive requests in flight on the first association (+1 / -1).
-  void interactive(int delta);
+  // Interactive requests in flight on association k (+1 / -1).
+  void interactive(size_t k, int delta);
+  // The association for an interactive request of a connection on `own`:
+  // the first one, unless it already carries kSpill interactive requests —
+  // node-scale load, where one association thread per side saturates
+  // (profiles/r05/b11/nodeprof: ~90 % busy at 1024 streams) — then the
+  // ready one with the fewest. -1: no ready association.
+  int pick_interactive(size_t own);
+  static constexpr size_t kSpill = 32;
   // Moves a client connection (its socket and the bytes read but not parsed)
   // to association k's session; k > 0 counts it there until release(k).
   void hand(size_t k, int fd, Bytes unparsed);
@@ -116,7 +123,7 @@ class ProxyRouter : public std::enable_shared_from_this<ProxyRouter> {
     std::weak_ptr<ProxySession> s;
     bool ready = false;
     size_t conns = 0;
-    size_t interactive = 0;  // the first association's interactive requests in flight
+    size_t interactive = 0;  // interactive requests in flight
   };
   std::mutex mu_;
   std::vector<Target> t_;

@@ -8,6 +8,8 @@
   moves off it;
 * a download route learnt as bulk moves to an extra association on its next
   request, and an SSE request on such a connection goes back to the first;
+* more concurrent SSE streams than the spill threshold spread over the
+  associations;
 * a WAN path (20 ms RTT) keeps the single association;
 * a side without the feature (--assoc 1, or a reference-like feature list)
   leaves the tunnel on its single data channel, and everything still works
@@ -178,5 +180,26 @@ def test_wan_path_keeps_one_association():
             t.proxy.wait_for("extra associations not used: path RTT", 10)
             assert _sse(t.proxy_port)[0] == 200
             assert t.proxy.count("association 1 ready") == 0
+    finally:
+        mock.stop()
+
+
+def test_interactive_load_spills_over_at_node_scale():
+    # More concurrent SSE streams than ProxyRouter::kSpill (32): the first
+    # association keeps 32, the rest spread over the extra ones; every event
+    # of every stream arrives.
+    mock, up = _mock(interval_us=20000, tokens=5)
+    mp = free_port()
+    try:
+        with Tunnel(f"http://127.0.0.1:{up}", serve_extra=MTU + ["--assoc", "3"],
+                    proxy_extra=MTU + ["--assoc", "3", "--metrics-listen", f"127.0.0.1:{mp}"]) as t:
+            _wait_assoc(t, 3)
+            r = _loadgen(t.proxy_port, 64, 3)
+            assert r["errors"] == 0 and r["requests"] == 192, r
+            assert _metric(mp, "tunnel_assoc_handoffs_total") >= 16
+            # A lone stream afterwards runs on the first association again.
+            h0 = _metric(mp, "tunnel_assoc_handoffs_total")
+            assert _sse(t.proxy_port)[0] == 200
+            assert _metric(mp, "tunnel_assoc_handoffs_total") == h0
     finally:
         mock.stop()
