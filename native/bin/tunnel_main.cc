@@ -105,9 +105,9 @@ const std::vector<Opt>& ext_opts() {
        "HTTP worker threads beside the association thread (auto: half the usable CPUs less one, 1..4; 0: single thread)", Kind::U64OrAuto, Role::Both, 0, 256},
       {"inline-streams", "TUNNEL_INLINE_STREAMS", "16",
        "Concurrent streams handled on the association thread before new ones go to workers", Kind::U64},
-      {"assoc", "TUNNEL_ASSOC", "1",
-       "Parallel associations (PeerConnections, one thread each) when the peer agrees; bulk requests go to the extra "
-       "ones, everything else stays on the first (1 = the reference's single data channel)",
+      {"assoc", "TUNNEL_ASSOC", "3",
+       "Parallel associations (PeerConnections, one thread each) when the peer agrees and the path is short (<= 10 ms): "
+       "bulk requests spread over them, interactive ones stay on the first (1 = the reference's single data channel)",
        Kind::U64, Role::Both, 1, 8},
       {"max-request-body", "TUNNEL_MAX_REQUEST_BODY", "0",
        "serve: answer 413 to request bodies larger than this many bytes (0 = unlimited)", Kind::U64, Role::Serve},

@@ -182,6 +182,10 @@ void DataChannel::set_closed(const std::string& why) {
 
 // ---------------------------------------------------------------- PeerConnection
 
+void PeerConnection::gauge(const char* name, std::function<double()> fn) {
+  if (cfg_.gauges) metrics::gauge_fn(name, std::move(fn));
+}
+
 std::shared_ptr<PeerConnection> PeerConnection::create(Reactor& r, PcConfig cfg, bool offerer) {
   auto pc = std::shared_ptr<PeerConnection>(new PeerConnection(r, std::move(cfg), offerer));
   std::weak_ptr<PeerConnection> w = pc;
@@ -604,188 +608,188 @@ void PeerConnection::start_sctp() {
       }
     }
   };
-  metrics::gauge_fn("tunnel_sctp_cwnd_bytes", [w] {
+  gauge("tunnel_sctp_cwnd_bytes", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->cwnd()) : 0.0;
   });
-  metrics::gauge_fn("tunnel_sctp_srtt_us", [w] {
+  gauge("tunnel_sctp_srtt_us", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->srtt_us()) : 0.0;
   });
-  metrics::gauge_fn("tunnel_sctp_min_rtt_us", [w] {
+  gauge("tunnel_sctp_min_rtt_us", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->min_rtt_us()) : 0.0;
   });
-  metrics::gauge_fn("tunnel_sctp_round_min_rtt_us", [w] {
+  gauge("tunnel_sctp_round_min_rtt_us", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->last_round_min_rtt_us()) : 0.0;
   });
-  metrics::gauge_fn("tunnel_sctp_queue_cuts", [w] {
+  gauge("tunnel_sctp_queue_cuts", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().queue_cuts) : 0.0;
   });
-  metrics::gauge_fn("tunnel_sctp_retransmits", [w] {
+  gauge("tunnel_sctp_retransmits", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().retransmits) : 0.0;
   });
-  metrics::gauge_fn("tunnel_sctp_fast_retransmits", [w] {
+  gauge("tunnel_sctp_fast_retransmits", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().fast_retransmits) : 0.0;
   });
-  metrics::gauge_fn("tunnel_sctp_t3_expirations", [w] {
+  gauge("tunnel_sctp_t3_expirations", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().t3_expirations) : 0.0;
   });
-  metrics::gauge_fn("tunnel_sctp_rto_us", [w] {
+  gauge("tunnel_sctp_rto_us", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->rto_us()) : 0.0;
   });
-  metrics::gauge_fn("tunnel_wan_queue_drops", [w] {
+  gauge("tunnel_wan_queue_drops", [w] {
     auto s = w.lock();
     return s && s->ice_ ? double(s->ice_->wan_queue_drops_) : 0.0;
   });
-  metrics::gauge_fn("tunnel_sctp_packets_sent", [w] {
+  gauge("tunnel_sctp_packets_sent", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().packets_sent) : 0.0;
   });
-  metrics::gauge_fn("tunnel_sctp_dup_copies", [w] {
+  gauge("tunnel_sctp_dup_copies", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().dup_copies_sent) : 0.0;
   });
-  metrics::gauge_fn("tunnel_sctp_tlp_probes", [w] {
+  gauge("tunnel_sctp_tlp_probes", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().tlp_probes) : 0.0;
   });
-  metrics::gauge_fn("tunnel_sctp_rack_marks", [w] {
+  gauge("tunnel_sctp_rack_marks", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().rack_marks) : 0.0;
   });
-  metrics::gauge_fn("tunnel_sctp_spurious_undos", [w] {
+  gauge("tunnel_sctp_spurious_undos", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().spurious_undos) : 0.0;
   });
-  metrics::gauge_fn("tunnel_sctp_probe_ambiguous", [w] {
+  gauge("tunnel_sctp_probe_ambiguous", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().probe_ambiguous) : 0.0;
   });
-  metrics::gauge_fn("tunnel_sctp_dup_tsns_received", [w] {
+  gauge("tunnel_sctp_dup_tsns_received", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().dup_tsns) : 0.0;
   });
-  metrics::gauge_fn("tunnel_sctp_late_tsns_received", [w] {
+  gauge("tunnel_sctp_late_tsns_received", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().late_tsns) : 0.0;
   });
-  metrics::gauge_fn("tunnel_sctp_rwnd_drops", [w] {
+  gauge("tunnel_sctp_rwnd_drops", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().rwnd_drops) : 0.0;
   });
-  metrics::gauge_fn("tunnel_dtls_rx_dropped", [w] {
+  gauge("tunnel_dtls_rx_dropped", [w] {
     auto s = w.lock();
     return s && s->dtls_ ? double(s->dtls_->rx_dropped()) : 0.0;
   });
-  metrics::gauge_fn("tunnel_sctp_hystart_exits", [w] {
+  gauge("tunnel_sctp_hystart_exits", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().hystart_exits) : 0.0;
   });
-  metrics::gauge_fn("tunnel_sctp_random_loss_cuts", [w] {
+  gauge("tunnel_sctp_random_loss_cuts", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().random_loss_cuts) : 0.0;
   });
-  metrics::gauge_fn("tunnel_sctp_congestion_cuts", [w] {
+  gauge("tunnel_sctp_congestion_cuts", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().congestion_cuts) : 0.0;
   });
-  metrics::gauge_fn("tunnel_sctp_over_bdp_losses", [w] {
+  gauge("tunnel_sctp_over_bdp_losses", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().over_bdp_losses) : 0.0;
   });
-  metrics::gauge_fn("tunnel_sctp_random_loss_events", [w] {
+  gauge("tunnel_sctp_random_loss_events", [w] {
     auto s = w.lock();
     return s && s->sctp_ ? double(s->sctp_->stats().random_loss_events) : 0.0;
   });
-  metrics::gauge_fn("tunnel_dtls_lane_tx_batches", [w] {
+  gauge("tunnel_dtls_lane_tx_batches", [w] {
     auto s = w.lock();
     return s && s->dtls_ ? double(s->dtls_->lane_tx_batches()) : 0.0;
   });
-  metrics::gauge_fn("tunnel_dtls_inline_tx_batches", [w] {
+  gauge("tunnel_dtls_inline_tx_batches", [w] {
     auto s = w.lock();
     return s && s->dtls_ ? double(s->dtls_->inline_tx_batches()) : 0.0;
   });
-  metrics::gauge_fn("tunnel_dtls_lane_rx_batches", [w] {
+  gauge("tunnel_dtls_lane_rx_batches", [w] {
     auto s = w.lock();
     return s && s->dtls_ ? double(s->dtls_->lane_rx_batches()) : 0.0;
   });
-  metrics::gauge_fn("tunnel_dtls_lane_datagrams", [w] {
+  gauge("tunnel_dtls_lane_datagrams", [w] {
     auto s = w.lock();
     auto* st = s && s->dtls_ ? s->dtls_->tx_lane_state() : nullptr;
     return st ? double(st->datagrams.load()) : 0.0;
   });
-  metrics::gauge_fn("tunnel_udp_reader_datagrams", [w] {
+  gauge("tunnel_udp_reader_datagrams", [w] {
     auto s = w.lock();
     return s && s->rx_reader_ ? double(s->rx_reader_->datagrams.load()) : 0.0;
   });
-  metrics::gauge_fn("tunnel_udp_reader_bursts", [w] {
+  gauge("tunnel_udp_reader_bursts", [w] {
     auto s = w.lock();
     return s && s->rx_reader_ ? double(s->rx_reader_->bursts.load()) : 0.0;
   });
-  metrics::gauge_fn("tunnel_udp_reader_raw", [w] {
+  gauge("tunnel_udp_reader_raw", [w] {
     auto s = w.lock();
     return s && s->rx_reader_ ? double(s->rx_reader_->raw_datagrams.load()) : 0.0;
   });
-  metrics::gauge_fn("tunnel_udp_reader_waits", [w] {
+  gauge("tunnel_udp_reader_waits", [w] {
     auto s = w.lock();
     return s && s->rx_reader_ ? double(s->rx_reader_->waits.load()) : 0.0;
   });
-  metrics::gauge_fn("tunnel_udp_reader_truncated", [w] {
+  gauge("tunnel_udp_reader_truncated", [w] {
     auto s = w.lock();
     return s && s->rx_reader_ ? double(s->rx_reader_->truncated.load()) : 0.0;
   });
-  metrics::gauge_fn("tunnel_udp_reader_escapes", [w] {
+  gauge("tunnel_udp_reader_escapes", [w] {
     auto s = w.lock();
     return s && s->rx_reader_ ? double(s->rx_reader_->escapes.load()) : 0.0;
   });
-  metrics::gauge_fn("tunnel_dtls_lane_gso_msgs", [w] {
+  gauge("tunnel_dtls_lane_gso_msgs", [w] {
     auto s = w.lock();
     auto* st = s && s->dtls_ ? s->dtls_->tx_lane_state() : nullptr;
     return st ? double(st->gso_msgs.load()) : 0.0;
   });
-  metrics::gauge_fn("tunnel_dtls_lane_send_drops", [w] {
+  gauge("tunnel_dtls_lane_send_drops", [w] {
     auto s = w.lock();
     auto* st = s && s->dtls_ ? s->dtls_->tx_lane_state() : nullptr;
     return st ? double(st->send_drops.load()) : 0.0;
   });
-  metrics::gauge_fn("tunnel_udp_gso_sends", [w] {
+  gauge("tunnel_udp_gso_sends", [w] {
     auto s = w.lock();
     return s && s->ice_ ? double(s->ice_->gso_sends_) : 0.0;
   });
   // Loss the stack cannot see otherwise: datagrams the kernel dropped on a
   // full receive buffer (every ICE socket, the reader's included).
-  metrics::gauge_fn("tunnel_udp_rx_overflow_total", [w] {
+  gauge("tunnel_udp_rx_overflow_total", [w] {
     auto s = w.lock();
     if (!s || !s->ice_) return 0.0;
     const uint64_t meminfo = s->ice_->rx_overflow();
     const uint64_t cmsg = s->rx_reader_ ? s->rx_reader_->rxq_ovfl.load() : 0;
     return double(std::max(meminfo, cmsg));
   });
-  metrics::gauge_fn("tunnel_sctp_coalesced_flushes", [w] {
+  gauge("tunnel_sctp_coalesced_flushes", [w] {
     auto s = w.lock();
     return s ? double(s->coalesced_flushes_) : 0.0;
   });
-  metrics::gauge_fn("tunnel_udp_send_drops", [w] {
+  gauge("tunnel_udp_send_drops", [w] {
     auto s = w.lock();
     return s && s->ice_ ? double(s->ice_->send_drops_) : 0.0;
   });
-  metrics::gauge_fn("tunnel_udp_rcvbuf_bytes", [w] {
+  gauge("tunnel_udp_rcvbuf_bytes", [w] {
     auto s = w.lock();
     return s && s->ice_ ? double(s->ice_->rcvbuf_bytes()) : 0.0;
   });
-  metrics::gauge_fn("tunnel_dtls_lane_send_waits", [w] {
+  gauge("tunnel_dtls_lane_send_waits", [w] {
     auto s = w.lock();
     auto* st = s && s->dtls_ ? s->dtls_->tx_lane_state() : nullptr;
     return st ? double(st->send_waits.load()) : 0.0;
   });
-  metrics::gauge_fn("tunnel_udp_gro_batches", [w] {
+  gauge("tunnel_udp_gro_batches", [w] {
     auto s = w.lock();
     if (!s || !s->ice_) return 0.0;
     return double(s->ice_->gro_batches_ + (s->rx_reader_ ? s->rx_reader_->gro_batches.load() : 0));

@@ -69,6 +69,11 @@ struct PcConfig {
   size_t rx_engage_bytes = 256 * 1024;
   uint64_t rx_idle_us = RxReader::kIdleUs;
   size_t rx_idle_bytes = RxReader::kIdleBytes;
+  // Register this connection's transport gauges (tunnel_sctp_*, tunnel_udp_*)
+  // with the metrics endpoint. Off for the "assoc" extension's extra
+  // connections: the gauges are read from the metrics thread and name one
+  // association (the first), not the last one to start.
+  bool gauges = true;
 };
 
 class PeerConnection;
@@ -164,6 +169,7 @@ class PeerConnection : public std::enable_shared_from_this<PeerConnection> {
   void set_state(PcState s);
   void fail(const std::string& why);
   void flush();
+  void gauge(const char* name, std::function<double()> fn);
   void start_rx_reader();
   void on_rx_burst(RxReader::Burst& b);
 

@@ -224,6 +224,7 @@ AssocGroup::AssocGroup(Reactor& primary, bool offerer, uint32_t count, const rtc
                        SessionFactory factory, SendFn send, StateFn state)
     : primary_(primary), offerer_(offerer), pc_(std::make_unique<rtc::PcConfig>(pc)), factory_(std::move(factory)),
       send_(std::move(send)), state_(std::move(state)) {
+  pc_->gauges = false;  // the metrics endpoint's transport gauges stay the first association's
   const uint32_t n = std::min(count, proto::kMaxAssoc);
   for (uint32_t k = 1; k < n; k++)
     threads_.push_back(std::make_unique<WorkerThread>(int(k), busy_poll_us, "p2pt-assoc", 80 + int(k)));

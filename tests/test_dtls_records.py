@@ -48,9 +48,11 @@ def test_record_layer_interop(mock_upstream, case):
             if env and env.get("TUNNEL_DTLS_RECORDS") == "openssl":
                 assert armed[name] == []
             else:
-                assert len(armed[name]) == 1
+                # One per association (the first, and the "assoc" extension's
+                # extra ones the 2.5 MB echo may have used), all on the same path.
+                assert 1 <= len(armed[name]) <= 3, armed[name]
                 if env and env.get("TUNNEL_DTLS_RECORDS") == "evp":
-                    assert "EVP AES-GCM" in armed[name][0]
+                    assert all("EVP AES-GCM" in a for a in armed[name])
     finally:
         for p in (proxy, serve, signal):
             p.stop()

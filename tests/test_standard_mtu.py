@@ -14,6 +14,9 @@ import pytest
 from p2p_llm_tunnel_amd.utils.procs import Tunnel, free_port
 
 STD = ["--no-jumbo-loopback"]
+# One association: the transport gauges checked below are the first
+# association's, and with "assoc" the bulk echo would run on an extra one.
+ONE = ["--assoc", "1"]
 
 
 def _metrics(port):
@@ -26,8 +29,8 @@ def test_standard_mtu_bulk_and_sse(mock_upstream, offload):
     ms, mp = free_port(), free_port()
     env = None if offload else {"TUNNEL_UDP_OFFLOAD": "none"}
     with Tunnel(mock_upstream, transport="webrtc", env=env,
-                serve_extra=STD + ["--metrics-listen", f"127.0.0.1:{ms}"],
-                proxy_extra=STD + ["--metrics-listen", f"127.0.0.1:{mp}"]) as t:
+                serve_extra=STD + ONE + ["--metrics-listen", f"127.0.0.1:{ms}"],
+                proxy_extra=STD + ONE + ["--metrics-listen", f"127.0.0.1:{mp}"]) as t:
         assert "mtu=1200" in t.serve.wait_for("connection established", 5)
         c = http.client.HTTPConnection("127.0.0.1", t.proxy_port, timeout=60)
         body = bytes((i * 7 + 3) & 0xFF for i in range(3 * 1024 * 1024 + 17))

@@ -64,7 +64,9 @@ def test_tunnel_through_turn_relay(mock_upstream, transport, request):
             r = c.getresponse()
             assert r.read().count(b"data: ") == 7
             assert "relay:" in t.serve.text() and "TURN server configured" in t.serve.text()
-            assert t.serve.count("TURN allocation: relayed") == 1
+            # One allocation per association (the first, plus the "assoc"
+            # extension's extra ones on this short path), each relayed.
+            assert 1 <= t.serve.count("TURN allocation: relayed") <= 3
         assert turn.stats["allocations"] >= 2
         assert turn.stats["relayed_to_peer"] > 50 and turn.stats["relayed_to_client"] > 50
         assert turn.stats["channel_binds"] >= 2

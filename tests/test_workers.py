@@ -165,8 +165,9 @@ def test_bulk_uploads_leave_the_association_thread():
     ms, ports = _mocks(1)
     try:
         with Tunnel(f"http://127.0.0.1:{ports[0]}", transport="webrtc",
-                    serve_extra=["--workers", "2", "--metrics-listen", f"127.0.0.1:{(mp := free_port())}"],
-                    proxy_extra=["--workers", "2", "--metrics-listen", f"127.0.0.1:{(pp := free_port())}"]) as t:
+                    serve_extra=["--workers", "2", "--assoc", "1", "--metrics-listen", f"127.0.0.1:{(mp := free_port())}"],
+                    proxy_extra=["--workers", "2", "--assoc", "1", "--metrics-listen",
+                                 f"127.0.0.1:{(pp := free_port())}"]) as t:
             import hashlib
             import urllib.request
             body = bytes(range(256)) * 4096  # 1 MiB
