@@ -57,7 +57,10 @@ def parse():
                     help="timed steps (and warm-up) of each extra curve point; default: the headline's --steps / --warmup, "
                          "so every point and its direct leg compare samples of the headline's size")
     ap.add_argument("--transport", default=os.environ.get("BENCH_TRANSPORT", "webrtc"))
-    ap.add_argument("--mock", choices=["native", "python"], default="native")
+    ap.add_argument("--mock", choices=["native", "python", "reference"], default="native",
+                    help="native: tunnel-mock; python: utils/mock_llm.py threaded; reference: utils/mock_llm.py "
+                         "single-threaded, as the reference's tmp/mock_llm.py:97 (one response at a time, ~2 req/s "
+                         "at 5 x 100 ms tokens, whatever the tunnel)")
     ap.add_argument("--interval-ms", type=float, default=100.0)
     ap.add_argument("--tokens", type=int, default=5)
     ap.add_argument("--topology", choices=["node", "independent"], default="node",
@@ -116,8 +119,9 @@ def start_mock(kind, interval_ms, tokens, cpus=None, threads=1):
         p = spawn("mock", pin + [binary("tunnel-mock"), "--port", str(port), "--interval-ms", str(int(interval_ms)),
                                  "--tokens", str(tokens), "--threads", str(threads)])
     else:
-        p = spawn("mock", [sys.executable, "-m", "p2p_llm_tunnel_amd.utils.mock_llm", "--port", str(port),
-                           "--threaded", "--interval-ms", str(interval_ms), "--tokens", str(tokens)])
+        threaded = ["--threaded"] if kind == "python" else []  # "reference": single-threaded TCPServer
+        p = spawn("mock", [sys.executable, "-m", "p2p_llm_tunnel_amd.utils.mock_llm", "--port", str(port)] + threaded +
+                  ["--interval-ms", str(interval_ms), "--tokens", str(tokens)])
     p.wait_for("Mock LLM server running", 30)
     return p, port
 

@@ -556,9 +556,12 @@ void RxReader::run() {
       }
       const int n = recvmmsg(fd_.fd, msgs, kBatch, MSG_DONTWAIT, nullptr);
       if (n <= 0) break;
-      if (round == 0 && traced) {
-        burst->t_read = Reactor::now_us();
-        burst->t_kernel = trace::kernel_rx_us(&msgs[0].msg_hdr);
+      if (traced) {
+        // A burst's frames are stamped with its latest datagram's kernel time
+        // (the first datagram's made a frame from a later one read as queued
+        // before it was sent); the read time is the first read's.
+        if (round == 0) burst->t_read = Reactor::now_us();
+        for (int i = 0; i < n; i++) burst->t_kernel = std::max(burst->t_kernel, trace::kernel_rx_us(&msgs[i].msg_hdr));
       }
       for (int i = 0; i < n; i++) {
         SockAddr a;

@@ -851,11 +851,13 @@ void IceAgent::on_readable(int si) {
     }
     int n = recvmmsg(socks_[si].fd, msgs, kBatch, MSG_DONTWAIT, nullptr);
     if (n <= 0) break;
-    if (round == 0 && trace::enabled()) {
-      const uint64_t now = Reactor::now_us();
-      trace::set_rx(trace::kernel_rx_us(&msgs[0].msg_hdr), now, now);
-    }
+    const bool traced = trace::enabled();
+    const uint64_t t_read = traced ? Reactor::now_us() : 0;
     for (int i = 0; i < n && !closed_; i++) {
+      // Each datagram's own kernel receive time (the batch's first one made a
+      // frame from a later datagram read as queued before it was sent:
+      // req_end -> udp_kernel < 0 in the hop tables).
+      if (traced) trace::set_rx(trace::kernel_rx_us(&msgs[i].msg_hdr), t_read, t_read);
       if (nat_mode_) {  // private address: unreachable from outside the emulated NAT
         nat_dropped_++;
         continue;
