@@ -190,13 +190,19 @@ def main():
                             serve_extra=extra + turn + ["--metrics-listen", f"127.0.0.1:{sm}"],
                             proxy_extra=extra + ["--metrics-listen", f"127.0.0.1:{pm}"], env=env,
                             room=f"wan-{os.getpid()}-{time.time_ns()}") as t:
+                    def progress(what):  # one line per phase: a long lossy row is not silent
+                        print(json.dumps({"rtt_ms": rtt, "loss": loss, "phase": what}), file=sys.stderr, flush=True)
+                    progress("warm")
                     result(sse(t.proxy_port, 1))  # warm: connections, cwnd
+                    progress("sse")
                     alone = result(sse(t.proxy_port, a.sse_steps))
+                    progress("sse+bulk")
                     bulk = lg(t.proxy_port, "--streams", 4, "--steps", 1, "--warmup", 0, "--method", "GET",
                               "--path", f"/bulk?bytes={a.bulk_mb << 20}", "--events", "none")
                     time.sleep(0.5)
                     mixed = result(sse(t.proxy_port, a.sse_steps))
                     bulk_r = result(bulk)
+                    progress("echo")
                     t0 = time.time()
                     echo = result(lg(t.proxy_port, "--streams", 8, "--steps", a.echo_steps, "--warmup", 0,
                                      "--post-bytes", 1 << 20))
@@ -214,8 +220,10 @@ def main():
                 if relay:
                     relay.stop()
                     row["relay"] = relay.stats
-                if True:
-                    res["rows"].append(row)
+                res["rows"].append(row)
+                if a.out:  # the rows so far, in case a later one never ends
+                    with open(a.out, "w") as f:
+                        f.write(json.dumps(res, indent=1) + "\n")
                     print(json.dumps(row), file=sys.stderr, flush=True)
     finally:
         mock.stop()

@@ -262,7 +262,7 @@ void Reactor::run_once(int64_t timeout_us) {
   // polling loop look half busy).
   if (wake_us_ && !idle_turn_) win_busy_us_ += t_wait - wake_us_;
   if (t_wait - win_start_us_ >= 2000) {
-    load_ = win_start_us_ ? double(win_busy_us_) / double(t_wait - win_start_us_) : 0.0;
+    load_.store(win_start_us_ ? double(win_busy_us_) / double(t_wait - win_start_us_) : 0.0, std::memory_order_relaxed);
     win_start_us_ = t_wait;
     win_busy_us_ = 0;
   }
@@ -282,7 +282,7 @@ void Reactor::run_once(int64_t timeout_us) {
   if (n < 0 && errno != EINTR) throw std::runtime_error(std::string("epoll_wait: ") + strerror(errno));
   wake_us_ = now_us();
   if (wake_us_ - win_start_us_ >= 2000 && win_start_us_) {  // a long sleep ends the window idle
-    load_ = double(win_busy_us_) / double(wake_us_ - win_start_us_);
+    load_.store(double(win_busy_us_) / double(wake_us_ - win_start_us_), std::memory_order_relaxed);
     win_start_us_ = wake_us_;
     win_busy_us_ = 0;
   }

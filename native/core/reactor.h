@@ -72,7 +72,7 @@ class Reactor {
   // Below half busy over the last load window: latency shortcuts (early
   // flushes, urgent hand-offs, busy polling) pay for themselves.
   static constexpr double kLightLoad = 0.5;
-  bool lightly_loaded() const { return load_ < kLightLoad; }
+  bool lightly_loaded() const { return load() < kLightLoad; }
   bool flushing_soon() const { return soon_active_; }
 
   // SIGINT/SIGTERM etc. delivered via signalfd on the loop thread.
@@ -90,7 +90,8 @@ class Reactor {
   void set_busy_poll_us(uint64_t us) { busy_poll_us_ = us; }
   // Share of wall time this loop spent outside epoll_wait over the last
   // window of >= 2 ms (0..1): lets a transport move work off a saturated loop.
-  double load() const { return load_; }
+  // Any thread may read it (the "assoc" router compares associations' loops).
+  double load() const { return load_.load(std::memory_order_relaxed); }
 
   static uint64_t now_us();
   static uint64_t now_ms() { return now_us() / 1000; }
@@ -136,7 +137,7 @@ class Reactor {
   // that matters, dense traffic sleeps between events as without polling.
   static constexpr uint64_t kSpinWindowUs = 10000, kSpinBudgetUs = 1000;
   uint64_t spin_win_start_us_ = 0, spin_win_used_us_ = 0;
-  double load_ = 0.0;
+  std::atomic<double> load_{0.0};
   uint64_t gen_ = 1;
   std::unordered_map<int, FdEntry> fds_;
   std::multimap<uint64_t, TimerId> timer_order_;

@@ -15,6 +15,7 @@
 #include "http/http.h"
 #include "proto/frame.h"
 #include "tunnel/assoc.h"
+#include "tunnel/proxy.h"
 #include "tests/testing.h"
 #include "ws/ws.h"
 
@@ -263,6 +264,62 @@ TEST(assoc_negotiation_falls_back_to_one_channel) {
   Json bad;
   CHECK(Json::parse("{\"proto\":\"httptunnel\",\"min_version\":1,\"max_version\":1,\"features\":[],\"assoc\":-1}", bad, &err));
   CHECK(!proto::Hello::from_json(bad, back, &err));
+}
+
+// ProxyRouter placement ("assoc"): bulk goes to the association with the
+// fewest bulk connections, the first only while nothing interactive runs on
+// it; interactive requests stay on the first unless it carries kSpill of them
+// and its thread is busy, then they spill to an extra association whose
+// thread has idle time — never when every thread is busy (a CPU-bound
+// process); a spilled connection goes home once the first is well below the
+// threshold.
+TEST(assoc_router_placement) {
+  Reactor r0, r1, r2;
+  auto rt = std::make_shared<ProxyRouter>();
+  double load[3] = {0, 0, 0};
+  rt->set_load_fn([&](size_t k) { return load[k]; });
+  CHECK_EQ(rt->pick_bulk(), -1);  // no extra association yet
+  rt->attach(0, &r0, {});
+  rt->attach(1, &r1, {});
+  rt->attach(2, &r2, {});
+  rt->set_ready(0, true);
+  CHECK_EQ(rt->pick_bulk(), -1);  // extras not ready
+  rt->set_ready(1, true);
+  rt->set_ready(2, true);
+  // Bulk: ties go to an extra one; the first takes its share while idle.
+  CHECK_EQ(rt->pick_bulk(), 1);
+  rt->count(1);
+  CHECK_EQ(rt->pick_bulk(), 2);
+  rt->count(2);
+  CHECK_EQ(rt->pick_bulk(), 0);
+  rt->count(0);
+  CHECK_EQ(rt->pick_bulk(true), 0);  // a connection counted on the first stays (no fewer elsewhere)
+  rt->interactive(0, +1);            // SSE on the first: bulk moves off it
+  CHECK_EQ(rt->pick_bulk(true), 1);
+  rt->interactive(0, -1);
+  rt->release(0);
+  rt->release(1);
+  rt->release(2);
+  // Interactive: the first, until it carries kSpill with a busy thread.
+  for (size_t i = 0; i < ProxyRouter::kSpill; i++) rt->interactive(0, +1);
+  CHECK_EQ(rt->pick_interactive(0), 0);  // its thread is idle
+  load[0] = 0.9;
+  CHECK_EQ(rt->pick_interactive(0), 1);  // spill to an idle extra one
+  rt->interactive(1, +1);
+  CHECK_EQ(rt->pick_interactive(0), 2);  // the one with fewer
+  load[1] = load[2] = 0.9;
+  CHECK_EQ(rt->pick_interactive(0), 0);  // every thread busy: stay
+  CHECK_EQ(rt->pick_interactive(1), 1);  // a spilled connection stays ...
+  for (size_t i = 0; i < ProxyRouter::kSpill; i++) rt->interactive(0, -1);
+  CHECK_EQ(rt->pick_interactive(1), 0);  // ... until the first is well below the threshold
+  rt->set_ready(1, false);
+  CHECK_EQ(rt->pick_interactive(1), 0);  // its association went away: home
+  // Route table shared by every thread.
+  CHECK(!rt->bulk_route("GET /bulk"));
+  rt->note_route("GET /bulk", 1 << 20, false);
+  CHECK(rt->bulk_route("GET /bulk"));
+  rt->note_route("GET /bulk", 1 << 20, true);  // streamed: never bulk
+  CHECK(!rt->bulk_route("GET /bulk"));
 }
 
 TEST(http_request_head) {

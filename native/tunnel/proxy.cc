@@ -1421,13 +1421,20 @@ int ProxyRouter::pick_interactive(size_t own) {
     // the load hovers around it).
     return t_[0].ready && t_[0].interactive < kSpill / 2 ? 0 : int(own);
   }
-  if (t_[0].interactive < kSpill || t_.size() < 2) return t_[0].ready || own == 0 ? 0 : -1;
-  // Node-scale load: the ready association with the fewest interactive
-  // requests (the first keeps it on a tie: no move for nothing).
-  size_t best = 0;
+  if (t_[0].interactive < kSpill || t_.size() < 2 || load(0) < kSpillLoad) return t_[0].ready || own == 0 ? 0 : -1;
+  // Node-scale load on a busy first association thread: the ready extra
+  // association with the fewest interactive requests whose thread still has
+  // idle time. When every thread is busy (a CPU-bound process: 1024 streams
+  // on the pool box's 16-CPU quota), spreading only adds per-association
+  // overhead — smaller batches, more packets and SACKs per token (node row,
+  // 1024 streams: events 0.96 -> 0.85 of direct, profiles/r06/b04) — so the
+  // request stays on the first.
+  int best = 0;
   for (size_t k = 1; k < t_.size(); k++)
-    if (t_[k].ready && t_[k].interactive < t_[best].interactive) best = k;
-  return int(best);
+    if (t_[k].ready && load(k) < kSpillLoad &&
+        (best == 0 || t_[k].interactive < t_[size_t(best)].interactive))
+      best = int(k);
+  return best;
 }
 
 void ProxyRouter::hand(size_t k, int fd, Bytes unparsed) {
@@ -1458,6 +1465,11 @@ void ProxyRouter::hand(size_t k, int fd, Bytes unparsed) {
       ::close(fd);
     }
   });
+}
+
+double ProxyRouter::load(size_t k) const {
+  if (load_fn_) return load_fn_(k);
+  return k < t_.size() && t_[k].r ? t_[k].r->load() : 1.0;
 }
 
 void ProxyRouter::release(size_t k) {

@@ -103,16 +103,20 @@ class ProxyRouter : public std::enable_shared_from_this<ProxyRouter> {
   // Interactive requests in flight on association k (+1 / -1).
   void interactive(size_t k, int delta);
   // The association for an interactive request of a connection on `own`:
-  // the first one, unless it already carries kSpill interactive requests —
-  // node-scale load, where one association thread per side saturates
-  // (profiles/r05/b11/nodeprof: ~90 % busy at 1024 streams) — then the
-  // ready one with the fewest. -1: no ready association.
+  // the first one, unless it already carries kSpill interactive requests and
+  // its thread is at least kSpillLoad busy — node-scale load (one association
+  // thread per side ~90 % busy at 1024 streams, profiles/r05/b11/nodeprof) —
+  // then the extra one with the fewest whose thread is below kSpillLoad.
+  // -1: no ready association.
   int pick_interactive(size_t own);
   static constexpr size_t kSpill = 32;
+  static constexpr double kSpillLoad = 0.5;  // Reactor::load() of a busy association thread
   // Moves a client connection (its socket and the bytes read but not parsed)
   // to association k's session; k > 0 counts it there until release(k).
   void hand(size_t k, int fd, Bytes unparsed);
   void release(size_t k);
+  // Tests: where association k's thread load comes from (default: its reactor).
+  void set_load_fn(std::function<double(size_t)> f) { load_fn_ = std::move(f); }
   bool bulk_route(const std::string& key);
   void note_route(const std::string& key, uint64_t bytes, bool streaming);
   size_t connections(size_t k);
@@ -125,9 +129,11 @@ class ProxyRouter : public std::enable_shared_from_this<ProxyRouter> {
     size_t conns = 0;
     size_t interactive = 0;  // interactive requests in flight
   };
+  double load(size_t k) const;  // mu_ held
   std::mutex mu_;
   std::vector<Target> t_;
   BulkRoutes routes_;
+  std::function<double(size_t)> load_fn_;
 };
 
 class ProxyConn;

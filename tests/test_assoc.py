@@ -185,9 +185,10 @@ def test_wan_path_keeps_one_association():
 
 
 def test_interactive_load_spills_over_at_node_scale():
-    # More concurrent SSE streams than ProxyRouter::kSpill (32): the first
-    # association keeps 32, the rest spread over the extra ones; every event
-    # of every stream arrives.
+    # More concurrent SSE streams than ProxyRouter::kSpill (32): past it, and
+    # while the first association's thread is busy, new ones spread over the
+    # extra ones (the policy itself: native assoc_router_placement); however
+    # they are placed, every event of every stream arrives.
     mock, up = _mock(interval_us=20000, tokens=5)
     mp = free_port()
     try:
@@ -196,8 +197,7 @@ def test_interactive_load_spills_over_at_node_scale():
             _wait_assoc(t, 3)
             r = _loadgen(t.proxy_port, 64, 3)
             assert r["errors"] == 0 and r["requests"] == 192, r
-            assert _metric(mp, "tunnel_assoc_handoffs_total") >= 16
-            # A lone stream afterwards runs on the first association again.
+            # A lone stream afterwards runs on the first association.
             h0 = _metric(mp, "tunnel_assoc_handoffs_total")
             assert _sse(t.proxy_port)[0] == 200
             assert _metric(mp, "tunnel_assoc_handoffs_total") == h0
