@@ -43,10 +43,6 @@
 #include "bf16_common.h"
 
 #include <algorithm>
-#include <map>
-#include <memory>
-#include <mutex>
-#include <vector>
 #include <cstdlib>
 
 namespace {
@@ -536,41 +532,6 @@ __global__ __launch_bounds__(256) void k_embed(const uint16_t* __restrict__ embe
   if (threadIdx.x == 0) ss_out[b] = red[0] + red[1] + red[2] + red[3];
 }
 
-// ------------------------------------------------------------ weight prefetch
-// Pulls the next projections' weights through the cache hierarchy into the
-// 256 MiB Infinity Cache while the attention (a few MB of K/V, latency-bound,
-// 16 workgroups at batch 1) leaves HBM idle; the O and gate/up GEMVs then
-// stream them on-die (≈8.6 vs ≈6 TB/s per chip, ≈545 vs ≈900-cycle first
-// load; MI355X_MICROARCH "Infinity Cache"). Runs on a side stream of the step
-// (P2PT_DECODE_PREFETCH=1): reads only, every lane keeps 8 independent
-// 16-byte loads in flight, and the result is folded into a store (to a
-// buffer the host owns, so the compiler cannot drop it) that never happens in
-// practice, so the loads stay.
-__global__ __launch_bounds__(256) void k_prefetch(const uint32_t* __restrict__ a, uint32_t na,
-                                                  const uint32_t* __restrict__ b, uint32_t nb,
-                                                  unsigned* __restrict__ sink) {
-  // One dword per 64-byte segment is enough to pull the whole line on-die;
-  // na / nb count segments.
-  constexpr int U = 8;
-  const uint32_t stride = gridDim.x * blockDim.x;
-  uint32_t acc = 0;
-  for (int r = 0; r < 2; r++) {
-    const uint32_t* p = r == 0 ? a : b;
-    const uint32_t n = r == 0 ? na : nb;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride * U) {
-      uint32_t v[U];
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        const uint32_t j = i + uint32_t(u) * stride;
-        v[u] = p[size_t(min(j, n - 1)) * 16];  // clamped: no branch between the loads
-      }
-#pragma unroll
-      for (int u = 0; u < U; u++) acc ^= v[u];
-    }
-  }
-  if (acc == 0x9E3779B9u) sink[blockIdx.x & 63] = acc;
-}
-
 // ------------------------------------------------------------ attention
 // GQA flash-decoding with a fixed grid of (span slot, row b, KV head)
 // workgroups: graph-captured steps launch the same grid whatever the context
@@ -1038,41 +999,6 @@ bool dims_ok(const LlamaDims& d) {
   return true;
 }
 
-// Side stream and events of the weight prefetch, per device, created on the
-// first step (outside graph capture: the warm-up steps run first). Null when
-// P2PT_DECODE_PREFETCH is off (the default until measured ahead).
-struct Prefetch {
-  hipStream_t side = nullptr;
-  unsigned* sink = nullptr;    // 64 words k_prefetch (practically) never writes
-  std::vector<hipEvent_t> ev;  // one per layer (fork) + one (join)
-  int blocks = 128;            // half the CUs: the attention's workgroups always find room
-};
-
-Prefetch* prefetch_for(int n_layers) {
-  // Read per step (not cached): a test compares both settings in one process;
-  // a captured graph keeps what its capture step decided.
-  if (env_int("P2PT_DECODE_PREFETCH", 0) == 0) return nullptr;
-  static std::mutex mu;
-  static std::map<int, std::unique_ptr<Prefetch>> by_dev;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lk(mu);
-  auto& p = by_dev[dev];
-  if (!p) {
-    p = std::make_unique<Prefetch>();
-    if (hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&p->sink), 64 * sizeof(unsigned)) != hipSuccess)
-      return nullptr;
-    p->blocks = std::max(16, env_int("P2PT_DECODE_PREFETCH_BLOCKS", 128));
-  }
-  while (int(p->ev.size()) < n_layers + 1) {
-    hipEvent_t e;
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
-    p->ev.push_back(e);
-  }
-  return p.get();
-}
-
 }  // namespace
 
 extern "C" {
@@ -1119,7 +1045,6 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
   int ss_parts = 1;
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return int(e);
-  Prefetch* pf = prefetch_for(d.n_layers);
 
   for (int L = 0; L < d.n_layers; L++) {
     const uint16_t* wqkv = bf(4 + 6 * L);
@@ -1150,14 +1075,6 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
       a.kpl = 0;
     if (a.kpl == 0) a.cwl = 0;
     if ((e = launch_gemm<EPI_ROPE, 1>(a, s)) != hipSuccess) return int(e);
-    if (pf) {  // O and gate/up weights into the Infinity Cache beside the attention
-      hipEventRecord(pf->ev[L], s);
-      hipStreamWaitEvent(pf->side, pf->ev[L], 0);
-      hipLaunchKernelGGL(k_prefetch, dim3(pf->blocks), dim3(256), 0, pf->side, reinterpret_cast<const uint32_t*>(wo),
-                         uint32_t(size_t(d.dim) * d.H * d.D * 2 / 64), reinterpret_cast<const uint32_t*>(wgu),
-                         uint32_t(size_t(2) * d.ffn * d.dim * 2 / 64), pf->sink);
-      if ((e = hipGetLastError()) != hipSuccess) return int(e);
-    }
 
     // attention: (span slot, row, KV head) workgroups of 8 waves
     {
@@ -1237,10 +1154,6 @@ int p2pt_llama_decode(const LlamaDims* dp, const void* const* w, void* k_cache, 
   // counter costing more than the launch (profiles/r03/decode/decode_ab_kparts.log).
   if ((e = launch_gemm<EPI_ARGMAX, kTnStore>(h, s, 4)) != hipSuccess) return int(e);
   hipLaunchKernelGGL(k_argmax_merge, dim3(emit_rows), dim3(256), 0, s, W.am_val, W.am_idx, parts, ids);
-  if (pf) {  // the side stream joins the step (graph capture needs every fork joined)
-    hipEventRecord(pf->ev[d.n_layers], pf->side);
-    hipStreamWaitEvent(s, pf->ev[d.n_layers], 0);
-  }
   return int(hipGetLastError());
 }
 
