@@ -337,6 +337,8 @@ def main():
                 "topology": "node" if node else ("independent" if world > 1 else "single"),
                 "transport": a.transport,
                 "mtu": a.mtu if a.transport == "webrtc" else "n/a",
+                # parallel associations offered by both tunnel processes (--assoc; used on short paths)
+                "assoc": int(os.environ.get("TUNNEL_ASSOC", "3")) if a.transport == "webrtc" else 1,
                 "path_rank0": path,
                 "pinned_rank0": {k: v for k, v in PLAN.items() if k != "set"} or None,
             },
