@@ -952,6 +952,9 @@ void ProxySession::release_links(const std::string& fail_why) {
 }
 
 ProxySession::~ProxySession() {
+  // No more connections handed to this session (its reactor may go next:
+  // an extra association's thread is joined after its session is dropped).
+  shared_->router->detach(cfg_.assoc_index);
   assoc_.reset();  // extra associations first (joins their threads)
   if (agree_timer_) r_.cancel(agree_timer_);
   if (ping_timer_) r_.cancel(ping_timer_);
@@ -1438,22 +1441,19 @@ int ProxyRouter::pick_interactive(size_t own) {
 }
 
 void ProxyRouter::hand(size_t k, int fd, Bytes unparsed) {
-  Reactor* r = nullptr;
-  std::weak_ptr<ProxySession> s;
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    if (k < t_.size()) {
-      r = t_[k].r;
-      s = t_[k].s;
-      if (k > 0 && r) t_[k].conns++;
-    }
-  }
-  if (!r) {
+  auto self = shared_from_this();
+  std::lock_guard<std::mutex> lk(mu_);
+  // An extra association that is gone (detached) sends the connection to the
+  // first one instead.
+  if (k > 0 && (k >= t_.size() || !t_[k].r)) k = 0;
+  if (k >= t_.size() || !t_[k].r) {
     ::close(fd);
     return;
   }
-  auto self = shared_from_this();
-  r->post_threadsafe([self, s, k, fd, unparsed = std::move(unparsed)]() mutable {
+  if (k > 0) t_[k].conns++;
+  // Posted under mu_: detach() takes mu_ before the association's reactor
+  // goes away, so nothing is posted to a destroyed reactor.
+  t_[k].r->post_threadsafe([self, s = t_[k].s, k, fd, unparsed = std::move(unparsed)]() mutable {
     if (auto x = s.lock()) {
       x->adopt_handed(fd, std::move(unparsed), k > 0);
       return;
@@ -1465,6 +1465,14 @@ void ProxyRouter::hand(size_t k, int fd, Bytes unparsed) {
       ::close(fd);
     }
   });
+}
+
+void ProxyRouter::detach(size_t k) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (k >= t_.size()) return;
+  t_[k].r = nullptr;
+  t_[k].s.reset();
+  t_[k].ready = false;
 }
 
 double ProxyRouter::load(size_t k) const {

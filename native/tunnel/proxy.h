@@ -93,6 +93,10 @@ class ProxySession;
 class ProxyRouter : public std::enable_shared_from_this<ProxyRouter> {
  public:
   void attach(size_t k, Reactor* r, std::weak_ptr<ProxySession> s);
+  // Association k's session is going away: nothing is handed to it any more
+  // (its connections go to the first association), and its reactor is not
+  // touched after this returns.
+  void detach(size_t k);
   void set_ready(size_t k, bool ready);
   // The association for a bulk request: the ready one with the fewest bulk
   // connections — the first association only while no interactive request
