@@ -1,9 +1,5 @@
 #include "tunnel/assoc.h"
 
-#include <sys/resource.h>
-#include <sys/syscall.h>
-#include <unistd.h>
-
 #include <algorithm>
 
 #include "core/json.h"
@@ -41,11 +37,6 @@ class AssocLink : public std::enable_shared_from_this<AssocLink> {
         factory_(std::move(f)) {}
 
   void start() {
-#ifdef P2PT_ASSOC_NICE
-    // Experiment: the extra associations' threads (this one and the lanes it
-    // starts, which inherit it) below the first association's priority.
-    setpriority(PRIO_PROCESS, pid_t(syscall(SYS_gettid)), P2PT_ASSOC_NICE);
-#endif
     pc_ = rtc::PeerConnection::create(r_, pcfg_, offerer_);
     std::weak_ptr<AssocLink> w = shared_from_this();
     pc_->on_ice_candidate = [w](const std::string& cand) {
