@@ -34,6 +34,16 @@ def test_bench_single_rank():
     d = _run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--curve", "1", "--curve-steps", "1"])
     _check(d, 1, 2, 1)
     assert "1" in d["curve_rank0"] and "8" in d["curve_rank0"]
+    assert d["curve_steps"] == 1
+    # The host the numbers came from (rows move 20-40 % between boxes).
+    assert {"cpu_model", "host_hash", "governor", "deepest_idle", "cpus_allowed", "cgroup_cpus", "io_uring"} <= set(d["box"])
+    assert d["config"]["assoc"] == int(os.environ.get("TUNNEL_ASSOC", "3"))
+
+
+def test_bench_curve_points_default_to_the_headline_steps():
+    d = _run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--curve", "2", "--no-jumbo-extra"])
+    _check(d, 1, 2, 1)
+    assert d["curve_steps"] == 2
 
 
 def test_bench_two_ranks_torchrun():
