@@ -528,7 +528,8 @@ void IceAgent::send(const uint8_t* p, size_t n) {
 // that RTT); rate_mbps makes the outbound path a bottleneck link of that rate
 // with a drop-tail queue of queue_kb (default 256) — serialization and
 // queueing delay, congestion losses — so SCTP's congestion control meets a
-// realistic path.
+// realistic path. assoc_down_ms=N: this process's extra associations ("assoc"
+// extension, tunnel/assoc.cc) fail N ms after they come up (fail-over tests).
 namespace {
 struct FaultCfg {
   double drop = 0, dup = 0;
@@ -537,6 +538,7 @@ struct FaultCfg {
   double rate_bps = 0;      // bottleneck rate (0 = unlimited)
   uint64_t queue_bytes = 256 * 1024;
   uint64_t bh_start_ms = 0, bh_len_ms = 0, t0_ms = 0;
+  uint64_t assoc_down_ms = 0;
   bool on = false;
   uint64_t rng = 0x9E3779B97F4A7C15ull;
   FaultCfg() {
@@ -557,6 +559,7 @@ struct FaultCfg {
       else if (k == "rtt_ms") fixed_us = uint64_t(atof(v) * 500);
       else if (k == "rate_mbps") rate_bps = atof(v) * 1e6;
       else if (k == "queue_kb") queue_bytes = uint64_t(atof(v) * 1024);
+      else if (k == "assoc_down_ms") assoc_down_ms = strtoull(v, nullptr, 10);
       else if (k == "blackhole") {
         bh_start_ms = strtoull(v, nullptr, 10);
         if (const char* c = strchr(v, ':')) bh_len_ms = strtoull(c + 1, nullptr, 10);
@@ -585,6 +588,8 @@ FaultCfg& fault() {
   return f;
 }
 }  // namespace
+
+uint64_t fault_assoc_down_ms() { return fault().assoc_down_ms; }
 
 bool IceAgent::direct_target(int* fd, SockAddr* to, size_t* coalesce) const {
   if (sel_local_ < 0 || closed_ || nat_mode_ || fault().on || locals_[sel_local_].relay) return false;

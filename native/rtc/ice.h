@@ -28,6 +28,10 @@
 
 namespace p2pt::rtc {
 
+// TUNNEL_FAULT assoc_down_ms (0: off): extra associations fail this long after
+// they come up (tunnel/assoc.cc; fail-over tests).
+uint64_t fault_assoc_down_ms();
+
 // Byte vector whose resize() leaves new bytes uninitialised (datagram
 // buffers are always fully written before use).
 template <class T>

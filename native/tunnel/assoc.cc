@@ -188,6 +188,11 @@ class AssocLink : public std::enable_shared_from_this<AssocLink> {
       };
       s->session_ = s->factory_(s->r_, s->dc_, s->k_, done);
       s->state(true, "");
+      if (const uint64_t ms = rtc::fault_assoc_down_ms()) {  // TUNNEL_FAULT fail-over tests
+        s->r_.call_later_ms(ms, [w] {
+          if (auto s2 = w.lock()) s2->down("fault injection (TUNNEL_FAULT assoc_down_ms)");
+        });
+      }
     };
     if (dc_->is_open()) opened();
     else dc_->on_open = opened;

@@ -10,6 +10,7 @@
   request, and an SSE request on such a connection goes back to the first;
 * more concurrent SSE streams than the spill threshold spread over the
   associations;
+* an extra association that fails is dropped from placement, the rest go on;
 * a WAN path (20 ms RTT) keeps the single association;
 * a side without the feature (--assoc 1, or a reference-like feature list)
   leaves the tunnel on its single data channel, and everything still works
@@ -201,5 +202,25 @@ def test_interactive_load_spills_over_at_node_scale():
             h0 = _metric(mp, "tunnel_assoc_handoffs_total")
             assert _sse(t.proxy_port)[0] == 200
             assert _metric(mp, "tunnel_assoc_handoffs_total") == h0
+    finally:
+        mock.stop()
+
+
+def test_a_failed_extra_association_is_dropped_from_placement():
+    # The extra associations fail 300 ms after they come up (TUNNEL_FAULT
+    # assoc_down_ms, both peers): each side drops them from placement ("bye"
+    # to the other), and later bulk requests run on the first association,
+    # without errors.
+    mock, up = _mock()
+    try:
+        with Tunnel(f"http://127.0.0.1:{up}", serve_extra=MTU + ["--assoc", "3"], proxy_extra=MTU + ["--assoc", "3"],
+                    env={"RUST_LOG": "info", "TUNNEL_FAULT": "assoc_down_ms=300"}) as t:
+            _wait_assoc(t, 3)
+            t.proxy.wait_for("association 1 down", 10)
+            t.proxy.wait_for("association 2 down", 10)
+            r = _loadgen(t.proxy_port, 8, 2, ["--post-bytes", str(1 << 20)])
+            assert r["errors"] == 0 and r["requests"] == 16, r
+            assert _sse(t.proxy_port)[0] == 200
+            assert t.proxy.count("proxy failed") == 0 and t.serve.count("serve failed") == 0
     finally:
         mock.stop()
