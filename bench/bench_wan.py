@@ -48,7 +48,23 @@ def lg(port, *args):
                             stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
 
 
-def result(p, timeout=900):
+PHASE = ["start"]  # what the run is doing (the heartbeat prints it)
+
+
+def heartbeat(period_s=30.0):
+    """A line on stderr every period_s: a slow lossy row is never silent, and a
+    stuck one says where it is."""
+    import threading
+
+    def beat():
+        t0 = time.time()
+        while True:
+            time.sleep(period_s)
+            print(json.dumps({"heartbeat_s": round(time.time() - t0), "phase": PHASE[0]}), file=sys.stderr, flush=True)
+    threading.Thread(target=beat, daemon=True).start()
+
+
+def result(p, timeout=600):
     out, _ = p.communicate(timeout=timeout)
     return json.loads(out.strip().splitlines()[-1])
 
@@ -151,6 +167,7 @@ def main():
                     help="serve's congestion response: default, or keep (TUNNEL_SCTP_CC=beta=100)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
+    heartbeat()
     ensure_native()
     mport = free_port()
     mock = spawn("mock", [binary("tunnel-mock"), "--port", str(mport), "--interval-ms", "10", "--tokens", "100",
@@ -177,6 +194,8 @@ def main():
             for loss in [float(x) for x in a.losses.split(",") if x]:
                 qkb = a.queue_kb or max(64.0, a.rate_mbps * 1e6 / 8 * rtt / 1e3 / 1024)
                 env = {"RUST_LOG": "warn,tunnel::rtc=info,tunnel::serve=info,tunnel::proxy=info", **policy_env}
+                PHASE[0] = f"rtt {rtt} loss {loss}: tunnel start"
+                print(json.dumps({"rtt_ms": rtt, "loss": loss, "phase": "tunnel start"}), file=sys.stderr, flush=True)
                 relay, turn = None, []
                 if a.relay:
                     sys.path.insert(0, os.path.join(ROOT, "bench"))
@@ -191,6 +210,7 @@ def main():
                             proxy_extra=extra + ["--metrics-listen", f"127.0.0.1:{pm}"], env=env,
                             room=f"wan-{os.getpid()}-{time.time_ns()}") as t:
                     def progress(what):  # one line per phase: a long lossy row is not silent
+                        PHASE[0] = f"rtt {rtt} loss {loss}: {what}"
                         print(json.dumps({"rtt_ms": rtt, "loss": loss, "phase": what}), file=sys.stderr, flush=True)
                     progress("warm")
                     result(sse(t.proxy_port, 1))  # warm: connections, cwnd

@@ -36,7 +36,14 @@ class AssocLink : public std::enable_shared_from_this<AssocLink> {
       : r_(r), primary_(primary), group_(std::move(g)), k_(index), offerer_(offerer), pcfg_(pc),
         factory_(std::move(f)) {}
 
+  // The offering side creates its connection at once; the answering side only
+  // when an offer arrives (a proxy that decides against the extra
+  // associations — a long path — then costs no sockets or TURN allocations).
   void start() {
+    if (offerer_) create_pc();
+  }
+
+  void create_pc() {
     pc_ = rtc::PeerConnection::create(r_, pcfg_, offerer_);
     std::weak_ptr<AssocLink> w = shared_from_this();
     pc_->on_ice_candidate = [w](const std::string& cand) {
@@ -66,8 +73,9 @@ class AssocLink : public std::enable_shared_from_this<AssocLink> {
   }
 
   void on_signal(const std::string& kind, const std::string& value) {
-    if (closed_ || !pc_) return;
+    if (closed_) return;
     if (kind == "offer" && !offerer_ && !remote_set_) {
+      if (!pc_) create_pc();
       apply_remote(value);
       if (closed_) return;
       if (pc_->gathering_complete()) {
