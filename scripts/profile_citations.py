@@ -27,6 +27,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PAT = re.compile(r"profiles/[A-Za-z0-9_.\-/{},*]+")
+# profiles/README.md names its files relative to profiles/ (`r05/b11/nodeprof/`).
+REL = re.compile(r"`(r\d\d/[A-Za-z0-9_.\-/{},*]+)`")
 # Placeholders in prose, not paths.
 PLACEHOLDERS = ("profiles/r05/bNN", "profiles/r06/bNN")
 
@@ -54,7 +56,11 @@ def citations(files: list[str] | None = None) -> dict[str, set[str]]:
     cites: dict[str, set[str]] = {}
     for f in files or doc_files():
         with open(os.path.join(ROOT, f), errors="ignore") as fh:
-            for m in PAT.findall(fh.read()):
+            text = fh.read()
+            found = PAT.findall(text)
+            if f == "profiles/README.md":
+                found += ["profiles/" + m for m in REL.findall(text)]
+            for m in found:
                 m = m.rstrip(".,;:)`'\"")
                 if m.startswith(PLACEHOLDERS):
                     continue
