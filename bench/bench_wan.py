@@ -64,8 +64,26 @@ def heartbeat(period_s=30.0):
     threading.Thread(target=beat, daemon=True).start()
 
 
-def result(p, timeout=600):
-    out, _ = p.communicate(timeout=timeout)
+TUNNEL = [None]  # the tunnel of the current row (its logs are printed if a load stalls)
+LOGDIR = [None]  # --logs: where a stalled row's full logs go
+
+
+def result(p, timeout=180):
+    try:
+        out, _ = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        t = TUNNEL[0]
+        if t is not None:
+            for proc in (t.serve, t.proxy):
+                lines = proc.text().splitlines()
+                print(f"---- {proc.name} log tail ({len(lines)} lines)", file=sys.stderr)
+                print("\n".join(lines[-80:]), file=sys.stderr, flush=True)
+                if LOGDIR[0]:
+                    os.makedirs(LOGDIR[0], exist_ok=True)
+                    with open(os.path.join(LOGDIR[0], f"stalled_{proc.name}.log"), "w") as f:
+                        f.write(proc.text() + "\n")
+        p.kill()
+        raise
     return json.loads(out.strip().splitlines()[-1])
 
 
@@ -88,6 +106,51 @@ def scrape(port):
         if len(parts) == 2 and parts[0] in SCTP_GAUGES:
             out[parts[0].replace("tunnel_sctp_", "")] = float(parts[1])
     return out
+
+
+def scrape_all(port):
+    """Every SCTP / UDP / DTLS gauge of one tunnel process (for --timeline)."""
+    try:
+        text = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=2).read().decode()
+    except OSError:
+        return {}
+    out = {}
+    for line in text.splitlines():
+        parts = line.split()
+        if len(parts) == 2 and parts[0].startswith(("tunnel_sctp_", "tunnel_udp_", "tunnel_dtls_")):
+            out[parts[0][len("tunnel_"):]] = float(parts[1])
+    return out
+
+
+class Timeline:
+    """Samples both tunnel processes' gauges every period_s while a phase
+    runs: a stalled transfer shows which counter stopped moving."""
+
+    def __init__(self, ports, period_s=0.5):
+        import threading
+        self.ports, self.period, self.rows, self.stop_ev = ports, period_s, [], threading.Event()
+        self.t0 = time.time()
+        self.th = threading.Thread(target=self.run, daemon=True)
+        self.th.start()
+
+    def run(self):
+        prev = {}
+        while not self.stop_ev.wait(self.period):
+            row = {"t": round(time.time() - self.t0, 2)}
+            for side, port in self.ports.items():
+                cur = scrape_all(port)
+                # counters as deltas since the last sample, gauges as is
+                row[side] = {k: (v - prev.get((side, k), 0.0)) if not k.endswith(("_bytes", "_us")) else v
+                             for k, v in cur.items() if v != prev.get((side, k))}
+                for k, v in cur.items():
+                    prev[(side, k)] = v
+            self.rows.append(row)
+            print(json.dumps({"timeline": row}), file=sys.stderr, flush=True)
+
+    def stop(self):
+        self.stop_ev.set()
+        self.th.join(5)
+        return self.rows
 
 
 def thread_cpu(pid):
@@ -165,9 +228,13 @@ def main():
     ap.add_argument("--relay", action="store_true", help="rows through the native TURN relay's emulated link")
     ap.add_argument("--policy", choices=["default", "keep"], default="default",
                     help="serve's congestion response: default, or keep (TUNNEL_SCTP_CC=beta=100)")
+    ap.add_argument("--timeline", action="store_true",
+                    help="sample both sides' SCTP/UDP/DTLS gauges every 0.5 s during sse+bulk (row['timeline'])")
+    ap.add_argument("--logs", default=None, help="write each row's serve/proxy/relay logs to this directory")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     heartbeat()
+    LOGDIR[0] = a.logs
     ensure_native()
     mport = free_port()
     mock = spawn("mock", [binary("tunnel-mock"), "--port", str(mport), "--interval-ms", "10", "--tokens", "100",
@@ -193,7 +260,8 @@ def main():
         for rtt in [float(x) for x in a.rtts.split(",") if x]:
             for loss in [float(x) for x in a.losses.split(",") if x]:
                 qkb = a.queue_kb or max(64.0, a.rate_mbps * 1e6 / 8 * rtt / 1e3 / 1024)
-                env = {"RUST_LOG": "warn,tunnel::rtc=info,tunnel::serve=info,tunnel::proxy=info", **policy_env}
+                env = {"RUST_LOG": "info,tunnel::sctp=debug,tunnel::ice=debug,tunnel::rtc=debug,tunnel::turn=debug"
+                       if a.logs else "info", **policy_env}
                 PHASE[0] = f"rtt {rtt} loss {loss}: tunnel start"
                 print(json.dumps({"rtt_ms": rtt, "loss": loss, "phase": "tunnel start"}), file=sys.stderr, flush=True)
                 relay, turn = None, []
@@ -209,6 +277,7 @@ def main():
                             serve_extra=extra + turn + ["--metrics-listen", f"127.0.0.1:{sm}"],
                             proxy_extra=extra + ["--metrics-listen", f"127.0.0.1:{pm}"], env=env,
                             room=f"wan-{os.getpid()}-{time.time_ns()}") as t:
+                    TUNNEL[0] = t
                     def progress(what):  # one line per phase: a long lossy row is not silent
                         PHASE[0] = f"rtt {rtt} loss {loss}: {what}"
                         print(json.dumps({"rtt_ms": rtt, "loss": loss, "phase": what}), file=sys.stderr, flush=True)
@@ -219,9 +288,11 @@ def main():
                     progress("sse+bulk")
                     bulk = lg(t.proxy_port, "--streams", 4, "--steps", 1, "--warmup", 0, "--method", "GET",
                               "--path", f"/bulk?bytes={a.bulk_mb << 20}", "--events", "none")
+                    tl = Timeline({"serve": sm, "proxy": pm}) if a.timeline else None
                     time.sleep(0.5)
                     mixed = result(sse(t.proxy_port, a.sse_steps))
                     bulk_r = result(bulk)
+                    timeline = tl.stop() if tl else None
                     progress("echo")
                     t0 = time.time()
                     echo = result(lg(t.proxy_port, "--streams", 8, "--steps", a.echo_steps, "--warmup", 0,
@@ -237,9 +308,20 @@ def main():
                            "echo_wall_s": round(time.time() - t0, 2),
                            "serve_sctp": scrape(sm), "proxy_sctp": scrape(pm),
                            "path": t.serve.wait_for("WebRTC connection established", 1).split(" via ", 1)[-1]}
+                    if timeline is not None:
+                        row["timeline"] = timeline
+                    if a.logs:
+                        os.makedirs(a.logs, exist_ok=True)
+                        tag = f"rtt{rtt:g}_loss{loss:g}_{len(res['rows'])}"
+                        for proc in (t.serve, t.proxy):
+                            with open(os.path.join(a.logs, f"{tag}_{proc.name}.log"), "w") as f:
+                                f.write(proc.text() + "\n")
                 if relay:
                     relay.stop()
                     row["relay"] = relay.stats
+                    if a.logs:
+                        with open(os.path.join(a.logs, f"{tag}_relay.log"), "w") as f:
+                            f.write(relay.proc.text() + "\n")
                 res["rows"].append(row)
                 if a.out:  # the rows so far, in case a later one never ends
                     with open(a.out, "w") as f:

@@ -455,14 +455,21 @@ void IceAgent::pair_up(int li, int ri) {
   if (laddr.family() != rc.addr.family()) return;
   // Loopback sockets only talk to loopback remotes and vice versa.
   if (!l.relay && socks_[l.sock].loopback != rc.addr.is_loopback()) return;
-  for (auto& p : pairs_)
-    if (p.local == li && p.remote == ri) return;
+  add_pair(li, ri);
+}
+
+int IceAgent::add_pair(int li, int ri) {
+  for (int pi = 0; pi < int(pairs_.size()); pi++)
+    if (pairs_[pi].local == li && pairs_[pi].remote == ri) return pi;
+  const Local& l = locals_[li];
+  const Candidate& rc = remotes_[ri];
   Pair p;
   p.local = li;
   p.remote = ri;
   p.prio = pair_priority(l, rc);
   pairs_.push_back(p);
   if (l.relay && turn_) turn_->permit(rc.addr);
+  return int(pairs_.size()) - 1;
 }
 
 void IceAgent::send_raw(int local_idx, const SockAddr& to, const uint8_t* p, size_t n) {
@@ -1056,14 +1063,24 @@ void IceAgent::handle_request(int si, const SockAddr& from, const stun::Message&
       set_state(IceState::Checking);
     }
   }
+  // The peer reached us on this socket from that address, so the pair works
+  // even where our own pairing rules left it out (a TURN relay on loopback
+  // forwarding to a non-loopback host candidate): add it, as a triggered
+  // check would (RFC 8445 §7.3.1.4), so that a nomination of it counts here.
+  // Without it the controlling agent selected a pair this agent never had.
+  if (!(cfg_.relay_only && !locals_[li].relay) && locals_[li].c.type != "srflx") add_pair(li, ri);
   bool use_cand = m.get(stun::kUseCandidate) != nullptr;
   for (int pi = 0; pi < int(pairs_.size()); pi++) {
     Pair& pr = pairs_[pi];
     if (pr.local != li || pr.remote != ri) continue;
     if (use_cand && !controlling_) {
       // Nominated by the controlling agent. Select right away (its check of
-      // this pair just succeeded end-to-end with our response).
-      if (sel_pair_ < 0) select_pair(pi);
+      // this pair just succeeded end-to-end with our response). Aggressive
+      // nomination nominates every pair it checks, so a later nomination of
+      // a higher-priority pair moves the selection there: both agents end on
+      // the highest-priority nominated pair (RFC 8445 §8.1.1) — the first to
+      // arrive here and the first to succeed there may differ.
+      if (sel_pair_ < 0 || pr.prio > pairs_[sel_pair_].prio) select_pair(pi);
     }
     if (pr.st == Pair::St::Waiting || pr.st == Pair::St::Failed) {
       pr.st = Pair::St::Waiting;  // triggered check
@@ -1125,9 +1142,10 @@ void IceAgent::handle_response(const SockAddr& from, const stun::Message& m, con
   }
   pr.st = Pair::St::Succeeded;
   if (controlling_ && pr.use_cand) {
-    if (sel_pair_ < 0) select_pair(pi);
-  } else if (!controlling_ && pr.nominate_on_success && sel_pair_ < 0) {
-    select_pair(pi);
+    // The first nominated pair to succeed carries the connection at once; a
+    // higher-priority one that succeeds later takes over (the controlled
+    // agent moves to it too when its nomination arrives).
+    if (sel_pair_ < 0 || pr.prio > pairs_[sel_pair_].prio) select_pair(pi);
   } else if (controlling_ && sel_pair_ < 0) {
     // Regular nomination: follow up with USE-CANDIDATE on the first valid pair.
     pr.use_cand = true;
@@ -1139,11 +1157,13 @@ void IceAgent::handle_response(const SockAddr& from, const stun::Message& m, con
 
 void IceAgent::select_pair(int pi) {
   Pair& pr = pairs_[pi];
+  const bool switched = sel_pair_ >= 0 && sel_pair_ != pi;
   sel_pair_ = pi;
   if (sel_local_ != pr.local || sel_remote_ != remotes_[pr.remote].addr) path_gen_++;
   sel_local_ = pr.local;
   sel_remote_ = remotes_[pr.remote].addr;
-  LOG_DEBUG(kT, "ICE selected pair %s", selected_desc().c_str());
+  if (switched) LOG_INFO(kT, "ICE pair switched to %s (higher-priority nominated pair)", selected_desc().c_str());
+  else LOG_DEBUG(kT, "ICE selected pair %s", selected_desc().c_str());
   last_rx_ = Reactor::now_ms();
   set_state(IceState::Connected);
 }
@@ -1193,10 +1213,14 @@ void IceAgent::tick() {
   if (closed_) return;
   uint64_t now = Reactor::now_ms();
   std::weak_ptr<IceAgent> w = shared_from_this();
-  if (!remote_pwd_.empty() && sel_pair_ < 0) {
-    // Retransmit in-progress checks; start the highest-priority waiting check (pacing Ta = 20 ms).
+  if (!remote_pwd_.empty() && (sel_pair_ < 0 || controlling_)) {
+    // Retransmit in-progress checks; start the highest-priority waiting check
+    // (pacing Ta = 20 ms). Once a pair is selected, only the controlling
+    // agent's checks of higher-priority pairs still run (a lost check or
+    // response must not leave the two agents on different pairs).
+    const uint64_t floor = sel_pair_ < 0 ? 0 : pairs_[sel_pair_].prio + 1;
     for (auto& pr : pairs_) {
-      if (pr.st != Pair::St::InProgress || now < pr.next_tx) continue;
+      if (pr.st != Pair::St::InProgress || now < pr.next_tx || pr.prio < floor) continue;
       if (pr.tries >= 7) {
         pr.st = Pair::St::Failed;
         continue;
@@ -1208,7 +1232,7 @@ void IceAgent::tick() {
     }
     Pair* best = nullptr;
     for (auto& pr : pairs_)
-      if (pr.st == Pair::St::Waiting && (!best || pr.prio > best->prio)) best = &pr;
+      if (pr.st == Pair::St::Waiting && pr.prio >= floor && (!best || pr.prio > best->prio)) best = &pr;
     if (best) {
       best->st = Pair::St::InProgress;
       best->tries = 1;

@@ -165,6 +165,7 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   // True when both ends of the selected pair are on this host.
   bool selected_same_host() const;
   std::string selected_desc() const;
+  size_t local_candidate_count() const { return locals_.size(); }
   IceState state() const { return state_; }
   // Datagrams the kernel dropped on this agent's sockets because their
   // receive buffer was full (sk_drops, the count SO_RXQ_OVFL reports; read
@@ -203,7 +204,6 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
     uint64_t next_tx = 0;
     uint64_t rto = 0;
     bool use_cand = false;
-    bool nominate_on_success = false;
     uint64_t sent_us = 0;  // when the check with `tid` went out
   };
 
@@ -236,6 +236,7 @@ class IceAgent : public std::enable_shared_from_this<IceAgent> {
   void maybe_gathering_done();
   void add_local(Candidate c, int sock, bool relay);
   void pair_up(int local, int remote);
+  int add_pair(int local, int remote);  // index of the (new or existing) pair
   uint64_t pair_priority(const Local& l, const Candidate& r) const;
   void tick();
   void kick();

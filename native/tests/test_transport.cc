@@ -1119,6 +1119,57 @@ TEST(ice_detached_socket_is_not_read_by_a_stale_event) {
   ans->close();
 }
 
+// Both agents end on the same candidate pair. The controlling agent nominates
+// aggressively (USE-CANDIDATE on every check), so with two host candidates a
+// side the controlled agent could take the first nominated pair to reach it
+// while the controlling one took the first to succeed: each then sent on a
+// different path (through the TURN relay on the MI355X host: the proxy's
+// socket reader held a socket the data never came to, and a 20 ms relay row
+// stalled). Both now move to the highest-priority nominated pair (RFC 8445
+// §8.1.1), the same on both sides.
+TEST(ice_agents_agree_on_the_selected_pair) {
+  int agreed = 0, runs = 0;
+  for (int run = 0; run < 8; run++) {
+    Reactor r;
+    PcConfig cfg;
+    cfg.ice.include_loopback = true;
+    auto off = PeerConnection::create(r, cfg, true);
+    auto ans = PeerConnection::create(r, cfg, false);
+    off->on_ice_candidate = [&](const std::string& c) { ans->add_ice_candidate(c, nullptr); };
+    ans->on_ice_candidate = [&](const std::string& c) { off->add_ice_candidate(c, nullptr); };
+    auto dc = off->create_data_channel("tunnel");
+    std::shared_ptr<DataChannel> rdc;
+    ans->on_data_channel = [&](std::shared_ptr<DataChannel> d) { rdc = d; };
+    off->start_gathering();
+    ans->start_gathering();
+    CHECK(r.run_until([&] { return off->gathering_complete() && ans->gathering_complete(); }, 3000));
+    if (off->ice()->local_candidate_count() < 2) {  // one interface: nothing to disagree on
+      off->close();
+      ans->close();
+      printf("  one host candidate: skipped\n");
+      return;
+    }
+    std::string err;
+    CHECK(ans->set_remote_description(off->local_description(), &err));
+    CHECK(off->set_remote_description(ans->local_description(), &err));
+    CHECK(r.run_until([&] { return dc->is_open() && rdc && rdc->is_open(); }, 5000));
+    r.run_until([] { return false; }, 300);  // late check responses / nominations
+    auto split = [](const std::string& d) {
+      const size_t c = d.find(':'), arrow = d.find(" <-> ");
+      return std::make_pair(d.substr(c + 1, arrow - c - 1), d.substr(arrow + 5));
+    };
+    const auto o = split(off->ice()->selected_desc()), a = split(ans->ice()->selected_desc());
+    runs++;
+    if (o.first == a.second && o.second == a.first) agreed++;
+    else printf("  run %d: offerer %s, answerer %s\n", run, off->ice()->selected_desc().c_str(),
+                ans->ice()->selected_desc().c_str());
+    off->close();
+    ans->close();
+  }
+  printf("  %d of %d runs on one pair\n", agreed, runs);
+  CHECK_EQ(agreed, runs);
+}
+
 // The socket reader follows the selected pair: when the ICE agent's path
 // changes (pair switch, remote rebinding) the reader gives the old socket back
 // and a new one reads the current pair (advice r3: it stayed pinned to the

@@ -113,3 +113,41 @@ def test_unsupported_turn_url_is_refused(url, msg):
     r = subprocess.run([binary("tunnel"), "proxy", "--room", "x", "--turn", url, "--signal", "ws://127.0.0.1:1",
                         "--max-retries", "0"], capture_output=True, text=True, timeout=10)
     assert r.returncode == 2 and msg in r.stderr, (r.returncode, r.stderr)
+
+
+def _final_pair(proc):
+    """The selected pair a tunnel process ended on: its "connection
+    established via" line, or a later ICE pair switch."""
+    pair = None
+    for line in proc.text().splitlines():
+        for key in ("WebRTC connection established", "ICE pair switched to "):
+            if key in line:
+                pair = (line.split(" via ", 1)[-1] if key.startswith("WebRTC") else line.split(key, 1)[1])
+                pair = pair.split(" mtu=")[0].split(" (")[0]
+    return pair
+
+
+def test_relay_only_side_and_host_side_agree_on_the_pair(mock_upstream):
+    # serve on its relayed candidate only, the proxy on its host candidates.
+    # The relay (on loopback) reaches every host candidate, so serve checks and
+    # nominates each; the proxy pairs loopback only with loopback and had no
+    # pair for a nominated non-loopback one: it kept sending from its loopback
+    # socket while serve sent to the other one (on the MI355X host the proxy's
+    # socket reader then held a socket the data never came to; a 20 ms relay
+    # row stalled). Both must end on the same pair.
+    turn = _server("udp")
+    env = {"RUST_LOG": "info"}
+    try:
+        extra = ["--turn", turn.url, "--turn-user", "alice", "--turn-pass", "s3cret", "--ice-relay-only"]
+        with Tunnel(mock_upstream, transport="webrtc", serve_extra=extra + ["--assoc", "1"],
+                    proxy_extra=["--assoc", "1"], env=env) as t:
+            c = http.client.HTTPConnection("127.0.0.1", t.proxy_port, timeout=30)
+            c.request("POST", "/echo", body=b"q" * 100000)
+            assert c.getresponse().read() == b"q" * 100000
+            s, p = _final_pair(t.serve), _final_pair(t.proxy)
+            assert s and p and s.startswith("relay:"), (s, p)
+            s_local, s_remote = s.split(":", 1)[1].split(" <-> ")
+            p_local, p_remote = p.split(":", 1)[1].split(" <-> ")
+            assert (s_local, s_remote) == (p_remote, p_local), (s, p)
+    finally:
+        turn.stop()
