@@ -849,22 +849,36 @@ void SctpAssociation::build_sack(std::vector<uint8_t>& b) {
   offs.reserve(ooo_.size());
   for (auto& kv : ooo_) offs.push_back(kv.first - peer_cum_tsn_);
   std::sort(offs.begin(), offs.end());
+  // As many blocks as fit in one packet beside the SACK's own headers (a
+  // 1200-byte packet: ~290), the lowest first — they hold the holes to repair
+  // next. A cap of 65 left every chunk held beyond the 65th block unreported:
+  // still "in flight" at the sender, it filled cwnd and kept the known holes
+  // from being retransmitted (hundreds of holes after a drop-tail queue
+  // overflowed under slow start stalled a relayed 20 ms path for minutes).
+  // Duplicate reports only tune the sender's spurious-loss undo: at most an
+  // eighth of the room.
+  const size_t room = (cfg_.mtu - kCommonHdr - 4 - 12) / 4;
+  const size_t ndup = std::min(dups_.size(), room / 8);
+  const size_t max_gaps = room - ndup;
   std::vector<std::pair<uint16_t, uint16_t>> gaps;
   for (uint32_t o : offs) {
     if (o > 0xFFFF) break;
-    if (!gaps.empty() && uint32_t(gaps.back().second) + 1 == o) gaps.back().second = uint16_t(o);
-    else gaps.emplace_back(uint16_t(o), uint16_t(o));
-    if (gaps.size() > 64) break;
+    if (!gaps.empty() && uint32_t(gaps.back().second) + 1 == o) {
+      gaps.back().second = uint16_t(o);
+      continue;
+    }
+    if (gaps.size() == max_gaps) break;
+    gaps.emplace_back(uint16_t(o), uint16_t(o));
   }
   put32(b, peer_cum_tsn_);
   put32(b, a_rwnd);
   put16(b, uint16_t(gaps.size()));
-  put16(b, uint16_t(dups_.size()));
+  put16(b, uint16_t(ndup));
   for (auto& g : gaps) {
     put16(b, g.first);
     put16(b, g.second);
   }
-  for (uint32_t d : dups_) put32(b, d);
+  for (size_t i = 0; i < ndup; i++) put32(b, dups_[i]);
   dups_.clear();
 }
 
@@ -1250,6 +1264,24 @@ void SctpAssociation::arm_tlp() {
 }
 
 void SctpAssociation::on_tlp() {
+  // Holes already known lost but held back by a full cwnd come first: the
+  // probe repairs the oldest one, so the cumulative ack moves and frees the
+  // window (re-sending a chunk the peer already holds would not).
+  if (!rtx_.empty()) {
+    const uint32_t k = *rtx_.begin() - (inflight_.empty() ? 0 : inflight_.front()->tsn);
+    if (k < inflight_.size()) {
+      Chunk* ch = inflight_[k];
+      if (ch->retransmit && !ch->acked) {
+        ch->fast = true;
+        ch->probe = true;
+        tlp_count_++;
+        stats_.tlp_probes++;
+        cwnd_bypass_ = 1;
+        start_t3();
+        return;
+      }
+    }
+  }
   for (Chunk* ch : inflight_) {
     if (ch->acked || ch->retransmit) continue;
     ch->retransmit = true;

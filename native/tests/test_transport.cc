@@ -315,6 +315,45 @@ TEST(sctp_tail_blackout_recovers_without_rtt_inflation) {
   CHECK(p.a->srtt_us() < 100000);
 }
 
+TEST(sctp_hundreds_of_holes_in_one_window_recover) {
+  // 20 ms RTT, a bulk transfer, and for a stretch of ~1000 packets every
+  // other a -> b packet lost (a drop-tail queue overflowing under slow start's
+  // 2:1 bursts): hundreds of holes in one window. The receiver reported the
+  // first 65 gap blocks only, so the chunks it held beyond them stayed "in
+  // flight" at the sender, filled cwnd, and kept the known holes from being
+  // retransmitted; the tail-loss probe re-sent chunks the peer already had,
+  // one per probe timeout. Seen through the TURN relay on the MI355X host: a
+  // 20 ms / 0 % loss row stalled for minutes (SRTT to 30 s).
+  for (const int stretch : {1000, 4000}) {  // ~500 holes; more than one SACK can list
+  SctpPair p(0, 0, 0, 1200, false, false, 100);
+  p.link.fixed_delay_us = 10000;
+  p.a->connect();
+  p.b->connect();
+  CHECK(p.r.run_until([&] { return p.a->established() && p.b->established(); }, 5000));
+  std::string blk = payload(10000, 4);
+  const int n = 800;  // 8 MB
+  for (int i = 0; i < n; i++) p.a->send(1, 53, {Bytes::copy(blk)});
+  const uint64_t t0 = Reactor::now_us();
+  std::weak_ptr<SctpAssociation> to_b = p.b;
+  uint64_t data_pkts = 0;
+  p.link.blackout = [&](const std::weak_ptr<SctpAssociation>& to) {
+    if (to.owner_before(to_b) || to_b.owner_before(to)) return false;  // b -> a: SACKs pass
+    const uint64_t k = data_pkts++;
+    return k >= 300 && k < uint64_t(300 + stretch) && k % 2 == 1;
+  };
+  CHECK(p.r.run_until([&] { return p.got_b.size() == size_t(n); }, 30000));
+  const double secs = double(Reactor::now_us() - t0) / 1e6;
+  CHECK_EQ(p.got_b.size(), size_t(n));
+  printf("  stretch %d: %llu dropped, %.2f s, %llu fast rtx, %llu TLP, %llu T3, srtt %llu us\n",
+         stretch, (unsigned long long)p.link.dropped, secs, (unsigned long long)p.a->stats().fast_retransmits,
+         (unsigned long long)p.a->stats().tlp_probes, (unsigned long long)p.a->stats().t3_expirations,
+         (unsigned long long)p.a->srtt_us());
+  CHECK(p.link.dropped >= 400);
+  CHECK(secs < 3.0);
+  CHECK(p.a->srtt_us() < 100000);
+  }
+}
+
 TEST(sctp_priority_messages_keep_stream_order) {
   // Small priority messages overtake queued bulk messages on the wire, but a
   // stream's messages are still delivered in the order they were sent.
