@@ -52,6 +52,28 @@ def rss_kb(pid):
     return 0
 
 
+def cpu_stat():
+    """The job cgroup's CPU-quota counters (cgroup v2 cpu.stat): usage and how
+    often / how long the quota throttled every thread of the job. {} when not
+    readable."""
+    out = {}
+    try:
+        for line in open("/sys/fs/cgroup/cpu.stat"):
+            k, v = line.split()
+            out[k] = int(v)
+    except (OSError, ValueError):
+        pass
+    return out
+
+
+def stat_delta(a, b):
+    """Usage, periods and throttling over one run (cpu_stat() before / after)."""
+    if not a or not b:
+        return None
+    d = {k: b[k] - a.get(k, 0) for k in ("usage_usec", "nr_periods", "nr_throttled", "throttled_usec") if k in b}
+    return d
+
+
 def lg(port, *args, timeout=600):
     return subprocess.Popen([binary("tunnel-loadgen"), "--target", f"127.0.0.1:{port}", *map(str, args)],
                             stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
@@ -169,7 +191,9 @@ def main():
             t.__enter__()
             tunnels[tr] = t
         for rep in range(a.reps):
+            c0 = cpu_stat()
             d_sse, d_bulk, _, _ = scenario(mport, a)
+            d_cg = stat_delta(c0, cpu_stat())
             print(json.dumps({"rep": rep, "direct_itl_p99_ms": d_sse["p99_itl_ms"],
                               "direct_ttft_p99_ms": d_sse["p99_ttft_ms"], "direct_bulk_MBps": d_bulk["MBps"]}),
                   file=sys.stderr, flush=True)
@@ -177,7 +201,9 @@ def main():
                 t = tunnels[tr]
                 path = t.serve.wait_for("WebRTC connection established", 5).split(" via ", 1)[-1]
                 base = rss_kb(t.proxy.popen.pid)
+                c0 = cpu_stat()
                 sse_r, bulk_r, stats, peak = scenario(t.proxy_port, a, t.proxy.popen.pid)
+                t_cg = stat_delta(c0, cpu_stat())
                 run = {"rep": rep, "transport": tr, "path": path,
                        "tunneled_itl_p50_ms": sse_r["p50_itl_ms"], "tunneled_itl_p99_ms": sse_r["p99_itl_ms"],
                        "tunneled_itl_max_ms": sse_r["max_itl_ms"], "direct_itl_p50_ms": d_sse["p50_itl_ms"],
@@ -190,7 +216,9 @@ def main():
                        "bulk_MBps": bulk_r["MBps"], "direct_bulk_MBps": d_bulk["MBps"],
                        "bulk_ratio": bulk_r["MBps"] / d_bulk["MBps"] if d_bulk["MBps"] else None,
                        "bulk_errors": bulk_r["errors"], "slow_client_bytes": stats.get("slow_bytes"),
-                       "proxy_rss_base_mib": round(base / 1024, 1), "proxy_rss_peak_mib": round(peak / 1024, 1)}
+                       "proxy_rss_base_mib": round(base / 1024, 1), "proxy_rss_peak_mib": round(peak / 1024, 1),
+                       # the job's CPU quota over the run (cgroup v2): a throttled period stops every thread
+                       "cgroup_tunneled": t_cg, "cgroup_direct": d_cg}
                 res["runs"].append(run)
                 print(json.dumps(run), file=sys.stderr, flush=True)
         keys = ["added_itl_p99_ms", "tunneled_itl_p99_ms", "direct_itl_p99_ms", "added_ttft_p99_ms",
