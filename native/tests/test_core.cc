@@ -267,8 +267,8 @@ TEST(assoc_negotiation_falls_back_to_one_channel) {
 }
 
 // ProxyRouter placement ("assoc"): bulk goes to the association with the
-// fewest bulk connections, the first only while nothing interactive runs on
-// it; interactive requests stay on the first unless it carries kSpill of them
+// fewest bulk connections, the first only while nothing interactive has run on
+// it for the quiet period; interactive requests stay on the first unless it carries kSpill of them
 // and its thread is busy, then they spill to an extra association whose
 // thread has idle time — never when every thread is busy (a CPU-bound
 // process); a spilled connection goes home once the first is well below the
@@ -297,6 +297,9 @@ TEST(assoc_router_placement) {
   rt->interactive(0, +1);            // SSE on the first: bulk moves off it
   CHECK_EQ(rt->pick_bulk(true), 1);
   rt->interactive(0, -1);
+  CHECK_EQ(rt->pick_bulk(true), 1);  // ... and stays off it for the quiet period after
+  rt->set_quiet_us(0);
+  CHECK_EQ(rt->pick_bulk(true), 0);  // quiet again: the first takes bulk
   rt->release(0);
   rt->release(1);
   rt->release(2);

@@ -1393,10 +1393,12 @@ int ProxyRouter::pick_bulk(bool counted_on_first) {
   for (size_t k = 1; k < t_.size(); k++)
     if (t_[k].ready && (best < 0 || t_[k].conns < t_[size_t(best)].conns)) best = int(k);
   if (best < 0) return -1;  // no extra association: placement as without the extension
-  // The first association is a candidate while no interactive request runs on
-  // it (ties go to an extra one; a connection already counted there stays
-  // unless another association has fewer).
-  if (!t_.empty() && t_[0].ready && t_[0].interactive == 0) {
+  // The first association is a candidate while no interactive request has run
+  // on it for quiet_us_ (ties go to an extra one; a connection already counted
+  // there stays unless another association has fewer). A bulk-only load uses
+  // every association; next to interactive traffic the first one stays clear.
+  const bool quiet = !last_interactive_us_ || Reactor::now_us() - last_interactive_us_ >= quiet_us_;
+  if (!t_.empty() && t_[0].ready && t_[0].interactive == 0 && quiet) {
     const size_t c0 = t_[0].conns - (counted_on_first && t_[0].conns ? 1 : 0);
     if (c0 < t_[size_t(best)].conns || (counted_on_first && c0 <= t_[size_t(best)].conns)) return 0;
   }
@@ -1411,6 +1413,7 @@ void ProxyRouter::count(size_t k) {
 void ProxyRouter::interactive(size_t k, int delta) {
   std::lock_guard<std::mutex> lk(mu_);
   if (k >= t_.size()) return;
+  if (k == 0) last_interactive_us_ = std::max<uint64_t>(Reactor::now_us(), 1);
   if (delta > 0) t_[k].interactive += size_t(delta);
   else t_[k].interactive -= std::min(t_[k].interactive, size_t(-delta));
 }

@@ -201,7 +201,13 @@ class Tunnel:
             p.stop()
 
     def __enter__(self):
-        return self.start()
+        # A start that fails (a side never ready) stops what it started: a
+        # `with` body that never ran gets no __exit__.
+        try:
+            return self.start()
+        except BaseException:
+            self.stop()
+            raise
 
     def __exit__(self, *exc):
         self.stop()
