@@ -186,9 +186,7 @@ class Stream : public std::enable_shared_from_this<Stream> {
         scan_events(d, k, now);
       });
       if (used == SIZE_MAX) {
-        res_->errors++;
-        active_ = false;
-        conn_->close();
+        fail();
         return;
       }
       if (body_.done()) {
@@ -205,9 +203,7 @@ class Stream : public std::enable_shared_from_this<Stream> {
       auto rs = http::parse_response_head(buf_, head_, used, nullptr);
       if (rs == http::ParseResult::Incomplete) return;
       if (rs == http::ParseResult::Error || head_.status != 200) {
-        res_->errors++;
-        active_ = false;
-        conn_->close();
+        fail();
         return;
       }
       buf_.erase(0, used);
@@ -233,9 +229,7 @@ class Stream : public std::enable_shared_from_this<Stream> {
       scan_events(d, k, now);
     });
     if (used == SIZE_MAX) {
-      res_->errors++;
-      active_ = false;
-      conn_->close();
+      fail();
       return;
     }
     buf_.erase(0, used);
@@ -270,6 +264,21 @@ class Stream : public std::enable_shared_from_this<Stream> {
       active_ = false;
       finish();
     }
+  }
+
+  // An error response or a malformed body: counted, the connection dropped,
+  // and the stream goes on to its next request (it used to stop here, and a
+  // step waiting for it never ended: a 502 from a failed association hung the
+  // run).
+  void fail() {
+    res_->errors++;
+    active_ = false;
+    if (conn_) {
+      conn_->on_close(nullptr);
+      conn_->close();
+      conn_.reset();
+    }
+    finish();
   }
 
   void complete() {

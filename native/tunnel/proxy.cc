@@ -800,6 +800,7 @@ void ProxyWorker::conn_closed(ProxyConn* c) {
 void ProxyWorker::fail_all(const std::string& why) {
   auto streams = std::move(streams_);
   streams_.clear();
+  LOG_DEBUG(kT, "worker %zu: failing %zu in-flight stream(s): %s", index_, streams.size(), why.c_str());
   for (auto& kv : streams)
     if (auto c = kv.second.lock()) c->on_res_error(why);
 }
@@ -967,7 +968,10 @@ ProxySession::~ProxySession() {
     ch_->on_open = nullptr;
     ch_->on_buffered_low = nullptr;
   }
-  release_links("");
+  // Dropped without stop() (an extra association torn down from its own
+  // side: its link drops the session): its in-flight requests still get an
+  // error, or their clients wait on a response that never comes.
+  release_links(stopped_ ? "" : "tunnel disconnected");
 }
 
 void ProxySession::stop(const std::string& why) {

@@ -224,3 +224,32 @@ def test_a_failed_extra_association_is_dropped_from_placement():
             assert t.proxy.count("proxy failed") == 0 and t.serve.count("serve failed") == 0
     finally:
         mock.stop()
+
+
+def test_extra_association_failing_mid_transfer():
+    # The extra associations fail while downloads run on them (TUNNEL_FAULT
+    # assoc_down_ms, both peers, 1.2 s after they come up): the requests they
+    # carried end (an error or a short body, never a hang), neither process
+    # fails, and the next requests run on the first association.
+    mock, up = _mock()
+    try:
+        with Tunnel(f"http://127.0.0.1:{up}", serve_extra=MTU + ["--assoc", "3"], proxy_extra=MTU + ["--assoc", "3"],
+                    env={"RUST_LOG": "info", "TUNNEL_FAULT": "assoc_down_ms=1200"}) as t:
+            _wait_assoc(t, 3)
+            t0 = time.time()
+            r = subprocess.run([binary("tunnel-loadgen"), "--target", f"127.0.0.1:{t.proxy_port}", "--streams", "8",
+                                "--steps", "1000", "--warmup", "0", "--method", "POST", "--post-bytes", str(4 << 20),
+                                "--events", "none", "--duration-s", "3"],
+                               capture_output=True, text=True, timeout=60)
+            assert time.time() - t0 < 30
+            first = json.loads(r.stdout.strip().splitlines()[-1])
+            t.proxy.wait_for("association 1 down", 10)
+            t.proxy.wait_for("association 2 down", 10)
+            assert first["requests"] > 0, first
+            after = _loadgen(t.proxy_port, 8, 2, ["--post-bytes", str(1 << 20)])
+            assert after["errors"] == 0 and after["requests"] == 16, after
+            assert _sse(t.proxy_port)[0] == 200
+            assert t.proxy.count("proxy failed") == 0 and t.serve.count("serve failed") == 0
+            assert t.proxy.popen.poll() is None and t.serve.popen.poll() is None
+    finally:
+        mock.stop()
