@@ -1431,7 +1431,8 @@ int ProxyRouter::pick_interactive(size_t own) {
     // the load hovers around it).
     return t_[0].ready && t_[0].interactive < kSpill / 2 ? 0 : int(own);
   }
-  if (t_[0].interactive < kSpill || t_.size() < 2 || load(0) < kSpillLoad) return t_[0].ready || own == 0 ? 0 : -1;
+  if (t_[0].interactive < kSpill || t_.size() < 2 || (kSpillGate && load(0) < kSpillLoad))
+    return t_[0].ready || own == 0 ? 0 : -1;
   // Node-scale load on a busy first association thread: the ready extra
   // association with the fewest interactive requests whose thread still has
   // idle time. When every thread is busy (a CPU-bound process: 1024 streams
@@ -1441,7 +1442,7 @@ int ProxyRouter::pick_interactive(size_t own) {
   // request stays on the first.
   int best = 0;
   for (size_t k = 1; k < t_.size(); k++)
-    if (t_[k].ready && load(k) < kSpillLoad &&
+    if (t_[k].ready && (!kSpillGate || load(k) < kSpillLoad) &&
         (best == 0 || t_[k].interactive < t_[size_t(best)].interactive))
       best = int(k);
   return best;

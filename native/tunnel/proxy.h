@@ -123,6 +123,11 @@ class ProxyRouter : public std::enable_shared_from_this<ProxyRouter> {
     quiet_us_ = us;
   }
   static constexpr double kSpillLoad = 0.5;  // Reactor::load() of a busy association thread
+#ifdef P2PT_SPILL_COUNT_ONLY  // experiment builds (bench/ab.py): spill on the count alone, round 6's first version
+  static constexpr bool kSpillGate = false;
+#else
+  static constexpr bool kSpillGate = true;
+#endif
   // Moves a client connection (its socket and the bytes read but not parsed)
   // to association k's session; k > 0 counts it there until release(k).
   void hand(size_t k, int fd, Bytes unparsed);
