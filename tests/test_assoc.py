@@ -253,3 +253,42 @@ def test_extra_association_failing_mid_transfer():
             assert t.proxy.popen.poll() is None and t.serve.popen.poll() is None
     finally:
         mock.stop()
+
+
+def test_associations_come_back_after_the_tunnel_reconnects():
+    # serve restarts (graceful exit, then a new process): the proxy's
+    # supervisor re-establishes the tunnel, the extra associations are
+    # negotiated again, bulk spreads over them again, and the old ones left
+    # no threads behind.
+    import os
+    from p2p_llm_tunnel_amd.utils.procs import start_serve
+    mock, up = _mock()
+    mp = free_port()
+    env = {"RUST_LOG": "info"}
+    try:
+        with Tunnel(f"http://127.0.0.1:{up}", serve_extra=MTU + ["--assoc", "3"],
+                    proxy_extra=MTU + ["--assoc", "3", "--metrics-listen", f"127.0.0.1:{mp}"], env=env) as t:
+            _wait_assoc(t, 3)
+            assert _loadgen(t.proxy_port, 8, 1, ["--post-bytes", str(1 << 20)])["errors"] == 0
+            tasks = lambda: len(os.listdir(f"/proc/{t.proxy.popen.pid}/task"))  # noqa: E731
+            threads0 = tasks()
+            h0 = _metric(mp, "tunnel_assoc_handoffs_total")
+            sp = int(next(l for l in t.signal.lines if "listening on" in l).rsplit(":", 1)[1])
+            t.serve.stop()
+            t.proxy.wait_for(r"proxy failed \(attempt 1\)", 10)
+            serve2 = start_serve(t.room, t.upstream, sp, MTU + ["--assoc", "3"], env)
+            t.procs.append(serve2)
+            serve2.wait_for("tunnel ready", 30)
+            deadline = time.time() + 30
+            while (t.proxy.count("association 1 ready") < 2 or t.proxy.count("association 2 ready") < 2) \
+                    and time.time() < deadline:
+                time.sleep(0.1)
+            assert t.proxy.count("association 2 ready") == 2
+            r = _loadgen(t.proxy_port, 16, 2, ["--post-bytes", str(1 << 20)])
+            assert r["errors"] == 0 and r["requests"] == 32, r
+            assert _metric(mp, "tunnel_assoc_handoffs_total") > h0
+            assert _sse(t.proxy_port)[0] == 200
+            time.sleep(0.5)
+            assert tasks() <= threads0 + 1, (threads0, tasks())
+    finally:
+        mock.stop()
