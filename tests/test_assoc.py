@@ -292,3 +292,57 @@ def test_associations_come_back_after_the_tunnel_reconnects():
             assert tasks() <= threads0 + 1, (threads0, tasks())
     finally:
         mock.stop()
+
+
+def test_pipelined_requests_across_associations():
+    # One write carries a 1 MB upload and, right behind it, an SSE request and
+    # a small POST: the connection moves to an extra association with the
+    # bytes read past the upload, the SSE request takes it back to the first
+    # one; every response comes back whole and in order.
+    import socket
+    mock, up = _mock()
+    mp = free_port()
+    try:
+        with Tunnel(f"http://127.0.0.1:{up}", serve_extra=MTU + ["--assoc", "3"],
+                    proxy_extra=MTU + ["--assoc", "3", "--metrics-listen", f"127.0.0.1:{mp}"],
+                    env={"RUST_LOG": "info"}) as t:
+            _wait_assoc(t, 3)
+            body = bytes(range(256)) * 4096
+            sse_req = json.dumps({"stream": True}).encode()
+            wire = (b"POST /echo HTTP/1.1\r\nHost: x\r\nContent-Length: %d\r\n\r\n" % len(body) + body +
+                    b"POST /v1/chat/completions HTTP/1.1\r\nHost: x\r\nContent-Length: %d\r\n\r\n" % len(sse_req) +
+                    sse_req + b"POST /echo HTTP/1.1\r\nHost: x\r\nContent-Length: 5\r\n\r\nhello")
+            s = socket.create_connection(("127.0.0.1", t.proxy_port), timeout=30)
+            s.sendall(wire)
+            f = s.makefile("rb")
+
+            def response():
+                status = f.readline()
+                headers = {}
+                while True:
+                    line = f.readline()
+                    if line in (b"\r\n", b""):
+                        break
+                    k, _, v = line.decode().partition(":")
+                    headers[k.strip().lower()] = v.strip()
+                if "content-length" in headers:
+                    return status, f.read(int(headers["content-length"]))
+                out = b""
+                while True:  # chunked
+                    n = int(f.readline().strip(), 16)
+                    if n == 0:
+                        f.readline()
+                        return status, out
+                    out += f.read(n)
+                    f.readline()
+
+            st1, b1 = response()
+            st2, b2 = response()
+            st3, b3 = response()
+            s.close()
+            assert b" 200 " in st1 and b1 == body
+            assert b" 200 " in st2 and b2.rstrip().endswith(b"data: [DONE]")
+            assert b" 200 " in st3 and b3 == b"hello"
+            assert _metric(mp, "tunnel_assoc_handoffs_total") >= 2  # out to an extra association and back
+    finally:
+        mock.stop()
