@@ -268,11 +268,11 @@ TEST(assoc_negotiation_falls_back_to_one_channel) {
 
 // ProxyRouter placement ("assoc"): bulk goes to the association with the
 // fewest bulk connections, the first only while nothing interactive has run on
-// it for the quiet period; interactive requests stay on the first unless it carries kSpill of them
-// and its thread is busy, then they spill to an extra association whose
-// thread has idle time — never when every thread is busy (a CPU-bound
-// process); a spilled connection goes home once the first is well below the
-// threshold.
+// it for the quiet period; interactive requests stay on the first unless it
+// carries kSpill of them, then they spill to the extra association with the
+// fewest (with the load gate: only while the first one's thread is busy, to a
+// thread with idle time, never when every thread is busy); a spilled
+// connection goes home once the first is well below the threshold.
 TEST(assoc_router_placement) {
   Reactor r0, r1, r2;
   auto rt = std::make_shared<ProxyRouter>();
@@ -303,8 +303,17 @@ TEST(assoc_router_placement) {
   rt->release(0);
   rt->release(1);
   rt->release(2);
-  // Interactive: the first, until it carries kSpill with a busy thread.
-  for (size_t i = 0; i < ProxyRouter::kSpill; i++) rt->interactive(0, +1);
+  // Interactive, on the count alone (the default): past kSpill on the first,
+  // the extra one with the fewest.
+  for (size_t i = 0; i + 1 < ProxyRouter::kSpill; i++) rt->interactive(0, +1);
+  CHECK_EQ(rt->pick_interactive(0), 0);
+  rt->interactive(0, +1);
+  CHECK_EQ(rt->pick_interactive(0), 1);
+  rt->interactive(1, +1);
+  CHECK_EQ(rt->pick_interactive(0), 2);
+  rt->interactive(1, -1);
+  // With the load gate: the first, until it carries kSpill with a busy thread.
+  rt->set_load_gate(true);
   CHECK_EQ(rt->pick_interactive(0), 0);  // its thread is idle
   load[0] = 0.9;
   CHECK_EQ(rt->pick_interactive(0), 1);  // spill to an idle extra one

@@ -110,10 +110,14 @@ class ProxyRouter : public std::enable_shared_from_this<ProxyRouter> {
   // Interactive requests in flight on association k (+1 / -1).
   void interactive(size_t k, int delta);
   // The association for an interactive request of a connection on `own`:
-  // the first one, unless it already carries kSpill interactive requests and
-  // its thread is at least kSpillLoad busy — node-scale load (one association
-  // thread per side ~90 % busy at 1024 streams, profiles/r05/b11/nodeprof) —
-  // then the extra one with the fewest whose thread is below kSpillLoad.
+  // the first one, unless it already carries kSpill interactive requests —
+  // node-scale load (one association thread per side ~90 % busy at 1024
+  // streams, profiles/r05/b11/nodeprof) — then the extra one with the fewest.
+  // With the load gate on, only while the first one's thread is at least
+  // kSpillLoad busy, and only to threads below it. Off by default: one box,
+  // 3 interleaved reps each (profiles/r06/b13), 256-stream added p50 TTFT
+  // 0.356 ms gated vs 0.293 on the count alone, 1024 streams p99 21.1 vs 19.8
+  // ms, events 0.855 vs 0.841 of direct.
   // -1: no ready association.
   int pick_interactive(size_t own);
   static constexpr size_t kSpill = 32;
@@ -123,11 +127,10 @@ class ProxyRouter : public std::enable_shared_from_this<ProxyRouter> {
     quiet_us_ = us;
   }
   static constexpr double kSpillLoad = 0.5;  // Reactor::load() of a busy association thread
-#ifdef P2PT_SPILL_COUNT_ONLY  // experiment builds (bench/ab.py): spill on the count alone, round 6's first version
-  static constexpr bool kSpillGate = false;
-#else
-  static constexpr bool kSpillGate = true;
-#endif
+  void set_load_gate(bool on) {
+    std::lock_guard<std::mutex> lk(mu_);
+    load_gate_ = on;
+  }
   // Moves a client connection (its socket and the bytes read but not parsed)
   // to association k's session; k > 0 counts it there until release(k).
   void hand(size_t k, int fd, Bytes unparsed);
@@ -151,6 +154,7 @@ class ProxyRouter : public std::enable_shared_from_this<ProxyRouter> {
   std::vector<Target> t_;
   BulkRoutes routes_;
   uint64_t quiet_us_ = kQuietUs;
+  bool load_gate_ = false;
   uint64_t last_interactive_us_ = 0;  // the last interactive request start / end on the first association (0: never)
   std::function<double(size_t)> load_fn_;
 };
