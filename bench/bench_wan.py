@@ -229,7 +229,7 @@ def main():
     ap.add_argument("--policy", choices=["default", "keep"], default="default",
                     help="serve's congestion response: default, or keep (TUNNEL_SCTP_CC=beta=100)")
     ap.add_argument("--timeline", action="store_true",
-                    help="sample both sides' SCTP/UDP/DTLS gauges every 0.5 s during sse+bulk (row['timeline'])")
+                    help="sample both sides' SCTP/UDP/DTLS gauges every 0.5 s during sse+bulk and echo (row['timeline'])")
     ap.add_argument("--logs", default=None, help="write each row's serve/proxy/relay logs to this directory")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
@@ -292,11 +292,13 @@ def main():
                     time.sleep(0.5)
                     mixed = result(sse(t.proxy_port, a.sse_steps))
                     bulk_r = result(bulk)
-                    timeline = tl.stop() if tl else None
                     progress("echo")
+                    if tl:
+                        tl.rows.append({"t": round(time.time() - tl.t0, 2), "phase": "echo"})
                     t0 = time.time()
                     echo = result(lg(t.proxy_port, "--streams", 8, "--steps", a.echo_steps, "--warmup", 0,
                                      "--post-bytes", 1 << 20))
+                    timeline = tl.stop() if tl else None
                     row = {"rtt_ms": rtt, "loss": loss, "queue_kb": round(qkb),
                            "sse_itl_p50_ms": alone["p50_itl_ms"], "sse_itl_p99_ms": alone["p99_itl_ms"],
                            "sse_itl_max_ms": alone["max_itl_ms"], "sse_ttft_p50_ms": alone["p50_ttft_ms"],

@@ -1111,7 +1111,15 @@ void SctpAssociation::handle_sack(const uint8_t* c, size_t len) {
   queue_bound(cum, rtt_sample);
   // Congestion control (RFC 9260 §7.2.1-7.2.2).
   const bool long_path = min_rtt_us_ >= kLongPathUs;
-  if (cwnd_ <= ssthresh_ && !hs_done_ && long_path && !fast_recovery_) hystart(cum, rtt_sample);
+  // HyStart judges only rounds that fill cwnd, from kHsLowWindow packets on
+  // (RFC 9406's low window): an app-limited sender's RTT says nothing about a
+  // queue of its own. Small requests whose SACKs came back behind a download
+  // queued the other way ended slow start at the initial window, and the next
+  // upload then grew by a packet per round trip (profiles/r06/b14).
+  const bool cwnd_limited = flight_before + cfg_.mtu >= cwnd_;
+  if (cwnd_ <= ssthresh_ && !hs_done_ && long_path && !fast_recovery_ && cwnd_limited &&
+      cwnd_ >= size_t(kHsLowWindow) * cfg_.mtu)
+    hystart(cum, rtt_sample);
   if (newly_acked && cum_advanced && !fast_recovery_) {
     if (cwnd_ <= ssthresh_) {
       // Byte counting with RFC 3465's limit L = 2 MTUs per SACK on short

@@ -285,7 +285,7 @@ class SctpAssociation : public std::enable_shared_from_this<SctpAssociation> {
   // HyStart++ state (hystart()).
   void hystart(uint32_t cum, uint64_t rtt_sample);
   static constexpr uint64_t kLongPathUs = 5000;  // base RTT from which a path counts as long (WAN)
-  static constexpr int kHsSamples = 8, kCssRounds = 5;
+  static constexpr int kHsSamples = 8, kCssRounds = 5, kHsLowWindow = 16;
   static constexpr size_t kCssDivisor = 4;
   // Delivery rate per round trip (bytes acknowledged between a round's first
   // SACK and the SACK covering the last TSN sent when it began), windowed max

@@ -432,6 +432,68 @@ TEST(sctp_shallow_queue_bottleneck_backs_off) {
   }
 }
 
+TEST(sctp_small_messages_under_a_queued_download_do_not_end_slow_start) {
+  // 20 ms RTT; b -> a is a 200 Mbit/s bottleneck with a one-BDP queue that b's
+  // download fills, a -> b is not limited. Meanwhile a sends only small
+  // messages (requests: never a full window), and their SACKs come back
+  // through that queue, 20 ms late. HyStart took the rise for a queue of a's
+  // own and ended slow start at the initial window (ssthresh 4380 bytes): a's
+  // next upload then grew by one packet per round trip — the relayed 8 x 1 MB
+  // echo at 3.3 instead of 13 req/s (profiles/r06/b14). HyStart now runs only
+  // on rounds that fill cwnd, from 16 packets on (RFC 9406's low window).
+  SctpPair p(0, 0, 0, 1200, false, false, 100);
+  p.link.fixed_delay_us = 10000;
+  p.link.rate_bps = 200e6;
+  p.link.queue_bytes = 500 * 1024;
+  p.link.bottleneck_to = p.a;
+  p.a->connect();
+  p.b->connect();
+  CHECK(p.r.run_until([&] { return p.a->established() && p.b->established(); }, 5000));
+  std::string blk = payload(10000, 6);
+  const int down = 2500, up = 1000;  // 25 MB down (1 s at the bottleneck), 10 MB up
+  for (int i = 0; i < down; i++) p.b->send(1, 53, {Bytes::copy(blk)});
+  size_t small = 0;
+  uint64_t next = Reactor::now_us();
+  p.r.run_until([&] {  // 0.8 s of small requests from a while the download runs
+    if (Reactor::now_us() >= next) {
+      p.a->send(5, 53, {Bytes::copy(payload(300, uint32_t(small++)))});
+      next += 2000;
+    }
+    return false;
+  }, 800);
+  const uint64_t hs0 = p.a->stats().hystart_exits;
+  const uint64_t t0 = Reactor::now_us();
+  for (int i = 0; i < up; i++) p.a->send(3, 53, {Bytes::copy(blk)});
+  CHECK(p.r.run_until([&] { return p.got_b.size() == small + size_t(up); }, 30000));
+  const double secs = double(Reactor::now_us() - t0) / 1e6;
+  printf("  %zu small messages, then 10 MB up: %.2f s, cwnd %zu, hystart exits %llu before the upload\n", small, secs,
+         p.a->cwnd(), (unsigned long long)hs0);
+  CHECK_EQ(hs0, 0u);
+  CHECK(secs < 0.5);
+}
+
+TEST(sctp_hystart_ends_slow_start_at_a_forward_queue) {
+  // The other side of the test above: a bulk transfer that fills cwnd into a
+  // deep drop-tail queue (200 Mbit/s, 4 MB = 160 ms, 20 ms RTT) leaves slow
+  // start on the delay rise before the queue overflows.
+  SctpPair p(0, 0, 0, 1200, false, false, 100);
+  p.link.fixed_delay_us = 10000;
+  p.link.rate_bps = 200e6;
+  p.link.queue_bytes = 4 << 20;
+  p.link.bottleneck_to = p.b;
+  p.a->connect();
+  p.b->connect();
+  CHECK(p.r.run_until([&] { return p.a->established() && p.b->established(); }, 5000));
+  std::string blk = payload(10000, 7);
+  const int n = 2000;  // 20 MB
+  for (int i = 0; i < n; i++) p.a->send(1, 53, {Bytes::copy(blk)});
+  CHECK(p.r.run_until([&] { return p.got_b.size() == size_t(n); }, 30000));
+  printf("  hystart exits %llu, queue drops %llu, cwnd %zu\n", (unsigned long long)p.a->stats().hystart_exits,
+         (unsigned long long)p.link.queue_drops, p.a->cwnd());
+  CHECK(p.a->stats().hystart_exits >= 1);
+  CHECK_EQ(p.link.queue_drops, 0u);
+}
+
 TEST(sctp_queue_bound_keeps_short_path_queue_small) {
   if (!cc_policy().queue_bound) {  // TUNNEL_SCTP_CC selects another policy: this tests the short-path queue bound
     printf("  skipped under TUNNEL_SCTP_CC\n");
