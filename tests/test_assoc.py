@@ -346,3 +346,39 @@ def test_pipelined_requests_across_associations():
             assert _metric(mp, "tunnel_assoc_handoffs_total") >= 2  # out to an extra association and back
     finally:
         mock.stop()
+
+
+def test_serve_killed_mid_transfer_every_association_fails_over():
+    # serve is SIGKILLed while uploads run on all three associations: nothing
+    # tells the proxy, so consent freshness (--ice-timeout-ms) must end each
+    # association; every in-flight request ends (error or done, no hang), and a
+    # new serve brings the tunnel and its extra associations back.
+    from p2p_llm_tunnel_amd.utils.procs import start_serve
+    mock, up = _mock()
+    extra = MTU + ["--assoc", "3", "--ice-timeout-ms", "2000"]
+    env = {"RUST_LOG": "info"}
+    try:
+        with Tunnel(f"http://127.0.0.1:{up}", serve_extra=extra, proxy_extra=extra, env=env) as t:
+            _wait_assoc(t, 3)
+            lg = subprocess.Popen([binary("tunnel-loadgen"), "--target", f"127.0.0.1:{t.proxy_port}", "--streams", "8",
+                                   "--steps", "1000", "--warmup", "0", "--post-bytes", str(4 << 20), "--events", "none",
+                                   "--duration-s", "2"], stdout=subprocess.PIPE, text=True)
+            time.sleep(0.8)
+            t.serve.kill()
+            out, _ = lg.communicate(timeout=40)
+            r = json.loads(out.strip().splitlines()[-1])
+            assert r["requests"] > 0, r
+            t.proxy.wait_for(r"proxy failed \(attempt 1\)", 15)
+            sp = int(next(l for l in t.signal.lines if "listening on" in l).rsplit(":", 1)[1])
+            serve2 = start_serve(t.room, t.upstream, sp, extra, env)
+            t.procs.append(serve2)
+            serve2.wait_for("tunnel ready", 30)
+            deadline = time.time() + 30
+            while t.proxy.count("association 2 ready") < 2 and time.time() < deadline:
+                time.sleep(0.1)
+            assert t.proxy.count("association 2 ready") == 2
+            after = _loadgen(t.proxy_port, 8, 2, ["--post-bytes", str(1 << 20)])
+            assert after["errors"] == 0 and after["requests"] == 16, after
+            assert t.proxy.popen.poll() is None
+    finally:
+        mock.stop()
