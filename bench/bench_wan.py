@@ -185,7 +185,7 @@ def steady_row(mport, rtt, loss, rate, qkb, mb, streams, extra):
         pid, ppid = t.serve.popen.pid, t.proxy.popen.pid
         c0, p0, t0 = thread_cpu(pid), thread_cpu(ppid), time.time()
         r = result(lg(t.proxy_port, "--streams", streams, "--steps", 1, "--warmup", 0, "--method", "GET",
-                      "--path", f"/bulk?bytes={mb << 20}", "--events", "none"))
+                      "--path", f"/bulk?bytes={mb << 20}", "--events", "none"), timeout=900)  # lossy 1 Gbit/s rows move GBs
         wall = time.time() - t0
         c1, p1 = thread_cpu(pid), thread_cpu(ppid)
         cpu = {k: round(100 * (c1[k] - c0.get(k, 0.0)) / wall, 1) for k in c1 if c1[k] - c0.get(k, 0.0) > 0}
