@@ -9,9 +9,17 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "scripts"))
 
+import pytest  # noqa: E402
+
 import profile_citations as pc  # noqa: E402
 
+# The GPU-box snapshot leaves the evidence tree out (.gpurunignore): nothing
+# to resolve there.
+needs_tree = pytest.mark.skipif(not os.path.isdir(os.path.join(ROOT, "profiles")),
+                                reason="no profiles/ in this tree (GPU-box snapshot)")
 
+
+@needs_tree
 def test_every_cited_profile_path_resolves():
     bad = pc.check()
     assert not bad, "\n".join(f"{c} (cited in {', '.join(sorted(d))})" for c, d in sorted(bad.items()))
@@ -25,5 +33,6 @@ def test_resolver_expands_braces_globs_and_directories():
     assert pc.resolve("profiles/r05/b14/", files) == []
 
 
+@needs_tree
 def test_profiles_tree_is_pruned():
     assert len(pc.tracked()) <= 500
