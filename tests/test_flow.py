@@ -350,3 +350,41 @@ def test_upload_answered_early_with_413_completes(chunked):
             assert r.status == 200 and r.read()
     finally:
         mock.stop()
+
+
+def test_slow_client_on_an_extra_association_bounds_proxy_memory():
+    """The same stalled 100 MB download, but on an extra association of the
+    "assoc" extension: the route is learnt as bulk first, so the download's
+    connection moves to another association before it starts; flow credit
+    still bounds what the proxy holds for the client."""
+    mock, mport = _native_mock()
+    ms, mp = free_port(), free_port()
+    try:
+        with Tunnel(f"http://127.0.0.1:{mport}", transport="webrtc",
+                    serve_extra=["--metrics-listen", f"127.0.0.1:{ms}", "--assoc", "3"],
+                    proxy_extra=["--metrics-listen", f"127.0.0.1:{mp}", "--assoc", "3"],
+                    env={"RUST_LOG": "info"}) as t:
+            for k in (1, 2):
+                t.proxy.wait_for(f"association {k} ready", 20)
+            urllib.request.urlopen(t.url + "/bulk?bytes=1000000", timeout=30).read()  # the route is bulk now
+            base = _rss_kb(t.proxy.popen.pid)
+            s = socket.create_connection(("127.0.0.1", t.proxy_port))
+            s.sendall(b"GET /bulk?bytes=100000000 HTTP/1.1\r\nHost: x\r\n\r\n")
+            head = s.recv(65536)
+            assert head.startswith(b"HTTP/1.1 200")
+            time.sleep(2.0)  # the client reads nothing
+            grown = _rss_kb(t.proxy.popen.pid) - base
+            m = urllib.request.urlopen(f"http://127.0.0.1:{mp}/metrics", timeout=5).read().decode()
+            handoffs = [float(l.split()[1]) for l in m.splitlines() if l.startswith("tunnel_assoc_handoffs_total")]
+            assert handoffs and handoffs[0] >= 1, m[:200]
+            assert grown < 24 * 1024 * RSS_SCALE, grown  # KiB
+            n = len(head) - head.index(b"\r\n\r\n") - 4
+            s.settimeout(30)
+            while n < 100_000_000:
+                d = s.recv(1 << 20)
+                assert d
+                n += len(d)
+            assert n == 100_000_000
+            s.close()
+    finally:
+        mock.stop()
