@@ -382,3 +382,36 @@ def test_serve_killed_mid_transfer_every_association_fails_over():
             assert t.proxy.popen.poll() is None
     finally:
         mock.stop()
+
+
+def test_client_disconnect_on_an_extra_association_cancels_upstream():
+    # A download runs on an extra association (route learnt as bulk); the
+    # client goes away mid-body: the proxy sends CANCEL on that association,
+    # serve aborts the upstream call (tunnel_streams_cancelled_total), and the
+    # association keeps serving.
+    import socket
+    mock, up = _mock()
+    ms, mp = free_port(), free_port()
+    try:
+        with Tunnel(f"http://127.0.0.1:{up}", serve_extra=MTU + ["--assoc", "3", "--metrics-listen", f"127.0.0.1:{ms}"],
+                    proxy_extra=MTU + ["--assoc", "3", "--metrics-listen", f"127.0.0.1:{mp}"],
+                    env={"RUST_LOG": "info"}) as t:
+            _wait_assoc(t, 3)
+            urllib.request.urlopen(f"http://127.0.0.1:{t.proxy_port}/bulk?bytes=1000000", timeout=30).read()
+            s = socket.create_connection(("127.0.0.1", t.proxy_port))
+            s.sendall(b"GET /bulk?bytes=500000000 HTTP/1.1\r\nHost: x\r\n\r\n")
+            got = 0
+            while got < 4 << 20:
+                d = s.recv(1 << 20)
+                assert d
+                got += len(d)
+            s.close()
+            deadline = time.time() + 10
+            while _metric(ms, "tunnel_streams_cancelled_total") < 1 and time.time() < deadline:
+                time.sleep(0.1)
+            assert _metric(ms, "tunnel_streams_cancelled_total") >= 1
+            assert _metric(mp, "tunnel_assoc_handoffs_total") >= 1
+            r = _loadgen(t.proxy_port, 4, 2, ["--method", "GET", "--path", "/bulk?bytes=1000000", "--events", "none"])
+            assert r["errors"] == 0 and r["requests"] == 8, r
+    finally:
+        mock.stop()
