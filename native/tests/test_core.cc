@@ -303,8 +303,9 @@ TEST(assoc_router_placement) {
   rt->release(0);
   rt->release(1);
   rt->release(2);
-  // Interactive, on the count alone (the default): past kSpill on the first,
-  // the extra one with the fewest.
+  // Interactive, on the count alone (set_load_gate(false)): past kSpill on the
+  // first, the extra one with the fewest.
+  rt->set_load_gate(false);
   for (size_t i = 0; i + 1 < ProxyRouter::kSpill; i++) rt->interactive(0, +1);
   CHECK_EQ(rt->pick_interactive(0), 0);
   rt->interactive(0, +1);
@@ -312,7 +313,8 @@ TEST(assoc_router_placement) {
   rt->interactive(1, +1);
   CHECK_EQ(rt->pick_interactive(0), 2);
   rt->interactive(1, -1);
-  // With the load gate: the first, until it carries kSpill with a busy thread.
+  // With the load gate (the default): the first, until it carries kSpill with
+  // a busy thread.
   rt->set_load_gate(true);
   CHECK_EQ(rt->pick_interactive(0), 0);  // its thread is idle
   load[0] = 0.9;

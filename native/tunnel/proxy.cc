@@ -1433,11 +1433,13 @@ int ProxyRouter::pick_interactive(size_t own) {
   }
   if (t_[0].interactive < kSpill || t_.size() < 2 || (load_gate_ && load(0) < kSpillLoad))
     return t_[0].ready || own == 0 ? 0 : -1;
-  // Node-scale load: the ready extra association with the fewest interactive
-  // requests (with the load gate: only one whose thread still has idle time;
-  // when every thread is busy the request stays on the first — the gate was
-  // meant to keep a CPU-bound process from paying per-association overhead,
-  // but on one box it measured no better, profiles/r06/b13).
+  // Node-scale load on a busy first association thread: the ready extra
+  // association with the fewest interactive requests whose thread still has
+  // idle time (with the load gate, the default). When every thread is busy (a
+  // CPU-bound process: 1024 streams on the pool box's 16-CPU quota), spreading
+  // only adds per-association overhead — smaller batches, more packets and
+  // SACKs per token — so the request stays on the first (profiles/r06/b13,
+  // b20: events 0.855 / 0.851 of direct gated vs 0.841 / 0.838 without).
   int best = 0;
   for (size_t k = 1; k < t_.size(); k++)
     if (t_[k].ready && (!load_gate_ || load(k) < kSpillLoad) &&

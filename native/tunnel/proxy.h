@@ -113,11 +113,12 @@ class ProxyRouter : public std::enable_shared_from_this<ProxyRouter> {
   // the first one, unless it already carries kSpill interactive requests —
   // node-scale load (one association thread per side ~90 % busy at 1024
   // streams, profiles/r05/b11/nodeprof) — then the extra one with the fewest.
-  // With the load gate on, only while the first one's thread is at least
-  // kSpillLoad busy, and only to threads below it. Off by default: one box,
-  // 3 interleaved reps each (profiles/r06/b13), 256-stream added p50 TTFT
-  // 0.356 ms gated vs 0.293 on the count alone, 1024 streams p99 21.1 vs 19.8
-  // ms, events 0.855 vs 0.841 of direct.
+  // With the load gate (the default), only while the first one's thread is
+  // at least kSpillLoad busy, and only to threads below it. Two boxes, 3
+  // interleaved reps each (profiles/r06/b13, b20): at 1024 streams the gate
+  // is ahead on both (events 0.855 / 0.851 of direct vs 0.841 / 0.838 on the
+  // count alone, added p50 TTFT 3.7 / 3.9 vs 4.5 / 4.5 ms); at 256 streams the
+  // two are within the spread (added p50 0.356 / 0.342 vs 0.293 / 0.338 ms).
   // -1: no ready association.
   int pick_interactive(size_t own);
   static constexpr size_t kSpill = 32;
@@ -154,7 +155,7 @@ class ProxyRouter : public std::enable_shared_from_this<ProxyRouter> {
   std::vector<Target> t_;
   BulkRoutes routes_;
   uint64_t quiet_us_ = kQuietUs;
-  bool load_gate_ = false;
+  bool load_gate_ = true;
   uint64_t last_interactive_us_ = 0;  // the last interactive request start / end on the first association (0: never)
   std::function<double(size_t)> load_fn_;
 };
